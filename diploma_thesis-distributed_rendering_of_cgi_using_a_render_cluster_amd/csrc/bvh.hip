@@ -1,0 +1,427 @@
+// LBVH build on the device: K1 world transform + centroid
+// bounds, K2 30-bit Morton codes, K3 stable 4x8-bit LSD radix sort, K4 Karras
+// 2012 topology + bottom-up refit with arrival counters, K5 leaf-order
+// triangle pack. Everything is integer or exact (min/max) except the world
+// transform and the Morton quantisation, whose float ops are written in the
+// same order as oracle/rr_oracle.c so the whole BVH is reproduced bit for bit.
+//
+// Replaces Cycles' BVH build inside bpy.ops.render.render
+// (/root/reference/scripts/render-timing-script.py:90); the reference rebuilds
+// the full Blender scene per frame, here only the per-frame rigid transforms are
+// uploaded and the LBVH is rebuilt when they change.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "device.hpp"
+
+namespace rr {
+
+namespace {
+
+constexpr int kSortItems = 4;                   // keys per thread
+constexpr int kSortTile = kBlock * kSortItems;  // 1024 keys per block
+constexpr int kScanTile = 1024;
+
+__device__ __forceinline__ uint32_t f2o(float f) {  // order-preserving float -> uint
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float o2f(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__device__ __forceinline__ uint32_t expand10(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__device__ __forceinline__ float xf(const float* m, float x, float y, float z) {
+    return m[0] * x + m[1] * y + m[2] * z + m[3];
+}
+
+// K1: object -> world, centroid sum (v0+v1)+v2 stored in the .w lanes,
+// block min/max of the centroid sums folded into 6 ordered-uint words (all
+// reduced as minima: slot 3..5 hold -max).
+__global__ __launch_bounds__(kBlock) void k_transform(int n, const float4* __restrict__ local,
+                                                      const int32_t* __restrict__ obj,
+                                                      const float* __restrict__ xform,
+                                                      float4* __restrict__ world,
+                                                      uint32_t* __restrict__ bounds) {
+    __shared__ uint32_t red[6];
+    if (threadIdx.x < 6) red[threadIdx.x] = 0xFFFFFFFFu;
+    __syncthreads();
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t mn[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (i < n) {
+        const float* m = xform + 12 * obj[i];
+        float3 w[3];
+        for (int k = 0; k < 3; ++k) {
+            const float4 v = local[3 * i + k];
+            w[k] = mk3(xf(m, v.x, v.y, v.z), xf(m + 4, v.x, v.y, v.z), xf(m + 8, v.x, v.y, v.z));
+        }
+        const float3 c = add3(add3(w[0], w[1]), w[2]);
+        world[3 * i + 0] = make_float4(w[0].x, w[0].y, w[0].z, c.x);
+        world[3 * i + 1] = make_float4(w[1].x, w[1].y, w[1].z, c.y);
+        world[3 * i + 2] = make_float4(w[2].x, w[2].y, w[2].z, c.z);
+        mn[0] = f2o(c.x); mn[1] = f2o(c.y); mn[2] = f2o(c.z);
+        mn[3] = f2o(-c.x); mn[4] = f2o(-c.y); mn[5] = f2o(-c.z);
+    }
+    for (int k = 0; k < 6; ++k) {
+        uint32_t v = mn[k];
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t o = __shfl_xor(v, off);
+            v = o < v ? o : v;
+        }
+        if ((threadIdx.x & 63) == 0) atomicMin(&red[k], v);
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) atomicMin(&bounds[threadIdx.x], red[threadIdx.x]);
+}
+
+// K2: 30-bit Morton code of the quantised centroid sum.
+__global__ __launch_bounds__(kBlock) void k_morton(int n, const float4* __restrict__ world,
+                                                   const uint32_t* __restrict__ bounds,
+                                                   uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float lo[3] = {o2f(bounds[0]), o2f(bounds[1]), o2f(bounds[2])};
+    const float hi[3] = {-o2f(bounds[3]), -o2f(bounds[4]), -o2f(bounds[5])};
+    const float c[3] = {world[3 * i].w, world[3 * i + 1].w, world[3 * i + 2].w};
+    uint32_t q[3];
+    for (int k = 0; k < 3; ++k) {
+        const float ext = hi[k] - lo[k];
+        const float s = ext > 0.0f ? 1024.0f / ext : 0.0f;
+        float f = (c[k] - lo[k]) * s;
+        f = fminf(fmaxf(f, 0.0f), 1023.0f);
+        q[k] = (uint32_t)f;
+    }
+    keys[i] = (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+    vals[i] = (uint32_t)i;
+}
+
+// K3a: per-block digit histogram, layout hist[digit * nblocks + block].
+__global__ __launch_bounds__(kBlock) void k_radix_hist(int n, int shift, const uint32_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ hist, int nblocks) {
+    __shared__ uint32_t cnt[256];
+    cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int base = blockIdx.x * kSortTile;
+    for (int k = 0; k < kSortItems; ++k) {
+        const int i = base + k * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// K3b: stable scatter. Wave w owns keys [w*256, w*256+256) of the tile, walked
+// in 4 rounds of 64; ranks within a round come from an 8-ballot digit match.
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(int n, int shift, const uint32_t* __restrict__ kin,
+                                                          const uint32_t* __restrict__ vin,
+                                                          uint32_t* __restrict__ kout,
+                                                          uint32_t* __restrict__ vout,
+                                                          const uint32_t* __restrict__ offs, int nblocks) {
+    __shared__ uint32_t wcnt[4][256];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    for (int k = 0; k < 4; ++k) wcnt[k][threadIdx.x] = 0;
+    __syncthreads();
+    const int base = blockIdx.x * kSortTile + w * 256;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t key[4], val[4], rank[4];
+    bool ok[4];
+    for (int r = 0; r < 4; ++r) {
+        const int i = base + r * 64 + lane;
+        ok[r] = i < n;
+        key[r] = ok[r] ? kin[i] : 0u;
+        val[r] = ok[r] ? vin[i] : 0u;
+        const uint32_t d = (key[r] >> shift) & 255u;
+        uint64_t peers = __ballot(ok[r]);
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t before = wcnt[w][d];
+        rank[r] = before + (uint32_t)__popcll(peers & lt);
+        __builtin_amdgcn_wave_barrier();
+        if (ok[r] && (peers & lt) == 0ull) wcnt[w][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    {   // exclusive prefix over the 4 waves, per digit
+        uint32_t s = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t t = wcnt[k][threadIdx.x];
+            wcnt[k][threadIdx.x] = s;
+            s += t;
+        }
+    }
+    __syncthreads();
+    for (int r = 0; r < 4; ++r) {
+        if (!ok[r]) continue;
+        const uint32_t d = (key[r] >> shift) & 255u;
+        const uint32_t pos = offs[d * nblocks + blockIdx.x] + wcnt[w][d] + rank[r];
+        kout[pos] = key[r];
+        vout[pos] = val[r];
+    }
+}
+
+// Block-wide exclusive scan helper for 1024 items (256 threads x 4).
+__device__ uint32_t block_scan4(uint32_t v[4], uint32_t* lds_waves) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t t = v[0] + v[1] + v[2] + v[3];
+    uint32_t inc = t;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(inc, off);
+        if (lane >= off) inc += o;
+    }
+    if (lane == 63) lds_waves[w] = inc;
+    __syncthreads();
+    uint32_t wave_off = 0, total = 0;
+    for (int k = 0; k < 4; ++k) {
+        if (k < w) wave_off += lds_waves[k];
+        total += lds_waves[k];
+    }
+    uint32_t run = wave_off + inc - t;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = v[k];
+        v[k] = run;
+        run += x;
+    }
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_tiles(int m, uint32_t* __restrict__ data,
+                                                       uint32_t* __restrict__ part) {
+    __shared__ uint32_t ws[4];
+    const int base = blockIdx.x * kScanTile + threadIdx.x * 4;
+    uint32_t v[4];
+    for (int k = 0; k < 4; ++k) v[k] = (base + k < m) ? data[base + k] : 0u;
+    const uint32_t total = block_scan4(v, ws);
+    for (int k = 0; k < 4; ++k)
+        if (base + k < m) data[base + k] = v[k];
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+// Exclusive scan of the tile totals by one block (loops over 1024-item slabs).
+__global__ __launch_bounds__(kBlock) void k_scan_parts(int np, uint32_t* __restrict__ part) {
+    __shared__ uint32_t ws[4];
+    uint32_t carry = 0;
+    for (int s = 0; s < np; s += kScanTile) {
+        const int base = s + threadIdx.x * 4;
+        uint32_t v[4];
+        for (int k = 0; k < 4; ++k) v[k] = (base + k < np) ? part[base + k] : 0u;
+        const uint32_t total = block_scan4(v, ws);
+        for (int k = 0; k < 4; ++k)
+            if (base + k < np) part[base + k] = v[k] + carry;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_add(int m, uint32_t* __restrict__ data,
+                                                     const uint32_t* __restrict__ part) {
+    const int base = blockIdx.x * kScanTile + threadIdx.x * 4;
+    const uint32_t add = part[blockIdx.x];
+    for (int k = 0; k < 4; ++k)
+        if (base + k < m) data[base + k] += add;
+}
+
+__device__ __forceinline__ int delta(const uint32_t* __restrict__ keys, int n, int i, int j) {
+    if (j < 0 || j >= n) return -1;
+    const uint32_t a = keys[i], b = keys[j];
+    if (a == b) return 32 + __clz((uint32_t)(i ^ j));
+    return __clz(a ^ b);
+}
+
+// K4a: Karras 2012 topology of internal node i.
+__global__ __launch_bounds__(kBlock) void k_karras(int n, const uint32_t* __restrict__ keys,
+                                                   int2* __restrict__ children,
+                                                   int32_t* __restrict__ node_parent,
+                                                   int32_t* __restrict__ leaf_parent) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n - 1) return;
+    const int d = (delta(keys, n, i, i + 1) - delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
+    const int dmin = delta(keys, n, i, i - d);
+    int lmax = 2;
+    while (delta(keys, n, i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (delta(keys, n, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = delta(keys, n, i, j);
+    int s = 0;
+    int t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (delta(keys, n, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int gamma = i + s * d + (d < 0 ? -1 : 0);
+    const int lo = i < j ? i : j, hi = i < j ? j : i;
+    int left, right;
+    if (lo == gamma) {
+        left = ~gamma;
+        leaf_parent[gamma] = 2 * i;
+    } else {
+        left = gamma;
+        node_parent[gamma] = 2 * i;
+    }
+    if (hi == gamma + 1) {
+        right = ~(gamma + 1);
+        leaf_parent[gamma + 1] = 2 * i + 1;
+    } else {
+        right = gamma + 1;
+        node_parent[gamma + 1] = 2 * i + 1;
+    }
+    children[i] = make_int2(left, right);
+    if (i == 0) node_parent[0] = -1;
+}
+
+__device__ __forceinline__ void st_agent(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// K4b + K5: pack leaf i, then climb. Boxes are handed between workgroups
+// through agent-scope (write-through, L1-bypassing) stores/loads and a
+// returning agent-scope arrival counter per node: the second arriver owns the
+// node (MI355X_MICROARCH.md "Valid forms": sc1 stores drained before the
+// counter add, sc1 loads after it).
+__global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restrict__ order,
+                                                  const float4* __restrict__ world,
+                                                  const int32_t* __restrict__ tri_mat,
+                                                  const int32_t* __restrict__ leaf_parent,
+                                                  const int32_t* __restrict__ node_parent,
+                                                  const int2* __restrict__ children,
+                                                  uint32_t* __restrict__ flags,
+                                                  BvhNode* __restrict__ nodes,
+                                                  TriPack* __restrict__ tris) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int orig = (int)order[i];
+    const float4 a = world[3 * orig], b = world[3 * orig + 1], c = world[3 * orig + 2];
+    TriPack tp;
+    tp.p0 = make_float4(a.x, a.y, a.z, i2f(orig));
+    tp.p1 = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, i2f(tri_mat[orig]));
+    tp.p2 = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.0f);
+    tris[i] = tp;
+    float bx[6] = {fminf(fminf(a.x, b.x), c.x), fminf(fminf(a.y, b.y), c.y), fminf(fminf(a.z, b.z), c.z),
+                   fmaxf(fmaxf(a.x, b.x), c.x), fmaxf(fmaxf(a.y, b.y), c.y), fmaxf(fmaxf(a.z, b.z), c.z)};
+    if (n == 1) {  // single triangle: root with both children = leaf 0
+        float* f = reinterpret_cast<float*>(&nodes[0]);
+        for (int k = 0; k < 6; ++k) {
+            f[k] = bx[k];
+            f[6 + k] = bx[k];
+        }
+        nodes[0].d = make_int4(~0, ~0, 0, 0);
+        return;
+    }
+    int penc = leaf_parent[i];
+    for (int guard = 0; guard < 4096 && penc >= 0; ++guard) {
+        const int p = penc >> 1, side = penc & 1;
+        float* f = reinterpret_cast<float*>(&nodes[p]);
+        for (int k = 0; k < 6; ++k) st_agent(f + 6 * side + k, bx[k]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t prev = __hip_atomic_fetch_add(&flags[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == 0u) return;  // first arrival: the sibling's thread finishes the node
+        const int o = 6 * (1 - side);
+        for (int k = 0; k < 3; ++k) bx[k] = fminf(bx[k], ld_agent(f + o + k));
+        for (int k = 3; k < 6; ++k) bx[k] = fmaxf(bx[k], ld_agent(f + o + k));
+        const int2 ch = children[p];
+        int* fi = reinterpret_cast<int*>(f);
+        __hip_atomic_store(fi + 12, ch.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fi + 13, ch.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fi + 14, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fi + 15, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        penc = node_parent[p];
+    }
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+void exclusive_scan(DevScene& s, uint32_t* data, int m, hipStream_t st) {
+    const int tiles = cdiv(m, kScanTile);
+    s.scan_part.ensure((size_t)tiles);
+    k_scan_tiles<<<tiles, kBlock, 0, st>>>(m, data, s.scan_part.ptr);
+    k_scan_parts<<<1, kBlock, 0, st>>>(tiles, s.scan_part.ptr);
+    k_scan_add<<<tiles, kBlock, 0, st>>>(m, data, s.scan_part.ptr);
+}
+
+}  // namespace
+
+void DevScene::release() {
+    tri_local.release(); tri_obj.release(); tri_mat.release(); obj_xform.release();
+    tri_world.release(); bounds.release();
+    for (int k = 0; k < 2; ++k) { keys[k].release(); vals[k].release(); }
+    hist.release(); scan_part.release(); children.release(); node_parent.release();
+    leaf_parent.release(); flags.release(); nodes.release(); tris.release();
+    built = false;
+    uploaded = false;
+}
+
+void build_lbvh(DevScene& s, hipStream_t st) {
+    const int n = s.n_tris;
+    if (n <= 0) {
+        s.built = true;
+        return;
+    }
+    const int nb = cdiv(n, kBlock);
+    s.tri_world.ensure((size_t)3 * n);
+    s.bounds.ensure(6);
+    for (int k = 0; k < 2; ++k) {
+        s.keys[k].ensure((size_t)n);
+        s.vals[k].ensure((size_t)n);
+    }
+    s.nodes.ensure((size_t)(n > 1 ? n - 1 : 1));
+    s.tris.ensure((size_t)n);
+    s.children.ensure((size_t)(n > 1 ? n - 1 : 1));
+    s.node_parent.ensure((size_t)(n > 1 ? n - 1 : 1));
+    s.leaf_parent.ensure((size_t)n);
+    s.flags.ensure((size_t)(n > 1 ? n - 1 : 1));
+
+    RR_HIP(hipMemsetAsync(s.bounds.ptr, 0xFF, 6 * sizeof(uint32_t), st));
+    k_transform<<<nb, kBlock, 0, st>>>(n, s.tri_local.ptr, s.tri_obj.ptr, s.obj_xform.ptr,
+                                        s.tri_world.ptr, s.bounds.ptr);
+    k_morton<<<nb, kBlock, 0, st>>>(n, s.tri_world.ptr, s.bounds.ptr, s.keys[0].ptr, s.vals[0].ptr);
+    // K3: four stable 8-bit passes over the 30-bit keys
+    const int sb = cdiv(n, kSortTile);
+    const int m = 256 * sb;
+    s.hist.ensure((size_t)m);
+    int cur = 0;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 8 * pass;
+        k_radix_hist<<<sb, kBlock, 0, st>>>(n, shift, s.keys[cur].ptr, s.hist.ptr, sb);
+        exclusive_scan(s, s.hist.ptr, m, st);
+        k_radix_scatter<<<sb, kBlock, 0, st>>>(n, shift, s.keys[cur].ptr, s.vals[cur].ptr,
+                                               s.keys[1 - cur].ptr, s.vals[1 - cur].ptr, s.hist.ptr, sb);
+        cur = 1 - cur;
+    }
+    if (cur != 0) {  // keep sorted data in slot 0 (4 passes: already back in 0)
+        std::swap(s.keys[0], s.keys[1]);
+        std::swap(s.vals[0], s.vals[1]);
+    }
+    if (n > 1) {
+        k_karras<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n, s.keys[0].ptr, s.children.ptr,
+                                                          s.node_parent.ptr, s.leaf_parent.ptr);
+        RR_HIP(hipMemsetAsync(s.flags.ptr, 0, (size_t)(n - 1) * sizeof(uint32_t), st));
+    }
+    k_refit<<<nb, kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr, s.leaf_parent.ptr,
+                                   s.node_parent.ptr, s.children.ptr, s.flags.ptr, s.nodes.ptr,
+                                   s.tris.ptr);
+    RR_HIP(hipGetLastError());
+    s.built = true;
+}
+
+}  // namespace rr

@@ -1,0 +1,124 @@
+// Host-side interface of the device module: buffers in HBM and the launch
+// sequences of the LBVH build (bvh.hip) and the wavefront integrator
+// (wavefront.hip). DESIGN.md §4 describes the layout.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rr_device.h"
+
+namespace rr {
+
+struct HipError : std::runtime_error {
+    int code;
+    HipError(const std::string& what, int c) : std::runtime_error(what), code(c) {}
+};
+
+#define RR_HIP(call)                                                                             \
+    do {                                                                                         \
+        hipError_t _e = (call);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            throw ::rr::HipError(std::string(#call) + ": " + hipGetErrorString(_e), (int)_e);   \
+    } while (0)
+
+// Grow-only device allocation.
+template <typename T>
+struct DevBuf {
+    T* ptr = nullptr;
+    size_t cap = 0;  // elements
+    void ensure(size_t n) {
+        if (n <= cap) return;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+        if (n == 0) return;
+        RR_HIP(hipMalloc(&ptr, n * sizeof(T)));
+        cap = n;
+    }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+};
+
+// Per-scene geometry + acceleration structure.
+struct DevScene {
+    int n_tris = 0;
+    int n_objs = 0;
+    DevBuf<float4> tri_local;  // 3 per triangle, object space
+    DevBuf<int32_t> tri_obj;
+    DevBuf<int32_t> tri_mat;
+    DevBuf<float> obj_xform;   // 12 per object
+    DevBuf<float4> tri_world;  // 3 per triangle, world space (this frame)
+    // LBVH build scratch
+    DevBuf<uint32_t> bounds;    // 6 ordered-uint words (centroid-sum AABB)
+    DevBuf<uint32_t> keys[2], vals[2];
+    DevBuf<uint32_t> hist;      // 256 * nblocks
+    DevBuf<uint32_t> scan_part; // partial sums of the scan
+    DevBuf<int2> children;      // n-1
+    DevBuf<int32_t> node_parent;  // n-1 : parent*2+side, -1 root
+    DevBuf<int32_t> leaf_parent;  // n
+    DevBuf<uint32_t> flags;       // n-1 arrival counters
+    // acceleration structure consumed by traversal
+    DevBuf<BvhNode> nodes;  // max(n-1, 1)
+    DevBuf<TriPack> tris;   // n, leaf order
+    std::vector<float> cached_xform;  // obj_xform of the current build
+    bool built = false;
+    bool uploaded = false;
+    void release();
+};
+
+// Per-context wavefront state (sized for the largest chunk seen).
+struct DevPaths {
+    size_t cap = 0;
+    DevBuf<float4> ray_o, ray_d, hit, thr, rad, sh_o, sh_d, sh_c;
+    DevBuf<int32_t> q[2], sq;
+    DevBuf<int32_t> counters;  // per chunk: [ext 0..B+1 | shadow 0..B]
+    DevBuf<int32_t> spill;     // traversal stack spill
+    DevBuf<float4> film;
+    DevBuf<uint8_t> rgba8;
+    DevBuf<float> filter_table;
+    DevBuf<float> srgb_lut;
+    DevBuf<float> lights, materials;
+    int grid_blocks = 0;  // persistent grid for path kernels
+    void ensure_paths(size_t n);
+    void release();
+};
+
+// Frame constants passed by value to the path kernels.
+struct FrameConsts {
+    float3 cam_pos, cam_right, cam_up, cam_back;
+    float half_w, half_h, clip_start, clip_end;
+    float inv_w2, inv_h2;  // 2/W, 2/H
+    int W, H, npix;
+    int spp_total, spp_chunk, first_sample, max_bounces, n_lights;
+    uint32_t seed;
+    float clamp_indirect, exposure_scale, inv_spp;
+    int view_transform;
+    float3 world;
+    int n_tris;
+};
+
+// LBVH build for the current obj_xform (uploaded by the caller).
+// Stream-ordered; no host synchronisation inside.
+void build_lbvh(DevScene& s, hipStream_t st);
+
+// Render all chunks of one frame: film accumulate + tonemap to rgba8.
+// counters_per_chunk receives the device counter layout for stats.
+void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int n_chunks,
+                         hipStream_t st);
+
+// Trace a batch of rays (debug / parity entry point).
+void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, float4* d_hits,
+                        int32_t* d_prims, uint8_t* d_occ, hipStream_t st);
+
+int counters_per_chunk(int max_bounces);
+int device_cu_count();
+
+}  // namespace rr

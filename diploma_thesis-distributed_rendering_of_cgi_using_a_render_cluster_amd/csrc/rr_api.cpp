@@ -1,0 +1,588 @@
+// C ABI of the renderer (include/rr.h). One rr_ctx per GPU; one rr_scene per
+// exported project, cached for the worker's lifetime.
+//
+// Reference behaviour mirrored here (BlenderJobRunner::render_frame,
+// /root/reference/worker/src/rendering/runner/mod.rs:72-203 and
+// scripts/render-timing-script.py:13-100):
+//  * loaded_at            <- time the frame request starts (scene already loaded;
+//                            the reference pays a Blender start + .blend read here)
+//  * frame_set(N)         -> host animation evaluation (scene.cpp)
+//  * started_rendering_at <- before the device work (script :86)
+//  * render               -> LBVH build (if transforms changed) + wavefront
+//  * finished_rendering_at = file_saving_started_at <- after the 8-bit image is on
+//                            the host (utilities.rs:185-192)
+//  * write_still          -> JPEG/PNG encode + write, "<path>.jpg|.png"
+//  * file_saving_finished_at <- after the write (utilities.rs:195-198)
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "device.hpp"
+#include "image_io.hpp"
+#include "rr.h"
+#include "scene.hpp"
+
+using namespace rr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+double unix_now() {
+    using namespace std::chrono;
+    return duration_cast<duration<double>>(system_clock::now().time_since_epoch()).count();
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+struct PinnedBuf {
+    uint8_t* ptr = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap) return;
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+        RR_HIP(hipHostMalloc(reinterpret_cast<void**>(&ptr), n, hipHostMallocDefault));
+        cap = n;
+    }
+    ~PinnedBuf() {
+        if (ptr) (void)hipHostFree(ptr);
+    }
+};
+
+}  // namespace
+
+struct rr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    DevPaths paths;
+    PinnedBuf host_rgba;
+    std::vector<float> filter_cache;
+    float filter_width_cached = -1.f;
+    bool srgb_uploaded = false;
+};
+
+struct rr_scene {
+    rr_ctx* ctx = nullptr;
+    SceneDesc desc;
+    DevScene dev;
+};
+
+namespace {
+
+// Catch-all wrapper: C++ exceptions never cross the C ABI.
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const HipError& e) {
+        return fail(RR_ENODEV, e.what());
+    } catch (const std::bad_alloc&) {
+        return fail(RR_ENOMEM, "out of host memory");
+    } catch (const std::exception& e) {
+        return fail(RR_EINVAL, e.what());
+    }
+}
+
+void set_device(rr_ctx* c) { RR_HIP(hipSetDevice(c->device)); }
+
+// One-time upload of the scene's object-space triangles.
+void upload_scene(rr_ctx* c, rr_scene* s) {
+    set_device(c);
+    DevScene& d = s->dev;
+    if (d.uploaded) return;
+    if (d.n_tris > 0) {
+        d.tri_local.ensure((size_t)3 * d.n_tris);
+        d.tri_obj.ensure((size_t)d.n_tris);
+        d.tri_mat.ensure((size_t)d.n_tris);
+        RR_HIP(hipMemcpy(d.tri_local.ptr, s->desc.tri_local.data(), s->desc.tri_local.size() * sizeof(float),
+                         hipMemcpyHostToDevice));
+        RR_HIP(hipMemcpy(d.tri_obj.ptr, s->desc.tri_obj.data(), d.n_tris * sizeof(int32_t), hipMemcpyHostToDevice));
+        RR_HIP(hipMemcpy(d.tri_mat.ptr, s->desc.tri_mat.data(), d.n_tris * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    d.uploaded = true;
+}
+
+// A scene is used with exactly one context; a host-only handle binds on first use.
+void bind_scene(rr_ctx* c, rr_scene* s) {
+    if (s->ctx && s->ctx != c) throw std::runtime_error("scene belongs to another context");
+    s->ctx = c;
+    upload_scene(c, s);
+}
+
+// Upload per-frame constants and (re)build the LBVH if object transforms changed.
+bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs) {
+    bind_scene(c, s);
+    hipStream_t st = c->stream;
+    DevPaths& p = c->paths;
+    // tables (built on the host once; identical construction in the oracle)
+    if (c->filter_width_cached != fs.filter_width) {
+        c->filter_cache.assign(kFilterTableSize, 0.f);
+        build_filter_table(fs.filter_width, c->filter_cache.data());
+        p.filter_table.ensure(kFilterTableSize);
+        RR_HIP(hipMemcpy(p.filter_table.ptr, c->filter_cache.data(), kFilterTableSize * sizeof(float),
+                         hipMemcpyHostToDevice));
+        c->filter_width_cached = fs.filter_width;
+    }
+    if (!c->srgb_uploaded) {
+        std::vector<float> lut(kSrgbLutSize + 1);
+        build_srgb_lut(lut.data());
+        p.srgb_lut.ensure(lut.size());
+        RR_HIP(hipMemcpy(p.srgb_lut.ptr, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice));
+        c->srgb_uploaded = true;
+    }
+    const size_t nl = fs.lights.size(), nm = fs.materials.size();
+    p.lights.ensure(nl ? nl : 1);
+    p.materials.ensure(nm ? nm : 1);
+    if (nl) RR_HIP(hipMemcpyAsync(p.lights.ptr, fs.lights.data(), nl * sizeof(float), hipMemcpyHostToDevice, st));
+    RR_HIP(hipMemcpyAsync(p.materials.ptr, fs.materials.data(), nm * sizeof(float), hipMemcpyHostToDevice, st));
+    DevScene& d = s->dev;
+    const bool rebuild = !d.built || d.cached_xform != fs.obj_xform;
+    if (rebuild && d.n_tris > 0) {
+        d.obj_xform.ensure(fs.obj_xform.size());
+        RR_HIP(hipMemcpyAsync(d.obj_xform.ptr, fs.obj_xform.data(), fs.obj_xform.size() * sizeof(float),
+                              hipMemcpyHostToDevice, st));
+        build_lbvh(d, st);
+        d.cached_xform = fs.obj_xform;
+    } else if (rebuild) {
+        d.built = true;
+        d.cached_xform = fs.obj_xform;
+    }
+    return rebuild;
+}
+
+FrameConsts make_consts(const FrameSetup& fs, int n_tris) {
+    FrameConsts k{};
+    k.cam_pos = make_float3(fs.cam[0], fs.cam[1], fs.cam[2]);
+    k.cam_right = make_float3(fs.cam[3], fs.cam[4], fs.cam[5]);
+    k.cam_up = make_float3(fs.cam[6], fs.cam[7], fs.cam[8]);
+    k.cam_back = make_float3(fs.cam[9], fs.cam[10], fs.cam[11]);
+    k.half_w = fs.cam[12];
+    k.half_h = fs.cam[13];
+    k.clip_start = fs.cam[14];
+    k.clip_end = fs.cam[15];
+    k.inv_w2 = 2.0f / (float)fs.W;
+    k.inv_h2 = 2.0f / (float)fs.H;
+    k.W = fs.W;
+    k.H = fs.H;
+    k.npix = fs.W * fs.H;
+    k.spp_total = fs.spp;
+    k.max_bounces = fs.max_bounces;
+    k.n_lights = (int)(fs.lights.size() / RR_LIGHT_FLOATS);
+    k.seed = fs.seed;
+    k.clamp_indirect = fs.clamp_indirect;
+    k.exposure_scale = fs.exposure_scale;
+    k.inv_spp = 1.0f / (float)fs.spp;
+    k.view_transform = fs.view_transform;
+    k.world = make_float3(fs.world[0], fs.world[1], fs.world[2]);
+    k.n_tris = n_tris;
+    return k;
+}
+
+int choose_spp_chunk(const FrameSetup& fs) {
+    if (fs.spp_per_chunk > 0) return std::min(fs.spp_per_chunk, fs.spp);
+    // ~16M paths in flight: fills 256 CUs many times over and keeps the SoA
+    // path state (~140 B/path, ~2.3 GB) well inside HBM.
+    const long target = 16L << 20;
+    long c = target / std::max(1, fs.W * fs.H);
+    if (c < 1) c = 1;
+    if (c > fs.spp) c = fs.spp;
+    return (int)c;
+}
+
+struct FrameRun {
+    int W, H, chunks, spp_chunk;
+    bool rebuilt;
+    float build_ms, trace_ms, readback_ms;
+    std::vector<int32_t> counters;
+};
+
+// Run the device part of one frame; leaves the 8-bit image in c->host_rgba.
+FrameRun run_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, float* film_out) {
+    set_device(c);
+    FrameRun r{};
+    r.W = fs.W;
+    r.H = fs.H;
+    hipStream_t st = c->stream;
+    RR_HIP(hipEventRecord(c->ev[0], st));
+    r.rebuilt = prepare_frame(c, s, fs);
+    RR_HIP(hipEventRecord(c->ev[1], st));
+    FrameConsts k = make_consts(fs, s->dev.n_tris);
+    r.spp_chunk = choose_spp_chunk(fs);
+    r.chunks = (fs.spp + r.spp_chunk - 1) / r.spp_chunk;
+    k.spp_chunk = r.spp_chunk;
+    render_frame_device(s->dev, c->paths, k, r.chunks, st);
+    RR_HIP(hipEventRecord(c->ev[2], st));
+    const size_t npix = (size_t)fs.W * fs.H;
+    c->host_rgba.ensure(npix * 4);
+    RR_HIP(hipMemcpyAsync(c->host_rgba.ptr, c->paths.rgba8.ptr, npix * 4, hipMemcpyDeviceToHost, st));
+    const int cpc = counters_per_chunk(fs.max_bounces);
+    r.counters.resize((size_t)cpc * r.chunks);
+    RR_HIP(hipMemcpyAsync(r.counters.data(), c->paths.counters.ptr, r.counters.size() * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, st));
+    if (film_out)
+        RR_HIP(hipMemcpyAsync(film_out, c->paths.film.ptr, npix * sizeof(float4), hipMemcpyDeviceToHost, st));
+    RR_HIP(hipEventRecord(c->ev[3], st));
+    RR_HIP(hipStreamSynchronize(st));
+    RR_HIP(hipEventElapsedTime(&r.build_ms, c->ev[0], c->ev[1]));
+    RR_HIP(hipEventElapsedTime(&r.trace_ms, c->ev[1], c->ev[2]));
+    RR_HIP(hipEventElapsedTime(&r.readback_ms, c->ev[2], c->ev[3]));
+    if (film_out) {  // film holds sums; report the mean
+        const float inv = 1.0f / (float)fs.spp;
+        for (size_t i = 0; i < npix; ++i) {
+            float* f = film_out + 4 * i;
+            f[0] = f[0] * inv;
+            f[1] = f[1] * inv;
+            f[2] = f[2] * inv;
+            f[3] = 1.0f;
+        }
+    }
+    return r;
+}
+
+void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int n_tris) {
+    if (!st) return;
+    std::memset(st, 0, sizeof *st);
+    st->width = fs.W;
+    st->height = fs.H;
+    st->spp = fs.spp;
+    st->chunks = r.chunks;
+    st->camera_rays = (uint64_t)fs.W * fs.H * fs.spp;
+    const int cpc = counters_per_chunk(fs.max_bounces);
+    for (int c = 0; c < r.chunks; ++c) {
+        const int32_t* ext = &r.counters[(size_t)cpc * c];
+        const int32_t* shc = ext + fs.max_bounces + 2;
+        for (int b = 1; b <= fs.max_bounces; ++b) st->extension_rays += (uint64_t)ext[b];
+        for (int b = 0; b <= fs.max_bounces; ++b) st->shadow_rays += (uint64_t)shc[b];
+    }
+    st->build_ms = r.rebuilt ? r.build_ms : 0.0;
+    st->trace_ms = r.trace_ms;
+    st->readback_ms = r.readback_ms;
+    st->bvh_rebuilt = r.rebuilt ? 1 : 0;
+    st->n_triangles = n_tris;
+}
+
+int do_encode(const uint8_t* rgba, int W, int H, const char* out_path, const char* format, int quality,
+              uint64_t* bytes) {
+    if (!out_path || !format) return fail(RR_EINVAL, "out_path and format are required");
+    const std::string fmt(format);
+    std::vector<uint8_t> data;
+    std::string ext;
+    if (fmt == "JPEG") {
+        if (quality < 1 || quality > 100) return fail(RR_EINVAL, "jpeg_quality must be 1..100");
+        if (!encode_jpeg(rgba, W, H, quality, data)) return fail(RR_EINVAL, "JPEG encode failed");
+        ext = ".jpg";
+    } else if (fmt == "PNG") {
+        if (!encode_png(rgba, W, H, data, 1)) return fail(RR_EIO, "PNG encode failed");
+        ext = ".png";
+    } else {
+        return fail(RR_ENOTSUP, "unsupported output format '" + fmt + "' (JPEG and PNG are supported)");
+    }
+    const std::string path = std::string(out_path) + ext;
+    if (!write_file(path, data)) return fail(RR_EIO, "cannot write " + path + ": " + std::strerror(errno));
+    if (bytes) *bytes = data.size();
+    return RR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void rr_render_params_default(rr_render_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof *p);
+    p->spp = 0;
+    p->max_bounces = -1;
+    p->clamp_indirect = -1.0f;
+    p->seed = 0;
+    p->use_scene_seed = 1;
+    p->width = 0;
+    p->height = 0;
+    p->view_transform = RR_VIEW_SCENE;
+    p->spp_per_chunk = 0;
+}
+
+int32_t rr_abi_version(void) { return RR_ABI_VERSION; }
+
+const char* rr_last_error(rr_ctx*) { return g_err.c_str(); }
+
+int rr_create(int device_ordinal, rr_ctx** out) {
+    if (!out) return fail(RR_EINVAL, "out is NULL");
+    *out = nullptr;
+    return guarded([&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RR_ENODEV, "no HIP device available");
+        if (device_ordinal < 0 || device_ordinal >= n)
+            return fail(RR_ENODEV, "device ordinal " + std::to_string(device_ordinal) + " out of range (" +
+                                       std::to_string(n) + " visible)");
+        std::unique_ptr<rr_ctx> c(new rr_ctx());
+        c->device = device_ordinal;
+        set_device(c.get());
+        RR_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        for (auto& e : c->ev) RR_HIP(hipEventCreate(&e));
+        *out = c.release();
+        return RR_OK;
+    });
+}
+
+void rr_destroy(rr_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->paths.release();
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int rr_scene_load(rr_ctx* c, const char* path, rr_scene** out) {
+    if (!path || !out) return fail(RR_EINVAL, "NULL argument");
+    *out = nullptr;
+    {
+        FILE* f = std::fopen(path, "rb");
+        if (!f) return fail(RR_ENOENT, std::string("scene file doesn't exist: ") + path);
+        std::fclose(f);
+    }
+    return guarded([&] {
+        std::unique_ptr<rr_scene> s(new rr_scene());
+        s->ctx = c;  // NULL: host-only handle, bound to a context at its first render
+        s->desc = load_scene(path);
+        s->dev.n_tris = (int)s->desc.tri_obj.size();
+        s->dev.n_objs = (int)s->desc.objects.size();
+        if (c) upload_scene(c, s.get());
+        *out = s.release();
+        return RR_OK;
+    });
+}
+
+void rr_scene_free(rr_scene* s) {
+    if (!s) return;
+    if (s->ctx) {
+        (void)hipSetDevice(s->ctx->device);
+        if (s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
+    }
+    s->dev.release();
+    delete s;
+}
+
+int rr_scene_resolution(rr_scene* s, const rr_render_params* p, int32_t* w, int32_t* h) {
+    if (!s) return fail(RR_EINVAL, "scene is NULL");
+    return guarded([&] {
+        rr_render_params d;
+        rr_render_params_default(&d);
+        const RenderDesc& r = s->desc.render;
+        const int W = (p && p->width > 0) ? p->width : (r.resx * r.percent) / 100;
+        const int H = (p && p->height > 0) ? p->height : (r.resy * r.percent) / 100;
+        if (w) *w = W;
+        if (h) *h = H;
+        return RR_OK;
+    });
+}
+
+int rr_render_frame(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_params* params, const char* out_path,
+                    const char* format, int32_t jpeg_quality, rr_frame_timing* timing, rr_frame_stats* stats) {
+    if (!c || !s) return fail(RR_EINVAL, "NULL ctx or scene");
+    if (s->ctx && s->ctx != c) return fail(RR_EINVAL, "scene belongs to another context");
+    if (out_path && !format) return fail(RR_EINVAL, "format is required when out_path is given");
+    if (format && std::string(format) != "JPEG" && std::string(format) != "PNG")
+        return fail(RR_ENOTSUP, std::string("unsupported output format '") + format + "'");
+    return guarded([&] {
+        const auto t_call = std::chrono::steady_clock::now();
+        rr_frame_timing tm{};
+        tm.loaded_at = unix_now();
+        const auto t_anim = std::chrono::steady_clock::now();
+        FrameSetup fs = setup_frame(s->desc, frame, params);
+        const double anim_ms = ms_since(t_anim);
+        tm.started_rendering_at = unix_now();
+        FrameRun r = run_frame(c, s, fs, nullptr);
+        tm.finished_rendering_at = unix_now();
+        tm.file_saving_started_at = tm.finished_rendering_at;
+        uint64_t bytes = 0;
+        const auto t_enc = std::chrono::steady_clock::now();
+        if (out_path) {
+            const int rc = do_encode(c->host_rgba.ptr, fs.W, fs.H, out_path, format, jpeg_quality, &bytes);
+            if (rc != RR_OK) return rc;
+        }
+        const double enc_ms = ms_since(t_enc);
+        tm.file_saving_finished_at = unix_now();
+        if (timing) *timing = tm;
+        if (stats) {
+            fill_stats(stats, fs, r, s->dev.n_tris);
+            stats->anim_ms = anim_ms;
+            stats->encode_ms = enc_ms;
+            stats->output_bytes = bytes;
+            stats->total_ms = ms_since(t_call);
+        }
+        return RR_OK;
+    });
+}
+
+int rr_render_frame_to_memory(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_params* params,
+                              float* film, uint8_t* rgba8, rr_frame_stats* stats) {
+    if (!c || !s) return fail(RR_EINVAL, "NULL ctx or scene");
+    if (s->ctx && s->ctx != c) return fail(RR_EINVAL, "scene belongs to another context");
+    return guarded([&] {
+        const auto t_call = std::chrono::steady_clock::now();
+        FrameSetup fs = setup_frame(s->desc, frame, params);
+        FrameRun r = run_frame(c, s, fs, film);
+        if (rgba8) std::memcpy(rgba8, c->host_rgba.ptr, (size_t)fs.W * fs.H * 4);
+        if (stats) {
+            fill_stats(stats, fs, r, s->dev.n_tris);
+            stats->total_ms = ms_since(t_call);
+        }
+        return RR_OK;
+    });
+}
+
+int rr_encode_image(const uint8_t* rgba8, int32_t w, int32_t h, const char* out_path, const char* format,
+                    int32_t quality, uint64_t* bytes) {
+    if (!rgba8 || w <= 0 || h <= 0) return fail(RR_EINVAL, "bad image");
+    return guarded([&] { return do_encode(rgba8, w, h, out_path, format, quality, bytes); });
+}
+
+int rr_debug_counts(rr_scene* s, int32_t* nt, int32_t* nl, int32_t* nm, int32_t* no) {
+    if (!s) return fail(RR_EINVAL, "scene is NULL");
+    int lights = 0;
+    for (auto& o : s->desc.objects) lights += o.type == OBJ_LIGHT;
+    if (nt) *nt = (int32_t)s->desc.tri_obj.size();
+    if (nl) *nl = lights;
+    if (nm) *nm = (int32_t)s->desc.materials.size();
+    if (no) *no = (int32_t)s->desc.objects.size();
+    return RR_OK;
+}
+
+int rr_debug_frame_state(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_params* params, float* tris_world,
+                         int32_t* tri_material, float* camera, float* lights, float* materials, float* world,
+                         int32_t* render_ints, float* render_floats) {
+    if (!s) return fail(RR_EINVAL, "NULL scene");
+    if (!c && tris_world) return fail(RR_EINVAL, "world triangles need a device context");
+    return guarded([&] {
+        FrameSetup fs = setup_frame(s->desc, frame, params);
+        const int n = s->dev.n_tris;
+        if (c) {  // host-only queries (c == NULL) skip the device part
+            set_device(c);
+            prepare_frame(c, s, fs);
+        }
+        if (tris_world && n > 0) {
+            std::vector<float4> w((size_t)3 * n);
+            RR_HIP(hipMemcpyAsync(w.data(), s->dev.tri_world.ptr, w.size() * sizeof(float4), hipMemcpyDeviceToHost,
+                                  c->stream));
+            RR_HIP(hipStreamSynchronize(c->stream));
+            for (size_t i = 0; i < w.size(); ++i) {
+                tris_world[3 * i] = w[i].x;
+                tris_world[3 * i + 1] = w[i].y;
+                tris_world[3 * i + 2] = w[i].z;
+            }
+        }
+        if (c) RR_HIP(hipStreamSynchronize(c->stream));
+        if (tri_material) std::memcpy(tri_material, s->desc.tri_mat.data(), n * sizeof(int32_t));
+        if (camera) std::memcpy(camera, fs.cam, sizeof fs.cam);
+        if (lights && !fs.lights.empty()) std::memcpy(lights, fs.lights.data(), fs.lights.size() * sizeof(float));
+        if (materials) std::memcpy(materials, fs.materials.data(), fs.materials.size() * sizeof(float));
+        if (world) std::memcpy(world, fs.world, sizeof fs.world);
+        if (render_ints) {
+            const int32_t ri[RR_RENDER_INTS] = {fs.W, fs.H, fs.spp, fs.max_bounces, (int32_t)fs.seed,
+                                               fs.view_transform, choose_spp_chunk(fs), 0};
+            std::memcpy(render_ints, ri, sizeof ri);
+        }
+        if (render_floats) {
+            const float rf[RR_RENDER_FLOATS] = {fs.clamp_indirect, fs.filter_width, fs.exposure_scale, 0.f};
+            std::memcpy(render_floats, rf, sizeof rf);
+        }
+        return RR_OK;
+    });
+}
+
+int rr_debug_bvh(rr_ctx* c, rr_scene* s, int32_t frame, uint32_t* keys, uint32_t* order, int32_t* children,
+                 float* boxes) {
+    if (!c || !s) return fail(RR_EINVAL, "NULL ctx or scene");
+    return guarded([&] {
+        FrameSetup fs = setup_frame(s->desc, frame, nullptr);
+        set_device(c);
+        prepare_frame(c, s, fs);
+        DevScene& d = s->dev;
+        const int n = d.n_tris;
+        hipStream_t st = c->stream;
+        if (n > 0) {
+            if (keys) RR_HIP(hipMemcpyAsync(keys, d.keys[0].ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            if (order) RR_HIP(hipMemcpyAsync(order, d.vals[0].ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            const int ni = n > 1 ? n - 1 : 1;
+            std::vector<BvhNode> nodes((size_t)ni);
+            RR_HIP(hipMemcpyAsync(nodes.data(), d.nodes.ptr, ni * sizeof(BvhNode), hipMemcpyDeviceToHost, st));
+            RR_HIP(hipStreamSynchronize(st));
+            for (int i = 0; i < ni; ++i) {
+                const float* f = reinterpret_cast<const float*>(&nodes[i]);
+                if (boxes) std::memcpy(boxes + 12 * i, f, 12 * sizeof(float));
+                if (children) {
+                    children[2 * i] = nodes[i].d.x;
+                    children[2 * i + 1] = nodes[i].d.y;
+                }
+            }
+        }
+        RR_HIP(hipStreamSynchronize(st));
+        return RR_OK;
+    });
+}
+
+int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t n, const float* rays, float* hits, int32_t* prims,
+                   uint8_t* occluded) {
+    if (!c || !s || n < 0 || (n > 0 && !rays)) return fail(RR_EINVAL, "bad arguments");
+    return guarded([&] {
+        FrameSetup fs = setup_frame(s->desc, frame, nullptr);
+        set_device(c);
+        prepare_frame(c, s, fs);
+        hipStream_t st = c->stream;
+        DevBuf<float4> dr, dh;
+        DevBuf<int32_t> dp;
+        DevBuf<uint8_t> dq;
+        const size_t m = n > 0 ? (size_t)n : 1;
+        dr.ensure(2 * m);
+        dh.ensure(m);
+        dp.ensure(m);
+        dq.ensure(m);
+        if (n > 0) RR_HIP(hipMemcpyAsync(dr.ptr, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice, st));
+        trace_batch_device(s->dev, c->paths, n, dr.ptr, dh.ptr, dp.ptr, dq.ptr, st);
+        std::vector<float4> h(m);
+        if (n > 0) {
+            RR_HIP(hipMemcpyAsync(h.data(), dh.ptr, n * sizeof(float4), hipMemcpyDeviceToHost, st));
+            if (prims) RR_HIP(hipMemcpyAsync(prims, dp.ptr, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            if (occluded) RR_HIP(hipMemcpyAsync(occluded, dq.ptr, n, hipMemcpyDeviceToHost, st));
+        }
+        RR_HIP(hipStreamSynchronize(st));
+        if (hits)
+            for (int i = 0; i < n; ++i) {
+                hits[4 * i] = h[i].x;
+                hits[4 * i + 1] = h[i].y;
+                hits[4 * i + 2] = h[i].z;
+                hits[4 * i + 3] = 0.0f;
+            }
+        dr.release(); dh.release(); dp.release(); dq.release();
+        return RR_OK;
+    });
+}
+
+int rr_debug_object_matrix(rr_scene* s, int32_t obj, double frame, double* m16) {
+    if (!s || !m16) return fail(RR_EINVAL, "NULL argument");
+    return guarded([&] {
+        object_matrix(s->desc, obj, frame, m16);
+        return RR_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,410 @@
+// Device-side building blocks of the MI355X path tracer.
+//
+// Every floating-point expression here is written in the exact operation order
+// of the CPU oracle (oracle/rr_oracle.c), compiled with contraction OFF on both
+// sides (-ffp-contract=off plus the pragma below), IEEE division/sqrt (hipcc's
+// default correctly rounded f32 div/sqrt), and no libm transcendentals on the
+// per-sample path (sin/cos by the fixed polynomial of sincos_small, sRGB by a
+// host-built table). That makes the GPU image reproducible bit for bit by the
+// oracle (tests/test_gpu_parity.py).
+//
+// The reference has no renderer of its own: this replaces Blender Cycles'
+// CPU path integration behind bpy.ops.render.render
+// (/root/reference/scripts/render-timing-script.py:90).
+#pragma once
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RR_HD __host__ __device__ __forceinline__
+#define RR_D __device__ __forceinline__
+
+namespace rr {
+
+// ---------------------------------------------------------------- layout ---
+// BVH2 node, 64 B = one cache line. The two CHILD boxes live in the parent, so
+// one node fetch decides both children (Karras LBVH, internal nodes 0..n-2).
+//   f[0..2] left min   f[3..5] left max   f[6..8] right min  f[9..11] right max
+//   i[12] left child   i[13] right child  (child < 0: leaf ~sorted_index)
+struct alignas(16) BvhNode {
+    float4 a, b, c;
+    int4 d;
+};
+static_assert(sizeof(BvhNode) == 64, "node must be one 64-byte line");
+
+// Triangle in leaf order, 48 B: v0 | e1 = v1-v0 | e2 = v2-v0, with the original
+// triangle id and material id in the .w lanes.
+struct alignas(16) TriPack {
+    float4 p0;  // v0.xyz, orig id (int bits)
+    float4 p1;  // e1.xyz, material (int bits)
+    float4 p2;  // e2.xyz, 0
+};
+static_assert(sizeof(TriPack) == 48, "tri pack is 48 bytes");
+
+constexpr int kMaxLights = 64;
+constexpr int kBlock = 256;         // threads per block for all path kernels
+constexpr int kLdsStack = 16;       // traversal stack entries kept in LDS per lane
+constexpr int kSpillStack = 64;     // further entries in the per-thread HBM spill area
+constexpr int kDimsPerBounce = 8;   // RNG dimensions consumed per bounce
+constexpr int kRrStartBounce = 3;   // Russian roulette from this bounce on
+
+// --------------------------------------------------------------- vectors ---
+RR_HD float3 mk3(float x, float y, float z) { return make_float3(x, y, z); }
+RR_HD float3 add3(float3 a, float3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RR_HD float3 sub3(float3 a, float3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RR_HD float3 mul3(float3 a, float3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RR_HD float3 scl3(float3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+RR_HD float dot3(float3 a, float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RR_HD float3 cross3(float3 a, float3 b) {
+    return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+RR_HD float3 norm3(float3 a) {
+    const float inv = 1.0f / sqrtf(dot3(a, a));
+    return scl3(a, inv);
+}
+RR_HD float max3f(float3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
+RR_HD float3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
+
+RR_HD int f2i(float f) { return __builtin_bit_cast(int, f); }
+RR_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
+
+// ------------------------------------------------------------------- RNG ---
+// Counter-based: u(dim) = hash(key + (dim+1)*golden), key = f(seed, pixel, sample).
+// Independent of execution order, so wavefront (GPU) and scalar (oracle)
+// traversals of the same path draw identical numbers.
+RR_HD uint32_t hash_u32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+RR_HD uint32_t path_key(uint32_t seed, uint32_t pixel, uint32_t sample) {
+    const uint32_t k = hash_u32(hash_u32(seed) + pixel);
+    return hash_u32(k ^ (sample * 0x9E3779B9u + 0x7F4A7C15u));
+}
+RR_HD float rng(uint32_t key, uint32_t dim) {
+    return (float)(hash_u32(key + (dim + 1u) * 0x9E3779B9u) >> 8) * 5.9604644775390625e-08f;
+}
+
+// ------------------------------------------------------------- sampling ---
+// sin/cos on |x| <= pi/4 (Cephes sinf/cosf kernels), fixed op order.
+RR_HD void sincos_small(float x, float& s, float& c) {
+    const float z = x * x;
+    s = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x + x;
+    c = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z -
+        0.5f * z + 1.0f;
+}
+
+// Shirley-Chiu concentric square->disk map; angles stay in [-pi/4, pi/4].
+RR_HD void concentric_disk(float u1, float u2, float& x, float& y) {
+    const float a = 2.0f * u1 - 1.0f;
+    const float b = 2.0f * u2 - 1.0f;
+    if (a == 0.0f && b == 0.0f) {
+        x = 0.0f;
+        y = 0.0f;
+        return;
+    }
+    float s, c;
+    if (fabsf(a) > fabsf(b)) {
+        sincos_small(0.785398163397448f * (b / a), s, c);
+        x = a * c;
+        y = a * s;
+    } else {
+        sincos_small(0.785398163397448f * (a / b), s, c);
+        x = b * s;
+        y = b * c;
+    }
+}
+
+// Orthonormal basis (Duff et al. 2017, branchless).
+RR_HD void make_onb(float3 n, float3& b1, float3& b2) {
+    const float sign = copysignf(1.0f, n.z);
+    const float a = -1.0f / (sign + n.z);
+    const float b = n.x * n.y * a;
+    b1 = mk3(1.0f + sign * n.x * n.x * a, sign * b, -sign * n.x);
+    b2 = mk3(b, sign + n.y * n.y * a, -n.y);
+}
+
+// Self-intersection-safe ray origin (Waechter & Binder, Ray Tracing Gems ch. 6).
+RR_HD float offset_axis(float p, float n) {
+    const int of = (int)(256.0f * n);
+    const float pi = i2f(f2i(p) + ((p < 0.0f) ? -of : of));
+    return fabsf(p) < 0.03125f ? p + 1.52587890625e-05f * n : pi;
+}
+RR_HD float3 offset_ray(float3 p, float3 n) {
+    return mk3(offset_axis(p.x, n.x), offset_axis(p.y, n.y), offset_axis(p.z, n.z));
+}
+
+// Piecewise-linear table read, u in [0,1].
+RR_HD float table_lerp(const float* t, int n, float u) {
+    const float f = u * (float)(n - 1);
+    int i = (int)f;
+    if (i >= n - 1) return t[n - 1];
+    if (i < 0) i = 0;
+    const float fr = f - (float)i;
+    return t[i] + (t[i + 1] - t[i]) * fr;
+}
+
+// ---------------------------------------------------------- intersection ---
+// Slab test against [bmin,bmax]; inclusive so equal-t candidates survive (the
+// closest hit is then independent of traversal order, see closest_tri()).
+RR_HD bool slab(float3 o, float3 invd, float bx0, float by0, float bz0, float bx1, float by1,
+                float bz1, float tmin, float tmax, float& tnear) {
+    const float tx0 = (bx0 - o.x) * invd.x, tx1 = (bx1 - o.x) * invd.x;
+    const float ty0 = (by0 - o.y) * invd.y, ty1 = (by1 - o.y) * invd.y;
+    const float tz0 = (bz0 - o.z) * invd.z, tz1 = (bz1 - o.z) * invd.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    tnear = tn;
+    return tn <= tf;
+}
+
+// Moeller-Trumbore, two-sided. Returns t (and u, v) or false.
+RR_HD bool tri_test(float3 o, float3 d, float3 v0, float3 e1, float3 e2, float& t, float& u,
+                    float& v) {
+    const float3 pv = cross3(d, e2);
+    const float det = dot3(e1, pv);
+    if (det == 0.0f) return false;
+    const float inv = 1.0f / det;
+    const float3 tv = sub3(o, v0);
+    u = dot3(tv, pv) * inv;
+    if (u < 0.0f || u > 1.0f) return false;
+    const float3 qv = cross3(tv, e1);
+    v = dot3(d, qv) * inv;
+    if (v < 0.0f || u + v > 1.0f) return false;
+    t = dot3(e2, qv) * inv;
+    return true;
+}
+
+struct Hit {
+    float t, u, v;
+    int idx;   // leaf (sorted) index, -1 miss
+    int orig;  // original triangle id, -1 miss
+};
+
+// Accept rule making the closest hit order-independent: smaller t wins; equal t
+// -> smaller original id wins.
+RR_HD void closest_tri(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
+    float t, u, v;
+    if (!tri_test(o, d, xyz(tp.p0), xyz(tp.p1), xyz(tp.p2), t, u, v)) return;
+    const int orig = f2i(tp.p0.w);
+    if (t > tmin && (t < h.t || (t == h.t && orig < h.orig))) {
+        h.t = t;
+        h.u = u;
+        h.v = v;
+        h.idx = idx;
+        h.orig = orig;
+    }
+}
+
+// Traversal stack: kLdsStack entries in LDS ([entry][thread] -> conflict-free
+// ds_read_b32 across a wave), deeper entries in a per-thread HBM spill area.
+struct TravStack {
+    int* lds;       // &lds_base[threadIdx.x], stride kBlock
+    int* spill;     // &spill_base[global thread], stride spill_stride
+    int spill_stride;
+    int sp;
+    RR_D void push(int x) {
+        if (sp < kLdsStack) lds[sp * kBlock] = x;
+        else spill[(sp - kLdsStack) * spill_stride] = x;
+        ++sp;
+    }
+    RR_D int pop() {
+        --sp;
+        return sp < kLdsStack ? lds[sp * kBlock] : spill[(sp - kLdsStack) * spill_stride];
+    }
+};
+
+// Closest hit over the LBVH. Near child first (left on ties); leaf children are
+// intersected as soon as their box passes.
+template <bool kAnyHit, typename Stack>
+RR_D bool traverse(const BvhNode* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
+                   float3 o, float3 d, float tmin, float tmax, Stack& st, Hit& h,
+                   uint32_t* nodes_visited = nullptr, uint32_t* tris_tested = nullptr) {
+    h.t = tmax;
+    h.u = h.v = 0.0f;
+    h.idx = -1;
+    h.orig = -1;
+    if (n_tris <= 0) return false;
+    const float3 invd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int node = 0;
+    st.sp = 0;
+    for (;;) {
+        const BvhNode nd = nodes[node];
+        if (nodes_visited) ++*nodes_visited;
+        float tl, tr;
+        bool hl = slab(o, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
+        bool hr = slab(o, invd, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
+        const int cl = nd.d.x, cr = nd.d.y;
+        if (hl && cl < 0) {
+            if (tris_tested) ++*tris_tested;
+            closest_tri(tris[~cl], ~cl, o, d, tmin, h);
+            if (kAnyHit && h.idx >= 0) return true;
+            hl = false;
+        }
+        if (hr && cr < 0) {
+            if (tris_tested) ++*tris_tested;
+            closest_tri(tris[~cr], ~cr, o, d, tmin, h);
+            if (kAnyHit && h.idx >= 0) return true;
+            hr = false;
+        }
+        if (hl && hr) {
+            const bool left_first = tl <= tr;
+            st.push(left_first ? cr : cl);
+            node = left_first ? cl : cr;
+        } else if (hl) {
+            node = cl;
+        } else if (hr) {
+            node = cr;
+        } else {
+            if (st.sp == 0) break;
+            node = st.pop();
+        }
+    }
+    return h.idx >= 0;
+}
+
+// ------------------------------------------------------------ materials ---
+struct Mat {
+    float3 base;
+    float metallic, specular, roughness, ior;
+    float3 emission;
+    int model;  // 0 Principled subset, 1 pure Lambert (analytic test scenes)
+};
+
+RR_HD float schlick_w(float c) {
+    float m = 1.0f - c;
+    if (m < 0.0f) m = 0.0f;
+    const float m2 = m * m;
+    return m2 * m2 * m;
+}
+
+// Principled BSDF (v1) subset: Disney diffuse with retro-reflection + GGX
+// specular (Smith separable G, Schlick Fresnel from F0 = lerp(0.08*specular,
+// base, metallic)). Returns f and the combined one-sample-MIS pdf.
+RR_HD float3 bsdf_eval(const Mat& m, float3 N, float3 wo, float3 wi, float ps, float& pdf) {
+    const float cosV = dot3(N, wo);
+    const float cosL = dot3(N, wi);
+    if (cosV <= 0.0f || cosL <= 0.0f) {
+        pdf = 0.0f;
+        return mk3(0.0f, 0.0f, 0.0f);
+    }
+    if (m.model == 1) {
+        pdf = cosL * 0.318309886183791f;
+        return scl3(m.base, 0.318309886183791f);
+    }
+    const float3 H = norm3(add3(wo, wi));
+    const float cosD = dot3(wi, H);
+    const float NdotH = dot3(N, H);
+    float alpha = m.roughness * m.roughness;
+    if (alpha < 1.0e-4f) alpha = 1.0e-4f;
+    const float a2 = alpha * alpha;
+    // diffuse
+    const float fd90 = 0.5f + 2.0f * m.roughness * cosD * cosD;
+    const float fl = schlick_w(cosL);
+    const float fv = schlick_w(cosV);
+    const float kd = (1.0f - m.metallic) * 0.318309886183791f * (1.0f + (fd90 - 1.0f) * fl) *
+                     (1.0f + (fd90 - 1.0f) * fv);
+    // specular
+    const float tt = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
+    const float D = a2 / (3.14159265358979f * tt * tt);
+    const float g1v = 2.0f * cosV / (cosV + sqrtf(a2 + (1.0f - a2) * cosV * cosV));
+    const float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
+    const float s0 = 0.08f * m.specular;
+    const float3 F0 = mk3(s0 + (m.base.x - s0) * m.metallic, s0 + (m.base.y - s0) * m.metallic,
+                          s0 + (m.base.z - s0) * m.metallic);
+    const float fw = schlick_w(cosD);
+    const float ks = D * g1v * g1l / (4.0f * cosV * cosL);
+    const float3 F = mk3(F0.x + (1.0f - F0.x) * fw, F0.y + (1.0f - F0.y) * fw, F0.z + (1.0f - F0.z) * fw);
+    const float pdf_d = cosL * 0.318309886183791f;
+    const float pdf_s = g1v * D / (4.0f * cosV);
+    pdf = (1.0f - ps) * pdf_d + ps * pdf_s;
+    return mk3(m.base.x * kd + F.x * ks, m.base.y * kd + F.y * ks, m.base.z * kd + F.z * ks);
+}
+
+// Probability of picking the specular lobe.
+RR_HD float spec_prob(const Mat& m, float cosV) {
+    if (m.model == 1) return 0.0f;
+    const float s0 = 0.08f * m.specular;
+    const float f0avg = ((s0 + (m.base.x - s0) * m.metallic) + (s0 + (m.base.y - s0) * m.metallic) +
+                         (s0 + (m.base.z - s0) * m.metallic)) *
+                        0.333333343f;
+    const float wsp = f0avg + (1.0f - f0avg) * schlick_w(cosV);
+    const float wd = (1.0f - m.metallic) * ((m.base.x + m.base.y + m.base.z) * 0.333333343f);
+    const float tot = wsp + wd;
+    return tot > 0.0f ? wsp / tot : 1.0f;
+}
+
+// GGX visible-normal sample (Heitz 2018) in the local frame (N = +z).
+RR_HD float3 sample_vndf(float3 v, float alpha, float u1, float u2) {
+    const float3 vh = norm3(mk3(alpha * v.x, alpha * v.y, v.z));
+    const float lensq = vh.x * vh.x + vh.y * vh.y;
+    float3 t1;
+    if (lensq > 0.0f) {
+        const float il = 1.0f / sqrtf(lensq);
+        t1 = mk3(-vh.y * il, vh.x * il, 0.0f);
+    } else {
+        t1 = mk3(1.0f, 0.0f, 0.0f);
+    }
+    const float3 t2 = cross3(vh, t1);
+    float dx, dy;
+    concentric_disk(u1, u2, dx, dy);
+    const float s = 0.5f * (1.0f + vh.z);
+    dy = (1.0f - s) * sqrtf(fmaxf(0.0f, 1.0f - dx * dx)) + s * dy;
+    const float nz = sqrtf(fmaxf(0.0f, 1.0f - dx * dx - dy * dy));
+    const float3 nh = mk3(dx * t1.x + dy * t2.x + nz * vh.x, dx * t1.y + dy * t2.y + nz * vh.y,
+                          dx * t1.z + dy * t2.z + nz * vh.z);
+    return norm3(mk3(alpha * nh.x, alpha * nh.y, fmaxf(0.0f, nh.z)));
+}
+
+// Sample a direction; returns false when the path must end.
+RR_HD bool bsdf_sample(const Mat& m, float3 N, float3 wo, float ul, float u1, float u2,
+                       float3& wi, float3& f, float& pdf) {
+    const float cosV = dot3(N, wo);
+    if (cosV <= 0.0f) return false;
+    const float ps = spec_prob(m, cosV);
+    float3 T, B;
+    make_onb(N, T, B);
+    if (ul < ps) {
+        float alpha = m.roughness * m.roughness;
+        if (alpha < 1.0e-4f) alpha = 1.0e-4f;
+        const float3 wl = mk3(dot3(wo, T), dot3(wo, B), cosV);
+        const float3 hl = sample_vndf(wl, alpha, u1, u2);
+        const float3 H = mk3(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,
+                             T.z * hl.x + B.z * hl.y + N.z * hl.z);
+        const float k = 2.0f * dot3(wo, H);
+        wi = mk3(H.x * k - wo.x, H.y * k - wo.y, H.z * k - wo.z);
+    } else {
+        float x, y;
+        concentric_disk(u1, u2, x, y);
+        const float z = sqrtf(fmaxf(0.0f, 1.0f - x * x - y * y));
+        wi = mk3(T.x * x + B.x * y + N.x * z, T.y * x + B.y * y + N.y * z, T.z * x + B.z * y + N.z * z);
+    }
+    f = bsdf_eval(m, N, wo, wi, ps, pdf);
+    return pdf > 0.0f;
+}
+
+RR_HD float3 clamp_contrib(float3 c, float clamp) {
+    if (clamp > 0.0f) {
+        const float mx = max3f(c);
+        if (mx > clamp) return scl3(c, clamp / mx);
+    }
+    return c;
+}
+
+// sRGB OETF: linear segment below 0.0031308, host-built table above.
+RR_HD float srgb_oetf(float x, const float* lut, int lut_n) {
+    if (x <= 0.0031308f) return x * 12.92f;
+    return table_lerp(lut, lut_n + 1, x);
+}
+
+RR_HD uint8_t quantize8(float f) {
+    if (f <= 0.0f) return 0;
+    if (f >= 1.0f) return 255;
+    return (uint8_t)(f * 255.0f + 0.5f);
+}
+
+}  // namespace rr

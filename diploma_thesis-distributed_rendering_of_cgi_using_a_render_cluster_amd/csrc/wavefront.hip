@@ -1,0 +1,414 @@
+// Wavefront path tracer: per chunk of spp_chunk samples x all
+// pixels, K6 raygen -> { K7 closest-hit traversal -> K9 shade (+NEE setup,
+// ballot/popcount queue compaction) -> K10 shadow any-hit } x bounces ->
+// K11 film accumulate (+ K12 tonemap on the last chunk).
+//
+// Path state is SoA float4 in HBM; every path kernel is a persistent
+// grid-stride loop over a device-side queue count (no host round trip between
+// bounces, so a frame is one stream of launches). The arithmetic is the
+// uncontracted, libm-free form of rr_device.h and matches oracle/rr_oracle.c.
+//
+// Replaces the per-pixel, per-sample path integration of Cycles behind
+// bpy.ops.render.render (/root/reference/scripts/render-timing-script.py:90).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include "device.hpp"
+
+namespace rr {
+
+namespace {
+
+struct LightsMats {
+    const float* lights;     // n_lights * RR_LIGHT_FLOATS
+    const float* materials;  // RR_MAT_FLOATS each
+    const float* filter;     // kFilterTableSize
+    const float* srgb;       // kSrgbLutSize + 1
+};
+
+constexpr int kFilterN = 1024;
+constexpr int kSrgbN = 4096;
+constexpr int kLightF = 12;
+constexpr int kMatF = 12;
+
+__device__ __forceinline__ Mat load_mat(const float* __restrict__ mats, int id) {
+    const float* m = mats + kMatF * id;
+    Mat r;
+    r.base = mk3(m[0], m[1], m[2]);
+    r.metallic = m[3];
+    r.specular = m[4];
+    r.roughness = m[5];
+    r.ior = m[6];
+    r.emission = mk3(m[7], m[8], m[9]);
+    r.model = (int)m[10];
+    return r;
+}
+
+// Camera ray for (pixel, sample): filter-importance-sampled subpixel position,
+// pinhole through the sensor plane at unit distance, z-depth clipping.
+__device__ __forceinline__ void camera_ray(const FrameConsts& fc, const float* __restrict__ filt,
+                                           int pix, uint32_t key, float3& o, float3& d, float& tmin,
+                                           float& tmax) {
+    const int px = pix % fc.W;
+    const int py = pix / fc.W;
+    const float fx = (float)px + 0.5f + table_lerp(filt, kFilterN, rng(key, 0));
+    const float fy = (float)py + 0.5f + table_lerp(filt, kFilterN, rng(key, 1));
+    const float sx = (fx * fc.inv_w2 - 1.0f) * fc.half_w;
+    const float sy = (1.0f - fy * fc.inv_h2) * fc.half_h;
+    const float len = sqrtf(sx * sx + sy * sy + 1.0f);
+    const float3 dw = mk3(fc.cam_right.x * sx + fc.cam_up.x * sy - fc.cam_back.x,
+                          fc.cam_right.y * sx + fc.cam_up.y * sy - fc.cam_back.y,
+                          fc.cam_right.z * sx + fc.cam_up.z * sy - fc.cam_back.z);
+    const float il = 1.0f / len;
+    d = scl3(dw, il);
+    o = fc.cam_pos;
+    tmin = fc.clip_start * len;
+    tmax = fc.clip_end * len;
+}
+
+// K6
+__global__ __launch_bounds__(kBlock) void k_raygen(FrameConsts fc, const float* __restrict__ filt,
+                                                   float4* __restrict__ ray_o, float4* __restrict__ ray_d,
+                                                   float4* __restrict__ thr, float4* __restrict__ rad,
+                                                   int npaths) {
+    for (int p = blockIdx.x * kBlock + threadIdx.x; p < npaths; p += gridDim.x * kBlock) {
+        const int sl = p / fc.npix;
+        const int pix = p - sl * fc.npix;
+        const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
+        float3 o, d;
+        float tmin, tmax;
+        camera_ray(fc, filt, pix, key, o, d, tmin, tmax);
+        ray_o[p] = make_float4(o.x, o.y, o.z, tmin);
+        ray_d[p] = make_float4(d.x, d.y, d.z, tmax);
+        thr[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+        rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+}
+
+// K7 / K10: traverse rays of a queue. kAny: shadow rays (any hit, adds the
+// pending NEE contribution when unoccluded); else closest hit -> hit buffer.
+template <bool kAny>
+__global__ __launch_bounds__(kBlock) void k_trace(const BvhNode* __restrict__ nodes,
+                                                  const TriPack* __restrict__ tris, int n_tris,
+                                                  const int32_t* __restrict__ queue,
+                                                  const int32_t* __restrict__ count_ptr, int count_fixed,
+                                                  const float4* __restrict__ ray_o,
+                                                  const float4* __restrict__ ray_d,
+                                                  float4* __restrict__ hit, const float4* __restrict__ contrib,
+                                                  float4* __restrict__ rad, int32_t* __restrict__ spill) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    const int count = count_ptr ? *count_ptr : count_fixed;
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    const int nthreads = gridDim.x * kBlock;
+    TravStack st{&lds_stack[threadIdx.x], spill + gtid, nthreads, 0};
+    for (int i = gtid; i < count; i += nthreads) {
+        const int p = queue ? queue[i] : i;
+        const float4 ro = ray_o[p], rd = ray_d[p];
+        Hit h;
+        const bool any = traverse<kAny>(nodes, tris, n_tris, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
+        if (kAny) {
+            if (!any) {
+                const float4 c = contrib[p];
+                float4 L = rad[p];
+                L.x = L.x + c.x;
+                L.y = L.y + c.y;
+                L.z = L.z + c.z;
+                rad[p] = L;
+            }
+        } else {
+            hit[p] = make_float4(h.t, h.u, h.v, i2f(h.idx));
+        }
+    }
+}
+
+// Wave-aggregated queue append (ballot + popcount, one atomic per wave).
+__device__ __forceinline__ void wave_append(bool want, int value, int32_t* __restrict__ q,
+                                            int32_t* __restrict__ cnt) {
+    const uint64_t mask = __ballot(want);
+    if (mask == 0ull) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(cnt, __popcll(mask));
+    base = __shfl(base, leader);
+    if (want) {
+        const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        q[base + __popcll(mask & lt)] = value;
+    }
+}
+
+// K9: shade bounce b.
+__global__ __launch_bounds__(kBlock) void k_shade(FrameConsts fc, int bounce, LightsMats lm,
+                                                  const TriPack* __restrict__ tris,
+                                                  const int32_t* __restrict__ q_in,
+                                                  const int32_t* __restrict__ cnt_in, int count_fixed,
+                                                  int32_t* __restrict__ q_out, int32_t* __restrict__ cnt_out,
+                                                  int32_t* __restrict__ sq, int32_t* __restrict__ cnt_sh,
+                                                  float4* __restrict__ ray_o, float4* __restrict__ ray_d,
+                                                  const float4* __restrict__ hit, float4* __restrict__ thr,
+                                                  float4* __restrict__ rad, float4* __restrict__ sh_o,
+                                                  float4* __restrict__ sh_d, float4* __restrict__ sh_c) {
+    const int count = cnt_in ? *cnt_in : count_fixed;
+    const int lane = threadIdx.x & 63;
+    const int stride = gridDim.x * kBlock;
+    const uint32_t dim0 = 2u + (uint32_t)(kDimsPerBounce * bounce);
+    for (int i0 = blockIdx.x * kBlock + threadIdx.x - lane; i0 < count; i0 += stride) {
+        const int i = i0 + lane;
+        const bool active = i < count;
+        bool cont = false, shadow = false;
+        int p = 0;
+        if (active) {
+            p = q_in ? q_in[i] : i;
+            const float4 ro = ray_o[p], rd = ray_d[p], hv = hit[p];
+            const float4 T4 = thr[p];
+            float3 T = xyz(T4);
+            float4 L = rad[p];
+            const int idx = f2i(hv.w);
+            const float3 d = xyz(rd);
+            if (idx < 0) {
+                float3 c = mul3(T, fc.world);
+                if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
+                L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;
+                rad[p] = L;
+            } else {
+                const TriPack tp = tris[idx];
+                const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2);
+                const Mat m = load_mat(lm.materials, f2i(tp.p1.w));
+                const float t = hv.x;
+                const float3 P = mk3(ro.x + rd.x * t, ro.y + rd.y * t, ro.z + rd.z * t);
+                float3 N = norm3(cross3(e1, e2));
+                if (dot3(N, d) > 0.0f) N = mk3(-N.x, -N.y, -N.z);
+                const float3 wo = mk3(-d.x, -d.y, -d.z);
+                if (m.emission.x != 0.0f || m.emission.y != 0.0f || m.emission.z != 0.0f) {
+                    float3 c = mul3(T, m.emission);
+                    if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
+                    L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;
+                }
+                if (bounce < fc.max_bounces) {
+                    const int p_pix = p % fc.npix;
+                    const int p_smp = fc.first_sample + p / fc.npix;
+                    const uint32_t key = path_key(fc.seed, (uint32_t)p_pix, (uint32_t)p_smp);
+                    const float3 Po = offset_ray(P, N);
+                    // next-event estimation toward one uniformly chosen light
+                    if (fc.n_lights > 0) {
+                        int li = (int)(rng(key, dim0) * (float)fc.n_lights);
+                        if (li > fc.n_lights - 1) li = fc.n_lights - 1;
+                        const float* lt = lm.lights + kLightF * li;
+                        float3 wi;
+                        float dist;
+                        float3 Li;  // radiance x cos_light / pdf (solid angle), i.e. I*cos/d^2
+                        if (lt[0] == 0.0f) {  // point / disk light
+                            const float3 lp = mk3(lt[1], lt[2], lt[3]);
+                            const float radius = lt[7];
+                            const float3 I = mk3(lt[8], lt[9], lt[10]);
+                            const float3 tl = sub3(lp, P);
+                            const float dl2 = dot3(tl, tl);
+                            if (radius > 0.0f) {
+                                const float3 wl = scl3(tl, 1.0f / sqrtf(dl2));
+                                float3 b1, b2;
+                                make_onb(wl, b1, b2);
+                                float dx, dy;
+                                concentric_disk(rng(key, dim0 + 1u), rng(key, dim0 + 2u), dx, dy);
+                                dx = dx * radius;
+                                dy = dy * radius;
+                                const float3 sp = mk3(lp.x + b1.x * dx + b2.x * dy, lp.y + b1.y * dx + b2.y * dy,
+                                                      lp.z + b1.z * dx + b2.z * dy);
+                                const float3 ts = sub3(sp, P);
+                                const float ds2 = dot3(ts, ts);
+                                dist = sqrtf(ds2);
+                                wi = scl3(ts, 1.0f / dist);
+                                const float cl = fabsf(dot3(wl, wi));
+                                Li = scl3(I, cl / ds2);
+                            } else {
+                                dist = sqrtf(dl2);
+                                wi = scl3(tl, 1.0f / dist);
+                                Li = scl3(I, 1.0f / dl2);
+                            }
+                        } else {  // sun: delta direction, irradiance
+                            wi = mk3(-lt[4], -lt[5], -lt[6]);
+                            dist = 3.402823466e+38f;
+                            Li = mk3(lt[8], lt[9], lt[10]);
+                        }
+                        const float cosN = dot3(N, wi);
+                        if (cosN > 0.0f) {
+                            float pdf;
+                            const float ps = spec_prob(m, dot3(N, wo));
+                            const float3 f = bsdf_eval(m, N, wo, wi, ps, pdf);
+                            const float k = cosN * (float)fc.n_lights;
+                            float3 c = mk3(T.x * f.x * k * Li.x, T.y * f.y * k * Li.y, T.z * f.z * k * Li.z);
+                            if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
+                            if (max3f(c) > 0.0f) {
+                                shadow = true;
+                                sh_o[p] = make_float4(Po.x, Po.y, Po.z, 0.0f);
+                                sh_d[p] = make_float4(wi.x, wi.y, wi.z, dist);
+                                sh_c[p] = make_float4(c.x, c.y, c.z, 0.0f);
+                            }
+                        }
+                    }
+                    // continue the path
+                    float3 wi, f;
+                    float pdf;
+                    if (bsdf_sample(m, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi,
+                                    f, pdf)) {
+                        const float cosL = dot3(N, wi);
+                        if (cosL > 0.0f) {
+                            const float k = cosL / pdf;
+                            T = mk3(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
+                            bool alive = max3f(T) > 0.0f;
+                            if (alive && bounce >= kRrStartBounce) {
+                                const float q = fminf(max3f(T), 1.0f);
+                                if (rng(key, dim0 + 6u) >= q) alive = false;
+                                else T = mk3(T.x / q, T.y / q, T.z / q);
+                            }
+                            if (alive) {
+                                cont = true;
+                                ray_o[p] = make_float4(Po.x, Po.y, Po.z, 0.0f);
+                                ray_d[p] = make_float4(wi.x, wi.y, wi.z, 3.402823466e+38f);
+                                thr[p] = make_float4(T.x, T.y, T.z, 0.0f);
+                            }
+                        }
+                    }
+                }
+                rad[p] = L;
+            }
+        }
+        wave_append(cont, p, q_out, cnt_out);
+        wave_append(shadow, p, sq, cnt_sh);
+    }
+}
+
+// K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
+// sample order; then mean -> exposure -> view transform -> 8-bit.
+__global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, const float4* __restrict__ rad,
+                                                       float4* __restrict__ film, int first_chunk,
+                                                       int last_chunk, const float* __restrict__ srgb,
+                                                       uchar4* __restrict__ out) {
+    for (int pix = blockIdx.x * kBlock + threadIdx.x; pix < fc.npix; pix += gridDim.x * kBlock) {
+        float4 acc = first_chunk ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : film[pix];
+        for (int s = 0; s < fc.spp_chunk; ++s) {
+            const float4 L = rad[(size_t)s * fc.npix + pix];
+            acc.x = acc.x + L.x;
+            acc.y = acc.y + L.y;
+            acc.z = acc.z + L.z;
+        }
+        film[pix] = acc;
+        if (last_chunk) {
+            float c[3] = {acc.x * fc.inv_spp * fc.exposure_scale, acc.y * fc.inv_spp * fc.exposure_scale,
+                          acc.z * fc.inv_spp * fc.exposure_scale};
+            uint8_t q[3];
+            for (int k = 0; k < 3; ++k) {
+                float v = fminf(fmaxf(c[k], 0.0f), 1.0f);
+                if (fc.view_transform == 0) v = srgb_oetf(v, srgb, kSrgbN);
+                q[k] = quantize8(v);
+            }
+            out[pix] = make_uchar4(q[0], q[1], q[2], 255);
+        }
+    }
+}
+
+__global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
+                              int n, const float4* __restrict__ rays, float4* __restrict__ hits,
+                              int32_t* __restrict__ prims, uint8_t* __restrict__ occ,
+                              int32_t* __restrict__ spill) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    const int nthreads = gridDim.x * kBlock;
+    TravStack st{&lds_stack[threadIdx.x], spill + gtid, nthreads, 0};
+    for (int i = gtid; i < n; i += nthreads) {
+        const float4 o = rays[2 * i], d = rays[2 * i + 1];
+        Hit h;
+        traverse<false>(nodes, tris, n_tris, xyz(o), xyz(d), o.w, d.w, st, h);
+        hits[i] = make_float4(h.t, h.u, h.v, 0.0f);
+        prims[i] = h.orig;
+        Hit h2;
+        occ[i] = traverse<true>(nodes, tris, n_tris, xyz(o), xyz(d), o.w, d.w, st, h2) ? 1 : 0;
+    }
+}
+
+}  // namespace
+
+int device_cu_count() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        RR_HIP(hipGetDevice(&dev));
+        RR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        if (cus <= 0) cus = 256;
+    }
+    return cus;
+}
+
+int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2); }
+
+void DevPaths::ensure_paths(size_t n) {
+    if (grid_blocks == 0) grid_blocks = device_cu_count() * 8;
+    if (n > cap) {
+        for (DevBuf<float4>* b : {&ray_o, &ray_d, &hit, &thr, &rad, &sh_o, &sh_d, &sh_c}) b->ensure(n);
+        q[0].ensure(n);
+        q[1].ensure(n);
+        sq.ensure(n);
+        cap = n;
+    }
+    spill.ensure((size_t)kSpillStack * grid_blocks * kBlock);
+}
+
+void DevPaths::release() {
+    for (DevBuf<float4>* b : {&ray_o, &ray_d, &hit, &thr, &rad, &sh_o, &sh_d, &sh_c, &film}) b->release();
+    q[0].release(); q[1].release(); sq.release(); counters.release(); spill.release();
+    rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
+    cap = 0;
+}
+
+void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_t st) {
+    const int npix = base.npix;
+    const size_t npaths = (size_t)npix * base.spp_chunk;
+    p.ensure_paths(npaths);
+    p.film.ensure((size_t)npix);
+    p.rgba8.ensure((size_t)npix * 4);
+    const int cpc = counters_per_chunk(base.max_bounces);
+    p.counters.ensure((size_t)cpc * n_chunks);
+    RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
+    LightsMats lm{p.lights.ptr, p.materials.ptr, p.filter_table.ptr, p.srgb_lut.ptr};
+    const int grid = p.grid_blocks;
+    for (int c = 0; c < n_chunks; ++c) {
+        FrameConsts fc = base;
+        fc.first_sample = c * base.spp_chunk;
+        fc.spp_chunk = base.spp_chunk;
+        if (fc.first_sample + fc.spp_chunk > base.spp_total) fc.spp_chunk = base.spp_total - fc.first_sample;
+        const int np = npix * fc.spp_chunk;
+        int32_t* ext = p.counters.ptr + (size_t)cpc * c;        // ext[b]: queue size of bounce b (b>=1)
+        int32_t* shc = ext + (base.max_bounces + 2);            // shc[b]: shadow rays of bounce b
+        const int g = (int)std::min<long>((np + kBlock - 1) / kBlock, grid);
+        k_raygen<<<g, kBlock, 0, st>>>(fc, p.filter_table.ptr, p.ray_o.ptr, p.ray_d.ptr, p.thr.ptr,
+                                       p.rad.ptr, np);
+        for (int b = 0; b <= base.max_bounces; ++b) {
+            const int32_t* qin = b == 0 ? nullptr : p.q[b & 1].ptr;
+            const int32_t* cin = b == 0 ? nullptr : ext + b;
+            k_trace<false><<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, qin, cin, np, p.ray_o.ptr,
+                                                 p.ray_d.ptr, p.hit.ptr, nullptr, nullptr, p.spill.ptr);
+            k_shade<<<g, kBlock, 0, st>>>(fc, b, lm, s.tris.ptr, qin, cin, np, p.q[(b + 1) & 1].ptr, ext + b + 1,
+                                          p.sq.ptr, shc + b, p.ray_o.ptr, p.ray_d.ptr, p.hit.ptr, p.thr.ptr,
+                                          p.rad.ptr, p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr);
+            k_trace<true><<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, p.sq.ptr, shc + b, 0,
+                                                p.sh_o.ptr, p.sh_d.ptr, nullptr, p.sh_c.ptr, p.rad.ptr,
+                                                p.spill.ptr);
+        }
+        const int ga = (int)std::min<long>((npix + kBlock - 1) / kBlock, grid);
+        k_accumulate<<<ga, kBlock, 0, st>>>(fc, p.rad.ptr, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
+                                            p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
+    }
+    RR_HIP(hipGetLastError());
+}
+
+void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, float4* d_hits, int32_t* d_prims,
+                        uint8_t* d_occ, hipStream_t st) {
+    p.ensure_paths(1);
+    const int g = (int)std::min<long>((n + kBlock - 1) / kBlock, p.grid_blocks);
+    if (n > 0)
+        k_debug_trace<<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,
+                                            p.spill.ptr);
+    RR_HIP(hipGetLastError());
+}
+
+}  // namespace rr

@@ -1,0 +1,297 @@
+"""ctypes binding of the renderer's C ABI (include/rr.h, lib/librr.so).
+
+This is the Python host's view of the drop-in boundary; the Rust worker binds
+the same symbols through an `extern "C"` block. The library is
+the in-tree build from __graft_entry__.build(); there is no fallback: if it is
+missing or fails to load, every entry point raises RRError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "librr.so")
+SHIM_PATH = os.path.join(_HERE, "lib", "rr-blender-shim")
+
+RR_OK, RR_ENOENT, RR_EIO, RR_ENOMEM, RR_ENODEV, RR_EINVAL, RR_ENOTSUP = 0, -2, -5, -12, -19, -22, -95
+RR_VIEW_SCENE, RR_VIEW_STANDARD, RR_VIEW_RAW = -1, 0, 1
+RR_CAM_FLOATS, RR_LIGHT_FLOATS, RR_MAT_FLOATS, RR_RENDER_INTS, RR_RENDER_FLOATS = 16, 12, 12, 8, 4
+
+
+class RRError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"rr error {code}: {message}")
+        self.code = code
+
+
+class RenderParams(ctypes.Structure):
+    _fields_ = [("spp", ctypes.c_int32), ("max_bounces", ctypes.c_int32),
+                ("clamp_indirect", ctypes.c_float), ("seed", ctypes.c_uint32),
+                ("use_scene_seed", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("height", ctypes.c_int32), ("view_transform", ctypes.c_int32),
+                ("spp_per_chunk", ctypes.c_int32)]
+
+
+class FrameTiming(ctypes.Structure):
+    _fields_ = [("loaded_at", ctypes.c_double), ("started_rendering_at", ctypes.c_double),
+                ("finished_rendering_at", ctypes.c_double), ("file_saving_started_at", ctypes.c_double),
+                ("file_saving_finished_at", ctypes.c_double)]
+
+
+class FrameStats(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("chunks", ctypes.c_int32), ("camera_rays", ctypes.c_uint64),
+                ("extension_rays", ctypes.c_uint64), ("shadow_rays", ctypes.c_uint64),
+                ("anim_ms", ctypes.c_double), ("build_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
+                ("readback_ms", ctypes.c_double), ("encode_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("bvh_rebuilt", ctypes.c_int32), ("n_triangles", ctypes.c_int32),
+                ("output_bytes", ctypes.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# Every symbol include/rr.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "rr_render_params_default", "rr_abi_version", "rr_create", "rr_scene_load", "rr_render_frame",
+    "rr_render_frame_to_memory", "rr_scene_resolution", "rr_encode_image", "rr_last_error",
+    "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
+    "rr_debug_trace", "rr_debug_object_matrix",
+]
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise RRError(RR_ENOENT, f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                                 "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, c_int, i32, u32, f32p, u8p = ctypes.c_void_p, ctypes.c_int, ctypes.c_int32, ctypes.c_uint32, \
+        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint8)
+    i32p, u32p = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint32)
+    sig = {
+        "rr_render_params_default": (None, [ctypes.POINTER(RenderParams)]),
+        "rr_abi_version": (i32, []),
+        "rr_create": (c_int, [c_int, ctypes.POINTER(P)]),
+        "rr_scene_load": (c_int, [P, ctypes.c_char_p, ctypes.POINTER(P)]),
+        "rr_render_frame": (c_int, [P, P, i32, ctypes.POINTER(RenderParams), ctypes.c_char_p, ctypes.c_char_p, i32,
+                                    ctypes.POINTER(FrameTiming), ctypes.POINTER(FrameStats)]),
+        "rr_render_frame_to_memory": (c_int, [P, P, i32, ctypes.POINTER(RenderParams), f32p, u8p,
+                                              ctypes.POINTER(FrameStats)]),
+        "rr_scene_resolution": (c_int, [P, ctypes.POINTER(RenderParams), i32p, i32p]),
+        "rr_encode_image": (c_int, [u8p, i32, i32, ctypes.c_char_p, ctypes.c_char_p, i32,
+                                    ctypes.POINTER(ctypes.c_uint64)]),
+        "rr_last_error": (ctypes.c_char_p, [P]),
+        "rr_scene_free": (None, [P]),
+        "rr_destroy": (None, [P]),
+        "rr_debug_counts": (c_int, [P, i32p, i32p, i32p, i32p]),
+        "rr_debug_frame_state": (c_int, [P, P, i32, ctypes.POINTER(RenderParams), f32p, i32p, f32p, f32p, f32p,
+                                         f32p, i32p, f32p]),
+        "rr_debug_bvh": (c_int, [P, P, i32, u32p, u32p, i32p, f32p]),
+        "rr_debug_trace": (c_int, [P, P, i32, i32, f32p, f32p, i32p, u8p]),
+        "rr_debug_object_matrix": (c_int, [P, i32, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int, ctx=None):
+    if rc != 0:
+        msg = lib().rr_last_error(ctx).decode("utf-8", "replace")
+        raise RRError(rc, msg)
+
+
+def _ptr(a: np.ndarray | None, ctype):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def default_params(**overrides) -> RenderParams:
+    p = RenderParams()
+    lib().rr_render_params_default(ctypes.byref(p))
+    for k, v in overrides.items():
+        if v is None:
+            continue
+        if k == "seed":
+            p.use_scene_seed = 0
+        setattr(p, k, v)
+    return p
+
+
+@dataclass
+class FrameState:
+    tris: np.ndarray        # (n, 3, 3) world-space vertices
+    tri_mat: np.ndarray     # (n,)
+    camera: np.ndarray      # (16,)
+    lights: np.ndarray      # (nl, 12)
+    materials: np.ndarray   # (nm, 12)
+    world: np.ndarray       # (3,)
+    render_ints: np.ndarray  # (8,)
+    render_floats: np.ndarray  # (4,)
+
+
+class Scene:
+    """An exported project (.rrscene) — host-only until a RenderContext uses it."""
+
+    def __init__(self, path: str, ctx: "RenderContext | None" = None):
+        self.path = os.fspath(path)
+        h = ctypes.c_void_p()
+        _check(lib().rr_scene_load(ctx.handle if ctx else None, self.path.encode(), ctypes.byref(h)))
+        self.handle = h
+        self.ctx = ctx
+
+    def close(self):
+        if self.handle:
+            lib().rr_scene_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def counts(self) -> dict:
+        v = [ctypes.c_int32() for _ in range(4)]
+        _check(lib().rr_debug_counts(self.handle, *[ctypes.byref(x) for x in v]))
+        return dict(zip(["triangles", "lights", "materials", "objects"], [x.value for x in v]))
+
+    def resolution(self, params: RenderParams | None = None) -> tuple[int, int]:
+        w, h = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().rr_scene_resolution(self.handle, ctypes.byref(params) if params else None,
+                                         ctypes.byref(w), ctypes.byref(h)))
+        return w.value, h.value
+
+    def frame_constants(self, frame: int, params: RenderParams | None = None) -> FrameState:
+        """Host-only frame evaluation (no device): camera, lights, materials, world, render ints/floats."""
+        c = self.counts()
+        nl, nm = c["lights"], c["materials"]
+        cam = np.zeros(RR_CAM_FLOATS, np.float32)
+        lights = np.zeros((max(nl, 1), RR_LIGHT_FLOATS), np.float32)
+        mats = np.zeros((max(nm, 1), RR_MAT_FLOATS), np.float32)
+        world = np.zeros(3, np.float32)
+        ri = np.zeros(RR_RENDER_INTS, np.int32)
+        rf = np.zeros(RR_RENDER_FLOATS, np.float32)
+        _check(lib().rr_debug_frame_state(None, self.handle, int(frame), ctypes.byref(params) if params else None,
+                                          None, None, _ptr(cam, ctypes.c_float), _ptr(lights, ctypes.c_float),
+                                          _ptr(mats, ctypes.c_float), _ptr(world, ctypes.c_float),
+                                          _ptr(ri, ctypes.c_int32), _ptr(rf, ctypes.c_float)))
+        return FrameState(np.zeros((0, 3, 3), np.float32), np.zeros(0, np.int32), cam, lights[:nl], mats[:nm],
+                          world, ri, rf)
+
+    def object_matrix(self, obj: int, frame: float) -> np.ndarray:
+        m = (ctypes.c_double * 16)()
+        _check(lib().rr_debug_object_matrix(self.handle, obj, float(frame), m))
+        return np.array(m[:], dtype=np.float64).reshape(4, 4)
+
+
+class RenderContext:
+    """One HIP device (rr_ctx). Not thread-safe; one frame in flight at a time."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().rr_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().rr_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def load_scene(self, path: str) -> Scene:
+        return Scene(path, self)
+
+    def render_frame(self, scene: Scene, frame: int, params: RenderParams | None = None,
+                     out_path: str | None = None, fmt: str | None = "JPEG", quality: int = 90):
+        t, s = FrameTiming(), FrameStats()
+        _check(lib().rr_render_frame(self.handle, scene.handle, int(frame),
+                                     ctypes.byref(params) if params else None,
+                                     out_path.encode() if out_path is not None else None,
+                                     fmt.encode() if (fmt is not None and out_path is not None) else None,
+                                     int(quality), ctypes.byref(t), ctypes.byref(s)), self.handle)
+        return t, s
+
+    def render_to_memory(self, scene: Scene, frame: int, params: RenderParams | None = None,
+                         film: bool = True, rgba: bool = True):
+        w, h = scene.resolution(params)
+        f = np.zeros((h, w, 4), np.float32) if film else None
+        r = np.zeros((h, w, 4), np.uint8) if rgba else None
+        s = FrameStats()
+        _check(lib().rr_render_frame_to_memory(self.handle, scene.handle, int(frame),
+                                               ctypes.byref(params) if params else None,
+                                               _ptr(f, ctypes.c_float), _ptr(r, ctypes.c_uint8),
+                                               ctypes.byref(s)), self.handle)
+        return f, r, s
+
+    def frame_state(self, scene: Scene, frame: int, params: RenderParams | None = None) -> FrameState:
+        c = scene.counts()
+        n, nl, nm = c["triangles"], c["lights"], c["materials"]
+        tris = np.zeros((max(n, 1), 3, 3), np.float32)
+        mats_i = np.zeros(max(n, 1), np.int32)
+        cam = np.zeros(RR_CAM_FLOATS, np.float32)
+        lights = np.zeros((max(nl, 1), RR_LIGHT_FLOATS), np.float32)
+        mats = np.zeros((max(nm, 1), RR_MAT_FLOATS), np.float32)
+        world = np.zeros(3, np.float32)
+        ri = np.zeros(RR_RENDER_INTS, np.int32)
+        rf = np.zeros(RR_RENDER_FLOATS, np.float32)
+        _check(lib().rr_debug_frame_state(self.handle, scene.handle, int(frame),
+                                          ctypes.byref(params) if params else None,
+                                          _ptr(tris, ctypes.c_float) if self.handle else None,
+                                          _ptr(mats_i, ctypes.c_int32),
+                                          _ptr(cam, ctypes.c_float), _ptr(lights, ctypes.c_float),
+                                          _ptr(mats, ctypes.c_float), _ptr(world, ctypes.c_float),
+                                          _ptr(ri, ctypes.c_int32), _ptr(rf, ctypes.c_float)), self.handle)
+        return FrameState(tris[:n], mats_i[:n], cam, lights[:nl], mats[:nm], world, ri, rf)
+
+    def bvh(self, scene: Scene, frame: int):
+        n = scene.counts()["triangles"]
+        ni = max(n - 1, 1)
+        keys = np.zeros(n, np.uint32)
+        order = np.zeros(n, np.uint32)
+        children = np.zeros((ni, 2), np.int32)
+        boxes = np.zeros((ni, 12), np.float32)
+        _check(lib().rr_debug_bvh(self.handle, scene.handle, int(frame), _ptr(keys, ctypes.c_uint32),
+                                  _ptr(order, ctypes.c_uint32), _ptr(children, ctypes.c_int32),
+                                  _ptr(boxes, ctypes.c_float)), self.handle)
+        return keys, order, children, boxes
+
+    def trace(self, scene: Scene, frame: int, rays: np.ndarray):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        hits = np.zeros((max(n, 1), 4), np.float32)
+        prims = np.zeros(max(n, 1), np.int32)
+        occ = np.zeros(max(n, 1), np.uint8)
+        _check(lib().rr_debug_trace(self.handle, scene.handle, int(frame), n, _ptr(rays, ctypes.c_float),
+                                    _ptr(hits, ctypes.c_float), _ptr(prims, ctypes.c_int32),
+                                    _ptr(occ, ctypes.c_uint8)), self.handle)
+        return hits[:n], prims[:n], occ[:n]
+
+
+def encode_image(rgba: np.ndarray, out_path_no_ext: str, fmt: str, quality: int = 90) -> int:
+    rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+    h, w = rgba.shape[:2]
+    nbytes = ctypes.c_uint64()
+    _check(lib().rr_encode_image(_ptr(rgba, ctypes.c_uint8), w, h, out_path_no_ext.encode(), fmt.encode(),
+                                 int(quality), ctypes.byref(nbytes)))
+    return nbytes.value

@@ -1,0 +1,199 @@
+/*
+ * rr.h — C ABI of the MI355X frame renderer ("rr" = render-runner backend).
+ *
+ * This is the drop-in boundary for the one hot path of the render cluster: the
+ * worker's per-frame render step. In the reference that step is a process
+ * boundary: BlenderJobRunner::render_frame spawns `blender <blend> --background
+ * --python render-timing-script.py -- --render-output … --render-format …
+ * --render-frame N` and parses its stdout
+ * (/root/reference/worker/src/rendering/runner/mod.rs:72-203, argv :140-158,
+ * spawn :165-174; stdout protocol worker/src/rendering/runner/utilities.rs:105-203).
+ * Here the same step is an in-process call: scene exported once per project,
+ * uploaded once, then rr_render_frame() per frame index.
+ *
+ * Plain C types only (no torch / HIP types). All functions return 0 on success
+ * and a negative errno-style code on failure; rr_last_error() then holds a
+ * UTF-8 message (thread-local, valid until the next call on this thread).
+ *
+ * Threading: one rr_ctx per GPU per process; a ctx is NOT thread-safe, calls on
+ * one ctx must be serialised by the caller (the reference worker renders one
+ * frame at a time per worker: worker/src/rendering/queue.rs:79-118).
+ * Ownership: the caller owns ctx and scene handles (Rust Drop -> rr_scene_free /
+ * rr_destroy).
+ */
+#ifndef RR_H
+#define RR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RR_ABI_VERSION 1
+
+/* error codes (negative errno values) */
+#define RR_OK 0
+#define RR_ENOENT (-2)   /* file missing (reference: runner/mod.rs:82-87, :99-104) */
+#define RR_EIO (-5)      /* read/write failure (reference: create_dir_all :117-121) */
+#define RR_ENOMEM (-12)  /* host or device allocation failure */
+#define RR_EINVAL (-22)  /* bad argument / malformed scene */
+#define RR_ENODEV (-19)  /* HIP device unavailable / kernel launch failure */
+#define RR_ENOTSUP (-95) /* unsupported output format or scene feature */
+
+typedef struct rr_ctx rr_ctx;
+typedef struct rr_scene rr_scene;
+
+/* View transform selector (scene "view_transform"). */
+#define RR_VIEW_SCENE (-1)  /* use the scene file's setting */
+#define RR_VIEW_STANDARD 0  /* sRGB OETF, Blender "Standard" */
+#define RR_VIEW_RAW 1       /* linear values, clamped, no OETF */
+
+/* Render parameters. Any field left at its "use scene" value takes the value
+ * exported from the project (scene file "render" block). Zero-initialising the
+ * struct and then calling rr_render_params_default() gives scene defaults. */
+typedef struct rr_render_params {
+    int32_t spp;            /* samples per pixel; <= 0: scene */
+    int32_t max_bounces;    /* path length cap; < 0: scene */
+    float clamp_indirect;   /* max component of indirect contributions; < 0: scene; 0: off */
+    uint32_t seed;          /* RNG seed (Cycles "seed") */
+    int32_t use_scene_seed; /* != 0: ignore .seed, use the scene's */
+    int32_t width;          /* <= 0: scene resolution_x * percentage */
+    int32_t height;         /* <= 0: scene resolution_y * percentage */
+    int32_t view_transform; /* RR_VIEW_* */
+    int32_t spp_per_chunk;  /* samples in flight per wavefront chunk; <= 0: auto */
+} rr_render_params;
+
+/* The five timestamps the reference recovers from Blender's stdout
+ * (PartialRenderStatistics, worker/src/rendering/runner/utilities.rs:14-20,
+ * derived at :177-194). UNIX seconds as f64, the serde representation of
+ * FrameRenderTime (shared/src/results/worker_trace.rs:13-34). The caller adds
+ * started_process_at / exited_process_at around the call exactly as
+ * runner/mod.rs:165,176 do. */
+typedef struct rr_frame_timing {
+    double loaded_at;              /* reference: script start, render-timing-script.py:13 */
+    double started_rendering_at;   /* reference: :86 */
+    double finished_rendering_at;  /* reference: project_finished_rendering_at - saving (utilities.rs:185-190) */
+    double file_saving_started_at; /* == finished_rendering_at (utilities.rs:191-192) */
+    double file_saving_finished_at;/* reference: project_finished_rendering_at (utilities.rs:195-198) */
+} rr_frame_timing;
+
+/* Per-frame statistics (sidecar metrics; never part of the trace JSON). */
+typedef struct rr_frame_stats {
+    int32_t width, height, spp, chunks;
+    uint64_t camera_rays;    /* primary rays traced */
+    uint64_t extension_rays; /* bounce rays traced (closest hit) */
+    uint64_t shadow_rays;    /* NEE shadow rays traced (any hit) */
+    double anim_ms;          /* host animation eval + upload */
+    double build_ms;         /* device: world transform + LBVH build (0 if cached) */
+    double trace_ms;         /* device: wavefront kernels (raygen .. accumulate) */
+    double readback_ms;      /* device->host of the 8-bit image */
+    double encode_ms;        /* host: JPEG/PNG encode + write */
+    double total_ms;         /* whole call */
+    int32_t bvh_rebuilt;     /* 1 if the LBVH was rebuilt for this frame */
+    int32_t n_triangles;
+    uint64_t output_bytes;   /* encoded file size */
+} rr_frame_stats;
+
+/* Fill p with "use the scene's value" for every field. */
+void rr_render_params_default(rr_render_params* p);
+
+/* Library / ABI version (RR_ABI_VERSION). */
+int32_t rr_abi_version(void);
+
+/* Create a renderer context on HIP device `device_ordinal` (index among the
+ * devices visible to this process). */
+int rr_create(int device_ordinal, rr_ctx** out);
+
+/* Load a scene exported once per project (".rrscene" JSON)
+ * and upload its meshes to ctx's device. ctx may be NULL: the handle is then
+ * host-only (animation / resolution queries) and binds to the first context
+ * that renders it. The reference re-reads the .blend on
+ * every frame (runner/mod.rs:142-146); here the scene is parsed and uploaded
+ * once and cached in the returned handle. */
+int rr_scene_load(rr_ctx* ctx, const char* scene_path, rr_scene** out);
+
+/* Render one frame. Replaces the Blender subprocess of runner/mod.rs:140-174
+ * plus scene.frame_set / render(write_still=True) of render-timing-script.py:81-92.
+ *  - frame_index: the frame to evaluate (Blender frame number, scene.frame_set).
+ *  - out_path: output path WITHOUT extension, '#' runs already substituted
+ *    (render-timing-script.py:69-78,82); the library appends ".jpg" / ".png"
+ *    as Blender's write_still does with R_EXTENSION. NULL: render only.
+ *  - format: "JPEG" or "PNG" (job output_file_format, shared/src/jobs/mod.rs:80).
+ *  - jpeg_quality: 1..100 (the reference script forces 90, :84).
+ *  - timing / stats: optional outputs (may be NULL). */
+int rr_render_frame(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
+                    const rr_render_params* params, const char* out_path,
+                    const char* format, int32_t jpeg_quality,
+                    rr_frame_timing* timing, rr_frame_stats* stats);
+
+/* Render one frame into caller memory (no file). film_rgba: W*H*4 floats of
+ * mean linear radiance (alpha = 1); rgba8: W*H*4 bytes after the view
+ * transform. Either may be NULL. Rows are top to bottom. */
+int rr_render_frame_to_memory(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
+                              const rr_render_params* params, float* film_rgba,
+                              uint8_t* rgba8, rr_frame_stats* stats);
+
+/* Resolved output size for these params (after scene defaults). */
+int rr_scene_resolution(rr_scene* scene, const rr_render_params* params,
+                        int32_t* width, int32_t* height);
+
+/* Encode an RGBA8 image (rows top to bottom) to `path` + extension.
+ * Host encoder used by rr_render_frame; exported for tests. */
+int rr_encode_image(const uint8_t* rgba8, int32_t width, int32_t height,
+                    const char* out_path_no_ext, const char* format,
+                    int32_t jpeg_quality, uint64_t* bytes_written);
+
+/* Thread-local message of the last failure on this thread (ctx may be NULL). */
+const char* rr_last_error(rr_ctx* ctx);
+
+void rr_scene_free(rr_scene* scene);
+void rr_destroy(rr_ctx* ctx);
+
+/* ------------------------------------------------------------------------ *
+ * Inspection entry points. Not on the production path; they expose the
+ * intermediate state of a frame so the parity tests (tests/) can compare every
+ * stage with the CPU oracle (oracle/) on identical inputs.
+ * ------------------------------------------------------------------------ */
+
+#define RR_CAM_FLOATS 16   /* pos3 right3 up3 back3 half_w half_h clip_start clip_end */
+#define RR_LIGHT_FLOATS 12 /* type pos3 dir3 radius intensity3 pad */
+#define RR_MAT_FLOATS 12   /* base3 metallic specular roughness ior emission3 model pad */
+#define RR_RENDER_INTS 8   /* W H spp max_bounces seed view_transform spp_per_chunk pad */
+#define RR_RENDER_FLOATS 4 /* clamp_indirect filter_width exposure_scale pad */
+
+int rr_debug_counts(rr_scene* scene, int32_t* n_triangles, int32_t* n_lights,
+                    int32_t* n_materials, int32_t* n_objects);
+
+/* Evaluate the frame on the device (animation, world transform, LBVH) and read
+ * back what the integrator consumes. Any output pointer may be NULL. */
+int rr_debug_frame_state(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
+                         const rr_render_params* params, float* tris_world /* n*9 */,
+                         int32_t* tri_material /* n */, float* camera /* RR_CAM_FLOATS */,
+                         float* lights /* n_lights*RR_LIGHT_FLOATS */,
+                         float* materials /* n_mat*RR_MAT_FLOATS */, float* world /* 3 */,
+                         int32_t* render_ints /* RR_RENDER_INTS */,
+                         float* render_floats /* RR_RENDER_FLOATS */);
+
+/* LBVH of the frame: sorted Morton keys and primitive order (n each), internal
+ * node children (2*(n-1); leaf = ~sorted_index) and child boxes (12*(n-1):
+ * lmin3 lmax3 rmin3 rmax3). n == 1 yields one root whose two children are leaf 0. */
+int rr_debug_bvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, uint32_t* keys,
+                 uint32_t* order, int32_t* children, float* boxes);
+
+/* Trace a batch of rays against the frame's LBVH. rays: n*8 floats
+ * (o.xyz, tmin, d.xyz, tmax). hits: n*4 floats (t, u, v, 0), prims: n original
+ * triangle ids (-1 miss), occluded: n bytes (any-hit result). */
+int rr_debug_trace(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t n_rays,
+                   const float* rays, float* hits, int32_t* prims, uint8_t* occluded);
+
+/* Host animation evaluation: object_to_world matrix (row-major 4x4, f64) of
+ * object `object_index` at (possibly fractional) frame. */
+int rr_debug_object_matrix(rr_scene* scene, int32_t object_index, double frame,
+                           double* m16);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RR_H */

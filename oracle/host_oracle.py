@@ -1,0 +1,279 @@
+"""TEST INFRASTRUCTURE ONLY — host-side restatements used as checkers.
+
+Each function restates a reference behaviour on the hot path's host side, for
+tests/ to compare the product (C++ in librr.so, Python in the package) against:
+
+  * eval_fcurve        Blender 3.6 F-Curve evaluation (third-party; the
+                       reference pins Blender 3.6.0, pull-blender-image.sh:3-4,
+                       and calls it through scene.frame_set,
+                       scripts/render-timing-script.py:81). Pinned by the
+                       golden z table of the 01 cube (tests/golden/fcurve_01_cube_z.json,
+                       SURVEY.md §8c) and the saved ob.loc.z at cfra=60.
+  * object_matrix      Blender loc / XYZ-Euler / scale object matrix.
+  * frame_constants    camera / light / material constants the integrator reads.
+  * parse_blender_stdout  worker/src/rendering/runner/utilities.rs:105-203
+                       (extract_blender_render_information) and :51-96.
+"""
+from __future__ import annotations
+
+import json
+import math
+import re
+
+import numpy as np
+
+F = np.float32
+
+
+# ------------------------------------------------------------ F-Curves ----
+def _sqrt3d(d: float) -> float:
+    if d == 0.0:
+        return 0.0
+    if d < 0.0:
+        return -math.exp(math.log(-d) / 3.0)
+    return math.exp(math.log(d) / 3.0)
+
+
+def _ok(x: np.float32) -> bool:
+    return x >= F(-1.0e-10) and x <= F(1.000001)
+
+
+def _solve_cubic(c0, c1, c2, c3):
+    """Roots in [0,1] of c0 + c1 t + c2 t^2 + c3 t^3 (double), as float32."""
+    out = []
+    if c3 != 0.0:
+        a, b, c = c2 / c3, c1 / c3, c0 / c3
+        a = a / 3
+        p = b / 3 - a * a
+        q = (2 * a * a * a - a * b + c) / 2
+        d = q * q + p * p * p
+        if d > 0.0:
+            t = math.sqrt(d)
+            r = F(_sqrt3d(-q + t) + _sqrt3d(-q - t) - a)
+            return [r] if _ok(r) else []
+        if d == 0.0:
+            t = _sqrt3d(-q)
+            cands = [F(2 * t - a), F(-t - a)]
+        else:
+            phi = math.acos(-q / math.sqrt(-(p * p * p)))
+            t = math.sqrt(-p)
+            p = math.cos(phi / 3)
+            q = math.sqrt(3 - 3 * p * p)
+            cands = [F(2 * t * p - a), F(-t * (p + q) - a), F(-t * (p - q) - a)]
+        return [r for r in cands if _ok(r)]
+    a, b, c = c2, c1, c0
+    if a != 0.0:
+        p = b * b - 4 * a * c
+        if p > 0:
+            p = math.sqrt(p)
+            return [r for r in (F((-b - p) / (2 * a)), F((-b + p) / (2 * a))) if _ok(r)]
+        if p == 0:
+            r = F(-b / (2 * a))
+            return [r] if _ok(r) else []
+        return []
+    if b != 0.0:
+        r = F(-c / b)
+        return [r] if _ok(r) else []
+    return [F(0.0)] if c == 0.0 else []
+
+
+def eval_fcurve(keys: list, extrapolation: str, t: float) -> np.float32:
+    """keys: [{"co":[x,y], "handle_left":[..], "handle_right":[..], "interpolation": ...}]."""
+    K = [{k: [F(v) for v in kk[k]] for k in ("co", "handle_left", "handle_right")} | {"ipo": kk["interpolation"]}
+         for kk in keys]
+    t = F(t)
+    n = len(K)
+
+    def extrap(e, nb_dir):
+        E = K[e]
+        if E["ipo"] == "CONSTANT" or extrapolation != "LINEAR":
+            return E["co"][1]
+        if E["ipo"] == "LINEAR":
+            if n == 1:
+                return E["co"][1]
+            N = K[e + nb_dir]
+            dx = F(E["co"][0] - t)
+            fac = F(N["co"][0] - E["co"][0])
+            if fac == 0:
+                return E["co"][1]
+            fac = F(F(N["co"][1] - E["co"][1]) / fac)
+            return F(E["co"][1] - F(fac * dx))
+        h = E["handle_left"] if nb_dir > 0 else E["handle_right"]
+        dx = F(E["co"][0] - t)
+        fac = F(E["co"][0] - h[0])
+        if fac == 0:
+            return E["co"][1]
+        fac = F(F(E["co"][1] - h[1]) / fac)
+        return F(E["co"][1] - F(fac * dx))
+
+    if t <= K[0]["co"][0]:
+        return extrap(0, +1)
+    if K[-1]["co"][0] <= t:
+        return extrap(n - 1, -1)
+    # segment containing t (keys strictly increasing in x)
+    for a in range(1, n):
+        if K[a]["co"][0] >= t:
+            break
+    B, P = K[a], K[a - 1]
+    if abs(float(B["co"][0] - t)) <= 0.0001 or abs(float(P["co"][0] - t)) <= 0.0001:
+        return B["co"][1] if abs(float(B["co"][0] - t)) <= 0.0001 else P["co"][1]
+    if P["ipo"] == "CONSTANT":
+        return P["co"][1]
+    if P["ipo"] == "LINEAR":
+        return F(F(F(B["co"][1] - P["co"][1]) * F(t - P["co"][0])) / F(B["co"][0] - P["co"][0]) + P["co"][1])
+    v1, v2 = list(P["co"]), list(P["handle_right"])
+    v3, v4 = list(B["handle_left"]), list(B["co"])
+    eps = F(np.finfo(np.float32).eps)
+    if abs(v1[1] - v4[1]) < eps and abs(v2[1] - v3[1]) < eps and abs(v3[1] - v4[1]) < eps:
+        return v1[1]
+    h1 = [F(v1[0] - v2[0]), F(v1[1] - v2[1])]
+    h2 = [F(v4[0] - v3[0]), F(v4[1] - v3[1])]
+    ln, l1, l2 = F(v4[0] - v1[0]), abs(h1[0]), abs(h2[0])
+    if F(l1 + l2) != 0 and F(l1 + l2) > ln:
+        fac = F(ln / F(l1 + l2))
+        v2 = [F(v1[0] - F(fac * h1[0])), F(v1[1] - F(fac * h1[1]))]
+        v3 = [F(v4[0] - F(fac * h2[0])), F(v4[1] - F(fac * h2[1]))]
+    q0, q1, q2, q3 = v1[0], v2[0], v3[0], v4[0]
+    c0 = float(F(q0 - t))
+    c1 = float(F(F(3.0) * F(q1 - q0)))
+    c2 = float(F(F(3.0) * F(F(q0 - F(F(2.0) * q1)) + q2)))
+    c3 = float(F(F(q3 - q0) + F(F(3.0) * F(q1 - q2))))
+    roots = _solve_cubic(c0, c1, c2, c3)
+    if not roots:
+        return F(0.0)
+    u = roots[0]
+    f1, f2, f3, f4 = v1[1], v2[1], v3[1], v4[1]
+    k0 = f1
+    k1 = F(F(3.0) * F(f2 - f1))
+    k2 = F(F(3.0) * F(F(f1 - F(F(2.0) * f2)) + f3))
+    k3 = F(F(f4 - f1) + F(F(3.0) * F(f2 - f3)))
+    return F(F(F(k0 + F(u * k1)) + F(F(u * u) * k2)) + F(F(F(u * u) * u) * k3))
+
+
+# ------------------------------------------------------------ matrices ----
+def euler_xyz(rx, ry, rz) -> np.ndarray:
+    ci, cj, ch = math.cos(rx), math.cos(ry), math.cos(rz)
+    si, sj, sh = math.sin(rx), math.sin(ry), math.sin(rz)
+    cc, cs, sc, ss = ci * ch, ci * sh, si * ch, si * sh
+    return np.array([[cj * ch, sj * sc - cs, sj * cc + ss],
+                     [cj * sh, sj * ss + cc, sj * cs - sc],
+                     [-sj, cj * si, cj * ci]], dtype=np.float64)
+
+
+def object_matrix(obj: dict, frame: float) -> np.ndarray:
+    loc = list(map(float, obj.get("location", [0, 0, 0])))
+    rot = list(map(float, obj.get("rotation_euler", [0, 0, 0])))
+    scl = list(map(float, obj.get("scale", [1, 1, 1])))
+    for fc in obj.get("animation", {}).get("fcurves", []):
+        v = float(eval_fcurve(fc["keyframes"], fc.get("extrapolation", "CONSTANT"), frame))
+        tgt = {"location": loc, "rotation_euler": rot, "scale": scl}.get(fc["data_path"])
+        if tgt is not None and 0 <= fc["index"] < 3:
+            tgt[fc["index"]] = v
+    if obj.get("rotation_mode", "XYZ") != "XYZ":
+        raise NotImplementedError("oracle restates XYZ Euler only")
+    R = euler_xyz(*rot)
+    M = np.eye(4)
+    M[:3, :3] = R * np.array(scl)[None, :]
+    M[:3, 3] = loc
+    return M
+
+
+def frame_constants(scene: dict, frame: int, width: int | None = None, height: int | None = None) -> dict:
+    """Camera (16 floats), lights (n x 12), materials (n x 12), world (3)."""
+    r = scene["render"]
+    W = width or (r["resolution_x"] * r["resolution_percentage"]) // 100
+    H = height or (r["resolution_y"] * r["resolution_percentage"]) // 100
+    cam_obj = scene["objects"][scene["camera"]]
+    M = object_matrix(cam_obj, frame)
+    axes = [M[:3, a] / np.linalg.norm(M[:3, a]) for a in range(3)]
+    c = cam_obj["camera"]
+    fit = c.get("sensor_fit", "AUTO")
+    sensor = c["sensor_height"] if fit == "VERTICAL" else c["sensor_width"]
+    horiz = fit == "HORIZONTAL" or (fit == "AUTO" and W >= H)
+    if horiz:
+        hw = 0.5 * sensor / c["lens"]
+        hh = hw * H / W
+    else:
+        hh = 0.5 * sensor / c["lens"]
+        hw = hh * W / H
+    cam = np.array([*M[:3, 3], *axes[0], *axes[1], *axes[2], hw, hh, c["clip_start"], c["clip_end"]], np.float32)
+    lights = []
+    for o in scene["objects"]:
+        if o["type"] != "LIGHT":
+            continue
+        Lm = object_matrix(o, frame)
+        li = o["light"]
+        dz = -Lm[:3, 2] / np.linalg.norm(Lm[:3, 2])
+        k = li["energy"] / (4.0 * math.pi) if li["type"] == "POINT" else li["energy"]
+        lights.append([0.0 if li["type"] == "POINT" else 1.0, *Lm[:3, 3], *dz,
+                       li.get("radius", 0.0) if li["type"] == "POINT" else 0.0, *(k * np.array(li["color"])), 0.0])
+    mats = []
+    for m in scene["materials"] + [{"base_color": [0.8] * 3, "metallic": 0.0, "specular": 0.5, "roughness": 0.5,
+                                    "ior": 1.45, "emission": [0, 0, 0], "emission_strength": 1.0}]:
+        mats.append([*m["base_color"], m["metallic"], m["specular"], m["roughness"], m["ior"],
+                     *(np.array(m["emission"]) * m.get("emission_strength", 1.0)),
+                     1.0 if m.get("model") == "lambert" else 0.0, 0.0])
+    w = scene["world"]
+    return {"camera": cam, "lights": np.array(lights, np.float32).reshape(-1, 12),
+            "materials": np.array(mats, np.float32), "world": np.array(w["color"], np.float64) * w["strength"],
+            "W": W, "H": H}
+
+
+def load_scene(path: str) -> dict:
+    with open(path) as f:
+        return json.load(f)
+
+
+# ------------------------------------------------------ stdout protocol ----
+_TIME_RE = re.compile(r"Time: (?P<total_time>\d+:\d+\.\d+) \(Saving: (?P<saving_time>\d+:\d+\.\d+)\)")
+
+
+class StdoutError(ValueError):
+    pass
+
+
+def parse_blender_human_time(s: str) -> float:
+    """utilities.rs:51-84: 'mm:ss.ff' -> seconds (exactly two ':'-separated parts)."""
+    parts = s.split(":")
+    if len(parts) != 2:
+        raise StdoutError(f"Invalid human time, not in 00:00.00 format: {s}")
+    try:
+        return float(parts[0]) * 60.0 + float(parts[1])
+    except ValueError as e:
+        raise StdoutError(str(e)) from e
+
+
+def f64_to_utc(ts: float) -> float:
+    """utilities.rs:86-96: whole seconds (as i64 truncation) + ns truncated."""
+    whole = int(ts)  # `timestamp as i64` truncates toward zero
+    sub = ts - math.floor(ts)
+    ns = int(sub * 1e9)
+    return whole + ns / 1e9
+
+
+def parse_blender_stdout(stdout: str) -> dict:
+    """utilities.rs:105-203. Returns the five PartialRenderStatistics fields."""
+    lines = stdout.splitlines()
+    i = 0
+    while i < len(lines) and not lines[i].startswith("Saved: '"):
+        i += 1
+    saving = None
+    raw = None
+    for line in lines[i:]:
+        if line.startswith(" Time:"):
+            m = _TIME_RE.search(line)
+            if not m:
+                continue
+            if saving is not None:
+                raise StdoutError('Invalid Blender output: " Time... (Saving ...)" line appears more than once.')
+            saving = parse_blender_human_time(m.group("saving_time"))
+        elif line.startswith("RESULTS="):
+            raw = json.loads(line[len("RESULTS="):])
+    if raw is None or saving is None:
+        raise StdoutError("Invalid output, missing data")
+    fin = raw["project_finished_rendering_at"] - saving
+    return {"loaded_at": f64_to_utc(raw["project_loaded_at"]),
+            "started_rendering_at": f64_to_utc(raw["project_started_rendering_at"]),
+            "finished_rendering_at": f64_to_utc(fin),
+            "file_saving_started_at": f64_to_utc(fin),
+            "file_saving_finished_at": f64_to_utc(raw["project_finished_rendering_at"])}

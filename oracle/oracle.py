@@ -1,0 +1,143 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes front-end of the CPU oracle (rr_oracle.c).
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as
+the checker. The product (the package's native.py / librr.so) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.isfile(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        f, i32, u32, u8 = (ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int32),
+                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint8))
+        c_int = ctypes.c_int
+        L.orc_build_lbvh.argtypes = [c_int, f, u32, u32, i32, f]
+        L.orc_trace.argtypes = [c_int, f, c_int, f, f, i32, u8]
+        L.orc_trace_brute.argtypes = [c_int, f, c_int, f, f, i32]
+        L.orc_render.argtypes = [c_int, f, i32, f, c_int, f, f, f, i32, f, f, u8, c_int, c_int, c_int]
+        L.orc_rng.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, c_int, f]
+        L.orc_disk.argtypes = [c_int, f, f]
+        L.orc_bsdf_eval.argtypes = [f, f, f, f, f, f]
+        L.orc_filter_table.argtypes = [ctypes.c_float, f]
+        L.orc_srgb_lut.argtypes = [f]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def build_lbvh(tris: np.ndarray):
+    tris = _f32(tris).reshape(-1, 9)
+    n = tris.shape[0]
+    ni = max(n - 1, 1)
+    keys, order = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+    children, boxes = np.zeros((ni, 2), np.int32), np.zeros((ni, 12), np.float32)
+    lib().orc_build_lbvh(n, _p(tris, ctypes.c_float), _p(keys, ctypes.c_uint32), _p(order, ctypes.c_uint32),
+                         _p(children, ctypes.c_int32), _p(boxes, ctypes.c_float))
+    return keys, order, children, boxes
+
+
+def trace(tris: np.ndarray, rays: np.ndarray):
+    tris = _f32(tris).reshape(-1, 9)
+    rays = _f32(rays).reshape(-1, 8)
+    n = rays.shape[0]
+    hits, prims, occ = np.zeros((n, 4), np.float32), np.zeros(n, np.int32), np.zeros(n, np.uint8)
+    lib().orc_trace(tris.shape[0], _p(tris, ctypes.c_float), n, _p(rays, ctypes.c_float),
+                    _p(hits, ctypes.c_float), _p(prims, ctypes.c_int32), _p(occ, ctypes.c_uint8))
+    return hits, prims, occ
+
+
+def trace_brute(tris: np.ndarray, rays: np.ndarray):
+    tris = _f32(tris).reshape(-1, 9)
+    rays = _f32(rays).reshape(-1, 8)
+    n = rays.shape[0]
+    hits, prims = np.zeros((n, 4), np.float32), np.zeros(n, np.int32)
+    lib().orc_trace_brute(tris.shape[0], _p(tris, ctypes.c_float), n, _p(rays, ctypes.c_float),
+                          _p(hits, ctypes.c_float), _p(prims, ctypes.c_int32))
+    return hits, prims
+
+
+def render(tris, tri_mat, camera, lights, materials, world, render_ints, render_floats,
+           rows: tuple[int, int] | None = None, threads: int = 0, film: bool = True, rgba: bool = True):
+    """Full-frame render of the oracle path tracer. Inputs as rr_debug_frame_state."""
+    tris = _f32(tris).reshape(-1, 9)
+    tri_mat = np.ascontiguousarray(tri_mat, dtype=np.int32)
+    cam = _f32(camera)
+    lights = _f32(lights).reshape(-1, 12)
+    mats = _f32(materials).reshape(-1, 12)
+    world = _f32(world)
+    ri = np.ascontiguousarray(render_ints, dtype=np.int32)
+    rf = _f32(render_floats)
+    W, H = int(ri[0]), int(ri[1])
+    f = np.zeros((H, W, 4), np.float32) if film else None
+    r = np.zeros((H, W, 4), np.uint8) if rgba else None
+    r0, r1 = rows if rows else (0, 0)
+    lib().orc_render(tris.shape[0], _p(tris, ctypes.c_float), _p(tri_mat, ctypes.c_int32), _p(cam, ctypes.c_float),
+                     lights.shape[0], _p(lights, ctypes.c_float), _p(mats, ctypes.c_float),
+                     _p(world, ctypes.c_float), _p(ri, ctypes.c_int32), _p(rf, ctypes.c_float),
+                     _p(f, ctypes.c_float), _p(r, ctypes.c_uint8), r0, r1, threads)
+    return f, r
+
+
+def render_state(state, **kw):
+    """Render from a product FrameState (native.RenderContext.frame_state)."""
+    return render(state.tris, state.tri_mat, state.camera, state.lights, state.materials, state.world,
+                  state.render_ints, state.render_floats, **kw)
+
+
+def rng(seed: int, pixel: int, sample: int, ndims: int) -> np.ndarray:
+    out = np.zeros(ndims, np.float32)
+    lib().orc_rng(seed, pixel, sample, ndims, _p(out, ctypes.c_float))
+    return out
+
+
+def disk(u: np.ndarray) -> np.ndarray:
+    u = _f32(u).reshape(-1, 2)
+    xy = np.zeros_like(u)
+    lib().orc_disk(u.shape[0], _p(u, ctypes.c_float), _p(xy, ctypes.c_float))
+    return xy
+
+
+def bsdf_eval(mat12, n, wo, wi):
+    m, n, wo, wi = _f32(mat12), _f32(n), _f32(wo), _f32(wi)
+    f3, pdf = np.zeros(3, np.float32), np.zeros(1, np.float32)
+    lib().orc_bsdf_eval(_p(m, ctypes.c_float), _p(n, ctypes.c_float), _p(wo, ctypes.c_float),
+                        _p(wi, ctypes.c_float), _p(f3, ctypes.c_float), _p(pdf, ctypes.c_float))
+    return f3, float(pdf[0])
+
+
+def filter_table(width: float) -> np.ndarray:
+    t = np.zeros(1024, np.float32)
+    lib().orc_filter_table(width, _p(t, ctypes.c_float))
+    return t
+
+
+def srgb_lut() -> np.ndarray:
+    t = np.zeros(4097, np.float32)
+    lib().orc_srgb_lut(_p(t, ctypes.c_float))
+    return t

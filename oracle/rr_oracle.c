@@ -1,0 +1,775 @@
+/*
+ * rr_oracle.c — TEST INFRASTRUCTURE ONLY. CPU restatement of the renderer's
+ * hot path, used by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg as the checker. The product (librr.so) never links or calls
+ * this file.
+ *
+ * What it restates, and from where:
+ *  - The reference's per-frame render step is Blender 3.6.0 Cycles on the CPU
+ *    (/root/reference/worker/src/rendering/runner/mod.rs:165-174 spawns
+ *    `blender`; /root/reference/scripts/render-timing-script.py:90 calls
+ *    bpy.ops.render.render). Cycles is a third-party dependency absent from
+ *    /root/reference (pinned only as the docker image linuxserver/blender:3.6.0,
+ *    /root/reference/pull-blender-image.sh:3-4), so Cycles-image parity is
+ *    UNPINNED here; see DESIGN.md §5.
+ *  - This oracle is the specification of the MI355X renderer's algorithm
+ *    (DESIGN.md §4): Karras LBVH over 30-bit Morton codes, closest/any-hit
+ *    traversal with an order-independent accept rule, a path tracer with the
+ *    Principled-BSDF subset, point/sun NEE, Cycles-style light units
+ *    (point: P/(4 pi) W/sr, eval_fac 1/(4 pi) * invarea), indirect clamp,
+ *    Russian roulette, Blackman-Harris filter importance sampling, sRGB
+ *    "Standard" view transform and 8-bit quantisation as Blender's
+ *    unit_float_to_uchar_clamp.
+ *  - Written scalar, one path at a time, in the same IEEE single-precision
+ *    operation order as the HIP kernels, without contraction (built with
+ *    -ffp-contract=off; x86-64 SSE has no FMA by default) and without libm
+ *    transcendentals on the per-sample path, so GPU and oracle agree bit for
+ *    bit on identical inputs (tests/test_gpu_parity.py).
+ *  - Pinning of this oracle against analytic known answers (white furnace,
+ *    point-light closed form, ray/triangle and LBVH vs brute force):
+ *    tests/test_oracle.py.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_FILTER_N 1024
+#define ORC_SRGB_N 4096
+#define ORC_MAXDEPTH 256
+
+typedef struct { float x, y, z; } v3;
+
+static v3 V(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+static v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static v3 vmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+static v3 vscl(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+static float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static v3 vcross(v3 a, v3 b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static v3 vnorm(v3 a) { float inv = 1.0f / sqrtf(vdot(a, a)); return vscl(a, inv); }
+static float vmax3(v3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
+
+static int fbits(float f) { int i; memcpy(&i, &f, 4); return i; }
+static float ibits(int i) { float f; memcpy(&f, &i, 4); return f; }
+
+/* ------------------------------------------------------------ tables ---- */
+/* Blackman-Harris inverse-CDF table, support [-w, w] (Cycles doubles the BH
+ * filter width). Double precision, midpoint rule on 16*N cells. */
+void orc_filter_table(float width, float* table) {
+    const int N = ORC_FILTER_N, M = 16 * ORC_FILTER_N;
+    const double w = 2.0 * (double)width;
+    double* cdf = (double*)calloc((size_t)M + 1, sizeof(double));
+    for (int i = 0; i < M; ++i) {
+        double x = ((double)i + 0.5) / M;
+        double v = 2.0 * M_PI * x;
+        double f = 0.35875 - 0.48829 * cos(v) + 0.14128 * cos(2.0 * v) - 0.01168 * cos(3.0 * v);
+        cdf[i + 1] = cdf[i] + (f > 0.0 ? f : 0.0);
+    }
+    for (int i = 0; i <= M; ++i) cdf[i] /= cdf[M];
+    int j = 0;
+    for (int i = 0; i < N; ++i) {
+        double u = (double)i / (N - 1);
+        while (j < M - 1 && cdf[j + 1] < u) ++j;
+        double d = cdf[j + 1] - cdf[j];
+        double fr = d > 0.0 ? (u - cdf[j]) / d : 0.0;
+        if (fr < 0.0) fr = 0.0;
+        if (fr > 1.0) fr = 1.0;
+        double x = ((double)j + fr) / M;
+        table[i] = (float)(w * (x - 0.5));
+    }
+    free(cdf);
+}
+
+void orc_srgb_lut(float* lut) {
+    for (int i = 0; i <= ORC_SRGB_N; ++i) lut[i] = (float)(1.055 * pow((double)i / ORC_SRGB_N, 1.0 / 2.4) - 0.055);
+}
+
+static float lerp_table(const float* t, int n, float u) {
+    float f = u * (float)(n - 1);
+    int i = (int)f;
+    if (i >= n - 1) return t[n - 1];
+    if (i < 0) i = 0;
+    float fr = f - (float)i;
+    return t[i] + (t[i + 1] - t[i]) * fr;
+}
+
+/* --------------------------------------------------------------- RNG ---- */
+static uint32_t hash32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+static uint32_t pkey(uint32_t seed, uint32_t pixel, uint32_t sample) {
+    uint32_t k = hash32(hash32(seed) + pixel);
+    return hash32(k ^ (sample * 0x9E3779B9u + 0x7F4A7C15u));
+}
+static float rnd(uint32_t key, uint32_t dim) {
+    return (float)(hash32(key + (dim + 1u) * 0x9E3779B9u) >> 8) * 5.9604644775390625e-08f;
+}
+
+/* ---------------------------------------------------------- sampling ---- */
+static void small_sincos(float x, float* s, float* c) {
+    float z = x * x;
+    *s = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x + x;
+    *c = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z - 0.5f * z + 1.0f;
+}
+
+static void disk(float u1, float u2, float* x, float* y) {
+    float a = 2.0f * u1 - 1.0f, b = 2.0f * u2 - 1.0f, s, c;
+    if (a == 0.0f && b == 0.0f) { *x = 0.0f; *y = 0.0f; return; }
+    if (fabsf(a) > fabsf(b)) {
+        small_sincos(0.785398163397448f * (b / a), &s, &c);
+        *x = a * c; *y = a * s;
+    } else {
+        small_sincos(0.785398163397448f * (a / b), &s, &c);
+        *x = b * s; *y = b * c;
+    }
+}
+
+static void onb(v3 n, v3* b1, v3* b2) {
+    float sign = copysignf(1.0f, n.z);
+    float a = -1.0f / (sign + n.z);
+    float b = n.x * n.y * a;
+    *b1 = V(1.0f + sign * n.x * n.x * a, sign * b, -sign * n.x);
+    *b2 = V(b, sign + n.y * n.y * a, -n.y);
+}
+
+static float off_axis(float p, float n) {
+    int of = (int)(256.0f * n);
+    float pi = ibits(fbits(p) + ((p < 0.0f) ? -of : of));
+    return fabsf(p) < 0.03125f ? p + 1.52587890625e-05f * n : pi;
+}
+static v3 offset_ray(v3 p, v3 n) { return V(off_axis(p.x, n.x), off_axis(p.y, n.y), off_axis(p.z, n.z)); }
+
+/* ---------------------------------------------------------------- LBVH --- */
+typedef struct {
+    int n;
+    uint32_t* keys;   /* sorted */
+    uint32_t* order;  /* sorted original ids */
+    int* child;       /* 2*(n-1) or 2 */
+    float* box;       /* 12 per internal node */
+    float* tri;       /* leaf order: v0 e1 e2 (9) */
+    int* tri_orig;
+    int* tri_mat;
+} lbvh;
+
+static uint32_t spread10(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+static int clz32(uint32_t x) { return x ? __builtin_clz(x) : 32; }
+
+static int kdelta(const uint32_t* k, int n, int i, int j) {
+    if (j < 0 || j >= n) return -1;
+    if (k[i] == k[j]) return 32 + clz32((uint32_t)(i ^ j));
+    return clz32(k[i] ^ k[j]);
+}
+
+static void tri_box(const float* t9, float b[6]) {
+    for (int a = 0; a < 3; ++a) {
+        b[a] = fminf(fminf(t9[a], t9[3 + a]), t9[6 + a]);
+        b[3 + a] = fmaxf(fmaxf(t9[a], t9[3 + a]), t9[6 + a]);
+    }
+}
+
+/* box of the subtree rooted at child code c */
+static void subtree_box(const lbvh* B, const float* tris9, int c, float out[6]) {
+    if (c < 0) {
+        tri_box(tris9 + 9 * (size_t)B->order[~c], out);
+        return;
+    }
+    const float* bx = B->box + 12 * (size_t)c;
+    for (int a = 0; a < 3; ++a) {
+        out[a] = fminf(bx[a], bx[6 + a]);
+        out[3 + a] = fmaxf(bx[3 + a], bx[9 + a]);
+    }
+}
+
+static void lbvh_free(lbvh* B) {
+    free(B->keys); free(B->order); free(B->child); free(B->box);
+    free(B->tri); free(B->tri_orig); free(B->tri_mat);
+    memset(B, 0, sizeof *B);
+}
+
+static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
+    memset(B, 0, sizeof *B);
+    B->n = n;
+    if (n <= 0) return;
+    B->keys = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    B->order = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    float* cen = (float*)malloc(sizeof(float) * 3 * (size_t)n);
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < n; ++i) {
+        const float* t = tris9 + 9 * (size_t)i;
+        for (int a = 0; a < 3; ++a) {
+            float c = (t[a] + t[3 + a]) + t[6 + a];  /* centroid sum */
+            cen[3 * (size_t)i + a] = c;
+            if (c < lo[a]) lo[a] = c;
+            if (c > hi[a]) hi[a] = c;
+        }
+    }
+    uint32_t* tmpk = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    uint32_t* tmpv = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    for (int i = 0; i < n; ++i) {
+        uint32_t q[3];
+        for (int a = 0; a < 3; ++a) {
+            float ext = hi[a] - lo[a];
+            float s = ext > 0.0f ? 1024.0f / ext : 0.0f;
+            float f = (cen[3 * (size_t)i + a] - lo[a]) * s;
+            f = fminf(fmaxf(f, 0.0f), 1023.0f);
+            q[a] = (uint32_t)f;
+        }
+        tmpk[i] = (spread10(q[0]) << 2) | (spread10(q[1]) << 1) | spread10(q[2]);
+        tmpv[i] = (uint32_t)i;
+    }
+    /* stable counting sort, 4 x 8 bits (LSD) */
+    for (int pass = 0; pass < 4; ++pass) {
+        int shift = 8 * pass;
+        size_t cnt[257] = {0};
+        for (int i = 0; i < n; ++i) cnt[((tmpk[i] >> shift) & 255u) + 1]++;
+        for (int d = 0; d < 256; ++d) cnt[d + 1] += cnt[d];
+        for (int i = 0; i < n; ++i) {
+            uint32_t d = (tmpk[i] >> shift) & 255u;
+            size_t pos = cnt[d]++;
+            B->keys[pos] = tmpk[i];
+            B->order[pos] = tmpv[i];
+        }
+        memcpy(tmpk, B->keys, sizeof(uint32_t) * n);
+        memcpy(tmpv, B->order, sizeof(uint32_t) * n);
+    }
+    free(tmpk); free(tmpv); free(cen);
+    int ni = n > 1 ? n - 1 : 1;
+    B->child = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
+    B->box = (float*)malloc(sizeof(float) * 12 * (size_t)ni);
+    if (n == 1) {
+        B->child[0] = ~0; B->child[1] = ~0;
+    } else {
+        const uint32_t* k = B->keys;
+        for (int i = 0; i < n - 1; ++i) {
+            int d = (kdelta(k, n, i, i + 1) - kdelta(k, n, i, i - 1)) >= 0 ? 1 : -1;
+            int dmin = kdelta(k, n, i, i - d);
+            int lmax = 2;
+            while (kdelta(k, n, i, i + lmax * d) > dmin) lmax <<= 1;
+            int l = 0;
+            for (int t = lmax >> 1; t >= 1; t >>= 1)
+                if (kdelta(k, n, i, i + (l + t) * d) > dmin) l += t;
+            int j = i + l * d;
+            int dn = kdelta(k, n, i, j);
+            int s = 0, t = l;
+            do {
+                t = (t + 1) >> 1;
+                if (kdelta(k, n, i, i + (s + t) * d) > dn) s += t;
+            } while (t > 1);
+            int g = i + s * d + (d < 0 ? -1 : 0);
+            int lo_ = i < j ? i : j, hi_ = i < j ? j : i;
+            B->child[2 * i] = (lo_ == g) ? ~g : g;
+            B->child[2 * i + 1] = (hi_ == g + 1) ? ~(g + 1) : g + 1;
+        }
+    }
+    /* boxes bottom-up: children of node i have larger indices or are leaves?
+     * Not guaranteed for Karras; use an explicit post-order walk. */
+    {
+        int* stack = (int*)malloc(sizeof(int) * 2 * (size_t)ni + 16);
+        unsigned char* done = (unsigned char*)calloc((size_t)ni, 1);
+        int sp = 0;
+        stack[sp++] = 0;
+        while (sp) {
+            int v = stack[sp - 1];
+            int c0 = B->child[2 * v], c1 = B->child[2 * v + 1];
+            int ready = 1;
+            if (n > 1) {
+                if (c0 >= 0 && !done[c0]) { stack[sp++] = c0; ready = 0; }
+                if (c1 >= 0 && !done[c1]) { stack[sp++] = c1; ready = 0; }
+            }
+            if (!ready) continue;
+            --sp;
+            float b0[6], b1[6];
+            subtree_box(B, tris9, c0, b0);
+            subtree_box(B, tris9, c1, b1);
+            memcpy(B->box + 12 * (size_t)v, b0, sizeof b0);
+            memcpy(B->box + 12 * (size_t)v + 6, b1, sizeof b1);
+            done[v] = 1;
+        }
+        free(stack); free(done);
+    }
+    B->tri = (float*)malloc(sizeof(float) * 9 * (size_t)n);
+    B->tri_orig = (int*)malloc(sizeof(int) * n);
+    B->tri_mat = (int*)malloc(sizeof(int) * n);
+    for (int i = 0; i < n; ++i) {
+        const float* t = tris9 + 9 * (size_t)B->order[i];
+        float* o = B->tri + 9 * (size_t)i;
+        o[0] = t[0]; o[1] = t[1]; o[2] = t[2];
+        o[3] = t[3] - t[0]; o[4] = t[4] - t[1]; o[5] = t[5] - t[2];
+        o[6] = t[6] - t[0]; o[7] = t[7] - t[1]; o[8] = t[8] - t[2];
+        B->tri_orig[i] = (int)B->order[i];
+        B->tri_mat[i] = mats ? mats[B->order[i]] : 0;
+    }
+}
+
+/* ------------------------------------------------------------ tracing ---- */
+typedef struct { float t, u, v; int idx, orig; } hitrec;
+
+static int slab_test(v3 o, v3 inv, const float* b, float tmin, float tmax, float* tnear) {
+    float tx0 = (b[0] - o.x) * inv.x, tx1 = (b[3] - o.x) * inv.x;
+    float ty0 = (b[1] - o.y) * inv.y, ty1 = (b[4] - o.y) * inv.y;
+    float tz0 = (b[2] - o.z) * inv.z, tz1 = (b[5] - o.z) * inv.z;
+    float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    *tnear = tn;
+    return tn <= tf;
+}
+
+static int mt_test(v3 o, v3 d, const float* t9, float* t, float* u, float* v) {
+    v3 v0 = V(t9[0], t9[1], t9[2]), e1 = V(t9[3], t9[4], t9[5]), e2 = V(t9[6], t9[7], t9[8]);
+    v3 pv = vcross(d, e2);
+    float det = vdot(e1, pv);
+    if (det == 0.0f) return 0;
+    float inv = 1.0f / det;
+    v3 tv = vsub(o, v0);
+    *u = vdot(tv, pv) * inv;
+    if (*u < 0.0f || *u > 1.0f) return 0;
+    v3 qv = vcross(tv, e1);
+    *v = vdot(d, qv) * inv;
+    if (*v < 0.0f || *u + *v > 1.0f) return 0;
+    *t = vdot(e2, qv) * inv;
+    return 1;
+}
+
+static void try_leaf(const lbvh* B, int leaf, v3 o, v3 d, float tmin, hitrec* h) {
+    float t, u, v;
+    if (!mt_test(o, d, B->tri + 9 * (size_t)leaf, &t, &u, &v)) return;
+    int orig = B->tri_orig[leaf];
+    if (t > tmin && (t < h->t || (t == h->t && orig < h->orig))) {
+        h->t = t; h->u = u; h->v = v; h->idx = leaf; h->orig = orig;
+    }
+}
+
+/* Same traversal order as the GPU (near child first, left on ties, leaves
+ * tested as soon as their box passes). */
+static int trace(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hitrec* h) {
+    h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
+    if (B->n <= 0) return 0;
+    v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int stack[ORC_MAXDEPTH];
+    int sp = 0, node = 0;
+    for (;;) {
+        const float* bx = B->box + 12 * (size_t)node;
+        float tl, tr;
+        int hl = slab_test(o, inv, bx, tmin, h->t, &tl);
+        int hr = slab_test(o, inv, bx + 6, tmin, h->t, &tr);
+        int cl = B->child[2 * node], cr = B->child[2 * node + 1];
+        if (hl && cl < 0) {
+            try_leaf(B, ~cl, o, d, tmin, h);
+            if (any && h->idx >= 0) return 1;
+            hl = 0;
+        }
+        if (hr && cr < 0) {
+            try_leaf(B, ~cr, o, d, tmin, h);
+            if (any && h->idx >= 0) return 1;
+            hr = 0;
+        }
+        if (hl && hr) {
+            int lf = tl <= tr;
+            if (sp < ORC_MAXDEPTH) stack[sp++] = lf ? cr : cl;
+            node = lf ? cl : cr;
+        } else if (hl) node = cl;
+        else if (hr) node = cr;
+        else {
+            if (sp == 0) break;
+            node = stack[--sp];
+        }
+    }
+    return h->idx >= 0;
+}
+
+/* ------------------------------------------------------------ material ---- */
+typedef struct { v3 base; float metallic, specular, roughness, ior; v3 emission; int model; } mat_t;
+
+static float sw(float c) { float m = 1.0f - c; if (m < 0.0f) m = 0.0f; float m2 = m * m; return m2 * m2 * m; }
+
+static v3 eval_bsdf(const mat_t* m, v3 N, v3 wo, v3 wi, float ps, float* pdf) {
+    float cosV = vdot(N, wo), cosL = vdot(N, wi);
+    if (cosV <= 0.0f || cosL <= 0.0f) { *pdf = 0.0f; return V(0.0f, 0.0f, 0.0f); }
+    if (m->model == 1) { /* pure Lambert */
+        *pdf = cosL * 0.318309886183791f;
+        return vscl(m->base, 0.318309886183791f);
+    }
+    v3 H = vnorm(vadd(wo, wi));
+    float cosD = vdot(wi, H), NdotH = vdot(N, H);
+    float alpha = m->roughness * m->roughness;
+    if (alpha < 1.0e-4f) alpha = 1.0e-4f;
+    float a2 = alpha * alpha;
+    float fd90 = 0.5f + 2.0f * m->roughness * cosD * cosD;
+    float fl = sw(cosL), fv = sw(cosV);
+    float kd = (1.0f - m->metallic) * 0.318309886183791f * (1.0f + (fd90 - 1.0f) * fl) * (1.0f + (fd90 - 1.0f) * fv);
+    float tt = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
+    float D = a2 / (3.14159265358979f * tt * tt);
+    float g1v = 2.0f * cosV / (cosV + sqrtf(a2 + (1.0f - a2) * cosV * cosV));
+    float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
+    float s0 = 0.08f * m->specular;
+    v3 F0 = V(s0 + (m->base.x - s0) * m->metallic, s0 + (m->base.y - s0) * m->metallic,
+              s0 + (m->base.z - s0) * m->metallic);
+    float fw = sw(cosD);
+    float ks = D * g1v * g1l / (4.0f * cosV * cosL);
+    v3 F = V(F0.x + (1.0f - F0.x) * fw, F0.y + (1.0f - F0.y) * fw, F0.z + (1.0f - F0.z) * fw);
+    float pdf_d = cosL * 0.318309886183791f;
+    float pdf_s = g1v * D / (4.0f * cosV);
+    *pdf = (1.0f - ps) * pdf_d + ps * pdf_s;
+    return V(m->base.x * kd + F.x * ks, m->base.y * kd + F.y * ks, m->base.z * kd + F.z * ks);
+}
+
+static float p_spec(const mat_t* m, float cosV) {
+    if (m->model == 1) return 0.0f;
+    float s0 = 0.08f * m->specular;
+    float f0avg = ((s0 + (m->base.x - s0) * m->metallic) + (s0 + (m->base.y - s0) * m->metallic) +
+                   (s0 + (m->base.z - s0) * m->metallic)) * 0.333333343f;
+    float wsp = f0avg + (1.0f - f0avg) * sw(cosV);
+    float wd = (1.0f - m->metallic) * ((m->base.x + m->base.y + m->base.z) * 0.333333343f);
+    float tot = wsp + wd;
+    return tot > 0.0f ? wsp / tot : 1.0f;
+}
+
+static v3 vndf(v3 v, float alpha, float u1, float u2) {
+    v3 vh = vnorm(V(alpha * v.x, alpha * v.y, v.z));
+    float lensq = vh.x * vh.x + vh.y * vh.y;
+    v3 t1;
+    if (lensq > 0.0f) {
+        float il = 1.0f / sqrtf(lensq);
+        t1 = V(-vh.y * il, vh.x * il, 0.0f);
+    } else t1 = V(1.0f, 0.0f, 0.0f);
+    v3 t2 = vcross(vh, t1);
+    float dx, dy;
+    disk(u1, u2, &dx, &dy);
+    float s = 0.5f * (1.0f + vh.z);
+    dy = (1.0f - s) * sqrtf(fmaxf(0.0f, 1.0f - dx * dx)) + s * dy;
+    float nz = sqrtf(fmaxf(0.0f, 1.0f - dx * dx - dy * dy));
+    v3 nh = V(dx * t1.x + dy * t2.x + nz * vh.x, dx * t1.y + dy * t2.y + nz * vh.y, dx * t1.z + dy * t2.z + nz * vh.z);
+    return vnorm(V(alpha * nh.x, alpha * nh.y, fmaxf(0.0f, nh.z)));
+}
+
+static int sample_bsdf(const mat_t* m, v3 N, v3 wo, float ul, float u1, float u2, v3* wi, v3* f, float* pdf) {
+    float cosV = vdot(N, wo);
+    if (cosV <= 0.0f) return 0;
+    float ps = p_spec(m, cosV);
+    v3 T, B;
+    onb(N, &T, &B);
+    if (ul < ps) {
+        float alpha = m->roughness * m->roughness;
+        if (alpha < 1.0e-4f) alpha = 1.0e-4f;
+        v3 wl = V(vdot(wo, T), vdot(wo, B), cosV);
+        v3 hl = vndf(wl, alpha, u1, u2);
+        v3 H = V(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,
+                 T.z * hl.x + B.z * hl.y + N.z * hl.z);
+        float k = 2.0f * vdot(wo, H);
+        *wi = V(H.x * k - wo.x, H.y * k - wo.y, H.z * k - wo.z);
+    } else {
+        float x, y;
+        disk(u1, u2, &x, &y);
+        float z = sqrtf(fmaxf(0.0f, 1.0f - x * x - y * y));
+        *wi = V(T.x * x + B.x * y + N.x * z, T.y * x + B.y * y + N.y * z, T.z * x + B.z * y + N.z * z);
+    }
+    *f = eval_bsdf(m, N, wo, *wi, ps, pdf);
+    return *pdf > 0.0f;
+}
+
+static v3 clampc(v3 c, float clamp) {
+    if (clamp > 0.0f) {
+        float mx = vmax3(c);
+        if (mx > clamp) return vscl(c, clamp / mx);
+    }
+    return c;
+}
+
+/* ------------------------------------------------------------- render ---- */
+typedef struct {
+    const lbvh* bvh;
+    const float* cam;     /* 16 */
+    int n_lights;
+    const float* lights;  /* 12 each */
+    const float* mats;    /* 12 each */
+    v3 world;
+    int W, H, spp, max_bounces, view;
+    uint32_t seed;
+    float clamp, inv_w2, inv_h2;
+    float filter[ORC_FILTER_N];
+    float srgb[ORC_SRGB_N + 1];
+} scene_t;
+
+static mat_t load_mat(const float* mats, int id) {
+    const float* m = mats + 12 * id;
+    mat_t r;
+    r.base = V(m[0], m[1], m[2]);
+    r.metallic = m[3]; r.specular = m[4]; r.roughness = m[5]; r.ior = m[6];
+    r.emission = V(m[7], m[8], m[9]);
+    r.model = (int)m[10];
+    return r;
+}
+
+static v3 radiance(const scene_t* S, int pix, int sample) {
+    const float* c = S->cam;
+    uint32_t key = pkey(S->seed, (uint32_t)pix, (uint32_t)sample);
+    int px = pix % S->W, py = pix / S->W;
+    float fx = (float)px + 0.5f + lerp_table(S->filter, ORC_FILTER_N, rnd(key, 0));
+    float fy = (float)py + 0.5f + lerp_table(S->filter, ORC_FILTER_N, rnd(key, 1));
+    float sx = (fx * S->inv_w2 - 1.0f) * c[12];
+    float sy = (1.0f - fy * S->inv_h2) * c[13];
+    float len = sqrtf(sx * sx + sy * sy + 1.0f);
+    v3 dw = V(c[3] * sx + c[6] * sy - c[9], c[4] * sx + c[7] * sy - c[10], c[5] * sx + c[8] * sy - c[11]);
+    float il = 1.0f / len;
+    v3 d = vscl(dw, il);
+    v3 o = V(c[0], c[1], c[2]);
+    float tmin = c[14] * len, tmax = c[15] * len;
+    v3 L = V(0.0f, 0.0f, 0.0f), T = V(1.0f, 1.0f, 1.0f);
+    for (int b = 0; b <= S->max_bounces; ++b) {
+        hitrec h;
+        trace(S->bvh, o, d, tmin, tmax, 0, &h);
+        if (h.idx < 0) {
+            v3 cc = vmul(T, S->world);
+            if (b > 0) cc = clampc(cc, S->clamp);
+            L = vadd(L, cc);
+            break;
+        }
+        const float* tp = S->bvh->tri + 9 * (size_t)h.idx;
+        v3 e1 = V(tp[3], tp[4], tp[5]), e2 = V(tp[6], tp[7], tp[8]);
+        mat_t m = load_mat(S->mats, S->bvh->tri_mat[h.idx]);
+        float t = h.t;
+        v3 P = V(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+        v3 N = vnorm(vcross(e1, e2));
+        if (vdot(N, d) > 0.0f) N = V(-N.x, -N.y, -N.z);
+        v3 wo = V(-d.x, -d.y, -d.z);
+        if (m.emission.x != 0.0f || m.emission.y != 0.0f || m.emission.z != 0.0f) {
+            v3 cc = vmul(T, m.emission);
+            if (b > 0) cc = clampc(cc, S->clamp);
+            L = vadd(L, cc);
+        }
+        if (b >= S->max_bounces) break;
+        uint32_t dim0 = 2u + 8u * (uint32_t)b;
+        v3 Po = offset_ray(P, N);
+        int shadow = 0;
+        v3 sh_dir = V(0, 0, 0), sh_c = V(0, 0, 0);
+        float sh_dist = 0.0f;
+        if (S->n_lights > 0) {
+            int li = (int)(rnd(key, dim0) * (float)S->n_lights);
+            if (li > S->n_lights - 1) li = S->n_lights - 1;
+            const float* lt = S->lights + 12 * li;
+            v3 wi, Li;
+            float dist;
+            if (lt[0] == 0.0f) {
+                v3 lp = V(lt[1], lt[2], lt[3]);
+                float radius = lt[7];
+                v3 I = V(lt[8], lt[9], lt[10]);
+                v3 tl = vsub(lp, P);
+                float dl2 = vdot(tl, tl);
+                if (radius > 0.0f) {
+                    v3 wl = vscl(tl, 1.0f / sqrtf(dl2));
+                    v3 b1, b2;
+                    onb(wl, &b1, &b2);
+                    float dx, dy;
+                    disk(rnd(key, dim0 + 1u), rnd(key, dim0 + 2u), &dx, &dy);
+                    dx = dx * radius;
+                    dy = dy * radius;
+                    v3 sp = V(lp.x + b1.x * dx + b2.x * dy, lp.y + b1.y * dx + b2.y * dy, lp.z + b1.z * dx + b2.z * dy);
+                    v3 ts = vsub(sp, P);
+                    float ds2 = vdot(ts, ts);
+                    dist = sqrtf(ds2);
+                    wi = vscl(ts, 1.0f / dist);
+                    float cl = fabsf(vdot(wl, wi));
+                    Li = vscl(I, cl / ds2);
+                } else {
+                    dist = sqrtf(dl2);
+                    wi = vscl(tl, 1.0f / dist);
+                    Li = vscl(I, 1.0f / dl2);
+                }
+            } else {
+                wi = V(-lt[4], -lt[5], -lt[6]);
+                dist = 3.402823466e+38f;
+                Li = V(lt[8], lt[9], lt[10]);
+            }
+            float cosN = vdot(N, wi);
+            if (cosN > 0.0f) {
+                float pdf;
+                float ps = p_spec(&m, vdot(N, wo));
+                v3 f = eval_bsdf(&m, N, wo, wi, ps, &pdf);
+                float k = cosN * (float)S->n_lights;
+                v3 cc = V(T.x * f.x * k * Li.x, T.y * f.y * k * Li.y, T.z * f.z * k * Li.z);
+                if (b > 0) cc = clampc(cc, S->clamp);
+                if (vmax3(cc) > 0.0f) { shadow = 1; sh_dir = wi; sh_dist = dist; sh_c = cc; }
+            }
+        }
+        int alive = 0;
+        v3 wi, f;
+        float pdf;
+        if (sample_bsdf(&m, N, wo, rnd(key, dim0 + 3u), rnd(key, dim0 + 4u), rnd(key, dim0 + 5u), &wi, &f, &pdf)) {
+            float cosL = vdot(N, wi);
+            if (cosL > 0.0f) {
+                float k = cosL / pdf;
+                T = V(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
+                alive = vmax3(T) > 0.0f;
+                if (alive && b >= 3) {
+                    float q = fminf(vmax3(T), 1.0f);
+                    if (rnd(key, dim0 + 6u) >= q) alive = 0;
+                    else T = V(T.x / q, T.y / q, T.z / q);
+                }
+            }
+        }
+        if (shadow) {
+            hitrec hs;
+            if (!trace(S->bvh, Po, sh_dir, 0.0f, sh_dist, 1, &hs)) L = vadd(L, sh_c);
+        }
+        if (!alive) break;
+        o = Po; d = wi; tmin = 0.0f; tmax = 3.402823466e+38f;
+    }
+    return L;
+}
+
+static unsigned char q8(float f) {
+    if (f <= 0.0f) return 0;
+    if (f >= 1.0f) return 255;
+    return (unsigned char)(f * 255.0f + 0.5f);
+}
+
+/* ------------------------------------------------------------ C entry ---- */
+
+int orc_abi(void) { return 1; }
+
+/* LBVH of n triangles (tris9: v0 v1 v2 per triangle). Outputs as rr_debug_bvh. */
+int orc_build_lbvh(int n, const float* tris9, uint32_t* keys, uint32_t* order, int32_t* children, float* boxes) {
+    lbvh B;
+    lbvh_build(&B, n, tris9, NULL);
+    if (n > 0) {
+        int ni = n > 1 ? n - 1 : 1;
+        if (keys) memcpy(keys, B.keys, sizeof(uint32_t) * n);
+        if (order) memcpy(order, B.order, sizeof(uint32_t) * n);
+        if (children) memcpy(children, B.child, sizeof(int32_t) * 2 * ni);
+        if (boxes) memcpy(boxes, B.box, sizeof(float) * 12 * ni);
+    }
+    lbvh_free(&B);
+    return 0;
+}
+
+/* Brute force closest hit (no BVH), for pinning the LBVH traversal. */
+int orc_trace_brute(int n, const float* tris9, int n_rays, const float* rays, float* hits, int32_t* prims) {
+    for (int r = 0; r < n_rays; ++r) {
+        const float* R = rays + 8 * (size_t)r;
+        v3 o = V(R[0], R[1], R[2]), d = V(R[4], R[5], R[6]);
+        float best = R[7];
+        int bo = -1;
+        float bu = 0, bv = 0;
+        for (int i = 0; i < n; ++i) {
+            const float* t = tris9 + 9 * (size_t)i;
+            float pk[9] = {t[0], t[1], t[2], t[3] - t[0], t[4] - t[1], t[5] - t[2], t[6] - t[0], t[7] - t[1], t[8] - t[2]};
+            float tt, u, v;
+            if (!mt_test(o, d, pk, &tt, &u, &v)) continue;
+            if (tt > R[3] && (tt < best || (tt == best && i < bo))) { best = tt; bo = i; bu = u; bv = v; }
+        }
+        if (hits) { hits[4 * r] = bo >= 0 ? best : R[7]; hits[4 * r + 1] = bu; hits[4 * r + 2] = bv; hits[4 * r + 3] = 0; }
+        if (prims) prims[r] = bo;
+    }
+    return 0;
+}
+
+int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* hits, int32_t* prims,
+              uint8_t* occluded) {
+    lbvh B;
+    lbvh_build(&B, n, tris9, NULL);
+    for (int r = 0; r < n_rays; ++r) {
+        const float* R = rays + 8 * (size_t)r;
+        v3 o = V(R[0], R[1], R[2]), d = V(R[4], R[5], R[6]);
+        hitrec h, h2;
+        trace(&B, o, d, R[3], R[7], 0, &h);
+        if (hits) { hits[4 * r] = h.t; hits[4 * r + 1] = h.u; hits[4 * r + 2] = h.v; hits[4 * r + 3] = 0.0f; }
+        if (prims) prims[r] = h.orig;
+        if (occluded) occluded[r] = (uint8_t)trace(&B, o, d, R[3], R[7], 1, &h2);
+    }
+    lbvh_free(&B);
+    return 0;
+}
+
+/* Full frame. render_ints: W H spp max_bounces seed view_transform (as rr.h);
+ * render_floats: clamp_indirect filter_width exposure_scale.
+ * film: W*H*4 floats of mean radiance; rgba8: W*H*4 bytes. Rows
+ * [row_begin, row_end) only (row_end <= 0: all rows), so a bounded sample of a
+ * frame can be timed. threads <= 0: OpenMP default. */
+int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const float* cam, int n_lights,
+               const float* lights, const float* mats, const float* world, const int32_t* ri, const float* rf,
+               float* film, uint8_t* rgba8, int row_begin, int row_end, int threads) {
+    lbvh B;
+    lbvh_build(&B, n_tris, tris9, tri_mat);
+    scene_t* S = (scene_t*)calloc(1, sizeof(scene_t));
+    S->bvh = &B;
+    S->cam = cam;
+    S->n_lights = n_lights;
+    S->lights = lights;
+    S->mats = mats;
+    S->world = V(world[0], world[1], world[2]);
+    S->W = ri[0]; S->H = ri[1]; S->spp = ri[2]; S->max_bounces = ri[3]; S->seed = (uint32_t)ri[4]; S->view = ri[5];
+    S->clamp = rf[0];
+    S->inv_w2 = 2.0f / (float)S->W;
+    S->inv_h2 = 2.0f / (float)S->H;
+    orc_filter_table(rf[1], S->filter);
+    orc_srgb_lut(S->srgb);
+    const float exposure = rf[2];
+    const float inv_spp = 1.0f / (float)S->spp;
+    if (row_end <= 0 || row_end > S->H) row_end = S->H;
+    if (row_begin < 0) row_begin = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int y = row_begin; y < row_end; ++y) {
+        for (int x = 0; x < S->W; ++x) {
+            int pix = y * S->W + x;
+            v3 acc = V(0.0f, 0.0f, 0.0f);
+            for (int s = 0; s < S->spp; ++s) {
+                v3 L = radiance(S, pix, s);
+                acc.x = acc.x + L.x;
+                acc.y = acc.y + L.y;
+                acc.z = acc.z + L.z;
+            }
+            if (film) {
+                film[4 * (size_t)pix] = acc.x * inv_spp;
+                film[4 * (size_t)pix + 1] = acc.y * inv_spp;
+                film[4 * (size_t)pix + 2] = acc.z * inv_spp;
+                film[4 * (size_t)pix + 3] = 1.0f;
+            }
+            if (rgba8) {
+                float c3[3] = {acc.x * inv_spp * exposure, acc.y * inv_spp * exposure, acc.z * inv_spp * exposure};
+                for (int k = 0; k < 3; ++k) {
+                    float v = fminf(fmaxf(c3[k], 0.0f), 1.0f);
+                    if (S->view == 0) v = v <= 0.0031308f ? v * 12.92f : lerp_table(S->srgb, ORC_SRGB_N + 1, v);
+                    rgba8[4 * (size_t)pix + k] = q8(v);
+                }
+                rgba8[4 * (size_t)pix + 3] = 255;
+            }
+        }
+    }
+    free(S);
+    lbvh_free(&B);
+    return 0;
+}
+
+/* Expose a few primitives for the known-answer tests. */
+void orc_rng(uint32_t seed, uint32_t pixel, uint32_t sample, int ndims, float* out) {
+    uint32_t k = pkey(seed, pixel, sample);
+    for (int i = 0; i < ndims; ++i) out[i] = rnd(k, (uint32_t)i);
+}
+
+void orc_disk(int n, const float* u, float* xy) {
+    for (int i = 0; i < n; ++i) disk(u[2 * i], u[2 * i + 1], &xy[2 * i], &xy[2 * i + 1]);
+}
+
+/* BSDF eval for known-answer tests: mat12, N, wo, wi -> f (3), pdf. */
+void orc_bsdf_eval(const float* mat12, const float* n3, const float* wo3, const float* wi3, float* f3, float* pdf) {
+    mat_t m = load_mat(mat12, 0);
+    v3 N = V(n3[0], n3[1], n3[2]), wo = V(wo3[0], wo3[1], wo3[2]), wi = V(wi3[0], wi3[1], wi3[2]);
+    float ps = p_spec(&m, vdot(N, wo));
+    v3 f = eval_bsdf(&m, N, wo, wi, ps, pdf);
+    f3[0] = f.x; f3[1] = f.y; f3[2] = f.z;
+}

@@ -1,0 +1,38 @@
+import importlib
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+PKG = "diploma_thesis-distributed_rendering_of_cgi_using_a_render_cluster_amd"
+SCENES = os.path.join(ROOT, "scenes")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+REFERENCE = "/root/reference"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu on the GPU box")
+
+
+@pytest.fixture(scope="session")
+def rr():
+    return importlib.import_module(PKG)
+
+
+@pytest.fixture(scope="session")
+def ctx(rr):
+    c = rr.RenderContext(0)
+    yield c
+    c.close()
+
+
+def scene_path(name: str) -> str:
+    return os.path.join(SCENES, name)
+
+
+def have_reference() -> bool:
+    return os.path.isdir(os.path.join(REFERENCE, "worker"))

@@ -1,0 +1,274 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle (oracle/).
+
+Integer/index work (Morton keys, sort order, BVH topology, hit primitive ids)
+must be bit-exact; float work is ALSO expected bit-exact because both sides run
+the same uncontracted IEEE single-precision op sequence (rr_device.h header);
+the asserted tolerance is 0 and the mismatch counts are printed on failure.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from conftest import scene_path
+from oracle import host_oracle as HO
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+S04 = scene_path("04_very-simple-standin.rrscene")
+S01 = scene_path("01_simple-animation.rrscene")
+
+
+@pytest.fixture(scope="module")
+def s04(ctx):
+    s = ctx.load_scene(S04)
+    yield s
+    s.close()
+
+
+def _rays_random(rng, n, center, spread):
+    o = center + rng.uniform(-spread, spread, (n, 3))
+    tgt = center + rng.uniform(-1.5, 1.5, (n, 3))
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r = np.zeros((n, 8), np.float32)
+    r[:, 0:3] = o
+    r[:, 3] = 0.0
+    r[:, 4:7] = d
+    r[:, 7] = 1e30
+    return r
+
+
+@pytest.mark.parametrize("frame", [1, 17, 30, 60, 300])
+def test_lbvh_bit_exact(ctx, s04, frame):
+    st = ctx.frame_state(s04, frame)
+    keys, order, children, boxes = ctx.bvh(s04, frame)
+    ok, oo, oc, ob = O.build_lbvh(st.tris)
+    assert np.array_equal(keys, ok)
+    assert np.array_equal(order, oo)
+    assert np.array_equal(children, oc)
+    assert np.array_equal(boxes, ob)
+
+
+def test_world_transform_matches_host_oracle(ctx, s04):
+    scene = HO.load_scene(S04)
+    for frame in (1, 2, 30, 59, 60, 61):
+        st = ctx.frame_state(s04, frame)
+        obj = scene["objects"][1]
+        M = HO.object_matrix(obj, frame).astype(np.float32)
+        mesh = scene["meshes"][0]
+        v = np.array(mesh["vertices"], np.float32).reshape(-1, 3)
+        t = np.array(mesh["triangles"]).reshape(-1, 3)
+        exp = np.empty((len(t), 3, 3), np.float32)
+        for i, tri in enumerate(t):
+            for k, vi in enumerate(tri):
+                for r in range(3):
+                    exp[i, k, r] = ((M[r, 0] * v[vi, 0] + M[r, 1] * v[vi, 1]) + M[r, 2] * v[vi, 2]) + M[r, 3]
+        assert np.array_equal(st.tris, exp), f"frame {frame}"
+
+
+def test_frame_constants_match_host_oracle(ctx, s04):
+    scene = HO.load_scene(S04)
+    for frame in (1, 30):
+        st = ctx.frame_state(s04, frame)
+        fc = HO.frame_constants(scene, frame)
+        np.testing.assert_allclose(st.camera, fc["camera"], rtol=0, atol=2e-7)
+        np.testing.assert_allclose(st.lights, fc["lights"], rtol=1e-7, atol=1e-7)
+        np.testing.assert_allclose(st.materials, fc["materials"], rtol=0, atol=1e-7)
+        np.testing.assert_allclose(st.world, fc["world"], rtol=1e-7)
+
+
+def test_trace_batches_bit_exact(ctx, s04):
+    rng = np.random.default_rng(1234)
+    st = ctx.frame_state(s04, 30)
+    center = st.tris.reshape(-1, 3).mean(axis=0)
+    rays = np.concatenate([_rays_random(rng, 20000, center, 6.0),
+                           _rays_random(rng, 2000, center, 0.5)])  # many origins inside the cube
+    hits, prims, occ = ctx.trace(s04, 30, rays)
+    oh, op, oo = O.trace(st.tris, rays)
+    assert np.array_equal(prims, op), f"{np.count_nonzero(prims != op)} prim mismatches"
+    assert np.array_equal(hits, oh), f"{np.count_nonzero(hits != oh)} hit-record mismatches"
+    assert np.array_equal(occ, oo)
+    assert (prims >= 0).mean() > 0.3
+    # the LBVH result equals brute force over all triangles
+    bh, bp = O.trace_brute(st.tris, rays)
+    assert np.array_equal(bp, op)
+    assert np.array_equal(bh[:, 0], oh[:, 0])
+
+
+def test_trace_edge_cases(ctx, s04):
+    st = ctx.frame_state(s04, 1)
+    v = st.tris[0, 0].astype(np.float64)
+    rays = np.array([
+        [*(v + [0, 0, 5]), 0.0, 0, 0, -1, 1e30],      # straight down through a vertex
+        [*(v + [0, 0, 5]), 0.0, 0, 0, 1, 1e30],       # away from the mesh
+        [0, 0, 10, 0.0, 0, 0, -1, 0.5],               # tmax too short
+        [0, 0, 10, 20.0, 0, 0, -1, 1e30],             # tmin past the mesh
+        [0, 0, 0, 0.0, 1, 0, 0, 1e30],                # axis-aligned, zero components
+    ], np.float32)
+    hits, prims, occ = ctx.trace(s04, 1, rays)
+    oh, op, oo = O.trace(st.tris, rays)
+    assert np.array_equal(prims, op) and np.array_equal(hits, oh) and np.array_equal(occ, oo)
+    assert prims[1] == -1 and prims[2] == -1 and prims[3] == -1
+    # empty batch
+    h0, p0, o0 = ctx.trace(s04, 1, np.zeros((0, 8), np.float32))
+    assert len(p0) == 0
+
+
+@pytest.mark.parametrize("frame,w,h,spp,chunk", [(1, 160, 90, 16, 0), (30, 96, 54, 8, 3), (60, 64, 36, 5, 1),
+                                                 (600, 33, 17, 7, 2)])
+def test_full_frame_bit_exact(ctx, rr, s04, frame, w, h, spp, chunk):
+    p = rr.default_params(width=w, height=h, spp=spp, spp_per_chunk=chunk)
+    film, rgba, stats = ctx.render_to_memory(s04, frame, p)
+    st = ctx.frame_state(s04, frame, p)
+    of, orgba = O.render_state(st)
+    assert stats.camera_rays == w * h * spp
+    assert stats.width == w and stats.height == h and stats.spp == spp
+    nbad = int(np.count_nonzero(rgba != orgba))
+    assert nbad == 0, f"{nbad} 8-bit mismatches"
+    assert np.array_equal(film, of), f"max film diff {np.max(np.abs(film - of))}"
+    assert film[..., :3].mean() > 0.01
+
+
+def test_chunking_and_determinism(ctx, rr, s04):
+    outs = []
+    for chunk in (1, 4, 0):
+        p = rr.default_params(width=80, height=45, spp=12, spp_per_chunk=chunk)
+        film, rgba, _ = ctx.render_to_memory(s04, 30, p)
+        outs.append((film, rgba))
+    for f, r in outs[1:]:
+        assert np.array_equal(f, outs[0][0]) and np.array_equal(r, outs[0][1])
+
+
+def test_seed_changes_noise(ctx, rr, s04):
+    a = ctx.render_to_memory(s04, 30, rr.default_params(width=64, height=36, spp=4, seed=1))[0]
+    b = ctx.render_to_memory(s04, 30, rr.default_params(width=64, height=36, spp=4, seed=2))[0]
+    assert not np.array_equal(a, b)
+    assert abs(float(a.mean()) - float(b.mean())) < 0.02
+
+
+def test_furnace_known_answer(ctx, rr):
+    """Lambert sphere, albedo 0.5, world (0.8, 0.6, 0.4): every camera sample on the
+    sphere is exactly 0.5*world after one bounce (zero variance)."""
+    s = ctx.load_scene(scene_path("test_furnace.rrscene"))
+    film, _, _ = ctx.render_to_memory(s, 1, None)
+    center = film[20:28, 28:36, :3].reshape(-1, 3)
+    np.testing.assert_allclose(center, np.tile([0.4, 0.3, 0.2], (len(center), 1)), rtol=2e-6)
+    corner = film[0, 0, :3]
+    np.testing.assert_allclose(corner, [0.8, 0.6, 0.4], rtol=1e-6)
+    st = ctx.frame_state(s, 1)
+    of, _ = O.render_state(st)
+    assert np.array_equal(film, of)
+    s.close()
+
+
+def test_point_light_closed_form(ctx, rr):
+    s = ctx.load_scene(scene_path("test_pointlight.rrscene"))
+    film, _, _ = ctx.render_to_memory(s, 1, rr.default_params(spp=64))
+    st = ctx.frame_state(s, 1)
+    cam = st.camera
+    W, H = 64, 64
+    # analytic radiance at the pixel centre's plane point (camera looks straight down)
+    py, px = np.mgrid[0:H, 0:W]
+    sx = ((px + 0.5) * (2.0 / W) - 1.0) * cam[12]
+    sy = (1.0 - (py + 0.5) * (2.0 / H)) * cam[13]
+    x, y = cam[0] + sx * 10.0, cam[1] + sy * 10.0
+    lx, ly, lz = 1.0, 0.5, 2.0
+    r2 = (x - lx) ** 2 + (y - ly) ** 2 + lz ** 2
+    I = 100.0 / (4 * np.pi)
+    L = 0.8 / np.pi * I * lz / r2 ** 1.5
+    rel = np.abs(film[..., 0] - L) / L
+    assert np.median(rel) < 0.01, np.median(rel)
+    of, _ = O.render_state(ctx.frame_state(s, 1, rr.default_params(spp=64)))
+    assert np.array_equal(film, of)
+    s.close()
+
+
+def test_render_frame_writes_named_files(ctx, rr, s04, tmp_path):
+    p = rr.default_params(width=128, height=72, spp=4)
+    out = str(tmp_path / "frames" / "000007")
+    os.makedirs(tmp_path / "frames")
+    t, stats = ctx.render_frame(s04, 7, p, out, "JPEG", 90)
+    f = tmp_path / "frames" / "000007.jpg"
+    assert f.is_file() and stats.output_bytes == f.stat().st_size
+    assert t.loaded_at <= t.started_rendering_at <= t.finished_rendering_at == t.file_saving_started_at
+    assert t.file_saving_started_at <= t.file_saving_finished_at
+    _, rgba, _ = ctx.render_to_memory(s04, 7, p)
+    jpg = np.asarray(Image.open(f).convert("RGB")).astype(np.float64)
+    mse = np.mean((jpg - rgba[..., :3]) ** 2)
+    assert 10 * np.log10(255 ** 2 / max(mse, 1e-9)) > 35.0
+    t2, _ = ctx.render_frame(s04, 7, p, str(tmp_path / "frames" / "00007"), "PNG", 90)
+    png = np.asarray(Image.open(tmp_path / "frames" / "00007.png").convert("RGBA"))
+    assert np.array_equal(png, rgba)
+    with pytest.raises(rr.RRError) as e:
+        ctx.render_frame(s04, 7, p, str(tmp_path / "x"), "TIFF", 90)
+    assert e.value.code == -95
+    with pytest.raises(rr.RRError) as e:
+        ctx.render_frame(s04, 7, p, str(tmp_path / "missing_dir" / "x"), "PNG", 90)
+    assert e.value.code == -5
+
+
+def test_bench_config_properties(ctx, rr, s04):
+    """The bench workload (1920x1080, 128 spp): too big for the oracle in a test,
+    so check size-independent properties plus a bit-exact oracle slice."""
+    film, rgba, stats = ctx.render_to_memory(s04, 5, None)
+    assert film.shape == (1080, 1920, 4)
+    assert stats.camera_rays == 1920 * 1080 * 128
+    assert stats.extension_rays > 0 and stats.shadow_rays > 0
+    film2, rgba2, _ = ctx.render_to_memory(s04, 5, None)
+    assert np.array_equal(film, film2)
+    st = ctx.frame_state(s04, 5)
+    of, orgba = O.render_state(st, rows=(500, 504))
+    assert np.array_equal(rgba[500:504], orgba[500:504])
+    assert np.array_equal(film[500:504], of[500:504])
+    bg = film[1060:1080, 0:20, :3]
+    np.testing.assert_allclose(bg, 0.050876088, rtol=1e-5)
+
+
+def test_01_scene_renders(ctx, rr):
+    s = ctx.load_scene(S01)
+    p = rr.default_params(width=64, height=36, spp=4)
+    film, rgba, _ = ctx.render_to_memory(s, 45, p)
+    of, orgba = O.render_state(ctx.frame_state(s, 45, p))
+    assert np.array_equal(rgba, orgba)
+    s.close()
+
+
+def test_backend_runner_job(rr, tmp_path):
+    """BackendRunner.render_frame over a job TOML: file names per the reference
+    naming rule, seven ordered timestamps in the trace."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    job = rr.BlenderJob.load_from_file(os.path.join(root, "jobs", "04_very-simple_demo_10f-1w.toml"))
+    job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": str(tmp_path / "out")})
+    runner = rr.BackendRunner(root, params=rr.default_params(width=64, height=36, spp=2))
+    try:
+        for f in job.frames()[:3]:
+            frt = runner.render_frame(job, f)
+            vals = [getattr(frt, k) for k in rr.traces.FRAME_FIELDS]
+            assert vals == sorted(vals), vals
+    finally:
+        runner.close()
+    names = sorted(os.listdir(tmp_path / "out"))
+    assert names == ["000001.jpg", "000002.jpg", "000003.jpg"]
+    assert [i for i, _ in runner.tracer.frames()] == [1, 2, 3]
+
+
+def test_blender_cli_shim(rr, tmp_path):
+    """The --blenderBinary seam: the reference argv in, the reference stdout out."""
+    out_fmt = str(tmp_path / "######")
+    argv = [rr.SHIM_PATH, S04.replace(".rrscene", ".blend"), "--background", "--python", "script.py", "--",
+            "--render-output", out_fmt, "--render-format", "PNG", "--render-frame", "12"]
+    env = dict(os.environ, RR_WIDTH="64", RR_HEIGHT="36", RR_SPP="2")
+    # the .blend does not exist: the shim resolves <stem>.rrscene next to it
+    res = subprocess.run(argv, capture_output=True, text=True, env=env, timeout=120)
+    assert res.returncode == 0, res.stdout + res.stderr
+    stats = HO.parse_blender_stdout(res.stdout)
+    assert (tmp_path / "000012.png").is_file()
+    assert f"Saved: '{tmp_path}/000012.png'" in res.stdout
+    assert stats["loaded_at"] <= stats["started_rendering_at"] <= stats["file_saving_finished_at"]
+    bad = subprocess.run([rr.SHIM_PATH, S04, "--", "--render-format", "PNG"], capture_output=True, text=True,
+                         timeout=60)
+    assert "Missing render-and-timing-script arguments!" in bad.stdout
