@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Whole-job frames/s of the per-frame render step on 1..N MI355X.
+
+One step = one frame of the 04_very-simple job through BackendRunner.render_frame
+(the reference's BlenderJobRunner::render_frame semantics, /root/reference/worker/
+src/rendering/runner/mod.rs:72-203): animation eval, LBVH rebuild, wavefront path
+tracing at the scene's 1920x1080 / 128 spp, tonemap, JPEG q90 encode and file
+write. Frames are independent; each rank (one per GPU) renders its own frames
+(static frame partition, no data-path collective) => weak scaling.
+
+Timed region: barrier + device sync on both sides, max over ranks. Per-kernel
+device times come from HIP events recorded by the library on its own stream
+around every launch during the timed steps (RR_FLAG_PROFILE_KERNELS). Traversal
+counts for the algorithmic-byte model come from one extra counting frame after
+the timed region (RR_FLAG_COUNT_TRAVERSAL).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "diploma_thesis-distributed_rendering_of_cgi_using_a_render_cluster_amd"
+
+METRIC = "job frames/sec at 1/2/4/8 MI355X (04_very-simple); Mrays/s per GPU"
+JOB = os.path.join(ROOT, "jobs", "04_very-simple_demo_10f-1w.toml")
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-profile", action="store_true", help="time without per-kernel HIP events")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(cls: str, stats, max_bounces: int) -> float:
+    """Algorithmic HBM bytes of one kernel class over a frame.
+    Uses the per-frame ray counts and, for traversal, the counted node / triangle
+    visits (64 B per BVH node, 48 B per packed triangle)."""
+    npaths = stats.camera_rays
+    ext = stats.extension_rays
+    sh = stats.shadow_rays
+    if cls == "raygen":
+        return npaths * 64.0                          # ray 32 + throughput 16 + radiance 16
+    if cls == "closest":
+        rays = npaths + ext
+        return rays * 48.0 + ext * 4.0 + 64.0 * stats.closest_nodes + 48.0 * stats.closest_tris
+    if cls == "shadow":
+        return sh * (4.0 + 32.0 + 16.0 + 32.0) + 64.0 * stats.shadow_nodes + 48.0 * stats.shadow_tris
+    if cls == "shade":
+        shaded = npaths + ext
+        # read hit+ray+thr+rad (80) + write rad (16) + queue read for b>0;
+        # continued paths write ray+thr+queue (52); NEE writes shadow ray+contrib+queue (52);
+        # hit paths read the 48-B triangle (lower bound: max(continued, shadowed) hits)
+        return shaded * 96.0 + ext * 4.0 + ext * 52.0 + sh * 52.0 + max(ext, sh) * 48.0
+    if cls == "accumulate":
+        npix = stats.width * stats.height
+        return npix * (stats.spp * 16.0 + 32.0 * max(stats.chunks - 1, 0) + 16.0 + 4.0)
+    return 0.0
+
+
+def cpu_baseline(oracle_mod, state, budget_s: float):
+    """Oracle (C restatement, OpenMP) on the host cores: evenly spread 4-row bands
+    of the same frame until the budget is spent, extrapolated to frames/s."""
+    H = int(state.render_ints[1])
+    threads = min(os.cpu_count() or 1, 16)
+    bands = list(range(0, H, max(4, H // 64)))
+    done_rows, t_used = 0, 0.0
+    order = bands[::2] + bands[1::2]
+    for b in order:
+        t0 = time.perf_counter()
+        oracle_mod.render_state(state, rows=(b, min(b + 4, H)), threads=threads, film=False)
+        t_used += time.perf_counter() - t0
+        done_rows += min(b + 4, H) - b
+        if t_used >= budget_s:
+            break
+    frac = done_rows / H
+    return {"value": frac / t_used, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{done_rows} of {H} rows (4-row bands spread over the frame) of 04vs-standin frame 1 "
+                      f"at {int(state.render_ints[0])}x{H}, {int(state.render_ints[2])} spp, "
+                      f"{t_used:.1f} s, extrapolated to whole frames; render only (no encode)"}
+
+
+def main():
+    args = parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend, init_method="env://")
+    gpu = torch.cuda.is_available()
+    if gpu:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        if gpu:
+            torch.cuda.synchronize()
+
+    rr = importlib.import_module(PKG)
+    job = rr.BlenderJob.load_from_file(JOB)
+    outdir = tempfile.mkdtemp(prefix=f"rr_bench_r{rank}_")
+    job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": outdir})
+    frames = job.frames()
+    flags = 0 if args.no_profile else rr.native.RR_FLAG_PROFILE_KERNELS
+    runner = rr.BackendRunner(ROOT, device=local, params=rr.default_params(flags=flags))
+
+    def frame_of(step):  # static round-robin partition of the job's frame set over ranks
+        return frames[(step * world + rank) % len(frames)]
+
+    for w in range(args.warmup):
+        runner.render_frame(job, frame_of(w))
+    kernel_ms = [0.0] * 8
+    launches = [0] * 8
+    rays = 0
+    barrier()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        runner.render_frame(job, frame_of(args.warmup + s))
+        st = runner.last_stats
+        for k in range(8):
+            kernel_ms[k] += st.kernel_ms[k]
+            launches[k] += st.kernel_launches[k]
+        rays += st.camera_rays + st.extension_rays + st.shadow_rays
+    barrier()
+    elapsed = time.perf_counter() - t0
+    last_stats = runner.last_stats
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist is not None and gpu else "cpu")
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t.item())
+
+    # traversal counts for the byte model: one counting frame, outside the timed region
+    scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, ROOT))
+    f_count = frame_of(args.warmup)
+    _, _, cstats = runner.ctx.render_to_memory(scene, f_count, rr.default_params(
+        flags=rr.native.RR_FLAG_COUNT_TRAVERSAL), film=False, rgba=True)
+
+    result = None
+    if rank == 0:
+        total_frames = args.steps * world
+        value = total_frames / t_max
+        names = rr.native.KERNEL_CLASSES
+        per_class = {names[k]: {"ms_total": kernel_ms[k], "launches": launches[k]} for k in range(len(names))}
+        roofline = None
+        if not args.no_profile:
+            dom = max(range(len(names)), key=lambda k: kernel_ms[k])
+            cls = names[dom]
+            bytes_frame = algorithmic_bytes(cls, cstats, 12)
+            launches_frame = max(launches[dom] / max(args.steps, 1), 1)
+            avg_ms = kernel_ms[dom] / max(launches[dom], 1)
+            per_launch = bytes_frame / launches_frame
+            achieved = per_launch / (avg_ms * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "kernel": cls, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": None, "bytes_per_launch": per_launch, "avg_launch_ms": avg_ms}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                from oracle import oracle as O
+                state = runner.ctx.frame_state(scene, 1)
+                cpu = cpu_baseline(O, state, args.cpu_seconds)
+            except Exception as e:  # baseline is reported, never the target
+                cpu = {"value": None, "unit": "frames/s", "error": str(e)}
+        result = {
+            "metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: 04_very-simple stand-in scene (01_simple-animation content; the 04 .blend is "
+                    "missing from the reference), frames of the 04vs demo job, JPEG q90 written per frame",
+            "config": {"workload": "04vs-standin, 1 frame per step: 1920x1080, 128 spp, max 12 bounces, "
+                                   "LBVH rebuild + wavefront path trace + JPEG q90 encode/write",
+                       "job": os.path.basename(JOB), "resolution": "1920x1080", "spp": int(last_stats.spp),
+                       "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)"},
+            "mrays_per_s_per_gpu": round(rays / elapsed / 1e6, 1),
+            "device_ms_per_frame": round(sum(kernel_ms) / max(args.steps, 1), 3),
+            "kernels": per_class,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    runner.close()
+    shutil.rmtree(outdir, ignore_errors=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -371,12 +371,13 @@ void DevScene::release() {
     uploaded = false;
 }
 
-void build_lbvh(DevScene& s, hipStream_t st) {
+void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof) {
     const int n = s.n_tris;
     if (n <= 0) {
         s.built = true;
         return;
     }
+    if (prof) prof->begin(st, 0);
     const int nb = cdiv(n, kBlock);
     s.tri_world.ensure((size_t)3 * n);
     s.bounds.ensure(6);
@@ -420,6 +421,7 @@ void build_lbvh(DevScene& s, hipStream_t st) {
     k_refit<<<nb, kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr, s.leaf_parent.ptr,
                                    s.node_parent.ptr, s.children.ptr, s.flags.ptr, s.nodes.ptr,
                                    s.tris.ptr);
+    if (prof) prof->end(st);
     RR_HIP(hipGetLastError());
     s.built = true;
 }

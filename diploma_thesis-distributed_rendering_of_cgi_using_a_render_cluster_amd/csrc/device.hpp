@@ -74,6 +74,48 @@ struct DevScene {
     void release();
 };
 
+// Optional per-launch HIP-event timing (RR_FLAG_PROFILE_KERNELS), on the
+// stream the kernels run on.
+struct KernelProfiler {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    std::vector<int> cls;  // class of event pair i
+    size_t used = 0;       // events in use (pairs * 2)
+    void reset(bool enable) {
+        on = enable;
+        used = 0;
+        cls.clear();
+    }
+    void begin(hipStream_t st, int c) {
+        if (!on) return;
+        while (pool.size() < used + 2) {
+            hipEvent_t e;
+            RR_HIP(hipEventCreate(&e));
+            pool.push_back(e);
+        }
+        cls.push_back(c);
+        RR_HIP(hipEventRecord(pool[used], st));
+    }
+    void end(hipStream_t st) {
+        if (!on) return;
+        RR_HIP(hipEventRecord(pool[used + 1], st));
+        used += 2;
+    }
+    // after the stream has been synchronised
+    void collect(double* ms, int32_t* launches) {
+        for (size_t i = 0; i < cls.size(); ++i) {
+            float t = 0.f;
+            RR_HIP(hipEventElapsedTime(&t, pool[2 * i], pool[2 * i + 1]));
+            ms[cls[i]] += t;
+            launches[cls[i]] += 1;
+        }
+    }
+    void release() {
+        for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+        pool.clear();
+    }
+};
+
 // Per-context wavefront state (sized for the largest chunk seen).
 struct DevPaths {
     size_t cap = 0;
@@ -86,6 +128,9 @@ struct DevPaths {
     DevBuf<float> filter_table;
     DevBuf<float> srgb_lut;
     DevBuf<float> lights, materials;
+    DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: 4 totals
+    KernelProfiler prof;
+    bool count_traversal = false;
     int grid_blocks = 0;  // persistent grid for path kernels
     void ensure_paths(size_t n);
     void release();
@@ -107,7 +152,7 @@ struct FrameConsts {
 
 // LBVH build for the current obj_xform (uploaded by the caller).
 // Stream-ordered; no host synchronisation inside.
-void build_lbvh(DevScene& s, hipStream_t st);
+void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof = nullptr);
 
 // Render all chunks of one frame: film accumulate + tonemap to rgba8.
 // counters_per_chunk receives the device counter layout for stats.

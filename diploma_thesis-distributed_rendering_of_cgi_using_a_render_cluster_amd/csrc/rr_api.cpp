@@ -157,7 +157,7 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs) {
         d.obj_xform.ensure(fs.obj_xform.size());
         RR_HIP(hipMemcpyAsync(d.obj_xform.ptr, fs.obj_xform.data(), fs.obj_xform.size() * sizeof(float),
                               hipMemcpyHostToDevice, st));
-        build_lbvh(d, st);
+        build_lbvh(d, st, &p.prof);
         d.cached_xform = fs.obj_xform;
     } else if (rebuild) {
         d.built = true;
@@ -210,6 +210,9 @@ struct FrameRun {
     bool rebuilt;
     float build_ms, trace_ms, readback_ms;
     std::vector<int32_t> counters;
+    double kernel_ms[RR_K_CLASSES];
+    int32_t kernel_launches[RR_K_CLASSES];
+    unsigned long long trav[4];
 };
 
 // Run the device part of one frame; leaves the 8-bit image in c->host_rgba.
@@ -219,6 +222,8 @@ FrameRun run_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, float* film_out
     r.W = fs.W;
     r.H = fs.H;
     hipStream_t st = c->stream;
+    c->paths.prof.reset((fs.flags & RR_FLAG_PROFILE_KERNELS) != 0);
+    c->paths.count_traversal = (fs.flags & RR_FLAG_COUNT_TRAVERSAL) != 0;
     RR_HIP(hipEventRecord(c->ev[0], st));
     r.rebuilt = prepare_frame(c, s, fs);
     RR_HIP(hipEventRecord(c->ev[1], st));
@@ -242,6 +247,12 @@ FrameRun run_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, float* film_out
     RR_HIP(hipEventElapsedTime(&r.build_ms, c->ev[0], c->ev[1]));
     RR_HIP(hipEventElapsedTime(&r.trace_ms, c->ev[1], c->ev[2]));
     RR_HIP(hipEventElapsedTime(&r.readback_ms, c->ev[2], c->ev[3]));
+    c->paths.prof.collect(r.kernel_ms, r.kernel_launches);
+    c->paths.prof.reset(false);
+    if (c->paths.count_traversal) {
+        RR_HIP(hipMemcpy(r.trav, c->paths.trav_counts.ptr, sizeof r.trav, hipMemcpyDeviceToHost));
+        c->paths.count_traversal = false;
+    }
     if (film_out) {  // film holds sums; report the mean
         const float inv = 1.0f / (float)fs.spp;
         for (size_t i = 0; i < npix; ++i) {
@@ -270,6 +281,14 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
         for (int b = 1; b <= fs.max_bounces; ++b) st->extension_rays += (uint64_t)ext[b];
         for (int b = 0; b <= fs.max_bounces; ++b) st->shadow_rays += (uint64_t)shc[b];
     }
+    for (int k = 0; k < RR_K_CLASSES; ++k) {
+        st->kernel_ms[k] = r.kernel_ms[k];
+        st->kernel_launches[k] = r.kernel_launches[k];
+    }
+    st->closest_nodes = r.trav[0];
+    st->closest_tris = r.trav[1];
+    st->shadow_nodes = r.trav[2];
+    st->shadow_tris = r.trav[3];
     st->build_ms = r.rebuilt ? r.build_ms : 0.0;
     st->trace_ms = r.trace_ms;
     st->readback_ms = r.readback_ms;

@@ -656,6 +656,7 @@ FrameSetup setup_frame(const SceneDesc& s, int frame, const rr_render_params* p)
     if (f.view_transform != VIEW_STANDARD && f.view_transform != VIEW_RAW)
         throw std::runtime_error("unsupported view transform");
     f.spp_per_chunk = p->spp_per_chunk > 0 ? p->spp_per_chunk : r.spp_per_chunk;
+    f.flags = p->flags;
     f.filter_width = (float)r.filter_width;
     f.exposure_scale = (float)std::pow(2.0, r.exposure);
 

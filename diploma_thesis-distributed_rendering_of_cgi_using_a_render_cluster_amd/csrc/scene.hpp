@@ -115,7 +115,7 @@ struct SceneDesc {
 
 // Everything the device needs for one frame (DESIGN.md §4 "frame constants").
 struct FrameSetup {
-    int32_t W = 0, H = 0, spp = 0, max_bounces = 0, view_transform = 0, spp_per_chunk = 0;
+    int32_t W = 0, H = 0, spp = 0, max_bounces = 0, view_transform = 0, spp_per_chunk = 0, flags = 0;
     uint32_t seed = 0;
     float clamp_indirect = 0.f, filter_width = 1.5f, exposure_scale = 1.f;
     float cam[RR_CAM_FLOATS] = {};

@@ -96,17 +96,21 @@ __global__ __launch_bounds__(kBlock) void k_trace(const BvhNode* __restrict__ no
                                                   const float4* __restrict__ ray_o,
                                                   const float4* __restrict__ ray_d,
                                                   float4* __restrict__ hit, const float4* __restrict__ contrib,
-                                                  float4* __restrict__ rad, int32_t* __restrict__ spill) {
+                                                  float4* __restrict__ rad, int32_t* __restrict__ spill,
+                                                  unsigned long long* __restrict__ trav_counts) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     const int count = count_ptr ? *count_ptr : count_fixed;
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int nthreads = gridDim.x * kBlock;
     TravStack st{&lds_stack[threadIdx.x], spill + gtid, nthreads, 0};
+    uint32_t nv = 0, nt = 0;
+    uint32_t* pnv = trav_counts ? &nv : nullptr;
+    uint32_t* pnt = trav_counts ? &nt : nullptr;
     for (int i = gtid; i < count; i += nthreads) {
         const int p = queue ? queue[i] : i;
         const float4 ro = ray_o[p], rd = ray_d[p];
         Hit h;
-        const bool any = traverse<kAny>(nodes, tris, n_tris, xyz(ro), xyz(rd), ro.w, rd.w, st, h);
+        const bool any = traverse<kAny>(nodes, tris, n_tris, xyz(ro), xyz(rd), ro.w, rd.w, st, h, pnv, pnt);
         if (kAny) {
             if (!any) {
                 const float4 c = contrib[p];
@@ -118,6 +122,17 @@ __global__ __launch_bounds__(kBlock) void k_trace(const BvhNode* __restrict__ no
             }
         } else {
             hit[p] = make_float4(h.t, h.u, h.v, i2f(h.idx));
+        }
+    }
+    if (trav_counts) {  // measurement mode only: one atomic pair per wave
+        unsigned long long a = nv, b = nt;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off);
+            b += __shfl_xor(b, off);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&trav_counts[kAny ? 2 : 0], a);
+            atomicAdd(&trav_counts[kAny ? 3 : 1], b);
         }
     }
 }
@@ -357,6 +372,8 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&ray_o, &ray_d, &hit, &thr, &rad, &sh_o, &sh_d, &sh_c, &film}) b->release();
     q[0].release(); q[1].release(); sq.release(); counters.release(); spill.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
+    trav_counts.release();
+    prof.release();
     cap = 0;
 }
 
@@ -371,6 +388,13 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
     LightsMats lm{p.lights.ptr, p.materials.ptr, p.filter_table.ptr, p.srgb_lut.ptr};
     const int grid = p.grid_blocks;
+    unsigned long long* tc = nullptr;
+    if (p.count_traversal) {
+        p.trav_counts.ensure(4);
+        RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 4 * sizeof(unsigned long long), st));
+        tc = p.trav_counts.ptr;
+    }
+    KernelProfiler& pr = p.prof;
     for (int c = 0; c < n_chunks; ++c) {
         FrameConsts fc = base;
         fc.first_sample = c * base.spp_chunk;
@@ -380,23 +404,33 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         int32_t* ext = p.counters.ptr + (size_t)cpc * c;        // ext[b]: queue size of bounce b (b>=1)
         int32_t* shc = ext + (base.max_bounces + 2);            // shc[b]: shadow rays of bounce b
         const int g = (int)std::min<long>((np + kBlock - 1) / kBlock, grid);
+        pr.begin(st, 1);
         k_raygen<<<g, kBlock, 0, st>>>(fc, p.filter_table.ptr, p.ray_o.ptr, p.ray_d.ptr, p.thr.ptr,
                                        p.rad.ptr, np);
+        pr.end(st);
         for (int b = 0; b <= base.max_bounces; ++b) {
             const int32_t* qin = b == 0 ? nullptr : p.q[b & 1].ptr;
             const int32_t* cin = b == 0 ? nullptr : ext + b;
+            pr.begin(st, 2);
             k_trace<false><<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, qin, cin, np, p.ray_o.ptr,
-                                                 p.ray_d.ptr, p.hit.ptr, nullptr, nullptr, p.spill.ptr);
+                                                 p.ray_d.ptr, p.hit.ptr, nullptr, nullptr, p.spill.ptr, tc);
+            pr.end(st);
+            pr.begin(st, 3);
             k_shade<<<g, kBlock, 0, st>>>(fc, b, lm, s.tris.ptr, qin, cin, np, p.q[(b + 1) & 1].ptr, ext + b + 1,
                                           p.sq.ptr, shc + b, p.ray_o.ptr, p.ray_d.ptr, p.hit.ptr, p.thr.ptr,
                                           p.rad.ptr, p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr);
+            pr.end(st);
+            pr.begin(st, 4);
             k_trace<true><<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, p.sq.ptr, shc + b, 0,
                                                 p.sh_o.ptr, p.sh_d.ptr, nullptr, p.sh_c.ptr, p.rad.ptr,
-                                                p.spill.ptr);
+                                                p.spill.ptr, tc);
+            pr.end(st);
         }
         const int ga = (int)std::min<long>((npix + kBlock - 1) / kBlock, grid);
+        pr.begin(st, 5);
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, p.rad.ptr, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
+        pr.end(st);
     }
     RR_HIP(hipGetLastError());
 }

@@ -33,7 +33,7 @@ class RenderParams(ctypes.Structure):
                 ("clamp_indirect", ctypes.c_float), ("seed", ctypes.c_uint32),
                 ("use_scene_seed", ctypes.c_int32), ("width", ctypes.c_int32),
                 ("height", ctypes.c_int32), ("view_transform", ctypes.c_int32),
-                ("spp_per_chunk", ctypes.c_int32)]
+                ("spp_per_chunk", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
 class FrameTiming(ctypes.Structure):
@@ -49,10 +49,21 @@ class FrameStats(ctypes.Structure):
                 ("anim_ms", ctypes.c_double), ("build_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
                 ("readback_ms", ctypes.c_double), ("encode_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("bvh_rebuilt", ctypes.c_int32), ("n_triangles", ctypes.c_int32),
-                ("output_bytes", ctypes.c_uint64)]
+                ("output_bytes", ctypes.c_uint64),
+                ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_int32 * 8),
+                ("closest_nodes", ctypes.c_uint64), ("closest_tris", ctypes.c_uint64),
+                ("shadow_nodes", ctypes.c_uint64), ("shadow_tris", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        out = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            out[k] = list(v) if not isinstance(v, (int, float)) else v
+        return out
+
+
+RR_FLAG_PROFILE_KERNELS, RR_FLAG_COUNT_TRAVERSAL = 1, 2
+KERNEL_CLASSES = ["build", "raygen", "closest", "shade", "shadow", "accumulate"]
 
 
 # Every symbol include/rr.h declares (checked by tests/test_abi.py).

@@ -62,7 +62,21 @@ typedef struct rr_render_params {
     int32_t height;         /* <= 0: scene resolution_y * percentage */
     int32_t view_transform; /* RR_VIEW_* */
     int32_t spp_per_chunk;  /* samples in flight per wavefront chunk; <= 0: auto */
+    int32_t flags;          /* RR_FLAG_* (measurement modes; 0 in production) */
 } rr_render_params;
+
+/* Measurement flags (rr_render_params.flags). */
+#define RR_FLAG_PROFILE_KERNELS 1  /* HIP events around every launch -> stats.kernel_ms[] */
+#define RR_FLAG_COUNT_TRAVERSAL 2  /* count BVH nodes visited / triangles tested -> stats */
+
+/* Kernel classes of rr_frame_stats.kernel_ms / kernel_launches. */
+#define RR_K_BUILD 0     /* world transform + Morton + radix sort + Karras + refit */
+#define RR_K_RAYGEN 1    /* camera rays */
+#define RR_K_CLOSEST 2   /* closest-hit traversal (camera + extension rays) */
+#define RR_K_SHADE 3     /* shading + NEE setup + queue compaction */
+#define RR_K_SHADOW 4    /* any-hit traversal of shadow rays */
+#define RR_K_ACCUM 5     /* film accumulate + tonemap */
+#define RR_K_CLASSES 8
 
 /* The five timestamps the reference recovers from Blender's stdout
  * (PartialRenderStatistics, worker/src/rendering/runner/utilities.rs:14-20,
@@ -93,6 +107,11 @@ typedef struct rr_frame_stats {
     int32_t bvh_rebuilt;     /* 1 if the LBVH was rebuilt for this frame */
     int32_t n_triangles;
     uint64_t output_bytes;   /* encoded file size */
+    /* RR_FLAG_PROFILE_KERNELS: summed device time and launch count per class */
+    double kernel_ms[RR_K_CLASSES];
+    int32_t kernel_launches[RR_K_CLASSES];
+    /* RR_FLAG_COUNT_TRAVERSAL: totals over the frame (closest / any hit) */
+    uint64_t closest_nodes, closest_tris, shadow_nodes, shadow_tris;
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */
