@@ -46,18 +46,21 @@ __device__ __forceinline__ float xf(const float* m, float x, float y, float z) {
 }
 
 // K1: object -> world, centroid sum (v0+v1)+v2 stored in the .w lanes,
-// block min/max of the centroid sums folded into 6 ordered-uint words (all
-// reduced as minima: slot 3..5 hold -max).
+// block min/max of the centroid sums folded into 6 ordered-uint words:
+// slots 0..2 minima (start 0xFFFFFFFF), slots 3..5 maxima (start 0).
+// (An earlier form stored -max as a minimum; hipcc 7.2's SLP packing of the
+// decode into v_pk_add_f32 dropped one of the negations, so no float negation
+// is left on this path.)
 __global__ __launch_bounds__(kBlock) void k_transform(int n, const float4* __restrict__ local,
                                                       const int32_t* __restrict__ obj,
                                                       const float* __restrict__ xform,
                                                       float4* __restrict__ world,
                                                       uint32_t* __restrict__ bounds) {
     __shared__ uint32_t red[6];
-    if (threadIdx.x < 6) red[threadIdx.x] = 0xFFFFFFFFu;
+    if (threadIdx.x < 6) red[threadIdx.x] = threadIdx.x < 3 ? 0xFFFFFFFFu : 0u;
     __syncthreads();
     const int i = blockIdx.x * kBlock + threadIdx.x;
-    uint32_t mn[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    uint32_t mn[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
     if (i < n) {
         const float* m = xform + 12 * obj[i];
         float3 w[3];
@@ -70,18 +73,15 @@ __global__ __launch_bounds__(kBlock) void k_transform(int n, const float4* __res
         world[3 * i + 1] = make_float4(w[1].x, w[1].y, w[1].z, c.y);
         world[3 * i + 2] = make_float4(w[2].x, w[2].y, w[2].z, c.z);
         mn[0] = f2o(c.x); mn[1] = f2o(c.y); mn[2] = f2o(c.z);
-        mn[3] = f2o(-c.x); mn[4] = f2o(-c.y); mn[5] = f2o(-c.z);
+        mn[3] = mn[0]; mn[4] = mn[1]; mn[5] = mn[2];
     }
-    for (int k = 0; k < 6; ++k) {
-        uint32_t v = mn[k];
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint32_t o = __shfl_xor(v, off);
-            v = o < v ? o : v;
-        }
-        if ((threadIdx.x & 63) == 0) atomicMin(&red[k], v);
+    if (i < n) {
+        for (int k = 0; k < 3; ++k) atomicMin(&red[k], mn[k]);
+        for (int k = 3; k < 6; ++k) atomicMax(&red[k], mn[k]);
     }
     __syncthreads();
-    if (threadIdx.x < 6) atomicMin(&bounds[threadIdx.x], red[threadIdx.x]);
+    if (threadIdx.x < 3) atomicMin(&bounds[threadIdx.x], red[threadIdx.x]);
+    else if (threadIdx.x < 6) atomicMax(&bounds[threadIdx.x], red[threadIdx.x]);
 }
 
 // K2: 30-bit Morton code of the quantised centroid sum.
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kBlock) void k_morton(int n, const float4* __restri
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const float lo[3] = {o2f(bounds[0]), o2f(bounds[1]), o2f(bounds[2])};
-    const float hi[3] = {-o2f(bounds[3]), -o2f(bounds[4]), -o2f(bounds[5])};
+    const float hi[3] = {o2f(bounds[3]), o2f(bounds[4]), o2f(bounds[5])};
     const float c[3] = {world[3 * i].w, world[3 * i + 1].w, world[3 * i + 2].w};
     uint32_t q[3];
     for (int k = 0; k < 3; ++k) {
@@ -392,7 +392,8 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof) {
     s.leaf_parent.ensure((size_t)n);
     s.flags.ensure((size_t)(n > 1 ? n - 1 : 1));
 
-    RR_HIP(hipMemsetAsync(s.bounds.ptr, 0xFF, 6 * sizeof(uint32_t), st));
+    RR_HIP(hipMemsetAsync(s.bounds.ptr, 0xFF, 3 * sizeof(uint32_t), st));
+    RR_HIP(hipMemsetAsync(s.bounds.ptr + 3, 0x00, 3 * sizeof(uint32_t), st));
     k_transform<<<nb, kBlock, 0, st>>>(n, s.tri_local.ptr, s.tri_obj.ptr, s.obj_xform.ptr,
                                         s.tri_world.ptr, s.bounds.ptr);
     k_morton<<<nb, kBlock, 0, st>>>(n, s.tri_world.ptr, s.bounds.ptr, s.keys[0].ptr, s.vals[0].ptr);

@@ -1,0 +1,168 @@
+"""Host-side logic of the render step vs the reference's own behaviour:
+output naming (golden vectors computed by the reference function), the Blender
+stdout protocol (restated utilities.rs), job TOML schema, traces."""
+import json
+import os
+import sys
+import types
+
+import pytest
+
+from conftest import GOLDEN, REFERENCE, ROOT, have_reference
+from oracle import host_oracle as HO
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+# ---------------------------------------------------------------- naming ---
+def test_naming_matches_reference_function(rr):
+    for case in load("naming.json"):
+        assert rr.format_hash_frame_placeholders(case["path"], case["frame"]) == case["expected"], case
+
+
+def test_output_files_for_job(rr):
+    job = rr.BlenderJob.load_from_file(os.path.join(ROOT, "jobs", "04_very-simple_demo_10f-1w.toml"))
+    files = rr.job_output_files(job, "/out")
+    assert files == [f"/out/{i:06d}.jpg" for i in range(1, 11)]
+    assert rr.output_file_path("/o", "#####", 3, "PNG") == "/o/00003.png"
+    with pytest.raises(ValueError):
+        rr.output_file_path("/o", "#####", 3, "TIFF")
+
+
+# ------------------------------------------------------- stdout protocol ---
+def test_stdout_protocol_golden():
+    for case in load("stdout_protocol.json")["cases"]:
+        if case.get("error"):
+            with pytest.raises((HO.StdoutError, ValueError)):
+                HO.parse_blender_stdout(case["stdout"])
+        else:
+            got = HO.parse_blender_stdout(case["stdout"])
+            for k, v in case["expected"].items():
+                assert got[k] == pytest.approx(v, abs=1e-9), (case["name"], k)
+
+
+def test_blender_time_parse():
+    assert HO.parse_blender_human_time("00:01.50") == 1.5
+    assert HO.parse_blender_human_time("02:00.00") == 120.0
+    with pytest.raises(HO.StdoutError):
+        HO.parse_blender_human_time("1:2:3")
+
+
+# -------------------------------------------------------------- jobs -------
+def test_reference_job_tomls_schema(rr):
+    """Every reference job TOML (captured in tests/golden/reference_jobs.json):
+    the 39 04_very-simple jobs load, the 18 01/02/03 jobs fail on the missing
+    `render_script_path` exactly as the reference master would."""
+    recs = load("reference_jobs.json")
+    assert len(recs) == 57
+    ok = 0
+    for r in recs:
+        if "error" in r:
+            with pytest.raises(rr.JobError) as e:
+                rr.BlenderJob.from_dict(r["raw"])
+            assert "render_script_path" in str(e.value) or "unknown variant" in str(e.value)
+        else:
+            j = rr.BlenderJob.from_dict(r["raw"])
+            assert j.job_name == r["job_name"]
+            assert [j.frame_range_from, j.frame_range_to] == r["frames"]
+            assert j.frame_distribution_strategy.strategy_type == r["strategy"]
+            ok += 1
+    assert ok == 39
+
+
+def test_strategy_variants(rr):
+    base = {"job_name": "j", "project_file_path": "p", "render_script_path": "s", "frame_range_from": 1,
+            "frame_range_to": 3, "wait_for_number_of_workers": 1, "output_directory_path": "o",
+            "output_file_name_format": "#", "output_file_format": "PNG"}
+    j = rr.BlenderJob.from_dict({**base, "frame_distribution_strategy": {"strategy_type": "naive-fine"}})
+    assert j.frames() == [1, 2, 3] and j.job_description is None
+    with pytest.raises(rr.JobError):  # serde name is "eager-naive-coarse"
+        rr.BlenderJob.from_dict({**base, "frame_distribution_strategy": {"strategy_type": "naive-coarse",
+                                                                          "target_queue_size": 4}})
+    with pytest.raises(rr.JobError):
+        rr.BlenderJob.from_dict({**base, "frame_distribution_strategy": {"strategy_type": "dynamic",
+                                                                          "target_queue_size": 4}})
+    with pytest.raises(rr.JobError):
+        rr.BlenderJob.from_dict({**base, "frame_range_to": -1,
+                                 "frame_distribution_strategy": {"strategy_type": "naive-fine"}})
+    d = {**base, "frame_distribution_strategy": {"strategy_type": "dynamic", "target_queue_size": 4,
+                                                 "min_queue_size_to_steal": 2,
+                                                 "min_seconds_before_resteal_to_elsewhere": 40,
+                                                 "min_seconds_before_resteal_to_original_worker": 80}}
+    j = rr.BlenderJob.from_dict(d)
+    assert j.to_dict()["frame_distribution_strategy"] == d["frame_distribution_strategy"]
+
+
+def test_our_jobs_load(rr):
+    for name in os.listdir(os.path.join(ROOT, "jobs")):
+        if name.endswith(".toml"):
+            j = rr.BlenderJob.load_from_file(os.path.join(ROOT, "jobs", name))
+            proj = rr.parse_with_base_directory_prefix(j.project_file_path, ROOT)
+            assert rr.scene_path_for_project(proj).is_file(), name
+            assert rr.parse_with_base_directory_prefix(j.render_script_path, ROOT).is_file(), name
+    with pytest.raises(rr.JobError):
+        rr.BlenderJob.load_from_file(os.path.join(ROOT, "jobs"))
+    with pytest.raises(rr.JobError):
+        rr.BlenderJob.load_from_file(os.path.join(ROOT, "jobs", "nope.toml"))
+
+
+def test_base_directory_prefix(rr):
+    from pathlib import Path
+    assert rr.parse_with_base_directory_prefix("%BASE%/a/b", "/base") == Path("/base/a/b")
+    assert rr.parse_with_base_directory_prefix("%BASE%\\a", "/base") == Path("/base/a")
+    assert rr.parse_with_base_directory_prefix("%BASE%a", "/base") == Path("/base/a")
+    assert rr.parse_with_base_directory_prefix("/abs/x", "/base") == Path("/abs/x")
+    with pytest.raises(rr.JobError):
+        rr.parse_with_base_directory_prefix("%BASE%/x", None)
+
+
+# ------------------------------------------------------------- traces ------
+def _trace(rr):
+    b = rr.WorkerTraceBuilder()
+    b.set_job_start_time(1000.25)
+    for i in range(3):
+        b.trace_new_frame_queued()
+    t = types.SimpleNamespace(loaded_at=1001.0, started_rendering_at=1001.5, finished_rendering_at=1002.0,
+                              file_saving_started_at=1002.0, file_saving_finished_at=1002.125)
+    for f in (1, 2, 3):
+        b.trace_new_rendered_frame(f, rr.FrameRenderTime.from_timing(1000.5 + f, t, 1002.5 + f))
+    b.trace_new_ping(1000.0, 1000.001)
+    b.set_job_finish_time(1010.0)
+    return b.build()
+
+
+def test_trace_shape(rr):
+    tr = _trace(rr).to_dict()
+    assert set(tr) == {"total_queued_frames", "total_queued_frames_removed_from_queue", "job_start_time",
+                       "job_finish_time", "frame_render_traces", "ping_traces", "reconnection_traces"}
+    d = tr["frame_render_traces"][0]
+    assert d["frame_index"] == 1 and set(d["details"]) == set(rr.traces.FRAME_FIELDS)
+    with pytest.raises(ValueError):
+        rr.WorkerTraceBuilder().build()
+
+
+def test_raw_trace_loads_in_reference_analysis(rr, tmp_path):
+    """The analysis scripts (reference, Python >= 3.11) must keep working on our
+    traces: load the raw trace with analysis/core/models.py (typing.Self shim)."""
+    job = rr.BlenderJob.load_from_file(os.path.join(ROOT, "jobs", "04_very-simple_demo_10f-1w.toml"))
+    path = rr.save_raw_traces(job, tmp_path, 1000.0, 1011.0, {rr.worker_name(0xdeadbeef, "127.0.0.1:5000"):
+                                                                _trace(rr)})
+    doc = json.loads(path.read_text())
+    assert doc["job"]["frame_distribution_strategy"]["strategy_type"] == "eager-naive-coarse"
+    assert path.name.endswith("_job-04vs_demo_10f-1w_eager-naive-coarse_raw-trace.json")
+    if not have_reference():
+        pytest.skip("reference analysis scripts not present (GPU box)")
+    import typing
+    import typing_extensions
+    if not hasattr(typing, "Self"):
+        typing.Self = typing_extensions.Self
+    sys.path.insert(0, os.path.join(REFERENCE, "analysis"))
+    try:
+        from core.models import JobTrace
+        jt = JobTrace.load_from_trace_file(str(path))
+    finally:
+        sys.path.remove(os.path.join(REFERENCE, "analysis"))
+    assert len(jt.worker_traces) == 1

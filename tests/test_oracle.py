@@ -1,0 +1,212 @@
+"""Pins the CPU oracle itself (oracle/rr_oracle.c) before it is trusted as the
+GPU's checker: Cycles (the reference's renderer) is third-party and absent, so
+the oracle is pinned by analytic known answers instead:
+ray/triangle cases, LBVH == brute force, uniform RNG and disk sampling, BSDF
+identities, the white furnace and the point-light closed form."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import scene_path
+from oracle import host_oracle as HO
+from oracle import oracle as O
+
+
+def world_tris(scene, frame):
+    tris, mats = [], []
+    for o in scene["objects"]:
+        if o["type"] != "MESH":
+            continue
+        m = scene["meshes"][o["mesh"]]
+        if "generator" in m:
+            raise NotImplementedError
+        M = HO.object_matrix(o, frame).astype(np.float32)
+        v = np.array(m["vertices"], np.float32).reshape(-1, 3)
+        for tri in np.array(m["triangles"]).reshape(-1, 3):
+            tris.append([[((M[r, 0] * v[i, 0] + M[r, 1] * v[i, 1]) + M[r, 2] * v[i, 2]) + M[r, 3]
+                          for r in range(3)] for i in tri])
+            mats.append(m["material_slots"][0])
+    return np.array(tris, np.float32), np.array(mats, np.int32)
+
+
+def icosphere_tris(sub=3, radius=1.0):
+    t = (1 + 5 ** 0.5) / 2
+    v = [[-1, t, 0], [1, t, 0], [-1, -t, 0], [1, -t, 0], [0, -1, t], [0, 1, t], [0, -1, -t], [0, 1, -t],
+         [t, 0, -1], [t, 0, 1], [-t, 0, -1], [-t, 0, 1]]
+    v = [list(np.array(p) / np.linalg.norm(p)) for p in v]
+    f = [[0, 11, 5], [0, 5, 1], [0, 1, 7], [0, 7, 10], [0, 10, 11], [1, 5, 9], [5, 11, 4], [11, 10, 2],
+         [10, 7, 6], [7, 1, 8], [3, 9, 4], [3, 4, 2], [3, 2, 6], [3, 6, 8], [3, 8, 9], [4, 9, 5], [2, 4, 11],
+         [6, 2, 10], [8, 6, 7], [9, 8, 1]]
+    for _ in range(sub):
+        cache, nf = {}, []
+
+        def mid(a, b):
+            k = (min(a, b), max(a, b))
+            if k not in cache:
+                p = (np.array(v[a]) + np.array(v[b])) / 2
+                v.append(list(p / np.linalg.norm(p)))
+                cache[k] = len(v) - 1
+            return cache[k]
+        for a, b, c in f:
+            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+            nf += [[a, ab, ca], [b, bc, ab], [c, ca, bc], [ab, bc, ca]]
+        f = nf
+    V = np.array(v) * radius
+    return V[np.array(f)].astype(np.float32)
+
+
+def test_rng_uniform():
+    u = np.concatenate([O.rng(0, p, s, 16) for p in range(200) for s in range(4)])
+    assert u.min() >= 0.0 and u.max() < 1.0
+    assert abs(u.mean() - 0.5) < 0.01 and abs(u.var() - 1 / 12) < 0.005
+    assert not np.array_equal(O.rng(0, 1, 0, 8), O.rng(1, 1, 0, 8))
+
+
+def test_concentric_disk_uniform():
+    u = np.random.default_rng(0).random((200000, 2), dtype=np.float32)
+    xy = O.disk(u)
+    r2 = (xy ** 2).sum(1)
+    assert r2.max() <= 1.0 + 1e-6
+    assert abs((r2 < 0.25).mean() - 0.25) < 0.005  # area-uniform
+    ang = np.arctan2(xy[:, 1], xy[:, 0])
+    hist = np.histogram(ang, bins=16)[0]
+    assert hist.min() > 0.9 * hist.mean()
+
+
+def test_ray_triangle_known_cases():
+    tri = np.array([[[0, 0, 0], [1, 0, 0], [0, 1, 0]]], np.float32)
+    rays = np.array([[0.25, 0.25, 1, 0, 0, 0, -1, 10],     # hit, t=1, u=v=0.25
+                     [0.25, 0.25, -1, 0, 0, 0, 1, 10],     # back side (two-sided)
+                     [0.9, 0.9, 1, 0, 0, 0, -1, 10],       # outside (u+v>1)
+                     [0.25, 0.25, 1, 0, 1, 0, 0, 10],      # parallel
+                     [0.25, 0.25, 1, 0, 0, 0, -1, 0.5],    # beyond tmax
+                     [0.25, 0.25, 1, 2, 0, 0, -1, 10]],    # before tmin
+                    np.float32)
+    hits, prims, occ = O.trace(tri, rays)
+    assert list(prims) == [0, 0, -1, -1, -1, -1]
+    assert hits[0, 0] == 1.0 and hits[0, 1] == 0.25 and hits[0, 2] == 0.25
+    assert list(occ) == [1, 1, 0, 0, 0, 0]
+
+
+def test_lbvh_structure_and_brute_force():
+    rng = np.random.default_rng(5)
+    n = 3000
+    c = rng.uniform(-10, 10, (n, 1, 3))
+    tris = (c + rng.normal(0, 0.4, (n, 3, 3))).astype(np.float32)
+    keys, order, children, boxes = O.build_lbvh(tris)
+    assert np.all(np.diff(keys.astype(np.int64)) >= 0)
+    assert sorted(order) == list(range(n))
+    leaves = children[children < 0]
+    assert sorted((~leaves).tolist()) == list(range(n))
+    internal = children[children >= 0]
+    assert sorted(internal.tolist()) == list(range(1, n - 1))  # every node but the root has one parent
+    # boxes contain their triangles
+    for node in range(0, n - 1, 97):
+        for side in range(2):
+            ch = children[node, side]
+            if ch < 0:
+                t = tris[order[~ch]]
+                lo, hi = boxes[node, 6 * side:6 * side + 3], boxes[node, 6 * side + 3:6 * side + 6]
+                assert np.all(t >= lo) and np.all(t <= hi)
+    o = rng.uniform(-15, 15, (4000, 3))
+    d = rng.normal(size=(4000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, np.zeros((4000, 1)), d, np.full((4000, 1), 1e30)], axis=1).astype(np.float32)
+    hits, prims, occ = O.trace(tris, rays)
+    bh, bp = O.trace_brute(tris, rays)
+    assert np.array_equal(prims, bp)
+    assert np.array_equal(hits[:, 0], bh[:, 0])
+    assert np.array_equal(occ.astype(bool), bp >= 0)
+    assert (prims >= 0).mean() > 0.1
+
+
+def test_lbvh_degenerate_inputs():
+    tri = np.array([[[0, 0, 0], [1, 0, 0], [0, 1, 0]]], np.float32)
+    k, o, ch, b = O.build_lbvh(tri)
+    assert list(ch[0]) == [~0, ~0]
+    same = np.repeat(tri, 50, axis=0)  # 50 identical triangles: duplicate Morton keys
+    k, o, ch, b = O.build_lbvh(same)
+    assert np.all(k == k[0]) and sorted(o) == list(range(50))
+    hits, prims, _ = O.trace(same, np.array([[0.2, 0.2, 1, 0, 0, 0, -1, 5]], np.float32))
+    assert prims[0] == 0  # equal t: the smallest original id wins
+
+
+def test_lambert_and_principled_bsdf():
+    n = [0, 0, 1]
+    wo = [0, 0.6, 0.8]
+    wi = [0.6, 0, 0.8]
+    lam = [0.5, 0.25, 1.0, 0, 0, 1.0, 1.45, 0, 0, 0, 1.0, 0]
+    f, pdf = O.bsdf_eval(lam, n, wo, wi)
+    np.testing.assert_allclose(f, np.array([0.5, 0.25, 1.0]) / np.pi, rtol=1e-6)
+    assert pdf == pytest.approx(0.8 / np.pi, rel=1e-6)
+    pr = [0.8, 0.8, 0.8, 0.0, 0.5, 0.5, 1.45, 0, 0, 0, 0.0, 0]
+    f1, _ = O.bsdf_eval(pr, n, wo, wi)
+    f2, _ = O.bsdf_eval(pr, n, wi, wo)
+    np.testing.assert_allclose(f1, f2, rtol=1e-6)  # reciprocity
+    f3, p3 = O.bsdf_eval(pr, n, wo, [0.6, 0, -0.8])
+    assert np.all(f3 == 0) and p3 == 0
+
+
+def _render_scene(name, frame=1, **over):
+    """Oracle render from the Python restatement (no product code involved)."""
+    scene = HO.load_scene(scene_path(name))
+    r = scene["render"]
+    W, H = r["resolution_x"], r["resolution_y"]
+    fc = HO.frame_constants(scene, frame)
+    tris, mats = [], []
+    for o in scene["objects"]:
+        if o["type"] != "MESH":
+            continue
+        g = scene["meshes"][o["mesh"]]["generator"]
+        if g["type"] == "icosphere":
+            t = icosphere_tris(g["subdivisions"], g["radius"])
+        else:
+            h = g["size"] / 2
+            t = np.array([[[-h, -h, 0], [h, -h, 0], [h, h, 0]], [[-h, -h, 0], [h, h, 0], [-h, h, 0]]], np.float32)
+        tris.append(t + np.array(o["location"], np.float32))
+        mats += [0] * len(t)
+    ri = np.array([W, H, over.get("spp", r["samples"]), r["max_bounces"], r["seed"],
+                   1 if r["view_transform"] == "Raw" else 0, 0, 0], np.int32)
+    rf = np.array([r["clamp_indirect"], r["filter_width"], 1.0, 0], np.float32)
+    return O.render(np.concatenate(tris), np.array(mats), fc["camera"], fc["lights"], fc["materials"],
+                    fc["world"], ri, rf, threads=4)
+
+
+def test_white_furnace():
+    film, rgba = _render_scene("test_furnace.rrscene")
+    center = film[20:28, 28:36, :3].reshape(-1, 3)
+    np.testing.assert_allclose(center, np.tile([0.4, 0.3, 0.2], (len(center), 1)), rtol=2e-6)
+    np.testing.assert_allclose(film[0, 0, :3], [0.8, 0.6, 0.4], rtol=1e-6)
+    assert rgba[0, 0, 0] == 204 and rgba[24, 32, 0] == 102  # Raw view: round(0.8*255), round(0.4*255)
+
+
+def test_point_light_closed_form():
+    film, _ = _render_scene("test_pointlight.rrscene", spp=64)
+    scene = HO.load_scene(scene_path("test_pointlight.rrscene"))
+    cam = HO.frame_constants(scene, 1)["camera"]
+    py, px = np.mgrid[0:64, 0:64]
+    sx = ((px + 0.5) * (2.0 / 64) - 1.0) * cam[12]
+    sy = (1.0 - (py + 0.5) * (2.0 / 64)) * cam[13]
+    x, y = sx * 10.0, sy * 10.0
+    r2 = (x - 1.0) ** 2 + (y - 0.5) ** 2 + 4.0
+    L = 0.8 / math.pi * (100.0 / (4 * math.pi)) * 2.0 / r2 ** 1.5
+    rel = np.abs(film[..., 0] - L) / L
+    assert np.median(rel) < 0.01 and np.percentile(rel, 95) < 0.05
+
+
+def test_04_frame_is_plausible():
+    scene = HO.load_scene(scene_path("04_very-simple-standin.rrscene"))
+    fc = HO.frame_constants(scene, 30, 96, 54)
+    tris, mats = world_tris(scene, 30)
+    ri = np.array([96, 54, 8, 12, 0, 0, 0, 0], np.int32)
+    rf = np.array([10.0, 1.5, 1.0, 0], np.float32)
+    film, rgba = O.render(tris, mats, fc["camera"], fc["lights"], fc["materials"], fc["world"], ri, rf,
+                          threads=4)
+    bg = film[50, 2, :3]
+    np.testing.assert_allclose(bg, fc["world"], rtol=1e-6)  # background pixel = world colour
+    assert film[..., 0].max() > 0.3  # the lit cube face
+    # deterministic, and row slices reproduce the full render exactly
+    f2, r2 = O.render(tris, mats, fc["camera"], fc["lights"], fc["materials"], fc["world"], ri, rf,
+                      rows=(10, 20), threads=2)
+    assert np.array_equal(f2[10:20], film[10:20]) and np.array_equal(r2[10:20], rgba[10:20])

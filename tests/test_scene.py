@@ -1,0 +1,137 @@
+"""Scene format, exporter and host-side frame evaluation (no GPU needed):
+the product's C++ animation/camera evaluation (through the C ABI, host-only
+scene handles) vs the Python restatement and the golden values decoded from
+the reference's .blend."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, have_reference, scene_path
+from oracle import host_oracle as HO
+
+S01 = scene_path("01_simple-animation.rrscene")
+S04 = scene_path("04_very-simple-standin.rrscene")
+BLEND = "/root/reference/blender-projects/01_simple-animation/01_simple-animation.blend"
+
+
+def test_fcurve_golden_table(rr):
+    g = json.load(open(os.path.join(GOLDEN, "fcurve_01_cube_z.json")))
+    s = rr.Scene(S01)
+    scene = HO.load_scene(S01)
+    obj = scene["objects"][g["object_index"]]
+    assert obj["name"] == g["object"]
+    for f, z in g["frames"].items():
+        zp = s.object_matrix(g["object_index"], int(f))[2, 3]
+        zo = HO.object_matrix(obj, int(f))[2, 3]
+        assert zp == zo, f"product and restatement differ at frame {f}"
+        assert abs(zp - z) <= g["tolerance"], (f, zp, z)
+    # Blender saved the file at cfra=60 with the evaluated location
+    assert s.object_matrix(1, g["saved_frame"])[2, 3] == g["saved_z"]
+    s.close()
+
+
+@pytest.mark.parametrize("frame", [1, 1.5, 7, 33.25, 59.999, 60, 61, 1000, -5])
+def test_fcurve_product_equals_restatement(rr, frame):
+    s = rr.Scene(S01)
+    scene = HO.load_scene(S01)
+    for i, o in enumerate(scene["objects"]):
+        assert np.array_equal(s.object_matrix(i, frame), HO.object_matrix(o, frame)), (i, frame)
+    s.close()
+
+
+def test_fcurve_interpolation_modes():
+    keys = [{"co": [1, 0], "handle_left": [0, 0], "handle_right": [2, 0], "interpolation": "LINEAR"},
+            {"co": [11, 10], "handle_left": [10, 10], "handle_right": [12, 10], "interpolation": "CONSTANT"},
+            {"co": [21, 0], "handle_left": [20, 0], "handle_right": [22, 0], "interpolation": "BEZIER"}]
+    assert HO.eval_fcurve(keys, "CONSTANT", 6) == pytest.approx(5.0)
+    assert HO.eval_fcurve(keys, "CONSTANT", 15) == 10.0   # constant segment holds the left key
+    assert HO.eval_fcurve(keys, "CONSTANT", -3) == 0.0
+    assert HO.eval_fcurve(keys, "LINEAR", -3) == pytest.approx(-4.0)  # linear extrapolation of a LINEAR key
+    assert HO.eval_fcurve(keys, "CONSTANT", 40) == 0.0
+
+
+def test_camera_matches_saved_blender_matrix(rr):
+    scene = HO.load_scene(S01)
+    cam = scene["objects"][scene["camera"]]
+    saved = np.array(cam["matrix_world_saved"]).reshape(4, 4).T  # Blender column-major
+    s = rr.Scene(S01)
+    np.testing.assert_allclose(s.object_matrix(scene["camera"], 60), saved, atol=2e-7)
+    s.close()
+
+
+def test_frame_constants_product_vs_restatement(rr):
+    for path in (S01, S04):
+        s = rr.Scene(path)
+        scene = HO.load_scene(path)
+        for frame in (1, 45):
+            st = s.frame_constants(frame)
+            fc = HO.frame_constants(scene, frame)
+            np.testing.assert_allclose(st.camera, fc["camera"], atol=2e-7)
+            np.testing.assert_allclose(st.lights, fc["lights"], rtol=1e-7, atol=1e-7)
+            np.testing.assert_allclose(st.materials, fc["materials"], atol=1e-7)
+            np.testing.assert_allclose(st.world, fc["world"], rtol=1e-7)
+        s.close()
+    # 01 light: 1000 W point light of radius 0.1 -> I = 1000/(4 pi) W/sr
+    st = rr.Scene(S01).frame_constants(1)
+    assert st.lights[0, 0] == 0 and st.lights[0, 7] == pytest.approx(0.1)
+    assert st.lights[0, 8] == pytest.approx(1000 / (4 * np.pi), rel=1e-6)
+    assert st.camera[12] == pytest.approx(0.36) and st.camera[13] == pytest.approx(0.36 * 1080 / 1920)
+
+
+def test_render_params_override(rr):
+    s = rr.Scene(S04)
+    st = s.frame_constants(1, rr.default_params(width=320, height=200, spp=7, max_bounces=3, seed=9))
+    assert list(st.render_ints[:5]) == [320, 200, 7, 3, 9]
+    assert st.camera[13] == pytest.approx(0.36 * 200 / 320)
+    st = s.frame_constants(1, rr.default_params(width=100, height=400))  # portrait: AUTO fits vertically
+    assert st.camera[13] == pytest.approx(0.36) and st.camera[12] == pytest.approx(0.09)
+
+
+@pytest.mark.skipif(not have_reference(), reason="needs the reference .blend")
+def test_exporter_reproduces_committed_scene():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from blend_export import export
+
+    class A:
+        samples, max_bounces, clamp_indirect, seed = 128, 12, 10.0, 0
+
+    fresh = export(BLEND, A)
+    committed = HO.load_scene(S01)
+    assert json.loads(json.dumps(fresh)) == committed
+    cube = fresh["meshes"][0]
+    assert len(cube["triangles"]) == 36 and len(cube["vertices"]) == 24
+    assert fresh["render"]["resolution_x"] == 1920 and fresh["source"]["engine"] == "BLENDER_EEVEE"
+    mat = fresh["materials"][cube["material_slots"][0]]
+    assert mat["base_color"] == pytest.approx([0.8, 0.8, 0.8]) and mat["roughness"] == pytest.approx(0.5)
+    assert mat["distribution"] == "GGX"
+
+
+def test_procedural_meshes(rr, tmp_path):
+    scene = {"format": "rrscene", "version": 1, "name": "gen",
+             "meshes": [{"generator": {"type": "icosphere", "subdivisions": 3, "radius": 2.0}},
+                        {"generator": {"type": "cube", "size": 1.0}}, {"generator": {"type": "plane"}}],
+             "objects": [{"type": "CAMERA", "camera": {"lens": 50}, "location": [0, -5, 0],
+                          "rotation_euler": [1.57, 0, 0]},
+                         {"type": "MESH", "mesh": 0}, {"type": "MESH", "mesh": 1}, {"type": "MESH", "mesh": 2}]}
+    p = tmp_path / "gen.rrscene"
+    p.write_text(json.dumps(scene))
+    s = rr.Scene(str(p))
+    assert s.counts()["triangles"] == 20 * 4 ** 3 + 12 + 2
+    s.close()
+
+
+def test_scene_validation(rr, tmp_path):
+    bad = [{"format": "rrscene", "version": 2, "objects": []},
+           {"format": "rrscene", "version": 1, "objects": [{"type": "MESH", "mesh": 0}],
+            "meshes": [{"vertices": [0, 0, 0], "triangles": [0, 1, 2]}]},
+           {"format": "rrscene", "version": 1, "objects": [{"type": "LIGHT", "light": {"type": "AREA"}}]},
+           {"format": "rrscene", "version": 1, "objects": [{"type": "EMPTY"}]}]
+    for i, d in enumerate(bad):
+        p = tmp_path / f"b{i}.rrscene"
+        p.write_text(json.dumps(d))
+        with pytest.raises(rr.RRError) as e:
+            rr.Scene(str(p))
+        assert e.value.code == -22, d
