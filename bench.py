@@ -55,19 +55,20 @@ def algorithmic_bytes(cls: str, stats, max_bounces: int) -> float:
     npaths = stats.camera_rays
     ext = stats.extension_rays
     sh = stats.shadow_rays
-    if cls == "raygen":
-        return npaths * 64.0                          # ray 32 + throughput 16 + radiance 16
-    if cls == "closest":
-        rays = npaths + ext
-        return rays * 48.0 + ext * 4.0 + 64.0 * stats.closest_nodes + 48.0 * stats.closest_tris
+    c0, s0 = stats.primary_continued, stats.primary_shadow
+    node, tri = 64.0, 48.0  # one BVH2 node line, one packed triangle
+    if cls == "primary":
+        # radiance record write 16 B per camera path; compacted writes of the
+        # continuing state (48 B) and shadow entries (48 B); BVH/triangle reads;
+        # the hit triangle re-read by shading (lower bound: max(continued, shadowed))
+        return (npaths * 16.0 + c0 * 48.0 + s0 * 48.0 + node * stats.trav_nodes[0] + tri * stats.trav_tris[0]
+                + tri * max(c0, s0))
+    if cls == "extend":
+        ce, se = ext - c0, sh - s0
+        return (ext * (48.0 + 32.0) + ce * 48.0 + se * 48.0 + node * stats.trav_nodes[1]
+                + tri * stats.trav_tris[1] + tri * max(ce, se))
     if cls == "shadow":
-        return sh * (4.0 + 32.0 + 16.0 + 32.0) + 64.0 * stats.shadow_nodes + 48.0 * stats.shadow_tris
-    if cls == "shade":
-        shaded = npaths + ext
-        # read hit+ray+thr+rad (80) + write rad (16) + queue read for b>0;
-        # continued paths write ray+thr+queue (52); NEE writes shadow ray+contrib+queue (52);
-        # hit paths read the 48-B triangle (lower bound: max(continued, shadowed) hits)
-        return shaded * 96.0 + ext * 4.0 + ext * 52.0 + sh * 52.0 + max(ext, sh) * 48.0
+        return sh * (48.0 + 32.0) + node * stats.trav_nodes[2] + tri * stats.trav_tris[2]
     if cls == "accumulate":
         npix = stats.width * stats.height
         return npix * (stats.spp * 16.0 + 32.0 * max(stats.chunks - 1, 0) + 16.0 + 4.0)

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "rr.h"
 #include "rr_device.h"
 
 namespace rr {
@@ -119,8 +120,9 @@ struct KernelProfiler {
 // Per-context wavefront state (sized for the largest chunk seen).
 struct DevPaths {
     size_t cap = 0;
-    DevBuf<float4> ray_o, ray_d, hit, thr, rad, sh_o, sh_d, sh_c;
-    DevBuf<int32_t> q[2], sq;
+    DevBuf<float4> rad;                        // per path (p-indexed) radiance record
+    DevBuf<float4> ps_o[2], ps_d[2], ps_t[2];  // dense path queue, ping-pong per bounce
+    DevBuf<float4> sh_o, sh_d, sh_c;           // dense shadow queue
     DevBuf<int32_t> counters;  // per chunk: [ext 0..B+1 | shadow 0..B]
     DevBuf<int32_t> spill;     // traversal stack spill
     DevBuf<float4> film;
@@ -128,7 +130,7 @@ struct DevPaths {
     DevBuf<float> filter_table;
     DevBuf<float> srgb_lut;
     DevBuf<float> lights, materials;
-    DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: 4 totals
+    DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: 6 totals
     KernelProfiler prof;
     bool count_traversal = false;
     int grid_blocks = 0;  // persistent grid for path kernels

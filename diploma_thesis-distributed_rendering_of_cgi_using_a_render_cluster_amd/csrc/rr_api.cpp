@@ -198,7 +198,7 @@ int choose_spp_chunk(const FrameSetup& fs) {
     if (fs.spp_per_chunk > 0) return std::min(fs.spp_per_chunk, fs.spp);
     // ~16M paths in flight: fills 256 CUs many times over and keeps the SoA
     // path state (~140 B/path, ~2.3 GB) well inside HBM.
-    const long target = 16L << 20;
+    const long target = 64L << 20;
     long c = target / std::max(1, fs.W * fs.H);
     if (c < 1) c = 1;
     if (c > fs.spp) c = fs.spp;
@@ -212,7 +212,7 @@ struct FrameRun {
     std::vector<int32_t> counters;
     double kernel_ms[RR_K_CLASSES];
     int32_t kernel_launches[RR_K_CLASSES];
-    unsigned long long trav[4];
+    unsigned long long trav[6];
 };
 
 // Run the device part of one frame; leaves the 8-bit image in c->host_rgba.
@@ -280,15 +280,17 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
         const int32_t* shc = ext + fs.max_bounces + 2;
         for (int b = 1; b <= fs.max_bounces; ++b) st->extension_rays += (uint64_t)ext[b];
         for (int b = 0; b <= fs.max_bounces; ++b) st->shadow_rays += (uint64_t)shc[b];
+        st->primary_continued += (uint64_t)ext[1];
+        st->primary_shadow += (uint64_t)shc[0];
     }
     for (int k = 0; k < RR_K_CLASSES; ++k) {
         st->kernel_ms[k] = r.kernel_ms[k];
         st->kernel_launches[k] = r.kernel_launches[k];
     }
-    st->closest_nodes = r.trav[0];
-    st->closest_tris = r.trav[1];
-    st->shadow_nodes = r.trav[2];
-    st->shadow_tris = r.trav[3];
+    for (int k = 0; k < 3; ++k) {
+        st->trav_nodes[k] = r.trav[2 * k];
+        st->trav_tris[k] = r.trav[2 * k + 1];
+    }
     st->build_ms = r.rebuilt ? r.build_ms : 0.0;
     st->trace_ms = r.trace_ms;
     st->readback_ms = r.readback_ms;

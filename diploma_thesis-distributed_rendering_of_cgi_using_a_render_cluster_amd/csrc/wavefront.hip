@@ -1,12 +1,25 @@
-// Wavefront path tracer: per chunk of spp_chunk samples x all
-// pixels, K6 raygen -> { K7 closest-hit traversal -> K9 shade (+NEE setup,
-// ballot/popcount queue compaction) -> K10 shadow any-hit } x bounces ->
-// K11 film accumulate (+ K12 tonemap on the last chunk).
+// Wavefront path tracer. Per chunk of spp_chunk samples x all
+// pixels:
+//   K-primary  (K6 raygen + K7 closest-hit traversal + K9 shade, bounce 0):
+//              the camera path lives in registers; it writes its radiance
+//              record and appends, through wave-level ballot/popcount queue
+//              compaction (K8), only what continues: the next ray + throughput
+//              to the dense path queue and the NEE ray to the shadow queue;
+//   K-shadow   (K10 any-hit): one launch per bounce over the dense shadow
+//              queue, adds the unoccluded NEE contribution to the radiance
+//              record;
+//   K-extend   (K7 + K9 + K8, bounce >= 1): one launch per bounce over the
+//              dense path queue (coalesced SoA reads, compacted writes);
+//   K-accumulate (K11 + K12 on the last chunk): film += chunk radiance in
+//              sample order, then mean -> exposure -> view transform -> 8-bit.
+// Every kernel is a persistent grid-stride loop over a device-side queue count,
+// so a frame is one stream of launches with no host round trip.
 //
-// Path state is SoA float4 in HBM; every path kernel is a persistent
-// grid-stride loop over a device-side queue count (no host round trip between
-// bounces, so a frame is one stream of launches). The arithmetic is the
-// uncontracted, libm-free form of rr_device.h and matches oracle/rr_oracle.c.
+// HBM per camera path: 16 B radiance write + 16 B accumulate read; per
+// continuing path per bounce: 48 B state write + read, 32 B radiance RMW;
+// per shadow ray: 48 B write + read (+32 B RMW). The arithmetic is the
+// uncontracted, libm-free form of rr_device.h and matches oracle/rr_oracle.c
+// bit for bit.
 //
 // Replaces the per-pixel, per-sample path integration of Cycles behind
 // bpy.ops.render.render (/root/reference/scripts/render-timing-script.py:90).
@@ -31,6 +44,19 @@ constexpr int kFilterN = 1024;
 constexpr int kSrgbN = 4096;
 constexpr int kLightF = 12;
 constexpr int kMatF = 12;
+constexpr float kFltMax = 3.402823466e+38f;
+
+// Dense queue state (SoA, ping-pong per bounce).
+struct PathQueue {
+    float4* o;  // origin.xyz, path id (int bits)
+    float4* d;  // direction.xyz, 0
+    float4* t;  // throughput.xyz, 0
+};
+struct ShadowQueue {
+    float4* o;  // origin.xyz, path id (int bits)
+    float4* d;  // direction.xyz, tmax
+    float4* c;  // contribution.xyz, 0
+};
 
 __device__ __forceinline__ Mat load_mat(const float* __restrict__ mats, int id) {
     const float* m = mats + kMatF * id;
@@ -47,9 +73,8 @@ __device__ __forceinline__ Mat load_mat(const float* __restrict__ mats, int id) 
 
 // Camera ray for (pixel, sample): filter-importance-sampled subpixel position,
 // pinhole through the sensor plane at unit distance, z-depth clipping.
-__device__ __forceinline__ void camera_ray(const FrameConsts& fc, const float* __restrict__ filt,
-                                           int pix, uint32_t key, float3& o, float3& d, float& tmin,
-                                           float& tmax) {
+__device__ __forceinline__ void camera_ray(const FrameConsts& fc, const float* __restrict__ filt, int pix,
+                                           uint32_t key, float3& o, float3& d, float& tmin, float& tmax) {
     const int px = pix % fc.W;
     const int py = pix / fc.W;
     const float fx = (float)px + 0.5f + table_lerp(filt, kFilterN, rng(key, 0));
@@ -67,230 +92,272 @@ __device__ __forceinline__ void camera_ray(const FrameConsts& fc, const float* _
     tmax = fc.clip_end * len;
 }
 
-// K6
-__global__ __launch_bounds__(kBlock) void k_raygen(FrameConsts fc, const float* __restrict__ filt,
-                                                   float4* __restrict__ ray_o, float4* __restrict__ ray_d,
-                                                   float4* __restrict__ thr, float4* __restrict__ rad,
-                                                   int npaths) {
-    for (int p = blockIdx.x * kBlock + threadIdx.x; p < npaths; p += gridDim.x * kBlock) {
-        const int sl = p / fc.npix;
-        const int pix = p - sl * fc.npix;
-        const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-        float3 o, d;
-        float tmin, tmax;
-        camera_ray(fc, filt, pix, key, o, d, tmin, tmax);
-        ray_o[p] = make_float4(o.x, o.y, o.z, tmin);
-        ray_d[p] = make_float4(d.x, d.y, d.z, tmax);
-        thr[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-        rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
+struct ShadeOut {
+    bool cont, shadow;
+    float3 o, d, T;          // continuation ray + throughput
+    float3 so, sd, sc;       // shadow ray + pending contribution
+    float sdist;
+};
+
+RR_D void add_to(float3& L, float3 c) {
+    L.x = L.x + c.x;
+    L.y = L.y + c.y;
+    L.z = L.z + c.z;
 }
 
-// K7 / K10: traverse rays of a queue. kAny: shadow rays (any hit, adds the
-// pending NEE contribution when unoccluded); else closest hit -> hit buffer.
-template <bool kAny>
-__global__ __launch_bounds__(kBlock) void k_trace(const BvhNode* __restrict__ nodes,
-                                                  const TriPack* __restrict__ tris, int n_tris,
-                                                  const int32_t* __restrict__ queue,
-                                                  const int32_t* __restrict__ count_ptr, int count_fixed,
-                                                  const float4* __restrict__ ray_o,
-                                                  const float4* __restrict__ ray_d,
-                                                  float4* __restrict__ hit, const float4* __restrict__ contrib,
-                                                  float4* __restrict__ rad, int32_t* __restrict__ spill,
-                                                  unsigned long long* __restrict__ trav_counts) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
-    const int count = count_ptr ? *count_ptr : count_fixed;
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
-    const int nthreads = gridDim.x * kBlock;
-    TravStack st{&lds_stack[threadIdx.x], spill + gtid, nthreads, 0};
-    uint32_t nv = 0, nt = 0;
-    uint32_t* pnv = trav_counts ? &nv : nullptr;
-    uint32_t* pnt = trav_counts ? &nt : nullptr;
-    for (int i = gtid; i < count; i += nthreads) {
-        const int p = queue ? queue[i] : i;
-        const float4 ro = ray_o[p], rd = ray_d[p];
-        Hit h;
-        const bool any = traverse<kAny>(nodes, tris, n_tris, xyz(ro), xyz(rd), ro.w, rd.w, st, h, pnv, pnt);
-        if (kAny) {
-            if (!any) {
-                const float4 c = contrib[p];
-                float4 L = rad[p];
-                L.x = L.x + c.x;
-                L.y = L.y + c.y;
-                L.z = L.z + c.z;
-                rad[p] = L;
+// K9: shade one path at `bounce` given its closest hit; L updated in place.
+__device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const LightsMats& lm,
+                                      const TriPack* __restrict__ tris, float3 o, float3 d, float3 T,
+                                      const Hit& h, uint32_t key, float3& L, ShadeOut& out) {
+    out.cont = false;
+    out.shadow = false;
+    if (h.idx < 0) {
+        float3 c = mul3(T, fc.world);
+        if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
+        add_to(L, c);
+        return;
+    }
+    const TriPack tp = tris[h.idx];
+    const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2);
+    const Mat m = load_mat(lm.materials, f2i(tp.p1.w));
+    const float t = h.t;
+    const float3 P = mk3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+    float3 N = norm3(cross3(e1, e2));
+    if (dot3(N, d) > 0.0f) N = mk3(-N.x, -N.y, -N.z);
+    const float3 wo = mk3(-d.x, -d.y, -d.z);
+    if (m.emission.x != 0.0f || m.emission.y != 0.0f || m.emission.z != 0.0f) {
+        float3 c = mul3(T, m.emission);
+        if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
+        add_to(L, c);
+    }
+    if (bounce >= fc.max_bounces) return;
+    const uint32_t dim0 = 2u + (uint32_t)(kDimsPerBounce * bounce);
+    const float3 Po = offset_ray(P, N);
+    // next-event estimation toward one uniformly chosen light
+    if (fc.n_lights > 0) {
+        int li = (int)(rng(key, dim0) * (float)fc.n_lights);
+        if (li > fc.n_lights - 1) li = fc.n_lights - 1;
+        const float* lt = lm.lights + kLightF * li;
+        float3 wi, Li;  // Li: radiance x cos_light / pdf (solid angle), i.e. I*cos/d^2
+        float dist;
+        if (lt[0] == 0.0f) {  // point / disk light
+            const float3 lp = mk3(lt[1], lt[2], lt[3]);
+            const float radius = lt[7];
+            const float3 I = mk3(lt[8], lt[9], lt[10]);
+            const float3 tl = sub3(lp, P);
+            const float dl2 = dot3(tl, tl);
+            if (radius > 0.0f) {
+                const float3 wl = scl3(tl, 1.0f / sqrtf(dl2));
+                float3 b1, b2;
+                make_onb(wl, b1, b2);
+                float dx, dy;
+                concentric_disk(rng(key, dim0 + 1u), rng(key, dim0 + 2u), dx, dy);
+                dx = dx * radius;
+                dy = dy * radius;
+                const float3 sp = mk3(lp.x + b1.x * dx + b2.x * dy, lp.y + b1.y * dx + b2.y * dy,
+                                      lp.z + b1.z * dx + b2.z * dy);
+                const float3 ts = sub3(sp, P);
+                const float ds2 = dot3(ts, ts);
+                dist = sqrtf(ds2);
+                wi = scl3(ts, 1.0f / dist);
+                const float cl = fabsf(dot3(wl, wi));
+                Li = scl3(I, cl / ds2);
+            } else {
+                dist = sqrtf(dl2);
+                wi = scl3(tl, 1.0f / dist);
+                Li = scl3(I, 1.0f / dl2);
             }
-        } else {
-            hit[p] = make_float4(h.t, h.u, h.v, i2f(h.idx));
+        } else {  // sun: delta direction, irradiance
+            wi = mk3(-lt[4], -lt[5], -lt[6]);
+            dist = kFltMax;
+            Li = mk3(lt[8], lt[9], lt[10]);
+        }
+        const float cosN = dot3(N, wi);
+        if (cosN > 0.0f) {
+            float pdf;
+            const float ps = spec_prob(m, dot3(N, wo));
+            const float3 f = bsdf_eval(m, N, wo, wi, ps, pdf);
+            const float k = cosN * (float)fc.n_lights;
+            float3 c = mk3(T.x * f.x * k * Li.x, T.y * f.y * k * Li.y, T.z * f.z * k * Li.z);
+            if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
+            if (max3f(c) > 0.0f) {
+                out.shadow = true;
+                out.so = Po;
+                out.sd = wi;
+                out.sdist = dist;
+                out.sc = c;
+            }
         }
     }
-    if (trav_counts) {  // measurement mode only: one atomic pair per wave
-        unsigned long long a = nv, b = nt;
-        for (int off = 32; off > 0; off >>= 1) {
-            a += __shfl_xor(a, off);
-            b += __shfl_xor(b, off);
-        }
-        if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&trav_counts[kAny ? 2 : 0], a);
-            atomicAdd(&trav_counts[kAny ? 3 : 1], b);
-        }
+    // continue the path
+    float3 wi, f;
+    float pdf;
+    if (!bsdf_sample(m, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f, pdf))
+        return;
+    const float cosL = dot3(N, wi);
+    if (!(cosL > 0.0f)) return;
+    const float k = cosL / pdf;
+    T = mk3(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
+    if (!(max3f(T) > 0.0f)) return;
+    if (bounce >= kRrStartBounce) {
+        const float q = fminf(max3f(T), 1.0f);
+        if (rng(key, dim0 + 6u) >= q) return;
+        T = mk3(T.x / q, T.y / q, T.z / q);
     }
+    out.cont = true;
+    out.o = Po;
+    out.d = wi;
+    out.T = T;
 }
 
-// Wave-aggregated queue append (ballot + popcount, one atomic per wave).
-__device__ __forceinline__ void wave_append(bool want, int value, int32_t* __restrict__ q,
-                                            int32_t* __restrict__ cnt) {
+// K8: wave-aggregated slot allocation (ballot + popcount, one atomic per wave).
+// Every lane of the wave must call it.
+__device__ __forceinline__ int wave_slot(bool want, int32_t* __restrict__ cnt) {
     const uint64_t mask = __ballot(want);
-    if (mask == 0ull) return;
+    if (mask == 0ull) return -1;
     const int lane = threadIdx.x & 63;
     const int leader = __ffsll((unsigned long long)mask) - 1;
     int base = 0;
     if (lane == leader) base = atomicAdd(cnt, __popcll(mask));
     base = __shfl(base, leader);
-    if (want) {
-        const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-        q[base + __popcll(mask & lt)] = value;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    return want ? base + __popcll(mask & lt) : -1;
+}
+
+__device__ __forceinline__ void emit(const ShadeOut& so, int pid, PathQueue out, int32_t* cnt_out,
+                                     ShadowQueue sq, int32_t* cnt_sh) {
+    const int s1 = wave_slot(so.cont, cnt_out);
+    if (s1 >= 0) {
+        out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
+        out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, 0.0f);
+        out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, 0.0f);
+    }
+    const int s2 = wave_slot(so.shadow, cnt_sh);
+    if (s2 >= 0) {
+        sq.o[s2] = make_float4(so.so.x, so.so.y, so.so.z, i2f(pid));
+        sq.d[s2] = make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist);
+        sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, 0.0f);
     }
 }
 
-// K9: shade bounce b.
-__global__ __launch_bounds__(kBlock) void k_shade(FrameConsts fc, int bounce, LightsMats lm,
-                                                  const TriPack* __restrict__ tris,
-                                                  const int32_t* __restrict__ q_in,
-                                                  const int32_t* __restrict__ cnt_in, int count_fixed,
-                                                  int32_t* __restrict__ q_out, int32_t* __restrict__ cnt_out,
-                                                  int32_t* __restrict__ sq, int32_t* __restrict__ cnt_sh,
-                                                  float4* __restrict__ ray_o, float4* __restrict__ ray_d,
-                                                  const float4* __restrict__ hit, float4* __restrict__ thr,
-                                                  float4* __restrict__ rad, float4* __restrict__ sh_o,
-                                                  float4* __restrict__ sh_d, float4* __restrict__ sh_c) {
-    const int count = cnt_in ? *cnt_in : count_fixed;
-    const int lane = threadIdx.x & 63;
-    const int stride = gridDim.x * kBlock;
-    const uint32_t dim0 = 2u + (uint32_t)(kDimsPerBounce * bounce);
-    for (int i0 = blockIdx.x * kBlock + threadIdx.x - lane; i0 < count; i0 += stride) {
-        const int i = i0 + lane;
-        const bool active = i < count;
-        bool cont = false, shadow = false;
-        int p = 0;
-        if (active) {
-            p = q_in ? q_in[i] : i;
-            const float4 ro = ray_o[p], rd = ray_d[p], hv = hit[p];
-            const float4 T4 = thr[p];
-            float3 T = xyz(T4);
-            float4 L = rad[p];
-            const int idx = f2i(hv.w);
-            const float3 d = xyz(rd);
-            if (idx < 0) {
-                float3 c = mul3(T, fc.world);
-                if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
-                L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;
-                rad[p] = L;
-            } else {
-                const TriPack tp = tris[idx];
-                const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2);
-                const Mat m = load_mat(lm.materials, f2i(tp.p1.w));
-                const float t = hv.x;
-                const float3 P = mk3(ro.x + rd.x * t, ro.y + rd.y * t, ro.z + rd.z * t);
-                float3 N = norm3(cross3(e1, e2));
-                if (dot3(N, d) > 0.0f) N = mk3(-N.x, -N.y, -N.z);
-                const float3 wo = mk3(-d.x, -d.y, -d.z);
-                if (m.emission.x != 0.0f || m.emission.y != 0.0f || m.emission.z != 0.0f) {
-                    float3 c = mul3(T, m.emission);
-                    if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
-                    L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;
-                }
-                if (bounce < fc.max_bounces) {
-                    const int p_pix = p % fc.npix;
-                    const int p_smp = fc.first_sample + p / fc.npix;
-                    const uint32_t key = path_key(fc.seed, (uint32_t)p_pix, (uint32_t)p_smp);
-                    const float3 Po = offset_ray(P, N);
-                    // next-event estimation toward one uniformly chosen light
-                    if (fc.n_lights > 0) {
-                        int li = (int)(rng(key, dim0) * (float)fc.n_lights);
-                        if (li > fc.n_lights - 1) li = fc.n_lights - 1;
-                        const float* lt = lm.lights + kLightF * li;
-                        float3 wi;
-                        float dist;
-                        float3 Li;  // radiance x cos_light / pdf (solid angle), i.e. I*cos/d^2
-                        if (lt[0] == 0.0f) {  // point / disk light
-                            const float3 lp = mk3(lt[1], lt[2], lt[3]);
-                            const float radius = lt[7];
-                            const float3 I = mk3(lt[8], lt[9], lt[10]);
-                            const float3 tl = sub3(lp, P);
-                            const float dl2 = dot3(tl, tl);
-                            if (radius > 0.0f) {
-                                const float3 wl = scl3(tl, 1.0f / sqrtf(dl2));
-                                float3 b1, b2;
-                                make_onb(wl, b1, b2);
-                                float dx, dy;
-                                concentric_disk(rng(key, dim0 + 1u), rng(key, dim0 + 2u), dx, dy);
-                                dx = dx * radius;
-                                dy = dy * radius;
-                                const float3 sp = mk3(lp.x + b1.x * dx + b2.x * dy, lp.y + b1.y * dx + b2.y * dy,
-                                                      lp.z + b1.z * dx + b2.z * dy);
-                                const float3 ts = sub3(sp, P);
-                                const float ds2 = dot3(ts, ts);
-                                dist = sqrtf(ds2);
-                                wi = scl3(ts, 1.0f / dist);
-                                const float cl = fabsf(dot3(wl, wi));
-                                Li = scl3(I, cl / ds2);
-                            } else {
-                                dist = sqrtf(dl2);
-                                wi = scl3(tl, 1.0f / dist);
-                                Li = scl3(I, 1.0f / dl2);
-                            }
-                        } else {  // sun: delta direction, irradiance
-                            wi = mk3(-lt[4], -lt[5], -lt[6]);
-                            dist = 3.402823466e+38f;
-                            Li = mk3(lt[8], lt[9], lt[10]);
-                        }
-                        const float cosN = dot3(N, wi);
-                        if (cosN > 0.0f) {
-                            float pdf;
-                            const float ps = spec_prob(m, dot3(N, wo));
-                            const float3 f = bsdf_eval(m, N, wo, wi, ps, pdf);
-                            const float k = cosN * (float)fc.n_lights;
-                            float3 c = mk3(T.x * f.x * k * Li.x, T.y * f.y * k * Li.y, T.z * f.z * k * Li.z);
-                            if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
-                            if (max3f(c) > 0.0f) {
-                                shadow = true;
-                                sh_o[p] = make_float4(Po.x, Po.y, Po.z, 0.0f);
-                                sh_d[p] = make_float4(wi.x, wi.y, wi.z, dist);
-                                sh_c[p] = make_float4(c.x, c.y, c.z, 0.0f);
-                            }
-                        }
-                    }
-                    // continue the path
-                    float3 wi, f;
-                    float pdf;
-                    if (bsdf_sample(m, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi,
-                                    f, pdf)) {
-                        const float cosL = dot3(N, wi);
-                        if (cosL > 0.0f) {
-                            const float k = cosL / pdf;
-                            T = mk3(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
-                            bool alive = max3f(T) > 0.0f;
-                            if (alive && bounce >= kRrStartBounce) {
-                                const float q = fminf(max3f(T), 1.0f);
-                                if (rng(key, dim0 + 6u) >= q) alive = false;
-                                else T = mk3(T.x / q, T.y / q, T.z / q);
-                            }
-                            if (alive) {
-                                cont = true;
-                                ray_o[p] = make_float4(Po.x, Po.y, Po.z, 0.0f);
-                                ray_d[p] = make_float4(wi.x, wi.y, wi.z, 3.402823466e+38f);
-                                thr[p] = make_float4(T.x, T.y, T.z, 0.0f);
-                            }
-                        }
-                    }
-                }
-                rad[p] = L;
-            }
-        }
-        wave_append(cont, p, q_out, cnt_out);
-        wave_append(shadow, p, sq, cnt_sh);
+// Traversal-count reduction (RR_FLAG_COUNT_TRAVERSAL only).
+__device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc, int slot, uint32_t nv,
+                                             uint32_t nt) {
+    unsigned long long a = nv, b = nt;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
     }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&tc[slot], a);
+        atomicAdd(&tc[slot + 1], b);
+    }
+}
+
+// K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
+__global__ __launch_bounds__(kBlock) void k_primary(FrameConsts fc, LightsMats lm, const BvhNode* __restrict__ nodes,
+                                                    const TriPack* __restrict__ tris, int np,
+                                                    float4* __restrict__ rad, PathQueue out,
+                                                    int32_t* __restrict__ cnt_out, ShadowQueue sq,
+                                                    int32_t* __restrict__ cnt_sh, int32_t* __restrict__ spill,
+                                                    unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    const int lane = threadIdx.x & 63;
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    const int stride = gridDim.x * kBlock;
+    TravStack st{&lds_stack[threadIdx.x], spill + gtid, stride, 0};
+    uint32_t nv = 0, nt = 0;
+    for (int i0 = gtid - lane; i0 < np; i0 += stride) {
+        const int p = i0 + lane;
+        ShadeOut so;
+        so.cont = so.shadow = false;
+        if (p < np) {
+            const int sl = p / fc.npix;
+            const int pix = p - sl * fc.npix;
+            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
+            float3 o, d;
+            float tmin, tmax;
+            camera_ray(fc, lm.filter, pix, key, o, d, tmin, tmax);
+            Hit h;
+            traverse<false>(nodes, tris, fc.n_tris, o, d, tmin, tmax, st, h, tc ? &nv : nullptr,
+                            tc ? &nt : nullptr);
+            float3 L = mk3(0.0f, 0.0f, 0.0f);
+            shade(fc, 0, lm, tris, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
+            rad[p] = make_float4(L.x, L.y, L.z, 0.0f);
+        }
+        emit(so, p, out, cnt_out, sq, cnt_sh);
+    }
+    if (tc) flush_counts(tc, 0, nv, nt);
+}
+
+// K-extend: closest hit + shade of bounce b >= 1 over the dense path queue.
+__global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, LightsMats lm,
+                                                   const BvhNode* __restrict__ nodes,
+                                                   const TriPack* __restrict__ tris,
+                                                   const int32_t* __restrict__ cnt_in, PathQueue in,
+                                                   float4* __restrict__ rad, PathQueue out,
+                                                   int32_t* __restrict__ cnt_out, ShadowQueue sq,
+                                                   int32_t* __restrict__ cnt_sh, int32_t* __restrict__ spill,
+                                                   unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    const int count = *cnt_in;
+    const int lane = threadIdx.x & 63;
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    const int stride = gridDim.x * kBlock;
+    TravStack st{&lds_stack[threadIdx.x], spill + gtid, stride, 0};
+    uint32_t nv = 0, nt = 0;
+    int pid = 0;
+    for (int i0 = gtid - lane; i0 < count; i0 += stride) {
+        const int i = i0 + lane;
+        ShadeOut so;
+        so.cont = so.shadow = false;
+        if (i < count) {
+            const float4 a = in.o[i], b = in.d[i], c = in.t[i];
+            pid = f2i(a.w);
+            const float3 o = xyz(a), d = xyz(b);
+            Hit h;
+            traverse<false>(nodes, tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, tc ? &nv : nullptr,
+                            tc ? &nt : nullptr);
+            const int sl = pid / fc.npix;
+            const int pix = pid - sl * fc.npix;
+            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
+            const float4 L4 = rad[pid];
+            float3 L = xyz(L4);
+            shade(fc, bounce, lm, tris, o, d, xyz(c), h, key, L, so);
+            rad[pid] = make_float4(L.x, L.y, L.z, 0.0f);
+        }
+        emit(so, pid, out, cnt_out, sq, cnt_sh);
+    }
+    if (tc) flush_counts(tc, 2, nv, nt);
+}
+
+// K10: shadow rays of one bounce; unoccluded -> radiance += contribution.
+__global__ __launch_bounds__(kBlock) void k_shadow(const BvhNode* __restrict__ nodes,
+                                                   const TriPack* __restrict__ tris, int n_tris,
+                                                   const int32_t* __restrict__ cnt_sh, ShadowQueue sq,
+                                                   float4* __restrict__ rad, int32_t* __restrict__ spill,
+                                                   unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    const int count = *cnt_sh;
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    const int stride = gridDim.x * kBlock;
+    TravStack st{&lds_stack[threadIdx.x], spill + gtid, stride, 0};
+    uint32_t nv = 0, nt = 0;
+    for (int i = gtid; i < count; i += stride) {
+        const float4 a = sq.o[i], b = sq.d[i];
+        Hit h;
+        if (!traverse<true>(nodes, tris, n_tris, xyz(a), xyz(b), 0.0f, b.w, st, h, tc ? &nv : nullptr,
+                            tc ? &nt : nullptr)) {
+            const int pid = f2i(a.w);
+            const float4 c = sq.c[i];
+            float4 L = rad[pid];
+            L.x = L.x + c.x;
+            L.y = L.y + c.y;
+            L.z = L.z + c.z;
+            rad[pid] = L;
+        }
+    }
+    if (tc) flush_counts(tc, 4, nv, nt);
 }
 
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
@@ -359,18 +426,19 @@ int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2); }
 void DevPaths::ensure_paths(size_t n) {
     if (grid_blocks == 0) grid_blocks = device_cu_count() * 8;
     if (n > cap) {
-        for (DevBuf<float4>* b : {&ray_o, &ray_d, &hit, &thr, &rad, &sh_o, &sh_d, &sh_c}) b->ensure(n);
-        q[0].ensure(n);
-        q[1].ensure(n);
-        sq.ensure(n);
+        for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
+                                  &sh_c})
+            b->ensure(n);
         cap = n;
     }
     spill.ensure((size_t)kSpillStack * grid_blocks * kBlock);
 }
 
 void DevPaths::release() {
-    for (DevBuf<float4>* b : {&ray_o, &ray_d, &hit, &thr, &rad, &sh_o, &sh_d, &sh_c, &film}) b->release();
-    q[0].release(); q[1].release(); sq.release(); counters.release(); spill.release();
+    for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
+                              &sh_c, &film})
+        b->release();
+    counters.release(); spill.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     trav_counts.release();
     prof.release();
@@ -390,10 +458,12 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     const int grid = p.grid_blocks;
     unsigned long long* tc = nullptr;
     if (p.count_traversal) {
-        p.trav_counts.ensure(4);
-        RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 4 * sizeof(unsigned long long), st));
+        p.trav_counts.ensure(6);
+        RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 6 * sizeof(unsigned long long), st));
         tc = p.trav_counts.ptr;
     }
+    PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
+    ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     KernelProfiler& pr = p.prof;
     for (int c = 0; c < n_chunks; ++c) {
         FrameConsts fc = base;
@@ -401,33 +471,27 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         fc.spp_chunk = base.spp_chunk;
         if (fc.first_sample + fc.spp_chunk > base.spp_total) fc.spp_chunk = base.spp_total - fc.first_sample;
         const int np = npix * fc.spp_chunk;
-        int32_t* ext = p.counters.ptr + (size_t)cpc * c;        // ext[b]: queue size of bounce b (b>=1)
-        int32_t* shc = ext + (base.max_bounces + 2);            // shc[b]: shadow rays of bounce b
+        int32_t* ext = p.counters.ptr + (size_t)cpc * c;  // ext[b]: paths entering bounce b (b >= 1)
+        int32_t* shc = ext + (base.max_bounces + 2);      // shc[b]: shadow rays of bounce b
         const int g = (int)std::min<long>((np + kBlock - 1) / kBlock, grid);
-        pr.begin(st, 1);
-        k_raygen<<<g, kBlock, 0, st>>>(fc, p.filter_table.ptr, p.ray_o.ptr, p.ray_d.ptr, p.thr.ptr,
-                                       p.rad.ptr, np);
+        pr.begin(st, RR_K_PRIMARY);
+        k_primary<<<g, kBlock, 0, st>>>(fc, lm, s.nodes.ptr, s.tris.ptr, np, p.rad.ptr, pq[1], ext + 1, sq, shc,
+                                        p.spill.ptr, tc);
         pr.end(st);
         for (int b = 0; b <= base.max_bounces; ++b) {
-            const int32_t* qin = b == 0 ? nullptr : p.q[b & 1].ptr;
-            const int32_t* cin = b == 0 ? nullptr : ext + b;
-            pr.begin(st, 2);
-            k_trace<false><<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, qin, cin, np, p.ray_o.ptr,
-                                                 p.ray_d.ptr, p.hit.ptr, nullptr, nullptr, p.spill.ptr, tc);
-            pr.end(st);
-            pr.begin(st, 3);
-            k_shade<<<g, kBlock, 0, st>>>(fc, b, lm, s.tris.ptr, qin, cin, np, p.q[(b + 1) & 1].ptr, ext + b + 1,
-                                          p.sq.ptr, shc + b, p.ray_o.ptr, p.ray_d.ptr, p.hit.ptr, p.thr.ptr,
-                                          p.rad.ptr, p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr);
-            pr.end(st);
-            pr.begin(st, 4);
-            k_trace<true><<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, p.sq.ptr, shc + b, 0,
-                                                p.sh_o.ptr, p.sh_d.ptr, nullptr, p.sh_c.ptr, p.rad.ptr,
-                                                p.spill.ptr, tc);
+            if (b > 0) {
+                pr.begin(st, RR_K_EXTEND);
+                k_extend<<<g, kBlock, 0, st>>>(fc, b, lm, s.nodes.ptr, s.tris.ptr, ext + b, pq[b & 1], p.rad.ptr,
+                                               pq[(b + 1) & 1], ext + b + 1, sq, shc + b, p.spill.ptr, tc);
+                pr.end(st);
+            }
+            pr.begin(st, RR_K_SHADOW);
+            k_shadow<<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, shc + b, sq, p.rad.ptr,
+                                           p.spill.ptr, tc);
             pr.end(st);
         }
         const int ga = (int)std::min<long>((npix + kBlock - 1) / kBlock, grid);
-        pr.begin(st, 5);
+        pr.begin(st, RR_K_ACCUM);
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, p.rad.ptr, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);

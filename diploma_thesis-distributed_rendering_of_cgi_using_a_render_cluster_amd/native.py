@@ -46,13 +46,13 @@ class FrameStats(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
                 ("chunks", ctypes.c_int32), ("camera_rays", ctypes.c_uint64),
                 ("extension_rays", ctypes.c_uint64), ("shadow_rays", ctypes.c_uint64),
+                ("primary_continued", ctypes.c_uint64), ("primary_shadow", ctypes.c_uint64),
                 ("anim_ms", ctypes.c_double), ("build_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
                 ("readback_ms", ctypes.c_double), ("encode_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("bvh_rebuilt", ctypes.c_int32), ("n_triangles", ctypes.c_int32),
                 ("output_bytes", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_int32 * 8),
-                ("closest_nodes", ctypes.c_uint64), ("closest_tris", ctypes.c_uint64),
-                ("shadow_nodes", ctypes.c_uint64), ("shadow_tris", ctypes.c_uint64)]
+                ("trav_nodes", ctypes.c_uint64 * 3), ("trav_tris", ctypes.c_uint64 * 3)]
 
     def as_dict(self) -> dict:
         out = {}
@@ -63,7 +63,7 @@ class FrameStats(ctypes.Structure):
 
 
 RR_FLAG_PROFILE_KERNELS, RR_FLAG_COUNT_TRAVERSAL = 1, 2
-KERNEL_CLASSES = ["build", "raygen", "closest", "shade", "shadow", "accumulate"]
+KERNEL_CLASSES = ["build", "primary", "extend", "shadow", "accumulate"]
 
 
 # Every symbol include/rr.h declares (checked by tests/test_abi.py).

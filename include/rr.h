@@ -71,11 +71,10 @@ typedef struct rr_render_params {
 
 /* Kernel classes of rr_frame_stats.kernel_ms / kernel_launches. */
 #define RR_K_BUILD 0     /* world transform + Morton + radix sort + Karras + refit */
-#define RR_K_RAYGEN 1    /* camera rays */
-#define RR_K_CLOSEST 2   /* closest-hit traversal (camera + extension rays) */
-#define RR_K_SHADE 3     /* shading + NEE setup + queue compaction */
-#define RR_K_SHADOW 4    /* any-hit traversal of shadow rays */
-#define RR_K_ACCUM 5     /* film accumulate + tonemap */
+#define RR_K_PRIMARY 1   /* bounce 0: raygen + closest hit + shade + queue compaction */
+#define RR_K_EXTEND 2    /* bounces >= 1: closest hit + shade + queue compaction */
+#define RR_K_SHADOW 3    /* any-hit traversal of shadow rays */
+#define RR_K_ACCUM 4     /* film accumulate + tonemap */
 #define RR_K_CLASSES 8
 
 /* The five timestamps the reference recovers from Blender's stdout
@@ -98,6 +97,8 @@ typedef struct rr_frame_stats {
     uint64_t camera_rays;    /* primary rays traced */
     uint64_t extension_rays; /* bounce rays traced (closest hit) */
     uint64_t shadow_rays;    /* NEE shadow rays traced (any hit) */
+    uint64_t primary_continued; /* camera paths that continue past bounce 0 */
+    uint64_t primary_shadow;    /* shadow rays spawned at bounce 0 */
     double anim_ms;          /* host animation eval + upload */
     double build_ms;         /* device: world transform + LBVH build (0 if cached) */
     double trace_ms;         /* device: wavefront kernels (raygen .. accumulate) */
@@ -110,8 +111,9 @@ typedef struct rr_frame_stats {
     /* RR_FLAG_PROFILE_KERNELS: summed device time and launch count per class */
     double kernel_ms[RR_K_CLASSES];
     int32_t kernel_launches[RR_K_CLASSES];
-    /* RR_FLAG_COUNT_TRAVERSAL: totals over the frame (closest / any hit) */
-    uint64_t closest_nodes, closest_tris, shadow_nodes, shadow_tris;
+    /* RR_FLAG_COUNT_TRAVERSAL: BVH nodes visited / triangles tested over the
+     * frame, per traversal kernel: [0] primary, [1] extend, [2] shadow */
+    uint64_t trav_nodes[3], trav_tris[3];
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */
