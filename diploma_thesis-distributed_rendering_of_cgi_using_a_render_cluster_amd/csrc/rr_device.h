@@ -202,28 +202,43 @@ RR_HD void closest_tri(const TriPack& tp, int idx, float3 o, float3 d, float tmi
 
 // Traversal stack: kLdsStack entries in LDS ([entry][thread] -> conflict-free
 // ds_read_b32 across a wave), deeper entries in a per-thread HBM spill area.
+// The LDS pointer carries its address space explicitly so push/pop compile to
+// ds_write/ds_read (a generic pointer would become flat_* accesses).
+typedef __attribute__((address_space(3))) int lds_int;
 struct TravStack {
-    int* lds;       // &lds_base[threadIdx.x], stride kBlock
+    lds_int* lds;   // &lds_base[threadIdx.x], stride kBlock
     int* spill;     // &spill_base[global thread], stride spill_stride
     int spill_stride;
     int sp;
     RR_D void push(int x) {
-        if (sp < kLdsStack) lds[sp * kBlock] = x;
-        else spill[(sp - kLdsStack) * spill_stride] = x;
+        if (sp < kLdsStack) {
+            lds[sp * kBlock] = x;
+        } else if (sp < kLdsStack + kSpillStack) {
+            spill[(sp - kLdsStack) * spill_stride] = x;
+        }
         ++sp;
     }
     RR_D int pop() {
         --sp;
-        return sp < kLdsStack ? lds[sp * kBlock] : spill[(sp - kLdsStack) * spill_stride];
+        if (sp < kLdsStack) return lds[sp * kBlock];
+        return spill[(sp - kLdsStack) * spill_stride];
     }
+};
+
+RR_D lds_int* lds_slot(int* shared_elem) {
+    return (lds_int*)(shared_elem);
+}
+
+// Traversal counters for RR_FLAG_COUNT_TRAVERSAL builds (kCount = true only).
+struct TravCount {
+    uint32_t nodes = 0, tris = 0;
 };
 
 // Closest hit over the LBVH. Near child first (left on ties); leaf children are
 // intersected as soon as their box passes.
-template <bool kAnyHit, typename Stack>
+template <bool kAnyHit, bool kCount = false, typename Stack>
 RR_D bool traverse(const BvhNode* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
-                   float3 o, float3 d, float tmin, float tmax, Stack& st, Hit& h,
-                   uint32_t* nodes_visited = nullptr, uint32_t* tris_tested = nullptr) {
+                   float3 o, float3 d, float tmin, float tmax, Stack& st, Hit& h, TravCount& cnt) {
     h.t = tmax;
     h.u = h.v = 0.0f;
     h.idx = -1;
@@ -234,19 +249,19 @@ RR_D bool traverse(const BvhNode* __restrict__ nodes, const TriPack* __restrict_
     st.sp = 0;
     for (;;) {
         const BvhNode nd = nodes[node];
-        if (nodes_visited) ++*nodes_visited;
+        if (kCount) ++cnt.nodes;
         float tl, tr;
         bool hl = slab(o, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
         bool hr = slab(o, invd, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
         const int cl = nd.d.x, cr = nd.d.y;
         if (hl && cl < 0) {
-            if (tris_tested) ++*tris_tested;
+            if (kCount) ++cnt.tris;
             closest_tri(tris[~cl], ~cl, o, d, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
             hl = false;
         }
         if (hr && cr < 0) {
-            if (tris_tested) ++*tris_tested;
+            if (kCount) ++cnt.tris;
             closest_tri(tris[~cr], ~cr, o, d, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
             hr = false;

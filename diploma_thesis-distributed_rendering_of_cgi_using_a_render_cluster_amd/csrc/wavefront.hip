@@ -27,6 +27,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "device.hpp"
 
 namespace rr {
@@ -255,7 +257,8 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
 }
 
 // K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
-__global__ __launch_bounds__(kBlock) void k_primary(FrameConsts fc, LightsMats lm, const BvhNode* __restrict__ nodes,
+template <bool kCount, int kMinWaves = 1>
+__global__ __launch_bounds__(kBlock, kMinWaves) void k_primary(FrameConsts fc, LightsMats lm, const BvhNode* __restrict__ nodes,
                                                     const TriPack* __restrict__ tris, int np,
                                                     float4* __restrict__ rad, PathQueue out,
                                                     int32_t* __restrict__ cnt_out, ShadowQueue sq,
@@ -265,8 +268,8 @@ __global__ __launch_bounds__(kBlock) void k_primary(FrameConsts fc, LightsMats l
     const int lane = threadIdx.x & 63;
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{&lds_stack[threadIdx.x], spill + gtid, stride, 0};
-    uint32_t nv = 0, nt = 0;
+    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
+    TravCount cnt;
     for (int i0 = gtid - lane; i0 < np; i0 += stride) {
         const int p = i0 + lane;
         ShadeOut so;
@@ -279,18 +282,18 @@ __global__ __launch_bounds__(kBlock) void k_primary(FrameConsts fc, LightsMats l
             float tmin, tmax;
             camera_ray(fc, lm.filter, pix, key, o, d, tmin, tmax);
             Hit h;
-            traverse<false>(nodes, tris, fc.n_tris, o, d, tmin, tmax, st, h, tc ? &nv : nullptr,
-                            tc ? &nt : nullptr);
+            traverse<false, kCount>(nodes, tris, fc.n_tris, o, d, tmin, tmax, st, h, cnt);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
             shade(fc, 0, lm, tris, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
             rad[p] = make_float4(L.x, L.y, L.z, 0.0f);
         }
         emit(so, p, out, cnt_out, sq, cnt_sh);
     }
-    if (tc) flush_counts(tc, 0, nv, nt);
+    if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
 }
 
 // K-extend: closest hit + shade of bounce b >= 1 over the dense path queue.
+template <bool kCount>
 __global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, LightsMats lm,
                                                    const BvhNode* __restrict__ nodes,
                                                    const TriPack* __restrict__ tris,
@@ -304,8 +307,8 @@ __global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, L
     const int lane = threadIdx.x & 63;
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{&lds_stack[threadIdx.x], spill + gtid, stride, 0};
-    uint32_t nv = 0, nt = 0;
+    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
+    TravCount cnt;
     int pid = 0;
     for (int i0 = gtid - lane; i0 < count; i0 += stride) {
         const int i = i0 + lane;
@@ -316,8 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, L
             pid = f2i(a.w);
             const float3 o = xyz(a), d = xyz(b);
             Hit h;
-            traverse<false>(nodes, tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, tc ? &nv : nullptr,
-                            tc ? &nt : nullptr);
+            traverse<false, kCount>(nodes, tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
             const int sl = pid / fc.npix;
             const int pix = pid - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
@@ -328,10 +330,11 @@ __global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, L
         }
         emit(so, pid, out, cnt_out, sq, cnt_sh);
     }
-    if (tc) flush_counts(tc, 2, nv, nt);
+    if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
 }
 
 // K10: shadow rays of one bounce; unoccluded -> radiance += contribution.
+template <bool kCount>
 __global__ __launch_bounds__(kBlock) void k_shadow(const BvhNode* __restrict__ nodes,
                                                    const TriPack* __restrict__ tris, int n_tris,
                                                    const int32_t* __restrict__ cnt_sh, ShadowQueue sq,
@@ -341,13 +344,12 @@ __global__ __launch_bounds__(kBlock) void k_shadow(const BvhNode* __restrict__ n
     const int count = *cnt_sh;
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{&lds_stack[threadIdx.x], spill + gtid, stride, 0};
-    uint32_t nv = 0, nt = 0;
+    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
+    TravCount cnt;
     for (int i = gtid; i < count; i += stride) {
         const float4 a = sq.o[i], b = sq.d[i];
         Hit h;
-        if (!traverse<true>(nodes, tris, n_tris, xyz(a), xyz(b), 0.0f, b.w, st, h, tc ? &nv : nullptr,
-                            tc ? &nt : nullptr)) {
+        if (!traverse<true, kCount>(nodes, tris, n_tris, xyz(a), xyz(b), 0.0f, b.w, st, h, cnt)) {
             const int pid = f2i(a.w);
             const float4 c = sq.c[i];
             float4 L = rad[pid];
@@ -357,7 +359,7 @@ __global__ __launch_bounds__(kBlock) void k_shadow(const BvhNode* __restrict__ n
             rad[pid] = L;
         }
     }
-    if (tc) flush_counts(tc, 4, nv, nt);
+    if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
 }
 
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
@@ -396,15 +398,16 @@ __global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* 
     __shared__ int lds_stack[kLdsStack * kBlock];
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int nthreads = gridDim.x * kBlock;
-    TravStack st{&lds_stack[threadIdx.x], spill + gtid, nthreads, 0};
+    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, nthreads, 0};
+    TravCount cnt;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
         Hit h;
-        traverse<false>(nodes, tris, n_tris, xyz(o), xyz(d), o.w, d.w, st, h);
+        traverse<false>(nodes, tris, n_tris, xyz(o), xyz(d), o.w, d.w, st, h, cnt);
         hits[i] = make_float4(h.t, h.u, h.v, 0.0f);
         prims[i] = h.orig;
         Hit h2;
-        occ[i] = traverse<true>(nodes, tris, n_tris, xyz(o), xyz(d), o.w, d.w, st, h2) ? 1 : 0;
+        occ[i] = traverse<true>(nodes, tris, n_tris, xyz(o), xyz(d), o.w, d.w, st, h2, cnt) ? 1 : 0;
     }
 }
 
@@ -422,6 +425,35 @@ int device_cu_count() {
 }
 
 int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2); }
+
+namespace {
+// Persistent grid = resident blocks: CUs x blocks per CU the kernel's register
+// and LDS budget admits (a grid-stride loop over more blocks than fit would
+// only queue the surplus behind the first wave of blocks).
+template <typename K>
+int resident_grid(K kernel) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 4;
+    return device_cu_count() * per_cu;
+}
+struct Grids {
+    int primary, primary5, extend, shadow, accum;
+    Grids()
+        : primary(resident_grid(k_primary<false>)), primary5(resident_grid(k_primary<false, 5>)),
+          extend(resident_grid(k_extend<false>)),
+          shadow(resident_grid(k_shadow<false>)),
+          accum(resident_grid(k_accumulate)) {}
+};
+const Grids& grids() {
+    static Grids g;
+    return g;
+}
+inline int clamp_grid(long work, int resident) {
+    const long g = (work + kBlock - 1) / kBlock;
+    return (int)std::max<long>(1, std::min<long>(g, resident));
+}
+}  // namespace
 
 void DevPaths::ensure_paths(size_t n) {
     if (grid_blocks == 0) grid_blocks = device_cu_count() * 8;
@@ -455,7 +487,6 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     p.counters.ensure((size_t)cpc * n_chunks);
     RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
     LightsMats lm{p.lights.ptr, p.materials.ptr, p.filter_table.ptr, p.srgb_lut.ptr};
-    const int grid = p.grid_blocks;
     unsigned long long* tc = nullptr;
     if (p.count_traversal) {
         p.trav_counts.ensure(6);
@@ -465,6 +496,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     KernelProfiler& pr = p.prof;
+    const Grids& G = grids();
     for (int c = 0; c < n_chunks; ++c) {
         FrameConsts fc = base;
         fc.first_sample = c * base.spp_chunk;
@@ -473,24 +505,27 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         const int np = npix * fc.spp_chunk;
         int32_t* ext = p.counters.ptr + (size_t)cpc * c;  // ext[b]: paths entering bounce b (b >= 1)
         int32_t* shc = ext + (base.max_bounces + 2);      // shc[b]: shadow rays of bounce b
-        const int g = (int)std::min<long>((np + kBlock - 1) / kBlock, grid);
         pr.begin(st, RR_K_PRIMARY);
-        k_primary<<<g, kBlock, 0, st>>>(fc, lm, s.nodes.ptr, s.tris.ptr, np, p.rad.ptr, pq[1], ext + 1, sq, shc,
-                                        p.spill.ptr, tc);
+        // RR_TUNE_PRIMARY_WAVES=5: register-capped variant (A/B tuning knob)
+        static const bool prim5 = getenv("RR_TUNE_PRIMARY_WAVES") && atoi(getenv("RR_TUNE_PRIMARY_WAVES")) == 5;
+        auto kprim = tc ? k_primary<true> : (prim5 ? k_primary<false, 5> : k_primary<false>);
+        kprim<<<clamp_grid(np, prim5 ? G.primary5 : G.primary), kBlock, 0, st>>>(fc, lm, s.nodes.ptr, s.tris.ptr, np, p.rad.ptr,
+                                                                 pq[1], ext + 1, sq, shc, p.spill.ptr, tc);
         pr.end(st);
         for (int b = 0; b <= base.max_bounces; ++b) {
             if (b > 0) {
                 pr.begin(st, RR_K_EXTEND);
-                k_extend<<<g, kBlock, 0, st>>>(fc, b, lm, s.nodes.ptr, s.tris.ptr, ext + b, pq[b & 1], p.rad.ptr,
-                                               pq[(b + 1) & 1], ext + b + 1, sq, shc + b, p.spill.ptr, tc);
+                (tc ? k_extend<true> : k_extend<false>)<<<clamp_grid(np, G.extend), kBlock, 0, st>>>(fc, b, lm, s.nodes.ptr, s.tris.ptr, ext + b,
+                                                                       pq[b & 1], p.rad.ptr, pq[(b + 1) & 1],
+                                                                       ext + b + 1, sq, shc + b, p.spill.ptr, tc);
                 pr.end(st);
             }
             pr.begin(st, RR_K_SHADOW);
-            k_shadow<<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, shc + b, sq, p.rad.ptr,
-                                           p.spill.ptr, tc);
+            (tc ? k_shadow<true> : k_shadow<false>)<<<clamp_grid(np, G.shadow), kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, shc + b, sq,
+                                                                   p.rad.ptr, p.spill.ptr, tc);
             pr.end(st);
         }
-        const int ga = (int)std::min<long>((npix + kBlock - 1) / kBlock, grid);
+        const int ga = clamp_grid(npix, G.accum);
         pr.begin(st, RR_K_ACCUM);
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, p.rad.ptr, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
