@@ -165,6 +165,9 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
 void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, float4* d_hits,
                         int32_t* d_prims, uint8_t* d_occ, hipStream_t st);
 
+// Device JPEG forward transform (jpeg.hip); tab = dct | qinv luma | qinv chroma.
+void jpeg_fdct_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, int16_t* d_out, hipStream_t st);
+
 int counters_per_chunk(int max_bounces);
 int device_cu_count();
 

@@ -18,6 +18,12 @@
 
 namespace rr {
 
+int encoder_threads() {
+    unsigned n = std::thread::hardware_concurrency();
+    if (n == 0) n = 4;
+    return (int)std::min(n, 16u);
+}
+
 namespace {
 
 // ---------------------------------------------------------------- JPEG ----
@@ -142,7 +148,7 @@ const Dct& dct() {
 }
 
 // Forward DCT + quantisation of one 8x8 block (level-shifted samples).
-void fdct_quant(const float in[64], const float qinv[64], int16_t out[64]) {
+void fdct_quant(const float in[64], const float qinv[64], int16_t* out) {
     const Dct& D = dct();
     float tmp[64];
     for (int y = 0; y < 8; ++y)
@@ -166,7 +172,7 @@ inline int bitlen(int v) {
     return n;
 }
 
-void encode_block(BitWriter& bw, const int16_t blk[64], int& pred, const HuffTable& dc, const HuffTable& ac) {
+void encode_block(BitWriter& bw, const int16_t* blk, int& pred, const HuffTable& dc, const HuffTable& ac) {
     const int diff = blk[0] - pred;
     pred = blk[0];
     int n = bitlen(diff);
@@ -207,15 +213,13 @@ void write_dht(std::vector<uint8_t>& o, int cls, int id, const uint8_t bits[16],
     o.insert(o.end(), vals, vals + n);
 }
 
-// Encode MCU row `my` (16 pixel rows) into its own buffer.
-void encode_mcu_row(const uint8_t* rgba, int W, int H, int my, const float qy[64], const float qc[64],
-                    std::vector<uint8_t>& out) {
-    const Tables& T = tables();
-    BitWriter bw(out);
-    int pred[3] = {0, 0, 0};
+// Forward DCT + quantisation of MCU row `my` (16 pixel rows) on the host:
+// coefficients [mcux][6][64] (blocks Y00 Y01 Y10 Y11 Cb Cr, natural order).
+// jpeg.hip computes the same values on the device with the same float ops.
+void mcu_row_coeffs(const uint8_t* rgba, int W, int H, int my, const float qy[64], const float qc[64],
+                    int16_t* out) {
     const int mcux = (W + 15) / 16;
     float Y[4][64], Cb[64], Cr[64];
-    int16_t q[64];
     for (int mx = 0; mx < mcux; ++mx) {
         float cbs[16][16], crs[16][16];
         for (int yy = 0; yy < 16; ++yy) {
@@ -237,52 +241,28 @@ void encode_mcu_row(const uint8_t* rgba, int W, int H, int my, const float qy[64
                 Cr[8 * yy + xx] = 0.25f * (crs[2 * yy][2 * xx] + crs[2 * yy][2 * xx + 1] + crs[2 * yy + 1][2 * xx] +
                                            crs[2 * yy + 1][2 * xx + 1]);
             }
-        for (int k = 0; k < 4; ++k) {
-            fdct_quant(Y[k], qy, q);
-            encode_block(bw, q, pred[0], T.dc[0], T.ac[0]);
-        }
-        fdct_quant(Cb, qc, q);
-        encode_block(bw, q, pred[1], T.dc[1], T.ac[1]);
-        fdct_quant(Cr, qc, q);
-        encode_block(bw, q, pred[2], T.dc[1], T.ac[1]);
+        int16_t* o = out + (size_t)mx * 6 * 64;
+        for (int k = 0; k < 4; ++k) fdct_quant(Y[k], qy, o + 64 * k);
+        fdct_quant(Cb, qc, o + 64 * 4);
+        fdct_quant(Cr, qc, o + 64 * 5);
+    }
+}
+
+// Huffman-code one MCU row (one restart interval) from its coefficients.
+void entropy_mcu_row(const int16_t* coeffs, int mcux, std::vector<uint8_t>& out) {
+    const Tables& T = tables();
+    BitWriter bw(out);
+    int pred[3] = {0, 0, 0};
+    for (int mx = 0; mx < mcux; ++mx) {
+        const int16_t* o = coeffs + (size_t)mx * 6 * 64;
+        for (int k = 0; k < 4; ++k) encode_block(bw, o + 64 * k, pred[0], T.dc[0], T.ac[0]);
+        encode_block(bw, o + 64 * 4, pred[1], T.dc[1], T.ac[1]);
+        encode_block(bw, o + 64 * 5, pred[2], T.dc[1], T.ac[1]);
     }
     bw.flush();
 }
 
-// --------------------------------------------------------------- PNG ------
-void png_chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* data, size_t n) {
-    const uint32_t len = (uint32_t)n;
-    o.push_back((uint8_t)(len >> 24)); o.push_back((uint8_t)(len >> 16));
-    o.push_back((uint8_t)(len >> 8)); o.push_back((uint8_t)len);
-    const size_t start = o.size();
-    o.insert(o.end(), type, type + 4);
-    if (n) o.insert(o.end(), data, data + n);
-    const uint32_t crc = (uint32_t)crc32(0L, o.data() + start, (uInt)(o.size() - start));
-    o.push_back((uint8_t)(crc >> 24)); o.push_back((uint8_t)(crc >> 16));
-    o.push_back((uint8_t)(crc >> 8)); o.push_back((uint8_t)crc);
-}
-
-}  // namespace
-
-int encoder_threads() {
-    unsigned n = std::thread::hardware_concurrency();
-    if (n == 0) n = 4;
-    return (int)std::min(n, 16u);
-}
-
-bool encode_jpeg(const uint8_t* rgba, int W, int H, int quality, std::vector<uint8_t>& out, int threads) {
-    if (W <= 0 || H <= 0 || W > 65535 || H > 65535) return false;
-    uint8_t ql[64], qc[64];
-    quant_table(kStdLuma, quality, ql);
-    quant_table(kStdChroma, quality, qc);
-    // quantisation folded with the DCT scale: coefficient / q
-    float qly[64], qcy[64];
-    for (int i = 0; i < 64; ++i) {
-        qly[i] = 1.0f / (float)ql[i];
-        qcy[i] = 1.0f / (float)qc[i];
-    }
-    out.clear();
-    out.reserve((size_t)W * H / 2);
+void jpeg_header(int W, int H, const uint8_t* ql, const uint8_t* qc, std::vector<uint8_t>& out) {
     // SOI + APP0 JFIF
     const uint8_t soi_app0[] = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0x00,
                                 0x01, 0x01, 0x00, 0x00, 0x01, 0x00, 0x01, 0x00, 0x00};
@@ -308,30 +288,34 @@ bool encode_jpeg(const uint8_t* rgba, int W, int H, int quality, std::vector<uin
     write_dht(out, 1, 0, kAcLumBits, kAcLumVal);
     write_dht(out, 0, 1, kDcChrBits, kDcChrVal);
     write_dht(out, 1, 1, kAcChrBits, kAcChrVal);
-    const int mcux = (W + 15) / 16, mcuy = (H + 15) / 16;
     // DRI: one restart interval per MCU row
     out.push_back(0xFF); out.push_back(0xDD);
     put16(out, 4);
-    put16(out, mcux);
+    put16(out, (W + 15) / 16);
     // SOS
     const uint8_t sos[] = {0xFF, 0xDA, 0x00, 0x0C, 0x03, 1, 0x00, 2, 0x11, 3, 0x11, 0x00, 0x3F, 0x00};
     out.insert(out.end(), sos, sos + sizeof sos);
-    std::vector<std::vector<uint8_t>> rows((size_t)mcuy);
+}
+
+// Run fn(my) for every MCU row on `threads` host threads.
+template <typename Fn>
+void for_rows(int mcuy, int threads, Fn fn) {
     if (threads <= 0) threads = encoder_threads();
     threads = std::max(1, std::min(threads, mcuy));
-    auto work = [&](int tid) {
-        for (int my = tid; my < mcuy; my += threads) {
-            rows[my].reserve((size_t)mcux * 256);
-            encode_mcu_row(rgba, W, H, my, qly, qcy, rows[my]);
-        }
-    };
     if (threads == 1) {
-        work(0);
-    } else {
-        std::vector<std::thread> pool;
-        for (int t = 0; t < threads; ++t) pool.emplace_back(work, t);
-        for (auto& th : pool) th.join();
+        for (int my = 0; my < mcuy; ++my) fn(my);
+        return;
     }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t)
+        pool.emplace_back([&, t] {
+            for (int my = t; my < mcuy; my += threads) fn(my);
+        });
+    for (auto& th : pool) th.join();
+}
+
+void join_rows(std::vector<std::vector<uint8_t>>& rows, std::vector<uint8_t>& out) {
+    const int mcuy = (int)rows.size();
     for (int my = 0; my < mcuy; ++my) {
         out.insert(out.end(), rows[my].begin(), rows[my].end());
         if (my + 1 < mcuy) {
@@ -340,6 +324,69 @@ bool encode_jpeg(const uint8_t* rgba, int W, int H, int quality, std::vector<uin
         }
     }
     out.push_back(0xFF); out.push_back(0xD9);
+}
+
+// --------------------------------------------------------------- PNG ------
+void png_chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* data, size_t n) {
+    const uint32_t len = (uint32_t)n;
+    o.push_back((uint8_t)(len >> 24)); o.push_back((uint8_t)(len >> 16));
+    o.push_back((uint8_t)(len >> 8)); o.push_back((uint8_t)len);
+    const size_t start = o.size();
+    o.insert(o.end(), type, type + 4);
+    if (n) o.insert(o.end(), data, data + n);
+    const uint32_t crc = (uint32_t)crc32(0L, o.data() + start, (uInt)(o.size() - start));
+    o.push_back((uint8_t)(crc >> 24)); o.push_back((uint8_t)(crc >> 16));
+    o.push_back((uint8_t)(crc >> 8)); o.push_back((uint8_t)crc);
+}
+
+}  // namespace
+
+void jpeg_tables(int quality, JpegTables& t) {
+    quant_table(kStdLuma, quality, t.ql);
+    quant_table(kStdChroma, quality, t.qc);
+    for (int i = 0; i < 64; ++i) {  // quantisation folded as a multiply by 1/q
+        t.dct[i] = dct().c[i / 8][i % 8];
+        t.qinv_l[i] = 1.0f / (float)t.ql[i];
+        t.qinv_c[i] = 1.0f / (float)t.qc[i];
+    }
+}
+
+size_t jpeg_coeff_count(int W, int H) { return (size_t)((W + 15) / 16) * ((H + 15) / 16) * 6 * 64; }
+
+bool encode_jpeg(const uint8_t* rgba, int W, int H, int quality, std::vector<uint8_t>& out, int threads) {
+    if (W <= 0 || H <= 0 || W > 65535 || H > 65535) return false;
+    JpegTables t;
+    jpeg_tables(quality, t);
+    const int mcux = (W + 15) / 16, mcuy = (H + 15) / 16;
+    out.clear();
+    out.reserve((size_t)W * H / 2);
+    jpeg_header(W, H, t.ql, t.qc, out);
+    std::vector<std::vector<uint8_t>> rows((size_t)mcuy);
+    for_rows(mcuy, threads, [&](int my) {
+        std::vector<int16_t> c((size_t)mcux * 6 * 64);
+        mcu_row_coeffs(rgba, W, H, my, t.qinv_l, t.qinv_c, c.data());
+        rows[my].reserve((size_t)mcux * 256);
+        entropy_mcu_row(c.data(), mcux, rows[my]);
+    });
+    join_rows(rows, out);
+    return true;
+}
+
+bool encode_jpeg_coeffs(const int16_t* coeffs, int W, int H, int quality, std::vector<uint8_t>& out,
+                        int threads) {
+    if (W <= 0 || H <= 0 || W > 65535 || H > 65535) return false;
+    JpegTables t;
+    jpeg_tables(quality, t);
+    const int mcux = (W + 15) / 16, mcuy = (H + 15) / 16;
+    out.clear();
+    out.reserve((size_t)W * H / 2);
+    jpeg_header(W, H, t.ql, t.qc, out);
+    std::vector<std::vector<uint8_t>> rows((size_t)mcuy);
+    for_rows(mcuy, threads, [&](int my) {
+        rows[my].reserve((size_t)mcux * 256);
+        entropy_mcu_row(coeffs + (size_t)my * mcux * 6 * 64, mcux, rows[my]);
+    });
+    join_rows(rows, out);
     return true;
 }
 

@@ -72,6 +72,11 @@ struct rr_ctx {
     hipEvent_t ev[4] = {};
     DevPaths paths;
     PinnedBuf host_rgba;
+    // device JPEG transform (jpeg.hip): tables for the last quality, coefficients
+    DevBuf<float> jpeg_tab;
+    int jpeg_tab_quality = -1;
+    DevBuf<int16_t> jpeg_coeffs;
+    PinnedBuf host_coeffs;
     std::vector<float> filter_cache;
     float filter_width_cached = -1.f;
     bool srgb_uploaded = false;
@@ -216,7 +221,10 @@ struct FrameRun {
 };
 
 // Run the device part of one frame; leaves the 8-bit image in c->host_rgba.
-FrameRun run_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, float* film_out) {
+// jpeg_quality > 0: also run the device JPEG transform and read back its
+// coefficients (c->host_coeffs); want_rgba: read back the 8-bit image.
+FrameRun run_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, float* film_out, int jpeg_quality = 0,
+                   bool want_rgba = true) {
     set_device(c);
     FrameRun r{};
     r.W = fs.W;
@@ -234,8 +242,29 @@ FrameRun run_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, float* film_out
     render_frame_device(s->dev, c->paths, k, r.chunks, st);
     RR_HIP(hipEventRecord(c->ev[2], st));
     const size_t npix = (size_t)fs.W * fs.H;
-    c->host_rgba.ensure(npix * 4);
-    RR_HIP(hipMemcpyAsync(c->host_rgba.ptr, c->paths.rgba8.ptr, npix * 4, hipMemcpyDeviceToHost, st));
+    if (jpeg_quality > 0) {
+        if (c->jpeg_tab_quality != jpeg_quality) {
+            JpegTables t;
+            jpeg_tables(jpeg_quality, t);
+            float tab[192];
+            std::memcpy(tab, t.dct, sizeof t.dct);
+            std::memcpy(tab + 64, t.qinv_l, sizeof t.qinv_l);
+            std::memcpy(tab + 128, t.qinv_c, sizeof t.qinv_c);
+            c->jpeg_tab.ensure(192);
+            RR_HIP(hipMemcpy(c->jpeg_tab.ptr, tab, sizeof tab, hipMemcpyHostToDevice));
+            c->jpeg_tab_quality = jpeg_quality;
+        }
+        const size_t nc = jpeg_coeff_count(fs.W, fs.H);
+        c->jpeg_coeffs.ensure(nc);
+        c->host_coeffs.ensure(nc * sizeof(int16_t));
+        jpeg_fdct_device(c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr, c->jpeg_coeffs.ptr, st);
+        RR_HIP(hipMemcpyAsync(c->host_coeffs.ptr, c->jpeg_coeffs.ptr, nc * sizeof(int16_t), hipMemcpyDeviceToHost,
+                              st));
+    }
+    if (want_rgba) {
+        c->host_rgba.ensure(npix * 4);
+        RR_HIP(hipMemcpyAsync(c->host_rgba.ptr, c->paths.rgba8.ptr, npix * 4, hipMemcpyDeviceToHost, st));
+    }
     const int cpc = counters_per_chunk(fs.max_bounces);
     r.counters.resize((size_t)cpc * r.chunks);
     RR_HIP(hipMemcpyAsync(r.counters.data(), c->paths.counters.ptr, r.counters.size() * sizeof(int32_t),
@@ -431,12 +460,25 @@ int rr_render_frame(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_param
         FrameSetup fs = setup_frame(s->desc, frame, params);
         const double anim_ms = ms_since(t_anim);
         tm.started_rendering_at = unix_now();
-        FrameRun r = run_frame(c, s, fs, nullptr);
-        tm.finished_rendering_at = unix_now();
+        const bool jpeg = out_path && std::string(format) == "JPEG";
+        if (jpeg && (jpeg_quality < 1 || jpeg_quality > 100)) return fail(RR_EINVAL, "jpeg_quality must be 1..100");
+        FrameRun r = run_frame(c, s, fs, nullptr, jpeg ? jpeg_quality : 0, !jpeg);
+        const double t_sync = unix_now();
+        // the device JPEG transform + readback belong to "saving" (Blender's
+        // write_still); move that device interval out of the render span
+        tm.finished_rendering_at = jpeg ? t_sync - r.readback_ms * 1e-3 : t_sync;
         tm.file_saving_started_at = tm.finished_rendering_at;
         uint64_t bytes = 0;
         const auto t_enc = std::chrono::steady_clock::now();
-        if (out_path) {
+        if (jpeg) {
+            std::vector<uint8_t> data;
+            if (!encode_jpeg_coeffs(reinterpret_cast<const int16_t*>(c->host_coeffs.ptr), fs.W, fs.H, jpeg_quality,
+                                    data))
+                return fail(RR_EINVAL, "JPEG encode failed");
+            const std::string path = std::string(out_path) + ".jpg";
+            if (!write_file(path, data)) return fail(RR_EIO, "cannot write " + path + ": " + std::strerror(errno));
+            bytes = data.size();
+        } else if (out_path) {
             const int rc = do_encode(c->host_rgba.ptr, fs.W, fs.H, out_path, format, jpeg_quality, &bytes);
             if (rc != RR_OK) return rc;
         }
