@@ -75,6 +75,21 @@ def algorithmic_bytes(cls: str, stats, max_bounces: int) -> float:
     return 0.0
 
 
+def frame_partition(frames, step: int, rank: int, world: int):
+    """Frame a rank renders at a step: static round-robin over the job's frame set
+    (frames are independent, so ranks never exchange data)."""
+    return frames[(step * world + rank) % len(frames)]
+
+
+def reduce_max_seconds(elapsed: float, dist=None, device="cpu") -> float:
+    """Max of the per-rank timed-region wall time (the job ends with its slowest rank)."""
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def cpu_baseline(oracle_mod, state, budget_s: float):
     """Oracle (C restatement, OpenMP) on the host cores: evenly spread 4-row bands
     of the same frame until the budget is spent, extrapolated to frames/s."""
@@ -129,8 +144,8 @@ def main():
     flags = 0 if args.no_profile else rr.native.RR_FLAG_PROFILE_KERNELS
     runner = rr.BackendRunner(ROOT, device=local, params=rr.default_params(flags=flags))
 
-    def frame_of(step):  # static round-robin partition of the job's frame set over ranks
-        return frames[(step * world + rank) % len(frames)]
+    def frame_of(step):
+        return frame_partition(frames, step, rank, world)
 
     for w in range(args.warmup):
         runner.render_frame(job, frame_of(w))
@@ -149,10 +164,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     last_stats = runner.last_stats
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist is not None and gpu else "cpu")
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t_max = float(t.item())
+    t_max = reduce_max_seconds(elapsed, dist, dev if dist is not None and gpu else "cpu")
 
     # traversal counts for the byte model: one counting frame, outside the timed region
     scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, ROOT))
