@@ -45,6 +45,8 @@ def parse_args():
     ap.add_argument("--no-profile", action="store_true", help="time without per-kernel HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r1_pmc.json"),
+                    help="PMC traffic summary for roofline.traffic (tools/pmc_summary.py)")
     return ap.parse_args()
 
 
@@ -73,6 +75,25 @@ def algorithmic_bytes(cls: str, stats, max_bounces: int) -> float:
         npix = stats.width * stats.height
         return npix * (stats.spp * 16.0 + 32.0 * max(stats.chunks - 1, 0) + 16.0 + 4.0)
     return 0.0
+
+
+KERNEL_OF_CLASS = {"build": None, "primary": "k_primary", "extend": "k_extend", "shadow": "k_shadow",
+                   "accumulate": "k_accumulate"}
+
+
+def pmc_traffic(cls: str, path: str):
+    """HBM bytes per launch of the class's timed kernel (not the counting
+    instantiation) from a committed rocprofv3 PMC summary (tools/pmc_summary.py
+    traffic), or None when absent."""
+    name = KERNEL_OF_CLASS.get(cls)
+    if not name or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        ks = json.load(fh)["kernels"]
+    for k, v in ks.items():
+        if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
+            return {"bytes": v["traffic_bytes"], "source": os.path.relpath(path, ROOT), "kernel": k}
+    return None
 
 
 def frame_partition(frames, step: int, rank: int, world: int):
@@ -187,9 +208,12 @@ def main():
             avg_ms = kernel_ms[dom] / max(launches[dom], 1)
             per_launch = bytes_frame / launches_frame
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
+            tr = pmc_traffic(cls, args.pmc_summary)
             roofline = {"bound": "hbm", "kernel": cls, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": None, "bytes_per_launch": per_launch, "avg_launch_ms": avg_ms}
+                        "traffic": round(tr["bytes"]) if tr else None,
+                        "traffic_source": tr["source"] if tr else None,
+                        "bytes_per_launch": round(per_launch), "avg_launch_ms": round(avg_ms, 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -121,9 +121,10 @@ struct KernelProfiler {
 struct DevPaths {
     size_t cap = 0;
     DevBuf<float4> rad;                        // per path (p-indexed) radiance record
-    DevBuf<float4> ps_o[2], ps_d[2], ps_t[2];  // dense path queue, ping-pong per bounce
-    DevBuf<float4> sh_o, sh_d, sh_c;           // dense shadow queue
-    DevBuf<int32_t> counters;  // per chunk: [ext 0..B+1 | shadow 0..B]
+    DevBuf<float4> ps_o[2], ps_d[2], ps_t[2];  // segmented path queue, ping-pong per bounce
+    DevBuf<float4> sh_o, sh_d, sh_c;           // segmented shadow queue
+    DevBuf<uint32_t> segs;     // segment lengths [bounce parity][path | shadow][producer block]
+    DevBuf<int32_t> counters;  // per chunk, per bounce b: {paths entering b+1, shadow rays of b}
     DevBuf<int32_t> spill;     // traversal stack spill
     DevBuf<float4> film;
     DevBuf<uint8_t> rgba8;

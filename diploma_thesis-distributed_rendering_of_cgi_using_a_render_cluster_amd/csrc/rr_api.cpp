@@ -18,6 +18,7 @@
 #include <cerrno>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -201,9 +202,12 @@ FrameConsts make_consts(const FrameSetup& fs, int n_tris) {
 
 int choose_spp_chunk(const FrameSetup& fs) {
     if (fs.spp_per_chunk > 0) return std::min(fs.spp_per_chunk, fs.spp);
-    // ~16M paths in flight: fills 256 CUs many times over and keeps the SoA
-    // path state (~140 B/path, ~2.3 GB) well inside HBM.
-    const long target = 64L << 20;
+    // Paths in flight per chunk: the SoA path state is 160 B/path (radiance
+    // record 16 B, two path-queue slots 2 x 48 B, shadow slot 48 B), so the
+    // default 256M paths take ~43 GB of the 288 GB HBM (a 1080p 128 spp frame is one chunk). RR_TUNE_CHUNK_MPATHS
+    // overrides it (A/B knob); np stays below 2^31 for 32-bit queue indices.
+    static const long mpaths = getenv("RR_TUNE_CHUNK_MPATHS") ? atol(getenv("RR_TUNE_CHUNK_MPATHS")) : 256;
+    const long target = std::min<long>(std::max<long>(mpaths, 1) << 20, (1L << 31) - 1);
     long c = target / std::max(1, fs.W * fs.H);
     if (c < 1) c = 1;
     if (c > fs.spp) c = fs.spp;
@@ -305,12 +309,12 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
     st->camera_rays = (uint64_t)fs.W * fs.H * fs.spp;
     const int cpc = counters_per_chunk(fs.max_bounces);
     for (int c = 0; c < r.chunks; ++c) {
-        const int32_t* ext = &r.counters[(size_t)cpc * c];
-        const int32_t* shc = ext + fs.max_bounces + 2;
-        for (int b = 1; b <= fs.max_bounces; ++b) st->extension_rays += (uint64_t)ext[b];
-        for (int b = 0; b <= fs.max_bounces; ++b) st->shadow_rays += (uint64_t)shc[b];
-        st->primary_continued += (uint64_t)ext[1];
-        st->primary_shadow += (uint64_t)shc[0];
+        // pair b: {paths entering bounce b+1, shadow rays of bounce b} (wavefront.hip)
+        const int32_t* q = &r.counters[(size_t)cpc * c];
+        for (int b = 0; b < fs.max_bounces; ++b) st->extension_rays += (uint64_t)q[2 * b];
+        for (int b = 0; b <= fs.max_bounces; ++b) st->shadow_rays += (uint64_t)q[2 * b + 1];
+        st->primary_continued += (uint64_t)q[0];
+        st->primary_shadow += (uint64_t)q[1];
     }
     for (int k = 0; k < RR_K_CLASSES; ++k) {
         st->kernel_ms[k] = r.kernel_ms[k];

@@ -205,6 +205,7 @@ RR_HD void closest_tri(const TriPack& tp, int idx, float3 o, float3 d, float tmi
 // The LDS pointer carries its address space explicitly so push/pop compile to
 // ds_write/ds_read (a generic pointer would become flat_* accesses).
 typedef __attribute__((address_space(3))) int lds_int;
+typedef __attribute__((address_space(3))) uint32_t lds_uint;
 struct TravStack {
     lds_int* lds;   // &lds_base[threadIdx.x], stride kBlock
     int* spill;     // &spill_base[global thread], stride spill_stride

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <string>
 
 #include "device.hpp"
 
@@ -212,34 +213,124 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const L
     out.T = T;
 }
 
-// K8: wave-aggregated slot allocation (ballot + popcount, one atomic per wave).
-// Every lane of the wave must call it.
-__device__ __forceinline__ int wave_slot(bool want, int32_t* __restrict__ cnt) {
-    const uint64_t mask = __ballot(want);
-    if (mask == 0ull) return -1;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((unsigned long long)mask) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(cnt, __popcll(mask));
-    base = __shfl(base, leader);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    return want ? base + __popcll(mask & lt) : -1;
-}
+// K8: segmented queues, no atomics. A producer block owns segment
+// [blockIdx.x * seg_cap, +seg_cap) of each output queue and appends to it in
+// block order: per iteration the waves' ballot counts meet in LDS (one
+// barrier), every lane takes base + earlier waves + its ballot prefix, and the
+// block's running cursor advances. At exit the block publishes its two segment
+// lengths. seg_cap = ceil(input count / grid threads) * kBlock bounds what one
+// block can emit. A consumer turns a dense index j into a slot with the prefix
+// over the producer's segment lengths (SegIndex below), so queue order is
+// deterministic and no global counter is contended.
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kMaxBlocksPerCu = 8;  // grid cap per CU (segment arrays are sized for it)
+struct QueueLds {
+    uint32_t c[2][kWavesPerBlock], s[2][kWavesPerBlock];  // double-buffered by iteration parity
+};
+struct SegCursor {
+    uint32_t c = 0, s = 0;  // items this block has appended (block-uniform)
+    int parity = 0;
+};
 
-__device__ __forceinline__ void emit(const ShadeOut& so, int pid, PathQueue out, int32_t* cnt_out,
-                                     ShadowQueue sq, int32_t* cnt_sh) {
-    const int s1 = wave_slot(so.cont, cnt_out);
-    if (s1 >= 0) {
+__device__ __forceinline__ void emit(const ShadeOut& so, int pid, PathQueue out, ShadowQueue sq, uint32_t seg_base,
+                                     SegCursor& cur, QueueLds& ql) {
+    const uint64_t mc = __ballot(so.cont), ms = __ballot(so.shadow);
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int par = cur.parity;
+    if (lane == 0) {
+        ql.c[par][w] = (uint32_t)__popcll(mc);
+        ql.s[par][w] = (uint32_t)__popcll(ms);
+    }
+    __syncthreads();
+    uint32_t pc = 0, ps = 0, tc = 0, ts = 0;
+    for (int k = 0; k < kWavesPerBlock; ++k) {
+        const uint32_t a = ql.c[par][k], b = ql.s[par][k];
+        if (k < w) {
+            pc += a;
+            ps += b;
+        }
+        tc += a;
+        ts += b;
+    }
+    if (so.cont) {
+        const uint32_t s1 = seg_base + cur.c + pc + (uint32_t)__popcll(mc & below);
         out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
         out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, 0.0f);
         out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, 0.0f);
     }
-    const int s2 = wave_slot(so.shadow, cnt_sh);
-    if (s2 >= 0) {
+    if (so.shadow) {
+        const uint32_t s2 = seg_base + cur.s + ps + (uint32_t)__popcll(ms & below);
         sq.o[s2] = make_float4(so.so.x, so.so.y, so.so.z, i2f(pid));
         sq.d[s2] = make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist);
         sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, 0.0f);
     }
+    cur.c += tc;
+    cur.s += ts;
+    cur.parity = par ^ 1;
+}
+
+// Producer epilogue: publish this block's segment lengths.
+__device__ __forceinline__ void publish(const SegCursor& cur, uint32_t* __restrict__ seg_c,
+                                        uint32_t* __restrict__ seg_s) {
+    if (threadIdx.x == 0) {
+        seg_c[blockIdx.x] = cur.c;
+        seg_s[blockIdx.x] = cur.s;
+    }
+}
+
+// Consumer side: exclusive prefix of the producer's nseg segment lengths in
+// LDS (dynamic shared memory, nseg + 1 words), then dense index -> slot.
+struct SegIndex {
+    lds_uint* pre;
+    int nseg;
+    uint32_t cap;
+    __device__ __forceinline__ uint32_t slot(uint32_t j) const {
+        int lo = 0, hi = nseg - 1;  // largest s with pre[s] <= j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pre[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        return (uint32_t)lo * cap + (j - pre[lo]);
+    }
+};
+
+// Builds the prefix (all threads of the block must call it) and returns the
+// total; block 0 records the total for the host's ray statistics.
+__device__ __forceinline__ uint32_t seg_prefix(const uint32_t* __restrict__ seg, int nseg, lds_uint* pre,
+                                               uint32_t* __restrict__ total_out) {
+    __shared__ uint32_t wsum[kWavesPerBlock];
+    const int per = (nseg + kBlock - 1) / kBlock;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int first = t * per;
+    uint32_t local = 0;
+    for (int k = 0; k < per; ++k)
+        if (first + k < nseg) local += seg[first + k];
+    // inclusive wave scan of the per-thread sums
+    uint32_t incl = local;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
+        if (lane >= off) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+    for (int k = 0; k < kWavesPerBlock; ++k) {
+        if (k < w) wbase += wsum[k];
+        total += wsum[k];
+    }
+    uint32_t run = wbase + incl - local;
+    for (int k = 0; k < per; ++k)
+        if (first + k < nseg) {
+            pre[first + k] = run;
+            run += seg[first + k];
+        }
+    if (t == 0) pre[nseg] = total;
+    if (blockIdx.x == 0 && t == 0 && total_out) *total_out = total;
+    __syncthreads();
+    return total;
 }
 
 // Traversal-count reduction (RR_FLAG_COUNT_TRAVERSAL only).
@@ -257,21 +348,25 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
 }
 
 // K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
-template <bool kCount, int kMinWaves = 1>
-__global__ __launch_bounds__(kBlock, kMinWaves) void k_primary(FrameConsts fc, LightsMats lm, const BvhNode* __restrict__ nodes,
+// Outputs: segment seg_cap per block of the path queue (bounce 1) and the
+// shadow queue (bounce 0), lengths published in seg_c / seg_s.
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void k_primary(FrameConsts fc, LightsMats lm, const BvhNode* __restrict__ nodes,
                                                     const TriPack* __restrict__ tris, int np,
-                                                    float4* __restrict__ rad, PathQueue out,
-                                                    int32_t* __restrict__ cnt_out, ShadowQueue sq,
-                                                    int32_t* __restrict__ cnt_sh, int32_t* __restrict__ spill,
+                                                    float4* __restrict__ rad, PathQueue out, ShadowQueue sq,
+                                                    uint32_t seg_cap, uint32_t* __restrict__ seg_c,
+                                                    uint32_t* __restrict__ seg_s, int32_t* __restrict__ spill,
                                                     unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
-    const int lane = threadIdx.x & 63;
+    __shared__ QueueLds ql;
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
     TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
     TravCount cnt;
-    for (int i0 = gtid - lane; i0 < np; i0 += stride) {
-        const int p = i0 + lane;
+    SegCursor cur;
+    const uint32_t seg_base = blockIdx.x * seg_cap;
+    for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {  // block-uniform trip count
+        const int p = b0 + (int)threadIdx.x;
         ShadeOut so;
         so.cont = so.shadow = false;
         if (p < np) {
@@ -287,34 +382,41 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_primary(FrameConsts fc, L
             shade(fc, 0, lm, tris, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
             rad[p] = make_float4(L.x, L.y, L.z, 0.0f);
         }
-        emit(so, p, out, cnt_out, sq, cnt_sh);
+        emit(so, p, out, sq, seg_base, cur, ql);
     }
+    publish(cur, seg_c, seg_s);
     if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
 }
 
-// K-extend: closest hit + shade of bounce b >= 1 over the dense path queue.
+// K-extend: closest hit + shade of bounce b >= 1 over the path queue of the
+// previous bounce (segments in_seg[0..in_nseg) of capacity in_cap).
 template <bool kCount>
 __global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, LightsMats lm,
                                                    const BvhNode* __restrict__ nodes,
-                                                   const TriPack* __restrict__ tris,
-                                                   const int32_t* __restrict__ cnt_in, PathQueue in,
-                                                   float4* __restrict__ rad, PathQueue out,
-                                                   int32_t* __restrict__ cnt_out, ShadowQueue sq,
-                                                   int32_t* __restrict__ cnt_sh, int32_t* __restrict__ spill,
-                                                   unsigned long long* __restrict__ tc) {
+                                                   const TriPack* __restrict__ tris, PathQueue in,
+                                                   const uint32_t* __restrict__ in_seg, int in_nseg, uint32_t in_cap,
+                                                   uint32_t* __restrict__ in_total, float4* __restrict__ rad,
+                                                   PathQueue out, ShadowQueue sq, uint32_t seg_cap,
+                                                   uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
+                                                   int32_t* __restrict__ spill, unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
-    const int count = *cnt_in;
-    const int lane = threadIdx.x & 63;
+    __shared__ QueueLds ql;
+    extern __shared__ uint32_t dyn_pre[];
+    const SegIndex ix{(lds_uint*)dyn_pre, in_nseg, in_cap};
+    const int count = (int)seg_prefix(in_seg, in_nseg, ix.pre, in_total);
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
     TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
     TravCount cnt;
+    SegCursor cur;
+    const uint32_t seg_base = blockIdx.x * seg_cap;
     int pid = 0;
-    for (int i0 = gtid - lane; i0 < count; i0 += stride) {
-        const int i = i0 + lane;
+    for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
+        const int j = b0 + (int)threadIdx.x;
         ShadeOut so;
         so.cont = so.shadow = false;
-        if (i < count) {
+        if (j < count) {
+            const uint32_t i = ix.slot((uint32_t)j);
             const float4 a = in.o[i], b = in.d[i], c = in.t[i];
             pid = f2i(a.w);
             const float3 o = xyz(a), d = xyz(b);
@@ -328,25 +430,29 @@ __global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, L
             shade(fc, bounce, lm, tris, o, d, xyz(c), h, key, L, so);
             rad[pid] = make_float4(L.x, L.y, L.z, 0.0f);
         }
-        emit(so, pid, out, cnt_out, sq, cnt_sh);
+        emit(so, pid, out, sq, seg_base, cur, ql);
     }
+    publish(cur, seg_c, seg_s);
     if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
 }
 
 // K10: shadow rays of one bounce; unoccluded -> radiance += contribution.
 template <bool kCount>
 __global__ __launch_bounds__(kBlock) void k_shadow(const BvhNode* __restrict__ nodes,
-                                                   const TriPack* __restrict__ tris, int n_tris,
-                                                   const int32_t* __restrict__ cnt_sh, ShadowQueue sq,
-                                                   float4* __restrict__ rad, int32_t* __restrict__ spill,
-                                                   unsigned long long* __restrict__ tc) {
+                                                   const TriPack* __restrict__ tris, int n_tris, ShadowQueue sq,
+                                                   const uint32_t* __restrict__ in_seg, int in_nseg, uint32_t in_cap,
+                                                   uint32_t* __restrict__ in_total, float4* __restrict__ rad,
+                                                   int32_t* __restrict__ spill, unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
-    const int count = *cnt_sh;
+    extern __shared__ uint32_t dyn_pre[];
+    const SegIndex ix{(lds_uint*)dyn_pre, in_nseg, in_cap};
+    const int count = (int)seg_prefix(in_seg, in_nseg, ix.pre, in_total);
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
     TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
     TravCount cnt;
-    for (int i = gtid; i < count; i += stride) {
+    for (int j = gtid; j < count; j += stride) {
+        const uint32_t i = ix.slot((uint32_t)j);
         const float4 a = sq.o[i], b = sq.d[i];
         Hit h;
         if (!traverse<true, kCount>(nodes, tris, n_tris, xyz(a), xyz(b), 0.0f, b.w, st, h, cnt)) {
@@ -424,6 +530,9 @@ int device_cu_count() {
     return cus;
 }
 
+// Per chunk, one pair per bounce b = 0..max_bounces: {paths entering bounce
+// b+1, shadow rays of bounce b}, written by the consuming kernels (+1 pair of
+// slack).
 int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2); }
 
 namespace {
@@ -431,19 +540,25 @@ namespace {
 // and LDS budget admits (a grid-stride loop over more blocks than fit would
 // only queue the surplus behind the first wave of blocks).
 template <typename K>
-int resident_grid(K kernel) {
+int resident_grid(K kernel, size_t dyn_lds = 0) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, dyn_lds) != hipSuccess || per_cu <= 0)
         per_cu = 4;
-    return device_cu_count() * per_cu;
+    return device_cu_count() * std::min(per_cu, kMaxBlocksPerCu);
 }
+// Consumers hold the producer's segment prefix in dynamic LDS: one word per
+// producer block + 1. Producers are k_primary and k_extend; giving k_extend
+// that LDS can only shrink its grid, so dyn_lds bounds both.
 struct Grids {
-    int primary, primary5, extend, shadow, accum;
-    Grids()
-        : primary(resident_grid(k_primary<false>)), primary5(resident_grid(k_primary<false, 5>)),
-          extend(resident_grid(k_extend<false>)),
-          shadow(resident_grid(k_shadow<false>)),
-          accum(resident_grid(k_accumulate)) {}
+    int primary, extend, shadow, accum;
+    size_t dyn_lds;
+    Grids() {
+        primary = resident_grid(k_primary<false>);
+        dyn_lds = sizeof(uint32_t) * (size_t)(std::max(primary, resident_grid(k_extend<false>)) + 1);
+        extend = resident_grid(k_extend<false>, dyn_lds);
+        shadow = resident_grid(k_shadow<false>, dyn_lds);
+        accum = resident_grid(k_accumulate);
+    }
 };
 const Grids& grids() {
     static Grids g;
@@ -453,10 +568,18 @@ inline int clamp_grid(long work, int resident) {
     const long g = (work + kBlock - 1) / kBlock;
     return (int)std::max<long>(1, std::min<long>(g, resident));
 }
+// Segment capacity of a producer launched with `grid` blocks over at most
+// `work` items: the most any one block can emit.
+inline uint32_t seg_cap(long work, int grid) {
+    const long stride = (long)grid * kBlock;
+    return (uint32_t)(((work + stride - 1) / stride) * kBlock);
+}
 }  // namespace
 
 void DevPaths::ensure_paths(size_t n) {
-    if (grid_blocks == 0) grid_blocks = device_cu_count() * 8;
+    if (grid_blocks == 0) grid_blocks = device_cu_count() * kMaxBlocksPerCu;
+    n += (size_t)grid_blocks * kBlock;  // segment round-up slack (seg_cap)
+    segs.ensure((size_t)4 * grid_blocks);
     if (n > cap) {
         for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                                   &sh_c})
@@ -470,7 +593,7 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
-    counters.release(); spill.release();
+    counters.release(); spill.release(); segs.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     trav_counts.release();
     prof.release();
@@ -503,26 +626,32 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         fc.spp_chunk = base.spp_chunk;
         if (fc.first_sample + fc.spp_chunk > base.spp_total) fc.spp_chunk = base.spp_total - fc.first_sample;
         const int np = npix * fc.spp_chunk;
-        int32_t* ext = p.counters.ptr + (size_t)cpc * c;  // ext[b]: paths entering bounce b (b >= 1)
-        int32_t* shc = ext + (base.max_bounces + 2);      // shc[b]: shadow rays of bounce b
+        // segment lengths, ping-pong by bounce parity: [parity][path | shadow][grid]
+        auto seg = [&](int b, int q) { return p.segs.ptr + ((size_t)(b & 1) * 2 + q) * p.grid_blocks; };
+        uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr + (size_t)cpc * c);
+        const size_t dyn = G.dyn_lds;
+        const int gp = clamp_grid(np, G.primary), ge = clamp_grid(np, G.extend), gs = clamp_grid(np, G.shadow);
+        const uint32_t cap_p = seg_cap(np, gp), cap_e = seg_cap(np, ge);
         pr.begin(st, RR_K_PRIMARY);
-        // RR_TUNE_PRIMARY_WAVES=5: register-capped variant (A/B tuning knob)
-        static const bool prim5 = getenv("RR_TUNE_PRIMARY_WAVES") && atoi(getenv("RR_TUNE_PRIMARY_WAVES")) == 5;
-        auto kprim = tc ? k_primary<true> : (prim5 ? k_primary<false, 5> : k_primary<false>);
-        kprim<<<clamp_grid(np, prim5 ? G.primary5 : G.primary), kBlock, 0, st>>>(fc, lm, s.nodes.ptr, s.tris.ptr, np, p.rad.ptr,
-                                                                 pq[1], ext + 1, sq, shc, p.spill.ptr, tc);
+        (tc ? k_primary<true> : k_primary<false>)<<<gp, kBlock, 0, st>>>(
+            fc, lm, s.nodes.ptr, s.tris.ptr, np, p.rad.ptr, pq[1], sq, cap_p, seg(0, 0), seg(0, 1), p.spill.ptr, tc);
         pr.end(st);
+        int g_prev = gp;        // grid of the producer of the current queues
+        uint32_t cap_prev = cap_p;
         for (int b = 0; b <= base.max_bounces; ++b) {
             if (b > 0) {
                 pr.begin(st, RR_K_EXTEND);
-                (tc ? k_extend<true> : k_extend<false>)<<<clamp_grid(np, G.extend), kBlock, 0, st>>>(fc, b, lm, s.nodes.ptr, s.tris.ptr, ext + b,
-                                                                       pq[b & 1], p.rad.ptr, pq[(b + 1) & 1],
-                                                                       ext + b + 1, sq, shc + b, p.spill.ptr, tc);
+                (tc ? k_extend<true> : k_extend<false>)<<<ge, kBlock, dyn, st>>>(
+                    fc, b, lm, s.nodes.ptr, s.tris.ptr, pq[b & 1], seg(b - 1, 0), g_prev, cap_prev,
+                    tot + 2 * (b - 1), p.rad.ptr, pq[(b + 1) & 1], sq, cap_e, seg(b, 0), seg(b, 1), p.spill.ptr, tc);
                 pr.end(st);
+                g_prev = ge;
+                cap_prev = cap_e;
             }
             pr.begin(st, RR_K_SHADOW);
-            (tc ? k_shadow<true> : k_shadow<false>)<<<clamp_grid(np, G.shadow), kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, shc + b, sq,
-                                                                   p.rad.ptr, p.spill.ptr, tc);
+            (tc ? k_shadow<true> : k_shadow<false>)<<<gs, kBlock, dyn, st>>>(
+                s.nodes.ptr, s.tris.ptr, s.n_tris, sq, seg(b, 1), g_prev, cap_prev, tot + 2 * b + 1, p.rad.ptr,
+                p.spill.ptr, tc);
             pr.end(st);
         }
         const int ga = clamp_grid(npix, G.accum);

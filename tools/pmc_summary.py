@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Per-kernel summaries of rocprofv3 output directories (CSV format), written
+into profiles/ so bench.py can quote PMC-measured HBM traffic per launch.
+
+  python tools/pmc_summary.py stats  <kernel-trace dir> > profiles/r1_kernel_stats.md
+  python tools/pmc_summary.py traffic --fetch <dir> --write <dir> [--sq <dir> ...] -o profiles/r1_pmc.json
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so the
+corrected read bytes are 2 x FETCH_SIZE x 1024 (the correction is calibrated for
+16 B/lane streaming loads only; raw values are kept beside it).
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+_NAME = re.compile(r"(k_\w+)(<[^>(]*>)?")
+
+
+def short_name(full: str) -> str:
+    m = _NAME.search(full)
+    if not m:
+        return full.split("(")[0][-60:]
+    return m.group(1) + (m.group(2) or "").replace(" ", "")
+
+
+def _rows(d: str, suffix: str):
+    files = sorted(glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True))
+    if not files:
+        raise SystemExit(f"no *{suffix} under {d}")
+    for f in files:
+        with open(f, newline="") as fh:
+            yield from csv.DictReader(fh)
+
+
+def kernel_stats(d: str) -> dict:
+    out = {}
+    for r in _rows(d, "kernel_stats.csv"):
+        out[short_name(r["Name"])] = {"calls": int(r["Calls"]), "total_ms": int(r["TotalDurationNs"]) / 1e6,
+                                      "avg_ms": float(r["AverageNs"]) / 1e6, "pct": float(r["Percentage"])}
+    return out
+
+
+def counters(d: str) -> dict:
+    """{kernel: {counter: [per-dispatch values]}} from a --pmc pass."""
+    acc = defaultdict(lambda: defaultdict(dict))
+    for r in _rows(d, "counter_collection.csv"):
+        k = short_name(r["Kernel_Name"])
+        acc[k][r["Counter_Name"]][r.get("Dispatch_Id") or r.get("Correlation_Id")] = float(r["Counter_Value"])
+    return {k: {c: list(v.values()) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def cmd_stats(a):
+    st = kernel_stats(a.dir)
+    print("| kernel | calls | total ms | avg ms | % |")
+    print("|---|---:|---:|---:|---:|")
+    for k, v in sorted(st.items(), key=lambda kv: -kv[1]["total_ms"]):
+        print(f"| `{k}` | {v['calls']} | {v['total_ms']:.3f} | {v['avg_ms']:.4f} | {v['pct']:.2f} |")
+
+
+def cmd_traffic(a):
+    fetch, write = counters(a.fetch), counters(a.write)
+    extra = {}
+    for d in a.sq or []:
+        for k, cs in counters(d).items():
+            extra.setdefault(k, {}).update(cs)
+    out = {"source": {"fetch": a.fetch, "write": a.write, "sq": a.sq or []},
+           "units": "bytes per launch; fetch_bytes = 2 x FETCH_SIZE(KiB) x 1024 (gfx950 correction)",
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, {}).get("FETCH_SIZE", [])
+        w = write.get(k, {}).get("WRITE_SIZE", [])
+        n = max(len(f), len(w), 1)
+        fr = sum(f) / max(len(f), 1) * 1024.0
+        wr = sum(w) / max(len(w), 1) * 1024.0
+        e = {"launches": n, "fetch_size_raw_bytes": fr, "fetch_bytes": 2.0 * fr, "write_bytes": wr,
+             "traffic_bytes": 2.0 * fr + wr}
+        for c, vals in extra.get(k, {}).items():
+            e[c] = sum(vals) / max(len(vals), 1)
+        out["kernels"][k] = e
+    with open(a.o, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps({k: round(v["traffic_bytes"] / 1e6, 3) for k, v in out["kernels"].items()}))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    s = sub.add_parser("stats")
+    s.add_argument("dir")
+    t = sub.add_parser("traffic")
+    t.add_argument("--fetch", required=True)
+    t.add_argument("--write", required=True)
+    t.add_argument("--sq", action="append")
+    t.add_argument("-o", required=True)
+    a = ap.parse_args(argv)
+    {"stats": cmd_stats, "traffic": cmd_traffic}[a.cmd](a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
