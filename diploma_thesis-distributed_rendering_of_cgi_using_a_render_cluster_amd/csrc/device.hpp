@@ -145,12 +145,13 @@ struct FrameConsts {
     float half_w, half_h, clip_start, clip_end;
     float inv_w2, inv_h2;  // 2/W, 2/H
     int W, H, npix;
+    FastDiv div_w, div_npix;  // pixel index -> (x, y), path index -> (sample, pixel)
     int spp_total, spp_chunk, first_sample, max_bounces, n_lights;
     uint32_t seed;
     float clamp_indirect, exposure_scale, inv_spp;
     int view_transform;
     float3 world;
-    int n_tris;
+    int n_tris, n_mats;
 };
 
 // LBVH build for the current obj_xform (uploaded by the caller).

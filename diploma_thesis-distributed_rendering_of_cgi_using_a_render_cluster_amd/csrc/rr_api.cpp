@@ -187,9 +187,12 @@ FrameConsts make_consts(const FrameSetup& fs, int n_tris) {
     k.W = fs.W;
     k.H = fs.H;
     k.npix = fs.W * fs.H;
+    k.div_w = FastDiv::make((uint32_t)fs.W);
+    k.div_npix = FastDiv::make((uint32_t)k.npix);
     k.spp_total = fs.spp;
     k.max_bounces = fs.max_bounces;
     k.n_lights = (int)(fs.lights.size() / RR_LIGHT_FLOATS);
+    k.n_mats = (int)(fs.materials.size() / RR_MAT_FLOATS);
     k.seed = fs.seed;
     k.clamp_indirect = fs.clamp_indirect;
     k.exposure_scale = fs.exposure_scale;

@@ -69,6 +69,27 @@ RR_HD float3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
 RR_HD int f2i(float f) { return __builtin_bit_cast(int, f); }
 RR_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
 
+// Division by a runtime-constant divisor d >= 1 for 0 <= n < 2^31 with one
+// mul_hi + shift (Granlund-Montgomery): k = 31 + ceil(log2 d), m = ceil(2^k / d)
+// < 2^32; n*m/2^k = n/d + n*e/(d*2^k) with e = m*d - 2^k < d, and n*e < n*d <=
+// 2^k keeps the floor exact. Integer results, so bit-exactness is unaffected.
+struct FastDiv {
+    uint32_t m;
+    int sh;    // k - 32
+    int one;   // d == 1
+    static FastDiv make(uint32_t d) {
+        FastDiv f{0u, 0, d == 1u ? 1 : 0};
+        if (d <= 1u) return f;
+        int c = 0;
+        while ((1ull << c) < d) ++c;
+        const int k = 31 + c;
+        f.m = (uint32_t)(((1ull << k) + d - 1) / d);
+        f.sh = k - 32;
+        return f;
+    }
+    RR_D uint32_t div(uint32_t n) const { return one ? n : (__umulhi(n, m) >> sh); }
+};
+
 // ------------------------------------------------------------------- RNG ---
 // Counter-based: u(dim) = hash(key + (dim+1)*golden), key = f(seed, pixel, sample).
 // Independent of execution order, so wavefront (GPU) and scalar (oracle)
@@ -138,8 +159,9 @@ RR_HD float3 offset_ray(float3 p, float3 n) {
     return mk3(offset_axis(p.x, n.x), offset_axis(p.y, n.y), offset_axis(p.z, n.z));
 }
 
-// Piecewise-linear table read, u in [0,1].
-RR_HD float table_lerp(const float* t, int n, float u) {
+// Piecewise-linear table read, u in [0,1] (t: global or LDS pointer).
+template <typename FloatP>
+RR_HD float table_lerp(FloatP t, int n, float u) {
     const float f = u * (float)(n - 1);
     int i = (int)f;
     if (i >= n - 1) return t[n - 1];
@@ -206,6 +228,38 @@ RR_HD void closest_tri(const TriPack& tp, int idx, float3 o, float3 d, float tmi
 // ds_write/ds_read (a generic pointer would become flat_* accesses).
 typedef __attribute__((address_space(3))) int lds_int;
 typedef __attribute__((address_space(3))) uint32_t lds_uint;
+// LDS-staged scene data (wavefront.hip stage_scene): HIP's float4 has no
+// address-space-3 copy, so 16-byte moves use a clang vector type.
+typedef float rr_f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) rr_f4v lds_f4w;
+typedef __attribute__((address_space(3))) const BvhNode lds_node;
+typedef __attribute__((address_space(3))) const TriPack lds_tri;
+typedef __attribute__((address_space(3))) const float lds_float;
+RR_D float4 lds_ld4(const __attribute__((address_space(3))) rr_f4v* p) {
+    const rr_f4v v = *p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+RR_D BvhNode load_node(const BvhNode* __restrict__ p, int i) { return p[i]; }
+RR_D BvhNode load_node(lds_node* p, int i) {
+    const __attribute__((address_space(3))) rr_f4v* q = (const __attribute__((address_space(3))) rr_f4v*)(p + i);
+    BvhNode n;
+    n.a = lds_ld4(q);
+    n.b = lds_ld4(q + 1);
+    n.c = lds_ld4(q + 2);
+    const float4 d = lds_ld4(q + 3);
+    n.d = make_int4(__builtin_bit_cast(int, d.x), __builtin_bit_cast(int, d.y), __builtin_bit_cast(int, d.z),
+                    __builtin_bit_cast(int, d.w));
+    return n;
+}
+RR_D TriPack load_tri(const TriPack* __restrict__ p, int i) { return p[i]; }
+RR_D TriPack load_tri(lds_tri* p, int i) {
+    const __attribute__((address_space(3))) rr_f4v* q = (const __attribute__((address_space(3))) rr_f4v*)(p + i);
+    TriPack t;
+    t.p0 = lds_ld4(q);
+    t.p1 = lds_ld4(q + 1);
+    t.p2 = lds_ld4(q + 2);
+    return t;
+}
 struct TravStack {
     lds_int* lds;   // &lds_base[threadIdx.x], stride kBlock
     int* spill;     // &spill_base[global thread], stride spill_stride
@@ -237,9 +291,10 @@ struct TravCount {
 
 // Closest hit over the LBVH. Near child first (left on ties); leaf children are
 // intersected as soon as their box passes.
-template <bool kAnyHit, bool kCount = false, typename Stack>
-RR_D bool traverse(const BvhNode* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
-                   float3 o, float3 d, float tmin, float tmax, Stack& st, Hit& h, TravCount& cnt) {
+// nodes / tris: global or LDS pointers (wavefront.hip SceneView).
+template <bool kAnyHit, bool kCount = false, typename NodeP, typename TriP, typename Stack>
+RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float tmin, float tmax, Stack& st, Hit& h,
+                   TravCount& cnt) {
     h.t = tmax;
     h.u = h.v = 0.0f;
     h.idx = -1;
@@ -249,7 +304,7 @@ RR_D bool traverse(const BvhNode* __restrict__ nodes, const TriPack* __restrict_
     int node = 0;
     st.sp = 0;
     for (;;) {
-        const BvhNode nd = nodes[node];
+        const BvhNode nd = load_node(nodes, node);
         if (kCount) ++cnt.nodes;
         float tl, tr;
         bool hl = slab(o, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
@@ -257,13 +312,13 @@ RR_D bool traverse(const BvhNode* __restrict__ nodes, const TriPack* __restrict_
         const int cl = nd.d.x, cr = nd.d.y;
         if (hl && cl < 0) {
             if (kCount) ++cnt.tris;
-            closest_tri(tris[~cl], ~cl, o, d, tmin, h);
+            closest_tri(load_tri(tris, ~cl), ~cl, o, d, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
             hl = false;
         }
         if (hr && cr < 0) {
             if (kCount) ++cnt.tris;
-            closest_tri(tris[~cr], ~cr, o, d, tmin, h);
+            closest_tri(load_tri(tris, ~cr), ~cr, o, d, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
             hr = false;
         }

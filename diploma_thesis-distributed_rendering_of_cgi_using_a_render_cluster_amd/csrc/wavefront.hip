@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <map>
 #include <string>
 
 #include "device.hpp"
@@ -35,13 +36,6 @@
 namespace rr {
 
 namespace {
-
-struct LightsMats {
-    const float* lights;     // n_lights * RR_LIGHT_FLOATS
-    const float* materials;  // RR_MAT_FLOATS each
-    const float* filter;     // kFilterTableSize
-    const float* srgb;       // kSrgbLutSize + 1
-};
 
 constexpr int kFilterN = 1024;
 constexpr int kSrgbN = 4096;
@@ -61,8 +55,22 @@ struct ShadowQueue {
     float4* c;  // contribution.xyz, 0
 };
 
-__device__ __forceinline__ Mat load_mat(const float* __restrict__ mats, int id) {
-    const float* m = mats + kMatF * id;
+// Read-only scene data of the path kernels: in HBM (GlobalView) or, for
+// scenes small enough, staged once per block into LDS (LdsView), which turns
+// every node / triangle / material / filter fetch of the traversal and shading
+// chains into a ds_read (~64-cycle latency instead of an L1/L2 round trip).
+template <typename NodeP, typename TriP, typename FloatP>
+struct SceneView {
+    NodeP nodes;
+    TriP tris;
+    FloatP mats, lights, filter;
+};
+using GlobalView = SceneView<const BvhNode*, const TriPack*, const float*>;
+using LdsView = SceneView<lds_node*, lds_tri*, lds_float*>;
+
+template <typename FloatP>
+__device__ __forceinline__ Mat load_mat(FloatP mats, int id) {
+    const FloatP m = mats + kMatF * id;
     Mat r;
     r.base = mk3(m[0], m[1], m[2]);
     r.metallic = m[3];
@@ -76,10 +84,11 @@ __device__ __forceinline__ Mat load_mat(const float* __restrict__ mats, int id) 
 
 // Camera ray for (pixel, sample): filter-importance-sampled subpixel position,
 // pinhole through the sensor plane at unit distance, z-depth clipping.
-__device__ __forceinline__ void camera_ray(const FrameConsts& fc, const float* __restrict__ filt, int pix,
+template <typename FloatP>
+__device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, int pix,
                                            uint32_t key, float3& o, float3& d, float& tmin, float& tmax) {
-    const int px = pix % fc.W;
-    const int py = pix / fc.W;
+    const int py = (int)fc.div_w.div((uint32_t)pix);
+    const int px = pix - py * fc.W;
     const float fx = (float)px + 0.5f + table_lerp(filt, kFilterN, rng(key, 0));
     const float fy = (float)py + 0.5f + table_lerp(filt, kFilterN, rng(key, 1));
     const float sx = (fx * fc.inv_w2 - 1.0f) * fc.half_w;
@@ -109,9 +118,9 @@ RR_D void add_to(float3& L, float3 c) {
 }
 
 // K9: shade one path at `bounce` given its closest hit; L updated in place.
-__device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const LightsMats& lm,
-                                      const TriPack* __restrict__ tris, float3 o, float3 d, float3 T,
-                                      const Hit& h, uint32_t key, float3& L, ShadeOut& out) {
+template <typename View>
+__device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const View& v, float3 o, float3 d,
+                                      float3 T, const Hit& h, uint32_t key, float3& L, ShadeOut& out) {
     out.cont = false;
     out.shadow = false;
     if (h.idx < 0) {
@@ -120,9 +129,9 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const L
         add_to(L, c);
         return;
     }
-    const TriPack tp = tris[h.idx];
+    const TriPack tp = load_tri(v.tris, h.idx);
     const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2);
-    const Mat m = load_mat(lm.materials, f2i(tp.p1.w));
+    const Mat m = load_mat(v.mats, f2i(tp.p1.w));
     const float t = h.t;
     const float3 P = mk3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
     float3 N = norm3(cross3(e1, e2));
@@ -140,7 +149,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const L
     if (fc.n_lights > 0) {
         int li = (int)(rng(key, dim0) * (float)fc.n_lights);
         if (li > fc.n_lights - 1) li = fc.n_lights - 1;
-        const float* lt = lm.lights + kLightF * li;
+        const auto lt = v.lights + kLightF * li;
         float3 wi, Li;  // Li: radiance x cos_light / pdf (solid angle), i.e. I*cos/d^2
         float dist;
         if (lt[0] == 0.0f) {  // point / disk light
@@ -213,75 +222,56 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const L
     out.T = T;
 }
 
-// K8: segmented queues, no atomics. A producer block owns segment
-// [blockIdx.x * seg_cap, +seg_cap) of each output queue and appends to it in
-// block order: per iteration the waves' ballot counts meet in LDS (one
-// barrier), every lane takes base + earlier waves + its ballot prefix, and the
-// block's running cursor advances. At exit the block publishes its two segment
-// lengths. seg_cap = ceil(input count / grid threads) * kBlock bounds what one
-// block can emit. A consumer turns a dense index j into a slot with the prefix
-// over the producer's segment lengths (SegIndex below), so queue order is
-// deterministic and no global counter is contended.
+// K8: segmented queues, no atomics, no barriers. Each producer WAVE owns
+// segment [wave * seg_cap, +seg_cap) of each output queue (wave = blockIdx.x *
+// kWavesPerBlock + wave in block) and appends to it in order: a lane's slot is
+// the wave's running cursor + its ballot prefix. At exit the wave publishes its
+// two segment lengths. seg_cap = ceil(input count / grid threads) * 64 bounds
+// what one wave can emit. A consumer turns a dense index j into a slot with
+// the prefix over the producer's segment lengths (SegIndex below), so queue
+// order is deterministic, no global counter is contended and waves of a block
+// never wait for each other.
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kMaxBlocksPerCu = 8;  // grid cap per CU (segment arrays are sized for it)
-struct QueueLds {
-    uint32_t c[2][kWavesPerBlock], s[2][kWavesPerBlock];  // double-buffered by iteration parity
-};
 struct SegCursor {
-    uint32_t c = 0, s = 0;  // items this block has appended (block-uniform)
-    int parity = 0;
+    uint32_t c = 0, s = 0;  // items this wave has appended (wave-uniform)
 };
 
+RR_D uint32_t wave_id() { return blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); }
+
 __device__ __forceinline__ void emit(const ShadeOut& so, int pid, PathQueue out, ShadowQueue sq, uint32_t seg_base,
-                                     SegCursor& cur, QueueLds& ql) {
+                                     SegCursor& cur) {
     const uint64_t mc = __ballot(so.cont), ms = __ballot(so.shadow);
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const int par = cur.parity;
-    if (lane == 0) {
-        ql.c[par][w] = (uint32_t)__popcll(mc);
-        ql.s[par][w] = (uint32_t)__popcll(ms);
-    }
-    __syncthreads();
-    uint32_t pc = 0, ps = 0, tc = 0, ts = 0;
-    for (int k = 0; k < kWavesPerBlock; ++k) {
-        const uint32_t a = ql.c[par][k], b = ql.s[par][k];
-        if (k < w) {
-            pc += a;
-            ps += b;
-        }
-        tc += a;
-        ts += b;
-    }
     if (so.cont) {
-        const uint32_t s1 = seg_base + cur.c + pc + (uint32_t)__popcll(mc & below);
+        const uint32_t s1 = seg_base + cur.c + (uint32_t)__popcll(mc & below);
         out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
         out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, 0.0f);
         out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, 0.0f);
     }
     if (so.shadow) {
-        const uint32_t s2 = seg_base + cur.s + ps + (uint32_t)__popcll(ms & below);
+        const uint32_t s2 = seg_base + cur.s + (uint32_t)__popcll(ms & below);
         sq.o[s2] = make_float4(so.so.x, so.so.y, so.so.z, i2f(pid));
         sq.d[s2] = make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist);
         sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, 0.0f);
     }
-    cur.c += tc;
-    cur.s += ts;
-    cur.parity = par ^ 1;
+    cur.c += (uint32_t)__popcll(mc);
+    cur.s += (uint32_t)__popcll(ms);
 }
 
-// Producer epilogue: publish this block's segment lengths.
+// Producer epilogue: publish this wave's segment lengths.
 __device__ __forceinline__ void publish(const SegCursor& cur, uint32_t* __restrict__ seg_c,
                                         uint32_t* __restrict__ seg_s) {
-    if (threadIdx.x == 0) {
-        seg_c[blockIdx.x] = cur.c;
-        seg_s[blockIdx.x] = cur.s;
+    if ((threadIdx.x & 63) == 0) {
+        seg_c[wave_id()] = cur.c;
+        seg_s[wave_id()] = cur.s;
     }
 }
 
-// Consumer side: exclusive prefix of the producer's nseg segment lengths in
-// LDS (dynamic shared memory, nseg + 1 words), then dense index -> slot.
+// Consumer side: exclusive prefix of the producer's nseg (= waves) segment
+// lengths in LDS (dynamic shared memory, nseg + 1 words), then dense index ->
+// slot.
 struct SegIndex {
     lds_uint* pre;
     int nseg;
@@ -348,68 +338,129 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
 }
 
 // K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
+// Scene data as kernel arguments (global pointers + counts).
+struct SceneArgs {
+    const BvhNode* nodes;
+    const TriPack* tris;
+    const float* mats;
+    const float* lights;
+    const float* filter;
+    int n_nodes, n_tris, n_mats, n_lights;
+};
+
+RR_D GlobalView global_view(const SceneArgs& a) { return {a.nodes, a.tris, a.mats, a.lights, a.filter}; }
+
+RR_D void lds_copy(lds_f4w* dst, const float4* __restrict__ src, int n4) {
+    const rr_f4v* s = reinterpret_cast<const rr_f4v*>(src);
+    for (int i = threadIdx.x; i < n4; i += kBlock) dst[i] = s[i];
+}
+// Stages the scene at the start of dynamic LDS (all threads call; ends with a
+// barrier). `shading`: also materials, lights and the filter table. Returns the
+// view; `used` receives the float4 slots taken (LDS layout: scene_lds_f4()).
+RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& used) {
+    lds_f4w* q = base;
+    LdsView v;
+    v.nodes = (lds_node*)q;
+    lds_copy(q, reinterpret_cast<const float4*>(a.nodes), 4 * a.n_nodes);
+    q += 4 * a.n_nodes;
+    v.tris = (lds_tri*)q;
+    lds_copy(q, reinterpret_cast<const float4*>(a.tris), 3 * a.n_tris);
+    q += 3 * a.n_tris;
+    v.mats = v.lights = v.filter = nullptr;
+    if (shading) {
+        v.mats = (lds_float*)q;
+        lds_copy(q, reinterpret_cast<const float4*>(a.mats), 3 * a.n_mats);
+        q += 3 * a.n_mats;
+        v.lights = (lds_float*)q;
+        lds_copy(q, reinterpret_cast<const float4*>(a.lights), 3 * a.n_lights);
+        q += 3 * a.n_lights;
+        v.filter = (lds_float*)q;
+        lds_copy(q, reinterpret_cast<const float4*>(a.filter), kFilterN / 4);
+        q += kFilterN / 4;
+    }
+    used = (int)(q - base);
+    __syncthreads();
+    return v;
+}
+
+// K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
 // Outputs: segment seg_cap per block of the path queue (bounce 1) and the
 // shadow queue (bounce 0), lengths published in seg_c / seg_s.
-template <bool kCount>
-__global__ __launch_bounds__(kBlock) void k_primary(FrameConsts fc, LightsMats lm, const BvhNode* __restrict__ nodes,
-                                                    const TriPack* __restrict__ tris, int np,
-                                                    float4* __restrict__ rad, PathQueue out, ShadowQueue sq,
-                                                    uint32_t seg_cap, uint32_t* __restrict__ seg_c,
-                                                    uint32_t* __restrict__ seg_s, int32_t* __restrict__ spill,
-                                                    unsigned long long* __restrict__ tc) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
-    __shared__ QueueLds ql;
+template <bool kCount, typename View>
+RR_D void primary_body(const FrameConsts& fc, const View& v, int np, float4* __restrict__ rad, PathQueue out,
+                       ShadowQueue sq, uint32_t seg_cap, uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
+                       int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
+    TravStack st{stack, spill + gtid, stride, 0};
     TravCount cnt;
     SegCursor cur;
-    const uint32_t seg_base = blockIdx.x * seg_cap;
+    const uint32_t seg_base = wave_id() * seg_cap;
     for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {  // block-uniform trip count
         const int p = b0 + (int)threadIdx.x;
         ShadeOut so;
         so.cont = so.shadow = false;
         if (p < np) {
-            const int sl = p / fc.npix;
+            const int sl = (int)fc.div_npix.div((uint32_t)p);
             const int pix = p - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             float3 o, d;
             float tmin, tmax;
-            camera_ray(fc, lm.filter, pix, key, o, d, tmin, tmax);
+            camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax);
             Hit h;
-            traverse<false, kCount>(nodes, tris, fc.n_tris, o, d, tmin, tmax, st, h, cnt);
+            traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, tmin, tmax, st, h, cnt);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
-            shade(fc, 0, lm, tris, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
+            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
             rad[p] = make_float4(L.x, L.y, L.z, 0.0f);
         }
-        emit(so, p, out, sq, seg_base, cur, ql);
+        emit(so, p, out, sq, seg_base, cur);
     }
     publish(cur, seg_c, seg_s);
     if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
 }
 
+template <bool kCount, bool kLds>
+__global__ __launch_bounds__(kBlock) void k_primary(FrameConsts fc, SceneArgs sa, int np, float4* __restrict__ rad,
+                                                    PathQueue out, ShadowQueue sq, uint32_t seg_cap,
+                                                    uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
+                                                    int32_t* __restrict__ spill,
+                                                    unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    if constexpr (kLds) {
+        extern __shared__ float4 dyn4[];
+        int used;
+        const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used);
+        primary_body<kCount>(fc, v, np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack);
+    } else {
+        primary_body<kCount>(fc, global_view(sa), np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack);
+    }
+}
+
 // K-extend: closest hit + shade of bounce b >= 1 over the path queue of the
 // previous bounce (segments in_seg[0..in_nseg) of capacity in_cap).
-template <bool kCount>
-__global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, LightsMats lm,
-                                                   const BvhNode* __restrict__ nodes,
-                                                   const TriPack* __restrict__ tris, PathQueue in,
-                                                   const uint32_t* __restrict__ in_seg, int in_nseg, uint32_t in_cap,
-                                                   uint32_t* __restrict__ in_total, float4* __restrict__ rad,
-                                                   PathQueue out, ShadowQueue sq, uint32_t seg_cap,
-                                                   uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
-                                                   int32_t* __restrict__ spill, unsigned long long* __restrict__ tc) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
-    __shared__ QueueLds ql;
-    extern __shared__ uint32_t dyn_pre[];
-    const SegIndex ix{(lds_uint*)dyn_pre, in_nseg, in_cap};
-    const int count = (int)seg_prefix(in_seg, in_nseg, ix.pre, in_total);
+struct SegIn {
+    const uint32_t* seg;
+    int nseg;
+    uint32_t cap;
+    uint32_t* total;  // block 0 records the queue length here (ray statistics)
+};
+struct SegOut {
+    uint32_t cap;
+    uint32_t* seg_c;
+    uint32_t* seg_s;
+};
+
+template <bool kCount, typename View>
+RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueue in, const SegIndex& ix, int count,
+                      float4* __restrict__ rad, PathQueue out, ShadowQueue sq, const SegOut& so_seg,
+                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
+    TravStack st{stack, spill + gtid, stride, 0};
     TravCount cnt;
     SegCursor cur;
-    const uint32_t seg_base = blockIdx.x * seg_cap;
+    const uint32_t seg_base = wave_id() * so_seg.cap;
     int pid = 0;
     for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
         const int j = b0 + (int)threadIdx.x;
@@ -421,35 +472,48 @@ __global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, L
             pid = f2i(a.w);
             const float3 o = xyz(a), d = xyz(b);
             Hit h;
-            traverse<false, kCount>(nodes, tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
-            const int sl = pid / fc.npix;
+            traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
+            const int sl = (int)fc.div_npix.div((uint32_t)pid);
             const int pix = pid - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             const float4 L4 = rad[pid];
             float3 L = xyz(L4);
-            shade(fc, bounce, lm, tris, o, d, xyz(c), h, key, L, so);
+            shade(fc, bounce, v, o, d, xyz(c), h, key, L, so);
             rad[pid] = make_float4(L.x, L.y, L.z, 0.0f);
         }
-        emit(so, pid, out, sq, seg_base, cur, ql);
+        emit(so, pid, out, sq, seg_base, cur);
     }
-    publish(cur, seg_c, seg_s);
+    publish(cur, so_seg.seg_c, so_seg.seg_s);
     if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
 }
 
-// K10: shadow rays of one bounce; unoccluded -> radiance += contribution.
-template <bool kCount>
-__global__ __launch_bounds__(kBlock) void k_shadow(const BvhNode* __restrict__ nodes,
-                                                   const TriPack* __restrict__ tris, int n_tris, ShadowQueue sq,
-                                                   const uint32_t* __restrict__ in_seg, int in_nseg, uint32_t in_cap,
-                                                   uint32_t* __restrict__ in_total, float4* __restrict__ rad,
-                                                   int32_t* __restrict__ spill, unsigned long long* __restrict__ tc) {
+template <bool kCount, bool kLds>
+__global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in, SegIn si,
+                                                   float4* __restrict__ rad, PathQueue out, ShadowQueue sq,
+                                                   SegOut sg, int32_t* __restrict__ spill,
+                                                   unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
-    extern __shared__ uint32_t dyn_pre[];
-    const SegIndex ix{(lds_uint*)dyn_pre, in_nseg, in_cap};
-    const int count = (int)seg_prefix(in_seg, in_nseg, ix.pre, in_total);
+    extern __shared__ float4 dyn4[];
+    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    int used = 0;
+    LdsView lv;
+    if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, true, used);
+    const SegIndex ix{(lds_uint*)((lds_f4w*)dyn4 + used), si.nseg, si.cap};
+    const int count = (int)seg_prefix(si.seg, si.nseg, ix.pre, si.total);
+    if constexpr (kLds)
+        extend_body<kCount>(fc, bounce, lv, in, ix, count, rad, out, sq, sg, spill, tc, stack);
+    else
+        extend_body<kCount>(fc, bounce, global_view(sa), in, ix, count, rad, out, sq, sg, spill, tc, stack);
+}
+
+// K10: shadow rays of one bounce; unoccluded -> radiance += contribution.
+template <bool kCount, typename NodeP, typename TriP>
+RR_D void shadow_body(NodeP nodes, TriP tris, int n_tris, ShadowQueue sq, const SegIndex& ix, int count,
+                      float4* __restrict__ rad, int32_t* __restrict__ spill, unsigned long long* __restrict__ tc,
+                      lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, stride, 0};
+    TravStack st{stack, spill + gtid, stride, 0};
     TravCount cnt;
     for (int j = gtid; j < count; j += stride) {
         const uint32_t i = ix.slot((uint32_t)j);
@@ -466,6 +530,23 @@ __global__ __launch_bounds__(kBlock) void k_shadow(const BvhNode* __restrict__ n
         }
     }
     if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
+}
+
+template <bool kCount, bool kLds>
+__global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq, SegIn si, float4* __restrict__ rad,
+                                                   int32_t* __restrict__ spill, unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    extern __shared__ float4 dyn4[];
+    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    int used = 0;
+    LdsView lv;
+    if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, false, used);
+    const SegIndex ix{(lds_uint*)((lds_f4w*)dyn4 + used), si.nseg, si.cap};
+    const int count = (int)seg_prefix(si.seg, si.nseg, ix.pre, si.total);
+    if constexpr (kLds)
+        shadow_body<kCount>(lv.nodes, lv.tris, sa.n_tris, sq, ix, count, rad, spill, tc, stack);
+    else
+        shadow_body<kCount>(sa.nodes, sa.tris, sa.n_tris, sq, ix, count, rad, spill, tc, stack);
 }
 
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
@@ -536,6 +617,11 @@ int device_cu_count() {
 int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2); }
 
 namespace {
+using PrimaryFn = void (*)(FrameConsts, SceneArgs, int, float4*, PathQueue, ShadowQueue, uint32_t, uint32_t*,
+                           uint32_t*, int32_t*, unsigned long long*);
+using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, float4*, PathQueue, ShadowQueue, SegOut,
+                          int32_t*, unsigned long long*);
+using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, float4*, int32_t*, unsigned long long*);
 // Persistent grid = resident blocks: CUs x blocks per CU the kernel's register
 // and LDS budget admits (a grid-stride loop over more blocks than fit would
 // only queue the surplus behind the first wave of blocks).
@@ -546,22 +632,57 @@ int resident_grid(K kernel, size_t dyn_lds = 0) {
         per_cu = 4;
     return device_cu_count() * std::min(per_cu, kMaxBlocksPerCu);
 }
-// Consumers hold the producer's segment prefix in dynamic LDS: one word per
-// producer block + 1. Producers are k_primary and k_extend; giving k_extend
-// that LDS can only shrink its grid, so dyn_lds bounds both.
+// Resident grid per (kernel, dynamic LDS bytes), cached.
+template <typename K>
+int grid_for(K kernel, size_t dyn_lds) {
+    static std::map<std::pair<const void*, size_t>, int> cache;
+    const auto key = std::make_pair(reinterpret_cast<const void*>(kernel), dyn_lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    return cache[key] = resident_grid(kernel, dyn_lds);
+}
+// Scene bytes staged in LDS (stage_scene), and the cap below which the path
+// kernels take the LDS-resident variant: at most ~12 KB next to the 16 KB
+// traversal stack and the <= 8 KB segment prefix keeps 4 blocks of the
+// register-limited kernels per CU.
+constexpr size_t kLdsSceneMax = 12 * 1024;
+size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
+    const int n_nodes = std::max(fc.n_tris - 1, 1);
+    size_t f4 = 4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris;
+    if (shading) f4 += 3 * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4;
+    return 16 * f4;
+}
+// Launch geometry of one frame's path kernels.
 struct Grids {
-    int primary, extend, shadow, accum;
-    size_t dyn_lds;
-    Grids() {
-        primary = resident_grid(k_primary<false>);
-        dyn_lds = sizeof(uint32_t) * (size_t)(std::max(primary, resident_grid(k_extend<false>)) + 1);
-        extend = resident_grid(k_extend<false>, dyn_lds);
-        shadow = resident_grid(k_shadow<false>, dyn_lds);
-        accum = resident_grid(k_accumulate);
+    bool lds;
+    int primary, extend, shadow;
+    size_t dyn_primary, dyn_extend, dyn_shadow;
+    PrimaryFn kp;
+    ExtendFn ke;
+    ShadowFn ks;
+    Grids(const FrameConsts& fc, bool count) {
+        lds = fc.n_tris > 0 && scene_lds_bytes(fc, true) <= kLdsSceneMax;
+        kp = lds ? (count ? k_primary<true, true> : k_primary<false, true>)
+                 : (count ? k_primary<true, false> : k_primary<false, false>);
+        ke = lds ? (count ? k_extend<true, true> : k_extend<false, true>)
+                 : (count ? k_extend<true, false> : k_extend<false, false>);
+        ks = lds ? (count ? k_shadow<true, true> : k_shadow<false, true>)
+                 : (count ? k_shadow<true, false> : k_shadow<false, false>);
+        const size_t sp = lds ? scene_lds_bytes(fc, true) : 0, ss = lds ? scene_lds_bytes(fc, false) : 0;
+        dyn_primary = sp;
+        primary = grid_for(kp, dyn_primary);
+        // consumers hold the producer's segment prefix after the scene: one word
+        // per producer block + 1; more LDS can only shrink k_extend's grid, so
+        // the bound taken without the prefix covers the grid taken with it.
+        const size_t pre = sizeof(uint32_t) * (size_t)(kWavesPerBlock * std::max(primary, grid_for(ke, sp)) + 1);
+        dyn_extend = sp + pre;
+        dyn_shadow = ss + pre;
+        extend = grid_for(ke, dyn_extend);
+        shadow = grid_for(ks, dyn_shadow);
     }
 };
-const Grids& grids() {
-    static Grids g;
+int accum_grid() {
+    static const int g = resident_grid(k_accumulate);
     return g;
 }
 inline int clamp_grid(long work, int resident) {
@@ -569,17 +690,17 @@ inline int clamp_grid(long work, int resident) {
     return (int)std::max<long>(1, std::min<long>(g, resident));
 }
 // Segment capacity of a producer launched with `grid` blocks over at most
-// `work` items: the most any one block can emit.
+// `work` items: the most any one wave can emit.
 inline uint32_t seg_cap(long work, int grid) {
     const long stride = (long)grid * kBlock;
-    return (uint32_t)(((work + stride - 1) / stride) * kBlock);
+    return (uint32_t)(((work + stride - 1) / stride) * 64);
 }
 }  // namespace
 
 void DevPaths::ensure_paths(size_t n) {
     if (grid_blocks == 0) grid_blocks = device_cu_count() * kMaxBlocksPerCu;
     n += (size_t)grid_blocks * kBlock;  // segment round-up slack (seg_cap)
-    segs.ensure((size_t)4 * grid_blocks);
+    segs.ensure((size_t)4 * grid_blocks * kWavesPerBlock);
     if (n > cap) {
         for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                                   &sh_c})
@@ -609,7 +730,6 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     const int cpc = counters_per_chunk(base.max_bounces);
     p.counters.ensure((size_t)cpc * n_chunks);
     RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
-    LightsMats lm{p.lights.ptr, p.materials.ptr, p.filter_table.ptr, p.srgb_lut.ptr};
     unsigned long long* tc = nullptr;
     if (p.count_traversal) {
         p.trav_counts.ensure(6);
@@ -619,7 +739,9 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     KernelProfiler& pr = p.prof;
-    const Grids& G = grids();
+    const Grids G(base, tc != nullptr);
+    const SceneArgs sa{s.nodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
+                       std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
     for (int c = 0; c < n_chunks; ++c) {
         FrameConsts fc = base;
         fc.first_sample = c * base.spp_chunk;
@@ -627,34 +749,35 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         if (fc.first_sample + fc.spp_chunk > base.spp_total) fc.spp_chunk = base.spp_total - fc.first_sample;
         const int np = npix * fc.spp_chunk;
         // segment lengths, ping-pong by bounce parity: [parity][path | shadow][grid]
-        auto seg = [&](int b, int q) { return p.segs.ptr + ((size_t)(b & 1) * 2 + q) * p.grid_blocks; };
+        auto seg = [&](int b, int q) {
+            return p.segs.ptr + ((size_t)(b & 1) * 2 + q) * p.grid_blocks * kWavesPerBlock;
+        };
         uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr + (size_t)cpc * c);
-        const size_t dyn = G.dyn_lds;
         const int gp = clamp_grid(np, G.primary), ge = clamp_grid(np, G.extend), gs = clamp_grid(np, G.shadow);
         const uint32_t cap_p = seg_cap(np, gp), cap_e = seg_cap(np, ge);
         pr.begin(st, RR_K_PRIMARY);
-        (tc ? k_primary<true> : k_primary<false>)<<<gp, kBlock, 0, st>>>(
-            fc, lm, s.nodes.ptr, s.tris.ptr, np, p.rad.ptr, pq[1], sq, cap_p, seg(0, 0), seg(0, 1), p.spill.ptr, tc);
+        G.kp<<<gp, kBlock, G.dyn_primary, st>>>(fc, sa, np, p.rad.ptr, pq[1], sq, cap_p, seg(0, 0), seg(0, 1),
+                                                p.spill.ptr, tc);
         pr.end(st);
-        int g_prev = gp;        // grid of the producer of the current queues
+        int g_prev = gp;  // grid of the producer of the current queues
         uint32_t cap_prev = cap_p;
         for (int b = 0; b <= base.max_bounces; ++b) {
             if (b > 0) {
                 pr.begin(st, RR_K_EXTEND);
-                (tc ? k_extend<true> : k_extend<false>)<<<ge, kBlock, dyn, st>>>(
-                    fc, b, lm, s.nodes.ptr, s.tris.ptr, pq[b & 1], seg(b - 1, 0), g_prev, cap_prev,
-                    tot + 2 * (b - 1), p.rad.ptr, pq[(b + 1) & 1], sq, cap_e, seg(b, 0), seg(b, 1), p.spill.ptr, tc);
+                G.ke<<<ge, kBlock, G.dyn_extend, st>>>(fc, b, sa, pq[b & 1],
+                                                       SegIn{seg(b - 1, 0), g_prev * kWavesPerBlock, cap_prev, tot + 2 * (b - 1)},
+                                                       p.rad.ptr, pq[(b + 1) & 1], sq,
+                                                       SegOut{cap_e, seg(b, 0), seg(b, 1)}, p.spill.ptr, tc);
                 pr.end(st);
                 g_prev = ge;
                 cap_prev = cap_e;
             }
             pr.begin(st, RR_K_SHADOW);
-            (tc ? k_shadow<true> : k_shadow<false>)<<<gs, kBlock, dyn, st>>>(
-                s.nodes.ptr, s.tris.ptr, s.n_tris, sq, seg(b, 1), g_prev, cap_prev, tot + 2 * b + 1, p.rad.ptr,
-                p.spill.ptr, tc);
+            G.ks<<<gs, kBlock, G.dyn_shadow, st>>>(sa, sq, SegIn{seg(b, 1), g_prev * kWavesPerBlock, cap_prev, tot + 2 * b + 1},
+                                                   p.rad.ptr, p.spill.ptr, tc);
             pr.end(st);
         }
-        const int ga = clamp_grid(npix, G.accum);
+        const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, p.rad.ptr, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
