@@ -50,31 +50,35 @@ def parse_args():
     return ap.parse_args()
 
 
-def algorithmic_bytes(cls: str, stats, max_bounces: int) -> float:
-    """Algorithmic HBM bytes of one kernel class over a frame (DESIGN.md §7).
-    Uses the per-frame ray counts and, for traversal, the counted node / triangle
-    visits (64 B per BVH node, 48 B per packed triangle)."""
+def algorithmic_bytes(cls: str, stats, scene_bytes: float) -> tuple[float, float]:
+    """Algorithmic HBM bytes of one kernel class over a frame (DESIGN.md §4, §6).
+
+    Returns (compulsory, survey): `compulsory` is the stream every launch must
+    move through HBM (radiance records, queue entries, film) plus the scene's
+    BVH and triangles read once; `survey` is SURVEY.md §8(d)'s literal figure,
+    which prices every counted node visit (64 B) and triangle test (48 B) as
+    HBM traffic even when the scene is cache/LDS resident."""
     npaths = stats.camera_rays
     ext = stats.extension_rays
     sh = stats.shadow_rays
     c0, s0 = stats.primary_continued, stats.primary_shadow
-    node, tri = 64.0, 48.0  # one BVH2 node line, one packed triangle
+    node, tri = 64.0, 48.0
     if cls == "primary":
-        # radiance record write 16 B per camera path; compacted writes of the
-        # continuing state (48 B) and shadow entries (48 B); BVH/triangle reads;
-        # the hit triangle re-read by shading (lower bound: max(continued, shadowed))
-        return (npaths * 16.0 + c0 * 48.0 + s0 * 48.0 + node * stats.trav_nodes[0] + tri * stats.trav_tris[0]
-                + tri * max(c0, s0))
-    if cls == "extend":
+        stream = npaths * 16.0 + c0 * 48.0 + s0 * 48.0
+        trav = node * stats.trav_nodes[0] + tri * stats.trav_tris[0] + tri * max(c0, s0)
+    elif cls == "extend":
         ce, se = ext - c0, sh - s0
-        return (ext * (48.0 + 32.0) + ce * 48.0 + se * 48.0 + node * stats.trav_nodes[1]
-                + tri * stats.trav_tris[1] + tri * max(ce, se))
-    if cls == "shadow":
-        return sh * (48.0 + 32.0) + node * stats.trav_nodes[2] + tri * stats.trav_tris[2]
-    if cls == "accumulate":
+        stream = ext * (48.0 + 32.0) + ce * 48.0 + se * 48.0
+        trav = node * stats.trav_nodes[1] + tri * stats.trav_tris[1] + tri * max(ce, se)
+    elif cls == "shadow":
+        stream = sh * (48.0 + 32.0)
+        trav = node * stats.trav_nodes[2] + tri * stats.trav_tris[2]
+    elif cls == "accumulate":
         npix = stats.width * stats.height
-        return npix * (stats.spp * 16.0 + 32.0 * max(stats.chunks - 1, 0) + 16.0 + 4.0)
-    return 0.0
+        return (npix * (stats.spp * 16.0 + 32.0 * max(stats.chunks - 1, 0) + 16.0 + 4.0),) * 2
+    else:
+        return 0.0, 0.0
+    return stream + min(trav, scene_bytes), stream + trav
 
 
 KERNEL_OF_CLASS = {"build": None, "primary": "k_primary", "extend": "k_extend", "shadow": "k_shadow",
@@ -203,17 +207,23 @@ def main():
         if not args.no_profile:
             dom = max(range(len(names)), key=lambda k: kernel_ms[k])
             cls = names[dom]
-            bytes_frame = algorithmic_bytes(cls, cstats, 12)
+            n = int(cstats.n_triangles)
+            scene_bytes = 64.0 * max(n - 1, 1) + 48.0 * n
+            bytes_frame, survey_frame = algorithmic_bytes(cls, cstats, scene_bytes)
             launches_frame = max(launches[dom] / max(args.steps, 1), 1)
             avg_ms = kernel_ms[dom] / max(launches[dom], 1)
             per_launch = bytes_frame / launches_frame
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
+            survey_achieved = survey_frame / launches_frame / (avg_ms * 1e-3) / 1e9
             tr = pmc_traffic(cls, args.pmc_summary)
             roofline = {"bound": "hbm", "kernel": cls, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                         "traffic": round(tr["bytes"]) if tr else None,
                         "traffic_source": tr["source"] if tr else None,
-                        "bytes_per_launch": round(per_launch), "avg_launch_ms": round(avg_ms, 4)}
+                        "bytes_per_launch": round(per_launch), "avg_launch_ms": round(avg_ms, 4),
+                        "achieved_survey_formula": round(survey_achieved, 2),
+                        "note": "achieved = compulsory bytes (stream + scene once); the SURVEY 8(d) formula "
+                                "also prices cache/LDS-resident node and triangle reads"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
