@@ -34,20 +34,55 @@ PKG = "diploma_thesis-distributed_rendering_of_cgi_using_a_render_cluster_amd"
 
 METRIC = "job frames/sec at 1/2/4/8 MI355X (04_very-simple); Mrays/s per GPU"
 JOB = os.path.join(ROOT, "jobs", "04_very-simple_demo_10f-1w.toml")
+# --workload: the default is BASELINE.json's metric config (configs[1], 04vs on
+# one MI355X); the others are the C4/C5 configs, reported in DESIGN.md/profiles.
+WORKLOADS = {
+    "04vs": {"job": JOB, "metric": METRIC, "steps": 10, "warmup": 2,
+             "data": "synthetic: 04_very-simple stand-in scene (01_simple-animation content; the 04 .blend is "
+                     "missing from the reference), frames of the 04vs demo job, JPEG q90 written per frame",
+             "workload": "04vs-standin, 1 frame per step: 1920x1080, 128 spp, max 12 bounces, "
+                         "LBVH rebuild + wavefront path trace + JPEG q90 encode/write"},
+    "02": {"job": os.path.join(ROOT, "jobs", "02_physics-standin_170f-5w_naive-fine.toml"),
+           "metric": "job frames/sec at 1/2/4/8 MI355X (02_physics stand-in)", "steps": 10, "warmup": 2,
+           "data": "synthetic: 02_physics stand-in (2,000 closed-form rigid bodies, 92,002 triangles; the 02 .blend "
+                   "is missing from the reference), PNG written per frame",
+           "workload": "02-physics-standin, 1 frame per step: 1920x1080, 64 spp, max 8 bounces, full LBVH "
+                       "rebuild every frame + wavefront path trace + PNG encode/write"},
+    "03": {"job": os.path.join(ROOT, "jobs", "03_physics-2-standin_480f-8w_dynamic.toml"),
+           "metric": "job frames/sec at 1/2/4/8 MI355X (03_physics-2 stand-in)", "steps": 10, "warmup": 2,
+           "data": "synthetic: 03_physics-2 stand-in (3,000 closed-form rigid bodies, 412,002 triangles), JPEG q90",
+           "workload": "03-physics-2-standin, 1 frame per step: 1920x1080, 64 spp, max 8 bounces, full LBVH "
+                       "rebuild every frame + wavefront path trace + JPEG q90 encode/write"},
+    "c5": {"job": os.path.join(ROOT, "jobs", "c5_synthetic-10m_240f-8w_dynamic.toml"),
+           "metric": "job frames/sec at 1/2/4/8 MI355X (C5 synthetic 10M triangles, 4K, 1024 spp)",
+           "steps": 2, "warmup": 1,
+           "data": "synthetic: 512 displaced icospheres x 20,480 triangles + ground (10,485,762 triangles), "
+                   "per-instance rigid motion, JPEG q90",
+           "workload": "c5-synthetic-10m, 1 frame per step: 3840x2160, 1024 spp, max 4 bounces, full LBVH "
+                       "rebuild every frame + wavefront path trace + JPEG q90 encode/write"},
+}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None, help="default: 10 (2 for c5)")
+    ap.add_argument("--warmup", type=int, default=None, help="default: 2 (1 for c5)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="04vs")
+    ap.add_argument("--spp", type=int, default=0, help="override the scene's samples (0 = scene)")
     ap.add_argument("--no-profile", action="store_true", help="time without per-kernel HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r1_pmc.json"),
                     help="PMC traffic summary for roofline.traffic (tools/pmc_summary.py)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    wl = WORKLOADS[a.workload]
+    if a.steps is None:
+        a.steps = wl["steps"]
+    if a.warmup is None:
+        a.warmup = wl["warmup"]
+    return a
 
 
 def algorithmic_bytes(cls: str, stats, scene_bytes: float) -> tuple[float, float]:
@@ -115,7 +150,7 @@ def reduce_max_seconds(elapsed: float, dist=None, device="cpu") -> float:
     return float(t.item())
 
 
-def cpu_baseline(oracle_mod, state, budget_s: float):
+def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin frame 1"):
     """Oracle (C restatement, OpenMP) on the host cores: evenly spread 4-row bands
     of the same frame until the budget is spent, extrapolated to frames/s."""
     H = int(state.render_ints[1])
@@ -132,7 +167,7 @@ def cpu_baseline(oracle_mod, state, budget_s: float):
             break
     frac = done_rows / H
     return {"value": frac / t_used, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{done_rows} of {H} rows (4-row bands spread over the frame) of 04vs-standin frame 1 "
+            "sample": f"{done_rows} of {H} rows (4-row bands spread over the frame) of {label} "
                       f"at {int(state.render_ints[0])}x{H}, {int(state.render_ints[2])} spp, "
                       f"{t_used:.1f} s, extrapolated to whole frames; render only (no encode)"}
 
@@ -162,12 +197,13 @@ def main():
             torch.cuda.synchronize()
 
     rr = importlib.import_module(PKG)
-    job = rr.BlenderJob.load_from_file(JOB)
+    wl = WORKLOADS[args.workload]
+    job = rr.BlenderJob.load_from_file(wl["job"])
     outdir = tempfile.mkdtemp(prefix=f"rr_bench_r{rank}_")
     job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": outdir})
     frames = job.frames()
     flags = 0 if args.no_profile else rr.native.RR_FLAG_PROFILE_KERNELS
-    runner = rr.BackendRunner(ROOT, device=local, params=rr.default_params(flags=flags))
+    runner = rr.BackendRunner(ROOT, device=local, params=rr.default_params(flags=flags, spp=args.spp))
 
     def frame_of(step):
         return frame_partition(frames, step, rank, world)
@@ -195,7 +231,7 @@ def main():
     scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, ROOT))
     f_count = frame_of(args.warmup)
     _, _, cstats = runner.ctx.render_to_memory(scene, f_count, rr.default_params(
-        flags=rr.native.RR_FLAG_COUNT_TRAVERSAL), film=False, rgba=True)
+        flags=rr.native.RR_FLAG_COUNT_TRAVERSAL, spp=args.spp), film=False, rgba=True)
 
     result = None
     if rank == 0:
@@ -228,19 +264,25 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             try:
                 from oracle import oracle as O
-                state = runner.ctx.frame_state(scene, 1)
-                cpu = cpu_baseline(O, state, args.cpu_seconds)
+                # the oracle renders at most 16 spp per sample and is scaled to
+                # the frame's spp (path cost is linear in spp)
+                spp_full = int(last_stats.spp)
+                spp_cpu = min(spp_full, 16)
+                state = runner.ctx.frame_state(scene, f_count, rr.default_params(spp=spp_cpu))
+                cpu = cpu_baseline(O, state, args.cpu_seconds,
+                                   f"{args.workload} frame {f_count} (each band call includes the oracle's BVH build)")
+                if spp_cpu != spp_full:
+                    cpu["value"] = cpu["value"] * spp_cpu / spp_full
+                    cpu["sample"] += f"; rendered at {spp_cpu} spp and scaled to {spp_full} spp"
             except Exception as e:  # baseline is reported, never the target
                 cpu = {"value": None, "unit": "frames/s", "error": str(e)}
         result = {
-            "metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world,
+            "metric": wl["metric"], "value": round(value, 4), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: 04_very-simple stand-in scene (01_simple-animation content; the 04 .blend is "
-                    "missing from the reference), frames of the 04vs demo job, JPEG q90 written per frame",
-            "config": {"workload": "04vs-standin, 1 frame per step: 1920x1080, 128 spp, max 12 bounces, "
-                                   "LBVH rebuild + wavefront path trace + JPEG q90 encode/write",
-                       "job": os.path.basename(JOB), "resolution": "1920x1080", "spp": int(last_stats.spp),
+            "data": wl["data"],
+            "config": {"workload": wl["workload"], "job": os.path.basename(wl["job"]),
+                       "resolution": f"{int(last_stats.width)}x{int(last_stats.height)}", "spp": int(last_stats.spp),
                        "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)"},
             "mrays_per_s_per_gpu": round(rays / elapsed / 1e6, 1),
             "device_ms_per_frame": round(sum(kernel_ms) / max(args.steps, 1), 3),

@@ -107,6 +107,22 @@ void gen_icosphere(MeshDesc& m, int subdiv, double radius) {
     m.mat_idx.assign(f.size() / 3, 0);
 }
 
+// Icosphere whose vertices are pushed along the normal by a smooth
+// deterministic field, r' = r (1 + amp sin(f x + 1.3) sin(f y + 0.7) sin(f z + 2.1))
+// on the unit sphere (the C5 synthetic scene's "displaced icospheres",
+// SURVEY.md §8d C5). Triangle count = 20 * 4^subdivisions.
+void gen_displaced_icosphere(MeshDesc& m, int subdiv, double radius, double amp, double freq) {
+    gen_icosphere(m, subdiv, 1.0);
+    for (size_t i = 0; i + 2 < m.verts.size(); i += 3) {
+        const double x = m.verts[i], y = m.verts[i + 1], z = m.verts[i + 2];
+        const double k = radius * (1.0 + amp * std::sin(freq * x + 1.3) * std::sin(freq * y + 0.7) *
+                                              std::sin(freq * z + 2.1));
+        m.verts[i] = (float)(x * k);
+        m.verts[i + 1] = (float)(y * k);
+        m.verts[i + 2] = (float)(z * k);
+    }
+}
+
 void parse_mesh(const Json& jm, MeshDesc& m) {
     m.name = jm.get_str("name", "");
     if (jm.has("generator")) {
@@ -115,6 +131,9 @@ void parse_mesh(const Json& jm, MeshDesc& m) {
         if (t == "cube") gen_cube(m, g.get_num("size", 2.0));
         else if (t == "plane") gen_plane(m, g.get_num("size", 2.0));
         else if (t == "icosphere") gen_icosphere(m, (int)g.get_num("subdivisions", 2), g.get_num("radius", 1.0));
+        else if (t == "displaced_icosphere")
+            gen_displaced_icosphere(m, (int)g.get_num("subdivisions", 3), g.get_num("radius", 1.0),
+                                    g.get_num("amplitude", 0.15), g.get_num("frequency", 5.0));
         else throw std::runtime_error("unknown mesh generator: " + t);
     } else {
         const Json& v = jm["vertices"];
@@ -388,6 +407,131 @@ void local_matrix(const ObjectDesc& o, double frame, double m[16]) {
 
 double clamp01d(double x) { return x < 0 ? 0 : (x > 1 ? 1 : x); }
 
+// ---- rigid-body stand-ins (RigidMotion, scene.hpp) --------------------------
+// splitmix64 stream per body: state = seed ^ (index * 0xD1B54A32D192ED03).
+struct SplitMix {
+    uint64_t s;
+    uint64_t next() {
+        s += 0x9E3779B97F4A7C15ull;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    double u01() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+
+// Pose at time t (seconds since frame_start): row-major 4x4 object_to_world.
+void rigid_matrix(const RigidMotion& r, double t, double m[16]) {
+    double travel = 0.0, zr = 0.0;  // weighted flight time, height above rest
+    const double trel = t - r.t_spawn;
+    const double g = r.gravity;
+    if (trel > 0.0) {
+        double z = r.p0[2] - r.ground_z - r.rest_height;
+        if (z < 0.0) z = 0.0;
+        double vz = r.v0[2], tt = trel, fac = 1.0;
+        double tau = (vz + std::sqrt(vz * vz + 2.0 * g * z)) / g;
+        int k = 0;
+        for (;;) {
+            if (tt <= tau) {
+                zr = z + vz * tt - 0.5 * g * tt * tt;
+                travel += fac * tt;
+                break;
+            }
+            travel += fac * tau;
+            tt -= tau;
+            const double vimp = g * tau - vz;
+            vz = r.restitution * vimp;
+            z = 0.0;
+            fac = fac * r.friction;
+            k += 1;
+            tau = 2.0 * vz / g;
+            if (k > r.max_bounces || vz < r.min_speed) {
+                zr = 0.0;
+                break;
+            }
+        }
+        if (zr < 0.0) zr = 0.0;
+    } else {
+        zr = r.p0[2] - r.ground_z - r.rest_height;
+    }
+    const double th = r.w * travel;
+    const double c = std::cos(th), sn = std::sin(th), oc = 1.0 - c;
+    const double x = r.axis[0], y = r.axis[1], z = r.axis[2];
+    const double R[9] = {c + x * x * oc,     x * y * oc - z * sn, x * z * oc + y * sn,
+                         y * x * oc + z * sn, c + y * y * oc,     y * z * oc - x * sn,
+                         z * x * oc - y * sn, z * y * oc + x * sn, c + z * z * oc};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) m[4 * i + j] = R[3 * i + j] * r.scale;
+    m[3] = r.p0[0] + r.v0[0] * travel;
+    m[7] = r.p0[1] + r.v0[1] * travel;
+    m[11] = r.ground_z + r.rest_height + zr;
+    m[12] = m[13] = m[14] = 0.0;
+    m[15] = 1.0;
+}
+
+// Expands one "rigid_bodies" group into `count` mesh objects (draw order per
+// body fixed: position xyz, scale, velocity xyz, axis xyz, spin, spawn time).
+void expand_rigid_group(const Json& g, const RenderDesc& rd, int n_meshes, std::vector<ObjectDesc>& out) {
+    const int count = (int)g["count"].as_num();
+    const uint64_t seed = (uint64_t)g.get_num("seed", 0);
+    std::vector<int> meshes;
+    for (const Json& x : g["meshes"].arr) meshes.push_back((int)x.as_num());
+    if (count < 0 || meshes.empty()) throw std::runtime_error("rigid_bodies: bad count or meshes");
+    for (int mi : meshes)
+        if (mi < 0 || mi >= n_meshes) throw std::runtime_error("rigid_bodies: mesh index out of range");
+    double c[3] = {0, 0, 5}, e[3] = {10, 10, 4}, sc[2] = {0.3, 0.6};
+    if (g.has("spawn_center")) vec3(g["spawn_center"], c);
+    if (g.has("spawn_extent")) vec3(g["spawn_extent"], e);
+    if (g.has("scale")) {
+        sc[0] = g["scale"][0].as_num();
+        sc[1] = g["scale"][1].as_num();
+    }
+    const double speed = g.get_num("speed", 1.0), vup = g.get_num("up_speed", 1.0), spin = g.get_num("spin", 2.0);
+    double win[2] = {(double)rd.frame_start, (double)rd.frame_start};
+    if (g.has("spawn_window")) {
+        win[0] = g["spawn_window"][0].as_num();
+        win[1] = g["spawn_window"][1].as_num();
+    }
+    const std::string prefix = g.get_str("name", "body");
+    for (int i = 0; i < count; ++i) {
+        SplitMix rng{seed ^ ((uint64_t)i * 0xD1B54A32D192ED03ull)};
+        ObjectDesc o;
+        o.name = prefix + "." + std::to_string(i);
+        o.type = OBJ_MESH;
+        o.mesh = meshes[(size_t)i % meshes.size()];
+        RigidMotion& r = o.motion;
+        r.on = 1;
+        for (int k = 0; k < 3; ++k) r.p0[k] = c[k] + (rng.u01() - 0.5) * e[k];
+        r.scale = sc[0] + rng.u01() * (sc[1] - sc[0]);
+        r.v0[0] = (rng.u01() - 0.5) * 2.0 * speed;
+        r.v0[1] = (rng.u01() - 0.5) * 2.0 * speed;
+        r.v0[2] = rng.u01() * vup;
+        double a[3];
+        for (int k = 0; k < 3; ++k) a[k] = rng.u01() * 2.0 - 1.0;
+        double l = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        if (l < 1e-6) {
+            a[0] = 0.0; a[1] = 0.0; a[2] = 1.0; l = 1.0;
+        }
+        for (int k = 0; k < 3; ++k) r.axis[k] = a[k] / l;
+        r.w = spin * (0.5 + rng.u01());
+        const double f = win[0] + rng.u01() * (win[1] - win[0]);
+        r.t_spawn = (f - rd.frame_start) / rd.fps;
+        r.gravity = g.get_num("gravity", 9.81);
+        r.restitution = g.get_num("restitution", 0.5);
+        r.friction = g.get_num("friction", 0.7);
+        r.ground_z = g.get_num("ground_z", 0.0);
+        r.rest_height = r.scale * g.get_num("mesh_half_height", 1.0);
+        r.min_speed = g.get_num("min_speed", 0.05);
+        r.max_bounces = (int)g.get_num("max_bounces", 8);
+        for (int k = 0; k < 3; ++k) {
+            o.loc[k] = r.p0[k];
+            o.scale[k] = r.scale;
+        }
+        out.push_back(std::move(o));
+    }
+}
+
 }  // namespace
 
 float eval_fcurve(const FCurve& fc, float evaltime) {
@@ -400,7 +544,9 @@ float eval_fcurve(const FCurve& fc, float evaltime) {
 void object_matrix(const SceneDesc& s, int obj, double frame, double m[16]) {
     if (obj < 0 || obj >= (int)s.objects.size()) throw std::runtime_error("object index out of range");
     const ObjectDesc& o = s.objects[obj];
-    if (o.baked_frames > 0) {
+    if (o.motion.on) {
+        rigid_matrix(o.motion, (frame - s.render.frame_start) / s.render.fps, m);
+    } else if (o.baked_frames > 0) {
         long f = (long)std::floor(frame) - o.baked_start;
         if (f < 0) f = 0;
         if (f >= o.baked_frames) f = o.baked_frames - 1;
@@ -416,7 +562,7 @@ void object_matrix(const SceneDesc& s, int obj, double frame, double m[16]) {
         if (++guard > 64) throw std::runtime_error("parent cycle");
         double pm[16];
         const ObjectDesc& po = s.objects[p];
-        if (po.baked_frames > 0) {
+        if (po.baked_frames > 0 || po.motion.on) {
             double tmp[16];
             object_matrix(s, p, frame, tmp);
             mat_mul(tmp, m, m);
@@ -601,6 +747,11 @@ SceneDesc load_scene(const std::string& path) {
         }
         s.objects.push_back(o);
     }
+    if (j.has("rigid_bodies"))
+        for (const Json& g : j["rigid_bodies"].arr) {
+            expand_rigid_group(g, s.render, (int)s.meshes.size(), s.objects);
+            s.animated = true;
+        }
     for (size_t i = 0; i < s.objects.size(); ++i) {
         const int p = s.objects[i].parent;
         if (p >= (int)s.objects.size() || p == (int)i) throw std::runtime_error("bad parent index");

@@ -50,6 +50,23 @@ struct LightDesc {
     double radius = 0.0;
 };
 
+// Closed-form rigid-body motion of the physics stand-ins (SURVEY.md §8d C4/C5:
+// the 02/03 .blend files and their simulation caches are missing from the
+// reference, .MISSING_LARGE_BLOBS). A body hangs at p0 until t_spawn, then
+// flies ballistically (gravity g) and bounces on the ground plane z = ground_z
+// with restitution e; every bounce scales its horizontal and angular travel
+// rate by `friction`; it rests after max_bounces or below min_speed. The pose
+// is a pure function of the frame, so frames stay independent. Expanded from
+// a scene's "rigid_bodies" groups at load; restated in oracle/host_oracle.py.
+struct RigidMotion {
+    int on = 0;
+    double p0[3] = {0, 0, 0}, v0[3] = {0, 0, 0}, axis[3] = {0, 0, 1};
+    double w = 0.0, scale = 1.0, t_spawn = 0.0;
+    double gravity = 9.81, restitution = 0.5, friction = 0.7, ground_z = 0.0, rest_height = 1.0;
+    double min_speed = 0.05;
+    int max_bounces = 8;
+};
+
 struct ObjectDesc {
     std::string name;
     int type = OBJ_EMPTY;
@@ -66,6 +83,7 @@ struct ObjectDesc {
     int baked_start = 0;
     int baked_frames = 0;
     std::vector<float> baked;
+    RigidMotion motion;
 };
 
 struct MeshDesc {

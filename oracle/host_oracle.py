@@ -11,6 +11,13 @@ tests/ to compare the product (C++ in librr.so, Python in the package) against:
                        SURVEY.md §8c) and the saved ob.loc.z at cfra=60.
   * object_matrix      Blender loc / XYZ-Euler / scale object matrix.
   * frame_constants    camera / light / material constants the integrator reads.
+  * rigid_matrix / expand_rigid_bodies
+                       closed-form rigid-body poses of the physics stand-ins
+                       (C4/C5; the reference's 02/03 .blend
+                       files and simulation caches are missing,
+                       .MISSING_LARGE_BLOBS), restating csrc/scene.cpp's
+                       generator so the product's poses are checked against an
+                       independent statement of the same model.
   * parse_blender_stdout  worker/src/rendering/runner/utilities.rs:105-203
                        (extract_blender_render_information) and :51-96.
 """
@@ -175,6 +182,104 @@ def object_matrix(obj: dict, frame: float) -> np.ndarray:
     M = np.eye(4)
     M[:3, :3] = R * np.array(scl)[None, :]
     M[:3, 3] = loc
+    return M
+
+
+# ------------------------------------------------------ rigid bodies ----
+_M64 = (1 << 64) - 1
+
+
+class _SplitMix:
+    def __init__(self, state: int):
+        self.s = state & _M64
+
+    def next(self) -> int:
+        self.s = (self.s + 0x9E3779B97F4A7C15) & _M64
+        z = self.s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+        return z ^ (z >> 31)
+
+    def u01(self) -> float:
+        return (self.next() >> 11) * (1.0 / 9007199254740992.0)
+
+
+def expand_rigid_bodies(scene: dict) -> list:
+    """The motion parameters of every body of every "rigid_bodies" group, in
+    object order after the scene's explicit objects."""
+    r = scene["render"]
+    fps, f0 = float(r.get("fps", 24)), float(r.get("frame_start", 1))
+    out = []
+    for g in scene.get("rigid_bodies", []):
+        c = [float(x) for x in g.get("spawn_center", [0, 0, 5])]
+        e = [float(x) for x in g.get("spawn_extent", [10, 10, 4])]
+        sc = [float(x) for x in g.get("scale", [0.3, 0.6])]
+        speed, vup, spin = float(g.get("speed", 1.0)), float(g.get("up_speed", 1.0)), float(g.get("spin", 2.0))
+        win = [float(x) for x in g.get("spawn_window", [f0, f0])]
+        meshes = g["meshes"]
+        for i in range(int(g["count"])):
+            rng = _SplitMix(int(g.get("seed", 0)) ^ ((i * 0xD1B54A32D192ED03) & _M64))
+            p0 = [c[k] + (rng.u01() - 0.5) * e[k] for k in range(3)]
+            scale = sc[0] + rng.u01() * (sc[1] - sc[0])
+            v0 = [(rng.u01() - 0.5) * 2.0 * speed, (rng.u01() - 0.5) * 2.0 * speed, rng.u01() * vup]
+            a = [rng.u01() * 2.0 - 1.0 for _ in range(3)]
+            ln = math.sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2])
+            if ln < 1e-6:
+                a, ln = [0.0, 0.0, 1.0], 1.0
+            w = spin * (0.5 + rng.u01())
+            f = win[0] + rng.u01() * (win[1] - win[0])
+            out.append({"mesh": meshes[i % len(meshes)], "p0": p0, "v0": v0, "axis": [x / ln for x in a],
+                        "w": w, "scale": scale, "t_spawn": (f - f0) / fps,
+                        "gravity": float(g.get("gravity", 9.81)), "restitution": float(g.get("restitution", 0.5)),
+                        "friction": float(g.get("friction", 0.7)), "ground_z": float(g.get("ground_z", 0.0)),
+                        "rest_height": scale * float(g.get("mesh_half_height", 1.0)),
+                        "min_speed": float(g.get("min_speed", 0.05)), "max_bounces": int(g.get("max_bounces", 8))})
+    return out
+
+
+def rigid_matrix(m: dict, t: float) -> np.ndarray:
+    """Pose at t seconds after frame_start: hang until t_spawn, ballistic
+    flight, bounces with restitution, per-bounce friction on horizontal and
+    angular travel, rest."""
+    travel, zr = 0.0, 0.0
+    trel = t - m["t_spawn"]
+    g = m["gravity"]
+    if trel > 0.0:
+        z = max(m["p0"][2] - m["ground_z"] - m["rest_height"], 0.0)
+        vz, tt, fac = m["v0"][2], trel, 1.0
+        tau = (vz + math.sqrt(vz * vz + 2.0 * g * z)) / g
+        k = 0
+        while True:
+            if tt <= tau:
+                zr = z + vz * tt - 0.5 * g * tt * tt
+                travel += fac * tt
+                break
+            travel += fac * tau
+            tt -= tau
+            vimp = g * tau - vz
+            vz = m["restitution"] * vimp
+            z = 0.0
+            fac = fac * m["friction"]
+            k += 1
+            tau = 2.0 * vz / g
+            if k > m["max_bounces"] or vz < m["min_speed"]:
+                zr = 0.0
+                break
+        zr = max(zr, 0.0)
+    else:
+        zr = m["p0"][2] - m["ground_z"] - m["rest_height"]
+    th = m["w"] * travel
+    c, s = math.cos(th), math.sin(th)
+    oc = 1.0 - c
+    x, y, z = m["axis"]
+    R = np.array([[c + x * x * oc, x * y * oc - z * s, x * z * oc + y * s],
+                  [y * x * oc + z * s, c + y * y * oc, y * z * oc - x * s],
+                  [z * x * oc - y * s, z * y * oc + x * s, c + z * z * oc]], np.float64)
+    M = np.eye(4)
+    M[:3, :3] = R * m["scale"]
+    M[0, 3] = m["p0"][0] + m["v0"][0] * travel
+    M[1, 3] = m["p0"][1] + m["v0"][1] * travel
+    M[2, 3] = m["ground_z"] + m["rest_height"] + zr
     return M
 
 

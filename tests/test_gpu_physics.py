@@ -1,0 +1,152 @@
+"""Parity of the HIP path with the CPU oracle on the large-scene configs:
+the C4 physics stand-ins (02/03: thousands of rigid bodies, LBVH rebuilt every
+frame) and the C5 synthetic 10M-triangle scene. These scenes
+take the HBM (non-LDS) traversal path. Integer work (Morton keys, radix order,
+BVH topology, hit ids) and the float work are bit-exact (tolerance 0), as in
+test_gpu_parity.py. Full-size C5 is checked through size-independent
+properties: the whole 10M-triangle LBVH equals the oracle's, and a ray batch
+through it equals the oracle's traversal; images at reduced resolution/spp.
+"""
+import numpy as np
+import pytest
+
+from conftest import scene_path
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+S02 = scene_path("02_physics-standin.rrscene")
+S03 = scene_path("03_physics-2-standin.rrscene")
+SC5 = scene_path("c5_synthetic-10m.rrscene")
+
+
+@pytest.fixture(scope="module")
+def s02(ctx):
+    s = ctx.load_scene(S02)
+    yield s
+    s.close()
+
+
+def _camera_rays(st, n, rng):
+    """Rays from the camera through random sensor points, plus random
+    secondary rays from points near the geometry (upward hemisphere)."""
+    cam = st.camera
+    o = np.array(cam[0:3], np.float64)
+    right, up, back = np.array(cam[3:6]), np.array(cam[6:9]), np.array(cam[9:12])
+    sx = rng.uniform(-cam[12], cam[12], n // 2)
+    sy = rng.uniform(-cam[13], cam[13], n // 2)
+    d1 = right[None] * sx[:, None] + up[None] * sy[:, None] - back[None]
+    d1 /= np.linalg.norm(d1, axis=1, keepdims=True)
+    v = st.tris.reshape(-1, 3)
+    pick = v[rng.integers(0, len(v), n - n // 2)].astype(np.float64) + rng.normal(0, 0.05, (n - n // 2, 3))
+    d2 = rng.normal(0, 1, (n - n // 2, 3))
+    d2[:, 2] = np.abs(d2[:, 2])
+    d2 /= np.linalg.norm(d2, axis=1, keepdims=True)
+    r = np.zeros((n, 8), np.float32)
+    r[: n // 2, 0:3] = o
+    r[: n // 2, 4:7] = d1
+    r[n // 2:, 0:3] = pick
+    r[n // 2:, 4:7] = d2
+    r[:, 3] = 0.0
+    r[:, 7] = 1e30
+    return r
+
+
+@pytest.mark.parametrize("frame", [1, 45, 170])
+def test_physics_lbvh_bit_exact(ctx, s02, frame):
+    st = ctx.frame_state(s02, frame)
+    assert st.tris.shape[0] == 92002
+    keys, order, children, boxes = ctx.bvh(s02, frame)
+    ok, oo, oc, ob = O.build_lbvh(st.tris)
+    assert np.array_equal(keys, ok)
+    assert np.array_equal(order, oo)
+    assert np.array_equal(children, oc)
+    assert np.array_equal(boxes, ob)
+
+
+def test_physics_rebuilds_every_frame(ctx, rr, s02):
+    p = rr.default_params(width=32, height=18, spp=1)
+    rebuilt = []
+    for f in (40, 41, 42):
+        _, _, stats = ctx.render_to_memory(s02, f, p)
+        rebuilt.append(stats.bvh_rebuilt)
+        assert stats.n_triangles == 92002
+    assert rebuilt == [1, 1, 1]
+    _, _, stats = ctx.render_to_memory(s02, 42, p)  # same frame again: cached BVH
+    assert stats.bvh_rebuilt == 0
+
+
+def test_physics_trace_bit_exact(ctx, s02):
+    st = ctx.frame_state(s02, 90)
+    rays = _camera_rays(st, 40000, np.random.default_rng(7))
+    hits, prims, occ = ctx.trace(s02, 90, rays)
+    oh, op, oo = O.trace(st.tris, rays)
+    assert np.array_equal(prims, op), f"{np.count_nonzero(prims != op)} prim mismatches"
+    assert np.array_equal(hits, oh)
+    assert np.array_equal(occ, oo)
+    assert (prims >= 0).mean() > 0.3
+
+
+@pytest.mark.parametrize("path,frame,w,h,spp", [(S02, 1, 96, 54, 4), (S02, 90, 80, 45, 3), (S03, 300, 64, 36, 2)])
+def test_physics_full_frame_bit_exact(ctx, rr, path, frame, w, h, spp):
+    s = ctx.load_scene(path)
+    try:
+        p = rr.default_params(width=w, height=h, spp=spp)
+        film, rgba, stats = ctx.render_to_memory(s, frame, p)
+        st = ctx.frame_state(s, frame, p)
+    finally:
+        s.close()
+    of, orgba = O.render_state(st)
+    nbad = int(np.count_nonzero(rgba != orgba))
+    assert nbad == 0, f"{nbad} 8-bit mismatches"
+    assert np.array_equal(film, of), f"max film diff {np.max(np.abs(film - of))}"
+    assert stats.shadow_rays > 0 and stats.extension_rays > 0
+
+
+@pytest.fixture(scope="module")
+def sc5(ctx):
+    s = ctx.load_scene(SC5)
+    yield s
+    s.close()
+
+
+def test_c5_full_size_lbvh_bit_exact(ctx, sc5):
+    """All 10,485,762 triangles: Morton keys, radix order, topology and every
+    node's child boxes equal the oracle's build."""
+    st = ctx.frame_state(sc5, 120)
+    n = st.tris.shape[0]
+    assert n == 512 * 20480 + 2
+    keys, order, children, boxes = ctx.bvh(sc5, 120)
+    ok, oo, oc, ob = O.build_lbvh(st.tris)
+    assert np.array_equal(keys, ok)
+    assert np.array_equal(order, oo)
+    assert np.array_equal(children, oc)
+    assert np.array_equal(boxes, ob)
+    # structural properties: every leaf referenced once, every internal node but the root once
+    leaves = -children[children < 0] - 1
+    assert np.array_equal(np.sort(leaves), np.arange(n))
+    inner = children[children >= 0]
+    assert np.array_equal(np.sort(inner), np.arange(1, n - 1))
+
+
+def test_c5_trace_bit_exact(ctx, sc5):
+    st = ctx.frame_state(sc5, 200)
+    rays = _camera_rays(st, 100000, np.random.default_rng(11))
+    hits, prims, occ = ctx.trace(sc5, 200, rays)
+    oh, op, oo = O.trace(st.tris, rays)
+    assert np.array_equal(prims, op), f"{np.count_nonzero(prims != op)} prim mismatches"
+    assert np.array_equal(hits, oh)
+    assert np.array_equal(occ, oo)
+    assert (prims >= 0).mean() > 0.2
+
+
+def test_c5_frame_bit_exact_reduced(ctx, rr, sc5):
+    """C5 at reduced resolution and spp (the full 4K x 1024 spp frame is the
+    bench workload, not an oracle case)."""
+    p = rr.default_params(width=96, height=54, spp=2)
+    film, rgba, stats = ctx.render_to_memory(sc5, 150, p)
+    st = ctx.frame_state(sc5, 150, p)
+    of, orgba = O.render_state(st)
+    assert int(np.count_nonzero(rgba != orgba)) == 0
+    assert np.array_equal(film, of)
+    assert stats.n_triangles == 512 * 20480 + 2

@@ -135,3 +135,70 @@ def test_scene_validation(rr, tmp_path):
         with pytest.raises(rr.RRError) as e:
             rr.Scene(str(p))
         assert e.value.code == -22, d
+
+
+# ---- physics stand-ins (C4/C5) -------------------------------
+PHYS = [scene_path("02_physics-standin.rrscene"), scene_path("03_physics-2-standin.rrscene"),
+        scene_path("c5_synthetic-10m.rrscene")]
+
+
+@pytest.mark.parametrize("path", PHYS)
+def test_rigid_body_poses_match_restatement(rr, path):
+    """Product poses (C++ generator through the C ABI) == the Python
+    restatement, for a spread of bodies and frames (before spawn, in flight,
+    bouncing, at rest). Same IEEE double ops and libm on both sides."""
+    scene = HO.load_scene(path)
+    bodies = HO.expand_rigid_bodies(scene)
+    n_explicit = len(scene["objects"])
+    s = rr.Scene(path)
+    assert s.counts()["objects"] == n_explicit + len(bodies)
+    fps, f0 = scene["render"]["fps"], scene["render"]["frame_start"]
+    idx = sorted(set([0, 1, len(bodies) // 2, len(bodies) - 1] + list(range(0, len(bodies), max(1, len(bodies) // 37)))))
+    for b in idx:
+        for frame in (1, 2, 17, 60, 61.5, 119, 170, 240, 480, 2000):
+            got = s.object_matrix(n_explicit + b, frame)
+            want = HO.rigid_matrix(bodies[b], (frame - f0) / fps)
+            np.testing.assert_allclose(got, want, rtol=0, atol=1e-12, err_msg=f"body {b} frame {frame}")
+    s.close()
+
+
+def test_rigid_body_motion_is_physical():
+    """Bodies never sink below their rest height, fall under gravity after
+    spawning, and come to rest (pose constant) long after the last spawn."""
+    scene = HO.load_scene(PHYS[0])
+    bodies = HO.expand_rigid_bodies(scene)
+    assert len(bodies) == 2000
+    fps = scene["render"]["fps"]
+    for m in bodies[:200]:
+        rest = m["ground_z"] + m["rest_height"]
+        for f in range(1, 400, 7):
+            z = HO.rigid_matrix(m, (f - 1) / fps)[2, 3]
+            assert z >= rest - 1e-12
+        before = HO.rigid_matrix(m, m["t_spawn"] - 1e-3)
+        assert np.allclose(before[:3, 3], m["p0"])
+        late1, late2 = HO.rigid_matrix(m, 1e4), HO.rigid_matrix(m, 2e4)
+        assert np.array_equal(late1, late2)
+        assert late1[2, 3] == pytest.approx(rest)
+        # rotation part stays a scaled rotation
+        R = late1[:3, :3] / m["scale"]
+        np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-12)
+
+
+def test_physics_standins_animate_every_frame(rr):
+    """C4 requires a BVH rebuild per frame: consecutive frames inside the
+    spawn window change at least one body's transform."""
+    s = rr.Scene(PHYS[0])
+    n = s.counts()["objects"]
+    for f in (2, 30, 90, 119):
+        moved = any(not np.array_equal(s.object_matrix(i, f), s.object_matrix(i, f + 1)) for i in range(4, n, 50))
+        assert moved, f
+    s.close()
+
+
+def test_c5_scene_size(rr):
+    """C5 synthetic scene: 512 x 20,480 displaced-icosphere triangles + ground."""
+    s = rr.Scene(PHYS[2])
+    c = s.counts()
+    assert c["triangles"] == 512 * 20480 + 2
+    assert s.resolution() == (3840, 2160)
+    s.close()
