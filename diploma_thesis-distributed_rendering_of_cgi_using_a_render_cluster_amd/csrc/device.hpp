@@ -123,6 +123,8 @@ struct DevPaths {
     DevBuf<float4> rad;                        // per path (p-indexed) radiance record
     DevBuf<float4> ps_o[2], ps_d[2], ps_t[2];  // segmented path queue, ping-pong per bounce
     DevBuf<float4> sh_o, sh_d, sh_c;           // segmented shadow queue
+    DevBuf<float2> hits;                       // split path: (t, leaf index) per queue entry
+    DevBuf<uint32_t> qctr;                     // split path: grouped queue append counters
     DevBuf<uint32_t> segs;     // segment lengths [bounce parity][path | shadow][producer block]
     DevBuf<int32_t> counters;  // per chunk, per bounce b: {paths entering b+1, shadow rays of b}
     DevBuf<int32_t> spill;     // traversal stack spill

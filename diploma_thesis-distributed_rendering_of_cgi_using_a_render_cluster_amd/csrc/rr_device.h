@@ -222,6 +222,45 @@ RR_HD void closest_tri(const TriPack& tp, int idx, float3 o, float3 d, float tmi
     }
 }
 
+// closest_tri without early exits: the same IEEE op sequence as tri_test +
+// closest_tri (so identical t/u/v and the identical accept decision, NaN
+// cases included: the rejections are written as the negations of tri_test's
+// exit tests), but straight-line code, so the lanes of a wave that test
+// different triangles stay converged and a triangle's three loads go out
+// together (tri_test's exits split them into two dependent round trips).
+RR_HD void closest_tri_nb(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
+    const float3 v0 = xyz(tp.p0), e1 = xyz(tp.p1), e2 = xyz(tp.p2);
+    const float3 pv = cross3(d, e2);
+    const float det = dot3(e1, pv);
+    const float inv = 1.0f / det;
+    const float3 tv = sub3(o, v0);
+    const float u = dot3(tv, pv) * inv;
+    const float3 qv = cross3(tv, e1);
+    const float v = dot3(d, qv) * inv;
+    const float t = dot3(e2, qv) * inv;
+    const int orig = f2i(tp.p0.w);
+    const bool ok = !(det == 0.0f) && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && t > tmin &&
+                    (t < h.t || (t == h.t && orig < h.orig));
+    if (ok) {
+        h.t = t;
+        h.u = u;
+        h.v = v;
+        h.idx = idx;
+        h.orig = orig;
+    }
+}
+
+#ifndef RR_TRI_BRANCHLESS
+#define RR_TRI_BRANCHLESS 0
+#endif
+RR_HD void leaf_test(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
+#if RR_TRI_BRANCHLESS
+    closest_tri_nb(tp, idx, o, d, tmin, h);
+#else
+    closest_tri(tp, idx, o, d, tmin, h);
+#endif
+}
+
 // Traversal stack: kLdsStack entries in LDS ([entry][thread] -> conflict-free
 // ds_read_b32 across a wave), deeper entries in a per-thread HBM spill area.
 // The LDS pointer carries its address space explicitly so push/pop compile to
@@ -289,21 +328,33 @@ struct TravCount {
     uint32_t nodes = 0, tris = 0;
 };
 
-// Closest hit over the LBVH. Near child first (left on ties); leaf children are
-// intersected as soon as their box passes.
+// Resumable traversal of one ray: start() then step() until it returns true.
+// Near child first (left on ties); leaf children are intersected as soon as
+// their box passes. The fused path kernels run it to completion per lane
+// (traverse() below); the split trace kernels of large scenes interleave
+// step() with lane refill (wavefront.hip trace_refill), which changes only the
+// schedule, never the visited nodes, so the hits are identical.
 // nodes / tris: global or LDS pointers (wavefront.hip SceneView).
-template <bool kAnyHit, bool kCount = false, typename NodeP, typename TriP, typename Stack>
-RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float tmin, float tmax, Stack& st, Hit& h,
-                   TravCount& cnt) {
-    h.t = tmax;
-    h.u = h.v = 0.0f;
-    h.idx = -1;
-    h.orig = -1;
-    if (n_tris <= 0) return false;
-    const float3 invd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    int node = 0;
-    st.sp = 0;
-    for (;;) {
+template <bool kAnyHit, bool kCount = false>
+struct TravState {
+    float3 o, d, invd;
+    float tmin;
+    Hit h;
+    int node;
+    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_) {
+        o = o_;
+        d = d_;
+        tmin = tmin_;
+        h.t = tmax_;
+        h.u = h.v = 0.0f;
+        h.idx = -1;
+        h.orig = -1;
+        invd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        node = 0;
+    }
+    // One node visit; true when the ray is finished (any-hit: on the first hit).
+    template <typename NodeP, typename TriP, typename Stack>
+    RR_D bool step(NodeP nodes, TriP tris, Stack& st, TravCount& cnt) {
         const BvhNode nd = load_node(nodes, node);
         if (kCount) ++cnt.nodes;
         float tl, tr;
@@ -312,13 +363,13 @@ RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float
         const int cl = nd.d.x, cr = nd.d.y;
         if (hl && cl < 0) {
             if (kCount) ++cnt.tris;
-            closest_tri(load_tri(tris, ~cl), ~cl, o, d, tmin, h);
+            leaf_test(load_tri(tris, ~cl), ~cl, o, d, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
             hl = false;
         }
         if (hr && cr < 0) {
             if (kCount) ++cnt.tris;
-            closest_tri(load_tri(tris, ~cr), ~cr, o, d, tmin, h);
+            leaf_test(load_tri(tris, ~cr), ~cr, o, d, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
             hr = false;
         }
@@ -331,10 +382,27 @@ RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float
         } else if (hr) {
             node = cr;
         } else {
-            if (st.sp == 0) break;
+            if (st.sp == 0) return true;
             node = st.pop();
         }
+        return false;
     }
+};
+
+// Closest hit (or any hit) over the LBVH, run to completion.
+template <bool kAnyHit, bool kCount = false, typename NodeP, typename TriP, typename Stack>
+RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float tmin, float tmax, Stack& st, Hit& h,
+                   TravCount& cnt) {
+    TravState<kAnyHit, kCount> ts;
+    ts.start(o, d, tmin, tmax);
+    if (n_tris <= 0) {
+        h = ts.h;
+        return false;
+    }
+    st.sp = 0;
+    while (!ts.step(nodes, tris, st, cnt)) {
+    }
+    h = ts.h;
     return h.idx >= 0;
 }
 

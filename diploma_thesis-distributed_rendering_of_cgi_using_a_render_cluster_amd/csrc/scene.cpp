@@ -57,12 +57,25 @@ void gen_cube(MeshDesc& m, double size) {
     }
 }
 
-void gen_plane(MeshDesc& m, double size) {
-    const float h = (float)(size * 0.5);
-    const float v[12] = {-h, -h, 0, h, -h, 0, h, h, 0, -h, h, 0};
-    m.verts.assign(v, v + 12);
-    m.tris = {0, 1, 2, 0, 2, 3};
-    m.mat_idx = {0, 0};
+// size x size plane at z = 0 cut into n x n quads (n = 1: Blender's 2-triangle
+// plane). Large scenes use n > 1: a 2-triangle ground spanning the whole scene
+// inflates every LBVH ancestor box of its Morton neighbourhood.
+void gen_plane(MeshDesc& m, double size, int n) {
+    if (n < 1) n = 1;
+    for (int y = 0; y <= n; ++y)
+        for (int x = 0; x <= n; ++x) {
+            m.verts.push_back((float)(size * ((double)x / n - 0.5)));
+            m.verts.push_back((float)(size * ((double)y / n - 0.5)));
+            m.verts.push_back(0.0f);
+        }
+    for (int y = 0; y < n; ++y)
+        for (int x = 0; x < n; ++x) {
+            const uint32_t a = (uint32_t)(y * (n + 1) + x), b = a + 1, c = a + (uint32_t)(n + 1) + 1,
+                           d = a + (uint32_t)(n + 1);
+            m.tris.insert(m.tris.end(), {a, b, c, a, c, d});
+            m.mat_idx.push_back(0);
+            m.mat_idx.push_back(0);
+        }
 }
 
 void gen_icosphere(MeshDesc& m, int subdiv, double radius) {
@@ -129,7 +142,7 @@ void parse_mesh(const Json& jm, MeshDesc& m) {
         const Json& g = jm["generator"];
         const std::string t = g["type"].as_str();
         if (t == "cube") gen_cube(m, g.get_num("size", 2.0));
-        else if (t == "plane") gen_plane(m, g.get_num("size", 2.0));
+        else if (t == "plane") gen_plane(m, g.get_num("size", 2.0), (int)g.get_num("subdivisions", 1));
         else if (t == "icosphere") gen_icosphere(m, (int)g.get_num("subdivisions", 2), g.get_num("radius", 1.0));
         else if (t == "displaced_icosphere")
             gen_displaced_icosphere(m, (int)g.get_num("subdivisions", 3), g.get_num("radius", 1.0),

@@ -549,6 +549,307 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
         shadow_body<kCount>(sa.nodes, sa.tris, sa.n_tris, sq, ix, count, rad, spill, tc, stack);
 }
 
+// ------------------------------------------------------------------------
+// Split path for scenes that do not fit in LDS (C4/C5-sized BVHs): traversal
+// and shading run as separate kernels so that the traversal kernels carry only
+// the ray + traversal state (≤ 64 VGPRs, 8 waves per SIMD to hide the
+// L2/MALL/HBM latency of the node fetches) and keep their lanes busy with
+// lane refill: each wave owns a contiguous range of the ray queue and, when
+// fewer than kRefillBelow of its lanes are still traversing, hands the idle
+// lanes the next rays of its range (ballot prefix, no atomics). Finished rays
+// write a hit record (t, leaf index) that the shading kernel consumes in queue
+// order.
+//
+// Queues here are GROUPED: a shading wave appends its ballot-compacted rays
+// to group g = wave % kQGroups with one atomicAdd on that group's counter
+// (counters 128 B apart). One counter per queue serialised the appends
+// (device-scope atomics on one address: ~11 ns each, measured as >80 % of the
+// shading kernels' time); 64 groups spread them over 64 lines. A consumer wave
+// scans the 64 group counts in registers (one load per lane + a 6-step shuffle
+// scan, no LDS, no barrier) and maps a dense index j to (group, offset) with a
+// 6-step shuffle binary search. Queue order may vary between runs; what each
+// path computes (and the per-path order of radiance additions) does not, so
+// images stay bit-identical to the fused kernels' and the oracle's.
+#ifndef RR_REFILL_BELOW
+#define RR_REFILL_BELOW 44
+#endif
+#ifndef RR_TRACE_WAVES
+#define RR_TRACE_WAVES 7
+#endif
+constexpr int kRefillBelow = RR_REFILL_BELOW;
+constexpr int kQGroups = 64;   // append groups per queue (one lane each in QueueMap)
+constexpr int kQStride = 32;   // words between group counters (128 B)
+
+// map(k) -> slot is called by every lane of the wave (converged: QueueMap
+// shuffles); ray_of(slot, ...) and done(k, slot, hit) per lane.
+template <bool kAnyHit, bool kCount, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
+RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack& st, TravCount& cnt, MapFn&& map,
+                       RayFn&& ray_of, DoneFn&& done) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int nw = gridDim.x * kWavesPerBlock;
+    const int per = (count + nw - 1) / nw;
+    int next = (int)wave_id() * per;  // wave-uniform cursor into this wave's range
+    const int end = min(count, next + per);
+    TravState<kAnyHit, kCount> ts;
+    int j = -1;
+    uint32_t js = 0;  // queue slot of ray j
+    for (;;) {
+        const uint64_t idle = __ballot(j < 0);
+        if (next < end && idle) {  // wave-uniform
+            const int k = next + (int)__popcll(idle & below);
+            const uint32_t ks = map(k < end ? k : end - 1);
+            if (j < 0 && k < end) {
+                float3 o, d;
+                float tmin, tmax;
+                ray_of(ks, o, d, tmin, tmax);
+                ts.start(o, d, tmin, tmax);
+                st.sp = 0;
+                if (n_tris > 0) {
+                    j = k;
+                    js = ks;
+                } else {
+                    done(k, ks, ts.h);
+                }
+            }
+            next += (int)__popcll(idle);
+        }
+        if (!__ballot(j >= 0)) {
+            if (next >= end) break;
+            continue;
+        }
+        for (;;) {
+            if (j >= 0 && ts.step(nodes, tris, st, cnt)) {
+                done(j, js, ts.h);
+                j = -1;
+            }
+            const int na = (int)__popcll(__ballot(j >= 0));
+            if (na == 0 || (next < end && na < kRefillBelow)) break;
+        }
+    }
+}
+
+RR_D float2 pack_hit(const Hit& h) { return make_float2(h.t, i2f(h.idx)); }
+RR_D Hit unpack_hit(float2 v) {
+    Hit h;
+    h.t = v.x;
+    h.idx = f2i(v.y);
+    h.u = h.v = 0.0f;
+    h.orig = -1;
+    return h;
+}
+
+// Grouped queue: counters (kQGroups, kQStride words apart) + group capacity.
+struct QueueIn {
+    const uint32_t* ctr;
+    uint32_t cap;       // slots per group
+    uint32_t* total;    // block 0 records the queue length (ray statistics), may be null
+};
+
+// Per-wave view of a grouped queue: lane g holds the exclusive prefix of the
+// group counts; slot(j) is a shuffle binary search (every lane of the wave
+// must call it, each with its own j).
+struct QueueMap {
+    int pre;     // this lane's group start in dense order
+    int total;
+    uint32_t cap;
+    RR_D void init(const QueueIn& q) {
+        const int lane = threadIdx.x & 63;
+        const int c = (int)q.ctr[lane * kQStride];
+        int incl = c;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
+        }
+        pre = incl - c;
+        total = __shfl(incl, 63);
+        cap = q.cap;
+        if (q.total && blockIdx.x == 0 && threadIdx.x == 0) *q.total = (uint32_t)total;
+    }
+    RR_D uint32_t slot(int j) const {
+        int g = 0;
+        for (int step = 32; step > 0; step >>= 1) {  // largest g with pre[g] <= j
+            const int cand = g + step;
+            if (__shfl(pre, cand) <= j) g = cand;
+        }
+        return (uint32_t)g * cap + (uint32_t)(j - __shfl(pre, g));
+    }
+};
+
+// Grouped append: one atomicAdd per queue per wave on its group's counter.
+struct QueueOut {
+    uint32_t* ctr_path;    // path queue group counters
+    uint32_t* ctr_shadow;  // shadow queue group counters
+    uint32_t cap;          // slots per group (both queues)
+};
+
+__device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQueue out, ShadowQueue sq,
+                                             const QueueOut& qo) {
+    const uint64_t mc = __ballot(so.cont), ms = __ballot(so.shadow);
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint32_t g = wave_id() % kQGroups;
+    uint32_t bc = 0, bs = 0;
+    if (lane == 0) {
+        if (mc) bc = atomicAdd(qo.ctr_path + g * kQStride, (uint32_t)__popcll(mc));
+        if (ms) bs = atomicAdd(qo.ctr_shadow + g * kQStride, (uint32_t)__popcll(ms));
+    }
+    bc = g * qo.cap + (uint32_t)__shfl((int)bc, 0);
+    bs = g * qo.cap + (uint32_t)__shfl((int)bs, 0);
+    if (so.cont) {
+        const uint32_t s1 = bc + (uint32_t)__popcll(mc & below);
+        out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
+        out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, 0.0f);
+        out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, 0.0f);
+    }
+    if (so.shadow) {
+        const uint32_t s2 = bs + (uint32_t)__popcll(ms & below);
+        sq.o[s2] = make_float4(so.so.x, so.so.y, so.so.z, i2f(pid));
+        sq.d[s2] = make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist);
+        sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, 0.0f);
+    }
+}
+
+// Camera paths: raygen + closest hit -> hits[p].
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
+                                                                          float2* __restrict__ hits,
+                                                                          int32_t* __restrict__ spill,
+                                                                          unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
+    TravCount cnt;
+    trace_refill<false, kCount>(
+        sa.nodes, sa.tris, sa.n_tris, np, st, cnt, [](int p) { return (uint32_t)p; },
+        [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
+            const int sl = (int)fc.div_npix.div(p);
+            const int pix = (int)p - sl * fc.npix;
+            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
+            camera_ray(fc, sa.filter, pix, key, o, d, tmin, tmax);
+        },
+        [&](int p, uint32_t, const Hit& h) { hits[p] = pack_hit(h); });
+    if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
+}
+
+// Camera paths: shade bounce 0 from hits[p]; appends the bounce-1 path queue
+// and the bounce-0 shadow queue.
+__global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np,
+                                                          const float2* __restrict__ hits, float4* __restrict__ rad,
+                                                          PathQueue out, ShadowQueue sq, QueueOut qo) {
+    const GlobalView v = global_view(sa);
+    const int stride = gridDim.x * kBlock;
+    for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {
+        const int p = b0 + (int)threadIdx.x;
+        ShadeOut so;
+        so.cont = so.shadow = false;
+        if (p < np) {
+            const int sl = (int)fc.div_npix.div((uint32_t)p);
+            const int pix = p - sl * fc.npix;
+            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
+            float3 o, d;
+            float tmin, tmax;
+            camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax);
+            const Hit h = unpack_hit(hits[p]);
+            float3 L = mk3(0.0f, 0.0f, 0.0f);
+            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
+            rad[p] = make_float4(L.x, L.y, L.z, 0.0f);
+        }
+        emit_grouped(so, p, out, sq, qo);
+    }
+}
+
+// Extension rays entering bounce b: closest hit -> hits[j] (j dense).
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
+                                                                         float2* __restrict__ hits,
+                                                                         int32_t* __restrict__ spill,
+                                                                         unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    QueueMap qm;
+    qm.init(qi);
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
+    TravCount cnt;
+    trace_refill<false, kCount>(
+        sa.nodes, sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
+        [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
+            o = xyz(in.o[i]);
+            d = xyz(in.d[i]);
+            tmin = 0.0f;
+            tmax = kFltMax;
+        },
+        [&](int j, uint32_t, const Hit& h) { hits[j] = pack_hit(h); });
+    if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
+}
+
+// Bounce b: shade from hits[j]; appends the next path queue and this bounce's
+// shadow queue.
+__global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in,
+                                                         QueueIn qi, const float2* __restrict__ hits,
+                                                         float4* __restrict__ rad, PathQueue out, ShadowQueue sq,
+                                                         QueueOut qo) {
+    QueueMap qm;
+    qm.init(qi);
+    const int count = qm.total;
+    const GlobalView v = global_view(sa);
+    const int stride = gridDim.x * kBlock;
+    int pid = 0;
+    for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
+        const int j = b0 + (int)threadIdx.x;
+        ShadeOut so;
+        so.cont = so.shadow = false;
+        const uint32_t i = qm.slot(j);  // all lanes (shuffles); used only when j < count
+        if (j < count) {
+            const float4 a = in.o[i], b = in.d[i], c = in.t[i];
+            pid = f2i(a.w);
+            const Hit h = unpack_hit(hits[j]);
+            const int sl = (int)fc.div_npix.div((uint32_t)pid);
+            const int pix = pid - sl * fc.npix;
+            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
+            const float4 L4 = rad[pid];
+            float3 L = xyz(L4);
+            shade(fc, bounce, v, xyz(a), xyz(b), xyz(c), h, key, L, so);
+            rad[pid] = make_float4(L.x, L.y, L.z, 0.0f);
+        }
+        emit_grouped(so, pid, out, sq, qo);
+    }
+}
+
+// Shadow rays with lane refill: unoccluded -> radiance += contribution.
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
+                                                                          float4* __restrict__ rad,
+                                                                          int32_t* __restrict__ spill,
+                                                                          unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    QueueMap qm;
+    qm.init(qi);
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
+    TravCount cnt;
+    trace_refill<true, kCount>(
+        sa.nodes, sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
+        [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
+            const float4 a = sq.o[i], b = sq.d[i];
+            o = xyz(a);
+            d = xyz(b);
+            tmin = 0.0f;
+            tmax = b.w;
+        },
+        [&](int, uint32_t i, const Hit& h) {
+            if (h.idx >= 0) return;
+            const int pid = f2i(sq.o[i].w);
+            const float4 c = sq.c[i];
+            float4 L = rad[pid];
+            L.x = L.x + c.x;
+            L.y = L.y + c.y;
+            L.z = L.z + c.z;
+            rad[pid] = L;
+        });
+    if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
+}
+
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
 // sample order; then mean -> exposure -> view transform -> 8-bit.
 __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, const float4* __restrict__ rad,
@@ -681,6 +982,31 @@ struct Grids {
         shadow = grid_for(ks, dyn_shadow);
     }
 };
+// Launch geometry of the split (trace / shade) path of large scenes.
+struct SplitGrids {
+    int trace_p, trace_e, shadow, shade_p, shade_e;
+    void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*);
+    void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
+    void (*kts)(SceneArgs, ShadowQueue, QueueIn, float4*, int32_t*, unsigned long long*);
+    explicit SplitGrids(bool count) {
+        ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
+        kte = count ? k_trace_extend<true> : k_trace_extend<false>;
+        kts = count ? k_shadow_refill<true> : k_shadow_refill<false>;
+        trace_p = grid_for(ktp, 0);
+        trace_e = grid_for(kte, 0);
+        shadow = grid_for(kts, 0);
+        shade_p = grid_for(k_shade_primary, 0);
+        shade_e = grid_for(k_shade_extend, 0);
+    }
+};
+// Slots per append group for a producer of `grid` blocks over at most `work`
+// items: each wave emits at most ceil(work / threads) * 64 per queue, and a
+// group holds ceil(waves / kQGroups) waves.
+inline uint32_t group_cap(long work, int grid) {
+    const long waves = (long)grid * kWavesPerBlock;
+    const long per_wave = ((work + (long)grid * kBlock - 1) / ((long)grid * kBlock)) * 64;
+    return (uint32_t)(((waves + kQGroups - 1) / kQGroups) * per_wave);
+}
 int accum_grid() {
     static const int g = resident_grid(k_accumulate);
     return g;
@@ -699,12 +1025,13 @@ inline uint32_t seg_cap(long work, int grid) {
 
 void DevPaths::ensure_paths(size_t n) {
     if (grid_blocks == 0) grid_blocks = device_cu_count() * kMaxBlocksPerCu;
-    n += (size_t)grid_blocks * kBlock;  // segment round-up slack (seg_cap)
+    n += (size_t)grid_blocks * kBlock + n / 64;  // segment / group round-up slack (seg_cap, group_cap)
     segs.ensure((size_t)4 * grid_blocks * kWavesPerBlock);
     if (n > cap) {
         for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                                   &sh_c})
             b->ensure(n);
+        hits.ensure(n);
         cap = n;
     }
     spill.ensure((size_t)kSpillStack * grid_blocks * kBlock);
@@ -714,12 +1041,76 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
-    counters.release(); spill.release(); segs.release();
+    counters.release(); spill.release(); segs.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     trav_counts.release();
     prof.release();
     cap = 0;
 }
+
+namespace {
+// Large scenes: per chunk trace_primary -> shade_primary -> for each bounce b:
+// shadow(b), trace_extend(b+1), shade_extend(b+1) -> accumulate. Radiance
+// additions per path happen in the same order as the fused kernels'.
+void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_t st, const SceneArgs& sa,
+                  unsigned long long* tc, PathQueue pq[2], const ShadowQueue& sq) {
+    KernelProfiler& pr = p.prof;
+    const SplitGrids G(tc != nullptr);
+    const int npix = base.npix;
+    const int cpc = counters_per_chunk(base.max_bounces);
+    // group counters: [chunk][bounce 0..max][path | shadow][kQGroups * kQStride]
+    const size_t per_q = (size_t)kQGroups * kQStride;
+    const size_t per_chunk = (size_t)(base.max_bounces + 1) * 2 * per_q;
+    p.qctr.ensure(per_chunk * n_chunks);
+    RR_HIP(hipMemsetAsync(p.qctr.ptr, 0, per_chunk * n_chunks * sizeof(uint32_t), st));
+    for (int c = 0; c < n_chunks; ++c) {
+        FrameConsts fc = base;
+        fc.first_sample = c * base.spp_chunk;
+        fc.spp_chunk = base.spp_chunk;
+        if (fc.first_sample + fc.spp_chunk > base.spp_total) fc.spp_chunk = base.spp_total - fc.first_sample;
+        const int np = npix * fc.spp_chunk;
+        uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr + (size_t)cpc * c);
+        uint32_t* qc = p.qctr.ptr + per_chunk * c;
+        auto qpath = [&](int b) { return qc + ((size_t)b * 2 + 0) * per_q; };    // paths entering b+1
+        auto qshadow = [&](int b) { return qc + ((size_t)b * 2 + 1) * per_q; };  // shadow rays of b
+        const int gsp = clamp_grid(np, G.shade_p), gse = clamp_grid(np, G.shade_e);
+        const uint32_t cap_p = group_cap(np, gsp), cap_e = group_cap(np, gse);
+        if ((size_t)std::max(cap_p, cap_e) * kQGroups > p.cap)
+            throw std::runtime_error("queue capacity exceeded (split path)");
+        pr.begin(st, RR_K_PRIMARY);
+        G.ktp<<<clamp_grid(np, G.trace_p), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc);
+        pr.end(st);
+        pr.begin(st, RR_K_SHADE);
+        k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.rad.ptr, pq[1], sq,
+                                                QueueOut{qpath(0), qshadow(0), cap_p});
+        pr.end(st);
+        uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
+        for (int b = 0; b <= base.max_bounces; ++b) {
+            pr.begin(st, RR_K_SHADOW);
+            G.kts<<<clamp_grid(np, G.shadow), kBlock, 0, st>>>(sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1},
+                                                               p.rad.ptr, p.spill.ptr, tc);
+            pr.end(st);
+            if (b == base.max_bounces) break;
+            const int nb = b + 1;  // bounce being traced and shaded
+            const QueueIn qin{qpath(b), cap_prev, tot + 2 * b};
+            pr.begin(st, RR_K_EXTEND);
+            G.kte<<<clamp_grid(np, G.trace_e), kBlock, 0, st>>>(sa, pq[nb & 1], qin, p.hits.ptr, p.spill.ptr, tc);
+            pr.end(st);
+            pr.begin(st, RR_K_SHADE);
+            k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},
+                                                   p.hits.ptr, p.rad.ptr, pq[(nb + 1) & 1], sq,
+                                                   QueueOut{qpath(nb), qshadow(nb), cap_e});
+            pr.end(st);
+            cap_prev = cap_e;
+        }
+        const int ga = clamp_grid(npix, accum_grid());
+        pr.begin(st, RR_K_ACCUM);
+        k_accumulate<<<ga, kBlock, 0, st>>>(fc, p.rad.ptr, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
+                                            p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
+        pr.end(st);
+    }
+}
+}  // namespace
 
 void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_t st) {
     const int npix = base.npix;
@@ -742,6 +1133,11 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     const Grids G(base, tc != nullptr);
     const SceneArgs sa{s.nodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
                        std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
+    if (!G.lds && base.n_tris > 0) {
+        render_split(p, base, n_chunks, st, sa, tc, pq, sq);
+        RR_HIP(hipGetLastError());
+        return;
+    }
     for (int c = 0; c < n_chunks; ++c) {
         FrameConsts fc = base;
         fc.first_sample = c * base.spp_chunk;

@@ -63,7 +63,7 @@ class FrameStats(ctypes.Structure):
 
 
 RR_FLAG_PROFILE_KERNELS, RR_FLAG_COUNT_TRAVERSAL = 1, 2
-KERNEL_CLASSES = ["build", "primary", "extend", "shadow", "accumulate"]
+KERNEL_CLASSES = ["build", "primary", "extend", "shadow", "accumulate", "shade"]
 
 
 # Every symbol include/rr.h declares (checked by tests/test_abi.py).
@@ -81,10 +81,13 @@ def lib() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.isfile(LIB_PATH):
-        raise RRError(RR_ENOENT, f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+    # RR_LIB_PATH: an alternative in-tree build of the same library (A/B timing
+    # of kernel variants, tools/ab_variants.sh); never a different implementation.
+    path = os.environ.get("RR_LIB_PATH", LIB_PATH)
+    if not os.path.isfile(path):
+        raise RRError(RR_ENOENT, f"{path} is missing: build it with __graft_entry__.build() "
                                  "(there is no CPU fallback)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, c_int, i32, u32, f32p, u8p = ctypes.c_void_p, ctypes.c_int, ctypes.c_int32, ctypes.c_uint32, \
         ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint8)
     i32p, u32p = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint32)

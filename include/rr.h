@@ -75,6 +75,7 @@ typedef struct rr_render_params {
 #define RR_K_EXTEND 2    /* bounces >= 1: closest hit + shade + queue compaction */
 #define RR_K_SHADOW 3    /* any-hit traversal of shadow rays */
 #define RR_K_ACCUM 4     /* film accumulate + tonemap */
+#define RR_K_SHADE 5     /* split path (large scenes): shading kernels; PRIMARY/EXTEND then time traversal only */
 #define RR_K_CLASSES 8
 
 /* The five timestamps the reference recovers from Blender's stdout
