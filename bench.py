@@ -72,6 +72,8 @@ def parse_args():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="04vs")
     ap.add_argument("--spp", type=int, default=0, help="override the scene's samples (0 = scene)")
     ap.add_argument("--no-profile", action="store_true", help="time without per-kernel HIP events")
+    ap.add_argument("--serial", action="store_true",
+                    help="one rr_render_frame per step (no overlap of frame N's encode with N+1's render)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r1_pmc.json"),
@@ -208,20 +210,33 @@ def main():
     def frame_of(step):
         return frame_partition(frames, step, rank, world)
 
-    for w in range(args.warmup):
-        runner.render_frame(job, frame_of(w))
+    if args.serial:
+        for w in range(args.warmup):
+            runner.render_frame(job, frame_of(w))
+    else:
+        runner.render_frames(job, [frame_of(w) for w in range(args.warmup)])
     kernel_ms = [0.0] * 8
     launches = [0] * 8
     rays = 0
-    barrier()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        runner.render_frame(job, frame_of(args.warmup + s))
-        st = runner.last_stats
+
+    def account(st):
+        nonlocal rays
         for k in range(8):
             kernel_ms[k] += st.kernel_ms[k]
             launches[k] += st.kernel_launches[k]
         rays += st.camera_rays + st.extension_rays + st.shadow_rays
+
+    barrier()
+    t0 = time.perf_counter()
+    if args.serial:
+        for s in range(args.steps):
+            runner.render_frame(job, frame_of(args.warmup + s))
+            account(runner.last_stats)
+    else:
+        # the worker's queued frames, frame N+1 rendering while N is encoded and
+        # written (rr_frame_submit / rr_frame_complete); every frame is written
+        runner.render_frames(job, [frame_of(args.warmup + s) for s in range(args.steps)],
+                             on_frame=lambda f, frt, st: account(st))
     barrier()
     elapsed = time.perf_counter() - t0
     last_stats = runner.last_stats
@@ -283,7 +298,9 @@ def main():
             "data": wl["data"],
             "config": {"workload": wl["workload"], "job": os.path.basename(wl["job"]),
                        "resolution": f"{int(last_stats.width)}x{int(last_stats.height)}", "spp": int(last_stats.spp),
-                       "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)"},
+                       "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)",
+                       "pipelining": "serial (rr_render_frame per frame)" if args.serial else
+                                     "2 frames in flight: frame N encoded + written while N+1 renders"},
             "mrays_per_s_per_gpu": round(rays / elapsed / 1e6, 1),
             "device_ms_per_frame": round(sum(kernel_ms) / max(args.steps, 1), 3),
             "kernels": per_class,

@@ -67,20 +67,52 @@ struct PinnedBuf {
 
 }  // namespace
 
+struct FrameRun {
+    int W, H, chunks, spp_chunk;
+    bool rebuilt;
+    float build_ms, trace_ms, readback_ms;
+    std::vector<int32_t> counters;
+    double kernel_ms[RR_K_CLASSES];
+    int32_t kernel_launches[RR_K_CLASSES];
+    unsigned long long trav[6];
+};
+
+// One frame between rr_frame_submit and rr_frame_complete: its host-side
+// outputs (pinned, so the device-to-host copies stay asynchronous), events,
+// kernel profiler and the request. Two slots = the next queued frame renders
+// while the host encodes and writes the previous one.
+struct FrameSlot {
+    bool busy = false;
+    uint64_t ticket = 0;
+    hipEvent_t ev[4] = {};
+    KernelProfiler prof;
+    PinnedBuf host_rgba, host_coeffs, host_counters, host_upload;
+    FrameSetup fs;
+    rr_scene* scene = nullptr;
+    std::string out_path, format;
+    int quality = 0;
+    bool jpeg = false, want_rgba = false, count = false;
+    float* film_out = nullptr;
+    FrameRun r{};
+    rr_frame_timing tm{};
+    double anim_ms = 0.0;
+    std::chrono::steady_clock::time_point t_call;
+};
+
 struct rr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {};
     DevPaths paths;
-    PinnedBuf host_rgba;
     // device JPEG transform (jpeg.hip): tables for the last quality, coefficients
     DevBuf<float> jpeg_tab;
     int jpeg_tab_quality = -1;
     DevBuf<int16_t> jpeg_coeffs;
-    PinnedBuf host_coeffs;
     std::vector<float> filter_cache;
     float filter_width_cached = -1.f;
     bool srgb_uploaded = false;
+    FrameSlot slots[RR_MAX_FRAMES_IN_FLIGHT];
+    uint64_t next_ticket = 1;     // tickets are issued in submission order
+    uint64_t next_complete = 1;   // the ticket rr_frame_complete expects next
 };
 
 struct rr_scene {
@@ -132,7 +164,9 @@ void bind_scene(rr_ctx* c, rr_scene* s) {
 }
 
 // Upload per-frame constants and (re)build the LBVH if object transforms changed.
-bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs) {
+// `staging` (pinned, per frame slot) keeps the host-to-device copies
+// asynchronous, so a frame can be enqueued while the previous one still runs.
+bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& staging) {
     bind_scene(c, s);
     hipStream_t st = c->stream;
     DevPaths& p = c->paths;
@@ -152,17 +186,21 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs) {
         RR_HIP(hipMemcpy(p.srgb_lut.ptr, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice));
         c->srgb_uploaded = true;
     }
-    const size_t nl = fs.lights.size(), nm = fs.materials.size();
+    const size_t nl = fs.lights.size(), nm = fs.materials.size(), nx = fs.obj_xform.size();
     p.lights.ensure(nl ? nl : 1);
     p.materials.ensure(nm ? nm : 1);
-    if (nl) RR_HIP(hipMemcpyAsync(p.lights.ptr, fs.lights.data(), nl * sizeof(float), hipMemcpyHostToDevice, st));
-    RR_HIP(hipMemcpyAsync(p.materials.ptr, fs.materials.data(), nm * sizeof(float), hipMemcpyHostToDevice, st));
+    staging.ensure((nl + nm + nx) * sizeof(float));
+    float* up = reinterpret_cast<float*>(staging.ptr);
+    std::memcpy(up, fs.lights.data(), nl * sizeof(float));
+    std::memcpy(up + nl, fs.materials.data(), nm * sizeof(float));
+    std::memcpy(up + nl + nm, fs.obj_xform.data(), nx * sizeof(float));
+    if (nl) RR_HIP(hipMemcpyAsync(p.lights.ptr, up, nl * sizeof(float), hipMemcpyHostToDevice, st));
+    RR_HIP(hipMemcpyAsync(p.materials.ptr, up + nl, nm * sizeof(float), hipMemcpyHostToDevice, st));
     DevScene& d = s->dev;
     const bool rebuild = !d.built || d.cached_xform != fs.obj_xform;
     if (rebuild && d.n_tris > 0) {
-        d.obj_xform.ensure(fs.obj_xform.size());
-        RR_HIP(hipMemcpyAsync(d.obj_xform.ptr, fs.obj_xform.data(), fs.obj_xform.size() * sizeof(float),
-                              hipMemcpyHostToDevice, st));
+        d.obj_xform.ensure(nx);
+        RR_HIP(hipMemcpyAsync(d.obj_xform.ptr, up + nl + nm, nx * sizeof(float), hipMemcpyHostToDevice, st));
         build_lbvh(d, st, &p.prof);
         d.cached_xform = fs.obj_xform;
     } else if (rebuild) {
@@ -217,89 +255,101 @@ int choose_spp_chunk(const FrameSetup& fs) {
     return (int)c;
 }
 
-struct FrameRun {
-    int W, H, chunks, spp_chunk;
-    bool rebuilt;
-    float build_ms, trace_ms, readback_ms;
-    std::vector<int32_t> counters;
-    double kernel_ms[RR_K_CLASSES];
-    int32_t kernel_launches[RR_K_CLASSES];
-    unsigned long long trav[6];
-};
-
-// Run the device part of one frame; leaves the 8-bit image in c->host_rgba.
-// jpeg_quality > 0: also run the device JPEG transform and read back its
-// coefficients (c->host_coeffs); want_rgba: read back the 8-bit image.
-FrameRun run_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, float* film_out, int jpeg_quality = 0,
-                   bool want_rgba = true) {
+// Enqueue the device part of one frame on the context stream (no host
+// synchronisation): LBVH (if needed), wavefront, tonemap, optionally the JPEG
+// transform, and the asynchronous copies of the slot's outputs.
+void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     set_device(c);
-    FrameRun r{};
+    rr_scene* s = sl.scene;
+    const FrameSetup& fs = sl.fs;
+    FrameRun& r = sl.r;
+    r = FrameRun{};
     r.W = fs.W;
     r.H = fs.H;
     hipStream_t st = c->stream;
-    c->paths.prof.reset((fs.flags & RR_FLAG_PROFILE_KERNELS) != 0);
-    c->paths.count_traversal = (fs.flags & RR_FLAG_COUNT_TRAVERSAL) != 0;
-    RR_HIP(hipEventRecord(c->ev[0], st));
-    r.rebuilt = prepare_frame(c, s, fs);
-    RR_HIP(hipEventRecord(c->ev[1], st));
+    for (auto& e : sl.ev)
+        if (!e) RR_HIP(hipEventCreate(&e));
+    sl.prof.reset((fs.flags & RR_FLAG_PROFILE_KERNELS) != 0);
+    struct ProfSwap {  // the device code records into paths.prof; swapped back on every exit
+        KernelProfiler &a, &b;
+        ProfSwap(KernelProfiler& x, KernelProfiler& y) : a(x), b(y) { std::swap(a, b); }
+        ~ProfSwap() { std::swap(a, b); }
+    } prof_swap(c->paths.prof, sl.prof);
+    sl.count = (fs.flags & RR_FLAG_COUNT_TRAVERSAL) != 0;
+    c->paths.count_traversal = sl.count;
+    RR_HIP(hipEventRecord(sl.ev[0], st));
+    r.rebuilt = prepare_frame(c, s, fs, sl.host_upload);
+    RR_HIP(hipEventRecord(sl.ev[1], st));
     FrameConsts k = make_consts(fs, s->dev.n_tris);
     r.spp_chunk = choose_spp_chunk(fs);
     r.chunks = (fs.spp + r.spp_chunk - 1) / r.spp_chunk;
     k.spp_chunk = r.spp_chunk;
     render_frame_device(s->dev, c->paths, k, r.chunks, st);
-    RR_HIP(hipEventRecord(c->ev[2], st));
+    RR_HIP(hipEventRecord(sl.ev[2], st));
     const size_t npix = (size_t)fs.W * fs.H;
-    if (jpeg_quality > 0) {
-        if (c->jpeg_tab_quality != jpeg_quality) {
+    if (sl.jpeg) {
+        if (c->jpeg_tab_quality != sl.quality) {
             JpegTables t;
-            jpeg_tables(jpeg_quality, t);
+            jpeg_tables(sl.quality, t);
             float tab[192];
             std::memcpy(tab, t.dct, sizeof t.dct);
             std::memcpy(tab + 64, t.qinv_l, sizeof t.qinv_l);
             std::memcpy(tab + 128, t.qinv_c, sizeof t.qinv_c);
             c->jpeg_tab.ensure(192);
             RR_HIP(hipMemcpy(c->jpeg_tab.ptr, tab, sizeof tab, hipMemcpyHostToDevice));
-            c->jpeg_tab_quality = jpeg_quality;
+            c->jpeg_tab_quality = sl.quality;
         }
         const size_t nc = jpeg_coeff_count(fs.W, fs.H);
         c->jpeg_coeffs.ensure(nc);
-        c->host_coeffs.ensure(nc * sizeof(int16_t));
+        sl.host_coeffs.ensure(nc * sizeof(int16_t));
         jpeg_fdct_device(c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr, c->jpeg_coeffs.ptr, st);
-        RR_HIP(hipMemcpyAsync(c->host_coeffs.ptr, c->jpeg_coeffs.ptr, nc * sizeof(int16_t), hipMemcpyDeviceToHost,
+        RR_HIP(hipMemcpyAsync(sl.host_coeffs.ptr, c->jpeg_coeffs.ptr, nc * sizeof(int16_t), hipMemcpyDeviceToHost,
                               st));
     }
-    if (want_rgba) {
-        c->host_rgba.ensure(npix * 4);
-        RR_HIP(hipMemcpyAsync(c->host_rgba.ptr, c->paths.rgba8.ptr, npix * 4, hipMemcpyDeviceToHost, st));
+    if (sl.want_rgba) {
+        sl.host_rgba.ensure(npix * 4);
+        RR_HIP(hipMemcpyAsync(sl.host_rgba.ptr, c->paths.rgba8.ptr, npix * 4, hipMemcpyDeviceToHost, st));
     }
     const int cpc = counters_per_chunk(fs.max_bounces);
-    r.counters.resize((size_t)cpc * r.chunks);
-    RR_HIP(hipMemcpyAsync(r.counters.data(), c->paths.counters.ptr, r.counters.size() * sizeof(int32_t),
-                          hipMemcpyDeviceToHost, st));
-    if (film_out)
-        RR_HIP(hipMemcpyAsync(film_out, c->paths.film.ptr, npix * sizeof(float4), hipMemcpyDeviceToHost, st));
-    RR_HIP(hipEventRecord(c->ev[3], st));
-    RR_HIP(hipStreamSynchronize(st));
-    RR_HIP(hipEventElapsedTime(&r.build_ms, c->ev[0], c->ev[1]));
-    RR_HIP(hipEventElapsedTime(&r.trace_ms, c->ev[1], c->ev[2]));
-    RR_HIP(hipEventElapsedTime(&r.readback_ms, c->ev[2], c->ev[3]));
-    c->paths.prof.collect(r.kernel_ms, r.kernel_launches);
-    c->paths.prof.reset(false);
-    if (c->paths.count_traversal) {
+    const size_t nctr = (size_t)cpc * r.chunks;
+    sl.host_counters.ensure(nctr * sizeof(int32_t));
+    RR_HIP(hipMemcpyAsync(sl.host_counters.ptr, c->paths.counters.ptr, nctr * sizeof(int32_t), hipMemcpyDeviceToHost,
+                          st));
+    if (sl.film_out)
+        RR_HIP(hipMemcpyAsync(sl.film_out, c->paths.film.ptr, npix * sizeof(float4), hipMemcpyDeviceToHost, st));
+    RR_HIP(hipEventRecord(sl.ev[3], st));
+    if (sl.count) {  // measurement mode: read the traversal counters now
+        RR_HIP(hipStreamSynchronize(st));
         RR_HIP(hipMemcpy(r.trav, c->paths.trav_counts.ptr, sizeof r.trav, hipMemcpyDeviceToHost));
         c->paths.count_traversal = false;
     }
-    if (film_out) {  // film holds sums; report the mean
+}
+
+// Wait for a slot's device work and collect its timings and counters.
+void finish_frame(rr_ctx* c, FrameSlot& sl) {
+    set_device(c);
+    FrameRun& r = sl.r;
+    const FrameSetup& fs = sl.fs;
+    RR_HIP(hipEventSynchronize(sl.ev[3]));
+    RR_HIP(hipEventElapsedTime(&r.build_ms, sl.ev[0], sl.ev[1]));
+    RR_HIP(hipEventElapsedTime(&r.trace_ms, sl.ev[1], sl.ev[2]));
+    RR_HIP(hipEventElapsedTime(&r.readback_ms, sl.ev[2], sl.ev[3]));
+    const int cpc = counters_per_chunk(fs.max_bounces);
+    r.counters.assign(reinterpret_cast<const int32_t*>(sl.host_counters.ptr),
+                      reinterpret_cast<const int32_t*>(sl.host_counters.ptr) + (size_t)cpc * r.chunks);
+    sl.prof.collect(r.kernel_ms, r.kernel_launches);
+    sl.prof.reset(false);
+    if (sl.film_out) {  // film holds sums; report the mean
+        const size_t npix = (size_t)fs.W * fs.H;
         const float inv = 1.0f / (float)fs.spp;
         for (size_t i = 0; i < npix; ++i) {
-            float* f = film_out + 4 * i;
+            float* f = sl.film_out + 4 * i;
             f[0] = f[0] * inv;
             f[1] = f[1] * inv;
             f[2] = f[2] * inv;
             f[3] = 1.0f;
         }
     }
-    return r;
 }
 
 void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int n_tris) {
@@ -356,6 +406,10 @@ int do_encode(const uint8_t* rgba, int W, int H, const char* out_path, const cha
     return RR_OK;
 }
 
+FrameSlot* slot_for(rr_ctx* c, uint64_t ticket) { return &c->slots[ticket % RR_MAX_FRAMES_IN_FLIGHT]; }
+
+bool idle(rr_ctx* c) { return c->next_complete == c->next_ticket; }
+
 }  // namespace
 
 extern "C" {
@@ -391,7 +445,6 @@ int rr_create(int device_ordinal, rr_ctx** out) {
         c->device = device_ordinal;
         set_device(c.get());
         RR_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        for (auto& e : c->ev) RR_HIP(hipEventCreate(&e));
         *out = c.release();
         return RR_OK;
     });
@@ -402,8 +455,11 @@ void rr_destroy(rr_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->paths.release();
-    for (auto& e : c->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto& sl : c->slots) {
+        for (auto& e : sl.ev)
+            if (e) (void)hipEventDestroy(e);
+        sl.prof.release();
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -452,69 +508,122 @@ int rr_scene_resolution(rr_scene* s, const rr_render_params* p, int32_t* w, int3
     });
 }
 
-int rr_render_frame(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_params* params, const char* out_path,
-                    const char* format, int32_t jpeg_quality, rr_frame_timing* timing, rr_frame_stats* stats) {
-    if (!c || !s) return fail(RR_EINVAL, "NULL ctx or scene");
+int rr_frame_submit(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_params* params, const char* out_path,
+                    const char* format, int32_t jpeg_quality, uint64_t* ticket) {
+    if (!c || !s || !ticket) return fail(RR_EINVAL, "NULL ctx, scene or ticket");
     if (s->ctx && s->ctx != c) return fail(RR_EINVAL, "scene belongs to another context");
     if (out_path && !format) return fail(RR_EINVAL, "format is required when out_path is given");
     if (format && std::string(format) != "JPEG" && std::string(format) != "PNG")
         return fail(RR_ENOTSUP, std::string("unsupported output format '") + format + "'");
+    const bool jpeg = out_path && std::string(format) == "JPEG";
+    if (jpeg && (jpeg_quality < 1 || jpeg_quality > 100)) return fail(RR_EINVAL, "jpeg_quality must be 1..100");
+    FrameSlot* sl = slot_for(c, c->next_ticket);
+    if (sl->busy) return fail(RR_EBUSY, "too many frames in flight (complete the oldest first)");
     return guarded([&] {
-        const auto t_call = std::chrono::steady_clock::now();
-        rr_frame_timing tm{};
-        tm.loaded_at = unix_now();
+        sl->t_call = std::chrono::steady_clock::now();
+        sl->tm = rr_frame_timing{};
+        sl->tm.loaded_at = unix_now();
         const auto t_anim = std::chrono::steady_clock::now();
-        FrameSetup fs = setup_frame(s->desc, frame, params);
-        const double anim_ms = ms_since(t_anim);
-        tm.started_rendering_at = unix_now();
-        const bool jpeg = out_path && std::string(format) == "JPEG";
-        if (jpeg && (jpeg_quality < 1 || jpeg_quality > 100)) return fail(RR_EINVAL, "jpeg_quality must be 1..100");
-        FrameRun r = run_frame(c, s, fs, nullptr, jpeg ? jpeg_quality : 0, !jpeg);
+        sl->fs = setup_frame(s->desc, frame, params);
+        sl->anim_ms = ms_since(t_anim);
+        sl->tm.started_rendering_at = unix_now();
+        sl->scene = s;
+        sl->out_path = out_path ? out_path : "";
+        sl->format = (out_path && format) ? format : "";
+        sl->quality = jpeg_quality;
+        sl->jpeg = jpeg;
+        sl->want_rgba = out_path && !jpeg;
+        sl->film_out = nullptr;
+        enqueue_frame(c, *sl);
+        sl->busy = true;
+        sl->ticket = c->next_ticket++;
+        *ticket = sl->ticket;
+        return RR_OK;
+    });
+}
+
+int rr_frame_complete(rr_ctx* c, uint64_t ticket, rr_frame_timing* timing, rr_frame_stats* stats) {
+    if (!c) return fail(RR_EINVAL, "NULL ctx");
+    if (ticket != c->next_complete) return fail(RR_EINVAL, "frames must be completed in submission order");
+    FrameSlot* sl = slot_for(c, ticket);
+    if (!sl->busy || sl->ticket != ticket) return fail(RR_EINVAL, "unknown ticket");
+    auto release = [&] {
+        sl->busy = false;
+        c->next_complete = ticket + 1;
+    };
+    const int rc = guarded([&] {
+        finish_frame(c, *sl);
+        const FrameSetup& fs = sl->fs;
+        const FrameRun& r = sl->r;
         const double t_sync = unix_now();
         // the device JPEG transform + readback belong to "saving" (Blender's
         // write_still); move that device interval out of the render span
-        tm.finished_rendering_at = jpeg ? t_sync - r.readback_ms * 1e-3 : t_sync;
-        tm.file_saving_started_at = tm.finished_rendering_at;
+        sl->tm.finished_rendering_at = sl->jpeg ? t_sync - r.readback_ms * 1e-3 : t_sync;
+        sl->tm.file_saving_started_at = sl->tm.finished_rendering_at;
         uint64_t bytes = 0;
         const auto t_enc = std::chrono::steady_clock::now();
-        if (jpeg) {
+        if (sl->jpeg) {
             std::vector<uint8_t> data;
-            if (!encode_jpeg_coeffs(reinterpret_cast<const int16_t*>(c->host_coeffs.ptr), fs.W, fs.H, jpeg_quality,
+            if (!encode_jpeg_coeffs(reinterpret_cast<const int16_t*>(sl->host_coeffs.ptr), fs.W, fs.H, sl->quality,
                                     data))
                 return fail(RR_EINVAL, "JPEG encode failed");
-            const std::string path = std::string(out_path) + ".jpg";
+            const std::string path = sl->out_path + ".jpg";
             if (!write_file(path, data)) return fail(RR_EIO, "cannot write " + path + ": " + std::strerror(errno));
             bytes = data.size();
-        } else if (out_path) {
-            const int rc = do_encode(c->host_rgba.ptr, fs.W, fs.H, out_path, format, jpeg_quality, &bytes);
-            if (rc != RR_OK) return rc;
+        } else if (!sl->out_path.empty()) {
+            const int e = do_encode(sl->host_rgba.ptr, fs.W, fs.H, sl->out_path.c_str(), sl->format.c_str(),
+                                    sl->quality, &bytes);
+            if (e != RR_OK) return e;
         }
         const double enc_ms = ms_since(t_enc);
-        tm.file_saving_finished_at = unix_now();
-        if (timing) *timing = tm;
+        sl->tm.file_saving_finished_at = unix_now();
+        if (timing) *timing = sl->tm;
         if (stats) {
-            fill_stats(stats, fs, r, s->dev.n_tris);
-            stats->anim_ms = anim_ms;
+            fill_stats(stats, fs, r, sl->scene->dev.n_tris);
+            stats->anim_ms = sl->anim_ms;
             stats->encode_ms = enc_ms;
             stats->output_bytes = bytes;
-            stats->total_ms = ms_since(t_call);
+            stats->total_ms = ms_since(sl->t_call);
         }
         return RR_OK;
     });
+    release();
+    return rc;
+}
+
+int rr_render_frame(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_params* params, const char* out_path,
+                    const char* format, int32_t jpeg_quality, rr_frame_timing* timing, rr_frame_stats* stats) {
+    if (c && c->next_complete != c->next_ticket)
+        return fail(RR_EBUSY, "rr_render_frame while submitted frames are pending");
+    uint64_t t = 0;
+    const int rc = rr_frame_submit(c, s, frame, params, out_path, format, jpeg_quality, &t);
+    if (rc != RR_OK) return rc;
+    return rr_frame_complete(c, t, timing, stats);
 }
 
 int rr_render_frame_to_memory(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_params* params,
                               float* film, uint8_t* rgba8, rr_frame_stats* stats) {
     if (!c || !s) return fail(RR_EINVAL, "NULL ctx or scene");
     if (s->ctx && s->ctx != c) return fail(RR_EINVAL, "scene belongs to another context");
+    if (c->next_complete != c->next_ticket) return fail(RR_EBUSY, "submitted frames are pending");
+    FrameSlot* sl = slot_for(c, c->next_ticket);
     return guarded([&] {
-        const auto t_call = std::chrono::steady_clock::now();
-        FrameSetup fs = setup_frame(s->desc, frame, params);
-        FrameRun r = run_frame(c, s, fs, film);
-        if (rgba8) std::memcpy(rgba8, c->host_rgba.ptr, (size_t)fs.W * fs.H * 4);
+        sl->t_call = std::chrono::steady_clock::now();
+        sl->fs = setup_frame(s->desc, frame, params);
+        sl->scene = s;
+        sl->out_path.clear();
+        sl->format.clear();
+        sl->jpeg = false;
+        sl->want_rgba = true;
+        sl->film_out = film;
+        enqueue_frame(c, *sl);
+        finish_frame(c, *sl);
+        sl->film_out = nullptr;
+        const FrameSetup& fs = sl->fs;
+        if (rgba8) std::memcpy(rgba8, sl->host_rgba.ptr, (size_t)fs.W * fs.H * 4);
         if (stats) {
-            fill_stats(stats, fs, r, s->dev.n_tris);
-            stats->total_ms = ms_since(t_call);
+            fill_stats(stats, fs, sl->r, s->dev.n_tris);
+            stats->total_ms = ms_since(sl->t_call);
         }
         return RR_OK;
     });
@@ -546,8 +655,11 @@ int rr_debug_frame_state(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_
         FrameSetup fs = setup_frame(s->desc, frame, params);
         const int n = s->dev.n_tris;
         if (c) {  // host-only queries (c == NULL) skip the device part
+            if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
             set_device(c);
-            prepare_frame(c, s, fs);
+            PinnedBuf staging;
+            prepare_frame(c, s, fs, staging);
+            RR_HIP(hipStreamSynchronize(c->stream));
         }
         if (tris_world && n > 0) {
             std::vector<float4> w((size_t)3 * n);
@@ -583,9 +695,11 @@ int rr_debug_bvh(rr_ctx* c, rr_scene* s, int32_t frame, uint32_t* keys, uint32_t
                  float* boxes) {
     if (!c || !s) return fail(RR_EINVAL, "NULL ctx or scene");
     return guarded([&] {
+        if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
-        prepare_frame(c, s, fs);
+        PinnedBuf staging;
+        prepare_frame(c, s, fs, staging);
         DevScene& d = s->dev;
         const int n = d.n_tris;
         hipStream_t st = c->stream;
@@ -614,9 +728,11 @@ int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t n, const float
                    uint8_t* occluded) {
     if (!c || !s || n < 0 || (n > 0 && !rays)) return fail(RR_EINVAL, "bad arguments");
     return guarded([&] {
+        if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
-        prepare_frame(c, s, fs);
+        PinnedBuf staging;
+        prepare_frame(c, s, fs, staging);
         hipStream_t st = c->stream;
         DevBuf<float4> dr, dh;
         DevBuf<int32_t> dp;

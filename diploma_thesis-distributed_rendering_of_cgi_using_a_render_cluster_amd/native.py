@@ -18,6 +18,8 @@ LIB_PATH = os.path.join(_HERE, "lib", "librr.so")
 SHIM_PATH = os.path.join(_HERE, "lib", "rr-blender-shim")
 
 RR_OK, RR_ENOENT, RR_EIO, RR_ENOMEM, RR_ENODEV, RR_EINVAL, RR_ENOTSUP = 0, -2, -5, -12, -19, -22, -95
+RR_EBUSY = -16
+RR_MAX_FRAMES_IN_FLIGHT = 2
 RR_VIEW_SCENE, RR_VIEW_STANDARD, RR_VIEW_RAW = -1, 0, 1
 RR_CAM_FLOATS, RR_LIGHT_FLOATS, RR_MAT_FLOATS, RR_RENDER_INTS, RR_RENDER_FLOATS = 16, 12, 12, 8, 4
 
@@ -69,6 +71,7 @@ KERNEL_CLASSES = ["build", "primary", "extend", "shadow", "accumulate", "shade"]
 # Every symbol include/rr.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "rr_render_params_default", "rr_abi_version", "rr_create", "rr_scene_load", "rr_render_frame",
+    "rr_frame_submit", "rr_frame_complete",
     "rr_render_frame_to_memory", "rr_scene_resolution", "rr_encode_image", "rr_last_error",
     "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
     "rr_debug_trace", "rr_debug_object_matrix",
@@ -98,6 +101,9 @@ def lib() -> ctypes.CDLL:
         "rr_scene_load": (c_int, [P, ctypes.c_char_p, ctypes.POINTER(P)]),
         "rr_render_frame": (c_int, [P, P, i32, ctypes.POINTER(RenderParams), ctypes.c_char_p, ctypes.c_char_p, i32,
                                     ctypes.POINTER(FrameTiming), ctypes.POINTER(FrameStats)]),
+        "rr_frame_submit": (c_int, [P, P, i32, ctypes.POINTER(RenderParams), ctypes.c_char_p, ctypes.c_char_p, i32,
+                                    ctypes.POINTER(ctypes.c_uint64)]),
+        "rr_frame_complete": (c_int, [P, ctypes.c_uint64, ctypes.POINTER(FrameTiming), ctypes.POINTER(FrameStats)]),
         "rr_render_frame_to_memory": (c_int, [P, P, i32, ctypes.POINTER(RenderParams), f32p, u8p,
                                               ctypes.POINTER(FrameStats)]),
         "rr_scene_resolution": (c_int, [P, ctypes.POINTER(RenderParams), i32p, i32p]),
@@ -244,6 +250,24 @@ class RenderContext:
                                      out_path.encode() if out_path is not None else None,
                                      fmt.encode() if (fmt is not None and out_path is not None) else None,
                                      int(quality), ctypes.byref(t), ctypes.byref(s)), self.handle)
+        return t, s
+
+    def submit_frame(self, scene: Scene, frame: int, params: RenderParams | None = None,
+                     out_path: str | None = None, fmt: str | None = "JPEG", quality: int = 90) -> int:
+        """rr_frame_submit: enqueue the frame's device work, return its ticket."""
+        t = ctypes.c_uint64()
+        _check(lib().rr_frame_submit(self.handle, scene.handle, int(frame),
+                                     ctypes.byref(params) if params else None,
+                                     out_path.encode() if out_path is not None else None,
+                                     fmt.encode() if (fmt is not None and out_path is not None) else None,
+                                     int(quality), ctypes.byref(t)), self.handle)
+        return int(t.value)
+
+    def complete_frame(self, ticket: int):
+        """rr_frame_complete: wait, encode + write; (timing, stats)."""
+        t, s = FrameTiming(), FrameStats()
+        _check(lib().rr_frame_complete(self.handle, ctypes.c_uint64(ticket), ctypes.byref(t), ctypes.byref(s)),
+               self.handle)
         return t, s
 
     def render_to_memory(self, scene: Scene, frame: int, params: RenderParams | None = None,

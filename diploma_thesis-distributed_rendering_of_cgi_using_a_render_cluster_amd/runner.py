@@ -63,7 +63,8 @@ class BackendRunner:
             self._scenes[key] = s
         return s
 
-    def render_frame(self, job: BlenderJob, frame_index: int) -> FrameRenderTime:
+    def _prepare(self, job: BlenderJob, frame_index: int):
+        """Path resolution, checks and output naming of runner/mod.rs:72-139."""
         try:
             blend = parse_with_base_directory_prefix(job.project_file_path, self.base_directory_path)
             script = parse_with_base_directory_prefix(job.render_script_path, self.base_directory_path)
@@ -83,6 +84,10 @@ class BackendRunner:
         if job.output_file_format not in EXTENSIONS:
             raise RenderError(f"Unsupported output file format {job.output_file_format!r}")
         out_no_ext = output_path_without_extension(str(out_dir), job.output_file_name_format, frame_index)
+        return blend, out_no_ext
+
+    def render_frame(self, job: BlenderJob, frame_index: int) -> FrameRenderTime:
+        blend, out_no_ext = self._prepare(job, frame_index)
         with self._lock:
             scene = self._scene(blend)
             started_process_at = time.time()
@@ -93,3 +98,45 @@ class BackendRunner:
         frt = FrameRenderTime.from_timing(started_process_at, timing, exited_process_at)
         self.tracer.trace_new_rendered_frame(frame_index, frt)
         return frt
+
+    def render_frames(self, job: BlenderJob, frame_indices, on_frame=None) -> list:
+        """Render a worker's queued frames in order with frame N+1's device
+        work in flight while frame N is encoded and written (rr_frame_submit /
+        rr_frame_complete). Every frame still gets its own
+        file, FrameRenderTime and trace entry, exactly as render_frame would
+        produce them; on_frame(frame_index, frt, stats) is called as each one
+        completes. started_process_at is the frame's submit time."""
+        frames = list(frame_indices)
+        out = []
+        with self._lock:
+            pending = []  # (frame, ticket, started_process_at)
+
+            def retire():
+                f, t, t0 = pending.pop(0)
+                timing, stats = self.ctx.complete_frame(t)
+                frt = FrameRenderTime.from_timing(t0, timing, time.time())
+                self.last_stats = stats
+                self.tracer.trace_new_rendered_frame(f, frt)
+                out.append(frt)
+                if on_frame is not None:
+                    on_frame(f, frt, stats)
+
+            try:
+                for f in frames:
+                    blend, out_no_ext = self._prepare(job, f)
+                    scene = self._scene(blend)
+                    t0 = time.time()
+                    ticket = self.ctx.submit_frame(scene, f, self.params, out_no_ext, job.output_file_format, 90)
+                    pending.append((f, ticket, t0))
+                    if len(pending) >= 2:
+                        retire()
+                while pending:
+                    retire()
+            finally:
+                while pending:  # an error above: drain what is still in flight
+                    f, t, _ = pending.pop(0)
+                    try:
+                        self.ctx.complete_frame(t)
+                    except Exception:
+                        pass
+        return out

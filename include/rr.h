@@ -40,6 +40,10 @@ extern "C" {
 #define RR_EINVAL (-22)  /* bad argument / malformed scene */
 #define RR_ENODEV (-19)  /* HIP device unavailable / kernel launch failure */
 #define RR_ENOTSUP (-95) /* unsupported output format or scene feature */
+#define RR_EBUSY (-16)   /* rr_frame_submit with RR_MAX_FRAMES_IN_FLIGHT frames pending */
+
+/* Frames a context keeps between rr_frame_submit and rr_frame_complete. */
+#define RR_MAX_FRAMES_IN_FLIGHT 2
 
 typedef struct rr_ctx rr_ctx;
 typedef struct rr_scene rr_scene;
@@ -148,6 +152,25 @@ int rr_render_frame(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
                     const rr_render_params* params, const char* out_path,
                     const char* format, int32_t jpeg_quality,
                     rr_frame_timing* timing, rr_frame_stats* stats);
+
+/* Two-phase form of rr_render_frame, for a worker that keeps its next queued
+ * frame in flight (eager-naive-coarse and dynamic keep
+ * frames queued per worker, master/src/cluster/strategies.rs:70-150,250-405,
+ * while the reference worker renders them strictly one after another,
+ * worker/src/rendering/queue.rs:79-118). rr_frame_submit evaluates the
+ * animation, enqueues the frame's device work and returns without waiting;
+ * rr_frame_complete waits for that frame's device work, encodes and writes
+ * the image and fills timing/stats exactly as rr_render_frame does. The
+ * intended loop is submit(N+1), complete(N): the host encodes and writes
+ * frame N while the GPU renders N+1. At most RR_MAX_FRAMES_IN_FLIGHT frames
+ * may be pending (RR_EBUSY otherwise); they complete in submission order.
+ * rr_render_frame == submit + complete. Same arguments and errors as
+ * rr_render_frame; a failed complete still retires its ticket. */
+int rr_frame_submit(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
+                    const rr_render_params* params, const char* out_path,
+                    const char* format, int32_t jpeg_quality, uint64_t* ticket);
+int rr_frame_complete(rr_ctx* ctx, uint64_t ticket, rr_frame_timing* timing,
+                      rr_frame_stats* stats);
 
 /* Render one frame into caller memory (no file). film_rgba: W*H*4 floats of
  * mean linear radiance (alpha = 1); rgba8: W*H*4 bytes after the view

@@ -276,3 +276,46 @@ def test_blender_cli_shim(rr, tmp_path):
     bad = subprocess.run([rr.SHIM_PATH, S04, "--", "--render-format", "PNG"], capture_output=True, text=True,
                          timeout=60)
     assert "Missing render-and-timing-script arguments!" in bad.stdout
+
+
+def test_pipelined_frames_match_serial(ctx, rr, tmp_path, s04):
+    """rr_frame_submit / rr_frame_complete with two frames in flight writes
+    byte-identical files to rr_render_frame, in submission order."""
+    p = rr.default_params(width=160, height=90, spp=4)
+    serial = {}
+    for f in (3, 4, 5):
+        ctx.render_frame(s04, f, p, str(tmp_path / f"s{f}"), "JPEG", 90)
+        serial[f] = (tmp_path / f"s{f}.jpg").read_bytes()
+    t3 = ctx.submit_frame(s04, 3, p, str(tmp_path / "p3"), "JPEG", 90)
+    t4 = ctx.submit_frame(s04, 4, p, str(tmp_path / "p4"), "JPEG", 90)
+    with pytest.raises(rr.RRError) as e:  # a third frame in flight
+        ctx.submit_frame(s04, 5, p, str(tmp_path / "p5"), "JPEG", 90)
+    assert e.value.code == rr.native.RR_EBUSY
+    with pytest.raises(rr.RRError):  # out of order
+        ctx.complete_frame(t4)
+    tm3, st3 = ctx.complete_frame(t3)
+    t5 = ctx.submit_frame(s04, 5, p, str(tmp_path / "p5"), "PNG", 90)
+    tm4, _ = ctx.complete_frame(t4)
+    tm5, _ = ctx.complete_frame(t5)
+    assert (tmp_path / "p3.jpg").read_bytes() == serial[3]
+    assert (tmp_path / "p4.jpg").read_bytes() == serial[4]
+    assert (tmp_path / "p5.png").is_file()
+    for tm in (tm3, tm4, tm5):
+        assert tm.loaded_at <= tm.started_rendering_at <= tm.finished_rendering_at <= tm.file_saving_finished_at
+    assert st3.camera_rays == 160 * 90 * 4
+    # a synchronous call works again once nothing is pending
+    ctx.render_frame(s04, 6, p, str(tmp_path / "s6"), "JPEG", 90)
+
+
+def test_backend_runner_render_frames_pipelined(rr, tmp_path):
+    """BackendRunner.render_frames: every frame written, traced once, in order."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    job = rr.BlenderJob.load_from_file(os.path.join(root, "jobs", "04_very-simple_demo_10f-1w.toml"))
+    job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": str(tmp_path)})
+    runner = rr.BackendRunner(root, params=rr.default_params(width=96, height=54, spp=2))
+    seen = []
+    frts = runner.render_frames(job, job.frames(), on_frame=lambda f, frt, st: seen.append(f))
+    runner.close()
+    assert seen == job.frames() and len(frts) == len(seen)
+    assert sorted(os.listdir(tmp_path)) == [f"{f:06d}.jpg" for f in job.frames()]
