@@ -419,8 +419,11 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, float4* __r
     if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
 }
 
+#ifndef RR_FUSED_WAVES
+#define RR_FUSED_WAVES 1
+#endif
 template <bool kCount, bool kLds>
-__global__ __launch_bounds__(kBlock) void k_primary(FrameConsts fc, SceneArgs sa, int np, float4* __restrict__ rad,
+__global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_primary(FrameConsts fc, SceneArgs sa, int np, float4* __restrict__ rad,
                                                     PathQueue out, ShadowQueue sq, uint32_t seg_cap,
                                                     uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
                                                     int32_t* __restrict__ spill,
@@ -488,7 +491,7 @@ RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueu
 }
 
 template <bool kCount, bool kLds>
-__global__ __launch_bounds__(kBlock) void k_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in, SegIn si,
+__global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in, SegIn si,
                                                    float4* __restrict__ rad, PathQueue out, ShadowQueue sq,
                                                    SegOut sg, int32_t* __restrict__ spill,
                                                    unsigned long long* __restrict__ tc) {
