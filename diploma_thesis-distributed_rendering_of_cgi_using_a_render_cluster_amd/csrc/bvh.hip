@@ -349,6 +349,73 @@ __global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restr
     }
 }
 
+// BVH4 collapse, step 1: depth parity of every internal node (walk to the
+// root through node_parent); flags[i] = 1 and rank[i] = 1 for even depth.
+__global__ __launch_bounds__(kBlock) void k_depth_parity(int ni, const int32_t* __restrict__ node_parent,
+                                                         uint32_t* __restrict__ flags, uint32_t* __restrict__ rank) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= ni) return;
+    int depth = 0;
+    for (int p = node_parent[i]; p >= 0 && depth < 4096; p = node_parent[p >> 1]) ++depth;
+    const uint32_t even = (depth & 1) ? 0u : 1u;
+    flags[i] = even;
+    rank[i] = even;
+}
+
+// BVH4 collapse, step 2 (after an exclusive scan of rank): every even-depth
+// BVH2 node i becomes BVH4 node rank[i]; its children, in slot order, are for
+// each side (left, right) either that leaf child, or both children of the
+// odd-depth internal child (leaf, or BVH4 node rank[grandchild]). Boxes come
+// from the parents' child boxes, so they are the BVH2 boxes bit for bit.
+__global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNode* __restrict__ nodes,
+                                                      const uint32_t* __restrict__ flags,
+                                                      const uint32_t* __restrict__ rank,
+                                                      Bvh4Node* __restrict__ out) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= ni || !flags[i]) return;
+    float lo[3][4], hi[3][4];
+    int ref[4];
+    int m = 0;
+    auto put = [&](const BvhNode& nd, int side) {
+        const float* f = reinterpret_cast<const float*>(&nd) + 6 * side;
+        const int c = side ? nd.d.y : nd.d.x;
+        for (int a = 0; a < 3; ++a) {
+            lo[a][m] = f[a];
+            hi[a][m] = f[3 + a];
+        }
+        ref[m] = c < 0 ? c : (int)rank[c];
+        ++m;
+    };
+    const BvhNode nd = nodes[i];
+    for (int side = 0; side < 2; ++side) {
+        const int c = side ? nd.d.y : nd.d.x;
+        if (c < 0 || n == 1) {
+            put(nd, side);
+        } else {
+            const BvhNode cn = nodes[c];
+            put(cn, 0);
+            put(cn, 1);
+        }
+    }
+    for (; m < 4; ++m) {
+        for (int a = 0; a < 3; ++a) {
+            lo[a][m] = 0.0f;
+            hi[a][m] = 0.0f;
+        }
+        ref[m] = kEmpty4;
+    }
+    Bvh4Node o;
+    o.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
+    o.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
+    o.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
+    o.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
+    o.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
+    o.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+    o.child = make_int4(ref[0], ref[1], ref[2], ref[3]);
+    o.pad = make_int4(0, 0, 0, 0);
+    out[rank[i]] = o;
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 void exclusive_scan(DevScene& s, uint32_t* data, int m, hipStream_t st) {
@@ -366,13 +433,15 @@ void DevScene::release() {
     tri_world.release(); bounds.release();
     for (int k = 0; k < 2; ++k) { keys[k].release(); vals[k].release(); }
     hist.release(); scan_part.release(); children.release(); node_parent.release();
-    leaf_parent.release(); flags.release(); nodes.release(); tris.release();
+    leaf_parent.release(); flags.release(); nodes.release(); tris.release(); nodes4.release(); rank4.release();
+    has4 = false;
     built = false;
     uploaded = false;
 }
 
-void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof) {
+void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4) {
     const int n = s.n_tris;
+    s.has4 = false;
     if (n <= 0) {
         s.built = true;
         return;
@@ -422,6 +491,23 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof) {
     k_refit<<<nb, kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr, s.leaf_parent.ptr,
                                    s.node_parent.ptr, s.children.ptr, s.flags.ptr, s.nodes.ptr,
                                    s.tris.ptr);
+    if (want4) {  // BVH4 collapse (flags are free again once refit is done)
+        const int ni = n > 1 ? n - 1 : 1;
+        s.rank4.ensure((size_t)ni + 1);
+        s.nodes4.ensure((size_t)ni);
+        if (n > 1) {
+            k_depth_parity<<<cdiv(ni, kBlock), kBlock, 0, st>>>(ni, s.node_parent.ptr, s.flags.ptr, s.rank4.ptr);
+        } else {
+            const uint32_t one = 1u;
+            RR_HIP(hipMemcpyAsync(s.flags.ptr, &one, sizeof one, hipMemcpyHostToDevice, st));
+            RR_HIP(hipMemcpyAsync(s.rank4.ptr, &one, sizeof one, hipMemcpyHostToDevice, st));
+        }
+        RR_HIP(hipMemsetAsync(s.rank4.ptr + ni, 0, sizeof(uint32_t), st));
+        exclusive_scan(s, s.rank4.ptr, ni + 1, st);  // rank4[ni] = BVH4 node count
+        k_collapse4<<<cdiv(ni, kBlock), kBlock, 0, st>>>(ni, n, s.nodes.ptr, s.flags.ptr, s.rank4.ptr,
+                                                         s.nodes4.ptr);
+        s.has4 = true;
+    }
     if (prof) prof->end(st);
     RR_HIP(hipGetLastError());
     s.built = true;

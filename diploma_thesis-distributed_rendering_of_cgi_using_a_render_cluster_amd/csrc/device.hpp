@@ -69,6 +69,9 @@ struct DevScene {
     // acceleration structure consumed by traversal
     DevBuf<BvhNode> nodes;  // max(n-1, 1)
     DevBuf<TriPack> tris;   // n, leaf order
+    DevBuf<Bvh4Node> nodes4;   // BVH4 collapse of `nodes` (split path), <= n-1
+    DevBuf<uint32_t> rank4;    // BVH2 node -> BVH4 index (exclusive scan); [n-1] = BVH4 count
+    bool has4 = false;
     std::vector<float> cached_xform;  // obj_xform of the current build
     bool built = false;
     bool uploaded = false;
@@ -158,7 +161,13 @@ struct FrameConsts {
 
 // LBVH build for the current obj_xform (uploaded by the caller).
 // Stream-ordered; no host synchronisation inside.
-void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof = nullptr);
+// want4: also collapse it into the BVH4 the split path traverses.
+void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof = nullptr, bool want4 = false);
+
+// Whether the path kernels take the LDS-resident (fused, BVH2) variant for a
+// scene of these sizes; otherwise the split path over the BVH4 in HBM.
+bool scene_in_lds(int n_tris, int n_mats, int n_lights);
+int split_bvh_width();  // hierarchy width of the split path (4)
 
 // Render all chunks of one frame: film accumulate + tonemap to rgba8.
 // counters_per_chunk receives the device counter layout for stats.
@@ -167,7 +176,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
 
 // Trace a batch of rays (debug / parity entry point).
 void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, float4* d_hits,
-                        int32_t* d_prims, uint8_t* d_occ, hipStream_t st);
+                        int32_t* d_prims, uint8_t* d_occ, hipStream_t st, int width);
 
 // Device JPEG forward transform (jpeg.hip); tab = dct | qinv luma | qinv chroma.
 void jpeg_fdct_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, int16_t* d_out, hipStream_t st);

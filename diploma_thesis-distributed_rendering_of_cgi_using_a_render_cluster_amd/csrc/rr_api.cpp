@@ -166,7 +166,7 @@ void bind_scene(rr_ctx* c, rr_scene* s) {
 // Upload per-frame constants and (re)build the LBVH if object transforms changed.
 // `staging` (pinned, per frame slot) keeps the host-to-device copies
 // asynchronous, so a frame can be enqueued while the previous one still runs.
-bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& staging) {
+bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& staging, bool force4 = false) {
     bind_scene(c, s);
     hipStream_t st = c->stream;
     DevPaths& p = c->paths;
@@ -197,11 +197,12 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     if (nl) RR_HIP(hipMemcpyAsync(p.lights.ptr, up, nl * sizeof(float), hipMemcpyHostToDevice, st));
     RR_HIP(hipMemcpyAsync(p.materials.ptr, up + nl, nm * sizeof(float), hipMemcpyHostToDevice, st));
     DevScene& d = s->dev;
-    const bool rebuild = !d.built || d.cached_xform != fs.obj_xform;
+    const bool want4 = force4 || !scene_in_lds(d.n_tris, (int)(nm / RR_MAT_FLOATS), (int)(nl / RR_LIGHT_FLOATS));
+    const bool rebuild = !d.built || d.cached_xform != fs.obj_xform || (want4 && !d.has4);
     if (rebuild && d.n_tris > 0) {
         d.obj_xform.ensure(nx);
         RR_HIP(hipMemcpyAsync(d.obj_xform.ptr, up + nl + nm, nx * sizeof(float), hipMemcpyHostToDevice, st));
-        build_lbvh(d, st, &p.prof);
+        build_lbvh(d, st, &p.prof, want4);
         d.cached_xform = fs.obj_xform;
     } else if (rebuild) {
         d.built = true;
@@ -404,6 +405,15 @@ int do_encode(const uint8_t* rgba, int W, int H, const char* out_path, const cha
     if (!write_file(path, data)) return fail(RR_EIO, "cannot write " + path + ": " + std::strerror(errno));
     if (bytes) *bytes = data.size();
     return RR_OK;
+}
+
+// BVH width the frame kernels traverse for this scene (2: LDS-resident fused
+// path, 4: split path from HBM).
+int frame_bvh_width(rr_scene* s, const FrameSetup& fs) {
+    return scene_in_lds(s->dev.n_tris, (int)(fs.materials.size() / RR_MAT_FLOATS),
+                        (int)(fs.lights.size() / RR_LIGHT_FLOATS))
+               ? 2
+               : split_bvh_width();
 }
 
 FrameSlot* slot_for(rr_ctx* c, uint64_t ticket) { return &c->slots[ticket % RR_MAX_FRAMES_IN_FLIGHT]; }
@@ -680,7 +690,7 @@ int rr_debug_frame_state(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_
         if (world) std::memcpy(world, fs.world, sizeof fs.world);
         if (render_ints) {
             const int32_t ri[RR_RENDER_INTS] = {fs.W, fs.H, fs.spp, fs.max_bounces, (int32_t)fs.seed,
-                                               fs.view_transform, choose_spp_chunk(fs), 0};
+                                               fs.view_transform, choose_spp_chunk(fs), frame_bvh_width(s, fs)};
             std::memcpy(render_ints, ri, sizeof ri);
         }
         if (render_floats) {
@@ -724,15 +734,55 @@ int rr_debug_bvh(rr_ctx* c, rr_scene* s, int32_t frame, uint32_t* keys, uint32_t
     });
 }
 
-int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t n, const float* rays, float* hits, int32_t* prims,
-                   uint8_t* occluded) {
-    if (!c || !s || n < 0 || (n > 0 && !rays)) return fail(RR_EINVAL, "bad arguments");
+int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* children4, float* boxes4) {
+    if (!c || !s || !n4) return fail(RR_EINVAL, "NULL ctx, scene or n4");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
         PinnedBuf staging;
-        prepare_frame(c, s, fs, staging);
+        prepare_frame(c, s, fs, staging, true);
+        DevScene& d = s->dev;
+        hipStream_t st = c->stream;
+        const int n = d.n_tris;
+        *n4 = 0;
+        if (n > 0) {
+            const int ni = n > 1 ? n - 1 : 1;
+            uint32_t cnt = 0;
+            RR_HIP(hipMemcpyAsync(&cnt, d.rank4.ptr + ni, sizeof cnt, hipMemcpyDeviceToHost, st));
+            RR_HIP(hipStreamSynchronize(st));
+            *n4 = (int32_t)cnt;
+            if (children4 || boxes4) {
+                std::vector<Bvh4Node> nodes(cnt);
+                RR_HIP(hipMemcpyAsync(nodes.data(), d.nodes4.ptr, cnt * sizeof(Bvh4Node), hipMemcpyDeviceToHost, st));
+                RR_HIP(hipStreamSynchronize(st));
+                for (uint32_t i = 0; i < cnt; ++i) {
+                    const Bvh4Node& q = nodes[i];
+                    if (children4) {
+                        children4[4 * i] = q.child.x;
+                        children4[4 * i + 1] = q.child.y;
+                        children4[4 * i + 2] = q.child.z;
+                        children4[4 * i + 3] = q.child.w;
+                    }
+                    if (boxes4) std::memcpy(boxes4 + 24 * (size_t)i, &q, 24 * sizeof(float));
+                }
+            }
+        }
+        return RR_OK;
+    });
+}
+
+int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int32_t n, const float* rays,
+                   float* hits, int32_t* prims, uint8_t* occluded) {
+    if (!c || !s || n < 0 || (n > 0 && !rays)) return fail(RR_EINVAL, "bad arguments");
+    if (bvh_width != 0 && bvh_width != 2 && bvh_width != 4) return fail(RR_EINVAL, "bvh_width must be 0, 2 or 4");
+    return guarded([&] {
+        if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
+        FrameSetup fs = setup_frame(s->desc, frame, nullptr);
+        set_device(c);
+        PinnedBuf staging;
+        const int width = bvh_width ? bvh_width : frame_bvh_width(s, fs);
+        prepare_frame(c, s, fs, staging, width == 4);
         hipStream_t st = c->stream;
         DevBuf<float4> dr, dh;
         DevBuf<int32_t> dp;
@@ -743,7 +793,7 @@ int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t n, const float
         dp.ensure(m);
         dq.ensure(m);
         if (n > 0) RR_HIP(hipMemcpyAsync(dr.ptr, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice, st));
-        trace_batch_device(s->dev, c->paths, n, dr.ptr, dh.ptr, dp.ptr, dq.ptr, st);
+        trace_batch_device(s->dev, c->paths, n, dr.ptr, dh.ptr, dp.ptr, dq.ptr, st, width);
         std::vector<float4> h(m);
         if (n > 0) {
             RR_HIP(hipMemcpyAsync(h.data(), dh.ptr, n * sizeof(float4), hipMemcpyDeviceToHost, st));

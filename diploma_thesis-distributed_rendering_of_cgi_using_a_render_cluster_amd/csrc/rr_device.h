@@ -33,6 +33,21 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "node must be one 64-byte line");
 
+// 4-wide node for scenes traversed from HBM (split path): the
+// LBVH collapsed two levels at a time (every even-depth BVH2 node becomes one
+// node whose children are its grandchildren, or its leaf children). 128 B =
+// one L2/HBM line carries four child boxes (SoA, so the four slab tests
+// vectorise) and four child refs: >= 0 BVH4 node, < 0 ~leaf, kEmpty4 unused.
+// Per ray this halves the node fetches of the BVH2 walk, and each fetched
+// line is fully used (a BVH2 node used 64 B of its 128 B line).
+struct alignas(16) Bvh4Node {
+    float4 lox, loy, loz, hix, hiy, hiz;
+    int4 child;
+    int4 pad;
+};
+static_assert(sizeof(Bvh4Node) == 128, "BVH4 node must be one 128-byte line");
+constexpr int kEmpty4 = 0x7fffffff;
+
 // Triangle in leaf order, 48 B: v0 | e1 = v1-v0 | e2 = v2-v0, with the original
 // triangle id and material id in the .w lanes.
 struct alignas(16) TriPack {
@@ -250,6 +265,12 @@ RR_HD void closest_tri_nb(const TriPack& tp, int idx, float3 o, float3 d, float 
     }
 }
 
+#ifndef RR_BVH4_SORT
+#define RR_BVH4_SORT 0
+#endif
+#ifndef RR_LEAF_LOOP
+#define RR_LEAF_LOOP 0
+#endif
 #ifndef RR_TRI_BRANCHLESS
 #define RR_TRI_BRANCHLESS 0
 #endif
@@ -304,11 +325,16 @@ struct TravStack {
     int* spill;     // &spill_base[global thread], stride spill_stride
     int spill_stride;
     int sp;
+    // A push beyond kLdsStack + kSpillStack entries is dropped (never reached
+    // by the LBVH/BVH4 depths of the test and bench scenes); the oracle's stack
+    // has the same capacity and the same rule (ORC_MAXDEPTH).
     RR_D void push(int x) {
         if (sp < kLdsStack) {
             lds[sp * kBlock] = x;
         } else if (sp < kLdsStack + kSpillStack) {
             spill[(sp - kLdsStack) * spill_stride] = x;
+        } else {
+            return;
         }
         ++sp;
     }
@@ -361,6 +387,21 @@ struct TravState {
         bool hl = slab(o, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
         bool hr = slab(o, invd, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
         const int cl = nd.d.x, cr = nd.d.y;
+#if RR_LEAF_LOOP
+        // passing leaf children, left first, as a loop: a wave runs the leaf
+        // test as often as its busiest lane needs (lanes with a left leaf and
+        // lanes with a right leaf share one pass)
+        uint32_t leaves = (hl && cl < 0 ? 1u : 0u) | (hr && cr < 0 ? 2u : 0u);
+        if (leaves & 1u) hl = false;
+        if (leaves & 2u) hr = false;
+        while (leaves) {
+            const int r = (leaves & 1u) ? cl : cr;
+            leaves &= leaves - 1;
+            if (kCount) ++cnt.tris;
+            leaf_test(load_tri(tris, ~r), ~r, o, d, tmin, h);
+            if (kAnyHit && h.idx >= 0) return true;
+        }
+#else
         if (hl && cl < 0) {
             if (kCount) ++cnt.tris;
             leaf_test(load_tri(tris, ~cl), ~cl, o, d, tmin, h);
@@ -373,6 +414,7 @@ struct TravState {
             if (kAnyHit && h.idx >= 0) return true;
             hr = false;
         }
+#endif
         if (hl && hr) {
             const bool left_first = tl <= tr;
             st.push(left_first ? cr : cl);
@@ -385,6 +427,122 @@ struct TravState {
             if (st.sp == 0) return true;
             node = st.pop();
         }
+        return false;
+    }
+};
+
+RR_D Bvh4Node load_node4(const Bvh4Node* __restrict__ p, int i) { return p[i]; }
+
+RR_D float f4get(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+RR_D int i4get(const int4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
+// Ordering of a node's hit children: ascending entry distance, ties by slot.
+struct ChildKey {
+    float t;
+    int slot, ref;
+};
+RR_D void cswap(ChildKey& a, ChildKey& b) {
+    if (b.t < a.t || (b.t == a.t && b.slot < a.slot)) {
+        const ChildKey x = a;
+        a = b;
+        b = x;
+    }
+}
+
+// Resumable traversal of the BVH4 (same contract as TravState): leaf children
+// whose boxes pass are intersected at once in slot order; the hit internal
+// children are sorted by (entry t, slot) with a 5-exchange network, the
+// nearest is visited next and the others pushed farthest first.
+// oracle/rr_oracle.c trace4() is the same walk.
+template <bool kAnyHit, bool kCount = false>
+struct TravState4 {
+    float3 o, d, invd;
+    float tmin;
+    Hit h;
+    int node;
+    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_) {
+        o = o_;
+        d = d_;
+        tmin = tmin_;
+        h.t = tmax_;
+        h.u = h.v = 0.0f;
+        h.idx = -1;
+        h.orig = -1;
+        invd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        node = 0;
+    }
+    template <typename TriP, typename Stack>
+    RR_D bool step(const Bvh4Node* __restrict__ nodes, TriP tris, Stack& st, TravCount& cnt) {
+        if (kCount) ++cnt.nodes;
+        const float tcur = h.t;
+        float tn[4];
+        int ref[4];
+        uint32_t leaves = 0, inner = 0;
+        {
+            const Bvh4Node nd = load_node4(nodes, node);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                ref[c] = i4get(nd.child, c);
+                const bool hit = ref[c] != kEmpty4 &&
+                                 slab(o, invd, f4get(nd.lox, c), f4get(nd.loy, c), f4get(nd.loz, c),
+                                      f4get(nd.hix, c), f4get(nd.hiy, c), f4get(nd.hiz, c), tmin, tcur, tn[c]);
+                if (hit) {
+                    if (ref[c] < 0) leaves |= 1u << c;
+                    else inner |= 1u << c;
+                }
+            }
+        }
+        // passing leaves in slot order; the loop runs as often as the lane with
+        // the most leaves needs (usually once), not once per slot
+        while (leaves) {
+            const int c = __builtin_ctz(leaves);
+            leaves &= leaves - 1;
+            const int r = c == 0 ? ref[0] : c == 1 ? ref[1] : c == 2 ? ref[2] : ref[3];
+            if (kCount) ++cnt.tris;
+            leaf_test(load_tri(tris, ~r), ~r, o, d, tmin, h);
+            if (kAnyHit && h.idx >= 0) return true;
+        }
+        if (!inner) {
+            if (st.sp == 0) return true;
+            node = st.pop();
+            return false;
+        }
+#if RR_BVH4_SORT
+        const float inf = __builtin_huge_valf();
+        ChildKey k[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            k[c].slot = c;
+            k[c].ref = ref[c];
+            k[c].t = (inner >> c) & 1u ? tn[c] : inf;
+        }
+        cswap(k[0], k[1]);
+        cswap(k[2], k[3]);
+        cswap(k[0], k[2]);
+        cswap(k[1], k[3]);
+        cswap(k[1], k[2]);
+        if (k[3].t != inf) st.push(k[3].ref);
+        if (k[2].t != inf) st.push(k[2].ref);
+        if (k[1].t != inf) st.push(k[1].ref);
+        node = k[0].ref;
+#else
+        // nearest hit child next (ties: lower slot); the other hit children are
+        // pushed in descending slot order (so they pop in slot order)
+        int best = __builtin_ctz(inner);
+        float bt = tn[best == 0 ? 0 : best == 1 ? 1 : best == 2 ? 2 : 3];
+#pragma unroll
+        for (int c = 1; c < 4; ++c)
+            if (((inner >> c) & 1u) && tn[c] < bt) {
+                bt = tn[c];
+                best = c;
+            }
+        const uint32_t rest = inner & ~(1u << best);
+        if (rest & 8u) st.push(ref[3]);
+        if (rest & 4u) st.push(ref[2]);
+        if (rest & 2u) st.push(ref[1]);
+        if (rest & 1u) st.push(ref[0]);
+        node = best == 0 ? ref[0] : best == 1 ? ref[1] : best == 2 ? ref[2] : ref[3];
+#endif
         return false;
     }
 };

@@ -29,6 +29,7 @@
 
 #include <cstdlib>
 #include <map>
+#include <type_traits>
 #include <string>
 
 #include "device.hpp"
@@ -341,6 +342,7 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
 // Scene data as kernel arguments (global pointers + counts).
 struct SceneArgs {
     const BvhNode* nodes;
+    const Bvh4Node* nodes4;  // split path (large scenes)
     const TriPack* tris;
     const float* mats;
     const float* lights;
@@ -580,12 +582,23 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
 #define RR_TRACE_WAVES 7
 #endif
 constexpr int kRefillBelow = RR_REFILL_BELOW;
+// Hierarchy of the split path: 4 = BVH4 collapse (Bvh4Node), 2 = the LBVH.
+#ifndef RR_SPLIT_WIDTH
+#define RR_SPLIT_WIDTH 2
+#endif
+template <bool kAnyHit, bool kCount>
+using SplitTrav = std::conditional_t<RR_SPLIT_WIDTH == 4, TravState4<kAnyHit, kCount>, TravState<kAnyHit, kCount>>;
+RR_D auto split_nodes(const SceneArgs& sa) {
+    if constexpr (RR_SPLIT_WIDTH == 4) return sa.nodes4;
+    else return sa.nodes;
+}
 constexpr int kQGroups = 64;   // append groups per queue (one lane each in QueueMap)
 constexpr int kQStride = 32;   // words between group counters (128 B)
 
 // map(k) -> slot is called by every lane of the wave (converged: QueueMap
 // shuffles); ray_of(slot, ...) and done(k, slot, hit) per lane.
-template <bool kAnyHit, bool kCount, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
+// TS: TravState4<kAnyHit, kCount> (BVH4 nodes) or TravState (BVH2).
+template <typename TS, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack& st, TravCount& cnt, MapFn&& map,
                        RayFn&& ray_of, DoneFn&& done) {
     const int lane = threadIdx.x & 63;
@@ -594,7 +607,7 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack&
     const int per = (count + nw - 1) / nw;
     int next = (int)wave_id() * per;  // wave-uniform cursor into this wave's range
     const int end = min(count, next + per);
-    TravState<kAnyHit, kCount> ts;
+    TS ts;
     int j = -1;
     uint32_t js = 0;  // queue slot of ray j
     for (;;) {
@@ -723,8 +736,8 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameC
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
-    trace_refill<false, kCount>(
-        sa.nodes, sa.tris, sa.n_tris, np, st, cnt, [](int p) { return (uint32_t)p; },
+    trace_refill<SplitTrav<false, kCount>>(
+        split_nodes(sa), sa.tris, sa.n_tris, np, st, cnt, [](int p) { return (uint32_t)p; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
             const int sl = (int)fc.div_npix.div(p);
             const int pix = (int)p - sl * fc.npix;
@@ -774,8 +787,8 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_extend(SceneAr
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
-    trace_refill<false, kCount>(
-        sa.nodes, sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
+    trace_refill<SplitTrav<false, kCount>>(
+        split_nodes(sa), sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
@@ -831,8 +844,8 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_shadow_refill(SceneA
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
-    trace_refill<true, kCount>(
-        sa.nodes, sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
+    trace_refill<SplitTrav<true, kCount>>(
+        split_nodes(sa), sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
@@ -902,6 +915,35 @@ __global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* 
     }
 }
 
+__global__ void k_debug_trace4(const Bvh4Node* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
+                               int n, const float4* __restrict__ rays, float4* __restrict__ hits,
+                               int32_t* __restrict__ prims, uint8_t* __restrict__ occ,
+                               int32_t* __restrict__ spill) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    const int nthreads = gridDim.x * kBlock;
+    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, nthreads, 0};
+    TravCount cnt;
+    for (int i = gtid; i < n; i += nthreads) {
+        const float4 o = rays[2 * i], d = rays[2 * i + 1];
+        TravState4<false> ts;
+        ts.start(xyz(o), xyz(d), o.w, d.w);
+        st.sp = 0;
+        if (n_tris > 0)
+            while (!ts.step(nodes, tris, st, cnt)) {
+            }
+        hits[i] = make_float4(ts.h.t, ts.h.u, ts.h.v, 0.0f);
+        prims[i] = ts.h.orig;
+        TravState4<true> ta;
+        ta.start(xyz(o), xyz(d), o.w, d.w);
+        st.sp = 0;
+        if (n_tris > 0)
+            while (!ta.step(nodes, tris, st, cnt)) {
+            }
+        occ[i] = ta.h.idx >= 0 ? 1 : 0;
+    }
+}
+
 }  // namespace
 
 int device_cu_count() {
@@ -956,6 +998,19 @@ size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
     if (shading) f4 += 3 * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4;
     return 16 * f4;
 }
+}  // namespace
+
+int split_bvh_width() { return RR_SPLIT_WIDTH; }
+
+bool scene_in_lds(int n_tris, int n_mats, int n_lights) {
+    FrameConsts fc{};
+    fc.n_tris = n_tris;
+    fc.n_mats = n_mats;
+    fc.n_lights = n_lights;
+    return n_tris > 0 && scene_lds_bytes(fc, true) <= kLdsSceneMax;
+}
+
+namespace {
 // Launch geometry of one frame's path kernels.
 struct Grids {
     bool lds;
@@ -965,7 +1020,7 @@ struct Grids {
     ExtendFn ke;
     ShadowFn ks;
     Grids(const FrameConsts& fc, bool count) {
-        lds = fc.n_tris > 0 && scene_lds_bytes(fc, true) <= kLdsSceneMax;
+        lds = scene_in_lds(fc.n_tris, fc.n_mats, fc.n_lights);
         kp = lds ? (count ? k_primary<true, true> : k_primary<false, true>)
                  : (count ? k_primary<true, false> : k_primary<false, false>);
         ke = lds ? (count ? k_extend<true, true> : k_extend<false, true>)
@@ -1134,9 +1189,10 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     KernelProfiler& pr = p.prof;
     const Grids G(base, tc != nullptr);
-    const SceneArgs sa{s.nodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
+    const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
                        std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
     if (!G.lds && base.n_tris > 0) {
+        if (RR_SPLIT_WIDTH == 4 && !s.has4) throw std::runtime_error("split path needs the BVH4 (scene built without it)");
         render_split(p, base, n_chunks, st, sa, tc, pq, sq);
         RR_HIP(hipGetLastError());
         return;
@@ -1186,10 +1242,15 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
 }
 
 void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, float4* d_hits, int32_t* d_prims,
-                        uint8_t* d_occ, hipStream_t st) {
+                        uint8_t* d_occ, hipStream_t st, int width) {
     p.ensure_paths(1);
     const int g = (int)std::min<long>((n + kBlock - 1) / kBlock, p.grid_blocks);
-    if (n > 0)
+    if (width == 4) {
+        if (!s.has4) throw std::runtime_error("BVH4 not built");
+        if (n > 0)
+            k_debug_trace4<<<g, kBlock, 0, st>>>(s.nodes4.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,
+                                                 p.spill.ptr);
+    } else if (n > 0)
         k_debug_trace<<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,
                                             p.spill.ptr);
     RR_HIP(hipGetLastError());

@@ -74,7 +74,7 @@ EXPORTS = [
     "rr_frame_submit", "rr_frame_complete",
     "rr_render_frame_to_memory", "rr_scene_resolution", "rr_encode_image", "rr_last_error",
     "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
-    "rr_debug_trace", "rr_debug_object_matrix",
+    "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_bvh4",
 ]
 
 _lib = None
@@ -116,7 +116,8 @@ def lib() -> ctypes.CDLL:
         "rr_debug_frame_state": (c_int, [P, P, i32, ctypes.POINTER(RenderParams), f32p, i32p, f32p, f32p, f32p,
                                          f32p, i32p, f32p]),
         "rr_debug_bvh": (c_int, [P, P, i32, u32p, u32p, i32p, f32p]),
-        "rr_debug_trace": (c_int, [P, P, i32, i32, f32p, f32p, i32p, u8p]),
+        "rr_debug_trace": (c_int, [P, P, i32, i32, i32, f32p, f32p, i32p, u8p]),
+        "rr_debug_bvh4": (c_int, [P, P, i32, i32p, i32p, f32p]),
         "rr_debug_object_matrix": (c_int, [P, i32, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
@@ -314,13 +315,24 @@ class RenderContext:
                                   _ptr(boxes, ctypes.c_float)), self.handle)
         return keys, order, children, boxes
 
-    def trace(self, scene: Scene, frame: int, rays: np.ndarray):
+    def bvh4(self, scene: Scene, frame: int):
+        """rr_debug_bvh4: (children4 (n4,4), boxes4 (n4,24))."""
+        n4 = ctypes.c_int32()
+        _check(lib().rr_debug_bvh4(self.handle, scene.handle, int(frame), ctypes.byref(n4), None, None), self.handle)
+        ch = np.zeros((max(n4.value, 1), 4), np.int32)
+        bx = np.zeros((max(n4.value, 1), 24), np.float32)
+        _check(lib().rr_debug_bvh4(self.handle, scene.handle, int(frame), ctypes.byref(n4), _ptr(ch, ctypes.c_int32),
+                                   _ptr(bx, ctypes.c_float)), self.handle)
+        return ch[:n4.value], bx[:n4.value]
+
+    def trace(self, scene: Scene, frame: int, rays: np.ndarray, width: int = 0):
+        """rr_debug_trace; width 0 = the hierarchy the frame kernels use."""
         rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
         n = rays.shape[0]
         hits = np.zeros((max(n, 1), 4), np.float32)
         prims = np.zeros(max(n, 1), np.int32)
         occ = np.zeros(max(n, 1), np.uint8)
-        _check(lib().rr_debug_trace(self.handle, scene.handle, int(frame), n, _ptr(rays, ctypes.c_float),
+        _check(lib().rr_debug_trace(self.handle, scene.handle, int(frame), int(width), n, _ptr(rays, ctypes.c_float),
                                     _ptr(hits, ctypes.c_float), _ptr(prims, ctypes.c_int32),
                                     _ptr(occ, ctypes.c_uint8)), self.handle)
         return hits[:n], prims[:n], occ[:n]

@@ -204,7 +204,7 @@ void rr_destroy(rr_ctx* ctx);
 #define RR_CAM_FLOATS 16   /* pos3 right3 up3 back3 half_w half_h clip_start clip_end */
 #define RR_LIGHT_FLOATS 12 /* type pos3 dir3 radius intensity3 pad */
 #define RR_MAT_FLOATS 12   /* base3 metallic specular roughness ior emission3 model pad */
-#define RR_RENDER_INTS 8   /* W H spp max_bounces seed view_transform spp_per_chunk pad */
+#define RR_RENDER_INTS 8   /* W H spp max_bounces seed view_transform spp_per_chunk bvh_width */
 #define RR_RENDER_FLOATS 4 /* clamp_indirect filter_width exposure_scale pad */
 
 int rr_debug_counts(rr_scene* scene, int32_t* n_triangles, int32_t* n_lights,
@@ -226,11 +226,22 @@ int rr_debug_frame_state(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
 int rr_debug_bvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, uint32_t* keys,
                  uint32_t* order, int32_t* children, float* boxes);
 
-/* Trace a batch of rays against the frame's LBVH. rays: n*8 floats
+/* BVH4 collapse of the frame's LBVH (the hierarchy the split path of large
+ * scenes traverses; built on demand here). *n4 receives the node count; if
+ * children4 / boxes4 are non-NULL they receive 4*n4 child refs (>= 0 node,
+ * < 0 ~leaf, 0x7fffffff empty) and 24*n4 floats per node:
+ * lox[4] loy[4] loz[4] hix[4] hiy[4] hiz[4]. Call once with NULL arrays to size them. */
+int rr_debug_bvh4(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t* n4,
+                  int32_t* children4, float* boxes4);
+
+/* Trace a batch of rays against the frame's hierarchy. bvh_width: 2 (LBVH),
+ * 4 (BVH4 collapse) or 0 (whichever the frame kernels use for this scene,
+ * render_ints[7] of rr_debug_frame_state). rays: n*8 floats
  * (o.xyz, tmin, d.xyz, tmax). hits: n*4 floats (t, u, v, 0), prims: n original
  * triangle ids (-1 miss), occluded: n bytes (any-hit result). */
-int rr_debug_trace(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t n_rays,
-                   const float* rays, float* hits, int32_t* prims, uint8_t* occluded);
+int rr_debug_trace(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t bvh_width,
+                   int32_t n_rays, const float* rays, float* hits, int32_t* prims,
+                   uint8_t* occluded);
 
 /* Host animation evaluation: object_to_world matrix (row-major 4x4, f64) of
  * object `object_index` at (possibly fractional) frame. */

@@ -32,6 +32,8 @@ def lib():
         c_int = ctypes.c_int
         L.orc_build_lbvh.argtypes = [c_int, f, u32, u32, i32, f]
         L.orc_trace.argtypes = [c_int, f, c_int, f, f, i32, u8]
+        L.orc_trace_w.argtypes = [c_int, f, c_int, c_int, f, f, i32, u8]
+        L.orc_build_bvh4.argtypes = [c_int, f, i32, i32, f]
         L.orc_trace_brute.argtypes = [c_int, f, c_int, f, f, i32]
         L.orc_render.argtypes = [c_int, f, i32, f, c_int, f, f, f, i32, f, f, u8, c_int, c_int, c_int]
         L.orc_rng.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, c_int, f]
@@ -62,14 +64,27 @@ def build_lbvh(tris: np.ndarray):
     return keys, order, children, boxes
 
 
-def trace(tris: np.ndarray, rays: np.ndarray):
+def trace(tris: np.ndarray, rays: np.ndarray, width: int = 2):
+    """Closest + any hit through the LBVH (width 2) or its BVH4 collapse (4)."""
     tris = _f32(tris).reshape(-1, 9)
     rays = _f32(rays).reshape(-1, 8)
     n = rays.shape[0]
     hits, prims, occ = np.zeros((n, 4), np.float32), np.zeros(n, np.int32), np.zeros(n, np.uint8)
-    lib().orc_trace(tris.shape[0], _p(tris, ctypes.c_float), n, _p(rays, ctypes.c_float),
-                    _p(hits, ctypes.c_float), _p(prims, ctypes.c_int32), _p(occ, ctypes.c_uint8))
+    lib().orc_trace_w(tris.shape[0], _p(tris, ctypes.c_float), int(width), n, _p(rays, ctypes.c_float),
+                      _p(hits, ctypes.c_float), _p(prims, ctypes.c_int32), _p(occ, ctypes.c_uint8))
     return hits, prims, occ
+
+
+def build_bvh4(tris: np.ndarray):
+    """BVH4 collapse: (children4 (n4,4), boxes4 (n4,24)) as rr_debug_bvh4."""
+    tris = _f32(tris).reshape(-1, 9)
+    n = tris.shape[0]
+    ni = max(n - 1, 1)
+    n4 = np.zeros(1, np.int32)
+    ch, bx = np.zeros((ni, 4), np.int32), np.zeros((ni, 24), np.float32)
+    lib().orc_build_bvh4(n, _p(tris, ctypes.c_float), _p(n4, ctypes.c_int32), _p(ch, ctypes.c_int32),
+                         _p(bx, ctypes.c_float))
+    return ch[:n4[0]], bx[:n4[0]]
 
 
 def trace_brute(tris: np.ndarray, rays: np.ndarray):

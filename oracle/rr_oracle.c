@@ -39,7 +39,7 @@
 
 #define ORC_FILTER_N 1024
 #define ORC_SRGB_N 4096
-#define ORC_MAXDEPTH 256
+#define ORC_MAXDEPTH 80 /* = the GPU traversal stack (kLdsStack + kSpillStack, rr_device.h) */
 
 typedef struct { float x, y, z; } v3;
 
@@ -154,7 +154,13 @@ typedef struct {
     float* tri;       /* leaf order: v0 e1 e2 (9) */
     int* tri_orig;
     int* tri_mat;
+    int width;        /* hierarchy trace() walks: 2 (LBVH) or 4 (BVH4 collapse) */
+    int n4;           /* BVH4 nodes */
+    int* child4;      /* 4 per node: >= 0 node, < 0 ~leaf, ORC_EMPTY4 unused */
+    float* box4;      /* 24 per node: lox[4] loy[4] loz[4] hix[4] hiy[4] hiz[4] */
 } lbvh;
+
+#define ORC_EMPTY4 0x7fffffff
 
 static uint32_t spread10(uint32_t v) {
     v = (v * 0x00010001u) & 0xFF0000FFu;
@@ -193,6 +199,7 @@ static void subtree_box(const lbvh* B, const float* tris9, int c, float out[6]) 
 }
 
 static void lbvh_free(lbvh* B) {
+    free(B->child4); free(B->box4);
     free(B->keys); free(B->order); free(B->child); free(B->box);
     free(B->tri); free(B->tri_orig); free(B->tri_mat);
     memset(B, 0, sizeof *B);
@@ -313,6 +320,68 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
     }
 }
 
+/* BVH4 collapse of the LBVH, as csrc/bvh.hip k_depth_parity + k_collapse4:
+ * every even-depth internal node (root depth 0) becomes BVH4 node rank(i) =
+ * number of even-depth nodes with a smaller index; its children in slot order
+ * are, per side (left, right), the leaf child itself or both children of the
+ * odd-depth internal child; boxes are the parents' child boxes. */
+static void lbvh_collapse4(lbvh* B) {
+    const int n = B->n;
+    B->n4 = 0;
+    if (n <= 0) return;
+    const int ni = n > 1 ? n - 1 : 1;
+    int* depth = (int*)malloc(sizeof(int) * (size_t)ni);
+    int* rank = (int*)malloc(sizeof(int) * (size_t)ni);
+    int* stack = (int*)malloc(sizeof(int) * (size_t)ni + 16);
+    int sp = 0;
+    depth[0] = 0;
+    stack[sp++] = 0;
+    while (sp && n > 1) {
+        int v = stack[--sp];
+        for (int s = 0; s < 2; ++s) {
+            int c = B->child[2 * v + s];
+            if (c >= 0) { depth[c] = depth[v] + 1; stack[sp++] = c; }
+        }
+    }
+    int n4 = 0;
+    for (int i = 0; i < ni; ++i) {
+        rank[i] = n4;
+        if ((depth[i] & 1) == 0) ++n4;
+    }
+    B->n4 = n4;
+    B->child4 = (int*)malloc(sizeof(int) * 4 * (size_t)n4);
+    B->box4 = (float*)malloc(sizeof(float) * 24 * (size_t)n4);
+    for (int i = 0; i < ni; ++i) {
+        if (depth[i] & 1) continue;
+        float lo[3][4], hi[3][4];
+        int ref[4], m = 0;
+        for (int side = 0; side < 2; ++side) {
+            int c = B->child[2 * i + side];
+            int par[2], sd[2], k = 0;
+            if (c < 0) { par[0] = i; sd[0] = side; k = 1; }
+            else { par[0] = c; sd[0] = 0; par[1] = c; sd[1] = 1; k = 2; }
+            for (int q = 0; q < k; ++q) {
+                const float* f = B->box + 12 * (size_t)par[q] + 6 * sd[q];
+                int cc = B->child[2 * par[q] + sd[q]];
+                for (int a = 0; a < 3; ++a) { lo[a][m] = f[a]; hi[a][m] = f[3 + a]; }
+                ref[m] = cc < 0 ? cc : rank[cc];
+                ++m;
+            }
+        }
+        for (; m < 4; ++m) {
+            for (int a = 0; a < 3; ++a) { lo[a][m] = 0.0f; hi[a][m] = 0.0f; }
+            ref[m] = ORC_EMPTY4;
+        }
+        float* o = B->box4 + 24 * (size_t)rank[i];
+        for (int c = 0; c < 4; ++c) {
+            o[c] = lo[0][c]; o[4 + c] = lo[1][c]; o[8 + c] = lo[2][c];
+            o[12 + c] = hi[0][c]; o[16 + c] = hi[1][c]; o[20 + c] = hi[2][c];
+            B->child4[4 * (size_t)rank[i] + c] = ref[c];
+        }
+    }
+    free(depth); free(rank); free(stack);
+}
+
 /* ------------------------------------------------------------ tracing ---- */
 typedef struct { float t, u, v; int idx, orig; } hitrec;
 
@@ -351,9 +420,57 @@ static void try_leaf(const lbvh* B, int leaf, v3 o, v3 d, float tmin, hitrec* h)
     }
 }
 
+typedef struct { float t; int slot, ref; } ckey;
+
+/* BVH4 walk of rr_device.h TravState4: the four slab tests against the box
+ * test bound at node entry, passing leaf children intersected in slot order,
+ * the nearest hit internal child (ties: lower slot) visited next, the other
+ * hit internal children pushed in descending slot order. */
+static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hitrec* h) {
+    h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
+    if (B->n <= 0) return 0;
+    v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int stack[ORC_MAXDEPTH];
+    int sp = 0, node = 0;
+    for (;;) {
+        const float* bx = B->box4 + 24 * (size_t)node;
+        const int* ch = B->child4 + 4 * (size_t)node;
+        const float tcur = h->t;
+        ckey k[4];
+        for (int c = 0; c < 4; ++c) {
+            int ref = ch[c];
+            float b6[6] = {bx[c], bx[4 + c], bx[8 + c], bx[12 + c], bx[16 + c], bx[20 + c]};
+            float tn = 0.0f;
+            int hit = ref != ORC_EMPTY4 && slab_test(o, inv, b6, tmin, tcur, &tn);
+            k[c].slot = c;
+            k[c].ref = ref;
+            k[c].t = (hit && ref >= 0) ? tn : INFINITY;
+            if (hit && ref < 0) {
+                try_leaf(B, ~ref, o, d, tmin, h);
+                if (any && h->idx >= 0) return 1;
+            }
+        }
+        /* nearest hit internal child next (ties: lower slot); the others are
+         * pushed in descending slot order */
+        int best = -1;
+        for (int c = 0; c < 4; ++c)
+            if (k[c].t != INFINITY && (best < 0 || k[c].t < k[best].t)) best = c;
+        if (best < 0) {
+            if (sp == 0) break;
+            node = stack[--sp];
+            continue;
+        }
+        for (int c = 3; c >= 0; --c)
+            if (c != best && k[c].t != INFINITY && sp < ORC_MAXDEPTH) stack[sp++] = k[c].ref;
+        node = k[best].ref;
+    }
+    return h->idx >= 0;
+}
+
 /* Same traversal order as the GPU (near child first, left on ties, leaves
  * tested as soon as their box passes). */
 static int trace(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hitrec* h) {
+    if (B->width == 4) return trace4(B, o, d, tmin, tmax, any, h);
     h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
     if (B->n <= 0) return 0;
     v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -675,10 +792,23 @@ int orc_trace_brute(int n, const float* tris9, int n_rays, const float* rays, fl
     return 0;
 }
 
-int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* hits, int32_t* prims,
-              uint8_t* occluded) {
+/* BVH4 collapse (rr_debug_bvh4 layout): n4 nodes, 4 child refs, 24 floats each. */
+int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, float* boxes4) {
     lbvh B;
     lbvh_build(&B, n, tris9, NULL);
+    lbvh_collapse4(&B);
+    *n4 = B.n4;
+    if (children4 && B.n4) memcpy(children4, B.child4, sizeof(int32_t) * 4 * (size_t)B.n4);
+    if (boxes4 && B.n4) memcpy(boxes4, B.box4, sizeof(float) * 24 * (size_t)B.n4);
+    lbvh_free(&B);
+    return 0;
+}
+
+int orc_trace_w(int n, const float* tris9, int width, int n_rays, const float* rays, float* hits, int32_t* prims,
+                uint8_t* occluded) {
+    lbvh B;
+    lbvh_build(&B, n, tris9, NULL);
+    if (width == 4) { lbvh_collapse4(&B); B.width = 4; }
     for (int r = 0; r < n_rays; ++r) {
         const float* R = rays + 8 * (size_t)r;
         v3 o = V(R[0], R[1], R[2]), d = V(R[4], R[5], R[6]);
@@ -692,6 +822,11 @@ int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* h
     return 0;
 }
 
+int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* hits, int32_t* prims,
+              uint8_t* occluded) {
+    return orc_trace_w(n, tris9, 2, n_rays, rays, hits, prims, occluded);
+}
+
 /* Full frame. render_ints: W H spp max_bounces seed view_transform (as rr.h);
  * render_floats: clamp_indirect filter_width exposure_scale.
  * film: W*H*4 floats of mean radiance; rgba8: W*H*4 bytes. Rows
@@ -702,6 +837,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
                float* film, uint8_t* rgba8, int row_begin, int row_end, int threads) {
     lbvh B;
     lbvh_build(&B, n_tris, tris9, tri_mat);
+    if (ri[7] == 4) { lbvh_collapse4(&B); B.width = 4; }  /* the hierarchy the product walks */
     scene_t* S = (scene_t*)calloc(1, sizeof(scene_t));
     S->bvh = &B;
     S->cam = cam;

@@ -99,6 +99,21 @@ def test_trace_batches_bit_exact(ctx, s04):
     assert np.array_equal(bh[:, 0], oh[:, 0])
 
 
+def test_trace_bvh4_small_scene(ctx, s04):
+    """The BVH4 walk on the 12-triangle scene (forced; frames use the LDS BVH2)."""
+    rng = np.random.default_rng(99)
+    st = ctx.frame_state(s04, 45)
+    assert int(st.render_ints[7]) == 2
+    center = st.tris.reshape(-1, 3).mean(axis=0)
+    rays = np.concatenate([_rays_random(rng, 5000, center, 6.0), _rays_random(rng, 500, center, 0.5)])
+    hits, prims, occ = ctx.trace(s04, 45, rays, width=4)
+    oh, op, oo = O.trace(st.tris, rays, width=4)
+    assert np.array_equal(prims, op) and np.array_equal(hits, oh) and np.array_equal(occ, oo)
+    ch, bx = ctx.bvh4(s04, 45)
+    och, obx = O.build_bvh4(st.tris)
+    assert np.array_equal(ch, och) and np.array_equal(bx, obx)
+
+
 def test_trace_edge_cases(ctx, s04):
     st = ctx.frame_state(s04, 1)
     v = st.tris[0, 0].astype(np.float64)

@@ -76,15 +76,34 @@ def test_physics_rebuilds_every_frame(ctx, rr, s02):
     assert stats.bvh_rebuilt == 0
 
 
-def test_physics_trace_bit_exact(ctx, s02):
+@pytest.mark.parametrize("width", [2, 4])
+def test_physics_trace_bit_exact(ctx, s02, width):
     st = ctx.frame_state(s02, 90)
+    assert int(st.render_ints[7]) in (2, 4)  # hierarchy the split-path frame kernels walk
     rays = _camera_rays(st, 40000, np.random.default_rng(7))
-    hits, prims, occ = ctx.trace(s02, 90, rays)
-    oh, op, oo = O.trace(st.tris, rays)
+    hits, prims, occ = ctx.trace(s02, 90, rays, width=width)
+    oh, op, oo = O.trace(st.tris, rays, width=width)
     assert np.array_equal(prims, op), f"{np.count_nonzero(prims != op)} prim mismatches"
     assert np.array_equal(hits, oh)
     assert np.array_equal(occ, oo)
     assert (prims >= 0).mean() > 0.3
+    if width == 4:  # both hierarchies find the same closest hits
+        h2, p2, o2 = O.trace(st.tris, rays, width=2)
+        assert np.array_equal(p2, op) and np.array_equal(o2, oo)
+
+
+@pytest.mark.parametrize("frame", [1, 90])
+def test_physics_bvh4_bit_exact(ctx, s02, frame):
+    st = ctx.frame_state(s02, frame)
+    ch, bx = ctx.bvh4(s02, frame)
+    och, obx = O.build_bvh4(st.tris)
+    assert ch.shape == och.shape and np.array_equal(ch, och)
+    assert np.array_equal(bx, obx)
+    # every leaf appears exactly once, every node but the root is referenced once
+    leaves = -ch[ch < 0] - 1
+    assert np.array_equal(np.sort(leaves), np.arange(st.tris.shape[0]))
+    inner = ch[(ch >= 0) & (ch != 0x7FFFFFFF)]
+    assert np.array_equal(np.sort(inner), np.arange(1, ch.shape[0]))
 
 
 @pytest.mark.parametrize("path,frame,w,h,spp", [(S02, 1, 96, 54, 4), (S02, 90, 80, 45, 3), (S03, 300, 64, 36, 2)])
@@ -129,11 +148,22 @@ def test_c5_full_size_lbvh_bit_exact(ctx, sc5):
     assert np.array_equal(np.sort(inner), np.arange(1, n - 1))
 
 
-def test_c5_trace_bit_exact(ctx, sc5):
+def test_c5_full_size_bvh4_bit_exact(ctx, sc5):
+    st = ctx.frame_state(sc5, 120)
+    ch, bx = ctx.bvh4(sc5, 120)
+    och, obx = O.build_bvh4(st.tris)
+    assert np.array_equal(ch, och)
+    assert np.array_equal(bx, obx)
+    leaves = -ch[ch < 0] - 1
+    assert np.array_equal(np.sort(leaves), np.arange(st.tris.shape[0]))
+
+
+@pytest.mark.parametrize("width", [2, 4])
+def test_c5_trace_bit_exact(ctx, sc5, width):
     st = ctx.frame_state(sc5, 200)
     rays = _camera_rays(st, 100000, np.random.default_rng(11))
-    hits, prims, occ = ctx.trace(sc5, 200, rays)
-    oh, op, oo = O.trace(st.tris, rays)
+    hits, prims, occ = ctx.trace(sc5, 200, rays, width=width)
+    oh, op, oo = O.trace(st.tris, rays, width=width)
     assert np.array_equal(prims, op), f"{np.count_nonzero(prims != op)} prim mismatches"
     assert np.array_equal(hits, oh)
     assert np.array_equal(occ, oo)

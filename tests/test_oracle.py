@@ -210,3 +210,29 @@ def test_04_frame_is_plausible():
     f2, r2 = O.render(tris, mats, fc["camera"], fc["lights"], fc["materials"], fc["world"], ri, rf,
                       rows=(10, 20), threads=2)
     assert np.array_equal(f2[10:20], film[10:20]) and np.array_equal(r2[10:20], rgba[10:20])
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (7, 2), (300, 3), (5000, 4)])
+def test_bvh4_collapse_and_walk_equal_brute_force(n, seed):
+    """BVH4 collapse: every leaf once, every node but the root once, boxes taken
+    from the LBVH; the BVH4 walk finds the brute-force closest hits."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-5, 5, (n, 1, 3))
+    tris = (c + rng.normal(0, 0.6, (n, 3, 3))).astype(np.float32)
+    ch, bx = O.build_bvh4(tris)
+    leaves = -ch[ch < 0] - 1
+    assert np.array_equal(np.sort(leaves), np.arange(n)) or (n == 1 and set(leaves) == {0})
+    inner = ch[(ch >= 0) & (ch != 0x7FFFFFFF)]
+    assert np.array_equal(np.sort(inner), np.arange(1, ch.shape[0]))
+    m = 4000
+    rays = np.zeros((m, 8), np.float32)
+    rays[:, 0:3] = rng.uniform(-8, 8, (m, 3))
+    d = rng.normal(0, 1, (m, 3))
+    rays[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 7] = 1e30
+    h4, p4, o4 = O.trace(tris, rays, width=4)
+    h2, p2, o2 = O.trace(tris, rays, width=2)
+    bh, bp = O.trace_brute(tris, rays)
+    assert np.array_equal(p4, bp) and np.array_equal(p2, bp)
+    assert np.array_equal(h4[:, 0], bh[:, 0])
+    assert np.array_equal(o4, o2)
