@@ -246,7 +246,8 @@ __device__ __forceinline__ int delta(const uint32_t* __restrict__ keys, int n, i
 __global__ __launch_bounds__(kBlock) void k_karras(int n, const uint32_t* __restrict__ keys,
                                                    int2* __restrict__ children,
                                                    int32_t* __restrict__ node_parent,
-                                                   int32_t* __restrict__ leaf_parent) {
+                                                   int32_t* __restrict__ leaf_parent,
+                                                   int2* __restrict__ range) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n - 1) return;
     const int d = (delta(keys, n, i, i + 1) - delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -282,6 +283,7 @@ __global__ __launch_bounds__(kBlock) void k_karras(int n, const uint32_t* __rest
         node_parent[gamma + 1] = 2 * i + 1;
     }
     children[i] = make_int2(left, right);
+    range[i] = make_int2(lo, hi - lo + 1);  // sorted leaves [lo, hi] under node i
     if (i == 0) node_parent[0] = -1;
 }
 
@@ -349,6 +351,27 @@ __global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restr
     }
 }
 
+// Small subtrees become leaf ranges: a child subtree over at most kLeafMax
+// sorted leaves (Karras nodes cover contiguous ranges) is referenced as
+// ~(first | (count - 1) << 28), so the walk tests its triangles (contiguous
+// TriPacks) instead of visiting its bottom nodes. Rewrites only the child refs
+// of nodes[] (the boxes are the subtrees' boxes already); `children` keeps the
+// full topology (BVH4 collapse, depth parity).
+__global__ __launch_bounds__(kBlock) void k_leafify(int ni, const int2* __restrict__ children,
+                                                    const int2* __restrict__ range, BvhNode* __restrict__ nodes) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= ni) return;
+    const int2 ch = children[p];
+    int ref[2] = {ch.x, ch.y};
+    for (int s = 0; s < 2; ++s)
+        if (ref[s] >= 0) {
+            const int2 r = range[ref[s]];
+            if (r.y <= kLeafMax) ref[s] = leaf_ref(r.x, r.y);
+        }
+    nodes[p].d.x = ref[0];
+    nodes[p].d.y = ref[1];
+}
+
 // BVH4 collapse, step 1: depth parity of every internal node (walk to the
 // root through node_parent); flags[i] = 1 and rank[i] = 1 for even depth.
 __global__ __launch_bounds__(kBlock) void k_depth_parity(int ni, const int32_t* __restrict__ node_parent,
@@ -368,6 +391,7 @@ __global__ __launch_bounds__(kBlock) void k_depth_parity(int ni, const int32_t* 
 // odd-depth internal child (leaf, or BVH4 node rank[grandchild]). Boxes come
 // from the parents' child boxes, so they are the BVH2 boxes bit for bit.
 __global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNode* __restrict__ nodes,
+                                                      const int2* __restrict__ children,
                                                       const uint32_t* __restrict__ flags,
                                                       const uint32_t* __restrict__ rank,
                                                       Bvh4Node* __restrict__ out) {
@@ -376,9 +400,9 @@ __global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNo
     float lo[3][4], hi[3][4];
     int ref[4];
     int m = 0;
-    auto put = [&](const BvhNode& nd, int side) {
+    auto put = [&](const BvhNode& nd, int2 ch, int side) {
         const float* f = reinterpret_cast<const float*>(&nd) + 6 * side;
-        const int c = side ? nd.d.y : nd.d.x;
+        const int c = side ? ch.y : ch.x;
         for (int a = 0; a < 3; ++a) {
             lo[a][m] = f[a];
             hi[a][m] = f[3 + a];
@@ -387,14 +411,16 @@ __global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNo
         ++m;
     };
     const BvhNode nd = nodes[i];
+    const int2 ch = n > 1 ? children[i] : make_int2(~0, ~0);
     for (int side = 0; side < 2; ++side) {
-        const int c = side ? nd.d.y : nd.d.x;
-        if (c < 0 || n == 1) {
-            put(nd, side);
+        const int c = side ? ch.y : ch.x;
+        if (c < 0) {
+            put(nd, ch, side);
         } else {
             const BvhNode cn = nodes[c];
-            put(cn, 0);
-            put(cn, 1);
+            const int2 cc = children[c];
+            put(cn, cc, 0);
+            put(cn, cc, 1);
         }
     }
     for (; m < 4; ++m) {
@@ -434,6 +460,7 @@ void DevScene::release() {
     for (int k = 0; k < 2; ++k) { keys[k].release(); vals[k].release(); }
     hist.release(); scan_part.release(); children.release(); node_parent.release();
     leaf_parent.release(); flags.release(); nodes.release(); tris.release(); nodes4.release(); rank4.release();
+    range.release();
     has4 = false;
     built = false;
     uploaded = false;
@@ -460,6 +487,7 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4) {
     s.node_parent.ensure((size_t)(n > 1 ? n - 1 : 1));
     s.leaf_parent.ensure((size_t)n);
     s.flags.ensure((size_t)(n > 1 ? n - 1 : 1));
+    s.range.ensure((size_t)(n > 1 ? n - 1 : 1));
 
     RR_HIP(hipMemsetAsync(s.bounds.ptr, 0xFF, 3 * sizeof(uint32_t), st));
     RR_HIP(hipMemsetAsync(s.bounds.ptr + 3, 0x00, 3 * sizeof(uint32_t), st));
@@ -485,7 +513,7 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4) {
     }
     if (n > 1) {
         k_karras<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n, s.keys[0].ptr, s.children.ptr,
-                                                          s.node_parent.ptr, s.leaf_parent.ptr);
+                                                          s.node_parent.ptr, s.leaf_parent.ptr, s.range.ptr);
         RR_HIP(hipMemsetAsync(s.flags.ptr, 0, (size_t)(n - 1) * sizeof(uint32_t), st));
     }
     k_refit<<<nb, kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr, s.leaf_parent.ptr,
@@ -504,10 +532,12 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4) {
         }
         RR_HIP(hipMemsetAsync(s.rank4.ptr + ni, 0, sizeof(uint32_t), st));
         exclusive_scan(s, s.rank4.ptr, ni + 1, st);  // rank4[ni] = BVH4 node count
-        k_collapse4<<<cdiv(ni, kBlock), kBlock, 0, st>>>(ni, n, s.nodes.ptr, s.flags.ptr, s.rank4.ptr,
-                                                         s.nodes4.ptr);
+        k_collapse4<<<cdiv(ni, kBlock), kBlock, 0, st>>>(ni, n, s.nodes.ptr, s.children.ptr, s.flags.ptr,
+                                                         s.rank4.ptr, s.nodes4.ptr);
         s.has4 = true;
     }
+    if (kLeafMax > 1 && n > 1)
+        k_leafify<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n - 1, s.children.ptr, s.range.ptr, s.nodes.ptr);
     if (prof) prof->end(st);
     RR_HIP(hipGetLastError());
     s.built = true;

@@ -66,6 +66,7 @@ struct DevScene {
     DevBuf<int32_t> node_parent;  // n-1 : parent*2+side, -1 root
     DevBuf<int32_t> leaf_parent;  // n
     DevBuf<uint32_t> flags;       // n-1 arrival counters
+    DevBuf<int2> range;           // n-1 : (first sorted leaf, leaf count) under each node
     // acceleration structure consumed by traversal
     DevBuf<BvhNode> nodes;  // max(n-1, 1)
     DevBuf<TriPack> tris;   // n, leaf order

@@ -57,6 +57,22 @@ struct alignas(16) TriPack {
 };
 static_assert(sizeof(TriPack) == 48, "tri pack is 48 bytes");
 
+// Leaf refs (< 0) name a range of sorted leaves: ~(first | (count - 1) << 28).
+// Subtrees over at most kLeafMax leaves are referenced as ranges (bvh.hip
+// k_leafify; oracle ORC_LEAF_MAX must be equal). Measured on the split path
+// (one 02 frame at 16 spp / C5 at 8 spp): kLeafMax 1 -> 61.7 / 115.1 ms,
+// 2 -> 70.0 / 132.5, 4 -> 87.7 / 165.1, 8 -> 121.7 / 229.9: the extra
+// triangle tests cost far more than the bottom node visits they save, so
+// leaves stay single triangles (kLeafMax 1: k_leafify is not launched).
+#ifndef RR_LEAF_MAX
+#define RR_LEAF_MAX 1
+#endif
+constexpr int kLeafMax = RR_LEAF_MAX;
+static_assert(kLeafMax >= 1 && kLeafMax <= 8, "count - 1 must fit bits 28..30 of a leaf ref");
+RR_HD int leaf_ref(int first, int count) { return ~(first | ((count - 1) << 28)); }
+RR_HD int leaf_first(int ref) { return (~ref) & 0x0FFFFFFF; }
+RR_HD int leaf_count(int ref) { return ((~ref) >> 28) + 1; }
+
 constexpr int kMaxLights = 64;
 constexpr int kBlock = 256;         // threads per block for all path kernels
 constexpr int kLdsStack = 16;       // traversal stack entries kept in LDS per lane
@@ -387,7 +403,27 @@ struct TravState {
         bool hl = slab(o, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
         bool hr = slab(o, invd, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
         const int cl = nd.d.x, cr = nd.d.y;
-#if RR_LEAF_LOOP
+#if 1
+        // passing leaf ranges, left then right, one triangle per iteration: a
+        // wave runs as many iterations as its busiest lane needs
+        int nl = 0, nr = 0, fl = 0, fr = 0;
+        if (hl && cl < 0) {
+            fl = leaf_first(cl);
+            nl = leaf_count(cl);
+            hl = false;
+        }
+        if (hr && cr < 0) {
+            fr = leaf_first(cr);
+            nr = leaf_count(cr);
+            hr = false;
+        }
+        for (int k = 0; k < nl + nr; ++k) {
+            const int ti = k < nl ? fl + k : fr + (k - nl);
+            if (kCount) ++cnt.tris;
+            leaf_test(load_tri(tris, ti), ti, o, d, tmin, h);
+            if (kAnyHit && h.idx >= 0) return true;
+        }
+#elif RR_LEAF_LOOP
         // passing leaf children, left first, as a loop: a wave runs the leaf
         // test as often as its busiest lane needs (lanes with a left leaf and
         // lanes with a right leaf share one pass)
@@ -498,9 +534,12 @@ struct TravState4 {
             const int c = __builtin_ctz(leaves);
             leaves &= leaves - 1;
             const int r = c == 0 ? ref[0] : c == 1 ? ref[1] : c == 2 ? ref[2] : ref[3];
-            if (kCount) ++cnt.tris;
-            leaf_test(load_tri(tris, ~r), ~r, o, d, tmin, h);
-            if (kAnyHit && h.idx >= 0) return true;
+            const int f = leaf_first(r), m = leaf_count(r);
+            for (int q = 0; q < m; ++q) {
+                if (kCount) ++cnt.tris;
+                leaf_test(load_tri(tris, f + q), f + q, o, d, tmin, h);
+                if (kAnyHit && h.idx >= 0) return true;
+            }
         }
         if (!inner) {
             if (st.sp == 0) return true;

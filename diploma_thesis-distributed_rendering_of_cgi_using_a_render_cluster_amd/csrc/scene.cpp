@@ -796,7 +796,7 @@ SceneDesc load_scene(const std::string& path) {
             s.tri_mat.push_back(g >= 0 && g < default_mat ? g : default_mat);
         }
     }
-    if (s.tri_obj.size() > (size_t)0x3fffffff) throw std::runtime_error("too many triangles");
+    if (s.tri_obj.size() > (size_t)0x0fffffff) throw std::runtime_error("too many triangles (max 2^28 - 1: leaf refs)");
     return s;
 }
 

@@ -149,7 +149,9 @@ typedef struct {
     int n;
     uint32_t* keys;   /* sorted */
     uint32_t* order;  /* sorted original ids */
-    int* child;       /* 2*(n-1) or 2 */
+    int* child;       /* 2*(n-1) or 2: full Karras topology */
+    int* child_lf;    /* the same with subtrees of <= ORC_LEAF_MAX leaves as leaf ranges (what trace() walks) */
+    int* range;       /* 2 per internal node: first sorted leaf, leaf count */
     float* box;       /* 12 per internal node */
     float* tri;       /* leaf order: v0 e1 e2 (9) */
     int* tri_orig;
@@ -161,6 +163,13 @@ typedef struct {
 } lbvh;
 
 #define ORC_EMPTY4 0x7fffffff
+/* Leaf refs name ranges of sorted leaves, ~(first | (count-1) << 28), for
+ * subtrees of at most ORC_LEAF_MAX leaves (rr_device.h kLeafMax, bvh.hip
+ * k_leafify; the two constants must be equal). */
+#define ORC_LEAF_MAX 1
+static int leaf_ref(int first, int count) { return ~(first | ((count - 1) << 28)); }
+static int leaf_first(int ref) { return (~ref) & 0x0FFFFFFF; }
+static int leaf_count(int ref) { return ((~ref) >> 28) + 1; }
 
 static uint32_t spread10(uint32_t v) {
     v = (v * 0x00010001u) & 0xFF0000FFu;
@@ -199,7 +208,7 @@ static void subtree_box(const lbvh* B, const float* tris9, int c, float out[6]) 
 }
 
 static void lbvh_free(lbvh* B) {
-    free(B->child4); free(B->box4);
+    free(B->child4); free(B->box4); free(B->child_lf); free(B->range);
     free(B->keys); free(B->order); free(B->child); free(B->box);
     free(B->tri); free(B->tri_orig); free(B->tri_mat);
     memset(B, 0, sizeof *B);
@@ -254,6 +263,8 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
     free(tmpk); free(tmpv); free(cen);
     int ni = n > 1 ? n - 1 : 1;
     B->child = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
+    B->child_lf = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
+    B->range = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->box = (float*)malloc(sizeof(float) * 12 * (size_t)ni);
     if (n == 1) {
         B->child[0] = ~0; B->child[1] = ~0;
@@ -278,6 +289,8 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
             int lo_ = i < j ? i : j, hi_ = i < j ? j : i;
             B->child[2 * i] = (lo_ == g) ? ~g : g;
             B->child[2 * i + 1] = (hi_ == g + 1) ? ~(g + 1) : g + 1;
+            B->range[2 * i] = lo_;
+            B->range[2 * i + 1] = hi_ - lo_ + 1;
         }
     }
     /* boxes bottom-up: children of node i have larger indices or are leaves?
@@ -305,6 +318,11 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
             done[v] = 1;
         }
         free(stack); free(done);
+    }
+    for (int i = 0; i < 2 * ni; ++i) {
+        int c = B->child[i];
+        B->child_lf[i] = (n > 1 && c >= 0 && B->range[2 * c + 1] <= ORC_LEAF_MAX)
+                             ? leaf_ref(B->range[2 * c], B->range[2 * c + 1]) : c;
     }
     B->tri = (float*)malloc(sizeof(float) * 9 * (size_t)n);
     B->tri_orig = (int*)malloc(sizeof(int) * n);
@@ -446,8 +464,10 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             k[c].ref = ref;
             k[c].t = (hit && ref >= 0) ? tn : INFINITY;
             if (hit && ref < 0) {
-                try_leaf(B, ~ref, o, d, tmin, h);
-                if (any && h->idx >= 0) return 1;
+                for (int q = 0; q < leaf_count(ref); ++q) {
+                    try_leaf(B, leaf_first(ref) + q, o, d, tmin, h);
+                    if (any && h->idx >= 0) return 1;
+                }
             }
         }
         /* nearest hit internal child next (ties: lower slot); the others are
@@ -481,16 +501,13 @@ static int trace(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hit
         float tl, tr;
         int hl = slab_test(o, inv, bx, tmin, h->t, &tl);
         int hr = slab_test(o, inv, bx + 6, tmin, h->t, &tr);
-        int cl = B->child[2 * node], cr = B->child[2 * node + 1];
-        if (hl && cl < 0) {
-            try_leaf(B, ~cl, o, d, tmin, h);
+        int cl = B->child_lf[2 * node], cr = B->child_lf[2 * node + 1];
+        int nl = 0, nr = 0, fl = 0, fr = 0;
+        if (hl && cl < 0) { fl = leaf_first(cl); nl = leaf_count(cl); hl = 0; }
+        if (hr && cr < 0) { fr = leaf_first(cr); nr = leaf_count(cr); hr = 0; }
+        for (int k = 0; k < nl + nr; ++k) {
+            try_leaf(B, k < nl ? fl + k : fr + (k - nl), o, d, tmin, h);
             if (any && h->idx >= 0) return 1;
-            hl = 0;
-        }
-        if (hr && cr < 0) {
-            try_leaf(B, ~cr, o, d, tmin, h);
-            if (any && h->idx >= 0) return 1;
-            hr = 0;
         }
         if (hl && hr) {
             int lf = tl <= tr;
@@ -764,7 +781,7 @@ int orc_build_lbvh(int n, const float* tris9, uint32_t* keys, uint32_t* order, i
         int ni = n > 1 ? n - 1 : 1;
         if (keys) memcpy(keys, B.keys, sizeof(uint32_t) * n);
         if (order) memcpy(order, B.order, sizeof(uint32_t) * n);
-        if (children) memcpy(children, B.child, sizeof(int32_t) * 2 * ni);
+        if (children) memcpy(children, B.child_lf, sizeof(int32_t) * 2 * ni);
         if (boxes) memcpy(boxes, B.box, sizeof(float) * 12 * ni);
     }
     lbvh_free(&B);

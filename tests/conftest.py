@@ -36,3 +36,27 @@ def scene_path(name: str) -> str:
 
 def have_reference() -> bool:
     return os.path.isdir(os.path.join(REFERENCE, "worker"))
+
+
+def walk_lbvh(children):
+    """Walk a BVH2 child-ref array from the root (refs >= 0: internal node,
+    < 0: leaf range ~(first | (count-1) << 28)). Returns (covered sorted leaf
+    indices in walk order, reachable internal nodes, leaf refs as (node, side,
+    first, count))."""
+    import numpy as np
+    children = np.asarray(children).reshape(-1, 2)
+    leaves, inner, refs = [], [], []
+    stack = [0]
+    while stack:
+        v = stack.pop()
+        inner.append(v)
+        for side in range(2):
+            c = int(children[v, side])
+            if c >= 0:
+                stack.append(c)
+            else:
+                x = ~c
+                first, count = x & 0x0FFFFFFF, (x >> 28) + 1
+                leaves.extend(range(first, first + count))
+                refs.append((v, side, first, count))
+    return leaves, inner, refs

@@ -10,7 +10,7 @@ through it equals the oracle's traversal; images at reduced resolution/spp.
 import numpy as np
 import pytest
 
-from conftest import scene_path
+from conftest import scene_path, walk_lbvh
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -141,11 +141,10 @@ def test_c5_full_size_lbvh_bit_exact(ctx, sc5):
     assert np.array_equal(order, oo)
     assert np.array_equal(children, oc)
     assert np.array_equal(boxes, ob)
-    # structural properties: every leaf referenced once, every internal node but the root once
-    leaves = -children[children < 0] - 1
-    assert np.array_equal(np.sort(leaves), np.arange(n))
-    inner = children[children >= 0]
-    assert np.array_equal(np.sort(inner), np.arange(1, n - 1))
+    # structural property: the walk from the root covers every leaf exactly once
+    leaves, inner, _ = walk_lbvh(children)
+    assert np.array_equal(np.sort(np.array(leaves)), np.arange(n))
+    assert len(set(inner)) == len(inner)
 
 
 def test_c5_full_size_bvh4_bit_exact(ctx, sc5):

@@ -8,7 +8,7 @@ import math
 import numpy as np
 import pytest
 
-from conftest import scene_path
+from conftest import walk_lbvh, scene_path
 from oracle import host_oracle as HO
 from oracle import oracle as O
 
@@ -97,18 +97,15 @@ def test_lbvh_structure_and_brute_force():
     keys, order, children, boxes = O.build_lbvh(tris)
     assert np.all(np.diff(keys.astype(np.int64)) >= 0)
     assert sorted(order) == list(range(n))
-    leaves = children[children < 0]
-    assert sorted((~leaves).tolist()) == list(range(n))
-    internal = children[children >= 0]
-    assert sorted(internal.tolist()) == list(range(1, n - 1))  # every node but the root has one parent
+    leaves, inner, refs = walk_lbvh(children)
+    assert sorted(leaves) == list(range(n))  # the walk covers every leaf exactly once
+    assert len(set(inner)) == len(inner)
+    assert max(c for (_, _, _, c) in refs) <= 8  # ORC_LEAF_MAX (1: one triangle per leaf)
     # boxes contain their triangles
-    for node in range(0, n - 1, 97):
-        for side in range(2):
-            ch = children[node, side]
-            if ch < 0:
-                t = tris[order[~ch]]
-                lo, hi = boxes[node, 6 * side:6 * side + 3], boxes[node, 6 * side + 3:6 * side + 6]
-                assert np.all(t >= lo) and np.all(t <= hi)
+    for node, side, first, count in refs[::37]:
+        t = tris[order[first:first + count]]
+        lo, hi = boxes[node, 6 * side:6 * side + 3], boxes[node, 6 * side + 3:6 * side + 6]
+        assert np.all(t >= lo) and np.all(t <= hi)
     o = rng.uniform(-15, 15, (4000, 3))
     d = rng.normal(size=(4000, 3))
     d /= np.linalg.norm(d, axis=1, keepdims=True)
