@@ -76,8 +76,9 @@ def parse_args():
                     help="one rr_render_frame per step (no overlap of frame N's encode with N+1's render)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r1_pmc.json"),
-                    help="PMC traffic summary for roofline.traffic (tools/pmc_summary.py)")
+    ap.add_argument("--pmc-summary", default=None,
+                    help="PMC traffic summary for roofline.traffic (tools/pmc_summary.py; default "
+                         "profiles/r1_pmc.json for 04vs, profiles/r1_pmc_<workload>.json otherwise)")
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
     if a.steps is None:
@@ -87,29 +88,42 @@ def parse_args():
     return a
 
 
-def algorithmic_bytes(cls: str, stats, scene_bytes: float) -> tuple[float, float]:
+def algorithmic_bytes(cls: str, stats, scene_bytes: float, split: bool) -> tuple[float, float]:
     """Algorithmic HBM bytes of one kernel class over a frame.
 
     Returns (compulsory, survey): `compulsory` is the stream every launch must
-    move through HBM (radiance records, queue entries, film) plus the scene's
-    BVH and triangles read once; `survey` is SURVEY.md §8(d)'s literal figure,
-    which prices every counted node visit (64 B) and triangle test (48 B) as
-    HBM traffic even when the scene is cache/LDS resident."""
+    move through HBM (radiance records, queue entries, hit records, film) plus
+    the scene's BVH and triangles read once; `survey` is SURVEY.md §8(d)'s
+    literal figure, which prices every counted node visit (64 B) and triangle
+    test (48 B) as HBM traffic even when the scene is cache/LDS resident.
+    `split`: the large-scene path (separate trace and shade kernels, 8 B hit
+    records; the shading stream is class "shade")."""
     npaths = stats.camera_rays
     ext = stats.extension_rays
     sh = stats.shadow_rays
     c0, s0 = stats.primary_continued, stats.primary_shadow
+    ce, se = ext - c0, sh - s0
     node, tri = 64.0, 48.0
+    trav = None
     if cls == "primary":
-        stream = npaths * 16.0 + c0 * 48.0 + s0 * 48.0
-        trav = node * stats.trav_nodes[0] + tri * stats.trav_tris[0] + tri * max(c0, s0)
+        if split:
+            stream = npaths * 8.0
+        else:
+            stream = npaths * 16.0 + c0 * 48.0 + s0 * 48.0
+        trav = node * stats.trav_nodes[0] + tri * stats.trav_tris[0]
     elif cls == "extend":
-        ce, se = ext - c0, sh - s0
-        stream = ext * (48.0 + 32.0) + ce * 48.0 + se * 48.0
-        trav = node * stats.trav_nodes[1] + tri * stats.trav_tris[1] + tri * max(ce, se)
+        if split:
+            stream = ext * (32.0 + 8.0)
+        else:
+            stream = ext * (48.0 + 32.0) + ce * 48.0 + se * 48.0
+        trav = node * stats.trav_nodes[1] + tri * stats.trav_tris[1]
     elif cls == "shadow":
         stream = sh * (48.0 + 32.0)
         trav = node * stats.trav_nodes[2] + tri * stats.trav_tris[2]
+    elif cls == "shade":
+        stream = (npaths * (8.0 + 16.0) + ext * (48.0 + 8.0 + 32.0) + (c0 + ce) * 48.0 + (s0 + se) * 48.0
+                  + tri * (npaths + ext))
+        return stream, stream
     elif cls == "accumulate":
         npix = stats.width * stats.height
         return (npix * (stats.spp * 16.0 + 32.0 * max(stats.chunks - 1, 0) + 16.0 + 4.0),) * 2
@@ -118,22 +132,24 @@ def algorithmic_bytes(cls: str, stats, scene_bytes: float) -> tuple[float, float
     return stream + min(trav, scene_bytes), stream + trav
 
 
-KERNEL_OF_CLASS = {"build": None, "primary": "k_primary", "extend": "k_extend", "shadow": "k_shadow",
-                   "accumulate": "k_accumulate"}
+# kernel names per class: fused (LDS scenes) and split (large scenes) paths
+KERNEL_OF_CLASS = {"build": [], "primary": ["k_primary", "k_trace_primary"],
+                   "extend": ["k_extend", "k_trace_extend"], "shadow": ["k_shadow", "k_shadow_refill"],
+                   "shade": ["k_shade_extend", "k_shade_primary"], "accumulate": ["k_accumulate"]}
 
 
 def pmc_traffic(cls: str, path: str):
     """HBM bytes per launch of the class's timed kernel (not the counting
     instantiation) from a committed rocprofv3 PMC summary (tools/pmc_summary.py
     traffic), or None when absent."""
-    name = KERNEL_OF_CLASS.get(cls)
-    if not name or not os.path.exists(path):
+    if not os.path.exists(path):
         return None
     with open(path) as fh:
         ks = json.load(fh)["kernels"]
-    for k, v in ks.items():
-        if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
-            return {"bytes": v["traffic_bytes"], "source": os.path.relpath(path, ROOT), "kernel": k}
+    for name in KERNEL_OF_CLASS.get(cls, []):
+        for k, v in ks.items():
+            if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
+                return {"bytes": v["traffic_bytes"], "source": os.path.relpath(path, ROOT), "kernel": k}
     return None
 
 
@@ -260,21 +276,26 @@ def main():
             cls = names[dom]
             n = int(cstats.n_triangles)
             scene_bytes = 64.0 * max(n - 1, 1) + 48.0 * n
-            bytes_frame, survey_frame = algorithmic_bytes(cls, cstats, scene_bytes)
+            split = launches[5] > 0
+            bytes_frame, survey_frame = algorithmic_bytes(cls, cstats, scene_bytes, split)
             launches_frame = max(launches[dom] / max(args.steps, 1), 1)
             avg_ms = kernel_ms[dom] / max(launches[dom], 1)
             per_launch = bytes_frame / launches_frame
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             survey_achieved = survey_frame / launches_frame / (avg_ms * 1e-3) / 1e9
-            tr = pmc_traffic(cls, args.pmc_summary)
+            pmc = args.pmc_summary or os.path.join(
+                ROOT, "profiles", "r1_pmc.json" if args.workload == "04vs" else f"r1_pmc_{args.workload}.json")
+            tr = pmc_traffic(cls, pmc)
             roofline = {"bound": "hbm", "kernel": cls, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                         "traffic": round(tr["bytes"]) if tr else None,
                         "traffic_source": tr["source"] if tr else None,
+                        "traffic_gbs": round(tr["bytes"] / (avg_ms * 1e-3) / 1e9, 1) if tr else None,
                         "bytes_per_launch": round(per_launch), "avg_launch_ms": round(avg_ms, 4),
                         "achieved_survey_formula": round(survey_achieved, 2),
                         "note": "achieved = compulsory bytes (stream + scene once); the SURVEY 8(d) formula "
-                                "also prices cache/LDS-resident node and triangle reads"}
+                                "also prices cache/LDS-resident node and triangle reads; traffic = PMC HBM "
+                                "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE), traffic_gbs its rate"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -1,29 +1,34 @@
 #!/usr/bin/env bash
-# Kernel-trace stats + separate PMC passes of the bench workload (one counter
+# Kernel-trace stats + separate PMC passes of a bench workload (one counter
 # group per run, MI355X_MICROARCH.md §rocprofv3 PMC slots), then per-kernel
 # summaries. Run on the GPU box from the repo root:
-#   tools/profile_round.sh r1
+#   tools/profile_round.sh <tag> [workload] [extra bench args]
+#   tools/profile_round.sh r1                 # 04vs, the headline config
+#   tools/profile_round.sh r1_c5 c5 "--spp 64" # C5 (same per-launch sizes: 32-spp chunks)
 # Outputs under gpurun_out/prof_<tag>/; copy the summaries into profiles/.
 set -euo pipefail
 tag=${1:-r1}
+wl=${2:-04vs}
+extra=${3:-}
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 
-B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile"
+if [ "$wl" == "c5" ]; then steps="--steps 2 --warmup 1"; psteps="--steps 1 --warmup 1"; else steps="--steps 10 --warmup 2"; psteps="--steps 3 --warmup 1"; fi
+B="bench.py --workload $wl $psteps --no-cpu-baseline --no-profile $extra"
 
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
-    -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$out/trace_bench.json"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
+    -- python3 bench.py --workload $wl $steps --no-cpu-baseline $extra > "$out/trace_bench.json"
 echo "trace done"
-timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- python3 $B > /dev/null
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- python3 $B > /dev/null
 echo "fetch done"
-timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- python3 $B > /dev/null
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- python3 $B > /dev/null
 echo "write done"
-timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
     SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
     --output-format csv -d "$out/sq1" -o run -- python3 $B > /dev/null
 echo "sq1 done"
-timeout -s KILL 150 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_WR \
+timeout -s KILL 240 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_WR \
     TCC_HIT_sum TCC_MISS_sum \
     --output-format csv -d "$out/sq2" -o run -- python3 $B > /dev/null
 echo "sq2 done"
