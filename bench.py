@@ -280,9 +280,15 @@ def main():
             bytes_frame, survey_frame = algorithmic_bytes(cls, cstats, scene_bytes, split)
             launches_frame = max(launches[dom] / max(args.steps, 1), 1)
             avg_ms = kernel_ms[dom] / max(launches[dom], 1)
-            per_launch = bytes_frame / launches_frame
+            # LDS-resident scenes (fused path): node/triangle reads never reach
+            # HBM, so `achieved` prices the compulsory stream; scenes traversed
+            # from HBM (split path): SURVEY 8(d)'s figure (every node visit 64 B,
+            # every triangle test 48 B) — DESIGN.md §6
+            model = "survey" if split else "compulsory"
+            per_launch = (survey_frame if split else bytes_frame) / launches_frame
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
             survey_achieved = survey_frame / launches_frame / (avg_ms * 1e-3) / 1e9
+            compulsory_achieved = bytes_frame / launches_frame / (avg_ms * 1e-3) / 1e9
             pmc = args.pmc_summary or os.path.join(
                 ROOT, "profiles", "r1_pmc.json" if args.workload == "04vs" else f"r1_pmc_{args.workload}.json")
             tr = pmc_traffic(cls, pmc)
@@ -292,10 +298,13 @@ def main():
                         "traffic_source": tr["source"] if tr else None,
                         "traffic_gbs": round(tr["bytes"] / (avg_ms * 1e-3) / 1e9, 1) if tr else None,
                         "bytes_per_launch": round(per_launch), "avg_launch_ms": round(avg_ms, 4),
+                        "byte_model": model,
                         "achieved_survey_formula": round(survey_achieved, 2),
-                        "note": "achieved = compulsory bytes (stream + scene once); the SURVEY 8(d) formula "
-                                "also prices cache/LDS-resident node and triangle reads; traffic = PMC HBM "
-                                "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE), traffic_gbs its rate"}
+                        "achieved_compulsory": round(compulsory_achieved, 2),
+                        "note": "achieved: LDS-resident scene -> compulsory bytes (stream + scene once); scene "
+                                "traversed from HBM -> SURVEY 8(d) formula (64 B per node visit, 48 B per "
+                                "triangle test + stream); traffic = PMC HBM bytes per launch (FETCH_SIZE x2 + "
+                                "WRITE_SIZE), traffic_gbs its rate"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -197,7 +197,8 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     if (nl) RR_HIP(hipMemcpyAsync(p.lights.ptr, up, nl * sizeof(float), hipMemcpyHostToDevice, st));
     RR_HIP(hipMemcpyAsync(p.materials.ptr, up + nl, nm * sizeof(float), hipMemcpyHostToDevice, st));
     DevScene& d = s->dev;
-    const bool want4 = force4 || !scene_in_lds(d.n_tris, (int)(nm / RR_MAT_FLOATS), (int)(nl / RR_LIGHT_FLOATS));
+    const bool want4 = force4 || (split_bvh_width() == 4 &&
+                                  !scene_in_lds(d.n_tris, (int)(nm / RR_MAT_FLOATS), (int)(nl / RR_LIGHT_FLOATS)));
     const bool rebuild = !d.built || d.cached_xform != fs.obj_xform || (want4 && !d.has4);
     if (rebuild && d.n_tris > 0) {
         d.obj_xform.ensure(nx);

@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU call that regenerates the round's evidence (run on the GPU box from the
+# repo root): parity tests, rocprof kernel-trace + PMC summaries per workload,
+# then bench lines that quote those summaries. Everything lands in gpurun_out/.
+#   tools/round_evidence.sh r1
+tag=${1:-r1}
+S=tools/gpu_steps.sh
+mkdir -p gpurun_out/ev
+$S 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread ::: \
+   900 tools/profile_round.sh $tag ::: \
+   900 tools/profile_round.sh ${tag}_02 02 ::: \
+   900 tools/profile_round.sh ${tag}_c5 c5 "--spp 64" || exit $?
+cp gpurun_out/prof_$tag/${tag}_pmc.json profiles/r1_pmc.json
+cp gpurun_out/prof_${tag}_02/${tag}_02_pmc.json profiles/r1_pmc_02.json
+cp gpurun_out/prof_${tag}_c5/${tag}_c5_pmc.json profiles/r1_pmc_c5.json
+for wl in 04vs 02 03 c5; do
+    $S 600 python bench.py --workload $wl > gpurun_out/ev/bench_$wl.json || exit $?
+done
+$S 200 python bench.py --serial --no-cpu-baseline > gpurun_out/ev/bench_04vs_serial.json
+$S 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/ev/smoke.log
