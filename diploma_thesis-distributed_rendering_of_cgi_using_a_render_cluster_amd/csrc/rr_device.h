@@ -201,6 +201,40 @@ RR_HD float table_lerp(FloatP t, int n, float u) {
     return t[i] + (t[i + 1] - t[i]) * fr;
 }
 
+// ------------------------------------------------------- screen culling ---
+// Screen-space bounds of the scene box [lo, hi] for the pinhole camera of
+// wavefront.hip camera_ray (pos, right, up, back, half_w, half_h; image W x H):
+// the 8 corners projected to subpixel coordinates (fx, fy of camera_ray), the
+// bounding rectangle widened by one pixel. A camera ray whose (fx, fy) lies
+// outside cannot meet the box, so it is a miss without traversal (every
+// triangle lies in the box, and a hit point projects into the corners' convex
+// hull; the pixel of slack covers rounding). Returns false — no culling — if a
+// corner is not at least 1e-4 in front of the camera. oracle/rr_oracle.c
+// screen_rect() is the same float computation.
+RR_HD bool screen_rect(float3 pos, float3 right, float3 up, float3 back, float half_w, float half_h, float W,
+                       float H, const float lo[3], const float hi[3], float rect[4]) {
+    float x0 = 3.402823466e+38f, x1 = -3.402823466e+38f, y0 = 3.402823466e+38f, y1 = -3.402823466e+38f;
+    for (int k = 0; k < 8; ++k) {
+        const float3 v = mk3(((k & 1) ? hi[0] : lo[0]) - pos.x, ((k & 2) ? hi[1] : lo[1]) - pos.y,
+                             ((k & 4) ? hi[2] : lo[2]) - pos.z);
+        const float depth = -dot3(v, back);
+        if (!(depth > 1.0e-4f)) return false;
+        const float sx = dot3(v, right) / depth;
+        const float sy = dot3(v, up) / depth;
+        const float fx = (sx / half_w + 1.0f) * (W * 0.5f);
+        const float fy = (1.0f - sy / half_h) * (H * 0.5f);
+        x0 = fminf(x0, fx);
+        x1 = fmaxf(x1, fx);
+        y0 = fminf(y0, fy);
+        y1 = fmaxf(y1, fy);
+    }
+    rect[0] = x0 - 1.0f;
+    rect[1] = x1 + 1.0f;
+    rect[2] = y0 - 1.0f;
+    rect[3] = y1 + 1.0f;
+    return true;
+}
+
 // ---------------------------------------------------------- intersection ---
 // Slab test against [bmin,bmax]; inclusive so equal-t candidates survive (the
 // closest hit is then independent of traversal order, see closest_tri()).

@@ -85,13 +85,38 @@ __device__ __forceinline__ Mat load_mat(FloatP mats, int id) {
 
 // Camera ray for (pixel, sample): filter-importance-sampled subpixel position,
 // pinhole through the sensor plane at unit distance, z-depth clipping.
+// Screen rectangle of the scene box (screen_rect), or disabled.
+struct ScreenCull {
+    bool on = false;
+    float r[4];
+    RR_D bool outside(float fx, float fy) const {
+        return on && (fx < r[0] || fx > r[1] || fy < r[2] || fy > r[3]);
+    }
+};
+// From the root node's two child boxes (global or LDS nodes).
+template <typename NodeP>
+RR_D ScreenCull screen_cull(const FrameConsts& fc, NodeP nodes) {
+    ScreenCull sc;
+    if (fc.n_tris <= 0) return sc;
+    const BvhNode nd = load_node(nodes, 0);
+    const float lo[3] = {fminf(nd.a.x, nd.b.z), fminf(nd.a.y, nd.b.w), fminf(nd.a.z, nd.c.x)};
+    const float hi[3] = {fmaxf(nd.a.w, nd.c.y), fmaxf(nd.b.x, nd.c.z), fmaxf(nd.b.y, nd.c.w)};
+    sc.on = screen_rect(fc.cam_pos, fc.cam_right, fc.cam_up, fc.cam_back, fc.half_w, fc.half_h, (float)fc.W,
+                        (float)fc.H, lo, hi, sc.r);
+    return sc;
+}
+
+// culled (optional): set when the ray's subpixel position is outside the
+// scene's screen rectangle (the ray misses everything).
 template <typename FloatP>
 __device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, int pix,
-                                           uint32_t key, float3& o, float3& d, float& tmin, float& tmax) {
+                                           uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
+                                           const ScreenCull* cull = nullptr, bool* culled = nullptr) {
     const int py = (int)fc.div_w.div((uint32_t)pix);
     const int px = pix - py * fc.W;
     const float fx = (float)px + 0.5f + table_lerp(filt, kFilterN, rng(key, 0));
     const float fy = (float)py + 0.5f + table_lerp(filt, kFilterN, rng(key, 1));
+    if (cull) *culled = cull->outside(fx, fy);
     const float sx = (fx * fc.inv_w2 - 1.0f) * fc.half_w;
     const float sy = (1.0f - fy * fc.inv_h2) * fc.half_h;
     const float len = sqrtf(sx * sx + sy * sy + 1.0f);
@@ -398,6 +423,7 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, float4* __r
     TravCount cnt;
     SegCursor cur;
     const uint32_t seg_base = wave_id() * seg_cap;
+    const ScreenCull cull = screen_cull(fc, v.nodes);
     for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {  // block-uniform trip count
         const int p = b0 + (int)threadIdx.x;
         ShadeOut so;
@@ -408,9 +434,10 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, float4* __r
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             float3 o, d;
             float tmin, tmax;
-            camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax);
+            bool culled;
+            camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
             Hit h;
-            traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, tmin, tmax, st, h, cnt);
+            traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cnt);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
             shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
             rad[p] = make_float4(L.x, L.y, L.z, 0.0f);
@@ -736,13 +763,16 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameC
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
+    const ScreenCull cull = screen_cull(fc, sa.nodes);
     trace_refill<SplitTrav<false, kCount>>(
         split_nodes(sa), sa.tris, sa.n_tris, np, st, cnt, [](int p) { return (uint32_t)p; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
             const int sl = (int)fc.div_npix.div(p);
             const int pix = (int)p - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            camera_ray(fc, sa.filter, pix, key, o, d, tmin, tmax);
+            bool culled;
+            camera_ray(fc, sa.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
+            if (culled) tmax = -1.0f;  // empty interval: every box test fails, the ray misses
         },
         [&](int p, uint32_t, const Hit& h) { hits[p] = pack_hit(h); });
     if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);

@@ -634,7 +634,32 @@ typedef struct {
     float clamp, inv_w2, inv_h2;
     float filter[ORC_FILTER_N];
     float srgb[ORC_SRGB_N + 1];
+    int cull_on;          /* screen_rect() succeeded */
+    float cull[4];        /* x0 x1 y0 y1 in subpixel coordinates */
 } scene_t;
+
+/* Screen-space bounds of the scene box, as rr_device.h screen_rect (same
+ * float operations): the 8 corners projected to camera_ray's subpixel
+ * coordinates, bounding rectangle widened by one pixel; 0 if a corner is not
+ * at least 1e-4 in front of the camera. A camera ray outside it misses. */
+static int screen_rect(const float* c, float W, float H, const float lo[3], const float hi[3], float rect[4]) {
+    float x0 = 3.402823466e+38f, x1 = -3.402823466e+38f, y0 = 3.402823466e+38f, y1 = -3.402823466e+38f;
+    v3 pos = V(c[0], c[1], c[2]), right = V(c[3], c[4], c[5]), up = V(c[6], c[7], c[8]), back = V(c[9], c[10], c[11]);
+    for (int k = 0; k < 8; ++k) {
+        v3 v = V(((k & 1) ? hi[0] : lo[0]) - pos.x, ((k & 2) ? hi[1] : lo[1]) - pos.y,
+                 ((k & 4) ? hi[2] : lo[2]) - pos.z);
+        float depth = -vdot(v, back);
+        if (!(depth > 1.0e-4f)) return 0;
+        float sx = vdot(v, right) / depth;
+        float sy = vdot(v, up) / depth;
+        float fx = (sx / c[12] + 1.0f) * (W * 0.5f);
+        float fy = (1.0f - sy / c[13]) * (H * 0.5f);
+        x0 = fminf(x0, fx); x1 = fmaxf(x1, fx);
+        y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
+    }
+    rect[0] = x0 - 1.0f; rect[1] = x1 + 1.0f; rect[2] = y0 - 1.0f; rect[3] = y1 + 1.0f;
+    return 1;
+}
 
 static mat_t load_mat(const float* mats, int id) {
     const float* m = mats + 12 * id;
@@ -661,9 +686,14 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
     v3 o = V(c[0], c[1], c[2]);
     float tmin = c[14] * len, tmax = c[15] * len;
     v3 L = V(0.0f, 0.0f, 0.0f), T = V(1.0f, 1.0f, 1.0f);
+    const int culled = S->cull_on && (fx < S->cull[0] || fx > S->cull[1] || fy < S->cull[2] || fy > S->cull[3]);
     for (int b = 0; b <= S->max_bounces; ++b) {
         hitrec h;
-        trace(S->bvh, o, d, tmin, tmax, 0, &h);
+        if (b == 0 && culled) {
+            h.t = tmax; h.u = h.v = 0.0f; h.idx = -1; h.orig = -1;
+        } else {
+            trace(S->bvh, o, d, tmin, tmax, 0, &h);
+        }
         if (h.idx < 0) {
             v3 cc = vmul(T, S->world);
             if (b > 0) cc = clampc(cc, S->clamp);
@@ -868,6 +898,12 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     S->inv_h2 = 2.0f / (float)S->H;
     orc_filter_table(rf[1], S->filter);
     orc_srgb_lut(S->srgb);
+    if (n_tris > 0) {
+        const float* r = B.box; /* root: two child boxes */
+        float lo[3] = {fminf(r[0], r[6]), fminf(r[1], r[7]), fminf(r[2], r[8])};
+        float hi[3] = {fmaxf(r[3], r[9]), fmaxf(r[4], r[10]), fmaxf(r[5], r[11])};
+        S->cull_on = screen_rect(cam, (float)S->W, (float)S->H, lo, hi, S->cull);
+    }
     const float exposure = rf[2];
     const float inv_spp = 1.0f / (float)S->spp;
     if (row_end <= 0 || row_end > S->H) row_end = S->H;
