@@ -538,6 +538,101 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_extend(FrameConsts f
         extend_body<kCount>(fc, bounce, global_view(sa), in, ix, count, rad, out, sq, sg, spill, tc, stack);
 }
 
+// K-tail (fused path): bounces b_first..max_bounces of every path still alive,
+// each path run to completion by one thread — closest hit, shade, its shadow
+// ray, continue — instead of two launches per bounce. After Russian roulette
+// starts the late bounces carry few paths, and per bounce a launch pair cost
+// ~35 us of fixed work (segment prefix, launch gap) for ~1 us of rays. The
+// radiance additions of a path keep their order (emission(b), NEE(b),
+// emission(b+1), ...), so results are bit-identical to the per-bounce kernels.
+constexpr int kTailBounce = 2;
+
+RR_D void count_wave(uint32_t* __restrict__ ctr, bool pred) {
+    const uint64_t m = __ballot(pred);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(ctr, (uint32_t)__popcll(m));
+}
+
+template <bool kCount, typename View>
+RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue in, const SegIndex& ix, int count,
+                    float4* __restrict__ rad, uint32_t* __restrict__ tot, int32_t* __restrict__ spill,
+                    unsigned long long* __restrict__ tc, lds_int* stack) {
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    const int stride = gridDim.x * kBlock;
+    TravStack st{stack, spill + gtid, stride, 0};
+    TravCount cc, cs;
+    for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
+        const int j = b0 + (int)threadIdx.x;
+        bool live = j < count;
+        float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = o, L = o;
+        uint32_t key = 0;
+        int pid = 0;
+        if (live) {
+            const uint32_t i = ix.slot((uint32_t)j);
+            const float4 a = in.o[i], b = in.d[i], c = in.t[i];
+            pid = f2i(a.w);
+            o = xyz(a);
+            d = xyz(b);
+            T = xyz(c);
+            const int sl = (int)fc.div_npix.div((uint32_t)pid);
+            const int pix = pid - sl * fc.npix;
+            key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
+            L = xyz(rad[pid]);
+        }
+        for (int b = b_first; b <= fc.max_bounces; ++b) {
+            if (!__any(live)) break;
+            ShadeOut so;
+            so.cont = so.shadow = false;
+            if (live) {
+                Hit h;
+                traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cc);
+                shade(fc, b, v, o, d, T, h, key, L, so);
+                if (so.shadow) {
+                    Hit hs;
+                    if (!traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs, cs)) {
+                        L.x = L.x + so.sc.x;
+                        L.y = L.y + so.sc.y;
+                        L.z = L.z + so.sc.z;
+                    }
+                }
+                if (so.cont) {
+                    o = so.o;
+                    d = so.d;
+                    T = so.T;
+                } else {
+                    live = false;
+                }
+            }
+            count_wave(tot + 2 * b, so.cont);        // paths entering b + 1
+            count_wave(tot + 2 * b + 1, so.shadow);  // shadow rays of bounce b
+        }
+        if (j < count) rad[pid] = make_float4(L.x, L.y, L.z, 0.0f);
+    }
+    if (kCount) {
+        flush_counts(tc, 2, cc.nodes, cc.tris);
+        flush_counts(tc, 4, cs.nodes, cs.tris);
+    }
+}
+
+template <bool kCount, bool kLds>
+__global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_tail(FrameConsts fc, int b_first, SceneArgs sa,
+                                                                 PathQueue in, SegIn si, float4* __restrict__ rad,
+                                                                 uint32_t* __restrict__ tot,
+                                                                 int32_t* __restrict__ spill,
+                                                                 unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    extern __shared__ float4 dyn4[];
+    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    int used = 0;
+    LdsView lv;
+    if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, true, used);
+    const SegIndex ix{(lds_uint*)((lds_f4w*)dyn4 + used), si.nseg, si.cap};
+    const int count = (int)seg_prefix(si.seg, si.nseg, ix.pre, si.total);
+    if constexpr (kLds)
+        tail_body<kCount>(fc, b_first, lv, in, ix, count, rad, tot, spill, tc, stack);
+    else
+        tail_body<kCount>(fc, b_first, global_view(sa), in, ix, count, rad, tot, spill, tc, stack);
+}
+
 // K10: shadow rays of one bounce; unoccluded -> radiance += contribution.
 template <bool kCount, typename NodeP, typename TriP>
 RR_D void shadow_body(NodeP nodes, TriP tris, int n_tris, ShadowQueue sq, const SegIndex& ix, int count,
@@ -998,6 +1093,8 @@ using PrimaryFn = void (*)(FrameConsts, SceneArgs, int, float4*, PathQueue, Shad
 using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, float4*, PathQueue, ShadowQueue, SegOut,
                           int32_t*, unsigned long long*);
 using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, float4*, int32_t*, unsigned long long*);
+using TailFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, float4*, uint32_t*, int32_t*,
+                        unsigned long long*);
 // Persistent grid = resident blocks: CUs x blocks per CU the kernel's register
 // and LDS budget admits (a grid-stride loop over more blocks than fit would
 // only queue the surplus behind the first wave of blocks).
@@ -1044,11 +1141,12 @@ namespace {
 // Launch geometry of one frame's path kernels.
 struct Grids {
     bool lds;
-    int primary, extend, shadow;
+    int primary, extend, shadow, tail;
     size_t dyn_primary, dyn_extend, dyn_shadow;
     PrimaryFn kp;
     ExtendFn ke;
     ShadowFn ks;
+    TailFn kt;
     Grids(const FrameConsts& fc, bool count) {
         lds = scene_in_lds(fc.n_tris, fc.n_mats, fc.n_lights);
         kp = lds ? (count ? k_primary<true, true> : k_primary<false, true>)
@@ -1057,6 +1155,8 @@ struct Grids {
                  : (count ? k_extend<true, false> : k_extend<false, false>);
         ks = lds ? (count ? k_shadow<true, true> : k_shadow<false, true>)
                  : (count ? k_shadow<true, false> : k_shadow<false, false>);
+        kt = lds ? (count ? k_tail<true, true> : k_tail<false, true>)
+                 : (count ? k_tail<true, false> : k_tail<false, false>);
         const size_t sp = lds ? scene_lds_bytes(fc, true) : 0, ss = lds ? scene_lds_bytes(fc, false) : 0;
         dyn_primary = sp;
         primary = grid_for(kp, dyn_primary);
@@ -1068,6 +1168,7 @@ struct Grids {
         dyn_shadow = ss + pre;
         extend = grid_for(ke, dyn_extend);
         shadow = grid_for(ks, dyn_shadow);
+        tail = grid_for(kt, dyn_extend);
     }
 };
 // Launch geometry of the split (trace / shade) path of large scenes.
@@ -1247,6 +1348,14 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         int g_prev = gp;  // grid of the producer of the current queues
         uint32_t cap_prev = cap_p;
         for (int b = 0; b <= base.max_bounces; ++b) {
+            if (b >= kTailBounce) {  // the remaining bounces in one launch
+                pr.begin(st, RR_K_EXTEND);
+                G.kt<<<clamp_grid(np, G.tail), kBlock, G.dyn_extend, st>>>(
+                    fc, b, sa, pq[b & 1], SegIn{seg(b - 1, 0), g_prev * kWavesPerBlock, cap_prev, tot + 2 * (b - 1)},
+                    p.rad.ptr, tot, p.spill.ptr, tc);
+                pr.end(st);
+                break;
+            }
             if (b > 0) {
                 pr.begin(st, RR_K_EXTEND);
                 G.ke<<<ge, kBlock, G.dyn_extend, st>>>(fc, b, sa, pq[b & 1],
