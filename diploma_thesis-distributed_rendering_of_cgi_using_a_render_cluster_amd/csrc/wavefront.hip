@@ -44,6 +44,22 @@ constexpr int kLightF = 12;
 constexpr int kMatF = 12;
 constexpr float kFltMax = 3.402823466e+38f;
 
+// Radiance record per path, 3 floats (12 B: dwordx3 loads/stores; a float4
+// record moved 33 % more bytes through the primary / accumulate stream).
+struct Rad {
+    float* p;
+    RR_D float3 get(size_t i) const {
+        const float* q = p + 3 * i;
+        return make_float3(q[0], q[1], q[2]);
+    }
+    RR_D void put(size_t i, float3 v) const {
+        float* q = p + 3 * i;
+        q[0] = v.x;
+        q[1] = v.y;
+        q[2] = v.z;
+    }
+};
+
 // Dense queue state (SoA, ping-pong per bounce).
 struct PathQueue {
     float4* o;  // origin.xyz, path id (int bits)
@@ -414,7 +430,7 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
 // Outputs: segment seg_cap per block of the path queue (bounce 1) and the
 // shadow queue (bounce 0), lengths published in seg_c / seg_s.
 template <bool kCount, typename View>
-RR_D void primary_body(const FrameConsts& fc, const View& v, int np, float4* __restrict__ rad, PathQueue out,
+RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, PathQueue out,
                        ShadowQueue sq, uint32_t seg_cap, uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
                        int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
@@ -440,7 +456,7 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, float4* __r
             traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cnt);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
             shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
-            rad[p] = make_float4(L.x, L.y, L.z, 0.0f);
+            rad.put(p, L);
         }
         emit(so, p, out, sq, seg_base, cur);
     }
@@ -452,7 +468,7 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, float4* __r
 #define RR_FUSED_WAVES 1
 #endif
 template <bool kCount, bool kLds>
-__global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_primary(FrameConsts fc, SceneArgs sa, int np, float4* __restrict__ rad,
+__global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_primary(FrameConsts fc, SceneArgs sa, int np, Rad rad,
                                                     PathQueue out, ShadowQueue sq, uint32_t seg_cap,
                                                     uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
                                                     int32_t* __restrict__ spill,
@@ -485,7 +501,7 @@ struct SegOut {
 
 template <bool kCount, typename View>
 RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueue in, const SegIndex& ix, int count,
-                      float4* __restrict__ rad, PathQueue out, ShadowQueue sq, const SegOut& so_seg,
+                      Rad rad, PathQueue out, ShadowQueue sq, const SegOut& so_seg,
                       int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
@@ -508,10 +524,9 @@ RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueu
             const int sl = (int)fc.div_npix.div((uint32_t)pid);
             const int pix = pid - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            const float4 L4 = rad[pid];
-            float3 L = xyz(L4);
+            float3 L = rad.get(pid);
             shade(fc, bounce, v, o, d, xyz(c), h, key, L, so);
-            rad[pid] = make_float4(L.x, L.y, L.z, 0.0f);
+            rad.put(pid, L);
         }
         emit(so, pid, out, sq, seg_base, cur);
     }
@@ -521,7 +536,7 @@ RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueu
 
 template <bool kCount, bool kLds>
 __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in, SegIn si,
-                                                   float4* __restrict__ rad, PathQueue out, ShadowQueue sq,
+                                                   Rad rad, PathQueue out, ShadowQueue sq,
                                                    SegOut sg, int32_t* __restrict__ spill,
                                                    unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
@@ -545,7 +560,10 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_extend(FrameConsts f
 // ~35 us of fixed work (segment prefix, launch gap) for ~1 us of rays. The
 // radiance additions of a path keep their order (emission(b), NEE(b),
 // emission(b+1), ...), so results are bit-identical to the per-bounce kernels.
-constexpr int kTailBounce = 2;
+#ifndef RR_TAIL_BOUNCE
+#define RR_TAIL_BOUNCE 2
+#endif
+constexpr int kTailBounce = RR_TAIL_BOUNCE;
 
 RR_D void count_wave(uint32_t* __restrict__ ctr, bool pred) {
     const uint64_t m = __ballot(pred);
@@ -554,7 +572,7 @@ RR_D void count_wave(uint32_t* __restrict__ ctr, bool pred) {
 
 template <bool kCount, typename View>
 RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue in, const SegIndex& ix, int count,
-                    float4* __restrict__ rad, uint32_t* __restrict__ tot, int32_t* __restrict__ spill,
+                    Rad rad, uint32_t* __restrict__ tot, int32_t* __restrict__ spill,
                     unsigned long long* __restrict__ tc, lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
@@ -576,7 +594,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
             const int sl = (int)fc.div_npix.div((uint32_t)pid);
             const int pix = pid - sl * fc.npix;
             key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            L = xyz(rad[pid]);
+            L = rad.get(pid);
         }
         for (int b = b_first; b <= fc.max_bounces; ++b) {
             if (!__any(live)) break;
@@ -605,7 +623,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
             count_wave(tot + 2 * b, so.cont);        // paths entering b + 1
             count_wave(tot + 2 * b + 1, so.shadow);  // shadow rays of bounce b
         }
-        if (j < count) rad[pid] = make_float4(L.x, L.y, L.z, 0.0f);
+        if (j < count) rad.put(pid, L);
     }
     if (kCount) {
         flush_counts(tc, 2, cc.nodes, cc.tris);
@@ -615,7 +633,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
 
 template <bool kCount, bool kLds>
 __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_tail(FrameConsts fc, int b_first, SceneArgs sa,
-                                                                 PathQueue in, SegIn si, float4* __restrict__ rad,
+                                                                 PathQueue in, SegIn si, Rad rad,
                                                                  uint32_t* __restrict__ tot,
                                                                  int32_t* __restrict__ spill,
                                                                  unsigned long long* __restrict__ tc) {
@@ -636,7 +654,7 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_tail(FrameConsts fc,
 // K10: shadow rays of one bounce; unoccluded -> radiance += contribution.
 template <bool kCount, typename NodeP, typename TriP>
 RR_D void shadow_body(NodeP nodes, TriP tris, int n_tris, ShadowQueue sq, const SegIndex& ix, int count,
-                      float4* __restrict__ rad, int32_t* __restrict__ spill, unsigned long long* __restrict__ tc,
+                      Rad rad, int32_t* __restrict__ spill, unsigned long long* __restrict__ tc,
                       lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
@@ -649,18 +667,18 @@ RR_D void shadow_body(NodeP nodes, TriP tris, int n_tris, ShadowQueue sq, const 
         if (!traverse<true, kCount>(nodes, tris, n_tris, xyz(a), xyz(b), 0.0f, b.w, st, h, cnt)) {
             const int pid = f2i(a.w);
             const float4 c = sq.c[i];
-            float4 L = rad[pid];
+            float3 L = rad.get(pid);
             L.x = L.x + c.x;
             L.y = L.y + c.y;
             L.z = L.z + c.z;
-            rad[pid] = L;
+            rad.put(pid, L);
         }
     }
     if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
 }
 
 template <bool kCount, bool kLds>
-__global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq, SegIn si, float4* __restrict__ rad,
+__global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq, SegIn si, Rad rad,
                                                    int32_t* __restrict__ spill, unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     extern __shared__ float4 dyn4[];
@@ -876,7 +894,7 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameC
 // Camera paths: shade bounce 0 from hits[p]; appends the bounce-1 path queue
 // and the bounce-0 shadow queue.
 __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np,
-                                                          const float2* __restrict__ hits, float4* __restrict__ rad,
+                                                          const float2* __restrict__ hits, Rad rad,
                                                           PathQueue out, ShadowQueue sq, QueueOut qo) {
     const GlobalView v = global_view(sa);
     const int stride = gridDim.x * kBlock;
@@ -894,7 +912,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
             const Hit h = unpack_hit(hits[p]);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
             shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
-            rad[p] = make_float4(L.x, L.y, L.z, 0.0f);
+            rad.put(p, L);
         }
         emit_grouped(so, p, out, sq, qo);
     }
@@ -928,7 +946,7 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_extend(SceneAr
 // shadow queue.
 __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in,
                                                          QueueIn qi, const float2* __restrict__ hits,
-                                                         float4* __restrict__ rad, PathQueue out, ShadowQueue sq,
+                                                         Rad rad, PathQueue out, ShadowQueue sq,
                                                          QueueOut qo) {
     QueueMap qm;
     qm.init(qi);
@@ -948,10 +966,9 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
             const int sl = (int)fc.div_npix.div((uint32_t)pid);
             const int pix = pid - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            const float4 L4 = rad[pid];
-            float3 L = xyz(L4);
+            float3 L = rad.get(pid);
             shade(fc, bounce, v, xyz(a), xyz(b), xyz(c), h, key, L, so);
-            rad[pid] = make_float4(L.x, L.y, L.z, 0.0f);
+            rad.put(pid, L);
         }
         emit_grouped(so, pid, out, sq, qo);
     }
@@ -960,7 +977,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
 // Shadow rays with lane refill: unoccluded -> radiance += contribution.
 template <bool kCount>
 __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
-                                                                          float4* __restrict__ rad,
+                                                                          Rad rad,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
@@ -982,25 +999,25 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_shadow_refill(SceneA
             if (h.idx >= 0) return;
             const int pid = f2i(sq.o[i].w);
             const float4 c = sq.c[i];
-            float4 L = rad[pid];
+            float3 L = rad.get(pid);
             L.x = L.x + c.x;
             L.y = L.y + c.y;
             L.z = L.z + c.z;
-            rad[pid] = L;
+            rad.put(pid, L);
         });
     if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
 }
 
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
 // sample order; then mean -> exposure -> view transform -> 8-bit.
-__global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, const float4* __restrict__ rad,
+__global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
                                                        float4* __restrict__ film, int first_chunk,
                                                        int last_chunk, const float* __restrict__ srgb,
                                                        uchar4* __restrict__ out) {
     for (int pix = blockIdx.x * kBlock + threadIdx.x; pix < fc.npix; pix += gridDim.x * kBlock) {
         float4 acc = first_chunk ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : film[pix];
         for (int s = 0; s < fc.spp_chunk; ++s) {
-            const float4 L = rad[(size_t)s * fc.npix + pix];
+            const float3 L = rad.get((size_t)s * fc.npix + pix);
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
@@ -1088,12 +1105,12 @@ int device_cu_count() {
 int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2); }
 
 namespace {
-using PrimaryFn = void (*)(FrameConsts, SceneArgs, int, float4*, PathQueue, ShadowQueue, uint32_t, uint32_t*,
+using PrimaryFn = void (*)(FrameConsts, SceneArgs, int, Rad, PathQueue, ShadowQueue, uint32_t, uint32_t*,
                            uint32_t*, int32_t*, unsigned long long*);
-using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, float4*, PathQueue, ShadowQueue, SegOut,
+using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, PathQueue, ShadowQueue, SegOut,
                           int32_t*, unsigned long long*);
-using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, float4*, int32_t*, unsigned long long*);
-using TailFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, float4*, uint32_t*, int32_t*,
+using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, Rad, int32_t*, unsigned long long*);
+using TailFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, uint32_t*, int32_t*,
                         unsigned long long*);
 // Persistent grid = resident blocks: CUs x blocks per CU the kernel's register
 // and LDS budget admits (a grid-stride loop over more blocks than fit would
@@ -1176,7 +1193,7 @@ struct SplitGrids {
     int trace_p, trace_e, shadow, shade_p, shade_e;
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
-    void (*kts)(SceneArgs, ShadowQueue, QueueIn, float4*, int32_t*, unsigned long long*);
+    void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
@@ -1270,14 +1287,14 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         G.ktp<<<clamp_grid(np, G.trace_p), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc);
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
-        k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.rad.ptr, pq[1], sq,
+        k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq,
                                                 QueueOut{qpath(0), qshadow(0), cap_p});
         pr.end(st);
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         for (int b = 0; b <= base.max_bounces; ++b) {
             pr.begin(st, RR_K_SHADOW);
             G.kts<<<clamp_grid(np, G.shadow), kBlock, 0, st>>>(sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1},
-                                                               p.rad.ptr, p.spill.ptr, tc);
+                                                               Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.spill.ptr, tc);
             pr.end(st);
             if (b == base.max_bounces) break;
             const int nb = b + 1;  // bounce being traced and shaded
@@ -1287,14 +1304,14 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             pr.end(st);
             pr.begin(st, RR_K_SHADE);
             k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},
-                                                   p.hits.ptr, p.rad.ptr, pq[(nb + 1) & 1], sq,
+                                                   p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[(nb + 1) & 1], sq,
                                                    QueueOut{qpath(nb), qshadow(nb), cap_e});
             pr.end(st);
             cap_prev = cap_e;
         }
         const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
-        k_accumulate<<<ga, kBlock, 0, st>>>(fc, p.rad.ptr, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
+        k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
     }
@@ -1342,7 +1359,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         const int gp = clamp_grid(np, G.primary), ge = clamp_grid(np, G.extend), gs = clamp_grid(np, G.shadow);
         const uint32_t cap_p = seg_cap(np, gp), cap_e = seg_cap(np, ge);
         pr.begin(st, RR_K_PRIMARY);
-        G.kp<<<gp, kBlock, G.dyn_primary, st>>>(fc, sa, np, p.rad.ptr, pq[1], sq, cap_p, seg(0, 0), seg(0, 1),
+        G.kp<<<gp, kBlock, G.dyn_primary, st>>>(fc, sa, np, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq, cap_p, seg(0, 0), seg(0, 1),
                                                 p.spill.ptr, tc);
         pr.end(st);
         int g_prev = gp;  // grid of the producer of the current queues
@@ -1352,7 +1369,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
                 pr.begin(st, RR_K_EXTEND);
                 G.kt<<<clamp_grid(np, G.tail), kBlock, G.dyn_extend, st>>>(
                     fc, b, sa, pq[b & 1], SegIn{seg(b - 1, 0), g_prev * kWavesPerBlock, cap_prev, tot + 2 * (b - 1)},
-                    p.rad.ptr, tot, p.spill.ptr, tc);
+                    Rad{reinterpret_cast<float*>(p.rad.ptr)}, tot, p.spill.ptr, tc);
                 pr.end(st);
                 break;
             }
@@ -1360,7 +1377,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
                 pr.begin(st, RR_K_EXTEND);
                 G.ke<<<ge, kBlock, G.dyn_extend, st>>>(fc, b, sa, pq[b & 1],
                                                        SegIn{seg(b - 1, 0), g_prev * kWavesPerBlock, cap_prev, tot + 2 * (b - 1)},
-                                                       p.rad.ptr, pq[(b + 1) & 1], sq,
+                                                       Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[(b + 1) & 1], sq,
                                                        SegOut{cap_e, seg(b, 0), seg(b, 1)}, p.spill.ptr, tc);
                 pr.end(st);
                 g_prev = ge;
@@ -1368,12 +1385,12 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
             }
             pr.begin(st, RR_K_SHADOW);
             G.ks<<<gs, kBlock, G.dyn_shadow, st>>>(sa, sq, SegIn{seg(b, 1), g_prev * kWavesPerBlock, cap_prev, tot + 2 * b + 1},
-                                                   p.rad.ptr, p.spill.ptr, tc);
+                                                   Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.spill.ptr, tc);
             pr.end(st);
         }
         const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
-        k_accumulate<<<ga, kBlock, 0, st>>>(fc, p.rad.ptr, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
+        k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
     }
