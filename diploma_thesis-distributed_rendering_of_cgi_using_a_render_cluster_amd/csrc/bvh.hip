@@ -442,6 +442,127 @@ __global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNo
     out[rank[i]] = o;
 }
 
+// ------------------------------------------------------------------ PLOC ---
+// Large scenes (split path) get a PLOC hierarchy (Meister & Bittner 2018,
+// parallel locally-ordered clustering) instead of the Karras LBVH: starting
+// from the Morton-sorted leaves, every cluster finds the neighbour within
+// kPlocR positions whose merged box has the smallest surface measure
+// (dx*dy + dy*dz + dz*dx; ties -> the lower position); mutual nearest
+// neighbours merge into a new node, the survivors are compacted in order, and
+// the rounds repeat until one cluster is left. Node indices are handed out
+// downwards from n-2 in creation order (rank of the merge within its round),
+// so the root — the last merge — is node 0. The result is a binary tree over
+// the same leaves in the same BvhNode format, with fewer node visits per ray
+// than the LBVH on scenes with uneven triangle sizes. oracle/rr_oracle.c
+// ploc_build() is the same algorithm, operation for operation.
+constexpr int kPlocR = 16;
+
+// cluster k: cl[2k] = (lo.xyz, ref bits), cl[2k+1] = (hi.xyz, 0)
+__device__ __forceinline__ float ploc_area(float4 alo, float4 ahi, float4 blo, float4 bhi) {
+    const float dx = fmaxf(ahi.x, bhi.x) - fminf(alo.x, blo.x);
+    const float dy = fmaxf(ahi.y, bhi.y) - fminf(alo.y, blo.y);
+    const float dz = fmaxf(ahi.z, bhi.z) - fminf(alo.z, blo.z);
+    return dx * dy + dy * dz + dz * dx;
+}
+
+// Leaf clusters in Morton order + the leaf-order triangle packs (refit's K5).
+__global__ __launch_bounds__(kBlock) void k_ploc_init(int n, const uint32_t* __restrict__ order,
+                                                      const float4* __restrict__ world,
+                                                      const int32_t* __restrict__ tri_mat,
+                                                      float4* __restrict__ cl, TriPack* __restrict__ tris) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int orig = (int)order[i];
+    const float4 a = world[3 * orig], b = world[3 * orig + 1], c = world[3 * orig + 2];
+    TriPack tp;
+    tp.p0 = make_float4(a.x, a.y, a.z, i2f(orig));
+    tp.p1 = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, i2f(tri_mat[orig]));
+    tp.p2 = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.0f);
+    tris[i] = tp;
+    cl[2 * i] = make_float4(fminf(fminf(a.x, b.x), c.x), fminf(fminf(a.y, b.y), c.y), fminf(fminf(a.z, b.z), c.z),
+                            i2f(~i));
+    cl[2 * i + 1] = make_float4(fmaxf(fmaxf(a.x, b.x), c.x), fmaxf(fmaxf(a.y, b.y), c.y),
+                                fmaxf(fmaxf(a.z, b.z), c.z), 0.0f);
+}
+
+// Nearest neighbour within kPlocR positions (ascending scan, strict <).
+__global__ __launch_bounds__(kBlock) void k_ploc_nn(const int* __restrict__ cnt_in, const float4* __restrict__ cl,
+                                                    int* __restrict__ nn) {
+    const int cnt = *cnt_in;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= cnt) return;
+    const float4 alo = cl[2 * i], ahi = cl[2 * i + 1];
+    float best = __builtin_huge_valf();
+    int bj = -1;
+    const int j0 = max(0, i - kPlocR), j1 = min(cnt - 1, i + kPlocR);
+    for (int j = j0; j <= j1; ++j) {
+        if (j == i) continue;
+        const float a = ploc_area(alo, ahi, cl[2 * j], cl[2 * j + 1]);
+        if (a < best) {
+            best = a;
+            bj = j;
+        }
+    }
+    nn[i] = bj;
+}
+
+// Flags for the two scans (length bound + 1, zero beyond the live count):
+// keep[i] = position i survives (not the upper half of a merge),
+// mrg[i] = position i starts a merge with nn[i] > i.
+__global__ __launch_bounds__(kBlock) void k_ploc_flags(const int* __restrict__ cnt_in, int bound,
+                                                       const int* __restrict__ nn, uint32_t* __restrict__ keep,
+                                                       uint32_t* __restrict__ mrg) {
+    const int cnt = *cnt_in;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i > bound) return;
+    uint32_t k = 0, m = 0;
+    if (i < cnt) {
+        const int j = nn[i];
+        const bool mutual = j >= 0 && nn[j] == i;
+        m = (mutual && i < j) ? 1u : 0u;
+        k = (mutual && j < i) ? 0u : 1u;
+    }
+    keep[i] = k;
+    mrg[i] = m;
+}
+
+// Merge and compact (keep / mrg hold exclusive prefix sums, [bound] = totals).
+__global__ __launch_bounds__(kBlock) void k_ploc_apply(const int* __restrict__ cnt_in, const int* __restrict__ next_in,
+                                                       int* __restrict__ cnt_out, int* __restrict__ next_out,
+                                                       int bound, const int* __restrict__ nn,
+                                                       const uint32_t* __restrict__ keep,
+                                                       const uint32_t* __restrict__ mrg,
+                                                       const float4* __restrict__ cl, float4* __restrict__ cl_out,
+                                                       BvhNode* __restrict__ nodes) {
+    const int cnt = *cnt_in, next = *next_in;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i == 0) {
+        *cnt_out = (int)keep[bound];
+        *next_out = next - (int)mrg[bound];
+    }
+    if (i >= cnt) return;
+    const int j = nn[i];
+    const bool mutual = j >= 0 && nn[j] == i;
+    if (mutual && j < i) return;  // merged into position j
+    const float4 alo = cl[2 * i], ahi = cl[2 * i + 1];
+    const uint32_t o = keep[i];
+    if (mutual) {
+        const int idx = next - (int)mrg[i];
+        const float4 blo = cl[2 * j], bhi = cl[2 * j + 1];
+        BvhNode nd;
+        nd.a = make_float4(alo.x, alo.y, alo.z, ahi.x);
+        nd.b = make_float4(ahi.y, ahi.z, blo.x, blo.y);
+        nd.c = make_float4(blo.z, bhi.x, bhi.y, bhi.z);
+        nd.d = make_int4(f2i(alo.w), f2i(blo.w), 0, 0);
+        nodes[idx] = nd;
+        cl_out[2 * o] = make_float4(fminf(alo.x, blo.x), fminf(alo.y, blo.y), fminf(alo.z, blo.z), i2f(idx));
+        cl_out[2 * o + 1] = make_float4(fmaxf(ahi.x, bhi.x), fmaxf(ahi.y, bhi.y), fmaxf(ahi.z, bhi.z), 0.0f);
+    } else {
+        cl_out[2 * o] = alo;
+        cl_out[2 * o + 1] = ahi;
+    }
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 void exclusive_scan(DevScene& s, uint32_t* data, int m, hipStream_t st) {
@@ -461,12 +582,57 @@ void DevScene::release() {
     hist.release(); scan_part.release(); children.release(); node_parent.release();
     leaf_parent.release(); flags.release(); nodes.release(); tris.release(); nodes4.release(); rank4.release();
     range.release();
+    for (int k = 0; k < 2; ++k) ploc_cl[k].release();
+    ploc_nn.release(); ploc_keep.release(); ploc_mrg.release(); ploc_ctl.release();
     has4 = false;
+    ploc = false;
     built = false;
     uploaded = false;
 }
 
-void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4) {
+// PLOC rounds after the Morton sort (sorted order in vals[0]).
+void build_ploc(DevScene& s, hipStream_t st) {
+    const int n = s.n_tris;
+    s.ploc_cl[0].ensure((size_t)2 * n);
+    s.ploc_cl[1].ensure((size_t)2 * n);
+    s.ploc_nn.ensure((size_t)n);
+    s.ploc_keep.ensure((size_t)n + 1);
+    s.ploc_mrg.ensure((size_t)n + 1);
+    s.ploc_ctl.ensure(4);
+    k_ploc_init<<<cdiv(n, kBlock), kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr,
+                                                     s.ploc_cl[0].ptr, s.tris.ptr);
+    const int init[4] = {n, n - 2, 0, 0};  // ctl[0/1]: count ping-pong, ctl[2/3]: next-index ping-pong
+    const int ctl_host[4] = {init[0], 0, init[1], 0};
+    RR_HIP(hipMemcpyAsync(s.ploc_ctl.ptr, ctl_host, sizeof ctl_host, hipMemcpyHostToDevice, st));
+    RR_HIP(hipStreamSynchronize(st));  // ctl_host is on the stack
+    int bound = n, cur = 0, rounds = 0;
+    for (;;) {
+        // a batch of rounds without host synchronisation; kernels read the live count
+        for (int r = 0; r < 4; ++r, ++rounds) {
+            int* cin = s.ploc_ctl.ptr + cur;
+            int* cout = s.ploc_ctl.ptr + (1 - cur);
+            int* nin = s.ploc_ctl.ptr + 2 + cur;
+            int* nout = s.ploc_ctl.ptr + 2 + (1 - cur);
+            const int g = cdiv(bound + 1, kBlock);
+            k_ploc_nn<<<g, kBlock, 0, st>>>(cin, s.ploc_cl[cur].ptr, s.ploc_nn.ptr);
+            k_ploc_flags<<<g, kBlock, 0, st>>>(cin, bound, s.ploc_nn.ptr, s.ploc_keep.ptr, s.ploc_mrg.ptr);
+            exclusive_scan(s, s.ploc_keep.ptr, bound + 1, st);
+            exclusive_scan(s, s.ploc_mrg.ptr, bound + 1, st);
+            k_ploc_apply<<<g, kBlock, 0, st>>>(cin, nin, cout, nout, bound, s.ploc_nn.ptr, s.ploc_keep.ptr,
+                                               s.ploc_mrg.ptr, s.ploc_cl[cur].ptr, s.ploc_cl[1 - cur].ptr,
+                                               s.nodes.ptr);
+            cur = 1 - cur;
+        }
+        int cnt = 0;
+        RR_HIP(hipMemcpyAsync(&cnt, s.ploc_ctl.ptr + cur, sizeof cnt, hipMemcpyDeviceToHost, st));
+        RR_HIP(hipStreamSynchronize(st));
+        if (cnt <= 1) break;
+        if (cnt >= bound || rounds > 4 * 64 + 2 * n) throw std::runtime_error("PLOC made no progress");
+        bound = cnt;
+    }
+}
+
+void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, bool want_ploc) {
     const int n = s.n_tris;
     s.has4 = false;
     if (n <= 0) {
@@ -510,6 +676,15 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4) {
     if (cur != 0) {  // keep sorted data in slot 0 (4 passes: already back in 0)
         std::swap(s.keys[0], s.keys[1]);
         std::swap(s.vals[0], s.vals[1]);
+    }
+    s.ploc = want_ploc && n > 2 && !want4;
+    if (s.ploc) {
+        build_ploc(s, st);
+        if (prof) prof->end(st);
+        RR_HIP(hipGetLastError());
+        s.has4 = false;
+        s.built = true;
+        return;
     }
     if (n > 1) {
         k_karras<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n, s.keys[0].ptr, s.children.ptr,

@@ -73,6 +73,12 @@ struct DevScene {
     DevBuf<Bvh4Node> nodes4;   // BVH4 collapse of `nodes` (split path), <= n-1
     DevBuf<uint32_t> rank4;    // BVH2 node -> BVH4 index (exclusive scan); [n-1] = BVH4 count
     bool has4 = false;
+    // PLOC build (large scenes): cluster ping-pong, neighbours, scan flags, counters
+    DevBuf<float4> ploc_cl[2];
+    DevBuf<int32_t> ploc_nn;
+    DevBuf<uint32_t> ploc_keep, ploc_mrg;
+    DevBuf<int32_t> ploc_ctl;
+    bool ploc = false;  // the current nodes come from PLOC (else the Karras LBVH)
     std::vector<float> cached_xform;  // obj_xform of the current build
     bool built = false;
     bool uploaded = false;
@@ -163,7 +169,9 @@ struct FrameConsts {
 // LBVH build for the current obj_xform (uploaded by the caller).
 // Stream-ordered; no host synchronisation inside.
 // want4: also collapse it into the BVH4 the split path traverses.
-void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof = nullptr, bool want4 = false);
+// want_ploc: build the PLOC hierarchy instead (large scenes; not with want4).
+void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof = nullptr, bool want4 = false,
+                bool want_ploc = false);
 
 // Whether the path kernels take the LDS-resident (fused, BVH2) variant for a
 // scene of these sizes; otherwise the split path over the BVH4 in HBM.

@@ -166,7 +166,19 @@ void bind_scene(rr_ctx* c, rr_scene* s) {
 // Upload per-frame constants and (re)build the LBVH if object transforms changed.
 // `staging` (pinned, per frame slot) keeps the host-to-device copies
 // asynchronous, so a frame can be enqueued while the previous one still runs.
-bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& staging, bool force4 = false) {
+// Hierarchy ids (render_ints[7] of rr_debug_frame_state, rr_debug_trace):
+// 2 = Karras LBVH (BVH2), 3 = PLOC (BVH2), 4 = LBVH collapsed to the BVH4.
+constexpr int kHierLbvh = 2, kHierPloc = 3, kHierBvh4 = 4;
+
+// The hierarchy the frame kernels walk: LDS-resident scenes the LBVH (fused
+// path), larger scenes PLOC (split path; or the BVH4 when built for it).
+int frame_hier(int n_tris, int n_mats, int n_lights) {
+    if (scene_in_lds(n_tris, n_mats, n_lights)) return kHierLbvh;
+    return split_bvh_width() == 4 ? kHierBvh4 : kHierPloc;
+}
+
+// hier: 0 = the frame's hierarchy, else a kHier* id (inspection entry points).
+bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& staging, int hier = 0) {
     bind_scene(c, s);
     hipStream_t st = c->stream;
     DevPaths& p = c->paths;
@@ -197,13 +209,15 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     if (nl) RR_HIP(hipMemcpyAsync(p.lights.ptr, up, nl * sizeof(float), hipMemcpyHostToDevice, st));
     RR_HIP(hipMemcpyAsync(p.materials.ptr, up + nl, nm * sizeof(float), hipMemcpyHostToDevice, st));
     DevScene& d = s->dev;
-    const bool want4 = force4 || (split_bvh_width() == 4 &&
-                                  !scene_in_lds(d.n_tris, (int)(nm / RR_MAT_FLOATS), (int)(nl / RR_LIGHT_FLOATS)));
-    const bool rebuild = !d.built || d.cached_xform != fs.obj_xform || (want4 && !d.has4);
+    if (hier == 0) hier = frame_hier(d.n_tris, (int)(nm / RR_MAT_FLOATS), (int)(nl / RR_LIGHT_FLOATS));
+    const bool want4 = hier == kHierBvh4;
+    const bool want_ploc = hier == kHierPloc && d.n_tris > 2;
+    const bool rebuild =
+        !d.built || d.cached_xform != fs.obj_xform || (want4 && !d.has4) || (want_ploc != d.ploc);
     if (rebuild && d.n_tris > 0) {
         d.obj_xform.ensure(nx);
         RR_HIP(hipMemcpyAsync(d.obj_xform.ptr, up + nl + nm, nx * sizeof(float), hipMemcpyHostToDevice, st));
-        build_lbvh(d, st, &p.prof, want4);
+        build_lbvh(d, st, &p.prof, want4, want_ploc);
         d.cached_xform = fs.obj_xform;
     } else if (rebuild) {
         d.built = true;
@@ -410,11 +424,9 @@ int do_encode(const uint8_t* rgba, int W, int H, const char* out_path, const cha
 
 // BVH width the frame kernels traverse for this scene (2: LDS-resident fused
 // path, 4: split path from HBM).
-int frame_bvh_width(rr_scene* s, const FrameSetup& fs) {
-    return scene_in_lds(s->dev.n_tris, (int)(fs.materials.size() / RR_MAT_FLOATS),
-                        (int)(fs.lights.size() / RR_LIGHT_FLOATS))
-               ? 2
-               : split_bvh_width();
+int frame_hier_of(rr_scene* s, const FrameSetup& fs) {
+    return frame_hier(s->dev.n_tris, (int)(fs.materials.size() / RR_MAT_FLOATS),
+                      (int)(fs.lights.size() / RR_LIGHT_FLOATS));
 }
 
 FrameSlot* slot_for(rr_ctx* c, uint64_t ticket) { return &c->slots[ticket % RR_MAX_FRAMES_IN_FLIGHT]; }
@@ -691,7 +703,7 @@ int rr_debug_frame_state(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_
         if (world) std::memcpy(world, fs.world, sizeof fs.world);
         if (render_ints) {
             const int32_t ri[RR_RENDER_INTS] = {fs.W, fs.H, fs.spp, fs.max_bounces, (int32_t)fs.seed,
-                                               fs.view_transform, choose_spp_chunk(fs), frame_bvh_width(s, fs)};
+                                               fs.view_transform, choose_spp_chunk(fs), frame_hier_of(s, fs)};
             std::memcpy(render_ints, ri, sizeof ri);
         }
         if (render_floats) {
@@ -742,7 +754,7 @@ int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* c
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
         PinnedBuf staging;
-        prepare_frame(c, s, fs, staging, true);
+        prepare_frame(c, s, fs, staging, kHierBvh4);
         DevScene& d = s->dev;
         hipStream_t st = c->stream;
         const int n = d.n_tris;
@@ -776,14 +788,16 @@ int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* c
 int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int32_t n, const float* rays,
                    float* hits, int32_t* prims, uint8_t* occluded) {
     if (!c || !s || n < 0 || (n > 0 && !rays)) return fail(RR_EINVAL, "bad arguments");
-    if (bvh_width != 0 && bvh_width != 2 && bvh_width != 4) return fail(RR_EINVAL, "bvh_width must be 0, 2 or 4");
+    if (bvh_width < 0 || bvh_width == 1 || bvh_width > 4)
+        return fail(RR_EINVAL, "hierarchy must be 0 (frame's), 2 (LBVH), 3 (PLOC) or 4 (BVH4)");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
         PinnedBuf staging;
-        const int width = bvh_width ? bvh_width : frame_bvh_width(s, fs);
-        prepare_frame(c, s, fs, staging, width == 4);
+        const int hier = bvh_width ? bvh_width : frame_hier_of(s, fs);
+        prepare_frame(c, s, fs, staging, hier);
+        const int width = hier == kHierBvh4 ? 4 : 2;
         hipStream_t st = c->stream;
         DevBuf<float4> dr, dh;
         DevBuf<int32_t> dp;

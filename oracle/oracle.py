@@ -31,6 +31,7 @@ def lib():
                            ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint8))
         c_int = ctypes.c_int
         L.orc_build_lbvh.argtypes = [c_int, f, u32, u32, i32, f]
+        L.orc_build_bvh.argtypes = [c_int, f, c_int, u32, u32, i32, f]
         L.orc_trace.argtypes = [c_int, f, c_int, f, f, i32, u8]
         L.orc_trace_w.argtypes = [c_int, f, c_int, c_int, f, f, i32, u8]
         L.orc_build_bvh4.argtypes = [c_int, f, i32, i32, f]
@@ -53,19 +54,21 @@ def _f32(a):
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
-def build_lbvh(tris: np.ndarray):
+def build_lbvh(tris: np.ndarray, hier: int = 2):
+    """Sorted keys, order, children and child boxes of the hierarchy `hier`
+    (2 = Karras LBVH, 3 = PLOC) as rr_debug_bvh."""
     tris = _f32(tris).reshape(-1, 9)
     n = tris.shape[0]
     ni = max(n - 1, 1)
     keys, order = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
     children, boxes = np.zeros((ni, 2), np.int32), np.zeros((ni, 12), np.float32)
-    lib().orc_build_lbvh(n, _p(tris, ctypes.c_float), _p(keys, ctypes.c_uint32), _p(order, ctypes.c_uint32),
-                         _p(children, ctypes.c_int32), _p(boxes, ctypes.c_float))
+    lib().orc_build_bvh(n, _p(tris, ctypes.c_float), int(hier), _p(keys, ctypes.c_uint32),
+                        _p(order, ctypes.c_uint32), _p(children, ctypes.c_int32), _p(boxes, ctypes.c_float))
     return keys, order, children, boxes
 
 
 def trace(tris: np.ndarray, rays: np.ndarray, width: int = 2):
-    """Closest + any hit through the LBVH (width 2) or its BVH4 collapse (4)."""
+    """Closest + any hit through the LBVH (2), PLOC (3) or the LBVH's BVH4 collapse (4)."""
     tris = _f32(tris).reshape(-1, 9)
     rays = _f32(rays).reshape(-1, 8)
     n = rays.shape[0]

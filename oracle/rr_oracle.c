@@ -13,7 +13,8 @@
  *    /root/reference/pull-blender-image.sh:3-4), so Cycles-image parity is
  *    UNPINNED here; see DESIGN.md §5.
  *  - This oracle is the specification of the MI355X renderer's algorithm
- *    (DESIGN.md §4): Karras LBVH over 30-bit Morton codes, closest/any-hit
+ *    (DESIGN.md §4): Karras LBVH over 30-bit Morton codes (PLOC over the same
+ *    sorted leaves for scenes traversed from HBM), closest/any-hit
  *    traversal with an order-independent accept rule, a path tracer with the
  *    Principled-BSDF subset, point/sun NEE, Cycles-style light units
  *    (point: P/(4 pi) W/sr, eval_fac 1/(4 pi) * invarea), indirect clamp,
@@ -214,7 +215,11 @@ static void lbvh_free(lbvh* B) {
     memset(B, 0, sizeof *B);
 }
 
-static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
+static void ploc_build(lbvh* B, const float* tris9);
+
+/* hier: 2 = Karras LBVH, 3 = PLOC over the same sorted leaves (csrc/bvh.hip
+ * build_ploc), 4 = LBVH (collapsed to the BVH4 by the caller). */
+static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats, int hier) {
     memset(B, 0, sizeof *B);
     B->n = n;
     if (n <= 0) return;
@@ -266,6 +271,11 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
     B->child_lf = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->range = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->box = (float*)malloc(sizeof(float) * 12 * (size_t)ni);
+    if (hier == 3 && n > 2) {
+        ploc_build(B, tris9);
+        for (int i = 0; i < 2 * ni; ++i) { B->child_lf[i] = B->child[i]; B->range[i] = 0; }
+        goto pack;
+    }
     if (n == 1) {
         B->child[0] = ~0; B->child[1] = ~0;
     } else {
@@ -324,6 +334,7 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
         B->child_lf[i] = (n > 1 && c >= 0 && B->range[2 * c + 1] <= ORC_LEAF_MAX)
                              ? leaf_ref(B->range[2 * c], B->range[2 * c + 1]) : c;
     }
+pack:
     B->tri = (float*)malloc(sizeof(float) * 9 * (size_t)n);
     B->tri_orig = (int*)malloc(sizeof(int) * n);
     B->tri_mat = (int*)malloc(sizeof(int) * n);
@@ -336,6 +347,78 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats) {
         B->tri_orig[i] = (int)B->order[i];
         B->tri_mat[i] = mats ? mats[B->order[i]] : 0;
     }
+}
+
+/* PLOC (Meister & Bittner 2018), as csrc/bvh.hip build_ploc: clusters start as
+ * the Morton-sorted leaves; each round every cluster takes the neighbour within
+ * ORC_PLOC_R positions with the smallest merged-box measure dx*dy + dy*dz +
+ * dz*dx (ascending scan, strict <: ties -> lower position), mutual nearest
+ * neighbours merge (the lower position keeps the new cluster), survivors are
+ * compacted in order; merge q of a round gets node index next - q, next
+ * starts at n-2 and drops by the round's merges, so the root is node 0. */
+#define ORC_PLOC_R 16
+static float ploc_area(const float* a, const float* b) {
+    float dx = fmaxf(a[3], b[3]) - fminf(a[0], b[0]);
+    float dy = fmaxf(a[4], b[4]) - fminf(a[1], b[1]);
+    float dz = fmaxf(a[5], b[5]) - fminf(a[2], b[2]);
+    return dx * dy + dy * dz + dz * dx;
+}
+
+static void ploc_build(lbvh* B, const float* tris9) {
+    const int n = B->n;
+    int* ref = (int*)malloc(sizeof(int) * (size_t)n);
+    int* ref2 = (int*)malloc(sizeof(int) * (size_t)n);
+    float* box = (float*)malloc(sizeof(float) * 6 * (size_t)n);
+    float* box2 = (float*)malloc(sizeof(float) * 6 * (size_t)n);
+    int* nn = (int*)malloc(sizeof(int) * (size_t)n);
+    for (int i = 0; i < n; ++i) {
+        tri_box(tris9 + 9 * (size_t)B->order[i], box + 6 * (size_t)i);
+        ref[i] = ~i;
+    }
+    int cnt = n, next = n - 2;
+    while (cnt > 1) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+        for (int i = 0; i < cnt; ++i) {
+            float best = INFINITY;
+            int bj = -1;
+            int j0 = i - ORC_PLOC_R < 0 ? 0 : i - ORC_PLOC_R;
+            int j1 = i + ORC_PLOC_R > cnt - 1 ? cnt - 1 : i + ORC_PLOC_R;
+            for (int j = j0; j <= j1; ++j) {
+                if (j == i) continue;
+                float a = ploc_area(box + 6 * (size_t)i, box + 6 * (size_t)j);
+                if (a < best) { best = a; bj = j; }
+            }
+            nn[i] = bj;
+        }
+        int q = 0, k = 0;
+        for (int i = 0; i < cnt; ++i) {
+            int j = nn[i];
+            int mutual = j >= 0 && nn[j] == i;
+            if (mutual && j < i) continue;
+            const float* a = box + 6 * (size_t)i;
+            float* o = box2 + 6 * (size_t)k;
+            if (mutual) {
+                const float* b = box + 6 * (size_t)j;
+                int idx = next - q++;
+                float* nb = B->box + 12 * (size_t)idx;
+                for (int t = 0; t < 6; ++t) { nb[t] = a[t]; nb[6 + t] = b[t]; }
+                B->child[2 * idx] = ref[i];
+                B->child[2 * idx + 1] = ref[j];
+                for (int t = 0; t < 3; ++t) { o[t] = fminf(a[t], b[t]); o[3 + t] = fmaxf(a[3 + t], b[3 + t]); }
+                ref2[k++] = idx;
+            } else {
+                for (int t = 0; t < 6; ++t) o[t] = a[t];
+                ref2[k++] = ref[i];
+            }
+        }
+        next -= q;
+        cnt = k;
+        int* tr = ref; ref = ref2; ref2 = tr;
+        float* tb = box; box = box2; box2 = tb;
+    }
+    free(ref); free(ref2); free(box); free(box2); free(nn);
 }
 
 /* BVH4 collapse of the LBVH, as csrc/bvh.hip k_depth_parity + k_collapse4:
@@ -804,9 +887,10 @@ static unsigned char q8(float f) {
 int orc_abi(void) { return 1; }
 
 /* LBVH of n triangles (tris9: v0 v1 v2 per triangle). Outputs as rr_debug_bvh. */
-int orc_build_lbvh(int n, const float* tris9, uint32_t* keys, uint32_t* order, int32_t* children, float* boxes) {
+int orc_build_bvh(int n, const float* tris9, int hier, uint32_t* keys, uint32_t* order, int32_t* children,
+                  float* boxes) {
     lbvh B;
-    lbvh_build(&B, n, tris9, NULL);
+    lbvh_build(&B, n, tris9, NULL, hier);
     if (n > 0) {
         int ni = n > 1 ? n - 1 : 1;
         if (keys) memcpy(keys, B.keys, sizeof(uint32_t) * n);
@@ -816,6 +900,10 @@ int orc_build_lbvh(int n, const float* tris9, uint32_t* keys, uint32_t* order, i
     }
     lbvh_free(&B);
     return 0;
+}
+
+int orc_build_lbvh(int n, const float* tris9, uint32_t* keys, uint32_t* order, int32_t* children, float* boxes) {
+    return orc_build_bvh(n, tris9, 2, keys, order, children, boxes);
 }
 
 /* Brute force closest hit (no BVH), for pinning the LBVH traversal. */
@@ -842,7 +930,7 @@ int orc_trace_brute(int n, const float* tris9, int n_rays, const float* rays, fl
 /* BVH4 collapse (rr_debug_bvh4 layout): n4 nodes, 4 child refs, 24 floats each. */
 int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, float* boxes4) {
     lbvh B;
-    lbvh_build(&B, n, tris9, NULL);
+    lbvh_build(&B, n, tris9, NULL, 4);
     lbvh_collapse4(&B);
     *n4 = B.n4;
     if (children4 && B.n4) memcpy(children4, B.child4, sizeof(int32_t) * 4 * (size_t)B.n4);
@@ -854,7 +942,7 @@ int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, f
 int orc_trace_w(int n, const float* tris9, int width, int n_rays, const float* rays, float* hits, int32_t* prims,
                 uint8_t* occluded) {
     lbvh B;
-    lbvh_build(&B, n, tris9, NULL);
+    lbvh_build(&B, n, tris9, NULL, width);
     if (width == 4) { lbvh_collapse4(&B); B.width = 4; }
     for (int r = 0; r < n_rays; ++r) {
         const float* R = rays + 8 * (size_t)r;
@@ -883,8 +971,8 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
                const float* lights, const float* mats, const float* world, const int32_t* ri, const float* rf,
                float* film, uint8_t* rgba8, int row_begin, int row_end, int threads) {
     lbvh B;
-    lbvh_build(&B, n_tris, tris9, tri_mat);
-    if (ri[7] == 4) { lbvh_collapse4(&B); B.width = 4; }  /* the hierarchy the product walks */
+    lbvh_build(&B, n_tris, tris9, tri_mat, ri[7] == 3 ? 3 : 2);  /* the hierarchy the product walks */
+    if (ri[7] == 4) { lbvh_collapse4(&B); B.width = 4; }
     scene_t* S = (scene_t*)calloc(1, sizeof(scene_t));
     S->bvh = &B;
     S->cam = cam;

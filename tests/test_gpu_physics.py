@@ -1,7 +1,7 @@
 """Parity of the HIP path with the CPU oracle on the large-scene configs:
-the C4 physics stand-ins (02/03: thousands of rigid bodies, LBVH rebuilt every
-frame) and the C5 synthetic 10M-triangle scene. These scenes
-take the HBM (non-LDS) traversal path. Integer work (Morton keys, radix order,
+the C4 physics stand-ins (02/03: thousands of rigid bodies, hierarchy rebuilt
+every frame) and the C5 synthetic 10M-triangle scene. These
+scenes take the HBM (non-LDS) traversal path over a PLOC hierarchy. Integer work (Morton keys, radix order,
 BVH topology, hit ids) and the float work are bit-exact (tolerance 0), as in
 test_gpu_parity.py. Full-size C5 is checked through size-independent
 properties: the whole 10M-triangle LBVH equals the oracle's, and a ray batch
@@ -53,11 +53,15 @@ def _camera_rays(st, n, rng):
 
 
 @pytest.mark.parametrize("frame", [1, 45, 170])
-def test_physics_lbvh_bit_exact(ctx, s02, frame):
+def test_physics_bvh_bit_exact(ctx, s02, frame):
+    """The frame's hierarchy (PLOC over the Morton-sorted leaves for scenes
+    traversed from HBM) equals the oracle's build, node for node."""
     st = ctx.frame_state(s02, frame)
     assert st.tris.shape[0] == 92002
+    hier = int(st.render_ints[7])
+    assert hier == 3
     keys, order, children, boxes = ctx.bvh(s02, frame)
-    ok, oo, oc, ob = O.build_lbvh(st.tris)
+    ok, oo, oc, ob = O.build_lbvh(st.tris, hier=hier)
     assert np.array_equal(keys, ok)
     assert np.array_equal(order, oo)
     assert np.array_equal(children, oc)
@@ -76,18 +80,19 @@ def test_physics_rebuilds_every_frame(ctx, rr, s02):
     assert stats.bvh_rebuilt == 0
 
 
-@pytest.mark.parametrize("width", [2, 4])
-def test_physics_trace_bit_exact(ctx, s02, width):
+@pytest.mark.parametrize("hier", [3, 2, 4])
+def test_physics_trace_bit_exact(ctx, s02, hier):
+    """Ray batches through PLOC (the frame's hierarchy), the LBVH and its BVH4
+    collapse, each against the oracle's walk of the same hierarchy."""
     st = ctx.frame_state(s02, 90)
-    assert int(st.render_ints[7]) in (2, 4)  # hierarchy the split-path frame kernels walk
     rays = _camera_rays(st, 40000, np.random.default_rng(7))
-    hits, prims, occ = ctx.trace(s02, 90, rays, width=width)
-    oh, op, oo = O.trace(st.tris, rays, width=width)
+    hits, prims, occ = ctx.trace(s02, 90, rays, width=hier)
+    oh, op, oo = O.trace(st.tris, rays, width=hier)
     assert np.array_equal(prims, op), f"{np.count_nonzero(prims != op)} prim mismatches"
     assert np.array_equal(hits, oh)
     assert np.array_equal(occ, oo)
     assert (prims >= 0).mean() > 0.3
-    if width == 4:  # both hierarchies find the same closest hits
+    if hier != 2:  # all hierarchies find the same closest hits here
         h2, p2, o2 = O.trace(st.tris, rays, width=2)
         assert np.array_equal(p2, op) and np.array_equal(o2, oo)
 
@@ -129,14 +134,14 @@ def sc5(ctx):
     s.close()
 
 
-def test_c5_full_size_lbvh_bit_exact(ctx, sc5):
-    """All 10,485,762 triangles: Morton keys, radix order, topology and every
-    node's child boxes equal the oracle's build."""
+def test_c5_full_size_bvh_bit_exact(ctx, sc5):
+    """All 10,485,762 triangles: Morton keys, radix order, the PLOC topology
+    and every node's child boxes equal the oracle's build."""
     st = ctx.frame_state(sc5, 120)
     n = st.tris.shape[0]
     assert n == 512 * 20480 + 2
     keys, order, children, boxes = ctx.bvh(sc5, 120)
-    ok, oo, oc, ob = O.build_lbvh(st.tris)
+    ok, oo, oc, ob = O.build_lbvh(st.tris, hier=int(st.render_ints[7]))
     assert np.array_equal(keys, ok)
     assert np.array_equal(order, oo)
     assert np.array_equal(children, oc)
@@ -157,7 +162,7 @@ def test_c5_full_size_bvh4_bit_exact(ctx, sc5):
     assert np.array_equal(np.sort(leaves), np.arange(st.tris.shape[0]))
 
 
-@pytest.mark.parametrize("width", [2, 4])
+@pytest.mark.parametrize("width", [3, 4])
 def test_c5_trace_bit_exact(ctx, sc5, width):
     st = ctx.frame_state(sc5, 200)
     rays = _camera_rays(st, 100000, np.random.default_rng(11))

@@ -233,3 +233,32 @@ def test_bvh4_collapse_and_walk_equal_brute_force(n, seed):
     assert np.array_equal(p4, bp) and np.array_equal(p2, bp)
     assert np.array_equal(h4[:, 0], bh[:, 0])
     assert np.array_equal(o4, o2)
+
+
+@pytest.mark.parametrize("n,seed", [(3, 0), (50, 1), (2000, 2)])
+def test_ploc_structure_and_walk_equal_brute_force(n, seed):
+    """PLOC (hier 3): a binary tree over all leaves with node 0 as the root,
+    boxes containing their subtrees, closest hits equal to brute force."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-8, 8, (n, 1, 3)) * rng.uniform(0.2, 1.0, (n, 1, 1))
+    tris = (c + rng.normal(0, 0.3, (n, 3, 3)) * rng.uniform(0.1, 3.0, (n, 1, 1))).astype(np.float32)
+    keys, order, children, boxes = O.build_lbvh(tris, hier=3)
+    k2, o2, _, _ = O.build_lbvh(tris, hier=2)
+    assert np.array_equal(keys, k2) and np.array_equal(order, o2)  # same sorted leaves
+    leaves, inner, refs = walk_lbvh(children)
+    assert sorted(leaves) == list(range(n))
+    assert sorted(inner) == list(range(n - 1))
+    for node, side, first, count in refs:
+        t = tris[order[first]]
+        lo, hi = boxes[node, 6 * side:6 * side + 3], boxes[node, 6 * side + 3:6 * side + 6]
+        assert np.all(t >= lo) and np.all(t <= hi)
+    m = 3000
+    rays = np.zeros((m, 8), np.float32)
+    rays[:, 0:3] = rng.uniform(-10, 10, (m, 3))
+    d = rng.normal(0, 1, (m, 3))
+    rays[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 7] = 1e30
+    h3, p3, o3 = O.trace(tris, rays, width=3)
+    bh, bp = O.trace_brute(tris, rays)
+    assert np.array_equal(p3, bp)
+    assert np.array_equal(h3[:, 0], bh[:, 0])
