@@ -455,7 +455,10 @@ __global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNo
 // the same leaves in the same BvhNode format, with fewer node visits per ray
 // than the LBVH on scenes with uneven triangle sizes. oracle/rr_oracle.c
 // ploc_build() is the same algorithm, operation for operation.
-constexpr int kPlocR = 16;
+#ifndef RR_PLOC_R
+#define RR_PLOC_R 16
+#endif
+constexpr int kPlocR = RR_PLOC_R;
 
 // cluster k: cl[2k] = (lo.xyz, ref bits), cl[2k+1] = (hi.xyz, 0)
 __device__ __forceinline__ float ploc_area(float4 alo, float4 ahi, float4 blo, float4 bhi) {
