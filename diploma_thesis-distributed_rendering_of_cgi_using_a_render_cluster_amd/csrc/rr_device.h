@@ -655,8 +655,18 @@ RR_HD float schlick_w(float c) {
 // Principled BSDF (v1) subset: Disney diffuse with retro-reflection + GGX
 // specular (Smith separable G, Schlick Fresnel from F0 = lerp(0.08*specular,
 // base, metallic)). Returns f and the combined one-sample-MIS pdf.
-RR_HD float3 bsdf_eval(const Mat& m, float3 N, float3 wo, float3 wi, float ps, float& pdf) {
-    const float cosV = dot3(N, wo);
+// Terms of the view direction shared by every evaluation at one shading point
+// (NEE and the sampled continuation): computed once, with exactly the
+// operations bsdf_eval used to repeat, so results are unchanged bit for bit.
+struct BsdfView {
+    float cosV, ps, fv, g1v;
+};
+
+// Principled BSDF (v1) subset: Disney diffuse with retro-reflection + GGX
+// specular (Smith separable G, Schlick Fresnel from F0 = lerp(0.08*specular,
+// base, metallic)). Returns f and the combined one-sample-MIS pdf.
+RR_HD float3 bsdf_eval_v(const Mat& m, const BsdfView& vw, float3 N, float3 wo, float3 wi, float& pdf) {
+    const float cosV = vw.cosV;
     const float cosL = dot3(N, wi);
     if (cosV <= 0.0f || cosL <= 0.0f) {
         pdf = 0.0f;
@@ -666,6 +676,7 @@ RR_HD float3 bsdf_eval(const Mat& m, float3 N, float3 wo, float3 wi, float ps, f
         pdf = cosL * 0.318309886183791f;
         return scl3(m.base, 0.318309886183791f);
     }
+    const float ps = vw.ps;
     const float3 H = norm3(add3(wo, wi));
     const float cosD = dot3(wi, H);
     const float NdotH = dot3(N, H);
@@ -675,13 +686,13 @@ RR_HD float3 bsdf_eval(const Mat& m, float3 N, float3 wo, float3 wi, float ps, f
     // diffuse
     const float fd90 = 0.5f + 2.0f * m.roughness * cosD * cosD;
     const float fl = schlick_w(cosL);
-    const float fv = schlick_w(cosV);
+    const float fv = vw.fv;
     const float kd = (1.0f - m.metallic) * 0.318309886183791f * (1.0f + (fd90 - 1.0f) * fl) *
                      (1.0f + (fd90 - 1.0f) * fv);
     // specular
     const float tt = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
     const float D = a2 / (3.14159265358979f * tt * tt);
-    const float g1v = 2.0f * cosV / (cosV + sqrtf(a2 + (1.0f - a2) * cosV * cosV));
+    const float g1v = vw.g1v;
     const float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
     const float s0 = 0.08f * m.specular;
     const float3 F0 = mk3(s0 + (m.base.x - s0) * m.metallic, s0 + (m.base.y - s0) * m.metallic,
@@ -708,6 +719,26 @@ RR_HD float spec_prob(const Mat& m, float cosV) {
     return tot > 0.0f ? wsp / tot : 1.0f;
 }
 
+RR_HD BsdfView bsdf_view(const Mat& m, float3 N, float3 wo) {
+    BsdfView v;
+    v.cosV = dot3(N, wo);
+    v.ps = spec_prob(m, v.cosV);
+    v.fv = schlick_w(v.cosV);
+    float alpha = m.roughness * m.roughness;
+    if (alpha < 1.0e-4f) alpha = 1.0e-4f;
+    const float a2 = alpha * alpha;
+    v.g1v = 2.0f * v.cosV / (v.cosV + sqrtf(a2 + (1.0f - a2) * v.cosV * v.cosV));
+    return v;
+}
+
+// The one-shot form (tests / inspection): same result as bsdf_eval_v with
+// bsdf_view(m, N, wo), except that the caller's ps is used.
+RR_HD float3 bsdf_eval(const Mat& m, float3 N, float3 wo, float3 wi, float ps, float& pdf) {
+    BsdfView v = bsdf_view(m, N, wo);
+    v.ps = ps;
+    return bsdf_eval_v(m, v, N, wo, wi, pdf);
+}
+
 // GGX visible-normal sample (Heitz 2018) in the local frame (N = +z).
 RR_HD float3 sample_vndf(float3 v, float alpha, float u1, float u2) {
     const float3 vh = norm3(mk3(alpha * v.x, alpha * v.y, v.z));
@@ -731,11 +762,11 @@ RR_HD float3 sample_vndf(float3 v, float alpha, float u1, float u2) {
 }
 
 // Sample a direction; returns false when the path must end.
-RR_HD bool bsdf_sample(const Mat& m, float3 N, float3 wo, float ul, float u1, float u2,
+RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, float ul, float u1, float u2,
                        float3& wi, float3& f, float& pdf) {
-    const float cosV = dot3(N, wo);
+    const float cosV = vw.cosV;
     if (cosV <= 0.0f) return false;
-    const float ps = spec_prob(m, cosV);
+    const float ps = vw.ps;
     float3 T, B;
     make_onb(N, T, B);
     if (ul < ps) {
@@ -753,7 +784,7 @@ RR_HD bool bsdf_sample(const Mat& m, float3 N, float3 wo, float ul, float u1, fl
         const float z = sqrtf(fmaxf(0.0f, 1.0f - x * x - y * y));
         wi = mk3(T.x * x + B.x * y + N.x * z, T.y * x + B.y * y + N.y * z, T.z * x + B.z * y + N.z * z);
     }
-    f = bsdf_eval(m, N, wo, wi, ps, pdf);
+    f = bsdf_eval_v(m, vw, N, wo, wi, pdf);
     return pdf > 0.0f;
 }
 

@@ -132,7 +132,16 @@ __device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, i
     const int px = pix - py * fc.W;
     const float fx = (float)px + 0.5f + table_lerp(filt, kFilterN, rng(key, 0));
     const float fy = (float)py + 0.5f + table_lerp(filt, kFilterN, rng(key, 1));
-    if (cull) *culled = cull->outside(fx, fy);
+    if (cull) {
+        *culled = cull->outside(fx, fy);
+        if (*culled) {  // a miss: no direction needed (shade() of a miss reads only T and the world)
+            o = fc.cam_pos;
+            d = mk3(0.0f, 0.0f, 1.0f);
+            tmin = 0.0f;
+            tmax = -1.0f;
+            return;
+        }
+    }
     const float sx = (fx * fc.inv_w2 - 1.0f) * fc.half_w;
     const float sy = (1.0f - fy * fc.inv_h2) * fc.half_h;
     const float len = sqrtf(sx * sx + sy * sy + 1.0f);
@@ -185,6 +194,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         add_to(L, c);
     }
     if (bounce >= fc.max_bounces) return;
+    const BsdfView vw = bsdf_view(m, N, wo);
     const uint32_t dim0 = 2u + (uint32_t)(kDimsPerBounce * bounce);
     const float3 Po = offset_ray(P, N);
     // next-event estimation toward one uniformly chosen light
@@ -229,8 +239,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         const float cosN = dot3(N, wi);
         if (cosN > 0.0f) {
             float pdf;
-            const float ps = spec_prob(m, dot3(N, wo));
-            const float3 f = bsdf_eval(m, N, wo, wi, ps, pdf);
+            const float3 f = bsdf_eval_v(m, vw, N, wo, wi, pdf);
             const float k = cosN * (float)fc.n_lights;
             float3 c = mk3(T.x * f.x * k * Li.x, T.y * f.y * k * Li.y, T.z * f.z * k * Li.z);
             if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
@@ -246,7 +255,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     // continue the path
     float3 wi, f;
     float pdf;
-    if (!bsdf_sample(m, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f, pdf))
+    if (!bsdf_sample(m, vw, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f, pdf))
         return;
     const float cosL = dot3(N, wi);
     if (!(cosL > 0.0f)) return;
@@ -455,7 +464,15 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, Pa
             Hit h;
             traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cnt);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
+#if RR_EXP_PRIMARY == 1  // timing experiment only: no shading
+            L = mk3(h.t, (float)h.idx, 0.0f);
+#elif RR_EXP_PRIMARY == 2  // timing experiment only: no traversal
+            h.idx = (pix & 3) == 0 ? (pix >> 2) % 12 : -1;
+            h.t = 10.0f;
             shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
+#else
+            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
+#endif
             rad.put(p, L);
         }
         emit(so, p, out, sq, seg_base, cur);
@@ -883,9 +900,8 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameC
             const int sl = (int)fc.div_npix.div(p);
             const int pix = (int)p - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            bool culled;
+            bool culled;  // culled: tmax = -1 < tmin, every box test fails, the ray misses
             camera_ray(fc, sa.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
-            if (culled) tmax = -1.0f;  // empty interval: every box test fails, the ray misses
         },
         [&](int p, uint32_t, const Hit& h) { hits[p] = pack_hit(h); });
     if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
