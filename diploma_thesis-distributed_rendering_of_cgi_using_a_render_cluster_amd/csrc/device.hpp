@@ -147,6 +147,10 @@ struct DevPaths {
     KernelProfiler prof;
     bool count_traversal = false;
     int grid_blocks = 0;  // persistent grid for path kernels
+    // Set by the caller: the previous frame's output copies (film / rgba8 /
+    // JPEG coefficients, on the copy stream) must finish before this frame's
+    // first k_accumulate overwrites those buffers.
+    hipEvent_t outputs_free = nullptr;
     void ensure_paths(size_t n);
     void release();
 };

@@ -84,7 +84,8 @@ struct FrameRun {
 struct FrameSlot {
     bool busy = false;
     uint64_t ticket = 0;
-    hipEvent_t ev[4] = {};
+    hipEvent_t ev[4] = {};  // 0 start, 1 built, 2 rendered (stream), 3 outputs on the host (copy stream)
+    DevBuf<int32_t> counters;  // this frame's ray counters (swapped into DevPaths while enqueuing)
     KernelProfiler prof;
     PinnedBuf host_rgba, host_coeffs, host_counters, host_upload;
     FrameSetup fs;
@@ -102,6 +103,11 @@ struct FrameSlot {
 struct rr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // device-to-host copies of a frame's outputs run here, so the next frame's
+    // kernels on `stream` do not wait for them (DevPaths::outputs_free orders
+    // the reuse of the output buffers)
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t prev_copies_done = nullptr;  // the last enqueued frame's ev[3]
     DevPaths paths;
     // device JPEG transform (jpeg.hip): tables for the last quality, coefficients
     DevBuf<float> jpeg_tab;
@@ -291,6 +297,12 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
         ProfSwap(KernelProfiler& x, KernelProfiler& y) : a(x), b(y) { std::swap(a, b); }
         ~ProfSwap() { std::swap(a, b); }
     } prof_swap(c->paths.prof, sl.prof);
+    struct CtrSwap {  // per-slot counters: the copy stream may still read the previous frame's
+        DevBuf<int32_t>&a, &b;
+        CtrSwap(DevBuf<int32_t>& x, DevBuf<int32_t>& y) : a(x), b(y) { std::swap(a, b); }
+        ~CtrSwap() { std::swap(a, b); }
+    } ctr_swap(c->paths.counters, sl.counters);
+    c->paths.outputs_free = c->prev_copies_done;
     sl.count = (fs.flags & RR_FLAG_COUNT_TRAVERSAL) != 0;
     c->paths.count_traversal = sl.count;
     RR_HIP(hipEventRecord(sl.ev[0], st));
@@ -301,7 +313,6 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     r.chunks = (fs.spp + r.spp_chunk - 1) / r.spp_chunk;
     k.spp_chunk = r.spp_chunk;
     render_frame_device(s->dev, c->paths, k, r.chunks, st);
-    RR_HIP(hipEventRecord(sl.ev[2], st));
     const size_t npix = (size_t)fs.W * fs.H;
     if (sl.jpeg) {
         if (c->jpeg_tab_quality != sl.quality) {
@@ -319,21 +330,28 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
         c->jpeg_coeffs.ensure(nc);
         sl.host_coeffs.ensure(nc * sizeof(int16_t));
         jpeg_fdct_device(c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr, c->jpeg_coeffs.ptr, st);
+    }
+    RR_HIP(hipEventRecord(sl.ev[2], st));
+    hipStream_t cs = c->copy_stream;
+    RR_HIP(hipStreamWaitEvent(cs, sl.ev[2], 0));
+    if (sl.jpeg) {
+        const size_t nc = jpeg_coeff_count(fs.W, fs.H);
         RR_HIP(hipMemcpyAsync(sl.host_coeffs.ptr, c->jpeg_coeffs.ptr, nc * sizeof(int16_t), hipMemcpyDeviceToHost,
-                              st));
+                              cs));
     }
     if (sl.want_rgba) {
         sl.host_rgba.ensure(npix * 4);
-        RR_HIP(hipMemcpyAsync(sl.host_rgba.ptr, c->paths.rgba8.ptr, npix * 4, hipMemcpyDeviceToHost, st));
+        RR_HIP(hipMemcpyAsync(sl.host_rgba.ptr, c->paths.rgba8.ptr, npix * 4, hipMemcpyDeviceToHost, cs));
     }
     const int cpc = counters_per_chunk(fs.max_bounces);
     const size_t nctr = (size_t)cpc * r.chunks;
     sl.host_counters.ensure(nctr * sizeof(int32_t));
     RR_HIP(hipMemcpyAsync(sl.host_counters.ptr, c->paths.counters.ptr, nctr * sizeof(int32_t), hipMemcpyDeviceToHost,
-                          st));
+                          cs));
     if (sl.film_out)
-        RR_HIP(hipMemcpyAsync(sl.film_out, c->paths.film.ptr, npix * sizeof(float4), hipMemcpyDeviceToHost, st));
-    RR_HIP(hipEventRecord(sl.ev[3], st));
+        RR_HIP(hipMemcpyAsync(sl.film_out, c->paths.film.ptr, npix * sizeof(float4), hipMemcpyDeviceToHost, cs));
+    RR_HIP(hipEventRecord(sl.ev[3], cs));
+    c->prev_copies_done = sl.ev[3];
     if (sl.count) {  // measurement mode: read the traversal counters now
         RR_HIP(hipStreamSynchronize(st));
         RR_HIP(hipMemcpy(r.trav, c->paths.trav_counts.ptr, sizeof r.trav, hipMemcpyDeviceToHost));
@@ -468,6 +486,7 @@ int rr_create(int device_ordinal, rr_ctx** out) {
         c->device = device_ordinal;
         set_device(c.get());
         RR_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        RR_HIP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
         *out = c.release();
         return RR_OK;
     });
@@ -477,6 +496,7 @@ void rr_destroy(rr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     c->paths.release();
     for (auto& sl : c->slots) {
         for (auto& e : sl.ev)
@@ -484,6 +504,8 @@ void rr_destroy(rr_ctx* c) {
         sl.prof.release();
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    for (auto& sl : c->slots) sl.counters.release();
     delete c;
 }
 

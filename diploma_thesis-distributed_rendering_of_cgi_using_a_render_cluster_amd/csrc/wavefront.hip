@@ -1327,6 +1327,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         }
         const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
+        if (c == 0 && p.outputs_free) RR_HIP(hipStreamWaitEvent(st, p.outputs_free, 0));
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
@@ -1406,6 +1407,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         }
         const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
+        if (c == 0 && p.outputs_free) RR_HIP(hipStreamWaitEvent(st, p.outputs_free, 0));
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
