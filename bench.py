@@ -124,6 +124,17 @@ def algorithmic_bytes(cls: str, stats, scene_bytes: float, split: bool) -> tuple
         stream = (npaths * (8.0 + 16.0) + ext * (48.0 + 8.0 + 32.0) + (c0 + ce) * 48.0 + (s0 + se) * 48.0
                   + tri * (npaths + ext))
         return stream, stream
+    elif cls == "tiles":
+        # k_tiles (LDS-resident scenes): no per-path stream at all; HBM sees the
+        # film (16 B) and RGBA8 (4 B) write per pixel. SURVEY 8(d)'s figure
+        # prices every ray (48 B), node visit, triangle test, path segment
+        # (128 B) and sample (32 B) as if they went through memory.
+        npix = stats.width * stats.height
+        stream = npix * (16.0 + 4.0)
+        trav = sum(node * stats.trav_nodes[k] + tri * stats.trav_tris[k] for k in range(3))
+        rays_all = npaths + ext + sh
+        survey = stream + trav + 48.0 * rays_all + 128.0 * (npaths + ext) + 32.0 * npaths
+        return stream + scene_bytes, survey
     elif cls == "accumulate":
         npix = stats.width * stats.height
         return (npix * (stats.spp * 16.0 + 32.0 * max(stats.chunks - 1, 0) + 16.0 + 4.0),) * 2
@@ -135,7 +146,8 @@ def algorithmic_bytes(cls: str, stats, scene_bytes: float, split: bool) -> tuple
 # kernel names per class: fused (LDS scenes) and split (large scenes) paths
 KERNEL_OF_CLASS = {"build": [], "primary": ["k_primary", "k_trace_primary"],
                    "extend": ["k_extend", "k_trace_extend"], "shadow": ["k_shadow", "k_shadow_refill"],
-                   "shade": ["k_shade_extend", "k_shade_primary"], "accumulate": ["k_accumulate"]}
+                   "shade": ["k_shade_extend", "k_shade_primary"], "accumulate": ["k_accumulate"],
+                   "tiles": ["k_tiles"]}
 
 
 def pmc_traffic(cls: str, path: str):
@@ -169,13 +181,14 @@ def reduce_max_seconds(elapsed: float, dist=None, device="cpu") -> float:
 
 
 def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin frame 1"):
-    """Oracle (C restatement, OpenMP) on the host cores: evenly spread 4-row bands
-    of the same frame until the budget is spent, extrapolated to frames/s."""
+    """Oracle (C restatement, OpenMP) on the host cores: 4-row bands of the same
+    frame, taken in an order spread over the image, until the budget is spent or
+    the frame is done; extrapolated to frames/s."""
     H = int(state.render_ints[1])
     threads = min(os.cpu_count() or 1, 16)
-    bands = list(range(0, H, max(4, H // 64)))
+    bands = list(range(0, H, 4))
     done_rows, t_used = 0, 0.0
-    order = bands[::2] + bands[1::2]
+    order = [b for k in range(16) for b in bands[k::16]]
     for b in order:
         t0 = time.perf_counter()
         oracle_mod.render_state(state, rows=(b, min(b + 4, H)), threads=threads, film=False)
@@ -309,10 +322,10 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             try:
                 from oracle import oracle as O
-                # the oracle renders at most 16 spp per sample and is scaled to
+                # the oracle renders at most 128 spp per sample and is scaled to
                 # the frame's spp (path cost is linear in spp)
                 spp_full = int(last_stats.spp)
-                spp_cpu = min(spp_full, 16)
+                spp_cpu = min(spp_full, 128)
                 state = runner.ctx.frame_state(scene, f_count, rr.default_params(spp=spp_cpu))
                 cpu = cpu_baseline(O, state, args.cpu_seconds,
                                    f"{args.workload} frame {f_count} (each band call includes the oracle's BVH build)")

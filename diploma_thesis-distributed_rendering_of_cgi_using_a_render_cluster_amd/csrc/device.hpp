@@ -146,12 +146,10 @@ struct DevPaths {
     DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: 6 totals
     KernelProfiler prof;
     bool count_traversal = false;
+    bool force_wavefront = false;  // RR_FLAG_WAVEFRONT: LDS-resident scenes skip k_tiles
     int grid_blocks = 0;  // persistent grid for path kernels
-    // Set by the caller: the previous frame's output copies (film / rgba8 /
-    // JPEG coefficients, on the copy stream) must finish before this frame's
-    // first k_accumulate overwrites those buffers.
-    hipEvent_t outputs_free = nullptr;
     void ensure_paths(size_t n);
+    void ensure_tiles();  // k_tiles: only the traversal stack spill area
     void release();
 };
 

@@ -86,6 +86,12 @@ struct FrameSlot {
     uint64_t ticket = 0;
     hipEvent_t ev[4] = {};  // 0 start, 1 built, 2 rendered (stream), 3 outputs on the host (copy stream)
     DevBuf<int32_t> counters;  // this frame's ray counters (swapped into DevPaths while enqueuing)
+    // this frame's device outputs (swapped into DevPaths / rr_ctx while enqueuing):
+    // the copy stream reads them while the next frame's kernels write the other
+    // slot's, so no frame waits for its predecessor's device-to-host copies
+    DevBuf<float4> film;
+    DevBuf<uint8_t> rgba8;
+    DevBuf<int16_t> coeffs;
     KernelProfiler prof;
     PinnedBuf host_rgba, host_coeffs, host_counters, host_upload;
     FrameSetup fs;
@@ -104,10 +110,9 @@ struct rr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // device-to-host copies of a frame's outputs run here, so the next frame's
-    // kernels on `stream` do not wait for them (DevPaths::outputs_free orders
-    // the reuse of the output buffers)
+    // kernels on `stream` do not wait for them (the output buffers are per
+    // frame slot, FrameSlot::film / rgba8 / coeffs)
     hipStream_t copy_stream = nullptr;
-    hipEvent_t prev_copies_done = nullptr;  // the last enqueued frame's ev[3]
     DevPaths paths;
     // device JPEG transform (jpeg.hip): tables for the last quality, coefficients
     DevBuf<float> jpeg_tab;
@@ -302,9 +307,20 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
         CtrSwap(DevBuf<int32_t>& x, DevBuf<int32_t>& y) : a(x), b(y) { std::swap(a, b); }
         ~CtrSwap() { std::swap(a, b); }
     } ctr_swap(c->paths.counters, sl.counters);
-    c->paths.outputs_free = c->prev_copies_done;
+    struct OutSwap {  // per-slot output buffers (film, rgba8, JPEG coefficients)
+        rr_ctx* c;
+        FrameSlot& sl;
+        void swap() {
+            std::swap(c->paths.film, sl.film);
+            std::swap(c->paths.rgba8, sl.rgba8);
+            std::swap(c->jpeg_coeffs, sl.coeffs);
+        }
+        OutSwap(rr_ctx* c_, FrameSlot& s_) : c(c_), sl(s_) { swap(); }
+        ~OutSwap() { swap(); }
+    } out_swap(c, sl);
     sl.count = (fs.flags & RR_FLAG_COUNT_TRAVERSAL) != 0;
     c->paths.count_traversal = sl.count;
+    c->paths.force_wavefront = (fs.flags & RR_FLAG_WAVEFRONT) != 0;
     RR_HIP(hipEventRecord(sl.ev[0], st));
     r.rebuilt = prepare_frame(c, s, fs, sl.host_upload);
     RR_HIP(hipEventRecord(sl.ev[1], st));
@@ -351,7 +367,6 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     if (sl.film_out)
         RR_HIP(hipMemcpyAsync(sl.film_out, c->paths.film.ptr, npix * sizeof(float4), hipMemcpyDeviceToHost, cs));
     RR_HIP(hipEventRecord(sl.ev[3], cs));
-    c->prev_copies_done = sl.ev[3];
     if (sl.count) {  // measurement mode: read the traversal counters now
         RR_HIP(hipStreamSynchronize(st));
         RR_HIP(hipMemcpy(r.trav, c->paths.trav_counts.ptr, sizeof r.trav, hipMemcpyDeviceToHost));
@@ -505,7 +520,12 @@ void rr_destroy(rr_ctx* c) {
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-    for (auto& sl : c->slots) sl.counters.release();
+    for (auto& sl : c->slots) {
+        sl.counters.release();
+        sl.film.release();
+        sl.rgba8.release();
+        sl.coeffs.release();
+    }
     delete c;
 }
 

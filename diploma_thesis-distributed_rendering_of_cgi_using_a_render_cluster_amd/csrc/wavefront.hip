@@ -125,11 +125,9 @@ RR_D ScreenCull screen_cull(const FrameConsts& fc, NodeP nodes) {
 // culled (optional): set when the ray's subpixel position is outside the
 // scene's screen rectangle (the ray misses everything).
 template <typename FloatP>
-__device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, int pix,
-                                           uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
-                                           const ScreenCull* cull = nullptr, bool* culled = nullptr) {
-    const int py = (int)fc.div_w.div((uint32_t)pix);
-    const int px = pix - py * fc.W;
+__device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt, int px, int py,
+                                              uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
+                                              const ScreenCull* cull = nullptr, bool* culled = nullptr) {
     const float fx = (float)px + 0.5f + table_lerp(filt, kFilterN, rng(key, 0));
     const float fy = (float)py + 0.5f + table_lerp(filt, kFilterN, rng(key, 1));
     if (cull) {
@@ -153,6 +151,13 @@ __device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, i
     o = fc.cam_pos;
     tmin = fc.clip_start * len;
     tmax = fc.clip_end * len;
+}
+template <typename FloatP>
+__device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, int pix,
+                                           uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
+                                           const ScreenCull* cull = nullptr, bool* culled = nullptr) {
+    const int py = (int)fc.div_w.div((uint32_t)pix);
+    camera_ray_xy(fc, filt, pix - py * fc.W, py, key, o, d, tmin, tmax, cull, culled);
 }
 
 struct ShadeOut {
@@ -1026,6 +1031,18 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_shadow_refill(SceneA
 
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
 // sample order; then mean -> exposure -> view transform -> 8-bit.
+RR_D uchar4 tonemap(const FrameConsts& fc, float4 acc, const float* __restrict__ srgb) {
+    float c[3] = {acc.x * fc.inv_spp * fc.exposure_scale, acc.y * fc.inv_spp * fc.exposure_scale,
+                  acc.z * fc.inv_spp * fc.exposure_scale};
+    uint8_t q[3];
+    for (int k = 0; k < 3; ++k) {
+        float v = fminf(fmaxf(c[k], 0.0f), 1.0f);
+        if (fc.view_transform == 0) v = srgb_oetf(v, srgb, kSrgbN);
+        q[k] = quantize8(v);
+    }
+    return make_uchar4(q[0], q[1], q[2], 255);
+}
+
 __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
                                                        float4* __restrict__ film, int first_chunk,
                                                        int last_chunk, const float* __restrict__ srgb,
@@ -1039,18 +1056,193 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
             acc.z = acc.z + L.z;
         }
         film[pix] = acc;
-        if (last_chunk) {
-            float c[3] = {acc.x * fc.inv_spp * fc.exposure_scale, acc.y * fc.inv_spp * fc.exposure_scale,
-                          acc.z * fc.inv_spp * fc.exposure_scale};
-            uint8_t q[3];
-            for (int k = 0; k < 3; ++k) {
-                float v = fminf(fmaxf(c[k], 0.0f), 1.0f);
-                if (fc.view_transform == 0) v = srgb_oetf(v, srgb, kSrgbN);
-                q[k] = quantize8(v);
+        if (last_chunk) out[pix] = tonemap(fc, acc, srgb);
+    }
+}
+
+// K-tiles (LDS-resident scenes): one wave per 8x8 pixel tile
+// runs every sample of its 64 pixels to completion — raygen, closest hit,
+// shade, the NEE shadow ray traced inline, continuation — adds each path's
+// radiance to its pixel's film sum in registers in sample order, then writes
+// the film and the tonemapped pixel once. No radiance records, no queues, no
+// accumulate pass: the per-path HBM stream of the wavefront kernels (12 B
+// record written + read, 48 B per queued ray) disappears. A path's radiance
+// additions keep their order (emission(0), NEE(0), emission(1), ...) and the
+// film sum runs over samples 0..spp-1 like k_accumulate's, so the result is
+// bit-identical to the wavefront kernels and to the oracle.
+// Tiles come from an atomic counter (one atomic per wave per tile), those
+// overlapping the scene's screen rectangle first: they carry the traversal
+// and shading work, so the long tiles start early and the background tiles,
+// whose samples are all culled camera rays, fill the tail.
+constexpr int kTile = 8;  // 8x8 pixels = one wave
+
+struct TileOrder {
+    int tx, n;               // tiles per row, tiles in the frame
+    int bx0, by0, bw, bh;    // tile box over the screen rectangle (bw = bh = 0: none)
+    // i-th tile: first the box row-major, then the rest row-major (wave-uniform).
+    RR_D void at(int i, int& x, int& y) const {
+        const int nb = bw * bh;
+        if (i < nb) {
+            y = i / bw;
+            x = bx0 + (i - y * bw);
+            y += by0;
+            return;
+        }
+        int j = i - nb;
+        const int ntop = by0 * tx;
+        if (j < ntop) {
+            y = j / tx;
+            x = j - y * tx;
+            return;
+        }
+        j -= ntop;
+        const int rw = tx - bw, nmid = bh * rw;
+        if (j < nmid) {
+            const int r = j / rw, cx = j - r * rw;
+            y = by0 + r;
+            x = cx < bx0 ? cx : cx + bw;
+            return;
+        }
+        j -= nmid;
+        y = j / tx;
+        x = j - y * tx;
+        y += by0 + bh;
+    }
+};
+
+// Tile box of the pixels whose samples can fall inside the screen rectangle
+// (filter offsets are below 2 px). Scheduling only: every sample still takes
+// its own culling test, so the box never changes a result.
+RR_D TileOrder tile_order(const FrameConsts& fc, const ScreenCull& sc) {
+    TileOrder to;
+    to.tx = (fc.W + kTile - 1) / kTile;
+    const int ty = (fc.H + kTile - 1) / kTile;
+    to.n = to.tx * ty;
+    to.bx0 = to.by0 = 0;
+    to.bw = to.tx;
+    to.bh = ty;
+    if (!sc.on) return to;  // no rectangle: every tile may carry work
+    const float m = 2.5f;
+    const float x0 = fmaxf(sc.r[0] - m, 0.0f), x1 = fminf(sc.r[1] + m, (float)fc.W - 1.0f);
+    const float y0 = fmaxf(sc.r[2] - m, 0.0f), y1 = fminf(sc.r[3] + m, (float)fc.H - 1.0f);
+    if (!(x0 <= x1 && y0 <= y1)) {
+        to.bw = to.bh = 0;
+        return to;
+    }
+    to.bx0 = (int)x0 / kTile;
+    to.by0 = (int)y0 / kTile;
+    to.bw = (int)x1 / kTile - to.bx0 + 1;
+    to.bh = (int)y1 / kTile - to.by0 + 1;
+    return to;
+}
+
+// Per-lane ray counts of the tile kernel, reduced once per wave at exit into
+// the chunk-0 counter pairs: {0, 1} = bounce 0, {2, 3} = all later bounces
+// (rr_api.cpp fill_stats sums the pairs).
+RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint32_t c1, uint32_t s1) {
+    uint32_t v[4] = {c0, s0, c1, s1};
+    for (int k = 0; k < 4; ++k) {
+        uint32_t a = v[k];
+        for (int off = 32; off > 0; off >>= 1) a += (uint32_t)__shfl_xor((int)a, off);
+        if ((threadIdx.x & 63) == 0 && a) atomicAdd(&tot[k], a);
+    }
+}
+
+template <bool kCount, typename View>
+RR_D void tiles_body(const FrameConsts& fc, const View& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
+                     const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
+                     int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
+    const int gtid = blockIdx.x * kBlock + threadIdx.x;
+    const int stride = gridDim.x * kBlock;
+    TravStack st{stack, spill + gtid, stride, 0};
+    TravCount cp, ce, cs;
+    uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0;
+    const ScreenCull cull = screen_cull(fc, v.nodes);
+    const TileOrder to = tile_order(fc, cull);
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        int t = 0;
+        if (lane == 0) t = (int)atomicAdd(tile_ctr, 1u);
+        t = __builtin_amdgcn_readlane(t, 0);
+        if (t >= to.n) break;
+        int tx, ty;
+        to.at(t, tx, ty);
+        const int px = tx * kTile + (lane & (kTile - 1)), py = ty * kTile + (lane >> 3);
+        const bool valid = px < fc.W && py < fc.H;
+        const int pix = py * fc.W + px;
+        float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int s = 0; s < fc.spp_total; ++s) {
+            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)s);
+            float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = mk3(1.0f, 1.0f, 1.0f), L = o;
+            float tmin = 0.0f, tmax = -1.0f;
+            bool culled = true;
+            if (valid) camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
+            bool live = valid;
+            for (int b = 0; b <= fc.max_bounces; ++b) {
+                if (!__any(live)) break;
+                if (live) {
+                    ShadeOut so;
+                    Hit h;
+                    if (b == 0)
+                        traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cp);
+                    else
+                        traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, ce);
+                    shade(fc, b, v, o, d, T, h, key, L, so);
+                    if (so.shadow) {
+                        Hit hs;
+                        if (!traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs, cs))
+                            add_to(L, so.sc);
+                    }
+                    if (b == 0) {
+                        n_c0 += so.cont ? 1u : 0u;
+                        n_s0 += so.shadow ? 1u : 0u;
+                    } else {
+                        n_c1 += so.cont ? 1u : 0u;
+                        n_s1 += so.shadow ? 1u : 0u;
+                    }
+                    if (so.cont) {
+                        o = so.o;
+                        d = so.d;
+                        T = so.T;
+                    } else {
+                        live = false;
+                    }
+                }
             }
-            out[pix] = make_uchar4(q[0], q[1], q[2], 255);
+            acc.x = acc.x + L.x;
+            acc.y = acc.y + L.y;
+            acc.z = acc.z + L.z;
+        }
+        if (valid) {
+            film[pix] = acc;
+            out[pix] = tonemap(fc, acc, srgb);
         }
     }
+    flush_rays(tot, n_c0, n_s0, n_c1, n_s1);
+    if (kCount) {
+        flush_counts(tc, 0, cp.nodes, cp.tris);
+        flush_counts(tc, 2, ce.nodes, ce.tris);
+        flush_counts(tc, 4, cs.nodes, cs.tris);
+    }
+}
+
+#ifndef RR_TILES_WAVES
+#define RR_TILES_WAVES 4  // waves per SIMD the register budget must admit (<= 128 VGPRs)
+#endif
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc, SceneArgs sa,
+                                                                  uint32_t* __restrict__ tile_ctr,
+                                                                  float4* __restrict__ film,
+                                                                  const float* __restrict__ srgb,
+                                                                  uchar4* __restrict__ out, uint32_t* __restrict__ tot,
+                                                                  int32_t* __restrict__ spill,
+                                                                  unsigned long long* __restrict__ tc) {
+    __shared__ int lds_stack[kLdsStack * kBlock];
+    extern __shared__ float4 dyn4[];
+    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    int used;
+    const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used);
+    tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack);
 }
 
 __global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
@@ -1128,6 +1320,14 @@ using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, Pa
 using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, Rad, int32_t*, unsigned long long*);
 using TailFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, uint32_t*, int32_t*,
                         unsigned long long*);
+using TilesFn = void (*)(FrameConsts, SceneArgs, uint32_t*, float4*, const float*, uchar4*, uint32_t*, int32_t*,
+                         unsigned long long*);
+// LDS-resident scenes render through k_tiles (default) or, with RR_TUNE_TILES=0,
+// through the wavefront kernels (A/B and parity of both paths).
+bool tiles_enabled() {
+    static const bool on = !(getenv("RR_TUNE_TILES") && atoi(getenv("RR_TUNE_TILES")) == 0);
+    return on;
+}
 // Persistent grid = resident blocks: CUs x blocks per CU the kernel's register
 // and LDS budget admits (a grid-stride loop over more blocks than fit would
 // only queue the surplus behind the first wave of blocks).
@@ -1180,6 +1380,8 @@ struct Grids {
     ExtendFn ke;
     ShadowFn ks;
     TailFn kt;
+    TilesFn kx;
+    int tiles;
     Grids(const FrameConsts& fc, bool count) {
         lds = scene_in_lds(fc.n_tris, fc.n_mats, fc.n_lights);
         kp = lds ? (count ? k_primary<true, true> : k_primary<false, true>)
@@ -1202,6 +1404,8 @@ struct Grids {
         extend = grid_for(ke, dyn_extend);
         shadow = grid_for(ks, dyn_shadow);
         tail = grid_for(kt, dyn_extend);
+        kx = count ? k_tiles<true> : k_tiles<false>;
+        tiles = lds ? grid_for(kx, dyn_primary) : 0;
     }
 };
 // Launch geometry of the split (trace / shade) path of large scenes.
@@ -1256,6 +1460,11 @@ void DevPaths::ensure_paths(size_t n) {
         hits.ensure(n);
         cap = n;
     }
+    spill.ensure((size_t)kSpillStack * grid_blocks * kBlock);
+}
+
+void DevPaths::ensure_tiles() {
+    if (grid_blocks == 0) grid_blocks = device_cu_count() * kMaxBlocksPerCu;
     spill.ensure((size_t)kSpillStack * grid_blocks * kBlock);
 }
 
@@ -1327,7 +1536,6 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         }
         const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
-        if (c == 0 && p.outputs_free) RR_HIP(hipStreamWaitEvent(st, p.outputs_free, 0));
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
@@ -1338,6 +1546,35 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
 void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_t st) {
     const int npix = base.npix;
     const size_t npaths = (size_t)npix * base.spp_chunk;
+    const Grids G(base, p.count_traversal);
+    if (G.lds && base.n_tris > 0 && tiles_enabled() && !p.force_wavefront) {  // one launch: all samples of every tile
+        p.ensure_tiles();
+        p.film.ensure((size_t)npix);
+        p.rgba8.ensure((size_t)npix * 4);
+        const int cpc = counters_per_chunk(base.max_bounces);
+        p.counters.ensure((size_t)cpc * n_chunks);
+        RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
+        unsigned long long* tc = nullptr;
+        if (p.count_traversal) {
+            p.trav_counts.ensure(6);
+            RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 6 * sizeof(unsigned long long), st));
+            tc = p.trav_counts.ptr;
+        }
+        const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
+                           std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
+        FrameConsts fc = base;
+        fc.first_sample = 0;
+        fc.spp_chunk = base.spp_total;
+        uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr);
+        const long tiles = (long)((base.W + 7) / 8) * ((base.H + 7) / 8);
+        const int g = clamp_grid(tiles * 64, G.tiles);
+        p.prof.begin(st, RR_K_TILES);
+        G.kx<<<g, kBlock, G.dyn_primary, st>>>(fc, sa, tot + 2 * (base.max_bounces + 1), p.film.ptr, p.srgb_lut.ptr,
+                                               reinterpret_cast<uchar4*>(p.rgba8.ptr), tot, p.spill.ptr, tc);
+        p.prof.end(st);
+        RR_HIP(hipGetLastError());
+        return;
+    }
     p.ensure_paths(npaths);
     p.film.ensure((size_t)npix);
     p.rgba8.ensure((size_t)npix * 4);
@@ -1353,7 +1590,6 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     KernelProfiler& pr = p.prof;
-    const Grids G(base, tc != nullptr);
     const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
                        std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
     if (!G.lds && base.n_tris > 0) {
@@ -1407,7 +1643,6 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         }
         const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
-        if (c == 0 && p.outputs_free) RR_HIP(hipStreamWaitEvent(st, p.outputs_free, 0));
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);

@@ -64,8 +64,8 @@ class FrameStats(ctypes.Structure):
         return out
 
 
-RR_FLAG_PROFILE_KERNELS, RR_FLAG_COUNT_TRAVERSAL = 1, 2
-KERNEL_CLASSES = ["build", "primary", "extend", "shadow", "accumulate", "shade"]
+RR_FLAG_PROFILE_KERNELS, RR_FLAG_COUNT_TRAVERSAL, RR_FLAG_WAVEFRONT = 1, 2, 4
+KERNEL_CLASSES = ["build", "primary", "extend", "shadow", "accumulate", "shade", "tiles"]
 
 
 # Every symbol include/rr.h declares (checked by tests/test_abi.py).

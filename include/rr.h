@@ -72,6 +72,7 @@ typedef struct rr_render_params {
 /* Measurement flags (rr_render_params.flags). */
 #define RR_FLAG_PROFILE_KERNELS 1  /* HIP events around every launch -> stats.kernel_ms[] */
 #define RR_FLAG_COUNT_TRAVERSAL 2  /* count BVH nodes visited / triangles tested -> stats */
+#define RR_FLAG_WAVEFRONT 4        /* LDS-resident scenes: wavefront kernels instead of k_tiles (A/B, parity) */
 
 /* Kernel classes of rr_frame_stats.kernel_ms / kernel_launches. */
 #define RR_K_BUILD 0     /* world transform + Morton + radix sort + Karras + refit */
@@ -80,6 +81,7 @@ typedef struct rr_render_params {
 #define RR_K_SHADOW 3    /* any-hit traversal of shadow rays */
 #define RR_K_ACCUM 4     /* film accumulate + tonemap */
 #define RR_K_SHADE 5     /* split path (large scenes): shading kernels; PRIMARY/EXTEND then time traversal only */
+#define RR_K_TILES 6     /* LDS-resident scenes: k_tiles, every sample of an 8x8 pixel tile run to completion + film + tonemap */
 #define RR_K_CLASSES 8
 
 /* The five timestamps the reference recovers from Blender's stdout

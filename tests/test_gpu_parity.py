@@ -133,10 +133,16 @@ def test_trace_edge_cases(ctx, s04):
     assert len(p0) == 0
 
 
+# "tiles": k_tiles (default for LDS-resident scenes); "wavefront": the queue
+# kernels (RR_FLAG_WAVEFRONT), the path large scenes take.
+PATHS = {"tiles": 0, "wavefront": 4}
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("frame,w,h,spp,chunk", [(1, 160, 90, 16, 0), (30, 96, 54, 8, 3), (60, 64, 36, 5, 1),
-                                                 (600, 33, 17, 7, 2)])
-def test_full_frame_bit_exact(ctx, rr, s04, frame, w, h, spp, chunk):
-    p = rr.default_params(width=w, height=h, spp=spp, spp_per_chunk=chunk)
+                                                 (600, 33, 17, 7, 2), (30, 1, 1, 9, 0), (45, 7, 130, 3, 0)])
+def test_full_frame_bit_exact(ctx, rr, s04, frame, w, h, spp, chunk, path):
+    p = rr.default_params(width=w, height=h, spp=spp, spp_per_chunk=chunk, flags=PATHS[path])
     film, rgba, stats = ctx.render_to_memory(s04, frame, p)
     st = ctx.frame_state(s04, frame, p)
     of, orgba = O.render_state(st)
@@ -146,6 +152,22 @@ def test_full_frame_bit_exact(ctx, rr, s04, frame, w, h, spp, chunk):
     assert nbad == 0, f"{nbad} 8-bit mismatches"
     assert np.array_equal(film, of), f"max film diff {np.max(np.abs(film - of))}"
     assert film[..., :3].mean() > 0.01
+
+
+def test_tiles_equal_wavefront_full_resolution(ctx, rr, s04):
+    """BASELINE size (1920x1080) at low spp: k_tiles and the wavefront kernels give
+    the same film bits, pixels and ray counts (the oracle is too slow here)."""
+    out = {}
+    for path, flags in PATHS.items():
+        p = rr.default_params(spp=4, flags=flags)
+        film, rgba, st = ctx.render_to_memory(s04, 30, p)
+        out[path] = (film, rgba, st.extension_rays, st.shadow_rays, st.primary_continued, st.primary_shadow)
+    a, b = out["tiles"], out["wavefront"]
+    assert a[0].shape == (1080, 1920, 4)
+    assert np.array_equal(a[0], b[0]), f"{np.count_nonzero(a[0] != b[0])} film mismatches"
+    assert np.array_equal(a[1], b[1])
+    assert a[2:] == b[2:], (a[2:], b[2:])
+    assert a[2] > 0 and a[3] > 0
 
 
 def test_chunking_and_determinism(ctx, rr, s04):
