@@ -166,6 +166,9 @@ struct FrameConsts {
     int view_transform;
     float3 world;
     int n_tris, n_mats;
+    // bound on |subpixel offset| of a camera sample (filter support + 1 px of
+    // rounding slack): k_tiles' whole-tile culling test
+    float filter_reach;
 };
 
 // LBVH build for the current obj_xform (uploaded by the caller).

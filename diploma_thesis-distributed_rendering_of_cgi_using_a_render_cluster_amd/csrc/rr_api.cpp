@@ -265,6 +265,8 @@ FrameConsts make_consts(const FrameSetup& fs, int n_tris) {
     k.view_transform = fs.view_transform;
     k.world = make_float3(fs.world[0], fs.world[1], fs.world[2]);
     k.n_tris = n_tris;
+    // build_filter_table: offsets within the support [-width, width]
+    k.filter_reach = std::fabs(fs.filter_width) + 1.0f;
     return k;
 }
 

@@ -133,9 +133,12 @@ RR_HD uint32_t hash_u32(uint32_t x) {
     x ^= x >> 16;
     return x;
 }
+// path_key = sample_key(pixel_key(seed, pixel), sample); the split lets a
+// per-pixel sample loop hash the pixel once.
+RR_HD uint32_t pixel_key(uint32_t seed, uint32_t pixel) { return hash_u32(hash_u32(seed) + pixel); }
+RR_HD uint32_t sample_key(uint32_t pk, uint32_t sample) { return hash_u32(pk ^ (sample * 0x9E3779B9u + 0x7F4A7C15u)); }
 RR_HD uint32_t path_key(uint32_t seed, uint32_t pixel, uint32_t sample) {
-    const uint32_t k = hash_u32(hash_u32(seed) + pixel);
-    return hash_u32(k ^ (sample * 0x9E3779B9u + 0x7F4A7C15u));
+    return sample_key(pixel_key(seed, pixel), sample);
 }
 RR_HD float rng(uint32_t key, uint32_t dim) {
     return (float)(hash_u32(key + (dim + 1u) * 0x9E3779B9u) >> 8) * 5.9604644775390625e-08f;
@@ -151,24 +154,20 @@ RR_HD void sincos_small(float x, float& s, float& c) {
 }
 
 // Shirley-Chiu concentric square->disk map; angles stay in [-pi/4, pi/4].
+// Written with selects instead of branches: each lane runs the operations of
+// its own case (|a| > |b|: angle (pi/4) b/a, x = a cos, y = a sin; else angle
+// (pi/4) a/b, x = b sin, y = b cos; a = b = 0: the origin), but a wave whose
+// lanes fall in both cases pays for one division and one sincos, not two.
 RR_HD void concentric_disk(float u1, float u2, float& x, float& y) {
     const float a = 2.0f * u1 - 1.0f;
     const float b = 2.0f * u2 - 1.0f;
-    if (a == 0.0f && b == 0.0f) {
-        x = 0.0f;
-        y = 0.0f;
-        return;
-    }
+    const bool wide = fabsf(a) > fabsf(b);
+    const float num = wide ? b : a, r = wide ? a : b;
     float s, c;
-    if (fabsf(a) > fabsf(b)) {
-        sincos_small(0.785398163397448f * (b / a), s, c);
-        x = a * c;
-        y = a * s;
-    } else {
-        sincos_small(0.785398163397448f * (a / b), s, c);
-        x = b * s;
-        y = b * c;
-    }
+    sincos_small(0.785398163397448f * (num / r), s, c);
+    const bool origin = a == 0.0f && b == 0.0f;
+    x = origin ? 0.0f : r * (wide ? c : s);
+    y = origin ? 0.0f : r * (wide ? s : c);
 }
 
 // Orthonormal basis (Duff et al. 2017, branchless).
@@ -624,12 +623,15 @@ struct TravState4 {
 template <bool kAnyHit, bool kCount = false, typename NodeP, typename TriP, typename Stack>
 RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float tmin, float tmax, Stack& st, Hit& h,
                    TravCount& cnt) {
-    TravState<kAnyHit, kCount> ts;
-    ts.start(o, d, tmin, tmax);
-    if (n_tris <= 0) {
-        h = ts.h;
+    if (n_tris <= 0) {  // the miss TravState::start would leave, without its three divisions
+        h.t = tmax;
+        h.u = h.v = 0.0f;
+        h.idx = -1;
+        h.orig = -1;
         return false;
     }
+    TravState<kAnyHit, kCount> ts;
+    ts.start(o, d, tmin, tmax);
     st.sp = 0;
     while (!ts.step(nodes, tris, st, cnt)) {
     }
@@ -740,7 +742,9 @@ RR_HD float3 bsdf_eval(const Mat& m, float3 N, float3 wo, float3 wi, float ps, f
 }
 
 // GGX visible-normal sample (Heitz 2018) in the local frame (N = +z).
-RR_HD float3 sample_vndf(float3 v, float alpha, float u1, float u2) {
+// (dx, dy): concentric_disk(u1, u2), drawn by the caller (bsdf_sample shares
+// it between the lobes).
+RR_HD float3 sample_vndf(float3 v, float alpha, float dx, float dy) {
     const float3 vh = norm3(mk3(alpha * v.x, alpha * v.y, v.z));
     const float lensq = vh.x * vh.x + vh.y * vh.y;
     float3 t1;
@@ -751,8 +755,6 @@ RR_HD float3 sample_vndf(float3 v, float alpha, float u1, float u2) {
         t1 = mk3(1.0f, 0.0f, 0.0f);
     }
     const float3 t2 = cross3(vh, t1);
-    float dx, dy;
-    concentric_disk(u1, u2, dx, dy);
     const float s = 0.5f * (1.0f + vh.z);
     dy = (1.0f - s) * sqrtf(fmaxf(0.0f, 1.0f - dx * dx)) + s * dy;
     const float nz = sqrtf(fmaxf(0.0f, 1.0f - dx * dx - dy * dy));
@@ -769,18 +771,18 @@ RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, fl
     const float ps = vw.ps;
     float3 T, B;
     make_onb(N, T, B);
+    float x, y;  // the disk sample both lobes start from
+    concentric_disk(u1, u2, x, y);
     if (ul < ps) {
         float alpha = m.roughness * m.roughness;
         if (alpha < 1.0e-4f) alpha = 1.0e-4f;
         const float3 wl = mk3(dot3(wo, T), dot3(wo, B), cosV);
-        const float3 hl = sample_vndf(wl, alpha, u1, u2);
+        const float3 hl = sample_vndf(wl, alpha, x, y);
         const float3 H = mk3(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,
                              T.z * hl.x + B.z * hl.y + N.z * hl.z);
         const float k = 2.0f * dot3(wo, H);
         wi = mk3(H.x * k - wo.x, H.y * k - wo.y, H.z * k - wo.z);
     } else {
-        float x, y;
-        concentric_disk(u1, u2, x, y);
         const float z = sqrtf(fmaxf(0.0f, 1.0f - x * x - y * y));
         wi = mk3(T.x * x + B.x * y + N.x * z, T.y * x + B.y * y + N.y * z, T.z * x + B.z * y + N.z * z);
     }

@@ -1075,6 +1075,9 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
 // and shading work, so the long tiles start early and the background tiles,
 // whose samples are all culled camera rays, fill the tail.
 constexpr int kTile = 8;  // 8x8 pixels = one wave
+#ifndef RR_EXP_TILES
+#define RR_EXP_TILES 0  // timing experiments (wrong images): 1 no shading, 2 no shadow rays, 3 no extension rays
+#endif
 
 struct TileOrder {
     int tx, n;               // tiles per row, tiles in the frame
@@ -1122,7 +1125,7 @@ RR_D TileOrder tile_order(const FrameConsts& fc, const ScreenCull& sc) {
     to.bw = to.tx;
     to.bh = ty;
     if (!sc.on) return to;  // no rectangle: every tile may carry work
-    const float m = 2.5f;
+    const float m = fc.filter_reach + 1.0f;
     const float x0 = fmaxf(sc.r[0] - m, 0.0f), x1 = fminf(sc.r[1] + m, (float)fc.W - 1.0f);
     const float y0 = fmaxf(sc.r[2] - m, 0.0f), y1 = fminf(sc.r[3] + m, (float)fc.H - 1.0f);
     if (!(x0 <= x1 && y0 <= y1)) {
@@ -1134,6 +1137,19 @@ RR_D TileOrder tile_order(const FrameConsts& fc, const ScreenCull& sc) {
     to.bw = (int)x1 / kTile - to.bx0 + 1;
     to.bh = (int)y1 / kTile - to.by0 + 1;
     return to;
+}
+
+// Whether no sample of tile (tx, ty) can land inside the screen rectangle:
+// every subpixel position is px + 0.5 + offset with |offset| < filter_reach
+// (which includes a pixel of rounding slack), so each sample's own test in
+// camera_ray_xy would cull it. Then every sample's radiance is exactly the
+// world term (T = 1 at bounce 0, no clamp).
+RR_D bool tile_culled(const FrameConsts& fc, const ScreenCull& sc, int tx, int ty) {
+    if (!sc.on) return false;
+    const float x0 = (float)(tx * kTile) + 0.5f, y0 = (float)(ty * kTile) + 0.5f;
+    const float x1 = x0 + (float)(kTile - 1), y1 = y0 + (float)(kTile - 1);
+    const float r = fc.filter_reach;
+    return x1 + r < sc.r[0] || x0 - r > sc.r[1] || y1 + r < sc.r[2] || y0 - r > sc.r[3];
 }
 
 // Per-lane ray counts of the tile kernel, reduced once per wave at exit into
@@ -1171,8 +1187,21 @@ RR_D void tiles_body(const FrameConsts& fc, const View& v, uint32_t* __restrict_
         const bool valid = px < fc.W && py < fc.H;
         const int pix = py * fc.W + px;
         float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (tile_culled(fc, cull, tx, ty)) {  // background tile: film = the world term summed spp times
+            for (int s = 0; s < fc.spp_total; ++s) {
+                acc.x = acc.x + fc.world.x;
+                acc.y = acc.y + fc.world.y;
+                acc.z = acc.z + fc.world.z;
+            }
+            if (valid) {
+                film[pix] = acc;
+                out[pix] = tonemap(fc, acc, srgb);
+            }
+            continue;
+        }
+        const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
         for (int s = 0; s < fc.spp_total; ++s) {
-            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)s);
+            const uint32_t key = sample_key(pk, (uint32_t)s);
             float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = mk3(1.0f, 1.0f, 1.0f), L = o;
             float tmin = 0.0f, tmax = -1.0f;
             bool culled = true;
@@ -1186,11 +1215,18 @@ RR_D void tiles_body(const FrameConsts& fc, const View& v, uint32_t* __restrict_
                     if (b == 0)
                         traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cp);
                     else
-                        traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, ce);
+                        traverse<false, kCount>(v.nodes, v.tris, RR_EXP_TILES == 3 ? 0 : fc.n_tris, o, d, 0.0f,
+                                                kFltMax, st, h, ce);
+#if RR_EXP_TILES == 1  // timing experiment only: camera rays, no shading
+                    so.cont = so.shadow = false;
+                    L = mk3(h.t, (float)h.idx, 0.0f);
+#else
                     shade(fc, b, v, o, d, T, h, key, L, so);
+#endif
                     if (so.shadow) {
                         Hit hs;
-                        if (!traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs, cs))
+                        if (!traverse<true, kCount>(v.nodes, v.tris, RR_EXP_TILES == 2 ? 0 : fc.n_tris, so.so, so.sd,
+                                                    0.0f, so.sdist, st, hs, cs))
                             add_to(L, so.sc);
                     }
                     if (b == 0) {

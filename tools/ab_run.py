@@ -29,7 +29,7 @@ with rr.RenderContext(0) as ctx:
             tot = sum(ms.values())
             if best is None or tot < best[0]:
                 best = (tot, ms)
-        out[path.split("/")[-1].split(".")[0] + ":" + spp] = {"total": round(best[0], 2), **best[1]}
+        out[path.split("/")[-1].split(".")[0][:6] + ":" + frame + ":" + spp] = {"total": round(best[0], 2), **best[1]}
         s.close()
 print(json.dumps(out))
 '''
