@@ -81,6 +81,7 @@ struct SceneView {
     NodeP nodes;
     TriP tris;
     FloatP mats, lights, filter;
+    lds_f4w* cam = nullptr;  // LDS scenes, camera kernels: 3 float4 per triangle (stage_camera)
 };
 using GlobalView = SceneView<const BvhNode*, const TriPack*, const float*>;
 using LdsView = SceneView<lds_node*, lds_tri*, lds_float*>;
@@ -414,7 +415,62 @@ RR_D void lds_copy(lds_f4w* dst, const float4* __restrict__ src, int n4) {
 // Stages the scene at the start of dynamic LDS (all threads call; ends with a
 // barrier). `shading`: also materials, lights and the filter table. Returns the
 // view; `used` receives the float4 slots taken (LDS layout: scene_lds_f4()).
-RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& used) {
+// Camera-ray data of one triangle (sorted index i), staged next to the scene
+// by the kernels that trace camera rays of LDS-resident scenes: every camera
+// ray starts at the camera, so tri_test's origin-only terms tv = o - v0,
+// qv = tv x e1 and tn = e2 . qv are computed once per block (the same float
+// operations, so camera_hit's t / u / v are bit-identical to tri_test's), and
+// the triangle's screen rectangle (tri_screen_rect) bins it to the 8x8 tiles
+// whose samples can hit it.
+//   [3i] = (tv, tn), [3i+1] = (qv, 0), [3i+2] = (x0, x1, y0, y1)
+RR_D void tri_screen_rect(const FrameConsts& fc, const float3 p[3], float r[4]) {
+    float x0 = kFltMax, x1 = -kFltMax, y0 = kFltMax, y1 = -kFltMax;
+    for (int k = 0; k < 3; ++k) {
+        const float3 v = sub3(p[k], fc.cam_pos);
+        const float depth = -dot3(v, fc.cam_back);
+        if (!(depth > 1.0e-4f)) {  // at or behind the camera plane: no bound, every tile keeps it
+            r[0] = r[2] = -kFltMax;
+            r[1] = r[3] = kFltMax;
+            return;
+        }
+        const float sx = dot3(v, fc.cam_right) / depth;
+        const float sy = dot3(v, fc.cam_up) / depth;
+        const float fx = (sx / fc.half_w + 1.0f) * ((float)fc.W * 0.5f);
+        const float fy = (1.0f - sy / fc.half_h) * ((float)fc.H * 0.5f);
+        x0 = fminf(x0, fx);
+        x1 = fmaxf(x1, fx);
+        y0 = fminf(y0, fy);
+        y1 = fmaxf(y1, fy);
+    }
+    r[0] = x0 - 1.0f;  // a pixel of slack covers rounding, as screen_rect's
+    r[1] = x1 + 1.0f;
+    r[2] = y0 - 1.0f;
+    r[3] = y1 + 1.0f;
+}
+
+RR_D void stage_camera(lds_f4w* q, lds_tri* tris, int n_tris, const FrameConsts& fc) {
+    for (int i = threadIdx.x; i < n_tris; i += kBlock) {
+        const TriPack tp = load_tri(tris, i);
+        const float3 v0 = xyz(tp.p0), e1 = xyz(tp.p1), e2 = xyz(tp.p2);
+        const float3 tv = sub3(fc.cam_pos, v0);
+        const float3 qv = cross3(tv, e1);
+        const float tn = dot3(e2, qv);
+        const float3 pts[3] = {v0, add3(v0, e1), add3(v0, e2)};
+        float r[4];
+        tri_screen_rect(fc, pts, r);
+        rr_f4v a, b, c;
+        a.x = tv.x; a.y = tv.y; a.z = tv.z; a.w = tn;
+        b.x = qv.x; b.y = qv.y; b.z = qv.z; b.w = 0.0f;
+        c.x = r[0]; c.y = r[1]; c.z = r[2]; c.w = r[3];
+        q[3 * i] = a;
+        q[3 * i + 1] = b;
+        q[3 * i + 2] = c;
+    }
+}
+
+// cam_fc: also stage the camera-ray data (stage_camera) after the scene.
+RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& used,
+                         const FrameConsts* cam_fc = nullptr) {
     lds_f4w* q = base;
     LdsView v;
     v.nodes = (lds_node*)q;
@@ -435,9 +491,80 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
         lds_copy(q, reinterpret_cast<const float4*>(a.filter), kFilterN / 4);
         q += kFilterN / 4;
     }
+    if (cam_fc) {
+        __syncthreads();  // the triangles are staged
+        v.cam = q;
+        stage_camera(q, v.tris, a.n_tris, *cam_fc);
+        q += 3 * a.n_tris;
+    }
     used = (int)(q - base);
     __syncthreads();
     return v;
+}
+
+// Closest hit of a camera ray (origin fc.cam_pos) over the triangles whose bits
+// are set in the wave-uniform mask {m0, m1} (sorted indices 0..127): tri_test
+// with the staged origin terms, closest_tri_nb's branch-free accept rule. The
+// rule is order-independent (smaller t, then smaller original id), so the
+// result equals testing every triangle whenever the mask holds every triangle
+// the ray can hit (tile_mask). LDS-resident scenes trace camera rays this way
+// instead of walking the LBVH; oracle/rr_oracle.c brute-forces them the same.
+template <bool kCount>
+RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float tmin, float tmax, Hit& h,
+                     TravCount& cnt) {
+    h.t = tmax;
+    h.u = h.v = 0.0f;
+    h.idx = -1;
+    h.orig = -1;
+    for (int w = 0; w < 2; ++w) {
+        uint64_t m = w ? m1 : m0;
+        while (m) {
+            const int i = (int)__builtin_ctzll(m) + 64 * w;
+            m &= m - 1;
+            if (kCount) ++cnt.tris;
+            const TriPack tp = load_tri(v.tris, i);
+            const float4 ca = lds_ld4(v.cam + 3 * i), cb = lds_ld4(v.cam + 3 * i + 1);
+            const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2), tv = xyz(ca), qv = xyz(cb);
+            const float3 pv = cross3(d, e2);
+            const float det = dot3(e1, pv);
+            const float inv = 1.0f / det;
+            const float u = dot3(tv, pv) * inv;
+            const float vv = dot3(d, qv) * inv;
+            const float t = ca.w * inv;
+            const int orig = f2i(tp.p0.w);
+            const bool ok = !(det == 0.0f) && !(u < 0.0f || u > 1.0f) && !(vv < 0.0f || u + vv > 1.0f) &&
+                            t > tmin && (t < h.t || (t == h.t && orig < h.orig));
+            if (ok) {
+                h.t = t;
+                h.u = u;
+                h.v = vv;
+                h.idx = i;
+                h.orig = orig;
+            }
+        }
+    }
+}
+
+// Triangles whose screen rectangle meets the sample positions of pixels
+// [x0, x1] x [y0, y1] (centres + filter offsets below fc.filter_reach), as a
+// wave-uniform 128-bit mask; n_tris <= 128 (every LDS-resident scene).
+RR_D void tile_mask(const FrameConsts& fc, const LdsView& v, int n_tris, float x0, float x1, float y0, float y1,
+                    uint64_t& m0, uint64_t& m1) {
+    const float r = fc.filter_reach;
+    const float X0 = x0 + 0.5f - r, X1 = x1 + 0.5f + r, Y0 = y0 + 0.5f - r, Y1 = y1 + 0.5f + r;
+    uint64_t a = 0, b = 0;
+    for (int i = 0; i < n_tris; ++i) {
+        const float4 q = lds_ld4(v.cam + 3 * i + 2);
+        const bool in = !(q.y < X0 || q.x > X1 || q.w < Y0 || q.z > Y1);
+        if (in) {
+            if (i < 64) a |= 1ull << i;
+            else b |= 1ull << (i - 64);
+        }
+    }
+    m0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    m1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
 }
 
 // K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
@@ -454,6 +581,8 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, Pa
     SegCursor cur;
     const uint32_t seg_base = wave_id() * seg_cap;
     const ScreenCull cull = screen_cull(fc, v.nodes);
+    const uint64_t cm0 = fc.n_tris >= 64 ? ~0ull : (1ull << fc.n_tris) - 1ull;
+    const uint64_t cm1 = fc.n_tris <= 64 ? 0ull : fc.n_tris >= 128 ? ~0ull : (1ull << (fc.n_tris - 64)) - 1ull;
     for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {  // block-uniform trip count
         const int p = b0 + (int)threadIdx.x;
         ShadeOut so;
@@ -467,7 +596,10 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, Pa
             bool culled;
             camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
             Hit h;
-            traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cnt);
+            if constexpr (std::is_same<View, LdsView>::value)  // LDS scenes: every triangle (camera_hit)
+                camera_hit<kCount>(v, culled ? 0ull : cm0, culled ? 0ull : cm1, d, tmin, tmax, h, cnt);
+            else
+                traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cnt);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
 #if RR_EXP_PRIMARY == 1  // timing experiment only: no shading
             L = mk3(h.t, (float)h.idx, 0.0f);
@@ -500,7 +632,7 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_primary(FrameConsts 
     if constexpr (kLds) {
         extern __shared__ float4 dyn4[];
         int used;
-        const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used);
+        const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used, &fc);
         primary_body<kCount>(fc, v, np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack);
     } else {
         primary_body<kCount>(fc, global_view(sa), np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack);
@@ -1164,8 +1296,8 @@ RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint3
     }
 }
 
-template <bool kCount, typename View>
-RR_D void tiles_body(const FrameConsts& fc, const View& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
+template <bool kCount>
+RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
                      const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
@@ -1199,6 +1331,9 @@ RR_D void tiles_body(const FrameConsts& fc, const View& v, uint32_t* __restrict_
             }
             continue;
         }
+        uint64_t cm0, cm1;
+        tile_mask(fc, v, fc.n_tris, (float)(tx * kTile), (float)(tx * kTile + kTile - 1), (float)(ty * kTile),
+                  (float)(ty * kTile + kTile - 1), cm0, cm1);
         const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
         for (int s = 0; s < fc.spp_total; ++s) {
             const uint32_t key = sample_key(pk, (uint32_t)s);
@@ -1213,7 +1348,7 @@ RR_D void tiles_body(const FrameConsts& fc, const View& v, uint32_t* __restrict_
                     ShadeOut so;
                     Hit h;
                     if (b == 0)
-                        traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cp);
+                        camera_hit<kCount>(v, culled ? 0ull : cm0, culled ? 0ull : cm1, d, tmin, tmax, h, cp);
                     else
                         traverse<false, kCount>(v.nodes, v.tris, RR_EXP_TILES == 3 ? 0 : fc.n_tris, o, d, 0.0f,
                                                 kFltMax, st, h, ce);
@@ -1277,7 +1412,7 @@ __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
     int used;
-    const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used);
+    const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used, &fc);
     tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack);
 }
 
@@ -1403,7 +1538,7 @@ bool scene_in_lds(int n_tris, int n_mats, int n_lights) {
     fc.n_tris = n_tris;
     fc.n_mats = n_mats;
     fc.n_lights = n_lights;
-    return n_tris > 0 && scene_lds_bytes(fc, true) <= kLdsSceneMax;
+    return n_tris > 0 && n_tris <= 128 && scene_lds_bytes(fc, true) <= kLdsSceneMax;  // 128: camera_hit's mask
 }
 
 namespace {
@@ -1429,7 +1564,7 @@ struct Grids {
         kt = lds ? (count ? k_tail<true, true> : k_tail<false, true>)
                  : (count ? k_tail<true, false> : k_tail<false, false>);
         const size_t sp = lds ? scene_lds_bytes(fc, true) : 0, ss = lds ? scene_lds_bytes(fc, false) : 0;
-        dyn_primary = sp;
+        dyn_primary = sp + (lds ? 48 * (size_t)fc.n_tris : 0);  // + stage_camera's 3 float4 per triangle
         primary = grid_for(kp, dyn_primary);
         // consumers hold the producer's segment prefix after the scene: one word
         // per producer block + 1; more LDS can only shrink k_extend's grid, so

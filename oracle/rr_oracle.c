@@ -717,6 +717,7 @@ typedef struct {
     float clamp, inv_w2, inv_h2;
     float filter[ORC_FILTER_N];
     float srgb[ORC_SRGB_N + 1];
+    int cam_all;          /* camera rays test every triangle (LDS-resident scenes, render_ints[7] == 2) */
     int cull_on;          /* screen_rect() succeeded */
     float cull[4];        /* x0 x1 y0 y1 in subpixel coordinates */
 } scene_t;
@@ -774,6 +775,13 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
         hitrec h;
         if (b == 0 && culled) {
             h.t = tmax; h.u = h.v = 0.0f; h.idx = -1; h.orig = -1;
+        } else if (b == 0 && S->cam_all) {
+            /* wavefront.hip camera_hit: LDS-resident scenes test camera rays
+             * against every triangle (the GPU bins them per 8x8 tile, which by
+             * construction keeps every triangle a ray can hit; the accept rule
+             * is order-independent, so the result is the same) */
+            h.t = tmax; h.u = h.v = 0.0f; h.idx = -1; h.orig = -1;
+            for (int i = 0; i < S->bvh->n; ++i) try_leaf(S->bvh, i, o, d, tmin, &h);
         } else {
             trace(S->bvh, o, d, tmin, tmax, 0, &h);
         }
@@ -980,6 +988,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     S->lights = lights;
     S->mats = mats;
     S->world = V(world[0], world[1], world[2]);
+    S->cam_all = ri[7] == 2;
     S->W = ri[0]; S->H = ri[1]; S->spp = ri[2]; S->max_bounces = ri[3]; S->seed = (uint32_t)ri[4]; S->view = ri[5];
     S->clamp = rf[0];
     S->inv_w2 = 2.0f / (float)S->W;
