@@ -645,7 +645,26 @@ struct Mat {
     float metallic, specular, roughness, ior;
     float3 emission;
     int model;  // 0 Principled subset, 1 pure Lambert (analytic test scenes)
+    // per-material terms of the BSDF (mat_derive), the expressions the BSDF
+    // functions used to evaluate at every shading point, unchanged
+    float alpha, a2;   // GGX roughness alpha = max(roughness^2, 1e-4), alpha^2
+    float3 F0;         // Schlick F0 = lerp(0.08 specular, base, metallic)
+    float f0avg, wd;   // spec_prob's lobe weights
+    float kd0;         // (1 - metallic) / pi
 };
+
+RR_HD void mat_derive(Mat& m) {
+    float alpha = m.roughness * m.roughness;
+    if (alpha < 1.0e-4f) alpha = 1.0e-4f;
+    m.alpha = alpha;
+    m.a2 = alpha * alpha;
+    const float s0 = 0.08f * m.specular;
+    m.F0 = mk3(s0 + (m.base.x - s0) * m.metallic, s0 + (m.base.y - s0) * m.metallic,
+               s0 + (m.base.z - s0) * m.metallic);
+    m.f0avg = (m.F0.x + m.F0.y + m.F0.z) * 0.333333343f;
+    m.wd = (1.0f - m.metallic) * ((m.base.x + m.base.y + m.base.z) * 0.333333343f);
+    m.kd0 = (1.0f - m.metallic) * 0.318309886183791f;
+}
 
 RR_HD float schlick_w(float c) {
     float m = 1.0f - c;
@@ -682,23 +701,18 @@ RR_HD float3 bsdf_eval_v(const Mat& m, const BsdfView& vw, float3 N, float3 wo, 
     const float3 H = norm3(add3(wo, wi));
     const float cosD = dot3(wi, H);
     const float NdotH = dot3(N, H);
-    float alpha = m.roughness * m.roughness;
-    if (alpha < 1.0e-4f) alpha = 1.0e-4f;
-    const float a2 = alpha * alpha;
+    const float a2 = m.a2;
     // diffuse
     const float fd90 = 0.5f + 2.0f * m.roughness * cosD * cosD;
     const float fl = schlick_w(cosL);
     const float fv = vw.fv;
-    const float kd = (1.0f - m.metallic) * 0.318309886183791f * (1.0f + (fd90 - 1.0f) * fl) *
-                     (1.0f + (fd90 - 1.0f) * fv);
+    const float kd = m.kd0 * (1.0f + (fd90 - 1.0f) * fl) * (1.0f + (fd90 - 1.0f) * fv);
     // specular
     const float tt = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
     const float D = a2 / (3.14159265358979f * tt * tt);
     const float g1v = vw.g1v;
     const float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
-    const float s0 = 0.08f * m.specular;
-    const float3 F0 = mk3(s0 + (m.base.x - s0) * m.metallic, s0 + (m.base.y - s0) * m.metallic,
-                          s0 + (m.base.z - s0) * m.metallic);
+    const float3 F0 = m.F0;
     const float fw = schlick_w(cosD);
     const float ks = D * g1v * g1l / (4.0f * cosV * cosL);
     const float3 F = mk3(F0.x + (1.0f - F0.x) * fw, F0.y + (1.0f - F0.y) * fw, F0.z + (1.0f - F0.z) * fw);
@@ -711,13 +725,9 @@ RR_HD float3 bsdf_eval_v(const Mat& m, const BsdfView& vw, float3 N, float3 wo, 
 // Probability of picking the specular lobe.
 RR_HD float spec_prob(const Mat& m, float cosV) {
     if (m.model == 1) return 0.0f;
-    const float s0 = 0.08f * m.specular;
-    const float f0avg = ((s0 + (m.base.x - s0) * m.metallic) + (s0 + (m.base.y - s0) * m.metallic) +
-                         (s0 + (m.base.z - s0) * m.metallic)) *
-                        0.333333343f;
+    const float f0avg = m.f0avg;
     const float wsp = f0avg + (1.0f - f0avg) * schlick_w(cosV);
-    const float wd = (1.0f - m.metallic) * ((m.base.x + m.base.y + m.base.z) * 0.333333343f);
-    const float tot = wsp + wd;
+    const float tot = wsp + m.wd;
     return tot > 0.0f ? wsp / tot : 1.0f;
 }
 
@@ -726,9 +736,7 @@ RR_HD BsdfView bsdf_view(const Mat& m, float3 N, float3 wo) {
     v.cosV = dot3(N, wo);
     v.ps = spec_prob(m, v.cosV);
     v.fv = schlick_w(v.cosV);
-    float alpha = m.roughness * m.roughness;
-    if (alpha < 1.0e-4f) alpha = 1.0e-4f;
-    const float a2 = alpha * alpha;
+    const float a2 = m.a2;
     v.g1v = 2.0f * v.cosV / (v.cosV + sqrtf(a2 + (1.0f - a2) * v.cosV * v.cosV));
     return v;
 }
@@ -774,10 +782,8 @@ RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, fl
     float x, y;  // the disk sample both lobes start from
     concentric_disk(u1, u2, x, y);
     if (ul < ps) {
-        float alpha = m.roughness * m.roughness;
-        if (alpha < 1.0e-4f) alpha = 1.0e-4f;
         const float3 wl = mk3(dot3(wo, T), dot3(wo, B), cosV);
-        const float3 hl = sample_vndf(wl, alpha, x, y);
+        const float3 hl = sample_vndf(wl, m.alpha, x, y);
         const float3 H = mk3(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,
                              T.z * hl.x + B.z * hl.y + N.z * hl.z);
         const float k = 2.0f * dot3(wo, H);

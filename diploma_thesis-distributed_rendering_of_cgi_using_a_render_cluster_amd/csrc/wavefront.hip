@@ -82,6 +82,7 @@ struct SceneView {
     TriP tris;
     FloatP mats, lights, filter;
     lds_f4w* cam = nullptr;  // LDS scenes, camera kernels: 3 float4 per triangle (stage_camera)
+    lds_f4w* nrm = nullptr;   // LDS scenes, shading kernels: unit geometric normal per triangle
 };
 using GlobalView = SceneView<const BvhNode*, const TriPack*, const float*>;
 using LdsView = SceneView<lds_node*, lds_tri*, lds_float*>;
@@ -98,6 +99,15 @@ __device__ __forceinline__ Mat load_mat(FloatP mats, int id) {
     r.emission = mk3(m[7], m[8], m[9]);
     r.model = (int)m[10];
     return r;
+}
+
+// Material `id` with its derived BSDF terms (mat_derive at load: staging them
+// in LDS measured slower — 2 more LDS reads and more live registers).
+template <typename View>
+RR_D Mat view_mat(const View& v, int id) {
+    Mat m = load_mat(v.mats, id);
+    mat_derive(m);
+    return m;
 }
 
 // Camera ray for (pixel, sample): filter-importance-sampled subpixel position,
@@ -187,11 +197,14 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         return;
     }
     const TriPack tp = load_tri(v.tris, h.idx);
-    const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2);
-    const Mat m = load_mat(v.mats, f2i(tp.p1.w));
+    const Mat m = view_mat(v, f2i(tp.p1.w));
     const float t = h.t;
     const float3 P = mk3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
-    float3 N = norm3(cross3(e1, e2));
+    float3 N;
+    if constexpr (std::is_same<View, LdsView>::value)
+        N = xyz(lds_ld4(v.nrm + h.idx));  // staged: norm3(cross3(e1, e2))
+    else
+        N = norm3(cross3(xyz(tp.p1), xyz(tp.p2)));
     if (dot3(N, d) > 0.0f) N = mk3(-N.x, -N.y, -N.z);
     const float3 wo = mk3(-d.x, -d.y, -d.z);
     if (m.emission.x != 0.0f || m.emission.y != 0.0f || m.emission.z != 0.0f) {
@@ -491,8 +504,19 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
         lds_copy(q, reinterpret_cast<const float4*>(a.filter), kFilterN / 4);
         q += kFilterN / 4;
     }
+    if (shading || cam_fc) __syncthreads();  // the copies above are visible
+    if (shading) {  // per-triangle unit normals
+        v.nrm = q;
+        for (int i = threadIdx.x; i < a.n_tris; i += kBlock) {
+            const TriPack tp = load_tri(v.tris, i);
+            const float3 n = norm3(cross3(xyz(tp.p1), xyz(tp.p2)));
+            rr_f4v x;
+            x.x = n.x; x.y = n.y; x.z = n.z; x.w = 0.0f;
+            q[i] = x;
+        }
+        q += a.n_tris;
+    }
     if (cam_fc) {
-        __syncthreads();  // the triangles are staged
         v.cam = q;
         stage_camera(q, v.tris, a.n_tris, *cam_fc);
         q += 3 * a.n_tris;
@@ -1523,10 +1547,17 @@ int grid_for(K kernel, size_t dyn_lds) {
 // traversal stack and the <= 8 KB segment prefix keeps 4 blocks of the
 // register-limited kernels per CU.
 constexpr size_t kLdsSceneMax = 12 * 1024;
+size_t scene_budget_bytes(const FrameConsts& fc) {  // the residency test's measure (scene_in_lds)
+    const int n_nodes = std::max(fc.n_tris - 1, 1);
+    return 16 * (4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris + 3 * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights +
+                 kFilterN / 4);
+}
+// What stage_scene stages (without the camera data): + the normals (1 float4
+// per triangle) when shading.
 size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
     const int n_nodes = std::max(fc.n_tris - 1, 1);
     size_t f4 = 4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris;
-    if (shading) f4 += 3 * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4;
+    if (shading) f4 += 3 * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4 + (size_t)fc.n_tris;
     return 16 * f4;
 }
 }  // namespace
@@ -1538,7 +1569,7 @@ bool scene_in_lds(int n_tris, int n_mats, int n_lights) {
     fc.n_tris = n_tris;
     fc.n_mats = n_mats;
     fc.n_lights = n_lights;
-    return n_tris > 0 && n_tris <= 128 && scene_lds_bytes(fc, true) <= kLdsSceneMax;  // 128: camera_hit's mask
+    return n_tris > 0 && n_tris <= 128 && scene_budget_bytes(fc) <= kLdsSceneMax;  // 128: camera_hit's mask
 }
 
 namespace {
