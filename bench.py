@@ -37,11 +37,14 @@ JOB = os.path.join(ROOT, "jobs", "04_very-simple_demo_10f-1w.toml")
 # --workload: the default is BASELINE.json's metric config (configs[1], 04vs on
 # one MI355X); the others are the C4/C5 configs, reported in DESIGN.md/profiles.
 WORKLOADS = {
-    "04vs": {"job": JOB, "metric": METRIC, "steps": 10, "warmup": 2,
+    # 40 steps (4 passes over the 10-frame job): at ~3 ms a frame the fill and
+    # drain of the two-frame pipeline would otherwise weigh ~15 % of a 10-step run
+    "04vs": {"job": JOB, "metric": METRIC, "steps": 40, "warmup": 4,
              "data": "synthetic: 04_very-simple stand-in scene (01_simple-animation content; the 04 .blend is "
                      "missing from the reference), frames of the 04vs demo job, JPEG q90 written per frame",
              "workload": "04vs-standin, 1 frame per step: 1920x1080, 128 spp, max 12 bounces, "
-                         "LBVH rebuild + wavefront path trace + JPEG q90 encode/write"},
+                         "LBVH rebuild + path trace (k_tiles: every sample of an 8x8 tile in one wave) + "
+                         "JPEG q90 encode/write"},
     "02": {"job": os.path.join(ROOT, "jobs", "02_physics-standin_170f-5w_naive-fine.toml"),
            "metric": "job frames/sec at 1/2/4/8 MI355X (02_physics stand-in)", "steps": 10, "warmup": 2,
            "data": "synthetic: 02_physics stand-in (2,000 closed-form rigid bodies, 92,002 triangles; the 02 .blend "
@@ -62,6 +65,10 @@ WORKLOADS = {
                        "rebuild every frame + wavefront path trace + JPEG q90 encode/write"},
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# Vector-issue peak: a wave64 VALU instruction issues over 2 cycles on a SIMD-32
+# (MI355X_MICROARCH.md, wave scheduling), 4 SIMDs per CU, 256 CUs.
+VALU_ISSUE_PER_CLK_PER_SIMD = 0.5
+SIMDS = 256 * 4
 
 
 def parse_args():
@@ -162,6 +169,31 @@ def pmc_traffic(cls: str, path: str):
         for k, v in ks.items():
             if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
                 return {"bytes": v["traffic_bytes"], "source": os.path.relpath(path, ROOT), "kernel": k}
+    return None
+
+
+def pmc_valu(cls: str, path: str, avg_ms: float):
+    """VALU issue utilisation of the class's timed kernel from the committed PMC
+    summary: SQ_INSTS_VALU wave-instructions per launch over the launch time,
+    against 0.5 per clock per SIMD at the clock the counters saw
+    (GRBM_GUI_ACTIVE / 8 XCDs / launch time, MI355X_MICROARCH.md DVFS note)."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        ks = json.load(fh)["kernels"]
+    for name in KERNEL_OF_CLASS.get(cls, []):
+        for k, v in ks.items():
+            if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
+                if "SQ_INSTS_VALU" not in v or "GRBM_GUI_ACTIVE" not in v:
+                    return None
+                pmc_ms = v.get("avg_ms") or avg_ms
+                clk = v["GRBM_GUI_ACTIVE"] / 8.0 / (pmc_ms * 1e-3)
+                achieved = v["SQ_INSTS_VALU"] / (avg_ms * 1e-3)  # wave-instructions/s at the bench's launch time
+                peak = VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * clk
+                return {"achieved": round(achieved / 1e9, 1), "peak": round(peak / 1e9, 1),
+                        "unit": "G wave-instr/s", "frac": round(achieved / peak, 3),
+                        "clock_ghz": round(clk / 1e9, 3), "valu_per_launch": round(v["SQ_INSTS_VALU"]),
+                        "source": os.path.relpath(path, ROOT)}
     return None
 
 
@@ -318,6 +350,11 @@ def main():
                                 "traversed from HBM -> SURVEY 8(d) formula (64 B per node visit, 48 B per "
                                 "triangle test + stream); traffic = PMC HBM bytes per launch (FETCH_SIZE x2 + "
                                 "WRITE_SIZE), traffic_gbs its rate"}
+            valu = pmc_valu(cls, pmc, avg_ms)
+            if valu is not None:
+                # what actually bounds an LDS-resident scene's kernel: vector issue
+                # (the HBM fraction is an honest small number there)
+                roofline["valu_issue"] = valu
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:

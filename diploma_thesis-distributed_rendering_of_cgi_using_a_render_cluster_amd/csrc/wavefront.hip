@@ -533,13 +533,16 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
 // result equals testing every triangle whenever the mask holds every triangle
 // the ray can hit (tile_mask). LDS-resident scenes trace camera rays this way
 // instead of walking the LBVH; oracle/rr_oracle.c brute-forces them the same.
-template <bool kCount>
-RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float tmin, float tmax, Hit& h,
-                     TravCount& cnt) {
+RR_D void set_miss(Hit& h, float tmax) {
     h.t = tmax;
     h.u = h.v = 0.0f;
     h.idx = -1;
     h.orig = -1;
+}
+template <bool kCount>
+RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float tmin, float tmax, Hit& h,
+                     TravCount& cnt) {
+    set_miss(h, tmax);
     for (int w = 0; w < 2; ++w) {
         uint64_t m = w ? m1 : m0;
         while (m) {
@@ -620,9 +623,10 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, Pa
             bool culled;
             camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
             Hit h;
-            if constexpr (std::is_same<View, LdsView>::value)  // LDS scenes: every triangle (camera_hit)
-                camera_hit<kCount>(v, culled ? 0ull : cm0, culled ? 0ull : cm1, d, tmin, tmax, h, cnt);
-            else
+            if constexpr (std::is_same<View, LdsView>::value) {  // LDS scenes: every triangle (camera_hit)
+                set_miss(h, tmax);
+                if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cnt);  // wave-uniform masks
+            } else
                 traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cnt);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
 #if RR_EXP_PRIMARY == 1  // timing experiment only: no shading
@@ -1231,6 +1235,9 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
 // and shading work, so the long tiles start early and the background tiles,
 // whose samples are all culled camera rays, fill the tail.
 constexpr int kTile = 8;  // 8x8 pixels = one wave
+#ifndef RR_TILES_PEEL
+#define RR_TILES_PEEL 0  // 1: bounce 0 outside the bounce loop (two inlined shade() copies, more spills)
+#endif
 #ifndef RR_EXP_TILES
 #define RR_EXP_TILES 0  // timing experiments (wrong images): 1 no shading, 2 no shadow rays, 3 no extension rays
 #endif
@@ -1358,6 +1365,67 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         uint64_t cm0, cm1;
         tile_mask(fc, v, fc.n_tris, (float)(tx * kTile), (float)(tx * kTile + kTile - 1), (float)(ty * kTile),
                   (float)(ty * kTile + kTile - 1), cm0, cm1);
+#if RR_TILES_PEEL
+        const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
+        for (int s = 0; s < fc.spp_total; ++s) {
+            const uint32_t key = sample_key(pk, (uint32_t)s);
+            float3 L = mk3(0.0f, 0.0f, 0.0f), T = mk3(1.0f, 1.0f, 1.0f), o = L, d = L;
+            ShadeOut so;
+            so.cont = so.shadow = false;
+            // bounce 0, peeled: the camera ray against the tile's triangles
+            if (valid) {
+                float tmin, tmax;
+                bool culled;
+                camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
+                Hit h;
+                set_miss(h, tmax);
+                if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);  // wave-uniform masks
+#if RR_EXP_TILES == 1  // timing experiment only: camera rays, no shading
+                L = mk3(h.t, (float)h.idx, 0.0f);
+#else
+                shade(fc, 0, v, o, d, T, h, key, L, so);
+#endif
+                n_c0 += so.cont ? 1u : 0u;
+                n_s0 += so.shadow ? 1u : 0u;
+            }
+            if (so.shadow) {
+                Hit hs;
+                if (!traverse<true, kCount>(v.nodes, v.tris, RR_EXP_TILES == 2 ? 0 : fc.n_tris, so.so, so.sd, 0.0f,
+                                            so.sdist, st, hs, cs))
+                    add_to(L, so.sc);
+            }
+            bool live = so.cont;
+            if (live) {
+                o = so.o;
+                d = so.d;
+                T = so.T;
+            }
+            for (int b = 1; b <= fc.max_bounces; ++b) {
+                if (!__any(live)) break;
+                if (live) {
+                    ShadeOut sb;
+                    Hit h;
+                    traverse<false, kCount>(v.nodes, v.tris, RR_EXP_TILES == 3 ? 0 : fc.n_tris, o, d, 0.0f, kFltMax,
+                                            st, h, ce);
+                    shade(fc, b, v, o, d, T, h, key, L, sb);
+                    if (sb.shadow) {
+                        Hit hs;
+                        if (!traverse<true, kCount>(v.nodes, v.tris, RR_EXP_TILES == 2 ? 0 : fc.n_tris, sb.so, sb.sd,
+                                                    0.0f, sb.sdist, st, hs, cs))
+                            add_to(L, sb.sc);
+                    }
+                    n_c1 += sb.cont ? 1u : 0u;
+                    n_s1 += sb.shadow ? 1u : 0u;
+                    if (sb.cont) {
+                        o = sb.o;
+                        d = sb.d;
+                        T = sb.T;
+                    } else {
+                        live = false;
+                    }
+                }
+            }
+#else
         const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
         for (int s = 0; s < fc.spp_total; ++s) {
             const uint32_t key = sample_key(pk, (uint32_t)s);
@@ -1371,11 +1439,13 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                 if (live) {
                     ShadeOut so;
                     Hit h;
-                    if (b == 0)
-                        camera_hit<kCount>(v, culled ? 0ull : cm0, culled ? 0ull : cm1, d, tmin, tmax, h, cp);
-                    else
+                    if (b == 0) {  // the camera ray against the tile's triangles (wave-uniform masks)
+                        set_miss(h, tmax);
+                        if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);
+                    } else {
                         traverse<false, kCount>(v.nodes, v.tris, RR_EXP_TILES == 3 ? 0 : fc.n_tris, o, d, 0.0f,
                                                 kFltMax, st, h, ce);
+                    }
 #if RR_EXP_TILES == 1  // timing experiment only: camera rays, no shading
                     so.cont = so.shadow = false;
                     L = mk3(h.t, (float)h.idx, 0.0f);
@@ -1404,6 +1474,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     }
                 }
             }
+#endif
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
