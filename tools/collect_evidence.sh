@@ -1,0 +1,18 @@
+#!/bin/bash
+# Copies the summaries of one tools/round_evidence.sh call (merged back into
+# gpurun_out/) into profiles/ (tracked). Run here, after the GPU call:
+#   tools/collect_evidence.sh r1
+set -euo pipefail
+tag=${1:-r1}
+for p in "" _02 _c5; do
+    d=gpurun_out/prof_${tag}${p}
+    cp $d/${tag}${p}_kernel_stats.md profiles/${tag}${p}_kernel_stats.md
+    cp $d/trace/run_kernel_stats.csv profiles/${tag}${p}_kernel_stats.csv
+    cp $d/${tag}${p}_pmc.json profiles/${tag}_pmc${p}.json
+    grep '^{' $d/trace_bench.json > profiles/${tag}${p}_bench_under_rocprof.json
+done
+for wl in 04vs 02 03 c5 04vs_serial; do
+    grep '^{' gpurun_out/ev/bench_$wl.json > profiles/${tag}_bench_$wl.json
+done
+grep -v '^===' gpurun_out/ev/smoke.log > profiles/${tag}_smoke.log
+grep -E 'passed|failed' gpurun_out/ev_log.txt | head -1 > profiles/${tag}_gpu_tests.txt

@@ -9,12 +9,12 @@ mkdir -p gpurun_out
 step=()
 run_step() {
     local secs=$1; shift
-    echo "=== [$(date +%T)] step (${secs}s): $*"
+    echo "=== [$(date +%T)] step (${secs}s): $*" >&2
     timeout -k 10 "$secs" "$@"
     local rc=$?
-    echo "=== step rc=$rc"
+    echo "=== step rc=$rc" >&2
     if [ $rc -ge 124 ]; then
-        echo "=== stopping: step ended with rc=$rc"
+        echo "=== stopping: step ended with rc=$rc" >&2
         exit $rc
     fi
 }
