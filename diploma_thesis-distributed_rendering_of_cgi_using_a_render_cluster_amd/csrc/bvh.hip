@@ -566,6 +566,197 @@ __global__ __launch_bounds__(kBlock) void k_ploc_apply(const int* __restrict__ c
     }
 }
 
+// ------------------------------------------------------- one-launch build ---
+// Scenes of at most kSmallBuild triangles (every LDS-resident scene: 04vs and
+// 01 are 12) build their whole LBVH in ONE workgroup, one thread per triangle,
+// with the intermediate arrays in LDS: the multi-kernel build above is ~26
+// launches (~0.14 ms of launch latency per frame at 12 triangles) around a few
+// hundred instructions of work. Same results, bit for bit:
+//  - K1/K2: the same float ops in the same order as k_transform / k_morton;
+//  - K3: the stable LSD radix sort of (key, index = i) is the order by
+//    (key, i); here each thread takes its rank by counting;
+//  - K4: k_karras on the sorted keys in LDS;
+//  - refit: a child's box is the min/max of the leaf boxes of its sorted leaf
+//    range (min/max are exact, so any grouping gives the tree-merge values);
+//  - K5 triangle packs and k_leafify's leaf-range refs as above.
+constexpr int kSmallBuild = 512;
+
+__global__ __launch_bounds__(kSmallBuild) void k_build_small(
+    int n, const float4* __restrict__ local, const int32_t* __restrict__ obj, const float* __restrict__ xform,
+    const int32_t* __restrict__ tri_mat, float4* __restrict__ world, uint32_t* __restrict__ bounds,
+    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, int2* __restrict__ children,
+    int32_t* __restrict__ node_parent, int32_t* __restrict__ leaf_parent, int2* __restrict__ range,
+    BvhNode* __restrict__ nodes, TriPack* __restrict__ tris) {
+    __shared__ uint32_t red[6];
+    __shared__ uint32_t key_in[kSmallBuild], key_s[kSmallBuild];
+    __shared__ float3 wv[kSmallBuild][3];  // world vertices, original order
+    __shared__ float lbox[kSmallBuild][6];  // leaf boxes, sorted order
+    __shared__ int2 rng[kSmallBuild];       // (first, count) per internal node
+    const int i = threadIdx.x;
+    if (i < 6) red[i] = i < 3 ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+    float3 c = mk3(0.0f, 0.0f, 0.0f);
+    if (i < n) {  // K1 (k_transform)
+        const float* m = xform + 12 * obj[i];
+        float3 w[3];
+        for (int k = 0; k < 3; ++k) {
+            const float4 v = local[3 * i + k];
+            w[k] = mk3(xf(m, v.x, v.y, v.z), xf(m + 4, v.x, v.y, v.z), xf(m + 8, v.x, v.y, v.z));
+            wv[i][k] = w[k];
+        }
+        c = add3(add3(w[0], w[1]), w[2]);
+        world[3 * i + 0] = make_float4(w[0].x, w[0].y, w[0].z, c.x);
+        world[3 * i + 1] = make_float4(w[1].x, w[1].y, w[1].z, c.y);
+        world[3 * i + 2] = make_float4(w[2].x, w[2].y, w[2].z, c.z);
+        atomicMin(&red[0], f2o(c.x));
+        atomicMin(&red[1], f2o(c.y));
+        atomicMin(&red[2], f2o(c.z));
+        atomicMax(&red[3], f2o(c.x));
+        atomicMax(&red[4], f2o(c.y));
+        atomicMax(&red[5], f2o(c.z));
+    }
+    __syncthreads();
+    if (i < 6) bounds[i] = red[i];
+    if (i < n) {  // K2 (k_morton)
+        const float lo[3] = {o2f(red[0]), o2f(red[1]), o2f(red[2])};
+        const float hi[3] = {o2f(red[3]), o2f(red[4]), o2f(red[5])};
+        const float cc[3] = {c.x, c.y, c.z};
+        uint32_t q[3];
+        for (int k = 0; k < 3; ++k) {
+            const float ext = hi[k] - lo[k];
+            const float s = ext > 0.0f ? 1024.0f / ext : 0.0f;
+            float f = (cc[k] - lo[k]) * s;
+            f = fminf(fmaxf(f, 0.0f), 1023.0f);
+            q[k] = (uint32_t)f;
+        }
+        key_in[i] = (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+    }
+    __syncthreads();
+    if (i < n) {  // K3: rank of (key, i)
+        const uint32_t k = key_in[i];
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+            const uint32_t kj = key_in[j];
+            r += (kj < k || (kj == k && j < i)) ? 1 : 0;
+        }
+        key_s[r] = k;
+        keys[r] = k;
+        vals[r] = (uint32_t)i;
+        // K5 pack of sorted leaf r (k_refit) and its box
+        const float3 a = wv[i][0], b = wv[i][1], e = wv[i][2];
+        TriPack tp;
+        tp.p0 = make_float4(a.x, a.y, a.z, i2f(i));
+        tp.p1 = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, i2f(tri_mat[i]));
+        tp.p2 = make_float4(e.x - a.x, e.y - a.y, e.z - a.z, 0.0f);
+        tris[r] = tp;
+        lbox[r][0] = fminf(fminf(a.x, b.x), e.x);
+        lbox[r][1] = fminf(fminf(a.y, b.y), e.y);
+        lbox[r][2] = fminf(fminf(a.z, b.z), e.z);
+        lbox[r][3] = fmaxf(fmaxf(a.x, b.x), e.x);
+        lbox[r][4] = fmaxf(fmaxf(a.y, b.y), e.y);
+        lbox[r][5] = fmaxf(fmaxf(a.z, b.z), e.z);
+    }
+    __syncthreads();
+    if (n == 1) {  // single triangle: root with both children = leaf 0 (k_refit)
+        if (i == 0) {
+            float* f = reinterpret_cast<float*>(&nodes[0]);
+            for (int k = 0; k < 6; ++k) {
+                f[k] = lbox[0][k];
+                f[6 + k] = lbox[0][k];
+            }
+            nodes[0].d = make_int4(~0, ~0, 0, 0);
+        }
+        return;
+    }
+    int2 ch = make_int2(0, 0);
+    if (i < n - 1) {  // K4a (k_karras) over the sorted keys in LDS
+        const int d = (delta(key_s, n, i, i + 1) - delta(key_s, n, i, i - 1)) >= 0 ? 1 : -1;
+        const int dmin = delta(key_s, n, i, i - d);
+        int lmax = 2;
+        while (delta(key_s, n, i, i + lmax * d) > dmin) lmax <<= 1;
+        int l = 0;
+        for (int t = lmax >> 1; t >= 1; t >>= 1)
+            if (delta(key_s, n, i, i + (l + t) * d) > dmin) l += t;
+        const int j = i + l * d;
+        const int dnode = delta(key_s, n, i, j);
+        int s = 0;
+        int t = l;
+        do {
+            t = (t + 1) >> 1;
+            if (delta(key_s, n, i, i + (s + t) * d) > dnode) s += t;
+        } while (t > 1);
+        const int gamma = i + s * d + (d < 0 ? -1 : 0);
+        const int lo = i < j ? i : j, hi = i < j ? j : i;
+        if (lo == gamma) {
+            ch.x = ~gamma;
+            leaf_parent[gamma] = 2 * i;
+        } else {
+            ch.x = gamma;
+            node_parent[gamma] = 2 * i;
+        }
+        if (hi == gamma + 1) {
+            ch.y = ~(gamma + 1);
+            leaf_parent[gamma + 1] = 2 * i + 1;
+        } else {
+            ch.y = gamma + 1;
+            node_parent[gamma + 1] = 2 * i + 1;
+        }
+        children[i] = ch;
+        rng[i] = make_int2(lo, hi - lo + 1);
+        range[i] = rng[i];
+        if (i == 0) node_parent[0] = -1;
+    }
+    __syncthreads();
+    if (i < n - 1) {  // K4b refit from leaf ranges + k_leafify
+        float f[12];
+        int ref[2] = {ch.x, ch.y};
+        for (int side = 0; side < 2; ++side) {
+            const int cref = side ? ch.y : ch.x;
+            int first, cnt;
+            if (cref < 0) {
+                first = ~cref;
+                cnt = 1;
+            } else {
+                first = rng[cref].x;
+                cnt = rng[cref].y;
+                if (kLeafMax > 1 && cnt <= kLeafMax) ref[side] = leaf_ref(first, cnt);
+            }
+            float bx[6];
+            for (int k = 0; k < 6; ++k) bx[k] = lbox[first][k];
+            for (int q = first + 1; q < first + cnt; ++q) {
+                for (int k = 0; k < 3; ++k) bx[k] = fminf(bx[k], lbox[q][k]);
+                for (int k = 3; k < 6; ++k) bx[k] = fmaxf(bx[k], lbox[q][k]);
+            }
+            for (int k = 0; k < 6; ++k) f[6 * side + k] = bx[k];
+        }
+        BvhNode nd;
+        nd.a = make_float4(f[0], f[1], f[2], f[3]);
+        nd.b = make_float4(f[4], f[5], f[6], f[7]);
+        nd.c = make_float4(f[8], f[9], f[10], f[11]);
+        nd.d = make_int4(ref[0], ref[1], 0, 0);
+        nodes[i] = nd;
+    }
+}
+
+struct UploadArgs {
+    float* dst[3];
+    int n[3];
+    float data[kUploadMax];
+};
+
+__global__ __launch_bounds__(kBlock) void k_upload(UploadArgs a) {
+    int off = 0;
+    for (int k = 0; k < 3; ++k) {
+        for (int i = threadIdx.x; i < a.n[k]; i += kBlock) a.dst[k][i] = a.data[off + i];
+        off += a.n[k];
+    }
+}
+
+bool small_build_enabled() {
+    static const bool on = !(getenv("RR_TUNE_SMALL_BUILD") && atoi(getenv("RR_TUNE_SMALL_BUILD")) == 0);
+    return on;
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 void exclusive_scan(DevScene& s, uint32_t* data, int m, hipStream_t st) {
@@ -577,6 +768,23 @@ void exclusive_scan(DevScene& s, uint32_t* data, int m, hipStream_t st) {
 }
 
 }  // namespace
+
+bool upload_by_kernarg(const float* src, const UploadSeg* segs, int nseg, hipStream_t st) {
+    static const bool on = !(getenv("RR_TUNE_KERNARG_UPLOAD") && atoi(getenv("RR_TUNE_KERNARG_UPLOAD")) == 0);
+    if (!on || nseg > 3) return false;
+    UploadArgs a{};
+    int total = 0;
+    for (int k = 0; k < nseg; ++k) total += segs[k].n;
+    if (total > kUploadMax) return false;
+    for (int k = 0; k < nseg; ++k) {
+        a.dst[k] = segs[k].dst;
+        a.n[k] = segs[k].n;
+    }
+    std::memcpy(a.data, src, total * sizeof(float));
+    k_upload<<<1, kBlock, 0, st>>>(a);
+    RR_HIP(hipGetLastError());
+    return true;
+}
 
 void DevScene::release() {
     tri_local.release(); tri_obj.release(); tri_mat.release(); obj_xform.release();
@@ -657,6 +865,18 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, b
     s.leaf_parent.ensure((size_t)n);
     s.flags.ensure((size_t)(n > 1 ? n - 1 : 1));
     s.range.ensure((size_t)(n > 1 ? n - 1 : 1));
+
+    if (n <= kSmallBuild && !want4 && !(want_ploc && n > 2) && small_build_enabled()) {
+        k_build_small<<<1, kSmallBuild, 0, st>>>(n, s.tri_local.ptr, s.tri_obj.ptr, s.obj_xform.ptr, s.tri_mat.ptr,
+                                                 s.tri_world.ptr, s.bounds.ptr, s.keys[0].ptr, s.vals[0].ptr,
+                                                 s.children.ptr, s.node_parent.ptr, s.leaf_parent.ptr, s.range.ptr,
+                                                 s.nodes.ptr, s.tris.ptr);
+        if (prof) prof->end(st);
+        RR_HIP(hipGetLastError());
+        s.ploc = false;
+        s.built = true;
+        return;
+    }
 
     RR_HIP(hipMemsetAsync(s.bounds.ptr, 0xFF, 3 * sizeof(uint32_t), st));
     RR_HIP(hipMemsetAsync(s.bounds.ptr + 3, 0x00, 3 * sizeof(uint32_t), st));

@@ -178,6 +178,20 @@ struct FrameConsts {
 void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof = nullptr, bool want4 = false,
                 bool want_ploc = false);
 
+// Per-frame constants (lights, materials, object transforms; up to
+// kUploadMax floats in all) copied into device buffers by one kernel whose
+// arguments carry the data (bvh.hip k_upload). A hipMemcpyAsync from pinned
+// host memory is a GPU read over PCIe, and such a read queues behind the
+// previous frame's 6 MB of device-to-host output writes (PCIe keeps reads
+// behind posted writes): measured 112 us per frame on 04vs. Kernel arguments
+// are written by the host into device memory, so nothing waits.
+constexpr int kUploadMax = 720;
+struct UploadSeg {
+    float* dst;
+    int n;
+};
+bool upload_by_kernarg(const float* src, const UploadSeg* segs, int nseg, hipStream_t st);
+
 // Whether the path kernels take the LDS-resident (fused, BVH2) variant for a
 // scene of these sizes; otherwise the split path over the BVH4 in HBM.
 bool scene_in_lds(int n_tris, int n_mats, int n_lights);
@@ -194,6 +208,24 @@ void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, f
 
 // Device JPEG forward transform (jpeg.hip); tab = dct | qinv luma | qinv chroma.
 void jpeg_fdct_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, int16_t* d_out, hipStream_t st);
+
+// Device JPEG encode (jpeg.hip): the forward transform above + Huffman coding
+// of the coefficients into the entropy-coded segment of the file (rows, RSTn
+// markers, EOI), written to pinned host memory as [uint64 length][8 B pad]
+// [bytes]. d_huff: 4 x 256 packed code | len << 16 (DC luma, AC luma, DC
+// chroma, AC chroma; image_io jpeg_huff_tables).
+constexpr int kJpegBlockMaxBytes = 216;  // >= the longest coded 8x8 block (1 + 63 x 26 + 27 bits)
+struct JpegDevBufs {
+    uint32_t* acbits;    // per block: AC bits
+    uint32_t* blk_off;   // per block: bit offset in its row
+    uint32_t* row_bits;  // mcuy
+    uint32_t* ready;     // mcuy: stuffed row length + 1 once counted (k_jpeg_finish)
+    uint32_t* scratch;   // mcuy x jpeg_row_scratch_words
+};
+size_t jpeg_row_scratch_words(int W);
+size_t jpeg_stream_max_bytes(int W, int H);
+void jpeg_encode_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, const uint32_t* d_huff,
+                        int16_t* d_coeffs, JpegDevBufs& b, uint8_t* host_out, hipStream_t st);
 
 int counters_per_chunk(int max_bounces);
 int device_cu_count();

@@ -351,6 +351,20 @@ void jpeg_tables(int quality, JpegTables& t) {
     }
 }
 
+void jpeg_header_bytes(int W, int H, int quality, std::vector<uint8_t>& out) {
+    JpegTables t;
+    jpeg_tables(quality, t);
+    out.clear();
+    jpeg_header(W, H, t.ql, t.qc, out);
+}
+
+void jpeg_huff_tables(uint32_t out[4 * 256]) {
+    const Tables& T = tables();
+    const HuffTable* order[4] = {&T.dc[0], &T.ac[0], &T.dc[1], &T.ac[1]};
+    for (int t = 0; t < 4; ++t)
+        for (int s = 0; s < 256; ++s) out[256 * t + s] = (uint32_t)order[t]->code[s] | ((uint32_t)order[t]->len[s] << 16);
+}
+
 size_t jpeg_coeff_count(int W, int H) { return (size_t)((W + 15) / 16) * ((H + 15) / 16) * 6 * 64; }
 
 bool encode_jpeg(const uint8_t* rgba, int W, int H, int quality, std::vector<uint8_t>& out, int threads) {

@@ -22,6 +22,11 @@ void jpeg_tables(int quality, JpegTables& t);
 size_t jpeg_coeff_count(int W, int H);
 bool encode_jpeg_coeffs(const int16_t* coeffs, int W, int H, int quality, std::vector<uint8_t>& out,
                         int threads = 0);
+// The file bytes in front of the entropy-coded segment (SOI ... SOS), and the
+// Huffman tables as 4 x 256 packed code | len << 16 (DC luma, AC luma, DC
+// chroma, AC chroma) for the device coder (jpeg.hip).
+void jpeg_header_bytes(int W, int H, int quality, std::vector<uint8_t>& out);
+void jpeg_huff_tables(uint32_t out[4 * 256]);
 bool encode_jpeg(const uint8_t* rgba, int W, int H, int quality, std::vector<uint8_t>& out, int threads = 0);
 bool encode_png(const uint8_t* rgba, int W, int H, std::vector<uint8_t>& out, int level = 1);
 bool write_file(const std::string& path, const std::vector<uint8_t>& data);

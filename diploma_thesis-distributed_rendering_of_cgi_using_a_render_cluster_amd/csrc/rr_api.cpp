@@ -94,6 +94,8 @@ struct FrameSlot {
     DevBuf<int16_t> coeffs;
     KernelProfiler prof;
     PinnedBuf host_rgba, host_coeffs, host_counters, host_upload;
+    PinnedBuf host_jpeg;   // device-coded JPEG stream: [uint64 length][pad][bytes]
+    bool jpeg_dev = false;  // this frame's entropy coding runs on the device
     FrameSetup fs;
     rr_scene* scene = nullptr;
     std::string out_path, format;
@@ -118,6 +120,9 @@ struct rr_ctx {
     DevBuf<float> jpeg_tab;
     int jpeg_tab_quality = -1;
     DevBuf<int16_t> jpeg_coeffs;
+    // device entropy coder (jpeg.hip): Huffman tables, per-row scratch, stream
+    DevBuf<uint32_t> jpeg_huff;
+    DevBuf<uint32_t> jpeg_scratch, jpeg_blk;
     std::vector<float> filter_cache;
     float filter_width_cached = -1.f;
     bool srgb_uploaded = false;
@@ -217,17 +222,23 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     std::memcpy(up, fs.lights.data(), nl * sizeof(float));
     std::memcpy(up + nl, fs.materials.data(), nm * sizeof(float));
     std::memcpy(up + nl + nm, fs.obj_xform.data(), nx * sizeof(float));
-    if (nl) RR_HIP(hipMemcpyAsync(p.lights.ptr, up, nl * sizeof(float), hipMemcpyHostToDevice, st));
-    RR_HIP(hipMemcpyAsync(p.materials.ptr, up + nl, nm * sizeof(float), hipMemcpyHostToDevice, st));
     DevScene& d = s->dev;
     if (hier == 0) hier = frame_hier(d.n_tris, (int)(nm / RR_MAT_FLOATS), (int)(nl / RR_LIGHT_FLOATS));
     const bool want4 = hier == kHierBvh4;
     const bool want_ploc = hier == kHierPloc && d.n_tris > 2;
     const bool rebuild =
         !d.built || d.cached_xform != fs.obj_xform || (want4 && !d.has4) || (want_ploc != d.ploc);
-    if (rebuild && d.n_tris > 0) {
-        d.obj_xform.ensure(nx);
-        RR_HIP(hipMemcpyAsync(d.obj_xform.ptr, up + nl + nm, nx * sizeof(float), hipMemcpyHostToDevice, st));
+    const bool upload_x = rebuild && d.n_tris > 0;
+    if (upload_x) d.obj_xform.ensure(nx);
+    const UploadSeg segs[3] = {{p.lights.ptr, (int)nl}, {p.materials.ptr, (int)nm},
+                               {upload_x ? d.obj_xform.ptr : nullptr, upload_x ? (int)nx : 0}};
+    if (!upload_by_kernarg(up, segs, 3, st)) {
+        if (nl) RR_HIP(hipMemcpyAsync(p.lights.ptr, up, nl * sizeof(float), hipMemcpyHostToDevice, st));
+        RR_HIP(hipMemcpyAsync(p.materials.ptr, up + nl, nm * sizeof(float), hipMemcpyHostToDevice, st));
+        if (upload_x)
+            RR_HIP(hipMemcpyAsync(d.obj_xform.ptr, up + nl + nm, nx * sizeof(float), hipMemcpyHostToDevice, st));
+    }
+    if (upload_x) {
         build_lbvh(d, st, &p.prof, want4, want_ploc);
         d.cached_xform = fs.obj_xform;
     } else if (rebuild) {
@@ -284,6 +295,48 @@ int choose_spp_chunk(const FrameSetup& fs) {
     return (int)c;
 }
 
+// Entropy coding on the device (jpeg.hip) unless RR_TUNE_DEVICE_ENTROPY=0
+// (then the coefficients are copied back and Huffman-coded on host threads).
+bool device_entropy_enabled() {
+    static const bool on = !(getenv("RR_TUNE_DEVICE_ENTROPY") && atoi(getenv("RR_TUNE_DEVICE_ENTROPY")) == 0);
+    return on;
+}
+
+// Device JPEG encode of an RGBA8 frame (transform into c->jpeg_coeffs +
+// Huffman coding) into the slot's pinned stream buffer, on the context stream.
+void enqueue_jpeg_device(rr_ctx* c, FrameSlot& sl, const uint8_t* d_rgba, int W, int H, const float* d_tab) {
+    if (!c->jpeg_huff.ptr) {
+        uint32_t h[4 * 256];
+        jpeg_huff_tables(h);
+        c->jpeg_huff.ensure(4 * 256);
+        RR_HIP(hipMemcpy(c->jpeg_huff.ptr, h, sizeof h, hipMemcpyHostToDevice));
+    }
+    const size_t mcuy = (size_t)(H + 15) / 16;
+    const size_t nblocks = mcuy * (size_t)((W + 15) / 16) * 6;
+    c->jpeg_coeffs.ensure(jpeg_coeff_count(W, H));
+    c->jpeg_blk.ensure(2 * nblocks + 2 * mcuy);
+    c->jpeg_scratch.ensure(mcuy * jpeg_row_scratch_words(W));
+    sl.host_jpeg.ensure(jpeg_stream_max_bytes(W, H) + 16);
+    void* dev_host = nullptr;
+    RR_HIP(hipHostGetDevicePointer(&dev_host, sl.host_jpeg.ptr, 0));
+    uint32_t* blk = c->jpeg_blk.ptr;
+    JpegDevBufs b{blk, blk + nblocks, blk + 2 * nblocks, blk + 2 * nblocks + mcuy, c->jpeg_scratch.ptr};
+    jpeg_encode_device(d_rgba, W, H, d_tab, c->jpeg_huff.ptr, c->jpeg_coeffs.ptr, b, static_cast<uint8_t*>(dev_host),
+                       c->stream);
+}
+
+// The file of a device-coded frame: host-built header + the device stream.
+bool write_device_jpeg(const FrameSlot& sl, const std::string& path, uint64_t* bytes) {
+    uint64_t len = 0;
+    std::memcpy(&len, sl.host_jpeg.ptr, sizeof len);
+    if (len + 16 > sl.host_jpeg.cap) throw std::runtime_error("device JPEG stream overflow");
+    std::vector<uint8_t> data;
+    jpeg_header_bytes(sl.fs.W, sl.fs.H, sl.quality, data);
+    data.insert(data.end(), sl.host_jpeg.ptr + 16, sl.host_jpeg.ptr + 16 + len);
+    *bytes = data.size();
+    return write_file(path, data);
+}
+
 // Enqueue the device part of one frame on the context stream (no host
 // synchronisation): LBVH (if needed), wavefront, tonemap, optionally the JPEG
 // transform, and the asynchronous copies of the slot's outputs.
@@ -320,6 +373,7 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
         OutSwap(rr_ctx* c_, FrameSlot& s_) : c(c_), sl(s_) { swap(); }
         ~OutSwap() { swap(); }
     } out_swap(c, sl);
+    sl.jpeg_dev = false;
     sl.count = (fs.flags & RR_FLAG_COUNT_TRAVERSAL) != 0;
     c->paths.count_traversal = sl.count;
     c->paths.force_wavefront = (fs.flags & RR_FLAG_WAVEFRONT) != 0;
@@ -346,14 +400,16 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
         }
         const size_t nc = jpeg_coeff_count(fs.W, fs.H);
         c->jpeg_coeffs.ensure(nc);
-        sl.host_coeffs.ensure(nc * sizeof(int16_t));
-        jpeg_fdct_device(c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr, c->jpeg_coeffs.ptr, st);
+        sl.jpeg_dev = device_entropy_enabled();
+        if (sl.jpeg_dev) enqueue_jpeg_device(c, sl, c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr);
+        else jpeg_fdct_device(c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr, c->jpeg_coeffs.ptr, st);
     }
     RR_HIP(hipEventRecord(sl.ev[2], st));
     hipStream_t cs = c->copy_stream;
     RR_HIP(hipStreamWaitEvent(cs, sl.ev[2], 0));
-    if (sl.jpeg) {
+    if (sl.jpeg && !sl.jpeg_dev) {
         const size_t nc = jpeg_coeff_count(fs.W, fs.H);
+        sl.host_coeffs.ensure(nc * sizeof(int16_t));
         RR_HIP(hipMemcpyAsync(sl.host_coeffs.ptr, c->jpeg_coeffs.ptr, nc * sizeof(int16_t), hipMemcpyDeviceToHost,
                               cs));
     }
@@ -515,6 +571,11 @@ void rr_destroy(rr_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     c->paths.release();
+    c->jpeg_tab.release();
+    c->jpeg_coeffs.release();
+    c->jpeg_huff.release();
+    c->jpeg_scratch.release();
+    c->jpeg_blk.release();
     for (auto& sl : c->slots) {
         for (auto& e : sl.ev)
             if (e) (void)hipEventDestroy(e);
@@ -629,7 +690,11 @@ int rr_frame_complete(rr_ctx* c, uint64_t ticket, rr_frame_timing* timing, rr_fr
         sl->tm.file_saving_started_at = sl->tm.finished_rendering_at;
         uint64_t bytes = 0;
         const auto t_enc = std::chrono::steady_clock::now();
-        if (sl->jpeg) {
+        if (sl->jpeg && sl->jpeg_dev) {
+            const std::string path = sl->out_path + ".jpg";
+            if (!write_device_jpeg(*sl, path, &bytes))
+                return fail(RR_EIO, "cannot write " + path + ": " + std::strerror(errno));
+        } else if (sl->jpeg) {
             std::vector<uint8_t> data;
             if (!encode_jpeg_coeffs(reinterpret_cast<const int16_t*>(sl->host_coeffs.ptr), fs.W, fs.H, sl->quality,
                                     data))
@@ -702,6 +767,48 @@ int rr_encode_image(const uint8_t* rgba8, int32_t w, int32_t h, const char* out_
     return guarded([&] { return do_encode(rgba8, w, h, out_path, format, quality, bytes); });
 }
 
+int rr_debug_jpeg_device(rr_ctx* c, const uint8_t* rgba8, int32_t w, int32_t h, int32_t quality, uint8_t* out,
+                         uint64_t cap, uint64_t* len) {
+    if (!c || !rgba8 || !len || w <= 0 || h <= 0 || w > 65535 || h > 65535) return fail(RR_EINVAL, "bad arguments");
+    if (quality < 1 || quality > 100) return fail(RR_EINVAL, "jpeg_quality must be 1..100");
+    return guarded([&] {
+        if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
+        set_device(c);
+        hipStream_t st = c->stream;
+        DevBuf<uint8_t> img;
+        img.ensure((size_t)w * h * 4);
+        RR_HIP(hipMemcpy(img.ptr, rgba8, (size_t)w * h * 4, hipMemcpyHostToDevice));
+        JpegTables t;
+        jpeg_tables(quality, t);
+        float tab[192];
+        std::memcpy(tab, t.dct, sizeof t.dct);
+        std::memcpy(tab + 64, t.qinv_l, sizeof t.qinv_l);
+        std::memcpy(tab + 128, t.qinv_c, sizeof t.qinv_c);
+        DevBuf<float> dtab;
+        dtab.ensure(192);
+        RR_HIP(hipMemcpy(dtab.ptr, tab, sizeof tab, hipMemcpyHostToDevice));
+        c->jpeg_tab_quality = -1;  // the context's cached table is not this one's
+        FrameSlot& sl = c->slots[0];
+        sl.fs.W = w;
+        sl.fs.H = h;
+        sl.quality = quality;
+        enqueue_jpeg_device(c, sl, img.ptr, w, h, dtab.ptr);
+        RR_HIP(hipStreamSynchronize(st));
+        uint64_t n = 0;
+        std::memcpy(&n, sl.host_jpeg.ptr, sizeof n);
+        std::vector<uint8_t> hdr;
+        jpeg_header_bytes(w, h, quality, hdr);
+        *len = hdr.size() + n;
+        if (out && cap >= *len) {
+            std::memcpy(out, hdr.data(), hdr.size());
+            std::memcpy(out + hdr.size(), sl.host_jpeg.ptr + 16, n);
+        }
+        img.release();
+        dtab.release();
+        return RR_OK;
+    });
+}
+
 int rr_debug_counts(rr_scene* s, int32_t* nt, int32_t* nl, int32_t* nm, int32_t* no) {
     if (!s) return fail(RR_EINVAL, "scene is NULL");
     int lights = 0;
@@ -760,13 +867,19 @@ int rr_debug_frame_state(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_
 
 int rr_debug_bvh(rr_ctx* c, rr_scene* s, int32_t frame, uint32_t* keys, uint32_t* order, int32_t* children,
                  float* boxes) {
+    return rr_debug_bvh_hier(c, s, frame, 0, keys, order, children, boxes);
+}
+
+int rr_debug_bvh_hier(rr_ctx* c, rr_scene* s, int32_t frame, int32_t hier, uint32_t* keys, uint32_t* order,
+                      int32_t* children, float* boxes) {
     if (!c || !s) return fail(RR_EINVAL, "NULL ctx or scene");
+    if (hier != 0 && hier != kHierLbvh && hier != kHierPloc) return fail(RR_EINVAL, "hier must be 0, 2 or 3");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
         PinnedBuf staging;
-        prepare_frame(c, s, fs, staging);
+        prepare_frame(c, s, fs, staging, hier);
         DevScene& d = s->dev;
         const int n = d.n_tris;
         hipStream_t st = c->stream;

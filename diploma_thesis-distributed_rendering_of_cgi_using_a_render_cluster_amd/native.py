@@ -74,7 +74,7 @@ EXPORTS = [
     "rr_frame_submit", "rr_frame_complete",
     "rr_render_frame_to_memory", "rr_scene_resolution", "rr_encode_image", "rr_last_error",
     "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
-    "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_bvh4",
+    "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_bvh4", "rr_debug_bvh_hier", "rr_debug_jpeg_device",
 ]
 
 _lib = None
@@ -118,6 +118,9 @@ def lib() -> ctypes.CDLL:
         "rr_debug_bvh": (c_int, [P, P, i32, u32p, u32p, i32p, f32p]),
         "rr_debug_trace": (c_int, [P, P, i32, i32, i32, f32p, f32p, i32p, u8p]),
         "rr_debug_bvh4": (c_int, [P, P, i32, i32p, i32p, f32p]),
+        "rr_debug_bvh_hier": (c_int, [P, P, i32, i32, u32p, u32p, i32p, f32p]),
+        "rr_debug_jpeg_device": (c_int, [P, u8p, i32, i32, i32, u8p, ctypes.c_uint64,
+                                         ctypes.POINTER(ctypes.c_uint64)]),
         "rr_debug_object_matrix": (c_int, [P, i32, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
@@ -303,14 +306,16 @@ class RenderContext:
                                           _ptr(ri, ctypes.c_int32), _ptr(rf, ctypes.c_float)), self.handle)
         return FrameState(tris[:n], mats_i[:n], cam, lights[:nl], mats[:nm], world, ri, rf)
 
-    def bvh(self, scene: Scene, frame: int):
+    def bvh(self, scene: Scene, frame: int, hier: int = 0):
+        """rr_debug_bvh_hier: (keys, order, children (ni,2), boxes (ni,12)); hier
+        2 = LBVH, 3 = PLOC, 0 = the frame's hierarchy."""
         n = scene.counts()["triangles"]
         ni = max(n - 1, 1)
         keys = np.zeros(n, np.uint32)
         order = np.zeros(n, np.uint32)
         children = np.zeros((ni, 2), np.int32)
         boxes = np.zeros((ni, 12), np.float32)
-        _check(lib().rr_debug_bvh(self.handle, scene.handle, int(frame), _ptr(keys, ctypes.c_uint32),
+        _check(lib().rr_debug_bvh_hier(self.handle, scene.handle, int(frame), int(hier), _ptr(keys, ctypes.c_uint32),
                                   _ptr(order, ctypes.c_uint32), _ptr(children, ctypes.c_int32),
                                   _ptr(boxes, ctypes.c_float)), self.handle)
         return keys, order, children, boxes
@@ -324,6 +329,19 @@ class RenderContext:
         _check(lib().rr_debug_bvh4(self.handle, scene.handle, int(frame), ctypes.byref(n4), _ptr(ch, ctypes.c_int32),
                                    _ptr(bx, ctypes.c_float)), self.handle)
         return ch[:n4.value], bx[:n4.value]
+
+    def jpeg_device(self, rgba: np.ndarray, quality: int = 90) -> bytes:
+        """rr_debug_jpeg_device: the JPEG file bytes of an (H, W, 4) uint8 image
+        encoded on the device (forward DCT + Huffman coding)."""
+        rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+        h, w = rgba.shape[:2]
+        n = ctypes.c_uint64()
+        _check(lib().rr_debug_jpeg_device(self.handle, _ptr(rgba, ctypes.c_uint8), w, h, int(quality), None, 0,
+                                          ctypes.byref(n)), self.handle)
+        out = np.zeros(n.value, np.uint8)
+        _check(lib().rr_debug_jpeg_device(self.handle, _ptr(rgba, ctypes.c_uint8), w, h, int(quality),
+                                          _ptr(out, ctypes.c_uint8), n.value, ctypes.byref(n)), self.handle)
+        return out.tobytes()
 
     def trace(self, scene: Scene, frame: int, rays: np.ndarray, width: int = 0):
         """rr_debug_trace; width 0 = the hierarchy the frame kernels use."""

@@ -191,6 +191,13 @@ int rr_encode_image(const uint8_t* rgba8, int32_t width, int32_t height,
                     const char* out_path_no_ext, const char* format,
                     int32_t jpeg_quality, uint64_t* bytes_written);
 
+/* Encode an RGBA8 image with the device JPEG path (forward DCT + Huffman
+ * coding on the GPU, jpeg.hip; the path rr_render_frame takes for "JPEG").
+ * *len receives the file size; the bytes are copied to out if cap >= *len.
+ * Exported for parity tests against rr_encode_image. */
+int rr_debug_jpeg_device(rr_ctx* ctx, const uint8_t* rgba8, int32_t width, int32_t height,
+                         int32_t jpeg_quality, uint8_t* out, uint64_t cap, uint64_t* len);
+
 /* Thread-local message of the last failure on this thread (ctx may be NULL). */
 const char* rr_last_error(rr_ctx* ctx);
 
@@ -222,11 +229,16 @@ int rr_debug_frame_state(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
                          int32_t* render_ints /* RR_RENDER_INTS */,
                          float* render_floats /* RR_RENDER_FLOATS */);
 
-/* LBVH of the frame: sorted Morton keys and primitive order (n each), internal
+/* Hierarchy of the frame (rr_debug_bvh_hier): sorted Morton keys and primitive order (n each), internal
  * node children (2*(n-1); leaf = ~sorted_index) and child boxes (12*(n-1):
  * lmin3 lmax3 rmin3 rmax3). n == 1 yields one root whose two children are leaf 0. */
 int rr_debug_bvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, uint32_t* keys,
                  uint32_t* order, int32_t* children, float* boxes);
+
+/* rr_debug_bvh of a chosen hierarchy: hier 2 = Karras LBVH, 3 = PLOC, 0 = the
+ * one the frame kernels use (what rr_debug_bvh returns). */
+int rr_debug_bvh_hier(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t hier, uint32_t* keys,
+                      uint32_t* order, int32_t* children, float* boxes);
 
 /* BVH4 collapse of the frame's LBVH (the hierarchy the split path of large
  * scenes traverses; built on demand here). *n4 receives the node count; if

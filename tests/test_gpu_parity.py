@@ -234,8 +234,8 @@ def test_render_frame_writes_named_files(ctx, rr, s04, tmp_path):
     assert t.loaded_at <= t.started_rendering_at <= t.finished_rendering_at == t.file_saving_started_at
     assert t.file_saving_started_at <= t.file_saving_finished_at
     _, rgba, _ = ctx.render_to_memory(s04, 7, p)
-    # the device JPEG transform (jpeg.hip) + host Huffman coding produce the same
-    # bytes as the all-host encoder on the same 8-bit image
+    # the device JPEG path (jpeg.hip: transform + Huffman coding) produces the
+    # same bytes as the all-host encoder on the same 8-bit image
     rr.encode_image(rgba, str(tmp_path / "host_encoded"), "JPEG", 90)
     assert (tmp_path / "host_encoded.jpg").read_bytes() == f.read_bytes()
     jpg = np.asarray(Image.open(f).convert("RGB")).astype(np.float64)
