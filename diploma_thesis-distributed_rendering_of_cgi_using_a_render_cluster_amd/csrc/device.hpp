@@ -139,6 +139,8 @@ struct DevPaths {
     DevBuf<int32_t> counters;  // per chunk, per bounce b: {paths entering b+1, shadow rays of b}
     DevBuf<int32_t> spill;     // traversal stack spill
     DevBuf<float4> film;
+    DevBuf<float4> film_part;  // open sample group's partial sum between chunks (k_accumulate)
+    DevBuf<float> tile_slab;   // k_tiles: per sliced tile, one group sum plane per sample group
     DevBuf<uint8_t> rgba8;
     DevBuf<float> filter_table;
     DevBuf<float> srgb_lut;

@@ -39,6 +39,12 @@ namespace rr {
 namespace {
 
 constexpr int kFilterN = 1024;
+// Film sum order (every path, and oracle/rr_oracle.c): samples are summed in
+// order within groups of kFilmGroup, and the group sums in order into the
+// film (sum = 0; per group: sum += group). Frames of <= kFilmGroup samples
+// are the plain in-order sum. Groups let k_tiles split a tile's samples
+// across waves without changing a bit.
+constexpr int kFilmGroup = 32;
 constexpr int kSrgbN = 4096;
 constexpr int kLightF = 12;
 constexpr int kMatF = 12;
@@ -1203,20 +1209,41 @@ RR_D uchar4 tonemap(const FrameConsts& fc, float4 acc, const float* __restrict__
     return make_uchar4(q[0], q[1], q[2], 255);
 }
 
+// Film sum in the grouped order (kFilmGroup, rr_device.h): the open group's
+// partial sum crosses chunk boundaries in `part` (touched only by frames of
+// several chunks).
 __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
-                                                       float4* __restrict__ film, int first_chunk,
-                                                       int last_chunk, const float* __restrict__ srgb,
+                                                       float4* __restrict__ film, float4* __restrict__ part,
+                                                       int first_chunk, int last_chunk, const float* __restrict__ srgb,
                                                        uchar4* __restrict__ out) {
     for (int pix = blockIdx.x * kBlock + threadIdx.x; pix < fc.npix; pix += gridDim.x * kBlock) {
-        float4 acc = first_chunk ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : film[pix];
+        float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f), P = acc;
+        if (!first_chunk) {
+            acc = film[pix];
+            P = part[pix];
+        }
         for (int s = 0; s < fc.spp_chunk; ++s) {
+            const int gs = fc.first_sample + s;
+            if (gs > 0 && (gs & (kFilmGroup - 1)) == 0) {  // close the group
+                acc.x = acc.x + P.x;
+                acc.y = acc.y + P.y;
+                acc.z = acc.z + P.z;
+                P = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
             const float3 L = rad.get((size_t)s * fc.npix + pix);
-            acc.x = acc.x + L.x;
-            acc.y = acc.y + L.y;
-            acc.z = acc.z + L.z;
+            P.x = P.x + L.x;
+            P.y = P.y + L.y;
+            P.z = P.z + L.z;
+        }
+        if (last_chunk) {
+            acc.x = acc.x + P.x;
+            acc.y = acc.y + P.y;
+            acc.z = acc.z + P.z;
+            out[pix] = tonemap(fc, acc, srgb);
+        } else {
+            part[pix] = P;
         }
         film[pix] = acc;
-        if (last_chunk) out[pix] = tonemap(fc, acc, srgb);
     }
 }
 
@@ -1327,10 +1354,23 @@ RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint3
     }
 }
 
+// Sample-group slices of the box tiles (load balance: a heavy tile does not
+// run as one wave's unit at the end of the launch). Slab of tile t: one plane
+// per sample group g (group sum, 3 x 64 floats: x, y, z per lane), folded in
+// group order by k_tiles_fold after the launch. (An in-launch hand-off — sc1
+// stores, a ticket per tile, the last slice folding — measured 0.5 ms slower
+// per 04vs frame than this second launch.)
+struct TileSlices {
+    int n;             // slices per box tile = sample groups (1: no slicing)
+    size_t floats;     // slab floats per tile: 192 * groups
+    float* slab;
+};
+
 template <bool kCount>
 RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
                      const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
-                     int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
+                     int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
+                     const TileSlices sl) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
     TravStack st{stack, spill + gtid, stride, 0};
@@ -1339,22 +1379,40 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     const ScreenCull cull = screen_cull(fc, v.nodes);
     const TileOrder to = tile_order(fc, cull);
     const int lane = threadIdx.x & 63;
+    // Work units: each tile of the screen-rectangle box is cut into sl.n slices,
+    // one per sample group (box tiles first), every other tile is one unit.
+    const int ng = (fc.spp_total + kFilmGroup - 1) / kFilmGroup;
+    const int nb = to.bw * to.bh;
+    const int n_sliced = nb * sl.n;
+    const int n_units = n_sliced + (to.n - nb);
     for (;;) {
-        int t = 0;
-        if (lane == 0) t = (int)atomicAdd(tile_ctr, 1u);
-        t = __builtin_amdgcn_readlane(t, 0);
-        if (t >= to.n) break;
+        int u = 0;
+        if (lane == 0) u = (int)atomicAdd(tile_ctr, 1u);
+        u = __builtin_amdgcn_readlane(u, 0);
+        if (u >= n_units) break;
+        int t, k = 0, nk = 1;  // tile, slice, slices of this tile
+        if (u < n_sliced) {
+            t = u / sl.n;
+            k = u - t * sl.n;
+            nk = sl.n;
+        } else {
+            t = u - n_sliced + nb;
+        }
         int tx, ty;
         to.at(t, tx, ty);
         const int px = tx * kTile + (lane & (kTile - 1)), py = ty * kTile + (lane >> 3);
         const bool valid = px < fc.W && py < fc.H;
         const int pix = py * fc.W + px;
         float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (tile_culled(fc, cull, tx, ty)) {  // background tile: film = the world term summed spp times
-            for (int s = 0; s < fc.spp_total; ++s) {
-                acc.x = acc.x + fc.world.x;
-                acc.y = acc.y + fc.world.y;
-                acc.z = acc.z + fc.world.z;
+        if (tile_culled(fc, cull, tx, ty)) {  // background tile: film = the world term, grouped sum
+            if (k != 0) continue;             // (slice 0 does the whole tile)
+            for (int g = 0; g < ng; ++g) {
+                float3 P = mk3(0.0f, 0.0f, 0.0f);
+                const int s_end = min(fc.spp_total, (g + 1) * kFilmGroup);
+                for (int s = g * kFilmGroup; s < s_end; ++s) add_to(P, fc.world);
+                acc.x = acc.x + P.x;
+                acc.y = acc.y + P.y;
+                acc.z = acc.z + P.z;
             }
             if (valid) {
                 film[pix] = acc;
@@ -1362,12 +1420,15 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             }
             continue;
         }
+        // samples of this unit: group k of a sliced tile, else all of them
+        const int s_lo = nk > 1 ? k * kFilmGroup : 0;
+        const int s_hi = nk > 1 ? min(fc.spp_total, s_lo + kFilmGroup) : fc.spp_total;
         uint64_t cm0, cm1;
         tile_mask(fc, v, fc.n_tris, (float)(tx * kTile), (float)(tx * kTile + kTile - 1), (float)(ty * kTile),
                   (float)(ty * kTile + kTile - 1), cm0, cm1);
 #if RR_TILES_PEEL
         const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
-        for (int s = 0; s < fc.spp_total; ++s) {
+        for (int s = s_lo; s < s_hi; ++s) {
             const uint32_t key = sample_key(pk, (uint32_t)s);
             float3 L = mk3(0.0f, 0.0f, 0.0f), T = mk3(1.0f, 1.0f, 1.0f), o = L, d = L;
             ShadeOut so;
@@ -1427,7 +1488,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             }
 #else
         const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
-        for (int s = 0; s < fc.spp_total; ++s) {
+        for (int s = s_lo; s < s_hi; ++s) {
             const uint32_t key = sample_key(pk, (uint32_t)s);
             float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = mk3(1.0f, 1.0f, 1.0f), L = o;
             float tmin = 0.0f, tmax = -1.0f;
@@ -1479,6 +1540,13 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
         }
+        if (nk > 1) {  // one group of a sliced tile: its sum goes to the slab, k_tiles_fold adds them up
+            float* const slab = sl.slab + (size_t)t * sl.floats + (size_t)k * 192;
+            slab[lane] = acc.x;
+            slab[64 + lane] = acc.y;
+            slab[128 + lane] = acc.z;
+            continue;
+        }
         if (valid) {
             film[pix] = acc;
             out[pix] = tonemap(fc, acc, srgb);
@@ -1502,13 +1570,44 @@ __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc
                                                                   const float* __restrict__ srgb,
                                                                   uchar4* __restrict__ out, uint32_t* __restrict__ tot,
                                                                   int32_t* __restrict__ spill,
-                                                                  unsigned long long* __restrict__ tc) {
+                                                                  unsigned long long* __restrict__ tc,
+                                                                  TileSlices sl) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
     int used;
     const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used, &fc);
-    tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack);
+    tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl);
+}
+
+// Film of the sliced tiles: the group sums of each box tile that is not
+// culled, added in group order (the same box and culling test as k_tiles,
+// from the same root node), then tonemapped. One wave per tile.
+__global__ __launch_bounds__(kBlock) void k_tiles_fold(FrameConsts fc, const BvhNode* __restrict__ nodes,
+                                                       TileSlices sl, float4* __restrict__ film,
+                                                       const float* __restrict__ srgb, uchar4* __restrict__ out) {
+    const ScreenCull cull = screen_cull(fc, nodes);
+    const TileOrder to = tile_order(fc, cull);
+    const int nb = to.bw * to.bh;
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    for (int t = wave; t < nb; t += gridDim.x * kWavesPerBlock) {
+        int tx, ty;
+        to.at(t, tx, ty);
+        if (tile_culled(fc, cull, tx, ty)) continue;
+        const int px = tx * kTile + (lane & (kTile - 1)), py = ty * kTile + (lane >> 3);
+        if (px >= fc.W || py >= fc.H) continue;
+        const float* slab = sl.slab + (size_t)t * sl.floats;
+        float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int g = 0; g < sl.n; ++g, slab += 192) {
+            acc.x = acc.x + slab[lane];
+            acc.y = acc.y + slab[64 + lane];
+            acc.z = acc.z + slab[128 + lane];
+        }
+        const int pix = py * fc.W + px;
+        film[pix] = acc;
+        out[pix] = tonemap(fc, acc, srgb);
+    }
 }
 
 __global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
@@ -1587,9 +1686,18 @@ using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, Rad, int32_t*, unsigned
 using TailFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, uint32_t*, int32_t*,
                         unsigned long long*);
 using TilesFn = void (*)(FrameConsts, SceneArgs, uint32_t*, float4*, const float*, uchar4*, uint32_t*, int32_t*,
-                         unsigned long long*);
+                         unsigned long long*, TileSlices);
 // LDS-resident scenes render through k_tiles (default) or, with RR_TUNE_TILES=0,
 // through the wavefront kernels (A/B and parity of both paths).
+// k_tiles slices a box tile into its sample groups: one unit per group, the
+// group sums handed to the slice finishing last through a slab of one plane
+// (3 x 64 floats) per group.
+int film_groups(int spp) { return (spp + kFilmGroup - 1) / kFilmGroup; }
+size_t tile_slab_bytes(int spp, long tiles) {
+    const int ng = film_groups(spp);
+    return ng > 1 ? (size_t)192 * sizeof(float) * ng * (size_t)tiles : 0;
+}
+constexpr size_t kTileSlabMax = (size_t)16 << 30;
 bool tiles_enabled() {
     static const bool on = !(getenv("RR_TUNE_TILES") && atoi(getenv("RR_TUNE_TILES")) == 0);
     return on;
@@ -1745,7 +1853,7 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
-    counters.release(); spill.release(); segs.release(); hits.release(); qctr.release();
+    counters.release(); spill.release(); tile_slab.release(); film_part.release(); segs.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     trav_counts.release();
     prof.release();
@@ -1809,7 +1917,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         }
         const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
-        k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
+        k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, p.film_part.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
     }
@@ -1820,13 +1928,17 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     const int npix = base.npix;
     const size_t npaths = (size_t)npix * base.spp_chunk;
     const Grids G(base, p.count_traversal);
-    if (G.lds && base.n_tris > 0 && tiles_enabled() && !p.force_wavefront) {  // one launch: all samples of every tile
+    const long n_tiles = (long)((base.W + 7) / 8) * ((base.H + 7) / 8);
+    if (G.lds && base.n_tris > 0 && tiles_enabled() && !p.force_wavefront &&
+        tile_slab_bytes(base.spp_total, n_tiles) <= kTileSlabMax) {  // one launch: all samples of every tile
         p.ensure_tiles();
         p.film.ensure((size_t)npix);
         p.rgba8.ensure((size_t)npix * 4);
         const int cpc = counters_per_chunk(base.max_bounces);
-        p.counters.ensure((size_t)cpc * n_chunks);
-        RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
+        const long tiles = (long)((base.W + 7) / 8) * ((base.H + 7) / 8);
+        const size_t n_ctr = (size_t)cpc * n_chunks;
+        p.counters.ensure(n_ctr);
+        RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * n_ctr, st));
         unsigned long long* tc = nullptr;
         if (p.count_traversal) {
             p.trav_counts.ensure(6);
@@ -1839,17 +1951,25 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         fc.first_sample = 0;
         fc.spp_chunk = base.spp_total;
         uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr);
-        const long tiles = (long)((base.W + 7) / 8) * ((base.H + 7) / 8);
+        TileSlices sl{film_groups(base.spp_total), (size_t)192 * film_groups(base.spp_total), nullptr};
+        if (sl.n > 1) {
+            p.tile_slab.ensure(sl.floats * (size_t)tiles);
+            sl.slab = p.tile_slab.ptr;
+        }
         const int g = clamp_grid(tiles * 64, G.tiles);
         p.prof.begin(st, RR_K_TILES);
         G.kx<<<g, kBlock, G.dyn_primary, st>>>(fc, sa, tot + 2 * (base.max_bounces + 1), p.film.ptr, p.srgb_lut.ptr,
-                                               reinterpret_cast<uchar4*>(p.rgba8.ptr), tot, p.spill.ptr, tc);
+                                               reinterpret_cast<uchar4*>(p.rgba8.ptr), tot, p.spill.ptr, tc, sl);
+        if (sl.n > 1)
+            k_tiles_fold<<<(int)std::min<long>((tiles + kWavesPerBlock - 1) / kWavesPerBlock, 2048), kBlock, 0, st>>>(
+                fc, s.nodes.ptr, sl, p.film.ptr, p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         p.prof.end(st);
         RR_HIP(hipGetLastError());
         return;
     }
     p.ensure_paths(npaths);
     p.film.ensure((size_t)npix);
+    if (n_chunks > 1) p.film_part.ensure((size_t)npix);
     p.rgba8.ensure((size_t)npix * 4);
     const int cpc = counters_per_chunk(base.max_bounces);
     p.counters.ensure((size_t)cpc * n_chunks);
@@ -1916,7 +2036,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         }
         const int ga = clamp_grid(npix, accum_grid());
         pr.begin(st, RR_K_ACCUM);
-        k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
+        k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, p.film_part.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
     }

@@ -975,6 +975,8 @@ int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* h
  * film: W*H*4 floats of mean radiance; rgba8: W*H*4 bytes. Rows
  * [row_begin, row_end) only (row_end <= 0: all rows), so a bounded sample of a
  * frame can be timed. threads <= 0: OpenMP default. */
+#define ORC_FILM_GROUP 32
+
 int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const float* cam, int n_lights,
                const float* lights, const float* mats, const float* world, const int32_t* ri, const float* rf,
                float* film, uint8_t* rgba8, int row_begin, int row_end, int threads) {
@@ -1012,12 +1014,21 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     for (int y = row_begin; y < row_end; ++y) {
         for (int x = 0; x < S->W; ++x) {
             int pix = y * S->W + x;
+            /* film sum order (the product's kFilmGroup, csrc/wavefront.hip): in
+             * order within groups of ORC_FILM_GROUP samples, group sums in order */
             v3 acc = V(0.0f, 0.0f, 0.0f);
-            for (int s = 0; s < S->spp; ++s) {
-                v3 L = radiance(S, pix, s);
-                acc.x = acc.x + L.x;
-                acc.y = acc.y + L.y;
-                acc.z = acc.z + L.z;
+            for (int g0 = 0; g0 < S->spp; g0 += ORC_FILM_GROUP) {
+                v3 P = V(0.0f, 0.0f, 0.0f);
+                const int g1 = g0 + ORC_FILM_GROUP < S->spp ? g0 + ORC_FILM_GROUP : S->spp;
+                for (int s = g0; s < g1; ++s) {
+                    v3 L = radiance(S, pix, s);
+                    P.x = P.x + L.x;
+                    P.y = P.y + L.y;
+                    P.z = P.z + L.z;
+                }
+                acc.x = acc.x + P.x;
+                acc.y = acc.y + P.y;
+                acc.z = acc.z + P.z;
             }
             if (film) {
                 film[4 * (size_t)pix] = acc.x * inv_spp;

@@ -140,7 +140,10 @@ PATHS = {"tiles": 0, "wavefront": 4}
 
 @pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("frame,w,h,spp,chunk", [(1, 160, 90, 16, 0), (30, 96, 54, 8, 3), (60, 64, 36, 5, 1),
-                                                 (600, 33, 17, 7, 2), (30, 1, 1, 9, 0), (45, 7, 130, 3, 0)])
+                                                 (600, 33, 17, 7, 2), (30, 1, 1, 9, 0), (45, 7, 130, 3, 0),
+                                                 # > kFilmGroup (32) samples: grouped film sum, k_tiles
+                                                 # sample-group slices, groups straddling chunks
+                                                 (5, 40, 24, 72, 20), (10, 48, 32, 128, 0), (20, 24, 16, 65, 7)])
 def test_full_frame_bit_exact(ctx, rr, s04, frame, w, h, spp, chunk, path):
     p = rr.default_params(width=w, height=h, spp=spp, spp_per_chunk=chunk, flags=PATHS[path])
     film, rgba, stats = ctx.render_to_memory(s04, frame, p)
@@ -163,6 +166,9 @@ def test_tiles_equal_wavefront_full_resolution(ctx, rr, s04):
         film, rgba, st = ctx.render_to_memory(s04, 30, p)
         out[path] = (film, rgba, st.extension_rays, st.shadow_rays, st.primary_continued, st.primary_shadow)
     a, b = out["tiles"], out["wavefront"]
+    # 40 samples: two film groups, k_tiles' box tiles in two slices
+    f40 = [ctx.render_to_memory(s04, 7, rr.default_params(spp=40, flags=flags))[0] for flags in PATHS.values()]
+    assert np.array_equal(f40[0], f40[1]), f"{np.count_nonzero(f40[0] != f40[1])} film mismatches at 40 spp"
     assert a[0].shape == (1080, 1920, 4)
     assert np.array_equal(a[0], b[0]), f"{np.count_nonzero(a[0] != b[0])} film mismatches"
     assert np.array_equal(a[1], b[1])
