@@ -45,6 +45,12 @@ WORKLOADS = {
              "workload": "04vs-standin, 1 frame per step: 1920x1080, 128 spp, max 12 bounces, "
                          "LBVH rebuild + path trace (k_tiles: every sample of an 8x8 tile in one wave) + "
                          "JPEG q90 encode/write"},
+    "01": {"job": os.path.join(ROOT, "jobs", "01_simple-animation_600f-8w_dynamic.toml"),
+           "metric": "job frames/sec at 1/2/4/8 MI355X (01_simple-animation)", "steps": 40, "warmup": 4,
+           "data": "01_simple-animation.rrscene exported from the reference's .blend (Filmic rendered as "
+                   "Standard: no OCIO LUTs in the image), frames of the 600-frame job, JPEG q90 written per frame",
+           "workload": "01-simple-animation, 1 frame per step: 1920x1080, 128 spp, max 12 bounces, "
+                       "LBVH rebuild + path trace (k_tiles) + JPEG q90 encode/write"},
     "02": {"job": os.path.join(ROOT, "jobs", "02_physics-standin_170f-5w_naive-fine.toml"),
            "metric": "job frames/sec at 1/2/4/8 MI355X (02_physics stand-in)", "steps": 10, "warmup": 2,
            "data": "synthetic: 02_physics stand-in (2,000 closed-form rigid bodies, 92,002 triangles; the 02 .blend "

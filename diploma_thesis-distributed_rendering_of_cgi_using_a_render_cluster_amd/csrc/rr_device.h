@@ -771,6 +771,9 @@ RR_HD float3 sample_vndf(float3 v, float alpha, float dx, float dy) {
     return norm3(mk3(alpha * nh.x, alpha * nh.y, fmaxf(0.0f, nh.z)));
 }
 
+#ifndef RR_EXP_NOSPEC
+#define RR_EXP_NOSPEC 0  // timing experiment (wrong images): 1 = never sample the specular lobe
+#endif
 // Sample a direction; returns false when the path must end.
 RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, float ul, float u1, float u2,
                        float3& wi, float3& f, float& pdf) {
@@ -781,7 +784,7 @@ RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, fl
     make_onb(N, T, B);
     float x, y;  // the disk sample both lobes start from
     concentric_disk(u1, u2, x, y);
-    if (ul < ps) {
+    if (RR_EXP_NOSPEC == 0 && ul < ps) {
         const float3 wl = mk3(dot3(wo, T), dot3(wo, B), cosV);
         const float3 hl = sample_vndf(wl, m.alpha, x, y);
         const float3 H = mk3(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,

@@ -190,6 +190,9 @@ RR_D void add_to(float3& L, float3 c) {
     L.z = L.z + c.z;
 }
 
+#ifndef RR_EXP_SHADE
+#define RR_EXP_SHADE 0  // timing experiments (wrong images): 1 no NEE, 2 no continuation
+#endif
 // K9: shade one path at `bounce` given its closest hit; L updated in place.
 template <typename View>
 __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const View& v, float3 o, float3 d,
@@ -223,7 +226,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     const uint32_t dim0 = 2u + (uint32_t)(kDimsPerBounce * bounce);
     const float3 Po = offset_ray(P, N);
     // next-event estimation toward one uniformly chosen light
-    if (fc.n_lights > 0) {
+    if (RR_EXP_SHADE != 1 && fc.n_lights > 0) {
         int li = (int)(rng(key, dim0) * (float)fc.n_lights);
         if (li > fc.n_lights - 1) li = fc.n_lights - 1;
         const auto lt = v.lights + kLightF * li;
@@ -278,6 +281,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         }
     }
     // continue the path
+    if (RR_EXP_SHADE == 2) return;
     float3 wi, f;
     float pdf;
     if (!bsdf_sample(m, vw, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f, pdf))
