@@ -11,7 +11,7 @@ for p in "" _02 _c5; do
     cp $d/${tag}${p}_pmc.json profiles/${tag}_pmc${p}.json
     grep '^{' $d/trace_bench.json > profiles/${tag}${p}_bench_under_rocprof.json
 done
-for wl in 04vs 02 03 c5 04vs_serial; do
+for wl in 04vs 01 02 03 c5 04vs_serial; do
     grep '^{' gpurun_out/ev/bench_$wl.json > profiles/${tag}_bench_$wl.json
 done
 grep -v '^===' gpurun_out/ev/smoke.log > profiles/${tag}_smoke.log

@@ -13,7 +13,7 @@ $S 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thr
 cp gpurun_out/prof_$tag/${tag}_pmc.json profiles/r1_pmc.json
 cp gpurun_out/prof_${tag}_02/${tag}_02_pmc.json profiles/r1_pmc_02.json
 cp gpurun_out/prof_${tag}_c5/${tag}_c5_pmc.json profiles/r1_pmc_c5.json
-for wl in 04vs 02 03 c5; do
+for wl in 04vs 01 02 03 c5; do
     $S 600 python bench.py --workload $wl > gpurun_out/ev/bench_$wl.json || exit $?
 done
 $S 200 python bench.py --serial --no-cpu-baseline > gpurun_out/ev/bench_04vs_serial.json
