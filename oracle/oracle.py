@@ -40,6 +40,8 @@ def lib():
         L.orc_rng.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, c_int, f]
         L.orc_disk.argtypes = [c_int, f, f]
         L.orc_bsdf_eval.argtypes = [f, f, f, f, f, f]
+        L.orc_bsdf_eval_n.argtypes = [f, f, f, c_int, f, f, f]
+        L.orc_bsdf_sample.argtypes = [f, f, f, c_int, f, f, f, f, i32]
         L.orc_filter_table.argtypes = [ctypes.c_float, f]
         L.orc_srgb_lut.argtypes = [f]
         _lib = L
@@ -147,6 +149,29 @@ def bsdf_eval(mat12, n, wo, wi):
     lib().orc_bsdf_eval(_p(m, ctypes.c_float), _p(n, ctypes.c_float), _p(wo, ctypes.c_float),
                         _p(wi, ctypes.c_float), _p(f3, ctypes.c_float), _p(pdf, ctypes.c_float))
     return f3, float(pdf[0])
+
+
+def bsdf_sample(mat12, n, wo, u):
+    """sample_bsdf at one shading point for each row (ul, u1, u2) of u:
+    (wi [k,3], f [k,3], pdf [k], ok [k] bool)."""
+    m, n, wo, u = _f32(mat12), _f32(n), _f32(wo), _f32(u).reshape(-1, 3)
+    k = u.shape[0]
+    wi, f = np.zeros((k, 3), np.float32), np.zeros((k, 3), np.float32)
+    pdf, ok = np.zeros(k, np.float32), np.zeros(k, np.int32)
+    lib().orc_bsdf_sample(_p(m, ctypes.c_float), _p(n, ctypes.c_float), _p(wo, ctypes.c_float), k,
+                          _p(u, ctypes.c_float), _p(wi, ctypes.c_float), _p(f, ctypes.c_float),
+                          _p(pdf, ctypes.c_float), _p(ok, ctypes.c_int32))
+    return wi, f, pdf, ok.astype(bool)
+
+
+def bsdf_eval_n(mat12, n, wo, wi):
+    """eval_bsdf at one shading point for each row of wi: (f [k,3], pdf [k])."""
+    m, n, wo, wi = _f32(mat12), _f32(n), _f32(wo), _f32(wi).reshape(-1, 3)
+    k = wi.shape[0]
+    f, pdf = np.zeros((k, 3), np.float32), np.zeros(k, np.float32)
+    lib().orc_bsdf_eval_n(_p(m, ctypes.c_float), _p(n, ctypes.c_float), _p(wo, ctypes.c_float), k,
+                          _p(wi, ctypes.c_float), _p(f, ctypes.c_float), _p(pdf, ctypes.c_float))
+    return f, pdf
 
 
 def filter_table(width: float) -> np.ndarray:

@@ -1062,6 +1062,35 @@ void orc_disk(int n, const float* u, float* xy) {
     for (int i = 0; i < n; ++i) disk(u[2 * i], u[2 * i + 1], &xy[2 * i], &xy[2 * i + 1]);
 }
 
+/* BSDF sampling for the estimator tests (tests/test_oracle.py): n draws of
+ * sample_bsdf at one shading point, u = n x (ul, u1, u2) -> wi (3), f (3),
+ * pdf and ok per draw (ok = 0: the path ends, as in radiance()). */
+void orc_bsdf_sample(const float* mat12, const float* n3, const float* wo3, int n, const float* u, float* wi3,
+                     float* f3, float* pdf, int32_t* ok) {
+    mat_t m = load_mat(mat12, 0);
+    v3 N = V(n3[0], n3[1], n3[2]), wo = V(wo3[0], wo3[1], wo3[2]);
+    for (int i = 0; i < n; ++i) {
+        v3 wi = V(0.0f, 0.0f, 0.0f), f = wi;
+        float p = 0.0f;
+        ok[i] = sample_bsdf(&m, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], &wi, &f, &p);
+        wi3[3 * i] = wi.x; wi3[3 * i + 1] = wi.y; wi3[3 * i + 2] = wi.z;
+        f3[3 * i] = f.x; f3[3 * i + 1] = f.y; f3[3 * i + 2] = f.z;
+        pdf[i] = p;
+    }
+}
+
+/* Batched BSDF eval at one shading point (estimator tests): n directions wi. */
+void orc_bsdf_eval_n(const float* mat12, const float* n3, const float* wo3, int n, const float* wi3, float* f3,
+                     float* pdf) {
+    mat_t m = load_mat(mat12, 0);
+    v3 N = V(n3[0], n3[1], n3[2]), wo = V(wo3[0], wo3[1], wo3[2]);
+    float ps = p_spec(&m, vdot(N, wo));
+    for (int i = 0; i < n; ++i) {
+        v3 f = eval_bsdf(&m, N, wo, V(wi3[3 * i], wi3[3 * i + 1], wi3[3 * i + 2]), ps, &pdf[i]);
+        f3[3 * i] = f.x; f3[3 * i + 1] = f.y; f3[3 * i + 2] = f.z;
+    }
+}
+
 /* BSDF eval for known-answer tests: mat12, N, wo, wi -> f (3), pdf. */
 void orc_bsdf_eval(const float* mat12, const float* n3, const float* wo3, const float* wi3, float* f3, float* pdf) {
     mat_t m = load_mat(mat12, 0);

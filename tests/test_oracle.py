@@ -145,6 +145,37 @@ def test_lambert_and_principled_bsdf():
     assert np.all(f3 == 0) and p3 == 0
 
 
+@pytest.mark.parametrize("cos_v", [0.95, 0.6, 0.2])
+@pytest.mark.parametrize("roughness,metallic", [(0.5, 0.0), (0.3, 1.0)])
+def test_principled_sampling_matches_evaluation(cos_v, roughness, metallic):
+    """The lobe sampler and the BSDF's pdf agree (what makes the path estimator
+    unbiased): E[f cos / pdf] over sample_bsdf draws equals a quadrature of
+    the same integral over the hemisphere (the directional albedo), and the
+    pdf integrates over the hemisphere to the fraction of draws that continue."""
+    mat = [0.8, 0.7, 0.6, metallic, 0.5, roughness, 1.45, 0, 0, 0, 0.0, 0]
+    n = [0.0, 0.0, 1.0]
+    wo = [math.sqrt(1.0 - cos_v * cos_v), 0.0, cos_v]
+    k = 400_000
+    g = np.random.default_rng(11)
+    wi, f, pdf, ok = O.bsdf_sample(mat, n, wo, g.random((k, 3), dtype=np.float32))
+    assert np.all(pdf[ok] > 0) and np.all(wi[ok, 2] > 0)
+    w = np.where(ok, wi[:, 2] / np.where(ok, pdf, 1.0), 0.0)
+    est_is = (f * w[:, None]).mean(0)
+    # midpoint quadrature over the hemisphere in (z = cos theta, phi): dω = dz dphi
+    nz, nphi = 2048, 512
+    z = (np.arange(nz) + 0.5) / nz
+    phi = (np.arange(nphi) + 0.5) * (2.0 * math.pi / nphi)
+    zz, pp = np.meshgrid(z, phi, indexing="ij")
+    r = np.sqrt(1.0 - zz * zz)
+    wu = np.stack([r * np.cos(pp), r * np.sin(pp), zz], -1).reshape(-1, 3)
+    fu, pu = O.bsdf_eval_n(mat, n, wo, wu)
+    dw = (1.0 / nz) * (2.0 * math.pi / nphi)
+    est_q = (fu.astype(np.float64) * (zz.reshape(-1) * dw)[:, None]).sum(0)
+    np.testing.assert_allclose(est_is, est_q, rtol=0.02)
+    assert 0.05 < est_is.min() and est_is.max() < 1.0          # energy: albedo below 1
+    assert float(pu.astype(np.float64).sum() * dw) == pytest.approx(float(ok.mean()), rel=0.01)
+
+
 def _render_scene(name, frame=1, **over):
     """Oracle render from the Python restatement (no product code involved)."""
     scene = HO.load_scene(scene_path(name))
