@@ -446,8 +446,15 @@ RR_D void lds_copy(lds_f4w* dst, const float4* __restrict__ src, int n4) {
 // the triangle's screen rectangle (tri_screen_rect) bins it to the 8x8 tiles
 // whose samples can hit it.
 //   [3i] = (tv, tn), [3i+1] = (qv, 0), [3i+2] = (x0, x1, y0, y1)
-RR_D void tri_screen_rect(const FrameConsts& fc, const float3 p[3], float r[4]) {
+// Screen rectangle of a triangle (pixels, one pixel of slack) and its three
+// edge lines e[k] = (nx, ny, c): nx*x + ny*y + c >= 0 inside, |n| = 1, so the
+// value is a signed distance in pixels. A triangle at or behind the camera
+// plane, or degenerate on screen, keeps the unbounded rectangle / edges that
+// every point satisfies.
+RR_D void tri_screen_rect(const FrameConsts& fc, const float3 p[3], float r[4], float e[3][3]) {
     float x0 = kFltMax, x1 = -kFltMax, y0 = kFltMax, y1 = -kFltMax;
+    float fx[3], fy[3];
+    for (int k = 0; k < 3; ++k) e[k][0] = e[k][1] = 0.0f, e[k][2] = 1.0f;
     for (int k = 0; k < 3; ++k) {
         const float3 v = sub3(p[k], fc.cam_pos);
         const float depth = -dot3(v, fc.cam_back);
@@ -458,19 +465,35 @@ RR_D void tri_screen_rect(const FrameConsts& fc, const float3 p[3], float r[4]) 
         }
         const float sx = dot3(v, fc.cam_right) / depth;
         const float sy = dot3(v, fc.cam_up) / depth;
-        const float fx = (sx / fc.half_w + 1.0f) * ((float)fc.W * 0.5f);
-        const float fy = (1.0f - sy / fc.half_h) * ((float)fc.H * 0.5f);
-        x0 = fminf(x0, fx);
-        x1 = fmaxf(x1, fx);
-        y0 = fminf(y0, fy);
-        y1 = fmaxf(y1, fy);
+        fx[k] = (sx / fc.half_w + 1.0f) * ((float)fc.W * 0.5f);
+        fy[k] = (1.0f - sy / fc.half_h) * ((float)fc.H * 0.5f);
+        x0 = fminf(x0, fx[k]);
+        x1 = fmaxf(x1, fx[k]);
+        y0 = fminf(y0, fy[k]);
+        y1 = fmaxf(y1, fy[k]);
     }
     r[0] = x0 - 1.0f;  // a pixel of slack covers rounding, as screen_rect's
     r[1] = x1 + 1.0f;
     r[2] = y0 - 1.0f;
     r[3] = y1 + 1.0f;
+    const float area = (fx[1] - fx[0]) * (fy[2] - fy[0]) - (fy[1] - fy[0]) * (fx[2] - fx[0]);
+    if (!(fabsf(area) > 1.0e-3f)) return;  // (near-)degenerate on screen: edges stay open
+    const float sgn = area > 0.0f ? 1.0f : -1.0f;
+    for (int k = 0; k < 3; ++k) {
+        const int a = k, b = (k + 1) % 3;
+        float nx = -(fy[b] - fy[a]) * sgn, ny = (fx[b] - fx[a]) * sgn;  // towards the third vertex
+        const float len = sqrtf(nx * nx + ny * ny);
+        nx = nx / len;
+        ny = ny / len;
+        e[k][0] = nx;
+        e[k][1] = ny;
+        e[k][2] = -(nx * fx[a] + ny * fy[a]);
+    }
 }
 
+// Camera-ray data per triangle in LDS: the origin terms of the triangle test
+// (2 float4), the screen rectangle, the three screen edge lines.
+constexpr int kCamF4 = 6;
 RR_D void stage_camera(lds_f4w* q, lds_tri* tris, int n_tris, const FrameConsts& fc) {
     for (int i = threadIdx.x; i < n_tris; i += kBlock) {
         const TriPack tp = load_tri(tris, i);
@@ -479,15 +502,20 @@ RR_D void stage_camera(lds_f4w* q, lds_tri* tris, int n_tris, const FrameConsts&
         const float3 qv = cross3(tv, e1);
         const float tn = dot3(e2, qv);
         const float3 pts[3] = {v0, add3(v0, e1), add3(v0, e2)};
-        float r[4];
-        tri_screen_rect(fc, pts, r);
+        float r[4], e[3][3];
+        tri_screen_rect(fc, pts, r, e);
         rr_f4v a, b, c;
         a.x = tv.x; a.y = tv.y; a.z = tv.z; a.w = tn;
         b.x = qv.x; b.y = qv.y; b.z = qv.z; b.w = 0.0f;
         c.x = r[0]; c.y = r[1]; c.z = r[2]; c.w = r[3];
-        q[3 * i] = a;
-        q[3 * i + 1] = b;
-        q[3 * i + 2] = c;
+        q[kCamF4 * i] = a;
+        q[kCamF4 * i + 1] = b;
+        q[kCamF4 * i + 2] = c;
+        for (int k = 0; k < 3; ++k) {
+            rr_f4v l;
+            l.x = e[k][0]; l.y = e[k][1]; l.z = e[k][2]; l.w = 0.0f;
+            q[kCamF4 * i + 3 + k] = l;
+        }
     }
 }
 
@@ -529,7 +557,7 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
     if (cam_fc) {
         v.cam = q;
         stage_camera(q, v.tris, a.n_tris, *cam_fc);
-        q += 3 * a.n_tris;
+        q += kCamF4 * a.n_tris;
     }
     used = (int)(q - base);
     __syncthreads();
@@ -560,7 +588,7 @@ RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float
             m &= m - 1;
             if (kCount) ++cnt.tris;
             const TriPack tp = load_tri(v.tris, i);
-            const float4 ca = lds_ld4(v.cam + 3 * i), cb = lds_ld4(v.cam + 3 * i + 1);
+            const float4 ca = lds_ld4(v.cam + kCamF4 * i), cb = lds_ld4(v.cam + kCamF4 * i + 1);
             const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2), tv = xyz(ca), qv = xyz(cb);
             const float3 pv = cross3(d, e2);
             const float det = dot3(e1, pv);
@@ -591,8 +619,13 @@ RR_D void tile_mask(const FrameConsts& fc, const LdsView& v, int n_tris, float x
     const float X0 = x0 + 0.5f - r, X1 = x1 + 0.5f + r, Y0 = y0 + 0.5f - r, Y1 = y1 + 0.5f + r;
     uint64_t a = 0, b = 0;
     for (int i = 0; i < n_tris; ++i) {
-        const float4 q = lds_ld4(v.cam + 3 * i + 2);
-        const bool in = !(q.y < X0 || q.x > X1 || q.w < Y0 || q.z > Y1);
+        const float4 q = lds_ld4(v.cam + kCamF4 * i + 2);
+        bool in = !(q.y < X0 || q.x > X1 || q.w < Y0 || q.z > Y1);
+        for (int k = 0; k < 3 && in; ++k) {  // the expanded tile wholly outside an edge (+1 px of slack)
+            const float4 l = lds_ld4(v.cam + kCamF4 * i + 3 + k);
+            const float m = l.x * (l.x > 0.0f ? X1 : X0) + l.y * (l.y > 0.0f ? Y1 : Y0) + l.z;
+            in = m >= -1.0f;
+        }
         if (in) {
             if (i < 64) a |= 1ull << i;
             else b |= 1ull << (i - 64);
@@ -1778,7 +1811,7 @@ struct Grids {
         kt = lds ? (count ? k_tail<true, true> : k_tail<false, true>)
                  : (count ? k_tail<true, false> : k_tail<false, false>);
         const size_t sp = lds ? scene_lds_bytes(fc, true) : 0, ss = lds ? scene_lds_bytes(fc, false) : 0;
-        dyn_primary = sp + (lds ? 48 * (size_t)fc.n_tris : 0);  // + stage_camera's 3 float4 per triangle
+        dyn_primary = sp + (lds ? 16 * kCamF4 * (size_t)fc.n_tris : 0);  // + stage_camera's float4s per triangle
         primary = grid_for(kp, dyn_primary);
         // consumers hold the producer's segment prefix after the scene: one word
         // per producer block + 1; more LDS can only shrink k_extend's grid, so
