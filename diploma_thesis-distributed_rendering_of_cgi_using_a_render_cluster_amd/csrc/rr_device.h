@@ -370,8 +370,11 @@ RR_D TriPack load_tri(lds_tri* p, int i) {
     return t;
 }
 struct TravStack {
-    lds_int* lds;   // &lds_base[threadIdx.x], stride kBlock
-    int* spill;     // &spill_base[global thread], stride spill_stride
+    // Bases only: the lane's slots are recomputed from threadIdx/blockIdx at each
+    // push/pop, so no per-lane pointer stays live in VGPRs across a kernel's
+    // ray loop (every kernel launches kBlock threads per block).
+    lds_int* lds;   // lds_base: lane slot lds[sp * kBlock + threadIdx.x]
+    int* spill;     // spill_base: lane slot spill[(sp - kLdsStack) * stride + global thread]
     int spill_stride;
     int sp;
     // A push beyond kLdsStack + kSpillStack entries is dropped (never reached
@@ -379,9 +382,9 @@ struct TravStack {
     // has the same capacity and the same rule (ORC_MAXDEPTH).
     RR_D void push(int x) {
         if (sp < kLdsStack) {
-            lds[sp * kBlock] = x;
+            lds[sp * kBlock + (int)threadIdx.x] = x;
         } else if (sp < kLdsStack + kSpillStack) {
-            spill[(sp - kLdsStack) * spill_stride] = x;
+            spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kBlock + threadIdx.x)] = x;
         } else {
             return;
         }
@@ -389,8 +392,8 @@ struct TravStack {
     }
     RR_D int pop() {
         --sp;
-        if (sp < kLdsStack) return lds[sp * kBlock];
-        return spill[(sp - kLdsStack) * spill_stride];
+        if (sp < kLdsStack) return lds[sp * kBlock + (int)threadIdx.x];
+        return spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kBlock + threadIdx.x)];
     }
 };
 

@@ -644,9 +644,8 @@ template <bool kCount, typename View>
 RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, PathQueue out,
                        ShadowQueue sq, uint32_t seg_cap, uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
                        int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill + gtid, stride, 0};
+    TravStack st{stack, spill, stride, 0};
     TravCount cnt;
     SegCursor cur;
     const uint32_t seg_base = wave_id() * seg_cap;
@@ -699,7 +698,7 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_primary(FrameConsts 
                                                     int32_t* __restrict__ spill,
                                                     unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
-    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    lds_int* stack = lds_slot(lds_stack);
     if constexpr (kLds) {
         extern __shared__ float4 dyn4[];
         int used;
@@ -728,9 +727,8 @@ template <bool kCount, typename View>
 RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueue in, const SegIndex& ix, int count,
                       Rad rad, PathQueue out, ShadowQueue sq, const SegOut& so_seg,
                       int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill + gtid, stride, 0};
+    TravStack st{stack, spill, stride, 0};
     TravCount cnt;
     SegCursor cur;
     const uint32_t seg_base = wave_id() * so_seg.cap;
@@ -766,7 +764,7 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_extend(FrameConsts f
                                                    unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     extern __shared__ float4 dyn4[];
-    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    lds_int* stack = lds_slot(lds_stack);
     int used = 0;
     LdsView lv;
     if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, true, used);
@@ -799,9 +797,8 @@ template <bool kCount, typename View>
 RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue in, const SegIndex& ix, int count,
                     Rad rad, uint32_t* __restrict__ tot, int32_t* __restrict__ spill,
                     unsigned long long* __restrict__ tc, lds_int* stack) {
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill + gtid, stride, 0};
+    TravStack st{stack, spill, stride, 0};
     TravCount cc, cs;
     for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
         const int j = b0 + (int)threadIdx.x;
@@ -864,7 +861,7 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_tail(FrameConsts fc,
                                                                  unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     extern __shared__ float4 dyn4[];
-    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    lds_int* stack = lds_slot(lds_stack);
     int used = 0;
     LdsView lv;
     if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, true, used);
@@ -883,7 +880,7 @@ RR_D void shadow_body(NodeP nodes, TriP tris, int n_tris, ShadowQueue sq, const 
                       lds_int* stack) {
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill + gtid, stride, 0};
+    TravStack st{stack, spill, stride, 0};
     TravCount cnt;
     for (int j = gtid; j < count; j += stride) {
         const uint32_t i = ix.slot((uint32_t)j);
@@ -907,7 +904,7 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
                                                    int32_t* __restrict__ spill, unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     extern __shared__ float4 dyn4[];
-    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    lds_int* stack = lds_slot(lds_stack);
     int used = 0;
     LdsView lv;
     if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, false, used);
@@ -1098,8 +1095,7 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameC
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
-    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
+    TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     trace_refill<SplitTrav<false, kCount>>(
@@ -1151,8 +1147,7 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_extend(SceneAr
     __shared__ int lds_stack[kLdsStack * kBlock];
     QueueMap qm;
     qm.init(qi);
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
-    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
+    TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
         split_nodes(sa), sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
@@ -1207,8 +1202,7 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_shadow_refill(SceneA
     __shared__ int lds_stack[kLdsStack * kBlock];
     QueueMap qm;
     qm.init(qi);
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
-    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, (int)(gridDim.x * kBlock), 0};
+    TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
         split_nodes(sa), sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
@@ -1383,13 +1377,17 @@ RR_D bool tile_culled(const FrameConsts& fc, const ScreenCull& sc, int tx, int t
 // the chunk-0 counter pairs: {0, 1} = bounce 0, {2, 3} = all later bounces
 // (rr_api.cpp fill_stats sums the pairs).
 RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint32_t c1, uint32_t s1) {
-    uint32_t v[4] = {c0, s0, c1, s1};
-    for (int k = 0; k < 4; ++k) {
-        uint32_t a = v[k];
-        for (int off = 32; off > 0; off >>= 1) a += (uint32_t)__shfl_xor((int)a, off);
-        if ((threadIdx.x & 63) == 0 && a) atomicAdd(&tot[k], a);
-    }
+    // the counts are wave totals already (wave_count): lane 0 adds them
+    const uint32_t v[4] = {c0, s0, c1, s1};
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 4; ++k)
+            if (v[k]) atomicAdd(&tot[k], v[k]);
 }
+
+// Active lanes of the wave whose predicate holds: the tile kernel's ray
+// counters are wave totals kept in scalar registers (no per-lane VGPRs live
+// across the unit loop).
+RR_D uint32_t wave_count(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
 // Sample-group slices of the box tiles (load balance: a heavy tile does not
 // run as one wave's unit at the end of the launch). Slab of tile t: one plane
@@ -1408,9 +1406,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                      const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
                      const TileSlices sl) {
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill + gtid, stride, 0};
+    TravStack st{stack, spill, stride, 0};
     TravCount cp, ce, cs;
     uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0;
     const ScreenCull cull = screen_cull(fc, v.nodes);
@@ -1483,8 +1480,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
 #else
                 shade(fc, 0, v, o, d, T, h, key, L, so);
 #endif
-                n_c0 += so.cont ? 1u : 0u;
-                n_s0 += so.shadow ? 1u : 0u;
+                n_c0 += wave_count(so.cont);
+                n_s0 += wave_count(so.shadow);
             }
             if (so.shadow) {
                 Hit hs;
@@ -1512,8 +1509,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                                                     0.0f, sb.sdist, st, hs, cs))
                             add_to(L, sb.sc);
                     }
-                    n_c1 += sb.cont ? 1u : 0u;
-                    n_s1 += sb.shadow ? 1u : 0u;
+                    n_c1 += wave_count(sb.cont);
+                    n_s1 += wave_count(sb.shadow);
                     if (sb.cont) {
                         o = sb.o;
                         d = sb.d;
@@ -1557,11 +1554,11 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                             add_to(L, so.sc);
                     }
                     if (b == 0) {
-                        n_c0 += so.cont ? 1u : 0u;
-                        n_s0 += so.shadow ? 1u : 0u;
+                        n_c0 += wave_count(so.cont);
+                        n_s0 += wave_count(so.shadow);
                     } else {
-                        n_c1 += so.cont ? 1u : 0u;
-                        n_s1 += so.shadow ? 1u : 0u;
+                        n_c1 += wave_count(so.cont);
+                        n_s1 += wave_count(so.shadow);
                     }
                     if (so.cont) {
                         o = so.o;
@@ -1611,7 +1608,7 @@ __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc
                                                                   TileSlices sl) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     extern __shared__ float4 dyn4[];
-    lds_int* stack = lds_slot(&lds_stack[threadIdx.x]);
+    lds_int* stack = lds_slot(lds_stack);
     int used;
     const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used, &fc);
     tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl);
@@ -1654,7 +1651,7 @@ __global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* 
     __shared__ int lds_stack[kLdsStack * kBlock];
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int nthreads = gridDim.x * kBlock;
-    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, nthreads, 0};
+    TravStack st{lds_slot(lds_stack), spill, nthreads, 0};
     TravCount cnt;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
@@ -1674,7 +1671,7 @@ __global__ void k_debug_trace4(const Bvh4Node* __restrict__ nodes, const TriPack
     __shared__ int lds_stack[kLdsStack * kBlock];
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int nthreads = gridDim.x * kBlock;
-    TravStack st{lds_slot(&lds_stack[threadIdx.x]), spill + gtid, nthreads, 0};
+    TravStack st{lds_slot(lds_stack), spill, nthreads, 0};
     TravCount cnt;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
