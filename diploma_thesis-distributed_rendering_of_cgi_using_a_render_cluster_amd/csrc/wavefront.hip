@@ -34,6 +34,12 @@
 
 #include "device.hpp"
 
+#if RR_TILES_TU  // tiles.hip builds only k_tiles from this file: the other kernels go unused there
+#pragma clang diagnostic ignored "-Wunused-function"
+#else            // and k_tiles' helpers go unused here
+#pragma clang diagnostic ignored "-Wunneeded-internal-declaration"
+#endif
+
 namespace rr {
 
 namespace {
@@ -419,6 +425,7 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
 
 // K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
 // Scene data as kernel arguments (global pointers + counts).
+}  // namespace
 struct SceneArgs {
     const BvhNode* nodes;
     const Bvh4Node* nodes4;  // split path (large scenes)
@@ -429,6 +436,7 @@ struct SceneArgs {
     int n_nodes, n_tris, n_mats, n_lights;
 };
 
+namespace {
 RR_D GlobalView global_view(const SceneArgs& a) { return {a.nodes, a.tris, a.mats, a.lights, a.filter}; }
 
 RR_D void lds_copy(lds_f4w* dst, const float4* __restrict__ src, int n4) {
@@ -1395,11 +1403,18 @@ RR_D uint32_t wave_count(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 // group order by k_tiles_fold after the launch. (An in-launch hand-off — sc1
 // stores, a ticket per tile, the last slice folding — measured 0.5 ms slower
 // per 04vs frame than this second launch.)
+}  // namespace
 struct TileSlices {
     int n;             // slices per box tile = sample groups (1: no slicing)
     size_t floats;     // slab floats per tile: 192 * groups
     float* slab;
 };
+using TilesFn = void (*)(FrameConsts, SceneArgs, uint32_t*, float4*, const float*, uchar4*, uint32_t*, int32_t*,
+                         unsigned long long*, TileSlices);
+// k_tiles<count> of tiles.hip: this file compiled again with RR_TILES_TU and
+// without SLP vectorisation (see the Makefile).
+TilesFn tiles_kernel(bool count);
+namespace {
 
 template <bool kCount>
 RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
@@ -1594,6 +1609,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     }
 }
 
+#if RR_TILES_TU
 #ifndef RR_TILES_WAVES
 #define RR_TILES_WAVES 4  // waves per SIMD the register budget must admit (<= 128 VGPRs)
 #endif
@@ -1613,6 +1629,8 @@ __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc
     const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used, &fc);
     tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl);
 }
+
+#endif  // RR_TILES_TU
 
 // Film of the sliced tiles: the group sums of each box tile that is not
 // culled, added in group order (the same box and culling test as k_tiles,
@@ -1695,6 +1713,9 @@ __global__ void k_debug_trace4(const Bvh4Node* __restrict__ nodes, const TriPack
 
 }  // namespace
 
+#if RR_TILES_TU
+TilesFn tiles_kernel(bool count) { return count ? k_tiles<true> : k_tiles<false>; }
+#else
 int device_cu_count() {
     static int cus = 0;
     if (!cus) {
@@ -1719,8 +1740,6 @@ using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, Pa
 using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, Rad, int32_t*, unsigned long long*);
 using TailFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, uint32_t*, int32_t*,
                         unsigned long long*);
-using TilesFn = void (*)(FrameConsts, SceneArgs, uint32_t*, float4*, const float*, uchar4*, uint32_t*, int32_t*,
-                         unsigned long long*, TileSlices);
 // LDS-resident scenes render through k_tiles (default) or, with RR_TUNE_TILES=0,
 // through the wavefront kernels (A/B and parity of both paths).
 // k_tiles slices a box tile into its sample groups: one unit per group, the
@@ -1819,7 +1838,7 @@ struct Grids {
         extend = grid_for(ke, dyn_extend);
         shadow = grid_for(ks, dyn_shadow);
         tail = grid_for(kt, dyn_extend);
-        kx = count ? k_tiles<true> : k_tiles<false>;
+        kx = tiles_kernel(count);
         tiles = lds ? grid_for(kx, dyn_primary) : 0;
     }
 };
@@ -2092,4 +2111,5 @@ void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, f
     RR_HIP(hipGetLastError());
 }
 
+#endif  // RR_TILES_TU
 }  // namespace rr
