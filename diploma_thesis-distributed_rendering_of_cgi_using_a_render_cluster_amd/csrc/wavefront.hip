@@ -1381,6 +1381,23 @@ RR_D bool tile_culled(const FrameConsts& fc, const ScreenCull& sc, int tx, int t
     return x1 + r < sc.r[0] || x0 - r > sc.r[1] || y1 + r < sc.r[2] || y0 - r > sc.r[3];
 }
 
+RR_D int uniform_i(int x) { return __builtin_amdgcn_readfirstlane(x); }
+RR_D float uniform_f(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+RR_D ScreenCull uniform_cull(ScreenCull c) {
+    c.on = uniform_i(c.on ? 1 : 0) != 0;
+    for (int k = 0; k < 4; ++k) c.r[k] = uniform_f(c.r[k]);
+    return c;
+}
+RR_D TileOrder uniform_order(TileOrder t) {
+    t.tx = uniform_i(t.tx);
+    t.n = uniform_i(t.n);
+    t.bx0 = uniform_i(t.bx0);
+    t.by0 = uniform_i(t.by0);
+    t.bw = uniform_i(t.bw);
+    t.bh = uniform_i(t.bh);
+    return t;
+}
+
 // Per-lane ray counts of the tile kernel, reduced once per wave at exit into
 // the chunk-0 counter pairs: {0, 1} = bounce 0, {2, 3} = all later bounces
 // (rr_api.cpp fill_stats sums the pairs).
@@ -1425,8 +1442,12 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     TravStack st{stack, spill, stride, 0};
     TravCount cp, ce, cs;
     uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0;
-    const ScreenCull cull = screen_cull(fc, v.nodes);
-    const TileOrder to = tile_order(fc, cull);
+    // The screen rectangle and the tile order come from the root node in LDS,
+    // so the compiler cannot tell they are wave-uniform and would keep (and
+    // spill) them in VGPRs for the whole kernel: every lane holds the same
+    // values, lane 0's copy goes to SGPRs.
+    const ScreenCull cull = uniform_cull(screen_cull(fc, v.nodes));
+    const TileOrder to = uniform_order(tile_order(fc, cull));
     const int lane = threadIdx.x & 63;
     // Work units: each tile of the screen-rectangle box is cut into sl.n slices,
     // one per sample group (box tiles first), every other tile is one unit.
