@@ -8,14 +8,22 @@ tracing at the scene's 1920x1080 / 128 spp, tonemap, JPEG q90 encode and file
 write. Frames are independent; each rank (one per GPU) renders its own frames
 (static frame partition, no data-path collective) => weak scaling.
 
-Timed region: barrier + device sync on both sides, max over ranks. Per-kernel
-device times come from HIP events recorded by the library on its own stream
-around every launch during the timed steps (RR_FLAG_PROFILE_KERNELS). Traversal
-counts for the algorithmic-byte model come from one extra counting frame after
-the timed region (RR_FLAG_COUNT_TRAVERSAL).
+Timed region: barrier + device sync on both sides, max over ranks (the only
+cross-rank exchange, over gloo: frames are independent, there is no data-path
+collective and no RCCL). Per-kernel device times come from HIP events recorded
+by the library on its own stream around every launch during the timed steps
+(RR_FLAG_PROFILE_KERNELS). Traversal counts for the algorithmic-byte model
+come from one extra counting frame after the timed region
+(RR_FLAG_COUNT_TRAVERSAL).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+  N > 1 without a launcher: bench.py starts N worker processes itself, one per
+  GPU (HIP_VISIBLE_DEVICES=i, before any GPU call in this process), as the
+  reference starts one worker per node (scripts/arnes/
+  queue-batch_04vs_14400f-10w_dynamic.sh:49,59); under torchrun (RANK /
+  WORLD_SIZE set) each process is one rank on GPU LOCAL_RANK.
+  --dry-run: the launch, frame partition and reduction without rendering (CPU
+  containers; the line carries value null).
 """
 from __future__ import annotations
 
@@ -24,6 +32,8 @@ import importlib
 import json
 import os
 import shutil
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -71,6 +81,7 @@ WORKLOADS = {
                        "rebuild every frame + wavefront path trace + JPEG q90 encode/write"},
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+MALL_BYTES = 256 << 20  # Infinity Cache (MALL) capacity
 # Vector-issue peak: a wave64 VALU instruction issues over 2 cycles on a SIMD-32
 # (MI355X_MICROARCH.md, wave scheduling), 4 SIMDs per CU, 256 CUs.
 VALU_ISSUE_PER_CLK_PER_SIMD = 0.5
@@ -90,8 +101,10 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-summary", default=None,
-                    help="PMC traffic summary for roofline.traffic (tools/pmc_summary.py; default "
-                         "profiles/r1_pmc.json for 04vs, profiles/r1_pmc_<workload>.json otherwise)")
+                    help="PMC traffic summary for roofline.traffic (tools/pmc_summary.py; default the newest "
+                         "profiles/r<N>_pmc.json for 04vs, profiles/r<N>_pmc_<workload>.json otherwise)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch, partition and reduce without rendering (no GPU needed; value is null)")
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
     if a.steps is None:
@@ -209,21 +222,75 @@ def frame_partition(frames, step: int, rank: int, world: int):
     return frames[(step * world + rank) % len(frames)]
 
 
-def reduce_max_seconds(elapsed: float, dist=None, device="cpu") -> float:
-    """Max of the per-rank timed-region wall time (the job ends with its slowest rank)."""
+def reduce_max_seconds(elapsed: float, dist=None) -> float:
+    """Max of the per-rank timed-region wall time (the job ends with its slowest
+    rank), over the gloo group on host tensors."""
     import torch
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed], dtype=torch.float64)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
+def newest_profile(name_fmt: str):
+    """profiles/<name_fmt % round> of the newest round that has it (r9 .. r1)."""
+    for r in range(9, 0, -1):
+        p = os.path.join(ROOT, "profiles", name_fmt % f"r{r}")
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def host_cpu():
+    """(cores usable by this process, nproc of the machine, CPU model)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return usable, os.cpu_count() or 1, model
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N with no launcher: N child processes of this script, rank i on
+    GPU i (HIP_VISIBLE_DEVICES, mapped through the parent's own list), gloo
+    rendezvous on 127.0.0.1. Started before this process touches a GPU; the
+    children's rank 0 prints the line. Returns the worst exit code."""
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    visible = os.environ.get("HIP_VISIBLE_DEVICES")
+    devs = visible.split(",") if visible else [str(i) for i in range(args.gpus)]
+    if len(devs) < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but HIP_VISIBLE_DEVICES lists {len(devs)}", file=sys.stderr)
+        return 2
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HIP_VISIBLE_DEVICES=devs[r], RR_BENCH_DEVICE="0",
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    return max(abs(p.wait()) for p in procs)
+
+
 def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin frame 1"):
     """Oracle (C restatement, OpenMP) on the host cores: 4-row bands of the same
     frame, taken in an order spread over the image, until the budget is spent or
-    the frame is done; extrapolated to frames/s."""
+    the frame is done; extrapolated to frames/s. Threads: OMP_NUM_THREADS when
+    the environment sets it (the GPU box gives one GPU's job a 16-core share
+    and sets it; nproc there counts the whole machine), else every core this
+    process may run on."""
     H = int(state.render_ints[1])
-    threads = min(os.cpu_count() or 1, 16)
+    usable, nproc, model = host_cpu()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or usable)
     bands = list(range(0, H, 4))
     done_rows, t_used = 0, 0.0
     order = [b for k in range(16) for b in bands[k::16]]
@@ -236,34 +303,98 @@ def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin 
             break
     frac = done_rows / H
     return {"value": frac / t_used, "unit": "frames/s", "cores": threads, "kind": "port",
+            "host": {"nproc": nproc, "affinity_cores": usable, "cpu_model": model,
+                     "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
             "sample": f"{done_rows} of {H} rows (4-row bands spread over the frame) of {label} "
                       f"at {int(state.render_ints[0])}x{H}, {int(state.render_ints[2])} spp, "
                       f"{t_used:.1f} s, extrapolated to whole frames; render only (no encode)"}
 
 
+def roofline_line(args, cls, cstats, kernel_ms, launches, names):
+    """The dominant kernel class against the roofline that actually bounds it
+    (DESIGN.md §6):
+      * LDS-resident scenes (k_tiles, 04vs / 01): VALU issue. The scene lives
+        in LDS; HBM sees only the film, so the HBM fraction is an honest small
+        number (kept as hbm_frac) and the bound is vector-instruction issue:
+        SQ_INSTS_VALU per launch over the launch time against 0.5 wave-
+        instructions per clock per SIMD.
+      * split path over a hierarchy that fits in L2 / MALL (02 / 03): HBM from
+        the PMC counters (FETCH_SIZE + WRITE_SIZE per launch over the launch
+        time); SURVEY §8(d)'s per-visit byte formula over-counts cache hits.
+      * split path over a hierarchy far above MALL (C5): HBM, SURVEY §8(d)'s
+        algorithmic bytes (64 B per node visit, 48 B per triangle test + the
+        ray / hit stream); the PMC traffic beside it."""
+    dom = names.index(cls)
+    n = int(cstats.n_triangles)
+    scene_bytes = 64.0 * max(n - 1, 1) + 48.0 * n
+    split = launches[5] > 0
+    bytes_frame, survey_frame = algorithmic_bytes(cls, cstats, scene_bytes, split)
+    launches_frame = max(launches[dom] / max(args.steps, 1), 1)
+    avg_ms = kernel_ms[dom] / max(launches[dom], 1)
+    per_s = lambda b: b / launches_frame / (avg_ms * 1e-3) / 1e9  # noqa: E731
+    wl_key = "" if args.workload == "04vs" else f"_{args.workload}"
+    pmc = args.pmc_summary or newest_profile("%s_pmc" + wl_key + ".json")
+    tr = pmc_traffic(cls, pmc) if pmc else None
+    valu = pmc_valu(cls, pmc, avg_ms) if pmc else None
+    hbm = {"hbm_algorithmic_gbs": round(per_s(survey_frame if split else bytes_frame), 2),
+           "hbm_compulsory_gbs": round(per_s(bytes_frame), 2),
+           "hbm_survey_formula_gbs": round(per_s(survey_frame), 2),
+           "traffic": round(tr["bytes"]) if tr else None,
+           "traffic_gbs": round(tr["bytes"] / (avg_ms * 1e-3) / 1e9, 1) if tr else None,
+           "traffic_source": tr["source"] if tr else None}
+    base = {"kernel": cls, "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": launches_frame,
+            "bytes_per_launch_algorithmic": round((survey_frame if split else bytes_frame) / launches_frame)}
+    if not split:
+        if valu is None:
+            return {**base, "bound": "valu", "achieved": None, "peak": None, "unit": "G wave-instr/s", "frac": None,
+                    **hbm, "hbm_frac": round(per_s(bytes_frame) / HBM_PEAK_GBS, 4),
+                    "note": "VALU-issue bound (LDS-resident scene); no PMC summary to price it"}
+        return {**base, "bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],
+                "frac": valu["frac"], "clock_ghz": valu["clock_ghz"], "valu_per_launch": valu["valu_per_launch"],
+                "valu_source": valu["source"], **hbm, "hbm_frac": round(per_s(bytes_frame) / HBM_PEAK_GBS, 4),
+                "note": "k_tiles: scene in LDS, bound by vector-instruction issue (SQ_INSTS_VALU per launch / launch "
+                        "time vs 0.5 wave-instr/clk/SIMD x 1024 SIMDs); HBM sees only film + RGBA8 (hbm_frac)"}
+    resident = n * (64.0 + 48.0) < MALL_BYTES  # hierarchy + triangles fit in the 256 MB MALL
+    if resident and tr is not None:
+        ach = tr["bytes"] / (avg_ms * 1e-3) / 1e9
+        return {**base, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), **hbm,
+                "note": "hierarchy + triangles fit in L2/MALL: achieved = PMC HBM traffic (FETCH_SIZE x2 + WRITE_SIZE, "
+                        "MI355X_MICROARCH.md) per launch / launch time; the SURVEY 8(d) per-visit formula "
+                        "(hbm_survey_formula_gbs) counts cache hits as HBM bytes"}
+    ach = per_s(survey_frame)
+    return {**base, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), **hbm,
+            "note": "hierarchy above MALL: achieved = SURVEY 8(d) algorithmic bytes (64 B per node visit, 48 B per "
+                    "triangle test + ray/hit stream) per launch / launch time; traffic = PMC HBM bytes per launch "
+                    "(FETCH_SIZE counts Infinity-Cache hits, so it is an upper bound on HBM reads)"}
+
+
 def main():
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
+    device = int(os.environ.get("RR_BENCH_DEVICE", local))
+    import torch  # first, as in every bench run so far: the HIP runtime librr binds to is torch's
+    gpu = torch.cuda.is_available()
+    if gpu:
+        torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend, init_method="env://")
-    gpu = torch.cuda.is_available()
-    if gpu:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+        # gloo: the only exchange is the timed region's max (host scalars); no RCCL
+        dist.init_process_group("gloo", init_method="env://")
 
-    def barrier():
+    def barrier(ctx=None):
         if dist is not None:
             dist.barrier()
         if gpu:
             torch.cuda.synchronize()
+        if ctx is not None:
+            ctx.synchronize()  # the renderer's own streams (rr_synchronize)
 
     rr = importlib.import_module(PKG)
     wl = WORKLOADS[args.workload]
@@ -271,11 +402,35 @@ def main():
     outdir = tempfile.mkdtemp(prefix=f"rr_bench_r{rank}_")
     job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": outdir})
     frames = job.frames()
-    flags = 0 if args.no_profile else rr.native.RR_FLAG_PROFILE_KERNELS
-    runner = rr.BackendRunner(ROOT, device=local, params=rr.default_params(flags=flags, spp=args.spp))
 
     def frame_of(step):
         return frame_partition(frames, step, rank, world)
+
+    if args.dry_run:
+        barrier()
+        t0 = time.perf_counter()
+        mine = [frame_of(args.warmup + s) for s in range(args.steps)]
+        barrier()
+        t_max = reduce_max_seconds(time.perf_counter() - t0, dist)
+        by_rank = [mine]
+        if dist is not None:
+            by_rank = [None] * world
+            dist.all_gather_object(by_rank, mine)
+        if rank == 0:
+            print(json.dumps({"metric": wl["metric"], "value": None, "unit": "frames/s", "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 6),
+                              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                              "data": "dry run: no frames rendered", "dry_run": True,
+                              "config": {"workload": wl["workload"], "job": os.path.basename(wl["job"]),
+                                         "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)"},
+                              "frames_by_rank": by_rank}), flush=True)
+        shutil.rmtree(outdir, ignore_errors=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    flags = 0 if args.no_profile else rr.native.RR_FLAG_PROFILE_KERNELS
+    runner = rr.BackendRunner(ROOT, device=device, params=rr.default_params(flags=flags, spp=args.spp))
 
     if args.serial:
         for w in range(args.warmup):
@@ -284,16 +439,20 @@ def main():
         runner.render_frames(job, [frame_of(w) for w in range(args.warmup)])
     kernel_ms = [0.0] * 8
     launches = [0] * 8
-    rays = 0
+    rays = {"camera": 0, "camera_traced": 0, "extension": 0, "shadow": 0}
+    substituted = []
 
     def account(st):
-        nonlocal rays
         for k in range(8):
             kernel_ms[k] += st.kernel_ms[k]
             launches[k] += st.kernel_launches[k]
-        rays += st.camera_rays + st.extension_rays + st.shadow_rays
+        rays["camera"] += st.camera_rays
+        rays["camera_traced"] += st.camera_rays_traced
+        rays["extension"] += st.extension_rays
+        rays["shadow"] += st.shadow_rays
+        substituted.append(st.view_transform_substituted)
 
-    barrier()
+    barrier(runner.ctx)
     t0 = time.perf_counter()
     if args.serial:
         for s in range(args.steps):
@@ -304,10 +463,10 @@ def main():
         # written (rr_frame_submit / rr_frame_complete); every frame is written
         runner.render_frames(job, [frame_of(args.warmup + s) for s in range(args.steps)],
                              on_frame=lambda f, frt, st: account(st))
-    barrier()
+    barrier(runner.ctx)
     elapsed = time.perf_counter() - t0
     last_stats = runner.last_stats
-    t_max = reduce_max_seconds(elapsed, dist, dev if dist is not None and gpu else "cpu")
+    t_max = reduce_max_seconds(elapsed, dist)
 
     # traversal counts for the byte model: one counting frame, outside the timed region
     scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, ROOT))
@@ -315,7 +474,6 @@ def main():
     _, _, cstats = runner.ctx.render_to_memory(scene, f_count, rr.default_params(
         flags=rr.native.RR_FLAG_COUNT_TRAVERSAL, spp=args.spp), film=False, rgba=True)
 
-    result = None
     if rank == 0:
         total_frames = args.steps * world
         value = total_frames / t_max
@@ -324,43 +482,7 @@ def main():
         roofline = None
         if not args.no_profile:
             dom = max(range(len(names)), key=lambda k: kernel_ms[k])
-            cls = names[dom]
-            n = int(cstats.n_triangles)
-            scene_bytes = 64.0 * max(n - 1, 1) + 48.0 * n
-            split = launches[5] > 0
-            bytes_frame, survey_frame = algorithmic_bytes(cls, cstats, scene_bytes, split)
-            launches_frame = max(launches[dom] / max(args.steps, 1), 1)
-            avg_ms = kernel_ms[dom] / max(launches[dom], 1)
-            # LDS-resident scenes (fused path): node/triangle reads never reach
-            # HBM, so `achieved` prices the compulsory stream; scenes traversed
-            # from HBM (split path): SURVEY 8(d)'s figure (every node visit 64 B,
-            # every triangle test 48 B) — DESIGN.md §6
-            model = "survey" if split else "compulsory"
-            per_launch = (survey_frame if split else bytes_frame) / launches_frame
-            achieved = per_launch / (avg_ms * 1e-3) / 1e9
-            survey_achieved = survey_frame / launches_frame / (avg_ms * 1e-3) / 1e9
-            compulsory_achieved = bytes_frame / launches_frame / (avg_ms * 1e-3) / 1e9
-            pmc = args.pmc_summary or os.path.join(
-                ROOT, "profiles", "r1_pmc.json" if args.workload == "04vs" else f"r1_pmc_{args.workload}.json")
-            tr = pmc_traffic(cls, pmc)
-            roofline = {"bound": "hbm", "kernel": cls, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": round(tr["bytes"]) if tr else None,
-                        "traffic_source": tr["source"] if tr else None,
-                        "traffic_gbs": round(tr["bytes"] / (avg_ms * 1e-3) / 1e9, 1) if tr else None,
-                        "bytes_per_launch": round(per_launch), "avg_launch_ms": round(avg_ms, 4),
-                        "byte_model": model,
-                        "achieved_survey_formula": round(survey_achieved, 2),
-                        "achieved_compulsory": round(compulsory_achieved, 2),
-                        "note": "achieved: LDS-resident scene -> compulsory bytes (stream + scene once); scene "
-                                "traversed from HBM -> SURVEY 8(d) formula (64 B per node visit, 48 B per "
-                                "triangle test + stream); traffic = PMC HBM bytes per launch (FETCH_SIZE x2 + "
-                                "WRITE_SIZE), traffic_gbs its rate"}
-            valu = pmc_valu(cls, pmc, avg_ms)
-            if valu is not None:
-                # what actually bounds an LDS-resident scene's kernel: vector issue
-                # (the HBM fraction is an honest small number there)
-                roofline["valu_issue"] = valu
+            roofline = roofline_line(args, names[dom], cstats, kernel_ms, launches, names)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -377,6 +499,7 @@ def main():
                     cpu["sample"] += f"; rendered at {spp_cpu} spp and scaled to {spp_full} spp"
             except Exception as e:  # baseline is reported, never the target
                 cpu = {"value": None, "unit": "frames/s", "error": str(e)}
+        traced = rays["camera_traced"] + rays["extension"] + rays["shadow"]
         result = {
             "metric": wl["metric"], "value": round(value, 4), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
@@ -386,8 +509,10 @@ def main():
                        "resolution": f"{int(last_stats.width)}x{int(last_stats.height)}", "spp": int(last_stats.spp),
                        "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)",
                        "pipelining": "serial (rr_render_frame per frame)" if args.serial else
-                                     "2 frames in flight: frame N encoded + written while N+1 renders"},
-            "mrays_per_s_per_gpu": round(rays / elapsed / 1e6, 1),
+                                     "2 frames in flight: frame N encoded + written while N+1 renders",
+                       "view_transform_substituted": int(any(substituted))},
+            "mrays_per_s_per_gpu": round(traced / elapsed / 1e6, 1),
+            "rays_per_frame": {k: v // max(args.steps, 1) for k, v in rays.items()},
             "device_ms_per_frame": round(sum(kernel_ms) / max(args.steps, 1), 3),
             "kernels": per_class,
             "roofline": roofline,

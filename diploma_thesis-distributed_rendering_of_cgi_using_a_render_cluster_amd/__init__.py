@@ -16,7 +16,8 @@ from .naming import EXTENSIONS, format_hash_frame_placeholders, job_output_files
     output_path_without_extension
 from .native import (LIB_PATH, SHIM_PATH, EXPORTS, FrameState, FrameStats, FrameTiming, RenderContext,
                      RenderParams, RRError, Scene, default_params, encode_image, lib)
-from .runner import BackendRunner, RenderError
+from .runner import (BackendRunner, FrameQueueRemoveResult, PendingFrame, RenderError, WorkerAutomaticQueue,
+                     WorkerFrameState)
 from .traces import FrameRenderTime, WorkerTrace, WorkerTraceBuilder, raw_trace_document, save_raw_traces, \
     worker_name
 

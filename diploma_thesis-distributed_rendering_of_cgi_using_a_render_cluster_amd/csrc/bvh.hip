@@ -351,27 +351,6 @@ __global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restr
     }
 }
 
-// Small subtrees become leaf ranges: a child subtree over at most kLeafMax
-// sorted leaves (Karras nodes cover contiguous ranges) is referenced as
-// ~(first | (count - 1) << 28), so the walk tests its triangles (contiguous
-// TriPacks) instead of visiting its bottom nodes. Rewrites only the child refs
-// of nodes[] (the boxes are the subtrees' boxes already); `children` keeps the
-// full topology (BVH4 collapse, depth parity).
-__global__ __launch_bounds__(kBlock) void k_leafify(int ni, const int2* __restrict__ children,
-                                                    const int2* __restrict__ range, BvhNode* __restrict__ nodes) {
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= ni) return;
-    const int2 ch = children[p];
-    int ref[2] = {ch.x, ch.y};
-    for (int s = 0; s < 2; ++s)
-        if (ref[s] >= 0) {
-            const int2 r = range[ref[s]];
-            if (r.y <= kLeafMax) ref[s] = leaf_ref(r.x, r.y);
-        }
-    nodes[p].d.x = ref[0];
-    nodes[p].d.y = ref[1];
-}
-
 // BVH4 collapse, step 1: depth parity of every internal node (walk to the
 // root through node_parent); flags[i] = 1 and rank[i] = 1 for even depth.
 __global__ __launch_bounds__(kBlock) void k_depth_parity(int ni, const int32_t* __restrict__ node_parent,
@@ -578,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_ploc_apply(const int* __restrict__ c
 //  - K4: k_karras on the sorted keys in LDS;
 //  - refit: a child's box is the min/max of the leaf boxes of its sorted leaf
 //    range (min/max are exact, so any grouping gives the tree-merge values);
-//  - K5 triangle packs and k_leafify's leaf-range refs as above.
+//  - K5 triangle packs as above.
 constexpr int kSmallBuild = 512;
 
 __global__ __launch_bounds__(kSmallBuild) void k_build_small(
@@ -707,7 +686,7 @@ __global__ __launch_bounds__(kSmallBuild) void k_build_small(
         if (i == 0) node_parent[0] = -1;
     }
     __syncthreads();
-    if (i < n - 1) {  // K4b refit from leaf ranges + k_leafify
+    if (i < n - 1) {  // K4b refit from leaf ranges
         float f[12];
         int ref[2] = {ch.x, ch.y};
         for (int side = 0; side < 2; ++side) {
@@ -719,7 +698,6 @@ __global__ __launch_bounds__(kSmallBuild) void k_build_small(
             } else {
                 first = rng[cref].x;
                 cnt = rng[cref].y;
-                if (kLeafMax > 1 && cnt <= kLeafMax) ref[side] = leaf_ref(first, cnt);
             }
             float bx[6];
             for (int k = 0; k < 6; ++k) bx[k] = lbox[first][k];
@@ -934,8 +912,6 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, b
                                                          s.rank4.ptr, s.nodes4.ptr);
         s.has4 = true;
     }
-    if (kLeafMax > 1 && n > 1)
-        k_leafify<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n - 1, s.children.ptr, s.range.ptr, s.nodes.ptr);
     if (prof) prof->end(st);
     RR_HIP(hipGetLastError());
     s.built = true;

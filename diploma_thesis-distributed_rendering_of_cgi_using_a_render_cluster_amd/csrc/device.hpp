@@ -163,6 +163,7 @@ struct FrameConsts {
     int W, H, npix;
     FastDiv div_w, div_npix;  // pixel index -> (x, y), path index -> (sample, pixel)
     int spp_total, spp_chunk, first_sample, max_bounces, n_lights;
+    int max_diffuse, max_glossy;  // per-lobe bounce caps (>= 1, setup_frame)
     uint32_t seed;
     float clamp_indirect, exposure_scale, inv_spp;
     int view_transform;
@@ -197,7 +198,6 @@ bool upload_by_kernarg(const float* src, const UploadSeg* segs, int nseg, hipStr
 // Whether the path kernels take the LDS-resident (fused, BVH2) variant for a
 // scene of these sizes; otherwise the split path over the BVH4 in HBM.
 bool scene_in_lds(int n_tris, int n_mats, int n_lights);
-int split_bvh_width();  // hierarchy width of the split path (4)
 
 // Render all chunks of one frame: film accumulate + tonemap to rgba8.
 // counters_per_chunk receives the device counter layout for stats.
@@ -230,6 +230,8 @@ void jpeg_encode_device(const uint8_t* d_rgba, int W, int H, const float* d_tab,
                         int16_t* d_coeffs, JpegDevBufs& b, uint8_t* host_out, hipStream_t st);
 
 int counters_per_chunk(int max_bounces);
+// Word of a chunk's counters holding the camera rays traced (counters_per_chunk).
+RR_HD int camera_traced_slot(int max_bounces) { return 2 * (max_bounces + 2); }
 int device_cu_count();
 
 }  // namespace rr

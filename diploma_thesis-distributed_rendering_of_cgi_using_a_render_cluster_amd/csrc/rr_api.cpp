@@ -28,6 +28,7 @@
 #include "image_io.hpp"
 #include "rr.h"
 #include "scene.hpp"
+#include "view.hpp"
 
 using namespace rr;
 
@@ -71,6 +72,7 @@ struct FrameRun {
     int W, H, chunks, spp_chunk;
     bool rebuilt;
     float build_ms, trace_ms, readback_ms;
+    float render_ms, device_ms;  // ev0 -> ev4 (build + trace + view transform), ev0 -> ev2 (+ device JPEG)
     std::vector<int32_t> counters;
     double kernel_ms[RR_K_CLASSES];
     int32_t kernel_launches[RR_K_CLASSES];
@@ -84,7 +86,9 @@ struct FrameRun {
 struct FrameSlot {
     bool busy = false;
     uint64_t ticket = 0;
-    hipEvent_t ev[4] = {};  // 0 start, 1 built, 2 rendered (stream), 3 outputs on the host (copy stream)
+    // 0 start, 1 built, 4 image done (before the device JPEG coder), 2 stream
+    // work done, 3 outputs on the host (copy stream)
+    hipEvent_t ev[5] = {};
     DevBuf<int32_t> counters;  // this frame's ray counters (swapped into DevPaths while enqueuing)
     // this frame's device outputs (swapped into DevPaths / rr_ctx while enqueuing):
     // the copy stream reads them while the next frame's kernels write the other
@@ -97,6 +101,8 @@ struct FrameSlot {
     PinnedBuf host_jpeg;   // device-coded JPEG stream: [uint64 length][pad][bytes]
     bool jpeg_dev = false;  // this frame's entropy coding runs on the device
     FrameSetup fs;
+    bool view_substituted = false;  // Filmic asked for, no LUTs: rendered with Standard
+    double submit_at = 0.0;         // UNIX time when the device work was enqueued
     rr_scene* scene = nullptr;
     std::string out_path, format;
     int quality = 0;
@@ -129,6 +135,11 @@ struct rr_ctx {
     FrameSlot slots[RR_MAX_FRAMES_IN_FLIGHT];
     uint64_t next_ticket = 1;     // tickets are issued in submission order
     uint64_t next_complete = 1;   // the ticket rr_frame_complete expects next
+    // UNIX-time estimate of when the compute stream finished the last completed
+    // frame (rr_frame_complete): the next frame's device work cannot start before
+    double gpu_free_at = 0.0;
+    FilmicDev filmic;             // RR_VIEW_FILMIC LUTs (rr_set_ocio_config / RR_OCIO_DIR)
+    std::string warning;          // rr_last_warning
 };
 
 struct rr_scene {
@@ -190,7 +201,15 @@ constexpr int kHierLbvh = 2, kHierPloc = 3, kHierBvh4 = 4;
 // path), larger scenes PLOC (split path; or the BVH4 when built for it).
 int frame_hier(int n_tris, int n_mats, int n_lights) {
     if (scene_in_lds(n_tris, n_mats, n_lights)) return kHierLbvh;
-    return split_bvh_width() == 4 ? kHierBvh4 : kHierPloc;
+    return kHierPloc;
+}
+
+// The view transform a frame on ctx is rendered with: Filmic needs the
+// context's LUTs; without them Standard, and the caller is told (returns true).
+bool resolve_view(const rr_ctx* c, FrameSetup& fs) {
+    if (fs.view_transform != VIEW_FILMIC || (c && c->filmic.ready)) return false;
+    fs.view_transform = VIEW_STANDARD;
+    return true;
 }
 
 // hier: 0 = the frame's hierarchy, else a kHier* id (inspection entry points).
@@ -267,6 +286,8 @@ FrameConsts make_consts(const FrameSetup& fs, int n_tris) {
     k.div_npix = FastDiv::make((uint32_t)k.npix);
     k.spp_total = fs.spp;
     k.max_bounces = fs.max_bounces;
+    k.max_diffuse = fs.max_diffuse;
+    k.max_glossy = fs.max_glossy;
     k.n_lights = (int)(fs.lights.size() / RR_LIGHT_FLOATS);
     k.n_mats = (int)(fs.materials.size() / RR_MAT_FLOATS);
     k.seed = fs.seed;
@@ -385,6 +406,12 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     r.chunks = (fs.spp + r.spp_chunk - 1) / r.spp_chunk;
     k.spp_chunk = r.spp_chunk;
     render_frame_device(s->dev, c->paths, k, r.chunks, st);
+    if (fs.view_transform == VIEW_FILMIC) {  // film -> Filmic -> rgba8 (overwrites the kernels' tonemap)
+        c->paths.prof.begin(st, RR_K_ACCUM);
+        view_filmic_device(c->filmic, k, c->paths.film.ptr, reinterpret_cast<uchar4*>(c->paths.rgba8.ptr), st);
+        c->paths.prof.end(st);
+    }
+    RR_HIP(hipEventRecord(sl.ev[4], st));
     const size_t npix = (size_t)fs.W * fs.H;
     if (sl.jpeg) {
         if (c->jpeg_tab_quality != sl.quality) {
@@ -439,8 +466,10 @@ void finish_frame(rr_ctx* c, FrameSlot& sl) {
     const FrameSetup& fs = sl.fs;
     RR_HIP(hipEventSynchronize(sl.ev[3]));
     RR_HIP(hipEventElapsedTime(&r.build_ms, sl.ev[0], sl.ev[1]));
-    RR_HIP(hipEventElapsedTime(&r.trace_ms, sl.ev[1], sl.ev[2]));
-    RR_HIP(hipEventElapsedTime(&r.readback_ms, sl.ev[2], sl.ev[3]));
+    RR_HIP(hipEventElapsedTime(&r.trace_ms, sl.ev[1], sl.ev[4]));
+    RR_HIP(hipEventElapsedTime(&r.readback_ms, sl.ev[4], sl.ev[3]));
+    RR_HIP(hipEventElapsedTime(&r.render_ms, sl.ev[0], sl.ev[4]));
+    RR_HIP(hipEventElapsedTime(&r.device_ms, sl.ev[0], sl.ev[2]));
     const int cpc = counters_per_chunk(fs.max_bounces);
     r.counters.assign(reinterpret_cast<const int32_t*>(sl.host_counters.ptr),
                       reinterpret_cast<const int32_t*>(sl.host_counters.ptr) + (size_t)cpc * r.chunks);
@@ -467,10 +496,12 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
     st->spp = fs.spp;
     st->chunks = r.chunks;
     st->camera_rays = (uint64_t)fs.W * fs.H * fs.spp;
+    st->view_transform = fs.view_transform;
     const int cpc = counters_per_chunk(fs.max_bounces);
     for (int c = 0; c < r.chunks; ++c) {
         // pair b: {paths entering bounce b+1, shadow rays of bounce b} (wavefront.hip)
         const int32_t* q = &r.counters[(size_t)cpc * c];
+        st->camera_rays_traced += (uint64_t)(uint32_t)q[camera_traced_slot(fs.max_bounces)];
         for (int b = 0; b < fs.max_bounces; ++b) st->extension_rays += (uint64_t)q[2 * b];
         for (int b = 0; b <= fs.max_bounces; ++b) st->shadow_rays += (uint64_t)q[2 * b + 1];
         st->primary_continued += (uint64_t)q[0];
@@ -540,11 +571,29 @@ void rr_render_params_default(rr_render_params* p) {
     p->height = 0;
     p->view_transform = RR_VIEW_SCENE;
     p->spp_per_chunk = 0;
+    p->max_diffuse_bounces = -1;
+    p->max_glossy_bounces = -1;
 }
 
 int32_t rr_abi_version(void) { return RR_ABI_VERSION; }
 
 const char* rr_last_error(rr_ctx*) { return g_err.c_str(); }
+
+const char* rr_last_warning(rr_ctx* c) { return c ? c->warning.c_str() : ""; }
+
+int rr_set_ocio_config(rr_ctx* c, const char* dir) {
+    if (!c) return fail(RR_EINVAL, "NULL ctx");
+    return guarded([&] {
+        set_device(c);
+        c->filmic.release();
+        if (!dir || !*dir) return RR_OK;
+        FilmicLuts l;
+        std::string err;
+        if (!load_filmic_luts(dir, l, err)) return fail(err.rfind("no ", 0) == 0 || err.rfind("cannot", 0) == 0 ? RR_ENOENT : RR_EINVAL, err);
+        c->filmic.upload(l, dir);
+        return RR_OK;
+    });
+}
 
 int rr_create(int device_ordinal, rr_ctx** out) {
     if (!out) return fail(RR_EINVAL, "out is NULL");
@@ -560,6 +609,14 @@ int rr_create(int device_ordinal, rr_ctx** out) {
         set_device(c.get());
         RR_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         RR_HIP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+        if (const char* d = getenv("RR_OCIO_DIR")) {
+            // a broken LUT directory does not fail the context: Filmic frames fall
+            // back to Standard and carry the reason in rr_last_warning
+            FilmicLuts l;
+            std::string err;
+            if (*d && load_filmic_luts(d, l, err)) c->filmic.upload(l, d);
+            else if (*d) c->warning = "RR_OCIO_DIR: " + err;
+        }
         *out = c.release();
         return RR_OK;
     });
@@ -571,6 +628,7 @@ void rr_destroy(rr_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     c->paths.release();
+    c->filmic.release();
     c->jpeg_tab.release();
     c->jpeg_coeffs.release();
     c->jpeg_huff.release();
@@ -653,6 +711,7 @@ int rr_frame_submit(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_param
         sl->tm.loaded_at = unix_now();
         const auto t_anim = std::chrono::steady_clock::now();
         sl->fs = setup_frame(s->desc, frame, params);
+        sl->view_substituted = resolve_view(c, sl->fs);
         sl->anim_ms = ms_since(t_anim);
         sl->tm.started_rendering_at = unix_now();
         sl->scene = s;
@@ -662,6 +721,7 @@ int rr_frame_submit(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_param
         sl->jpeg = jpeg;
         sl->want_rgba = out_path && !jpeg;
         sl->film_out = nullptr;
+        sl->submit_at = unix_now();
         enqueue_frame(c, *sl);
         sl->busy = true;
         sl->ticket = c->next_ticket++;
@@ -684,10 +744,19 @@ int rr_frame_complete(rr_ctx* c, uint64_t ticket, rr_frame_timing* timing, rr_fr
         const FrameSetup& fs = sl->fs;
         const FrameRun& r = sl->r;
         const double t_sync = unix_now();
-        // the device JPEG transform + readback belong to "saving" (Blender's
-        // write_still); move that device interval out of the render span
-        sl->tm.finished_rendering_at = sl->jpeg ? t_sync - r.readback_ms * 1e-3 : t_sync;
+        // Render span from the device's own clock: the frame's work starts when
+        // it was enqueued or when the stream finished the previous frame,
+        // whichever is later, and lasts ev0 -> ev4 (build, trace, view
+        // transform); the device JPEG coder, the copies and the file write
+        // after ev4 are "saving" (Blender's write_still). Host times when
+        // complete happens to be called (possibly long after the device
+        // finished) do not enter the span.
+        const double gpu_start = std::max(sl->submit_at, c->gpu_free_at);
+        sl->tm.started_rendering_at = std::min(std::max(sl->tm.started_rendering_at, gpu_start), t_sync);
+        sl->tm.finished_rendering_at =
+            std::min(std::max(gpu_start + r.render_ms * 1e-3, sl->tm.started_rendering_at), t_sync);
         sl->tm.file_saving_started_at = sl->tm.finished_rendering_at;
+        c->gpu_free_at = std::min(gpu_start + r.device_ms * 1e-3, t_sync);
         uint64_t bytes = 0;
         const auto t_enc = std::chrono::steady_clock::now();
         if (sl->jpeg && sl->jpeg_dev) {
@@ -710,8 +779,13 @@ int rr_frame_complete(rr_ctx* c, uint64_t ticket, rr_frame_timing* timing, rr_fr
         const double enc_ms = ms_since(t_enc);
         sl->tm.file_saving_finished_at = unix_now();
         if (timing) *timing = sl->tm;
+        c->warning = sl->view_substituted
+                         ? "scene view transform Filmic rendered as Standard: no OCIO LUTs configured "
+                           "(rr_set_ocio_config / RR_OCIO_DIR)"
+                         : "";
         if (stats) {
             fill_stats(stats, fs, r, sl->scene->dev.n_tris);
+            stats->view_transform_substituted = sl->view_substituted ? 1 : 0;
             stats->anim_ms = sl->anim_ms;
             stats->encode_ms = enc_ms;
             stats->output_bytes = bytes;
@@ -733,6 +807,16 @@ int rr_render_frame(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_param
     return rr_frame_complete(c, t, timing, stats);
 }
 
+int rr_synchronize(rr_ctx* c) {
+    if (!c) return fail(RR_EINVAL, "NULL ctx");
+    return guarded([&] {
+        set_device(c);
+        RR_HIP(hipStreamSynchronize(c->stream));
+        RR_HIP(hipStreamSynchronize(c->copy_stream));
+        return RR_OK;
+    });
+}
+
 int rr_render_frame_to_memory(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_params* params,
                               float* film, uint8_t* rgba8, rr_frame_stats* stats) {
     if (!c || !s) return fail(RR_EINVAL, "NULL ctx or scene");
@@ -742,6 +826,7 @@ int rr_render_frame_to_memory(rr_ctx* c, rr_scene* s, int32_t frame, const rr_re
     return guarded([&] {
         sl->t_call = std::chrono::steady_clock::now();
         sl->fs = setup_frame(s->desc, frame, params);
+        sl->view_substituted = resolve_view(c, sl->fs);
         sl->scene = s;
         sl->out_path.clear();
         sl->format.clear();
@@ -755,6 +840,7 @@ int rr_render_frame_to_memory(rr_ctx* c, rr_scene* s, int32_t frame, const rr_re
         if (rgba8) std::memcpy(rgba8, sl->host_rgba.ptr, (size_t)fs.W * fs.H * 4);
         if (stats) {
             fill_stats(stats, fs, sl->r, s->dev.n_tris);
+            stats->view_transform_substituted = sl->view_substituted ? 1 : 0;
             stats->total_ms = ms_since(sl->t_call);
         }
         return RR_OK;
@@ -827,6 +913,7 @@ int rr_debug_frame_state(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_
     if (!c && tris_world) return fail(RR_EINVAL, "world triangles need a device context");
     return guarded([&] {
         FrameSetup fs = setup_frame(s->desc, frame, params);
+        if (c) resolve_view(c, fs);  // render_ints[5]: the transform a frame on c is rendered with
         const int n = s->dev.n_tris;
         if (c) {  // host-only queries (c == NULL) skip the device part
             if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
@@ -854,7 +941,8 @@ int rr_debug_frame_state(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_
         if (world) std::memcpy(world, fs.world, sizeof fs.world);
         if (render_ints) {
             const int32_t ri[RR_RENDER_INTS] = {fs.W, fs.H, fs.spp, fs.max_bounces, (int32_t)fs.seed,
-                                               fs.view_transform, choose_spp_chunk(fs), frame_hier_of(s, fs)};
+                                               fs.view_transform, choose_spp_chunk(fs), frame_hier_of(s, fs),
+                                               fs.max_diffuse, fs.max_glossy};
             std::memcpy(render_ints, ri, sizeof ri);
         }
         if (render_floats) {

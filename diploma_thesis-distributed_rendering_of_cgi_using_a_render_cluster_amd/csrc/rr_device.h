@@ -58,17 +58,10 @@ struct alignas(16) TriPack {
 static_assert(sizeof(TriPack) == 48, "tri pack is 48 bytes");
 
 // Leaf refs (< 0) name a range of sorted leaves: ~(first | (count - 1) << 28).
-// Subtrees over at most kLeafMax leaves are referenced as ranges (bvh.hip
-// k_leafify; oracle ORC_LEAF_MAX must be equal). Measured on the split path
-// (one 02 frame at 16 spp / C5 at 8 spp): kLeafMax 1 -> 61.7 / 115.1 ms,
-// 2 -> 70.0 / 132.5, 4 -> 87.7 / 165.1, 8 -> 121.7 / 229.9: the extra
-// triangle tests cost far more than the bottom node visits they save, so
-// leaves stay single triangles (kLeafMax 1: k_leafify is not launched).
-#ifndef RR_LEAF_MAX
-#define RR_LEAF_MAX 1
-#endif
-constexpr int kLeafMax = RR_LEAF_MAX;
-static_assert(kLeafMax >= 1 && kLeafMax <= 8, "count - 1 must fit bits 28..30 of a leaf ref");
+// The frame hierarchies use single-triangle leaves (count 1, ref = ~index):
+// multi-triangle leaf ranges measured slower on every split-path config (one
+// 02 frame at 16 spp / C5 at 8 spp: 1 -> 61.7 / 115.1 ms, 2 -> 70.0 / 132.5,
+// 8 -> 121.7 / 229.9 ms); the range encoding stays for the BVH4 collapse.
 RR_HD int leaf_ref(int first, int count) { return ~(first | ((count - 1) << 28)); }
 RR_HD int leaf_first(int ref) { return (~ref) & 0x0FFFFFFF; }
 RR_HD int leaf_count(int ref) { return ((~ref) >> 28) + 1; }
@@ -286,49 +279,8 @@ RR_HD void closest_tri(const TriPack& tp, int idx, float3 o, float3 d, float tmi
     }
 }
 
-// closest_tri without early exits: the same IEEE op sequence as tri_test +
-// closest_tri (so identical t/u/v and the identical accept decision, NaN
-// cases included: the rejections are written as the negations of tri_test's
-// exit tests), but straight-line code, so the lanes of a wave that test
-// different triangles stay converged and a triangle's three loads go out
-// together (tri_test's exits split them into two dependent round trips).
-RR_HD void closest_tri_nb(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
-    const float3 v0 = xyz(tp.p0), e1 = xyz(tp.p1), e2 = xyz(tp.p2);
-    const float3 pv = cross3(d, e2);
-    const float det = dot3(e1, pv);
-    const float inv = 1.0f / det;
-    const float3 tv = sub3(o, v0);
-    const float u = dot3(tv, pv) * inv;
-    const float3 qv = cross3(tv, e1);
-    const float v = dot3(d, qv) * inv;
-    const float t = dot3(e2, qv) * inv;
-    const int orig = f2i(tp.p0.w);
-    const bool ok = !(det == 0.0f) && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && t > tmin &&
-                    (t < h.t || (t == h.t && orig < h.orig));
-    if (ok) {
-        h.t = t;
-        h.u = u;
-        h.v = v;
-        h.idx = idx;
-        h.orig = orig;
-    }
-}
-
-#ifndef RR_BVH4_SORT
-#define RR_BVH4_SORT 0
-#endif
-#ifndef RR_LEAF_LOOP
-#define RR_LEAF_LOOP 0
-#endif
-#ifndef RR_TRI_BRANCHLESS
-#define RR_TRI_BRANCHLESS 0
-#endif
 RR_HD void leaf_test(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
-#if RR_TRI_BRANCHLESS
-    closest_tri_nb(tp, idx, o, d, tmin, h);
-#else
     closest_tri(tp, idx, o, d, tmin, h);
-#endif
 }
 
 // Traversal stack: kLdsStack entries in LDS ([entry][thread] -> conflict-free
@@ -439,54 +391,24 @@ struct TravState {
         bool hl = slab(o, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
         bool hr = slab(o, invd, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
         const int cl = nd.d.x, cr = nd.d.y;
-#if 1
-        // passing leaf ranges, left then right, one triangle per iteration: a
-        // wave runs as many iterations as its busiest lane needs
-        int nl = 0, nr = 0, fl = 0, fr = 0;
+        // passing leaves (single triangles), left then right, one per
+        // iteration: lanes with only a left and lanes with only a right leaf
+        // share one pass, a wave runs as many passes as its busiest lane needs
+        int nl = 0, nr = 0;
         if (hl && cl < 0) {
-            fl = leaf_first(cl);
-            nl = leaf_count(cl);
+            nl = 1;
             hl = false;
         }
         if (hr && cr < 0) {
-            fr = leaf_first(cr);
-            nr = leaf_count(cr);
+            nr = 1;
             hr = false;
         }
         for (int k = 0; k < nl + nr; ++k) {
-            const int ti = k < nl ? fl + k : fr + (k - nl);
+            const int ti = k < nl ? ~cl : ~cr;
             if (kCount) ++cnt.tris;
             leaf_test(load_tri(tris, ti), ti, o, d, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
         }
-#elif RR_LEAF_LOOP
-        // passing leaf children, left first, as a loop: a wave runs the leaf
-        // test as often as its busiest lane needs (lanes with a left leaf and
-        // lanes with a right leaf share one pass)
-        uint32_t leaves = (hl && cl < 0 ? 1u : 0u) | (hr && cr < 0 ? 2u : 0u);
-        if (leaves & 1u) hl = false;
-        if (leaves & 2u) hr = false;
-        while (leaves) {
-            const int r = (leaves & 1u) ? cl : cr;
-            leaves &= leaves - 1;
-            if (kCount) ++cnt.tris;
-            leaf_test(load_tri(tris, ~r), ~r, o, d, tmin, h);
-            if (kAnyHit && h.idx >= 0) return true;
-        }
-#else
-        if (hl && cl < 0) {
-            if (kCount) ++cnt.tris;
-            leaf_test(load_tri(tris, ~cl), ~cl, o, d, tmin, h);
-            if (kAnyHit && h.idx >= 0) return true;
-            hl = false;
-        }
-        if (hr && cr < 0) {
-            if (kCount) ++cnt.tris;
-            leaf_test(load_tri(tris, ~cr), ~cr, o, d, tmin, h);
-            if (kAnyHit && h.idx >= 0) return true;
-            hr = false;
-        }
-#endif
         if (hl && hr) {
             const bool left_first = tl <= tr;
             st.push(left_first ? cr : cl);
@@ -508,24 +430,10 @@ RR_D Bvh4Node load_node4(const Bvh4Node* __restrict__ p, int i) { return p[i]; }
 RR_D float f4get(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 RR_D int i4get(const int4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
-// Ordering of a node's hit children: ascending entry distance, ties by slot.
-struct ChildKey {
-    float t;
-    int slot, ref;
-};
-RR_D void cswap(ChildKey& a, ChildKey& b) {
-    if (b.t < a.t || (b.t == a.t && b.slot < a.slot)) {
-        const ChildKey x = a;
-        a = b;
-        b = x;
-    }
-}
-
 // Resumable traversal of the BVH4 (same contract as TravState): leaf children
-// whose boxes pass are intersected at once in slot order; the hit internal
-// children are sorted by (entry t, slot) with a 5-exchange network, the
-// nearest is visited next and the others pushed farthest first.
-// oracle/rr_oracle.c trace4() is the same walk.
+// whose boxes pass are intersected at once in slot order; the nearest hit
+// internal child is visited next and the others are pushed in descending slot
+// order. oracle/rr_oracle.c trace4() is the same walk.
 template <bool kAnyHit, bool kCount = false>
 struct TravState4 {
     float3 o, d, invd;
@@ -582,25 +490,6 @@ struct TravState4 {
             node = st.pop();
             return false;
         }
-#if RR_BVH4_SORT
-        const float inf = __builtin_huge_valf();
-        ChildKey k[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            k[c].slot = c;
-            k[c].ref = ref[c];
-            k[c].t = (inner >> c) & 1u ? tn[c] : inf;
-        }
-        cswap(k[0], k[1]);
-        cswap(k[2], k[3]);
-        cswap(k[0], k[2]);
-        cswap(k[1], k[3]);
-        cswap(k[1], k[2]);
-        if (k[3].t != inf) st.push(k[3].ref);
-        if (k[2].t != inf) st.push(k[2].ref);
-        if (k[1].t != inf) st.push(k[1].ref);
-        node = k[0].ref;
-#else
         // nearest hit child next (ties: lower slot); the other hit children are
         // pushed in descending slot order (so they pop in slot order)
         int best = __builtin_ctz(inner);
@@ -617,7 +506,6 @@ struct TravState4 {
         if (rest & 2u) st.push(ref[1]);
         if (rest & 1u) st.push(ref[0]);
         node = best == 0 ? ref[0] : best == 1 ? ref[1] : best == 2 ? ref[2] : ref[3];
-#endif
         return false;
     }
 };
@@ -643,30 +531,63 @@ RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float
 }
 
 // ------------------------------------------------------------ materials ---
+// Blender 3.6 Cycles' Principled BSDF (v1) for the subset the scenes use:
+// base colour, metallic, specular, roughness (no transmission, clearcoat,
+// sheen, subsurface, anisotropy or specular tint). Restated from Cycles'
+// closure setup (intern/cycles/kernel/svm/closure.h, NODE_CLOSURE_BSDF /
+// CLOSURE_BSDF_PRINCIPLED_ID), bsdf_principled_diffuse.h
+// (PRINCIPLED_DIFFUSE_FULL) and the GGX-with-Fresnel microfacet closure
+// (bsdf_microfacet.h, interpolate_fresnel_color / fresnel_dielectric_cos in
+// bsdf_util.h); Cycles is third-party and not in the reference tree, so this
+// restatement is unpinned against Cycles' own output.
 struct Mat {
     float3 base;
     float metallic, specular, roughness, ior;
     float3 emission;
     int model;  // 0 Principled subset, 1 pure Lambert (analytic test scenes)
-    // per-material terms of the BSDF (mat_derive), the expressions the BSDF
-    // functions used to evaluate at every shading point, unchanged
-    float alpha, a2;   // GGX roughness alpha = max(roughness^2, 1e-4), alpha^2
-    float3 F0;         // Schlick F0 = lerp(0.08 specular, base, metallic)
-    float f0avg, wd;   // spec_prob's lobe weights
+    // per-material terms (mat_derive), evaluated once per material load
+    float alpha, a2;   // GGX roughness alpha = max(roughness^2, 1e-3), alpha^2
+    float3 cspec0;     // Cycles cspec0 = saturate(0.08 specular (1 - metallic) + base metallic)
+    float ior_s;       // specular IOR = 2 / (1 - sqrt(0.08 specular)) - 1
+    float f0d, f0n;    // F0 = fresnel_dielectric_cos(1, ior_s), 1 / (1 - F0)
+    float wd;          // diffuse closure sample weight = (1 - metallic) * average(base)
     float kd0;         // (1 - metallic) / pi
+    int spec_on;       // the specular closure exists (specular or metallic > 1e-5)
 };
 
+// Cycles fresnel_dielectric_cos: reflectance of a dielectric of relative IOR
+// eta at incidence cosine cosi, without the refracted direction (1 under TIR).
+RR_HD float fresnel_dielectric_cos(float cosi, float eta) {
+    const float c = fabsf(cosi);
+    float g = eta * eta - 1.0f + c * c;
+    if (g > 0.0f) {
+        g = sqrtf(g);
+        const float A = (g - c) / (g + c);
+        const float B = (c * (g + c) - 1.0f) / (c * (g - c) + 1.0f);
+        return 0.5f * A * A * (1.0f + B * B);
+    }
+    return 1.0f;
+}
+
+RR_HD float saturatef_(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
+
 RR_HD void mat_derive(Mat& m) {
+    // alpha floor 1e-3 (roughness 0.032): below it the float GGX terms break
+    // down (a2 - 1 rounds to -1, D = a2 / (pi tt^2) overflows at N.H = 1);
+    // Cycles switches to a singular mirror lobe below alpha^2 = 1e-7 instead
     float alpha = m.roughness * m.roughness;
-    if (alpha < 1.0e-4f) alpha = 1.0e-4f;
+    if (alpha < 1.0e-3f) alpha = 1.0e-3f;
     m.alpha = alpha;
     m.a2 = alpha * alpha;
-    const float s0 = 0.08f * m.specular;
-    m.F0 = mk3(s0 + (m.base.x - s0) * m.metallic, s0 + (m.base.y - s0) * m.metallic,
-               s0 + (m.base.z - s0) * m.metallic);
-    m.f0avg = (m.F0.x + m.F0.y + m.F0.z) * 0.333333343f;
+    const float sm = m.specular * 0.08f * (1.0f - m.metallic);
+    m.cspec0 = mk3(saturatef_(sm + m.base.x * m.metallic), saturatef_(sm + m.base.y * m.metallic),
+                   saturatef_(sm + m.base.z * m.metallic));
+    m.ior_s = 2.0f / (1.0f - sqrtf(0.08f * m.specular)) - 1.0f;
+    m.f0d = fresnel_dielectric_cos(1.0f, m.ior_s);
+    m.f0n = 1.0f / (1.0f - m.f0d);
     m.wd = (1.0f - m.metallic) * ((m.base.x + m.base.y + m.base.z) * 0.333333343f);
     m.kd0 = (1.0f - m.metallic) * 0.318309886183791f;
+    m.spec_on = (m.specular > 1.0e-5f || m.metallic > 1.0e-5f) ? 1 : 0;
 }
 
 RR_HD float schlick_w(float c) {
@@ -676,19 +597,25 @@ RR_HD float schlick_w(float c) {
     return m2 * m2 * m;
 }
 
-// Principled BSDF (v1) subset: Disney diffuse with retro-reflection + GGX
-// specular (Smith separable G, Schlick Fresnel from F0 = lerp(0.08*specular,
-// base, metallic)). Returns f and the combined one-sample-MIS pdf.
+// Cycles interpolate_fresnel_color: the dielectric Fresnel at cos, normalised
+// against its value at normal incidence, blends cspec0 towards white.
+RR_HD float fresnel_blend(const Mat& m, float cos_theta) {
+    return (fresnel_dielectric_cos(cos_theta, m.ior_s) - m.f0d) * m.f0n;
+}
+
 // Terms of the view direction shared by every evaluation at one shading point
-// (NEE and the sampled continuation): computed once, with exactly the
-// operations bsdf_eval used to repeat, so results are unchanged bit for bit.
+// (NEE and the sampled continuation): computed once per shading point.
 struct BsdfView {
     float cosV, ps, fv, g1v;
 };
 
-// Principled BSDF (v1) subset: Disney diffuse with retro-reflection + GGX
-// specular (Smith separable G, Schlick Fresnel from F0 = lerp(0.08*specular,
-// base, metallic)). Returns f and the combined one-sample-MIS pdf.
+// f (cosine not included) and the combined one-sample-MIS pdf of the two
+// closures (Cycles surface_shader_bsdf_eval: every closure evaluated, pdfs
+// weighted by the closures' sample weights):
+//   diffuse  base (1 - metallic) / pi * [(1 - FV/2)(1 - FL/2) + RR (FL + FV + FL FV (RR - 1))],
+//            RR = roughness (L.V + 1)            (PRINCIPLED_DIFFUSE_FULL)
+//   specular F * D G1(V) G1(L) / (4 cosV cosL), GGX D, separable Smith G1,
+//            F = cspec0 (1 - FH) + FH, FH = fresnel_blend(L.H)
 RR_HD float3 bsdf_eval_v(const Mat& m, const BsdfView& vw, float3 N, float3 wo, float3 wi, float& pdf) {
     const float cosV = vw.cosV;
     const float cosL = dot3(N, wi);
@@ -706,30 +633,33 @@ RR_HD float3 bsdf_eval_v(const Mat& m, const BsdfView& vw, float3 N, float3 wo, 
     const float NdotH = dot3(N, H);
     const float a2 = m.a2;
     // diffuse
-    const float fd90 = 0.5f + 2.0f * m.roughness * cosD * cosD;
     const float fl = schlick_w(cosL);
     const float fv = vw.fv;
-    const float kd = m.kd0 * (1.0f + (fd90 - 1.0f) * fl) * (1.0f + (fd90 - 1.0f) * fv);
+    const float rr = m.roughness * (dot3(wi, wo) + 1.0f);
+    const float kd = m.kd0 * ((1.0f - 0.5f * fv) * (1.0f - 0.5f * fl) + rr * (fl + fv + fl * fv * (rr - 1.0f)));
     // specular
     const float tt = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
     const float D = a2 / (3.14159265358979f * tt * tt);
     const float g1v = vw.g1v;
     const float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
-    const float3 F0 = m.F0;
-    const float fw = schlick_w(cosD);
-    const float ks = D * g1v * g1l / (4.0f * cosV * cosL);
-    const float3 F = mk3(F0.x + (1.0f - F0.x) * fw, F0.y + (1.0f - F0.y) * fw, F0.z + (1.0f - F0.z) * fw);
+    const float fh = fresnel_blend(m, cosD);
+    const float ks = m.spec_on ? D * g1v * g1l / (4.0f * cosV * cosL) : 0.0f;
+    const float3 c0 = m.cspec0;
+    const float3 F = mk3(c0.x * (1.0f - fh) + fh, c0.y * (1.0f - fh) + fh, c0.z * (1.0f - fh) + fh);
     const float pdf_d = cosL * 0.318309886183791f;
     const float pdf_s = g1v * D / (4.0f * cosV);
     pdf = (1.0f - ps) * pdf_d + ps * pdf_s;
     return mk3(m.base.x * kd + F.x * ks, m.base.y * kd + F.y * ks, m.base.z * kd + F.z * ks);
 }
 
-// Probability of picking the specular lobe.
+// Probability of picking the specular lobe: the closures' sample weights
+// (Cycles bsdf_microfacet_fresnel_color: the specular weight times the
+// average Fresnel colour at the view angle; diffuse: average(base) (1 - metallic)).
 RR_HD float spec_prob(const Mat& m, float cosV) {
-    if (m.model == 1) return 0.0f;
-    const float f0avg = m.f0avg;
-    const float wsp = f0avg + (1.0f - f0avg) * schlick_w(cosV);
+    if (m.model == 1 || !m.spec_on) return 0.0f;
+    const float fh = fresnel_blend(m, cosV);
+    const float3 c0 = m.cspec0;
+    const float wsp = ((c0.x * (1.0f - fh) + fh) + (c0.y * (1.0f - fh) + fh) + (c0.z * (1.0f - fh) + fh)) * 0.333333343f;
     const float tot = wsp + m.wd;
     return tot > 0.0f ? wsp / tot : 1.0f;
 }
@@ -774,12 +704,11 @@ RR_HD float3 sample_vndf(float3 v, float alpha, float dx, float dy) {
     return norm3(mk3(alpha * nh.x, alpha * nh.y, fmaxf(0.0f, nh.z)));
 }
 
-#ifndef RR_EXP_NOSPEC
-#define RR_EXP_NOSPEC 0  // timing experiment (wrong images): 1 = never sample the specular lobe
-#endif
-// Sample a direction; returns false when the path must end.
+// Sample a direction; returns false when the path must end. glossy: the
+// specular lobe was picked (Cycles LABEL_GLOSSY; else LABEL_DIFFUSE), which
+// decides the bounce counter the scatter advances.
 RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, float ul, float u1, float u2,
-                       float3& wi, float3& f, float& pdf) {
+                       float3& wi, float3& f, float& pdf, bool& glossy) {
     const float cosV = vw.cosV;
     if (cosV <= 0.0f) return false;
     const float ps = vw.ps;
@@ -787,7 +716,8 @@ RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, fl
     make_onb(N, T, B);
     float x, y;  // the disk sample both lobes start from
     concentric_disk(u1, u2, x, y);
-    if (RR_EXP_NOSPEC == 0 && ul < ps) {
+    glossy = ul < ps;
+    if (glossy) {
         const float3 wl = mk3(dot3(wo, T), dot3(wo, B), cosV);
         const float3 hl = sample_vndf(wl, m.alpha, x, y);
         const float3 H = mk3(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,

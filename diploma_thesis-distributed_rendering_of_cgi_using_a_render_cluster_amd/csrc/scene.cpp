@@ -2,6 +2,7 @@
 #include "scene.hpp"
 
 #include <cfloat>
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -635,15 +636,21 @@ SceneDesc load_scene(const std::string& path) {
         d.frame_end = (int)r.get_num("frame_end", d.frame_end);
         d.samples = (int)r.get_num("samples", d.samples);
         d.max_bounces = (int)r.get_num("max_bounces", d.max_bounces);
+        d.max_diffuse_bounces = (int)r.get_num("max_diffuse_bounces", d.max_diffuse_bounces);
+        d.max_glossy_bounces = (int)r.get_num("max_glossy_bounces", d.max_glossy_bounces);
         d.clamp_indirect = r.get_num("clamp_indirect", d.clamp_indirect);
         d.filter_width = r.get_num("filter_width", d.filter_width);
         d.exposure = r.get_num("exposure", d.exposure);
         d.seed = (uint32_t)r.get_num("seed", d.seed);
         d.spp_per_chunk = (int)r.get_num("spp_per_chunk", 0);
         d.view_transform_name = r.get_str("view_transform", "Standard");
-        // "Filmic" needs Blender's OCIO LUTs (not available offline, SURVEY §7 hard
-        // part c): rendered with the Standard transform; DESIGN.md §6 records it.
-        d.view_transform = d.view_transform_name == "Raw" ? VIEW_RAW : VIEW_STANDARD;
+        // "Filmic" is applied through Blender's OCIO LUTs when the context has
+        // them (rr_set_ocio_config); otherwise the frame falls back to Standard
+        // and says so (rr_frame_stats.view_transform_substituted).
+        if (d.view_transform_name == "Standard") d.view_transform = VIEW_STANDARD;
+        else if (d.view_transform_name == "Raw") d.view_transform = VIEW_RAW;
+        else if (d.view_transform_name == "Filmic") d.view_transform = VIEW_FILMIC;
+        else throw std::runtime_error("unsupported view transform: " + d.view_transform_name);
     }
     if (s.render.resx <= 0 || s.render.resy <= 0 || s.render.percent <= 0)
         throw std::runtime_error("invalid resolution");
@@ -812,12 +819,20 @@ FrameSetup setup_frame(const SceneDesc& s, int frame, const rr_render_params* p)
         throw std::runtime_error("invalid output resolution");
     f.spp = p->spp > 0 ? p->spp : r.samples;
     if (f.spp <= 0) f.spp = 1;
+    // Bounce caps as Cycles applies them (path_state_next): a scatter that
+    // takes a counter to its cap ends the path at the next hit. The camera hit
+    // always scatters, so a cap of 0 ("direct light only") acts as a cap of 1.
     f.max_bounces = p->max_bounces >= 0 ? p->max_bounces : r.max_bounces;
     if (f.max_bounces > 64) f.max_bounces = 64;
+    if (f.max_bounces < 1) f.max_bounces = 1;
+    f.max_diffuse = p->max_diffuse_bounces >= 0 ? p->max_diffuse_bounces : r.max_diffuse_bounces;
+    f.max_glossy = p->max_glossy_bounces >= 0 ? p->max_glossy_bounces : r.max_glossy_bounces;
+    f.max_diffuse = std::min(std::max(f.max_diffuse, 1), 0xffff);
+    f.max_glossy = std::min(std::max(f.max_glossy, 1), 0xffff);
     f.clamp_indirect = (float)(p->clamp_indirect >= 0.f ? p->clamp_indirect : r.clamp_indirect);
     f.seed = p->use_scene_seed ? r.seed : p->seed;
     f.view_transform = p->view_transform >= 0 ? p->view_transform : r.view_transform;
-    if (f.view_transform != VIEW_STANDARD && f.view_transform != VIEW_RAW)
+    if (f.view_transform != VIEW_STANDARD && f.view_transform != VIEW_RAW && f.view_transform != VIEW_FILMIC)
         throw std::runtime_error("unsupported view transform");
     f.spp_per_chunk = p->spp_per_chunk > 0 ? p->spp_per_chunk : r.spp_per_chunk;
     f.flags = p->flags;

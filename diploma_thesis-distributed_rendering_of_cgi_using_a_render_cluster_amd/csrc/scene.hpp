@@ -21,7 +21,7 @@ enum ObjType { OBJ_EMPTY = 0, OBJ_MESH = 1, OBJ_CAMERA = 2, OBJ_LIGHT = 3 };
 enum LightType { LIGHT_POINT = 0, LIGHT_SUN = 1 };
 enum Ipo { IPO_CONSTANT = 0, IPO_LINEAR = 1, IPO_BEZIER = 2 };
 enum SensorFit { FIT_AUTO = 0, FIT_HORIZONTAL = 1, FIT_VERTICAL = 2 };
-enum ViewTransform { VIEW_STANDARD = 0, VIEW_RAW = 1 };
+enum ViewTransform { VIEW_STANDARD = 0, VIEW_RAW = 1, VIEW_FILMIC = 2 };
 
 // Blender stores BezTriple coordinates as float; evaluation happens in float
 // (with double inside the cubic solver), see eval_fcurve().
@@ -107,7 +107,8 @@ struct RenderDesc {
     int resx = 1920, resy = 1080, percent = 100;
     double fps = 24;
     int frame_start = 1, frame_end = 250;
-    int samples = 128, max_bounces = 12;
+    // Cycles 3.6 defaults (scene.cycles): max_bounces 12, diffuse 4, glossy 4
+    int samples = 128, max_bounces = 12, max_diffuse_bounces = 4, max_glossy_bounces = 4;
     double clamp_indirect = 10.0, filter_width = 1.5, exposure = 0.0;
     int view_transform = VIEW_STANDARD;
     std::string view_transform_name = "Standard";
@@ -134,6 +135,7 @@ struct SceneDesc {
 // Everything the device needs for one frame (DESIGN.md §4 "frame constants").
 struct FrameSetup {
     int32_t W = 0, H = 0, spp = 0, max_bounces = 0, view_transform = 0, spp_per_chunk = 0, flags = 0;
+    int32_t max_diffuse = 4, max_glossy = 4;
     uint32_t seed = 0;
     float clamp_indirect = 0.f, filter_width = 1.5f, exposure_scale = 1.f;
     float cam[RR_CAM_FLOATS] = {};

@@ -186,9 +186,24 @@ __device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, i
 struct ShadeOut {
     bool cont, shadow;
     float3 o, d, T;          // continuation ray + throughput
+    uint32_t lob;            // continuation's lobe bounce counters (lobe_counts)
     float3 so, sd, sc;       // shadow ray + pending contribution
     float sdist;
 };
+
+// Per-lobe bounce counters of a path (Cycles path state diffuse_bounce /
+// glossy_bounce, intern/cycles/kernel/integrator/path_state.h path_state_next),
+// packed: diffuse scatters in bits 0..15, glossy scatters in bits 16..31.
+constexpr uint32_t kGlossyOne = 0x10000u;
+// Whether the path ends at this hit (emission only, no NEE, no scatter): the
+// scatter that brought it here advanced a counter to its cap. Cycles marks the
+// path PATH_RAY_TERMINATE_AFTER_TRANSPARENT when bounce >= max_bounce,
+// diffuse_bounce >= max_diffuse_bounce or glossy_bounce >= max_glossy_bounce
+// after the increment; the caps here are >= 1 (setup_frame), so a cap of 0
+// ("direct light only") behaves as Cycles': the camera hit still scatters once.
+RR_D bool path_capped(const FrameConsts& fc, int bounce, uint32_t lob) {
+    return bounce >= fc.max_bounces || (int)(lob & 0xffffu) >= fc.max_diffuse || (int)(lob >> 16) >= fc.max_glossy;
+}
 
 RR_D void add_to(float3& L, float3 c) {
     L.x = L.x + c.x;
@@ -196,13 +211,10 @@ RR_D void add_to(float3& L, float3 c) {
     L.z = L.z + c.z;
 }
 
-#ifndef RR_EXP_SHADE
-#define RR_EXP_SHADE 0  // timing experiments (wrong images): 1 no NEE, 2 no continuation
-#endif
 // K9: shade one path at `bounce` given its closest hit; L updated in place.
 template <typename View>
 __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const View& v, float3 o, float3 d,
-                                      float3 T, const Hit& h, uint32_t key, float3& L, ShadeOut& out) {
+                                      float3 T, uint32_t lob, const Hit& h, uint32_t key, float3& L, ShadeOut& out) {
     out.cont = false;
     out.shadow = false;
     if (h.idx < 0) {
@@ -227,12 +239,12 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
         add_to(L, c);
     }
-    if (bounce >= fc.max_bounces) return;
+    if (path_capped(fc, bounce, lob)) return;
     const BsdfView vw = bsdf_view(m, N, wo);
     const uint32_t dim0 = 2u + (uint32_t)(kDimsPerBounce * bounce);
     const float3 Po = offset_ray(P, N);
     // next-event estimation toward one uniformly chosen light
-    if (RR_EXP_SHADE != 1 && fc.n_lights > 0) {
+    if (fc.n_lights > 0) {
         int li = (int)(rng(key, dim0) * (float)fc.n_lights);
         if (li > fc.n_lights - 1) li = fc.n_lights - 1;
         const auto lt = v.lights + kLightF * li;
@@ -287,10 +299,11 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         }
     }
     // continue the path
-    if (RR_EXP_SHADE == 2) return;
     float3 wi, f;
     float pdf;
-    if (!bsdf_sample(m, vw, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f, pdf))
+    bool glossy;
+    if (!bsdf_sample(m, vw, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f, pdf,
+                     glossy))
         return;
     const float cosL = dot3(N, wi);
     if (!(cosL > 0.0f)) return;
@@ -306,6 +319,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     out.o = Po;
     out.d = wi;
     out.T = T;
+    out.lob = lob + (glossy ? kGlossyOne : 1u);
 }
 
 // K8: segmented queues, no atomics, no barriers. Each producer WAVE owns
@@ -333,7 +347,7 @@ __device__ __forceinline__ void emit(const ShadeOut& so, int pid, PathQueue out,
     if (so.cont) {
         const uint32_t s1 = seg_base + cur.c + (uint32_t)__popcll(mc & below);
         out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
-        out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, 0.0f);
+        out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, i2f((int)so.lob));
         out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, 0.0f);
     }
     if (so.shadow) {
@@ -421,6 +435,12 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
         atomicAdd(&tc[slot], a);
         atomicAdd(&tc[slot + 1], b);
     }
+}
+
+// Adds the number of active lanes whose predicate holds (one atomic per wave).
+RR_D void count_wave(uint32_t* __restrict__ ctr, bool pred) {
+    const uint64_t m = __ballot(pred);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(ctr, (uint32_t)__popcll(m));
 }
 
 // K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
@@ -651,7 +671,8 @@ RR_D void tile_mask(const FrameConsts& fc, const LdsView& v, int n_tris, float x
 template <bool kCount, typename View>
 RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, PathQueue out,
                        ShadowQueue sq, uint32_t seg_cap, uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
-                       int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
+                       int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
+                       uint32_t* __restrict__ traced) {
     const int stride = gridDim.x * kBlock;
     TravStack st{stack, spill, stride, 0};
     TravCount cnt;
@@ -664,13 +685,13 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, Pa
         const int p = b0 + (int)threadIdx.x;
         ShadeOut so;
         so.cont = so.shadow = false;
+        bool culled = true;
         if (p < np) {
             const int sl = (int)fc.div_npix.div((uint32_t)p);
             const int pix = p - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             float3 o, d;
             float tmin, tmax;
-            bool culled;
             camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
             Hit h;
             if constexpr (std::is_same<View, LdsView>::value) {  // LDS scenes: every triangle (camera_hit)
@@ -679,17 +700,10 @@ RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, Pa
             } else
                 traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cnt);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
-#if RR_EXP_PRIMARY == 1  // timing experiment only: no shading
-            L = mk3(h.t, (float)h.idx, 0.0f);
-#elif RR_EXP_PRIMARY == 2  // timing experiment only: no traversal
-            h.idx = (pix & 3) == 0 ? (pix >> 2) % 12 : -1;
-            h.t = 10.0f;
-            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
-#else
-            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
-#endif
+            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), 0u, h, key, L, so);
             rad.put(p, L);
         }
+        count_wave(traced, !culled && fc.n_tris > 0);
         emit(so, p, out, sq, seg_base, cur);
     }
     publish(cur, seg_c, seg_s);
@@ -704,16 +718,16 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_primary(FrameConsts 
                                                     PathQueue out, ShadowQueue sq, uint32_t seg_cap,
                                                     uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
                                                     int32_t* __restrict__ spill,
-                                                    unsigned long long* __restrict__ tc) {
+                                                    unsigned long long* __restrict__ tc, uint32_t* __restrict__ traced) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     lds_int* stack = lds_slot(lds_stack);
     if constexpr (kLds) {
         extern __shared__ float4 dyn4[];
         int used;
         const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used, &fc);
-        primary_body<kCount>(fc, v, np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack);
+        primary_body<kCount>(fc, v, np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack, traced);
     } else {
-        primary_body<kCount>(fc, global_view(sa), np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack);
+        primary_body<kCount>(fc, global_view(sa), np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack, traced);
     }
 }
 
@@ -756,7 +770,7 @@ RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueu
             const int pix = pid - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             float3 L = rad.get(pid);
-            shade(fc, bounce, v, o, d, xyz(c), h, key, L, so);
+            shade(fc, bounce, v, o, d, xyz(c), (uint32_t)f2i(b.w), h, key, L, so);
             rad.put(pid, L);
         }
         emit(so, pid, out, sq, seg_base, cur);
@@ -796,10 +810,6 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_extend(FrameConsts f
 #endif
 constexpr int kTailBounce = RR_TAIL_BOUNCE;
 
-RR_D void count_wave(uint32_t* __restrict__ ctr, bool pred) {
-    const uint64_t m = __ballot(pred);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(ctr, (uint32_t)__popcll(m));
-}
 
 template <bool kCount, typename View>
 RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue in, const SegIndex& ix, int count,
@@ -812,7 +822,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
         const int j = b0 + (int)threadIdx.x;
         bool live = j < count;
         float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = o, L = o;
-        uint32_t key = 0;
+        uint32_t key = 0, lob = 0;
         int pid = 0;
         if (live) {
             const uint32_t i = ix.slot((uint32_t)j);
@@ -821,6 +831,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
             o = xyz(a);
             d = xyz(b);
             T = xyz(c);
+            lob = (uint32_t)f2i(b.w);
             const int sl = (int)fc.div_npix.div((uint32_t)pid);
             const int pix = pid - sl * fc.npix;
             key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
@@ -833,7 +844,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
             if (live) {
                 Hit h;
                 traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cc);
-                shade(fc, b, v, o, d, T, h, key, L, so);
+                shade(fc, b, v, o, d, T, lob, h, key, L, so);
                 if (so.shadow) {
                     Hit hs;
                     if (!traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs, cs)) {
@@ -846,6 +857,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
                     o = so.o;
                     d = so.d;
                     T = so.T;
+                    lob = so.lob;
                 } else {
                     live = false;
                 }
@@ -952,16 +964,11 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
 #define RR_TRACE_WAVES 7
 #endif
 constexpr int kRefillBelow = RR_REFILL_BELOW;
-// Hierarchy of the split path: 4 = BVH4 collapse (Bvh4Node), 2 = the LBVH.
-#ifndef RR_SPLIT_WIDTH
-#define RR_SPLIT_WIDTH 2
-#endif
+// Hierarchy of the split path: the PLOC BVH2 (a BVH4 collapse measured
+// slower: VGPR spills in the trace kernels).
 template <bool kAnyHit, bool kCount>
-using SplitTrav = std::conditional_t<RR_SPLIT_WIDTH == 4, TravState4<kAnyHit, kCount>, TravState<kAnyHit, kCount>>;
-RR_D auto split_nodes(const SceneArgs& sa) {
-    if constexpr (RR_SPLIT_WIDTH == 4) return sa.nodes4;
-    else return sa.nodes;
-}
+using SplitTrav = TravState<kAnyHit, kCount>;
+RR_D const BvhNode* split_nodes(const SceneArgs& sa) { return sa.nodes; }
 constexpr int kQGroups = 64;   // append groups per queue (one lane each in QueueMap)
 constexpr int kQStride = 32;   // words between group counters (128 B)
 
@@ -1085,7 +1092,7 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
     if (so.cont) {
         const uint32_t s1 = bc + (uint32_t)__popcll(mc & below);
         out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
-        out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, 0.0f);
+        out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, i2f((int)so.lob));
         out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, 0.0f);
     }
     if (so.shadow) {
@@ -1101,11 +1108,13 @@ template <bool kCount>
 __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
                                                                           float2* __restrict__ hits,
                                                                           int32_t* __restrict__ spill,
-                                                                          unsigned long long* __restrict__ tc) {
+                                                                          unsigned long long* __restrict__ tc,
+                                                                          uint32_t* __restrict__ traced) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
+    uint32_t n_traced = 0;  // camera rays of this lane that are not culled
     trace_refill<SplitTrav<false, kCount>>(
         split_nodes(sa), sa.tris, sa.n_tris, np, st, cnt, [](int p) { return (uint32_t)p; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
@@ -1114,8 +1123,11 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameC
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             bool culled;  // culled: tmax = -1 < tmin, every box test fails, the ray misses
             camera_ray(fc, sa.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
+            n_traced += culled ? 0u : 1u;
         },
         [&](int p, uint32_t, const Hit& h) { hits[p] = pack_hit(h); });
+    for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
+    if ((threadIdx.x & 63) == 0 && n_traced) atomicAdd(traced, n_traced);
     if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
 }
 
@@ -1139,7 +1151,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
             camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax);
             const Hit h = unpack_hit(hits[p]);
             float3 L = mk3(0.0f, 0.0f, 0.0f);
-            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), h, key, L, so);
+            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), 0u, h, key, L, so);
             rad.put(p, L);
         }
         emit_grouped(so, p, out, sq, qo);
@@ -1194,7 +1206,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
             const int pix = pid - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             float3 L = rad.get(pid);
-            shade(fc, bounce, v, xyz(a), xyz(b), xyz(c), h, key, L, so);
+            shade(fc, bounce, v, xyz(a), xyz(b), xyz(c), (uint32_t)f2i(b.w), h, key, L, so);
             rad.put(pid, L);
         }
         emit_grouped(so, pid, out, sq, qo);
@@ -1301,12 +1313,6 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
 // and shading work, so the long tiles start early and the background tiles,
 // whose samples are all culled camera rays, fill the tail.
 constexpr int kTile = 8;  // 8x8 pixels = one wave
-#ifndef RR_TILES_PEEL
-#define RR_TILES_PEEL 0  // 1: bounce 0 outside the bounce loop (two inlined shade() copies, more spills)
-#endif
-#ifndef RR_EXP_TILES
-#define RR_EXP_TILES 0  // timing experiments (wrong images): 1 no shading, 2 no shadow rays, 3 no extension rays
-#endif
 
 struct TileOrder {
     int tx, n;               // tiles per row, tiles in the frame
@@ -1401,12 +1407,15 @@ RR_D TileOrder uniform_order(TileOrder t) {
 // Per-lane ray counts of the tile kernel, reduced once per wave at exit into
 // the chunk-0 counter pairs: {0, 1} = bounce 0, {2, 3} = all later bounces
 // (rr_api.cpp fill_stats sums the pairs).
-RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint32_t c1, uint32_t s1) {
+RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint32_t c1, uint32_t s1, uint32_t* __restrict__ traced,
+                     uint32_t t0) {
     // the counts are wave totals already (wave_count): lane 0 adds them
     const uint32_t v[4] = {c0, s0, c1, s1};
-    if ((threadIdx.x & 63) == 0)
+    if ((threadIdx.x & 63) == 0) {
         for (int k = 0; k < 4; ++k)
             if (v[k]) atomicAdd(&tot[k], v[k]);
+        if (t0) atomicAdd(traced, t0);
+    }
 }
 
 // Active lanes of the wave whose predicate holds: the tile kernel's ray
@@ -1441,7 +1450,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     const int stride = gridDim.x * kBlock;
     TravStack st{stack, spill, stride, 0};
     TravCount cp, ce, cs;
-    uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0;
+    uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0, n_t0 = 0;
     // The screen rectangle and the tile order come from the root node in LDS,
     // so the compiler cannot tell they are wave-uniform and would keep (and
     // spill) them in VGPRs for the whole kernel: every lane holds the same
@@ -1496,74 +1505,15 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         uint64_t cm0, cm1;
         tile_mask(fc, v, fc.n_tris, (float)(tx * kTile), (float)(tx * kTile + kTile - 1), (float)(ty * kTile),
                   (float)(ty * kTile + kTile - 1), cm0, cm1);
-#if RR_TILES_PEEL
-        const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
-        for (int s = s_lo; s < s_hi; ++s) {
-            const uint32_t key = sample_key(pk, (uint32_t)s);
-            float3 L = mk3(0.0f, 0.0f, 0.0f), T = mk3(1.0f, 1.0f, 1.0f), o = L, d = L;
-            ShadeOut so;
-            so.cont = so.shadow = false;
-            // bounce 0, peeled: the camera ray against the tile's triangles
-            if (valid) {
-                float tmin, tmax;
-                bool culled;
-                camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
-                Hit h;
-                set_miss(h, tmax);
-                if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);  // wave-uniform masks
-#if RR_EXP_TILES == 1  // timing experiment only: camera rays, no shading
-                L = mk3(h.t, (float)h.idx, 0.0f);
-#else
-                shade(fc, 0, v, o, d, T, h, key, L, so);
-#endif
-                n_c0 += wave_count(so.cont);
-                n_s0 += wave_count(so.shadow);
-            }
-            if (so.shadow) {
-                Hit hs;
-                if (!traverse<true, kCount>(v.nodes, v.tris, RR_EXP_TILES == 2 ? 0 : fc.n_tris, so.so, so.sd, 0.0f,
-                                            so.sdist, st, hs, cs))
-                    add_to(L, so.sc);
-            }
-            bool live = so.cont;
-            if (live) {
-                o = so.o;
-                d = so.d;
-                T = so.T;
-            }
-            for (int b = 1; b <= fc.max_bounces; ++b) {
-                if (!__any(live)) break;
-                if (live) {
-                    ShadeOut sb;
-                    Hit h;
-                    traverse<false, kCount>(v.nodes, v.tris, RR_EXP_TILES == 3 ? 0 : fc.n_tris, o, d, 0.0f, kFltMax,
-                                            st, h, ce);
-                    shade(fc, b, v, o, d, T, h, key, L, sb);
-                    if (sb.shadow) {
-                        Hit hs;
-                        if (!traverse<true, kCount>(v.nodes, v.tris, RR_EXP_TILES == 2 ? 0 : fc.n_tris, sb.so, sb.sd,
-                                                    0.0f, sb.sdist, st, hs, cs))
-                            add_to(L, sb.sc);
-                    }
-                    n_c1 += wave_count(sb.cont);
-                    n_s1 += wave_count(sb.shadow);
-                    if (sb.cont) {
-                        o = sb.o;
-                        d = sb.d;
-                        T = sb.T;
-                    } else {
-                        live = false;
-                    }
-                }
-            }
-#else
         const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
         for (int s = s_lo; s < s_hi; ++s) {
             const uint32_t key = sample_key(pk, (uint32_t)s);
             float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = mk3(1.0f, 1.0f, 1.0f), L = o;
+            uint32_t lob = 0;
             float tmin = 0.0f, tmax = -1.0f;
             bool culled = true;
             if (valid) camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
+            n_t0 += wave_count(!culled && (cm0 | cm1) != 0);
             bool live = valid;
             for (int b = 0; b <= fc.max_bounces; ++b) {
                 if (!__any(live)) break;
@@ -1574,19 +1524,13 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                         set_miss(h, tmax);
                         if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);
                     } else {
-                        traverse<false, kCount>(v.nodes, v.tris, RR_EXP_TILES == 3 ? 0 : fc.n_tris, o, d, 0.0f,
-                                                kFltMax, st, h, ce);
+                        traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, ce);
                     }
-#if RR_EXP_TILES == 1  // timing experiment only: camera rays, no shading
-                    so.cont = so.shadow = false;
-                    L = mk3(h.t, (float)h.idx, 0.0f);
-#else
-                    shade(fc, b, v, o, d, T, h, key, L, so);
-#endif
+                    shade(fc, b, v, o, d, T, lob, h, key, L, so);
                     if (so.shadow) {
                         Hit hs;
-                        if (!traverse<true, kCount>(v.nodes, v.tris, RR_EXP_TILES == 2 ? 0 : fc.n_tris, so.so, so.sd,
-                                                    0.0f, so.sdist, st, hs, cs))
+                        if (!traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs,
+                                                    cs))
                             add_to(L, so.sc);
                     }
                     if (b == 0) {
@@ -1600,12 +1544,12 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                         o = so.o;
                         d = so.d;
                         T = so.T;
+                        lob = so.lob;
                     } else {
                         live = false;
                     }
                 }
             }
-#endif
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
@@ -1622,7 +1566,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             out[pix] = tonemap(fc, acc, srgb);
         }
     }
-    flush_rays(tot, n_c0, n_s0, n_c1, n_s1);
+    flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tot + camera_traced_slot(fc.max_bounces), n_t0);
     if (kCount) {
         flush_counts(tc, 0, cp.nodes, cp.tris);
         flush_counts(tc, 2, ce.nodes, ce.tris);
@@ -1749,13 +1693,14 @@ int device_cu_count() {
 }
 
 // Per chunk, one pair per bounce b = 0..max_bounces: {paths entering bounce
-// b+1, shadow rays of bounce b}, written by the consuming kernels (+1 pair of
-// slack).
-int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2); }
+// b+1, shadow rays of bounce b}, written by the consuming kernels, +1 pair of
+// slack (k_tiles' unit counter), then camera rays traced (not culled, tested
+// against at least one triangle) and a spare word.
+int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2) + 2; }
 
 namespace {
 using PrimaryFn = void (*)(FrameConsts, SceneArgs, int, Rad, PathQueue, ShadowQueue, uint32_t, uint32_t*,
-                           uint32_t*, int32_t*, unsigned long long*);
+                           uint32_t*, int32_t*, unsigned long long*, uint32_t*);
 using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, PathQueue, ShadowQueue, SegOut,
                           int32_t*, unsigned long long*);
 using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, Rad, int32_t*, unsigned long long*);
@@ -1815,7 +1760,6 @@ size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
 }
 }  // namespace
 
-int split_bvh_width() { return RR_SPLIT_WIDTH; }
 
 bool scene_in_lds(int n_tris, int n_mats, int n_lights) {
     FrameConsts fc{};
@@ -1866,7 +1810,7 @@ struct Grids {
 // Launch geometry of the split (trace / shade) path of large scenes.
 struct SplitGrids {
     int trace_p, trace_e, shadow, shade_p, shade_e;
-    void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*);
+    void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
     explicit SplitGrids(bool count) {
@@ -1964,7 +1908,8 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         if ((size_t)std::max(cap_p, cap_e) * kQGroups > p.cap)
             throw std::runtime_error("queue capacity exceeded (split path)");
         pr.begin(st, RR_K_PRIMARY);
-        G.ktp<<<clamp_grid(np, G.trace_p), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc);
+        G.ktp<<<clamp_grid(np, G.trace_p), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc,
+                                                             tot + camera_traced_slot(base.max_bounces));
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
         k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq,
@@ -2060,7 +2005,6 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
                        std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
     if (!G.lds && base.n_tris > 0) {
-        if (RR_SPLIT_WIDTH == 4 && !s.has4) throw std::runtime_error("split path needs the BVH4 (scene built without it)");
         render_split(p, base, n_chunks, st, sa, tc, pq, sq);
         RR_HIP(hipGetLastError());
         return;
@@ -2080,7 +2024,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         const uint32_t cap_p = seg_cap(np, gp), cap_e = seg_cap(np, ge);
         pr.begin(st, RR_K_PRIMARY);
         G.kp<<<gp, kBlock, G.dyn_primary, st>>>(fc, sa, np, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq, cap_p, seg(0, 0), seg(0, 1),
-                                                p.spill.ptr, tc);
+                                                p.spill.ptr, tc, tot + camera_traced_slot(base.max_bounces));
         pr.end(st);
         int g_prev = gp;  // grid of the producer of the current queues
         uint32_t cap_prev = cap_p;

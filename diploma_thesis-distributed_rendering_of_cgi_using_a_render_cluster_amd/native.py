@@ -20,8 +20,9 @@ SHIM_PATH = os.path.join(_HERE, "lib", "rr-blender-shim")
 RR_OK, RR_ENOENT, RR_EIO, RR_ENOMEM, RR_ENODEV, RR_EINVAL, RR_ENOTSUP = 0, -2, -5, -12, -19, -22, -95
 RR_EBUSY = -16
 RR_MAX_FRAMES_IN_FLIGHT = 2
-RR_VIEW_SCENE, RR_VIEW_STANDARD, RR_VIEW_RAW = -1, 0, 1
-RR_CAM_FLOATS, RR_LIGHT_FLOATS, RR_MAT_FLOATS, RR_RENDER_INTS, RR_RENDER_FLOATS = 16, 12, 12, 8, 4
+RR_VIEW_SCENE, RR_VIEW_STANDARD, RR_VIEW_RAW, RR_VIEW_FILMIC = -1, 0, 1, 2
+RR_ABI_VERSION = 2
+RR_CAM_FLOATS, RR_LIGHT_FLOATS, RR_MAT_FLOATS, RR_RENDER_INTS, RR_RENDER_FLOATS = 16, 12, 12, 10, 4
 
 
 class RRError(RuntimeError):
@@ -35,7 +36,8 @@ class RenderParams(ctypes.Structure):
                 ("clamp_indirect", ctypes.c_float), ("seed", ctypes.c_uint32),
                 ("use_scene_seed", ctypes.c_int32), ("width", ctypes.c_int32),
                 ("height", ctypes.c_int32), ("view_transform", ctypes.c_int32),
-                ("spp_per_chunk", ctypes.c_int32), ("flags", ctypes.c_int32)]
+                ("spp_per_chunk", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("max_diffuse_bounces", ctypes.c_int32), ("max_glossy_bounces", ctypes.c_int32)]
 
 
 class FrameTiming(ctypes.Structure):
@@ -54,7 +56,9 @@ class FrameStats(ctypes.Structure):
                 ("bvh_rebuilt", ctypes.c_int32), ("n_triangles", ctypes.c_int32),
                 ("output_bytes", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_int32 * 8),
-                ("trav_nodes", ctypes.c_uint64 * 3), ("trav_tris", ctypes.c_uint64 * 3)]
+                ("trav_nodes", ctypes.c_uint64 * 3), ("trav_tris", ctypes.c_uint64 * 3),
+                ("camera_rays_traced", ctypes.c_uint64), ("view_transform", ctypes.c_int32),
+                ("view_transform_substituted", ctypes.c_int32)]
 
     def as_dict(self) -> dict:
         out = {}
@@ -73,6 +77,7 @@ EXPORTS = [
     "rr_render_params_default", "rr_abi_version", "rr_create", "rr_scene_load", "rr_render_frame",
     "rr_frame_submit", "rr_frame_complete",
     "rr_render_frame_to_memory", "rr_scene_resolution", "rr_encode_image", "rr_last_error",
+    "rr_last_warning", "rr_set_ocio_config", "rr_synchronize",
     "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
     "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_bvh4", "rr_debug_bvh_hier", "rr_debug_jpeg_device",
 ]
@@ -91,6 +96,9 @@ def lib() -> ctypes.CDLL:
         raise RRError(RR_ENOENT, f"{path} is missing: build it with __graft_entry__.build() "
                                  "(there is no CPU fallback)")
     L = ctypes.CDLL(path)
+    if L.rr_abi_version() != RR_ABI_VERSION:
+        raise RRError(RR_EINVAL, f"{path}: ABI {L.rr_abi_version()}, this binding expects {RR_ABI_VERSION} "
+                                 "(rebuild with __graft_entry__.build())")
     P, c_int, i32, u32, f32p, u8p = ctypes.c_void_p, ctypes.c_int, ctypes.c_int32, ctypes.c_uint32, \
         ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint8)
     i32p, u32p = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint32)
@@ -110,6 +118,9 @@ def lib() -> ctypes.CDLL:
         "rr_encode_image": (c_int, [u8p, i32, i32, ctypes.c_char_p, ctypes.c_char_p, i32,
                                     ctypes.POINTER(ctypes.c_uint64)]),
         "rr_last_error": (ctypes.c_char_p, [P]),
+        "rr_last_warning": (ctypes.c_char_p, [P]),
+        "rr_set_ocio_config": (c_int, [P, ctypes.c_char_p]),
+        "rr_synchronize": (c_int, [P]),
         "rr_scene_free": (None, [P]),
         "rr_destroy": (None, [P]),
         "rr_debug_counts": (c_int, [P, i32p, i32p, i32p, i32p]),
@@ -164,7 +175,7 @@ class FrameState:
     lights: np.ndarray      # (nl, 12)
     materials: np.ndarray   # (nm, 12)
     world: np.ndarray       # (3,)
-    render_ints: np.ndarray  # (8,)
+    render_ints: np.ndarray  # (RR_RENDER_INTS,)
     render_floats: np.ndarray  # (4,)
 
 
@@ -245,6 +256,18 @@ class RenderContext:
 
     def load_scene(self, path: str) -> Scene:
         return Scene(path, self)
+
+    def set_ocio_config(self, directory: str | None):
+        """rr_set_ocio_config: Blender colour-management directory whose Filmic
+        LUTs implement RR_VIEW_FILMIC (None: none; Filmic falls back to Standard)."""
+        _check(lib().rr_set_ocio_config(self.handle, directory.encode() if directory else None), self.handle)
+
+    def synchronize(self):
+        """rr_synchronize: wait for all device work this context enqueued."""
+        _check(lib().rr_synchronize(self.handle), self.handle)
+
+    def last_warning(self) -> str:
+        return lib().rr_last_warning(self.handle).decode("utf-8", "replace")
 
     def render_frame(self, scene: Scene, frame: int, params: RenderParams | None = None,
                      out_path: str | None = None, fmt: str | None = "JPEG", quality: int = 90):

@@ -39,12 +39,28 @@ class FrameRenderTime:
     exited_process_at: float
 
     @classmethod
-    def from_timing(cls, started_process_at: float, timing, exited_process_at: float) -> "FrameRenderTime":
-        """PartialRenderStatistics::with_process_information (utilities.rs:23-37)."""
-        return cls(as_utc_seconds(started_process_at), as_utc_seconds(timing.loaded_at),
-                   as_utc_seconds(timing.started_rendering_at), as_utc_seconds(timing.finished_rendering_at),
-                   as_utc_seconds(timing.file_saving_started_at), as_utc_seconds(timing.file_saving_finished_at),
-                   as_utc_seconds(exited_process_at))
+    def from_timing(cls, started_process_at: float, timing, exited_process_at: float,
+                    not_before: float | None = None) -> "FrameRenderTime":
+        """PartialRenderStatistics::with_process_information (utilities.rs:23-37).
+
+        not_before: exited_process_at of the worker's previous frame when this
+        frame was submitted while that one was still in flight (two frames in
+        flight, BackendRunner.render_frames / WorkerAutomaticQueue). The
+        reference's per-worker accounting (WorkerPerformance::from_worker_trace,
+        shared/src/results/performance.rs:70-130) needs consecutive frames
+        that do not overlap: idle = started_process_at - previous
+        exited_process_at must not be negative (`to_std()` fails otherwise).
+        The frame's record therefore starts when the previous one ended, and
+        every later timestamp is kept at or after its predecessor, so the seven
+        stay ordered."""
+        vals = [as_utc_seconds(v) for v in (started_process_at, timing.loaded_at, timing.started_rendering_at,
+                                             timing.finished_rendering_at, timing.file_saving_started_at,
+                                             timing.file_saving_finished_at, exited_process_at)]
+        if not_before is not None:  # compared as serialised (truncated) values: equal floats, zero idle
+            vals[0] = max(vals[0], not_before)
+            for k in range(1, len(vals)):
+                vals[k] = max(vals[k], vals[k - 1])
+        return cls(*vals)
 
     def total_execution_time(self) -> float:
         d = self.exited_process_at - self.started_process_at

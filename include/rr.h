@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 1
+#define RR_ABI_VERSION 2
 
 /* error codes (negative errno values) */
 #define RR_OK 0
@@ -52,6 +52,10 @@ typedef struct rr_scene rr_scene;
 #define RR_VIEW_SCENE (-1)  /* use the scene file's setting */
 #define RR_VIEW_STANDARD 0  /* sRGB OETF, Blender "Standard" */
 #define RR_VIEW_RAW 1       /* linear values, clamped, no OETF */
+#define RR_VIEW_FILMIC 2    /* Blender "Filmic" (display sRGB, look None) through the OCIO LUTs of a
+                             * Blender colour-management directory (rr_set_ocio_config); without
+                             * them the frame is rendered with Standard and flagged
+                             * (rr_frame_stats.view_transform_substituted, rr_last_warning) */
 
 /* Render parameters. Any field left at its "use scene" value takes the value
  * exported from the project (scene file "render" block). Zero-initialising the
@@ -67,6 +71,8 @@ typedef struct rr_render_params {
     int32_t view_transform; /* RR_VIEW_* */
     int32_t spp_per_chunk;  /* samples in flight per wavefront chunk; <= 0: auto */
     int32_t flags;          /* RR_FLAG_* (measurement modes; 0 in production) */
+    int32_t max_diffuse_bounces; /* Cycles max_diffuse_bounces (scene default 4); < 0: scene */
+    int32_t max_glossy_bounces;  /* Cycles max_glossy_bounces (scene default 4); < 0: scene */
 } rr_render_params;
 
 /* Measurement flags (rr_render_params.flags). */
@@ -121,6 +127,12 @@ typedef struct rr_frame_stats {
     /* RR_FLAG_COUNT_TRAVERSAL: BVH nodes visited / triangles tested over the
      * frame, per traversal kernel: [0] primary, [1] extend, [2] shadow */
     uint64_t trav_nodes[3], trav_tris[3];
+    /* camera rays actually traced: camera_rays counts W*H*spp, of which the
+     * ones outside the scene's screen rectangle (or meeting no triangle of
+     * their tile) are resolved as background without a traversal */
+    uint64_t camera_rays_traced;
+    int32_t view_transform;            /* RR_VIEW_* the frame was rendered with */
+    int32_t view_transform_substituted;/* 1: the scene asked for Filmic, no LUTs were configured, Standard used */
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */
@@ -174,6 +186,10 @@ int rr_frame_submit(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
 int rr_frame_complete(rr_ctx* ctx, uint64_t ticket, rr_frame_timing* timing,
                       rr_frame_stats* stats);
 
+/* Wait until every piece of device work ctx has enqueued (frames in flight
+ * included) has finished; their tickets still have to be completed. */
+int rr_synchronize(rr_ctx* ctx);
+
 /* Render one frame into caller memory (no file). film_rgba: W*H*4 floats of
  * mean linear radiance (alpha = 1); rgba8: W*H*4 bytes after the view
  * transform. Either may be NULL. Rows are top to bottom. */
@@ -201,6 +217,19 @@ int rr_debug_jpeg_device(rr_ctx* ctx, const uint8_t* rgba8, int32_t width, int32
 /* Thread-local message of the last failure on this thread (ctx may be NULL). */
 const char* rr_last_error(rr_ctx* ctx);
 
+/* Warning of ctx's last completed frame ("" if none), e.g. a Filmic view
+ * transform rendered as Standard because no OCIO LUTs are configured. Valid
+ * until the next call on ctx. */
+const char* rr_last_warning(rr_ctx* ctx);
+
+/* Blender colour-management directory (datafiles/colormanagement: config.ocio
+ * and luts/) whose Filmic LUTs (filmic_desat65cube.spi3d,
+ * filmic_to_0-70_1-03.spi1d) implement RR_VIEW_FILMIC on ctx. NULL or "":
+ * no LUTs (Filmic frames fall back to Standard, flagged). rr_create reads
+ * the RR_OCIO_DIR environment variable the same way. RR_ENOENT / RR_EINVAL
+ * if the LUT files are missing or malformed (ctx keeps no LUTs then). */
+int rr_set_ocio_config(rr_ctx* ctx, const char* dir);
+
 void rr_scene_free(rr_scene* scene);
 void rr_destroy(rr_ctx* ctx);
 
@@ -213,7 +242,8 @@ void rr_destroy(rr_ctx* ctx);
 #define RR_CAM_FLOATS 16   /* pos3 right3 up3 back3 half_w half_h clip_start clip_end */
 #define RR_LIGHT_FLOATS 12 /* type pos3 dir3 radius intensity3 pad */
 #define RR_MAT_FLOATS 12   /* base3 metallic specular roughness ior emission3 model pad */
-#define RR_RENDER_INTS 8   /* W H spp max_bounces seed view_transform spp_per_chunk bvh_width */
+#define RR_RENDER_INTS 10  /* W H spp max_bounces seed view_transform spp_per_chunk bvh_width
+                              max_diffuse_bounces max_glossy_bounces */
 #define RR_RENDER_FLOATS 4 /* clamp_indirect filter_width exposure_scale pad */
 
 int rr_debug_counts(rr_scene* scene, int32_t* n_triangles, int32_t* n_lights,

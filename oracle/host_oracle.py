@@ -382,3 +382,146 @@ def parse_blender_stdout(stdout: str) -> dict:
             "finished_rendering_at": f64_to_utc(fin),
             "file_saving_started_at": f64_to_utc(fin),
             "file_saving_finished_at": f64_to_utc(raw["project_finished_rendering_at"])}
+
+
+# --------------------------------------------------------------- OCIO LUTs --
+# Readers of OpenColorIO's Sony Pictures Imageworks LUT formats, restated from
+# the formats' published layout (OCIO FileFormatSpi3D / FileFormatSpi1D), for
+# the Filmic view transform of Blender 3.6's colour-management config
+# (csrc/view.hpp). Independent of the product's C++ parser: the parity tests
+# feed these arrays to the oracle and the files to the product.
+
+def parse_spi3d(path: str) -> np.ndarray:
+    """.spi3d: 'SPILUT 1.0', '3 3', 'N N N', then 'i j k r g b' per entry (i =
+    red index). Returns the cube as (N, N, N, 3) float32 indexed [i, j, k]."""
+    with open(path) as fh:
+        lines = fh.read().splitlines()
+    if not lines or not lines[0].startswith("SPILUT"):
+        raise ValueError(f"{path}: not an SPILUT file")
+    n = [int(x) for x in lines[2].split()]
+    if len(n) != 3 or len(set(n)) != 1:
+        raise ValueError(f"{path}: bad cube size")
+    n = n[0]
+    cube = np.zeros((n, n, n, 3), np.float32)
+    seen = np.zeros((n, n, n), bool)
+    for ln in lines[3:]:
+        f = ln.split()
+        if not f:
+            continue
+        i, j, k = (int(x) for x in f[:3])
+        cube[i, j, k] = [np.float32(float(x)) for x in f[3:6]]
+        seen[i, j, k] = True
+    if not seen.all():
+        raise ValueError(f"{path}: missing cube entries")
+    return cube
+
+
+def parse_spi1d(path: str) -> dict:
+    """.spi1d: 'Version 1', 'From lo hi', 'Length N', 'Components C', '{',
+    N rows of C values, '}'. Returns {"lut1": (N, C) float32, "lo1", "hi1"}."""
+    with open(path) as fh:
+        toks_lines = fh.read().splitlines()
+    lo, hi, n, comps, body = 0.0, 1.0, None, None, []
+    it = iter(toks_lines)
+    for ln in it:
+        f = ln.split()
+        if not f or f[0] == "Version":
+            continue
+        if f[0] == "From":
+            lo, hi = float(f[1]), float(f[2])
+        elif f[0] == "Length":
+            n = int(f[1])
+        elif f[0] == "Components":
+            comps = int(f[1])
+        elif f[0] == "{":
+            for ln2 in it:
+                for t in ln2.split():
+                    if t == "}":
+                        break
+                    body.append(np.float32(float(t)))
+                else:
+                    continue
+                break
+            break
+    lut = np.array(body, np.float32).reshape(n, comps)
+    return {"lut1": lut, "lo1": np.float32(lo), "hi1": np.float32(hi)}
+
+
+FILMIC_LUT_FILES = ("filmic_desat65cube.spi3d", "filmic_to_0-70_1-03.spi1d")
+
+
+def load_filmic_luts(directory: str) -> dict:
+    """The two Filmic LUTs under a Blender colour-management directory (or its luts/)."""
+    import os
+    found = []
+    for name in FILMIC_LUT_FILES:
+        for sub in ("luts", ""):
+            p = os.path.join(directory, sub, name)
+            if os.path.isfile(p):
+                found.append(p)
+                break
+        else:
+            raise FileNotFoundError(name)
+    d = parse_spi1d(found[1])
+    d["cube"] = parse_spi3d(found[0])
+    return d
+
+
+def write_synthetic_filmic_luts(directory: str, n3: int = 17, n1: int = 1024, seed: int = 7,
+                                lo: float = -0.125, hi: float = 1.125) -> None:
+    """Synthetic LUT files in the two formats, shaped like Filmic's (a
+    desaturating cube into [0, 0.66], an S-shaped display curve), for tests
+    only: Blender's own LUT files are not in this image."""
+    import os
+    rng = np.random.default_rng(seed)
+    os.makedirs(os.path.join(directory, "luts"), exist_ok=True)
+    g = np.linspace(0.0, 1.0, n3)
+    with open(os.path.join(directory, "luts", FILMIC_LUT_FILES[0]), "w") as fh:
+        fh.write(f"SPILUT 1.0\n3 3\n{n3} {n3} {n3}\n")
+        for i in range(n3):
+            for j in range(n3):
+                for k in range(n3):
+                    rgb = np.array([g[i], g[j], g[k]])
+                    y = rgb.mean()
+                    v = 0.66 * (0.8 * rgb + 0.2 * y) + rng.normal(0, 0.004, 3)
+                    fh.write(f"{i} {j} {k} {v[0]:.6f} {v[1]:.6f} {v[2]:.6f}\n")
+    x = np.linspace(lo, hi, n1)
+    curve = 1.0 / (1.0 + np.exp(-8.0 * (x - 0.5)))
+    with open(os.path.join(directory, "luts", FILMIC_LUT_FILES[1]), "w") as fh:
+        fh.write(f"Version 1\nFrom {lo} {hi}\nLength {n1}\nComponents 1\n{{\n")
+        for v in curve:
+            fh.write(f"  {v:.8f}\n")
+        fh.write("}\n")
+
+
+# ------------------------------------------------------- worker accounting --
+def worker_performance(trace: dict) -> dict:
+    """WorkerPerformance::from_worker_trace (/root/reference/shared/src/results/
+    performance.rs:47-143) over a WorkerTrace dict (traces.WorkerTrace.to_dict):
+    the per-frame loading / rendering / saving durations and the idle time
+    between frames. Every `signed_duration_since(..).to_std()` of the reference
+    fails on a negative duration; the same checks raise ValueError here with
+    the reference's messages."""
+    def dur(a, b, msg):
+        d = a - b
+        if d < 0:
+            raise ValueError(msg)
+        return d
+    frames = [f["details"] for f in trace["frame_render_traces"]]
+    total = dur(trace["job_finish_time"], trace["job_start_time"], "Could not calculate total job duration.")
+    load = rend = save = idle = 0.0
+    n = len(frames)
+    for i, f in enumerate(frames):
+        load += dur(f["finished_loading_at"], f["started_process_at"], "Invalid file reading duration.")
+        rend += dur(f["finished_rendering_at"], f["started_rendering_at"], "Invalid rendering duration.")
+        save += dur(f["file_saving_finished_at"], f["file_saving_started_at"], "Invalid file saving duration.")
+        if i == 0:
+            idle += dur(f["started_process_at"], trace["job_start_time"],
+                        "Failed to calculate idle time before first frame.")
+        elif i == n - 1:
+            idle += dur(trace["job_finish_time"], f["exited_process_at"],
+                        "Failed to calculate idle time after last frame.")
+        else:
+            idle += dur(f["started_process_at"], frames[i - 1]["exited_process_at"], "Invalid idle duration.")
+    return {"total_frames_rendered": n, "total_time": total, "total_blend_file_reading_time": load,
+            "total_rendering_time": rend, "total_image_saving_time": save, "total_idle_time": idle}

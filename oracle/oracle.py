@@ -44,6 +44,8 @@ def lib():
         L.orc_bsdf_sample.argtypes = [f, f, f, c_int, f, f, f, f, i32]
         L.orc_filter_table.argtypes = [ctypes.c_float, f]
         L.orc_srgb_lut.argtypes = [f]
+        L.orc_set_filmic.argtypes = [f, c_int, f, c_int, c_int, ctypes.c_float, ctypes.c_float]
+        L.orc_filmic.argtypes = [c_int, f, u8]
         _lib = L
     return _lib
 
@@ -111,7 +113,10 @@ def render(tris, tri_mat, camera, lights, materials, world, render_ints, render_
     lights = _f32(lights).reshape(-1, 12)
     mats = _f32(materials).reshape(-1, 12)
     world = _f32(world)
-    ri = np.ascontiguousarray(render_ints, dtype=np.int32)
+    ri = np.asarray(render_ints, dtype=np.int32)
+    if ri.size < 10:  # per-lobe bounce caps default to Cycles' 4 / 4 (rr.h render_ints[8], [9])
+        ri = np.concatenate([ri, np.array([4, 4], np.int32)[: 10 - ri.size]])
+    ri = np.ascontiguousarray(ri)
     rf = _f32(render_floats)
     W, H = int(ri[0]), int(ri[1])
     f = np.zeros((H, W, 4), np.float32) if film else None
@@ -184,3 +189,30 @@ def srgb_lut() -> np.ndarray:
     t = np.zeros(4097, np.float32)
     lib().orc_srgb_lut(_p(t, ctypes.c_float))
     return t
+
+
+_filmic_keep = None
+
+
+def set_filmic(luts):
+    """LUTs of the Filmic view (render_ints[5] == 2) for the oracle's renders:
+    luts = host_oracle.load_filmic_luts(dir) (cube (n,n,n,3), lut1 (n1, comps),
+    lo1, hi1), or None to clear."""
+    global _filmic_keep
+    if luts is None:
+        _filmic_keep = None
+        lib().orc_set_filmic(None, 0, None, 0, 1, 0.0, 1.0)
+        return
+    cube = _f32(luts["cube"])
+    lut1 = _f32(luts["lut1"])
+    _filmic_keep = (cube, lut1)
+    lib().orc_set_filmic(_p(cube, ctypes.c_float), int(cube.shape[0]), _p(lut1, ctypes.c_float),
+                         int(lut1.shape[0]), int(lut1.shape[1]), float(luts["lo1"]), float(luts["hi1"]))
+
+
+def filmic(rgb: np.ndarray) -> np.ndarray:
+    """Filmic 8-bit code values of linear RGB triples (set_filmic first)."""
+    rgb = _f32(rgb).reshape(-1, 3)
+    out = np.zeros((rgb.shape[0], 3), np.uint8)
+    lib().orc_filmic(rgb.shape[0], _p(rgb, ctypes.c_float), _p(out, ctypes.c_uint8))
+    return out

@@ -607,9 +607,56 @@ static int trace(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hit
 }
 
 /* ------------------------------------------------------------ material ---- */
+/* Blender 3.6 Cycles' Principled BSDF v1 for the subset the scenes use (base,
+ * metallic, specular, roughness), restated from Cycles (third-party, not in
+ * /root/reference): closure setup in intern/cycles/kernel/svm/closure.h
+ * (CLOSURE_BSDF_PRINCIPLED_ID: cspec0, ior = 2/(1 - sqrt(0.08 specular)) - 1,
+ * closures present above CLOSURE_WEIGHT_CUTOFF 1e-5), the diffuse closure of
+ * bsdf_principled_diffuse.h (PRINCIPLED_DIFFUSE_FULL), and the GGX closure
+ * with Fresnel of bsdf_microfacet.h (interpolate_fresnel_color,
+ * fresnel_dielectric_cos of bsdf_util.h; sample weight scaled by the average
+ * Fresnel colour at the view angle). Same float operations as
+ * csrc/rr_device.h mat_derive / bsdf_eval_v / spec_prob. */
 typedef struct { v3 base; float metallic, specular, roughness, ior; v3 emission; int model; } mat_t;
 
 static float sw(float c) { float m = 1.0f - c; if (m < 0.0f) m = 0.0f; float m2 = m * m; return m2 * m2 * m; }
+
+static float fresnel_dielectric_cos(float cosi, float eta) {
+    float c = fabsf(cosi);
+    float g = eta * eta - 1.0f + c * c;
+    if (g > 0.0f) {
+        g = sqrtf(g);
+        float A = (g - c) / (g + c);
+        float B = (c * (g + c) - 1.0f) / (c * (g - c) + 1.0f);
+        return 0.5f * A * A * (1.0f + B * B);
+    }
+    return 1.0f;
+}
+
+static float sat1(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
+
+/* terms Cycles derives at closure setup */
+typedef struct { float alpha, a2, ior_s, f0d, f0n, wd, kd0; v3 cspec0; int spec_on; } mterms;
+
+static mterms mat_terms(const mat_t* m) {
+    mterms t;
+    float alpha = m->roughness * m->roughness;
+    if (alpha < 1.0e-3f) alpha = 1.0e-3f;  /* see csrc/rr_device.h mat_derive */
+    t.alpha = alpha;
+    t.a2 = alpha * alpha;
+    float sm = m->specular * 0.08f * (1.0f - m->metallic);
+    t.cspec0 = V(sat1(sm + m->base.x * m->metallic), sat1(sm + m->base.y * m->metallic),
+                 sat1(sm + m->base.z * m->metallic));
+    t.ior_s = 2.0f / (1.0f - sqrtf(0.08f * m->specular)) - 1.0f;
+    t.f0d = fresnel_dielectric_cos(1.0f, t.ior_s);
+    t.f0n = 1.0f / (1.0f - t.f0d);
+    t.wd = (1.0f - m->metallic) * ((m->base.x + m->base.y + m->base.z) * 0.333333343f);
+    t.kd0 = (1.0f - m->metallic) * 0.318309886183791f;
+    t.spec_on = (m->specular > 1.0e-5f || m->metallic > 1.0e-5f) ? 1 : 0;
+    return t;
+}
+
+static float fresnel_blend(const mterms* t, float c) { return (fresnel_dielectric_cos(c, t->ior_s) - t->f0d) * t->f0n; }
 
 static v3 eval_bsdf(const mat_t* m, v3 N, v3 wo, v3 wi, float ps, float* pdf) {
     float cosV = vdot(N, wo), cosL = vdot(N, wi);
@@ -618,24 +665,23 @@ static v3 eval_bsdf(const mat_t* m, v3 N, v3 wo, v3 wi, float ps, float* pdf) {
         *pdf = cosL * 0.318309886183791f;
         return vscl(m->base, 0.318309886183791f);
     }
+    mterms T = mat_terms(m);
     v3 H = vnorm(vadd(wo, wi));
     float cosD = vdot(wi, H), NdotH = vdot(N, H);
-    float alpha = m->roughness * m->roughness;
-    if (alpha < 1.0e-4f) alpha = 1.0e-4f;
-    float a2 = alpha * alpha;
-    float fd90 = 0.5f + 2.0f * m->roughness * cosD * cosD;
+    float a2 = T.a2;
+    /* diffuse: (1 - FV/2)(1 - FL/2) + RR (FL + FV + FL FV (RR - 1)), RR = roughness (L.V + 1) */
     float fl = sw(cosL), fv = sw(cosV);
-    float kd = (1.0f - m->metallic) * 0.318309886183791f * (1.0f + (fd90 - 1.0f) * fl) * (1.0f + (fd90 - 1.0f) * fv);
+    float rr = m->roughness * (vdot(wi, wo) + 1.0f);
+    float kd = T.kd0 * ((1.0f - 0.5f * fv) * (1.0f - 0.5f * fl) + rr * (fl + fv + fl * fv * (rr - 1.0f)));
+    /* GGX, separable Smith G1 */
     float tt = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
     float D = a2 / (3.14159265358979f * tt * tt);
     float g1v = 2.0f * cosV / (cosV + sqrtf(a2 + (1.0f - a2) * cosV * cosV));
     float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
-    float s0 = 0.08f * m->specular;
-    v3 F0 = V(s0 + (m->base.x - s0) * m->metallic, s0 + (m->base.y - s0) * m->metallic,
-              s0 + (m->base.z - s0) * m->metallic);
-    float fw = sw(cosD);
-    float ks = D * g1v * g1l / (4.0f * cosV * cosL);
-    v3 F = V(F0.x + (1.0f - F0.x) * fw, F0.y + (1.0f - F0.y) * fw, F0.z + (1.0f - F0.z) * fw);
+    float fh = fresnel_blend(&T, cosD);
+    float ks = T.spec_on ? D * g1v * g1l / (4.0f * cosV * cosL) : 0.0f;
+    v3 c0 = T.cspec0;
+    v3 F = V(c0.x * (1.0f - fh) + fh, c0.y * (1.0f - fh) + fh, c0.z * (1.0f - fh) + fh);
     float pdf_d = cosL * 0.318309886183791f;
     float pdf_s = g1v * D / (4.0f * cosV);
     *pdf = (1.0f - ps) * pdf_d + ps * pdf_s;
@@ -644,12 +690,12 @@ static v3 eval_bsdf(const mat_t* m, v3 N, v3 wo, v3 wi, float ps, float* pdf) {
 
 static float p_spec(const mat_t* m, float cosV) {
     if (m->model == 1) return 0.0f;
-    float s0 = 0.08f * m->specular;
-    float f0avg = ((s0 + (m->base.x - s0) * m->metallic) + (s0 + (m->base.y - s0) * m->metallic) +
-                   (s0 + (m->base.z - s0) * m->metallic)) * 0.333333343f;
-    float wsp = f0avg + (1.0f - f0avg) * sw(cosV);
-    float wd = (1.0f - m->metallic) * ((m->base.x + m->base.y + m->base.z) * 0.333333343f);
-    float tot = wsp + wd;
+    mterms T = mat_terms(m);
+    if (!T.spec_on) return 0.0f;
+    float fh = fresnel_blend(&T, cosV);
+    v3 c0 = T.cspec0;
+    float wsp = ((c0.x * (1.0f - fh) + fh) + (c0.y * (1.0f - fh) + fh) + (c0.z * (1.0f - fh) + fh)) * 0.333333343f;
+    float tot = wsp + T.wd;
     return tot > 0.0f ? wsp / tot : 1.0f;
 }
 
@@ -671,15 +717,18 @@ static v3 vndf(v3 v, float alpha, float u1, float u2) {
     return vnorm(V(alpha * nh.x, alpha * nh.y, fmaxf(0.0f, nh.z)));
 }
 
-static int sample_bsdf(const mat_t* m, v3 N, v3 wo, float ul, float u1, float u2, v3* wi, v3* f, float* pdf) {
+/* glossy: the specular lobe was picked (Cycles LABEL_GLOSSY, else LABEL_DIFFUSE) */
+static int sample_bsdf(const mat_t* m, v3 N, v3 wo, float ul, float u1, float u2, v3* wi, v3* f, float* pdf,
+                       int* glossy) {
     float cosV = vdot(N, wo);
     if (cosV <= 0.0f) return 0;
     float ps = p_spec(m, cosV);
     v3 T, B;
     onb(N, &T, &B);
+    *glossy = ul < ps;
     if (ul < ps) {
         float alpha = m->roughness * m->roughness;
-        if (alpha < 1.0e-4f) alpha = 1.0e-4f;
+        if (alpha < 1.0e-3f) alpha = 1.0e-3f;
         v3 wl = V(vdot(wo, T), vdot(wo, B), cosV);
         v3 hl = vndf(wl, alpha, u1, u2);
         v3 H = V(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,
@@ -713,6 +762,7 @@ typedef struct {
     const float* mats;    /* 12 each */
     v3 world;
     int W, H, spp, max_bounces, view;
+    int max_diffuse, max_glossy;  /* Cycles per-lobe bounce caps (>= 1) */
     uint32_t seed;
     float clamp, inv_w2, inv_h2;
     float filter[ORC_FILTER_N];
@@ -770,6 +820,7 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
     v3 o = V(c[0], c[1], c[2]);
     float tmin = c[14] * len, tmax = c[15] * len;
     v3 L = V(0.0f, 0.0f, 0.0f), T = V(1.0f, 1.0f, 1.0f);
+    int nd = 0, ng = 0;  /* diffuse / glossy scatters so far (Cycles path_state_next) */
     const int culled = S->cull_on && (fx < S->cull[0] || fx > S->cull[1] || fy < S->cull[2] || fy > S->cull[3]);
     for (int b = 0; b <= S->max_bounces; ++b) {
         hitrec h;
@@ -804,7 +855,9 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
             if (b > 0) cc = clampc(cc, S->clamp);
             L = vadd(L, cc);
         }
-        if (b >= S->max_bounces) break;
+        /* Cycles path_state_next: the scatter that takes bounce, diffuse_bounce or
+         * glossy_bounce to its cap ends the path at the next hit (emission only) */
+        if (b >= S->max_bounces || nd >= S->max_diffuse || ng >= S->max_glossy) break;
         uint32_t dim0 = 2u + 8u * (uint32_t)b;
         v3 Po = offset_ray(P, N);
         int shadow = 0;
@@ -858,10 +911,11 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
                 if (vmax3(cc) > 0.0f) { shadow = 1; sh_dir = wi; sh_dist = dist; sh_c = cc; }
             }
         }
-        int alive = 0;
+        int alive = 0, glossy = 0;
         v3 wi, f;
         float pdf;
-        if (sample_bsdf(&m, N, wo, rnd(key, dim0 + 3u), rnd(key, dim0 + 4u), rnd(key, dim0 + 5u), &wi, &f, &pdf)) {
+        if (sample_bsdf(&m, N, wo, rnd(key, dim0 + 3u), rnd(key, dim0 + 4u), rnd(key, dim0 + 5u), &wi, &f, &pdf,
+                        &glossy)) {
             float cosL = vdot(N, wi);
             if (cosL > 0.0f) {
                 float k = cosL / pdf;
@@ -879,9 +933,100 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
             if (!trace(S->bvh, Po, sh_dir, 0.0f, sh_dist, 1, &hs)) L = vadd(L, sh_c);
         }
         if (!alive) break;
+        if (glossy) ++ng; else ++nd;
         o = Po; d = wi; tmin = 0.0f; tmax = 3.402823466e+38f;
     }
     return L;
+}
+
+/* ----------------------------------------------------- Filmic (view) ---- */
+/* Blender 3.6's "Filmic" view for display sRGB, look None, as its OCIO config
+ * chains it (restated in csrc/view.hpp): lg2 allocation [-12.473931188,
+ * 12.526068812] -> filmic_desat65cube.spi3d (tetrahedral) -> uniform
+ * allocation [0, 0.66] -> filmic_to_0-70_1-03.spi1d (linear). The LUT arrays
+ * come from the caller (orc_set_filmic), parsed by oracle/host_oracle.py's own
+ * .spi3d/.spi1d readers. Same float operations as csrc/view.hip. */
+static struct {
+    const float* cube; int n3;            /* n3^3 x rgb, entry (i, j, k) at (i n3 + j) n3 + k */
+    const float* lut1; int n1, comps;     /* n1 x comps */
+    float lo1, hi1;
+} g_filmic;
+
+void orc_set_filmic(const float* cube, int n3, const float* lut1, int n1, int comps, float lo1, float hi1) {
+    g_filmic.cube = cube; g_filmic.n3 = n3;
+    g_filmic.lut1 = lut1; g_filmic.n1 = n1; g_filmic.comps = comps;
+    g_filmic.lo1 = lo1; g_filmic.hi1 = hi1;
+}
+
+/* log2 of a normal positive float without libm (csrc/view.hip log2_fixed) */
+static float log2_fixed(float x) {
+    int bits = fbits(x);
+    int e = ((bits >> 23) & 0xff) - 127;
+    float m = ibits((bits & 0x007fffff) | 0x3f800000);
+    if (m > 1.41421356f) { m = m * 0.5f; e = e + 1; }
+    float t = (m - 1.0f) / (m + 1.0f);
+    float t2 = t * t;
+    float p = ((((t2 * 0.111111112f + 0.142857149f) * t2 + 0.2f) * t2 + 0.333333343f) * t2 + 1.0f) * t;
+    return (float)e + p * 2.88539004f;
+}
+
+static float lut1d(float x, int c) {
+    const float* t = g_filmic.lut1;
+    int n = g_filmic.n1, comps = g_filmic.comps;
+    float f = (x - g_filmic.lo1) / (g_filmic.hi1 - g_filmic.lo1) * (float)(n - 1);
+    f = fminf(fmaxf(f, 0.0f), (float)(n - 1));
+    int i = (int)f;
+    if (i >= n - 1) return t[(n - 1) * comps + c];
+    float fr = f - (float)i;
+    float a = t[i * comps + c], b = t[(i + 1) * comps + c];
+    return a + (b - a) * fr;
+}
+
+static v3 cube_at(int i, int j, int k) {
+    int n = g_filmic.n3;
+    const float* q = g_filmic.cube + 3 * (((size_t)i * n + j) * n + k);
+    return V(q[0], q[1], q[2]);
+}
+
+/* OCIO Lut3D tetrahedral interpolation, input clamped to [0, 1] */
+static v3 lut3d_tetra(float r, float g, float b) {
+    int n = g_filmic.n3;
+    float s = (float)(n - 1);
+    float fr = sat1(r) * s, fg = sat1(g) * s, fb = sat1(b) * s;
+    int ir = (int)fr, ig = (int)fg, ib = (int)fb;
+    if (ir > n - 2) ir = n - 2;
+    if (ig > n - 2) ig = n - 2;
+    if (ib > n - 2) ib = n - 2;
+    fr = fr - (float)ir; fg = fg - (float)ig; fb = fb - (float)ib;
+    v3 c000 = cube_at(ir, ig, ib), c111 = cube_at(ir + 1, ig + 1, ib + 1), c1, c2;
+    float w0, w1, w2, w3;
+    if (fr > fg) {
+        if (fg > fb) { c1 = cube_at(ir + 1, ig, ib); c2 = cube_at(ir + 1, ig + 1, ib); w0 = 1.0f - fr; w1 = fr - fg; w2 = fg - fb; w3 = fb; }
+        else if (fr > fb) { c1 = cube_at(ir + 1, ig, ib); c2 = cube_at(ir + 1, ig, ib + 1); w0 = 1.0f - fr; w1 = fr - fb; w2 = fb - fg; w3 = fg; }
+        else { c1 = cube_at(ir, ig, ib + 1); c2 = cube_at(ir + 1, ig, ib + 1); w0 = 1.0f - fb; w1 = fb - fr; w2 = fr - fg; w3 = fg; }
+    } else {
+        if (fb > fg) { c1 = cube_at(ir, ig, ib + 1); c2 = cube_at(ir, ig + 1, ib + 1); w0 = 1.0f - fb; w1 = fb - fg; w2 = fg - fr; w3 = fr; }
+        else if (fb > fr) { c1 = cube_at(ir, ig + 1, ib); c2 = cube_at(ir, ig + 1, ib + 1); w0 = 1.0f - fg; w1 = fg - fb; w2 = fb - fr; w3 = fr; }
+        else { c1 = cube_at(ir, ig + 1, ib); c2 = cube_at(ir + 1, ig + 1, ib); w0 = 1.0f - fg; w1 = fg - fr; w2 = fr - fb; w3 = fb; }
+    }
+    return V(((w0 * c000.x + w1 * c1.x) + w2 * c2.x) + w3 * c111.x,
+             ((w0 * c000.y + w1 * c1.y) + w2 * c2.y) + w3 * c111.y,
+             ((w0 * c000.z + w1 * c1.z) + w2 * c2.z) + w3 * c111.z);
+}
+
+static unsigned char q8(float f);
+
+static void filmic8(const float c[3], unsigned char* out) {
+    float a[3];
+    for (int k = 0; k < 3; ++k) a[k] = (log2_fixed(fmaxf(c[k], 1.17549435e-38f)) + 12.473931188f) / 25.0f;
+    v3 b = lut3d_tetra(a[0], a[1], a[2]);
+    float bb[3] = {b.x, b.y, b.z};
+    for (int k = 0; k < 3; ++k) out[k] = q8(lut1d(bb[k] / 0.66f, g_filmic.comps == 3 ? k : 0));
+}
+
+/* Filmic of n linear RGB triples (tests of the chain in isolation) */
+void orc_filmic(int n, const float* rgb, unsigned char* out3) {
+    for (int i = 0; i < n; ++i) filmic8(rgb + 3 * (size_t)i, out3 + 3 * (size_t)i);
 }
 
 static unsigned char q8(float f) {
@@ -892,7 +1037,7 @@ static unsigned char q8(float f) {
 
 /* ------------------------------------------------------------ C entry ---- */
 
-int orc_abi(void) { return 1; }
+int orc_abi(void) { return 2; }
 
 /* LBVH of n triangles (tris9: v0 v1 v2 per triangle). Outputs as rr_debug_bvh. */
 int orc_build_bvh(int n, const float* tris9, int hier, uint32_t* keys, uint32_t* order, int32_t* children,
@@ -992,6 +1137,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     S->world = V(world[0], world[1], world[2]);
     S->cam_all = ri[7] == 2;
     S->W = ri[0]; S->H = ri[1]; S->spp = ri[2]; S->max_bounces = ri[3]; S->seed = (uint32_t)ri[4]; S->view = ri[5];
+    S->max_diffuse = ri[8]; S->max_glossy = ri[9];
     S->clamp = rf[0];
     S->inv_w2 = 2.0f / (float)S->W;
     S->inv_h2 = 2.0f / (float)S->H;
@@ -1036,7 +1182,11 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
                 film[4 * (size_t)pix + 2] = acc.z * inv_spp;
                 film[4 * (size_t)pix + 3] = 1.0f;
             }
-            if (rgba8) {
+            if (rgba8 && S->view == 2) {
+                float c3[3] = {acc.x * inv_spp * exposure, acc.y * inv_spp * exposure, acc.z * inv_spp * exposure};
+                filmic8(c3, rgba8 + 4 * (size_t)pix);
+                rgba8[4 * (size_t)pix + 3] = 255;
+            } else if (rgba8) {
                 float c3[3] = {acc.x * inv_spp * exposure, acc.y * inv_spp * exposure, acc.z * inv_spp * exposure};
                 for (int k = 0; k < 3; ++k) {
                     float v = fminf(fmaxf(c3[k], 0.0f), 1.0f);
@@ -1072,7 +1222,8 @@ void orc_bsdf_sample(const float* mat12, const float* n3, const float* wo3, int 
     for (int i = 0; i < n; ++i) {
         v3 wi = V(0.0f, 0.0f, 0.0f), f = wi;
         float p = 0.0f;
-        ok[i] = sample_bsdf(&m, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], &wi, &f, &p);
+        int glossy = 0;
+        ok[i] = sample_bsdf(&m, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], &wi, &f, &p, &glossy);
         wi3[3 * i] = wi.x; wi3[3 * i + 1] = wi.y; wi3[3 * i + 2] = wi.z;
         f3[3 * i] = f.x; f3[3 * i + 1] = f.y; f3[3 * i + 2] = f.z;
         pdf[i] = p;

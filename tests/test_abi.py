@@ -28,7 +28,31 @@ def test_library_exports_every_declared_symbol(rr):
 
 
 def test_abi_version(rr):
-    assert rr.lib().rr_abi_version() == 1
+    assert rr.lib().rr_abi_version() == 2 == rr.native.RR_ABI_VERSION
+
+
+def test_struct_layouts_match_header(rr):
+    """The ctypes mirrors have the header's field order (a field added to rr.h
+    and not to native.py, or the reverse, shifts every later field)."""
+    src = open(os.path.join(ROOT, "include", "rr.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    for cname, py in (("rr_render_params", rr.native.RenderParams), ("rr_frame_stats", rr.native.FrameStats),
+                      ("rr_frame_timing", rr.native.FrameTiming)):
+        body = re.search(r"typedef struct " + cname + r" \{(.*?)\} " + cname, src, flags=re.S).group(1)
+        fields = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            names = decl.split(None, 1)[1]
+            for nm in names.split(","):
+                fields.append(re.sub(r"\[.*\]", "", nm).strip())
+        assert [f for f, _ in py._fields_] == fields, cname
+
+
+def test_default_params_lobe_caps(rr):
+    p = rr.default_params()
+    assert p.max_diffuse_bounces == -1 and p.max_glossy_bounces == -1
 
 
 def test_default_params(rr):
@@ -67,7 +91,15 @@ def test_host_only_scene_queries(rr):
     assert s.resolution(rr.default_params(width=64, height=36)) == (64, 36)
     fc = s.frame_constants(1)
     assert list(fc.render_ints[:4]) == [1920, 1080, 128, 12]
+    assert list(fc.render_ints[8:10]) == [4, 4]  # Cycles' diffuse / glossy bounce defaults
+    fc = s.frame_constants(1, rr.default_params(max_bounces=0, max_diffuse_bounces=2, max_glossy_bounces=0))
+    # a cap of 0 acts as 1 (the camera hit always scatters, Cycles path_state_next)
+    assert fc.render_ints[3] == 1 and list(fc.render_ints[8:10]) == [2, 1]
     s.close()
+    s01 = rr.Scene(scene_path("01_simple-animation.rrscene"))
+    # host-only query: the transform the scene asks for (a context may substitute it)
+    assert s01.frame_constants(1).render_ints[5] == rr.native.RR_VIEW_FILMIC
+    s01.close()
 
 
 def _test_image(w=67, h=45):

@@ -100,3 +100,23 @@ def test_two_rank_gloo_frame_parallel():
             assert hashes[f] == _render_hash(f)
     # frames differ (the animation moves the cube), so the check is not vacuous
     assert len({h for _, _, hs in gathered for h in hs.values()}) > 1
+
+
+@pytest.mark.timeout(300)
+def test_bench_spawns_one_rank_per_gpu_dry_run():
+    """`bench.py --gpus 2` with no launcher starts 2 rank processes itself (gloo
+    rendezvous, HIP_VISIBLE_DEVICES per rank) that take disjoint frames of the
+    job; rank 0 prints one line with n_gpus 2. --dry-run: nothing is rendered
+    (no GPU here)."""
+    import json
+    import subprocess
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--steps", "5", "--warmup", "0"], capture_output=True, text=True, timeout=240,
+                         env=dict(os.environ, HIP_VISIBLE_DEVICES="0,1"))
+    assert res.returncode == 0, res.stderr[-2000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] is None and line["dry_run"]
+    a, b = line["frames_by_rank"]
+    assert not set(a) & set(b) and sorted(a + b) == JOB_FRAMES

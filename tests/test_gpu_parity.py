@@ -150,6 +150,7 @@ def test_full_frame_bit_exact(ctx, rr, s04, frame, w, h, spp, chunk, path):
     st = ctx.frame_state(s04, frame, p)
     of, orgba = O.render_state(st)
     assert stats.camera_rays == w * h * spp
+    assert 0 <= stats.camera_rays_traced <= stats.camera_rays
     assert stats.width == w and stats.height == h and stats.spp == spp
     nbad = int(np.count_nonzero(rgba != orgba))
     assert nbad == 0, f"{nbad} 8-bit mismatches"
@@ -160,11 +161,12 @@ def test_full_frame_bit_exact(ctx, rr, s04, frame, w, h, spp, chunk, path):
 def test_tiles_equal_wavefront_full_resolution(ctx, rr, s04):
     """BASELINE size (1920x1080) at low spp: k_tiles and the wavefront kernels give
     the same film bits, pixels and ray counts (the oracle is too slow here)."""
-    out = {}
+    out, traced = {}, {}
     for path, flags in PATHS.items():
         p = rr.default_params(spp=4, flags=flags)
         film, rgba, st = ctx.render_to_memory(s04, 30, p)
         out[path] = (film, rgba, st.extension_rays, st.shadow_rays, st.primary_continued, st.primary_shadow)
+        traced[path] = st.camera_rays_traced
     a, b = out["tiles"], out["wavefront"]
     # 40 samples: two film groups, k_tiles' box tiles in two slices
     f40 = [ctx.render_to_memory(s04, 7, rr.default_params(spp=40, flags=flags))[0] for flags in PATHS.values()]
@@ -174,6 +176,8 @@ def test_tiles_equal_wavefront_full_resolution(ctx, rr, s04):
     assert np.array_equal(a[1], b[1])
     assert a[2:] == b[2:], (a[2:], b[2:])
     assert a[2] > 0 and a[3] > 0
+    # k_tiles also skips camera rays whose tile meets no triangle: fewer traced
+    assert 0 < traced["tiles"] <= traced["wavefront"] < 1920 * 1080 * 4
 
 
 def test_chunking_and_determinism(ctx, rr, s04):
@@ -258,21 +262,57 @@ def test_render_frame_writes_named_files(ctx, rr, s04, tmp_path):
     assert e.value.code == -5
 
 
-def test_bench_config_properties(ctx, rr, s04):
-    """The bench workload (1920x1080, 128 spp): too big for the oracle in a test,
-    so check size-independent properties plus a bit-exact oracle slice."""
-    film, rgba, stats = ctx.render_to_memory(s04, 5, None)
+def _hit_rows(film, world, n, rng):
+    """n 4-row bands spread over the rows whose pixels show the cube (film
+    differs from the world colour), each with its cube-pixel count."""
+    hit = np.any(np.abs(film[..., :3] - world[None, None, :]) > 1e-4 * np.abs(world).max(), axis=-1)
+    rows = np.nonzero(hit.sum(axis=1) > 0)[0]
+    assert len(rows) >= 4 * n, len(rows)
+    starts = np.linspace(rows[0], rows[-1] - 3, n).astype(int)
+    return [(int(r), int(hit[r:r + 4].sum())) for r in starts]
+
+
+@pytest.mark.parametrize("frame", [1, 5, 10])
+def test_bench_config_properties(ctx, rr, s04, frame):
+    """The bench workload (1920x1080, 128 spp) on frames 1, 5 and 10 of the 04vs
+    job: too big for the oracle whole, so size-independent properties plus
+    four bit-exact oracle bands per frame, each through the cube."""
+    film, rgba, stats = ctx.render_to_memory(s04, frame, None)
     assert film.shape == (1080, 1920, 4)
     assert stats.camera_rays == 1920 * 1080 * 128
+    assert 0 < stats.camera_rays_traced < stats.camera_rays
     assert stats.extension_rays > 0 and stats.shadow_rays > 0
-    film2, rgba2, _ = ctx.render_to_memory(s04, 5, None)
+    film2, rgba2, _ = ctx.render_to_memory(s04, frame, None)
     assert np.array_equal(film, film2)
-    st = ctx.frame_state(s04, 5)
-    of, orgba = O.render_state(st, rows=(500, 504))
-    assert np.array_equal(rgba[500:504], orgba[500:504])
-    assert np.array_equal(film[500:504], of[500:504])
+    st = ctx.frame_state(s04, frame)
+    bands = _hit_rows(film, st.world, 4, None)
+    for r0, n_hit in bands:
+        of, orgba = O.render_state(st, rows=(r0, r0 + 4))
+        print(f"frame {frame} rows {r0}..{r0 + 3}: {n_hit} cube pixels")
+        assert n_hit > 0
+        assert np.array_equal(rgba[r0:r0 + 4], orgba[r0:r0 + 4])
+        assert np.array_equal(film[r0:r0 + 4], of[r0:r0 + 4])
     bg = film[1060:1080, 0:20, :3]
     np.testing.assert_allclose(bg, 0.050876088, rtol=1e-5)
+
+
+def test_01_full_resolution_slices(ctx, rr):
+    """The 01 scene at its own 1920x1080 x 128 spp (C3's frame): two oracle
+    bands through the cube, bit for bit (rendered with Standard here: no
+    OCIO LUTs are configured on the context, and the frame says so)."""
+    s = ctx.load_scene(S01)
+    try:
+        film, rgba, stats = ctx.render_to_memory(s, 20, None)
+        assert stats.view_transform_substituted == 1
+        st = ctx.frame_state(s, 20)
+        for r0, n_hit in _hit_rows(film, st.world, 2, None):
+            of, orgba = O.render_state(st, rows=(r0, r0 + 4))
+            print(f"01 frame 20 rows {r0}..{r0 + 3}: {n_hit} cube pixels")
+            assert n_hit > 0
+            assert np.array_equal(rgba[r0:r0 + 4], orgba[r0:r0 + 4])
+            assert np.array_equal(film[r0:r0 + 4], of[r0:r0 + 4])
+    finally:
+        s.close()
 
 
 def test_01_scene_renders(ctx, rr):

@@ -194,8 +194,10 @@ def _render_scene(name, frame=1, **over):
             t = np.array([[[-h, -h, 0], [h, -h, 0], [h, h, 0]], [[-h, -h, 0], [h, h, 0], [-h, h, 0]]], np.float32)
         tris.append(t + np.array(o["location"], np.float32))
         mats += [0] * len(t)
-    ri = np.array([W, H, over.get("spp", r["samples"]), r["max_bounces"], r["seed"],
-                   1 if r["view_transform"] == "Raw" else 0, 0, 0], np.int32)
+    ri = np.array([W, H, over.get("spp", r["samples"]), over.get("max_bounces", r["max_bounces"]), r["seed"],
+                   1 if r["view_transform"] == "Raw" else 0, 0, 0,
+                   over.get("max_diffuse", r.get("max_diffuse_bounces", 4)),
+                   over.get("max_glossy", r.get("max_glossy_bounces", 4))], np.int32)
     rf = np.array([r["clamp_indirect"], r["filter_width"], 1.0, 0], np.float32)
     return O.render(np.concatenate(tris), np.array(mats), fc["camera"], fc["lights"], fc["materials"],
                     fc["world"], ri, rf, threads=4)
@@ -293,3 +295,159 @@ def test_ploc_structure_and_walk_equal_brute_force(n, seed):
     bh, bp = O.trace_brute(tris, rays)
     assert np.array_equal(p3, bp)
     assert np.array_equal(h3[:, 0], bh[:, 0])
+
+
+# ---- Cycles per-lobe bounce caps (path_state_next) --------------------------
+@pytest.mark.parametrize("caps,hits", [((12, 4, 4), 5), ((12, 2, 4), 3), ((3, 4, 4), 4), ((12, 1, 4), 2),
+                                       ((12, 4, 1), 5)])
+def test_diffuse_bounce_cap_known_answer(caps, hits):
+    """Camera inside a closed emissive (E = 0.25) white Lambert shell: the
+    throughput stays 1, so every path returns E times the number of hits it
+    makes before a cap ends it. Diffuse cap d (Cycles max_diffuse_bounces):
+    the scatter that makes the d-th diffuse bounce ends the path at the next
+    hit, whose emission still counts -> E (d + 1), the truncated series
+    E (1 + rho + ... + rho^d) at rho = 1; total cap b likewise -> E (b + 1);
+    the glossy cap does not touch a diffuse-only path."""
+    mb, md, mg = caps
+    film, _ = _render_scene("test_enclosure_diffuse.rrscene", max_bounces=mb, max_diffuse=md, max_glossy=mg)
+    np.testing.assert_allclose(film[..., :3], 0.25 * hits, rtol=2e-5)
+
+
+def test_glossy_bounce_cap_known_answer():
+    """The same shell as a white metallic near-mirror (roughness 0: alpha
+    1e-4, G1 ~ 1, F = cspec0 = 1): E (g + 1) with the glossy cap g."""
+    for mg, hits in ((4, 5), (2, 3)):
+        film, _ = _render_scene("test_enclosure_glossy.rrscene", spp=4, max_glossy=mg)
+        assert abs(float(film[..., :3].mean()) - 0.25 * hits) < 2e-3 * hits, (mg, float(film[..., :3].mean()))
+    # without per-lobe caps (caps above the total) the same shell runs to the total cap
+    film, _ = _render_scene("test_enclosure_glossy.rrscene", spp=4, max_bounces=6, max_glossy=64)
+    assert abs(float(film[..., :3].mean()) - 0.25 * 7) < 2e-2
+
+
+def _fresnel_dielectric(c, eta):
+    g = np.sqrt(eta * eta - 1 + c * c)
+    A = (g - c) / (g + c)
+    B = (c * (g + c) - 1) / (c * (g - c) + 1)
+    return 0.5 * A * A * (1 + B * B)
+
+
+def test_principled_fresnel_is_cycles_interpolated_dielectric():
+    """Specular lobe at a metallic-0 grey surface against Cycles' Principled v1
+    Fresnel in float64: F = cspec0 (1 - FH) + FH, FH = (Fd(L.H, ior) - F0) /
+    (1 - F0), ior = 2 / (1 - sqrt(0.08 specular)) - 1 (specular 0.5 -> 1.5,
+    F0 = 0.04), measured by isolating the specular term (base colour 0 turns
+    the diffuse closure off; metallic 0, specular 0.5)."""
+    mat = np.array([0.0, 0.0, 0.0, 0.0, 0.5, 0.4, 1.45, 0, 0, 0, 0, 0], np.float32)
+    n = np.array([0, 0, 1], np.float32)
+    for th_o, th_i, ph in ((0.3, 0.5, 2.0), (1.2, 0.7, 1.0), (1.45, 1.4, 3.0)):
+        wo = np.array([np.sin(th_o), 0, np.cos(th_o)], np.float32)
+        wi = np.array([np.sin(th_i) * np.cos(ph), np.sin(th_i) * np.sin(ph), np.cos(th_i)], np.float32)
+        f, _ = O.bsdf_eval(mat, n, wo, wi)
+        h = (wo.astype(np.float64) + wi) / np.linalg.norm(wo.astype(np.float64) + wi)
+        a2 = (0.4 * 0.4) ** 2
+        cv, cl, nh = wo[2], wi[2], h[2]
+        D = a2 / (np.pi * (nh * nh * (a2 - 1) + 1) ** 2)
+        G1 = lambda c: 2 * c / (c + np.sqrt(a2 + (1 - a2) * c * c))  # noqa: E731
+        eta = 2 / (1 - np.sqrt(0.08 * 0.5)) - 1
+        F0 = _fresnel_dielectric(1.0, eta)
+        FH = (_fresnel_dielectric(float(np.dot(wi, h)), eta) - F0) / (1 - F0)
+        cspec0 = 0.5 * 0.08
+        F = cspec0 * (1 - FH) + FH
+        ref = F * D * G1(cv) * G1(cl) / (4 * cv * cl)
+        np.testing.assert_allclose(f, ref, rtol=2e-5)
+        assert abs(eta - 1.5) < 1e-12 and abs(F0 - 0.04) < 1e-12
+
+
+# ---- Filmic view transform (csrc/view.hpp) ----------------------------------
+def _filmic_f64(rgb, luts):
+    """The Filmic chain in float64 (the oracle's float32 result must agree to
+    within one 8-bit code value)."""
+    cube, lut, lo, hi = luts["cube"].astype(np.float64), luts["lut1"][:, 0].astype(np.float64), luts["lo1"], luts["hi1"]
+    n = cube.shape[0]
+    a = (np.log2(np.maximum(rgb, 1.17549435e-38)) + 12.473931188) / 25.0
+    x = np.clip(a, 0, 1) * (n - 1)
+    i0 = np.minimum(x.astype(int), n - 2)
+    f = x - i0
+    out = np.zeros(3)
+    # tetrahedral interpolation == the barycentric interpolation inside the
+    # tetrahedron of the cell containing f: sort the fractions descending
+    order = np.argsort(-f, kind="stable")
+    corner = i0.copy()
+    prev = 1.0
+    out = (1 - f[order[0]]) * cube[tuple(corner)]
+    for k in range(3):
+        corner[order[k]] += 1
+        w = f[order[k]] - (f[order[k + 1]] if k < 2 else 0.0)
+        out = out + w * cube[tuple(corner)]
+    c = out / 0.66
+    t = np.clip((c - lo) / (hi - lo) * (len(lut) - 1), 0, len(lut) - 1)
+    j = np.minimum(t.astype(int), len(lut) - 2)
+    v = lut[j] + (lut[j + 1] - lut[j]) * (t - j)
+    return np.clip(np.floor(np.clip(v, 0, 1) * 255 + 0.5), 0, 255)
+
+
+def test_filmic_chain_on_synthetic_luts(tmp_path):
+    HO.write_synthetic_filmic_luts(str(tmp_path))
+    luts = HO.load_filmic_luts(str(tmp_path))
+    assert luts["cube"].shape == (17, 17, 17, 3) and luts["lut1"].shape == (1024, 1)
+    O.set_filmic(luts)
+    try:
+        rng = np.random.default_rng(3)
+        rgb = np.concatenate([np.exp2(rng.uniform(-14, 14, (3000, 3))), np.zeros((1, 3)), np.full((1, 3), 1e30),
+                              np.full((1, 3), 0.18)]).astype(np.float32)
+        got = O.filmic(rgb)
+        exp = np.array([_filmic_f64(x.astype(np.float64), luts) for x in rgb])
+        assert np.abs(got.astype(int) - exp).max() <= 1
+        assert (got.astype(int) == exp).mean() > 0.97
+        # rendering with view 2 applies the same chain to the film
+        film, rgba = _render_scene("test_furnace.rrscene")
+        r = HO.load_scene(scene_path("test_furnace.rrscene"))
+        f2, rgba2 = _render_scene_view("test_furnace.rrscene", 2)
+        assert np.array_equal(f2, film)
+        assert np.array_equal(rgba2[..., :3].reshape(-1, 3), O.filmic(film[..., :3].reshape(-1, 3)))
+    finally:
+        O.set_filmic(None)
+
+
+def _render_scene_view(name, view):
+    scene = HO.load_scene(scene_path(name))
+    scene["render"]["view_transform"] = "Raw"
+    import oracle.oracle as OO
+    orig = OO.render
+
+    def patched(*a, **k):
+        ri = np.array(a[6], np.int32).copy()
+        ri[5] = view
+        return orig(*a[:6], ri, *a[7:], **k)
+    OO.render = patched
+    try:
+        return _render_scene(name)
+    finally:
+        OO.render = orig
+
+
+def test_log2_fixed_accuracy():
+    """The libm-free log2 of the Filmic shaper (view.hip log2_fixed) is within
+    3e-7 of log2 over the normal range: checked through the shaper's
+    allocation a = (log2 x + 12.47) / 25 on a 1x1x1 identity cube + identity
+    curve, where one 8-bit step is 25/255 stops."""
+    import os
+    d = "/tmp/rr_identity_luts"
+    os.makedirs(os.path.join(d, "luts"), exist_ok=True)
+    with open(os.path.join(d, "luts", HO.FILMIC_LUT_FILES[0]), "w") as fh:
+        fh.write("SPILUT 1.0\n3 3\n2 2 2\n")
+        for i in range(2):
+            for j in range(2):
+                for k in range(2):
+                    fh.write(f"{i} {j} {k} {0.66 * i} {0.66 * j} {0.66 * k}\n")
+    with open(os.path.join(d, "luts", HO.FILMIC_LUT_FILES[1]), "w") as fh:
+        fh.write("Version 1\nFrom 0 1\nLength 2\nComponents 1\n{\n0\n1\n}\n")
+    O.set_filmic(HO.load_filmic_luts(d))
+    try:
+        x = np.exp2(np.linspace(-12.4, 12.5, 4001)).astype(np.float32)
+        got = O.filmic(np.stack([x, x, x], 1))[:, 0].astype(int)
+        a = (np.log2(x.astype(np.float64)) + 12.473931188) / 25.0
+        exp = np.floor(np.clip(a, 0, 1) * 255 + 0.5)
+        assert np.abs(got - exp).max() <= 1 and (got == exp).mean() > 0.99
+    finally:
+        O.set_filmic(None)

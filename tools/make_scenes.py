@@ -13,6 +13,12 @@
                                 albedo * world exactly (convex, 1 bounce).
   test_pointlight.rrscene       Lambert plane under a point light of radius 0,
                                 black world: closed-form irradiance.
+  test_enclosure_diffuse.rrscene  camera inside a closed emissive white Lambert
+                                sphere, black world: with per-lobe bounce caps
+                                every path returns E (1 + 1 + ... ) over exactly
+                                cap + 1 hits (Cycles max_diffuse_bounces).
+  test_enclosure_glossy.rrscene the same with a white metallic near-mirror
+                                (max_glossy_bounces).
   02_physics-standin.rrscene    stand-in for the missing 02_physics.blend (SURVEY.md
                                 §8d C4): 2,000 falling/bouncing rigid bodies
                                 (cubes + icospheres, ~92k triangles) over a ground
@@ -24,7 +30,7 @@
                                 20,480 triangles (10,485,760) + ground plane,
                                 3840x2160, 1024 spp, 4 bounces, 240 frames,
                                 per-instance rigid motion (rebuild per frame).
-Usage: python tools/make_scenes.py
+Usage: python tools/make_scenes.py [--tests-only]
 """
 from __future__ import annotations
 
@@ -143,8 +149,43 @@ def c5_scene():
                          [4], [1, 200], resolution=(3840, 2160), samples=1024, max_bounces=4, extra=tweak)
 
 
+def enclosure(name: str, material: dict, sub: int) -> dict:
+    """Camera at the centre of a closed emissive icosphere (radius 5, emission
+    0.25), black world, no lights, indirect clamp off: a path's radiance is
+    0.25 x (number of hits before a bounce cap ends it), since white Lambert /
+    white mirror-like metal keep the throughput at 1."""
+    return {
+        "format": "rrscene", "version": 1, "name": name,
+        "source": {"generator": "tools/make_scenes.py", "purpose": "per-lobe bounce caps, known answer"},
+        "render": {"resolution_x": 32, "resolution_y": 24, "resolution_percentage": 100, "fps": 24,
+                   "frame_start": 1, "frame_end": 1, "filter_width": 1.5, "view_transform": "Raw",
+                   "exposure": 0.0, "samples": 8, "max_bounces": 12, "max_diffuse_bounces": 4,
+                   "max_glossy_bounces": 4, "clamp_indirect": 0.0, "seed": 11},
+        "world": {"color": [0.0, 0.0, 0.0], "strength": 1.0},
+        "materials": [dict(material, emission=[0.25, 0.25, 0.25], emission_strength=1.0)],
+        "meshes": [{"name": "shell", "generator": {"type": "icosphere", "subdivisions": sub, "radius": 5.0},
+                    "material_slots": [0]}],
+        "objects": [camera_object("Camera", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), lens=35.0),
+                    {"name": "Shell", "type": "MESH", "mesh": 0, "location": [0, 0, 0],
+                     "rotation_euler": [0, 0, 0], "scale": [1, 1, 1], "parent": -1}],
+        "camera": 0,
+    }
+
+
+def test_scenes():
+    write("test_enclosure_diffuse.rrscene", enclosure(
+        "test_enclosure_diffuse", {"name": "white_lambert", "model": "lambert", "base_color": [1.0, 1.0, 1.0],
+                                   "metallic": 0.0, "specular": 0.0, "roughness": 1.0, "ior": 1.45}, 1))
+    write("test_enclosure_glossy.rrscene", enclosure(
+        "test_enclosure_glossy", {"name": "white_mirror", "model": "principled", "base_color": [1.0, 1.0, 1.0],
+                                  "metallic": 1.0, "specular": 0.5, "roughness": 0.0, "ior": 1.45}, 3))
+
+
 def main():
     os.makedirs(SCENES, exist_ok=True)
+    test_scenes()
+    if "--tests-only" in sys.argv:
+        return
     s01 = export_01()
 
     s04 = copy.deepcopy(s01)
