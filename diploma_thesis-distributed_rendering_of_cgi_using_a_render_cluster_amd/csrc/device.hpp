@@ -208,6 +208,10 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
 void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, float4* d_hits,
                         int32_t* d_prims, uint8_t* d_occ, hipStream_t st, int width);
 
+// BSDF sampling batch at one shading point (debug / parity entry point).
+void bsdf_batch_device(const float* d_mat12, const float n3[3], const float wo3[3], int n, const float* d_u,
+                       float* d_wi, float* d_f, float* d_pdf, int32_t* d_ok, hipStream_t st);
+
 // Device JPEG forward transform (jpeg.hip); tab = dct | qinv luma | qinv chroma.
 void jpeg_fdct_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, int16_t* d_out, hipStream_t st);
 

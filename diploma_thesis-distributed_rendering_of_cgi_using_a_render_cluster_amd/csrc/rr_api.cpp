@@ -1073,6 +1073,34 @@ int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int
     });
 }
 
+int rr_debug_bsdf_sample(rr_ctx* c, const float* mat12, const float* n3, const float* wo3, int32_t n,
+                         const float* u, float* wi3, float* f3, float* pdf, int32_t* ok) {
+    if (!c || !mat12 || !n3 || !wo3 || n < 0 || (n > 0 && (!u || !wi3 || !f3 || !pdf || !ok)))
+        return fail(RR_EINVAL, "bad arguments");
+    return guarded([&] {
+        if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
+        set_device(c);
+        hipStream_t st = c->stream;
+        const size_t m = n > 0 ? (size_t)n : 1;
+        DevBuf<float> dm, du, dw, df, dp;
+        DevBuf<int32_t> dk;
+        dm.ensure(RR_MAT_FLOATS);
+        du.ensure(3 * m); dw.ensure(3 * m); df.ensure(3 * m); dp.ensure(m); dk.ensure(m);
+        RR_HIP(hipMemcpyAsync(dm.ptr, mat12, RR_MAT_FLOATS * sizeof(float), hipMemcpyHostToDevice, st));
+        if (n > 0) RR_HIP(hipMemcpyAsync(du.ptr, u, 3 * (size_t)n * sizeof(float), hipMemcpyHostToDevice, st));
+        bsdf_batch_device(dm.ptr, n3, wo3, n, du.ptr, dw.ptr, df.ptr, dp.ptr, dk.ptr, st);
+        if (n > 0) {
+            RR_HIP(hipMemcpyAsync(wi3, dw.ptr, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));
+            RR_HIP(hipMemcpyAsync(f3, df.ptr, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));
+            RR_HIP(hipMemcpyAsync(pdf, dp.ptr, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));
+            RR_HIP(hipMemcpyAsync(ok, dk.ptr, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        }
+        RR_HIP(hipStreamSynchronize(st));
+        dm.release(); du.release(); dw.release(); df.release(); dp.release(); dk.release();
+        return RR_OK;
+    });
+}
+
 int rr_debug_object_matrix(rr_scene* s, int32_t obj, double frame, double* m16) {
     if (!s || !m16) return fail(RR_EINVAL, "NULL argument");
     return guarded([&] {

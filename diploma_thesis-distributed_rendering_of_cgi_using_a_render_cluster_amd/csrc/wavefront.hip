@@ -1647,6 +1647,28 @@ __global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* 
     }
 }
 
+// BSDF sampling at one shading point for n draws (parity with oracle
+// orc_bsdf_sample): the material as the frame kernels load it (mat_derive),
+// the view terms once (bsdf_view), then bsdf_sample per (ul, u1, u2).
+// ok: 0 the path ends, 1 diffuse lobe, 2 glossy lobe.
+__global__ void k_debug_bsdf(const float* __restrict__ mat12, float3 N, float3 wo, int n, const float* __restrict__ u,
+                             float* __restrict__ wi3, float* __restrict__ f3, float* __restrict__ pdf,
+                             int32_t* __restrict__ ok) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    Mat m = load_mat(mat12, 0);
+    mat_derive(m);
+    const BsdfView vw = bsdf_view(m, N, wo);
+    float3 wi = mk3(0.0f, 0.0f, 0.0f), f = wi;
+    float p = 0.0f;
+    bool glossy = false;
+    const bool good = bsdf_sample(m, vw, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], wi, f, p, glossy);
+    wi3[3 * i] = wi.x; wi3[3 * i + 1] = wi.y; wi3[3 * i + 2] = wi.z;
+    f3[3 * i] = f.x; f3[3 * i + 1] = f.y; f3[3 * i + 2] = f.z;
+    pdf[i] = p;
+    ok[i] = good ? (glossy ? 2 : 1) : 0;
+}
+
 __global__ void k_debug_trace4(const Bvh4Node* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
                                int n, const float4* __restrict__ rays, float4* __restrict__ hits,
                                int32_t* __restrict__ prims, uint8_t* __restrict__ occ,
@@ -2058,6 +2080,15 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
     }
+    RR_HIP(hipGetLastError());
+}
+
+void bsdf_batch_device(const float* d_mat12, const float n3[3], const float wo3[3], int n, const float* d_u,
+                       float* d_wi, float* d_f, float* d_pdf, int32_t* d_ok, hipStream_t st) {
+    if (n > 0)
+        k_debug_bsdf<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(d_mat12, mk3(n3[0], n3[1], n3[2]),
+                                                                   mk3(wo3[0], wo3[1], wo3[2]), n, d_u, d_wi, d_f,
+                                                                   d_pdf, d_ok);
     RR_HIP(hipGetLastError());
 }
 

@@ -80,6 +80,7 @@ EXPORTS = [
     "rr_last_warning", "rr_set_ocio_config", "rr_synchronize",
     "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
     "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_bvh4", "rr_debug_bvh_hier", "rr_debug_jpeg_device",
+    "rr_debug_bsdf_sample",
 ]
 
 _lib = None
@@ -133,6 +134,7 @@ def lib() -> ctypes.CDLL:
         "rr_debug_jpeg_device": (c_int, [P, u8p, i32, i32, i32, u8p, ctypes.c_uint64,
                                          ctypes.POINTER(ctypes.c_uint64)]),
         "rr_debug_object_matrix": (c_int, [P, i32, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
+        "rr_debug_bsdf_sample": (c_int, [P, f32p, f32p, f32p, i32, f32p, f32p, f32p, f32p, i32p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -365,6 +367,19 @@ class RenderContext:
         _check(lib().rr_debug_jpeg_device(self.handle, _ptr(rgba, ctypes.c_uint8), w, h, int(quality),
                                           _ptr(out, ctypes.c_uint8), n.value, ctypes.byref(n)), self.handle)
         return out.tobytes()
+
+    def bsdf_sample(self, mat12, n, wo, u):
+        """rr_debug_bsdf_sample: (wi [k,3], f [k,3], pdf [k], ok [k]: 0 end, 1 diffuse, 2 glossy)."""
+        f32 = lambda a: np.ascontiguousarray(a, dtype=np.float32)  # noqa: E731
+        m, n, wo, u = f32(mat12), f32(n), f32(wo), f32(u).reshape(-1, 3)
+        k = u.shape[0]
+        wi, f = np.zeros((k, 3), np.float32), np.zeros((k, 3), np.float32)
+        pdf, ok = np.zeros(k, np.float32), np.zeros(k, np.int32)
+        _check(lib().rr_debug_bsdf_sample(self.handle, _ptr(m, ctypes.c_float), _ptr(n, ctypes.c_float),
+                                          _ptr(wo, ctypes.c_float), k, _ptr(u, ctypes.c_float),
+                                          _ptr(wi, ctypes.c_float), _ptr(f, ctypes.c_float),
+                                          _ptr(pdf, ctypes.c_float), _ptr(ok, ctypes.c_int32)), self.handle)
+        return wi, f, pdf, ok
 
     def trace(self, scene: Scene, frame: int, rays: np.ndarray, width: int = 0):
         """rr_debug_trace; width 0 = the hierarchy the frame kernels use."""

@@ -287,6 +287,14 @@ int rr_debug_trace(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t bv
                    int32_t n_rays, const float* rays, float* hits, int32_t* prims,
                    uint8_t* occluded);
 
+/* BSDF sampling at one shading point, as the frame kernels sample it: the
+ * material (RR_MAT_FLOATS, rr_debug_frame_state layout), unit normal n3 and
+ * view direction wo3; per draw i the three numbers u[3i..3i+2] (lobe pick,
+ * disk u1, u2). Outputs per draw: wi3, f3 (BSDF value), pdf and ok (0 the
+ * path ends, 1 diffuse lobe, 2 glossy lobe). */
+int rr_debug_bsdf_sample(rr_ctx* ctx, const float* mat12, const float* n3, const float* wo3, int32_t n,
+                         const float* u, float* wi3, float* f3, float* pdf, int32_t* ok);
+
 /* Host animation evaluation: object_to_world matrix (row-major 4x4, f64) of
  * object `object_index` at (possibly fractional) frame. */
 int rr_debug_object_matrix(rr_scene* scene, int32_t object_index, double frame,

@@ -169,6 +169,18 @@ def bsdf_sample(mat12, n, wo, u):
     return wi, f, pdf, ok.astype(bool)
 
 
+def bsdf_sample_lobes(mat12, n, wo, u):
+    """bsdf_sample with the lobe: ok 0 (path ends), 1 diffuse, 2 glossy (rr_debug_bsdf_sample)."""
+    m, n, wo, u = _f32(mat12), _f32(n), _f32(wo), _f32(u).reshape(-1, 3)
+    k = u.shape[0]
+    wi, f = np.zeros((k, 3), np.float32), np.zeros((k, 3), np.float32)
+    pdf, ok = np.zeros(k, np.float32), np.zeros(k, np.int32)
+    lib().orc_bsdf_sample(_p(m, ctypes.c_float), _p(n, ctypes.c_float), _p(wo, ctypes.c_float), k,
+                          _p(u, ctypes.c_float), _p(wi, ctypes.c_float), _p(f, ctypes.c_float),
+                          _p(pdf, ctypes.c_float), _p(ok, ctypes.c_int32))
+    return wi, f, pdf, ok
+
+
 def bsdf_eval_n(mat12, n, wo, wi):
     """eval_bsdf at one shading point for each row of wi: (f [k,3], pdf [k])."""
     m, n, wo, wi = _f32(mat12), _f32(n), _f32(wo), _f32(wi).reshape(-1, 3)

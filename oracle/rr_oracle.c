@@ -1224,6 +1224,7 @@ void orc_bsdf_sample(const float* mat12, const float* n3, const float* wo3, int 
         float p = 0.0f;
         int glossy = 0;
         ok[i] = sample_bsdf(&m, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], &wi, &f, &p, &glossy);
+        if (ok[i]) ok[i] = 1 + glossy;  /* 1 diffuse lobe, 2 glossy lobe (rr_debug_bsdf_sample) */
         wi3[3 * i] = wi.x; wi3[3 * i + 1] = wi.y; wi3[3 * i + 2] = wi.z;
         f3[3 * i] = f.x; f3[3 * i + 1] = f.y; f3[3 * i + 2] = f.z;
         pdf[i] = p;
