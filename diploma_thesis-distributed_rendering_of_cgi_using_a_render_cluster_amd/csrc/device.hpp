@@ -141,10 +141,13 @@ struct DevPaths {
     DevBuf<float4> film;
     DevBuf<float4> film_part;  // open sample group's partial sum between chunks (k_accumulate)
     DevBuf<float> tile_slab;   // k_tiles: per sliced tile, one group sum plane per sample group
+    DevBuf<uint32_t> tile_ctrs;  // k_tiles: work-unit counters, one 128-B line per shard
     DevBuf<uint8_t> rgba8;
     DevBuf<float> filter_table;
     DevBuf<float> srgb_lut;
     DevBuf<float> lights, materials;
+    DevBuf<float> mat_lut;             // material tables (build_material_lut), uploaded when they change
+    std::vector<float> mat_lut_cached;
     DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: 6 totals
     KernelProfiler prof;
     bool count_traversal = false;
@@ -209,8 +212,8 @@ void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, f
                         int32_t* d_prims, uint8_t* d_occ, hipStream_t st, int width);
 
 // BSDF sampling batch at one shading point (debug / parity entry point).
-void bsdf_batch_device(const float* d_mat12, const float n3[3], const float wo3[3], int n, const float* d_u,
-                       float* d_wi, float* d_f, float* d_pdf, int32_t* d_ok, hipStream_t st);
+void bsdf_batch_device(const float* d_mat12, const float* d_lut, const float n3[3], const float wo3[3], int n,
+                       const float* d_u, float* d_wi, float* d_f, float* d_pdf, int32_t* d_ok, hipStream_t st);
 
 // Device JPEG forward transform (jpeg.hip); tab = dct | qinv luma | qinv chroma.
 void jpeg_fdct_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, int16_t* d_out, hipStream_t st);

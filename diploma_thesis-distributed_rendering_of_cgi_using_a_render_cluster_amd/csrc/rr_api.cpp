@@ -32,6 +32,9 @@
 
 using namespace rr;
 
+static_assert(kMatLutIntervals == kMatLutN && kMatLutFloatsPerMat == kMatLutStride,
+              "scene.hpp material-table layout must match rr_device.h");
+
 namespace {
 
 thread_local std::string g_err;
@@ -232,6 +235,13 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
         p.srgb_lut.ensure(lut.size());
         RR_HIP(hipMemcpy(p.srgb_lut.ptr, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice));
         c->srgb_uploaded = true;
+    }
+    if (p.mat_lut_cached != fs.mat_lut) {  // material tables: static per scene, uploaded when they change
+        p.mat_lut.ensure(fs.mat_lut.size());
+        RR_HIP(hipMemcpyAsync(p.mat_lut.ptr, fs.mat_lut.data(), fs.mat_lut.size() * sizeof(float),
+                              hipMemcpyHostToDevice, st));
+        RR_HIP(hipStreamSynchronize(st));  // pageable source: the copy must be done before fs goes away
+        p.mat_lut_cached = fs.mat_lut;
     }
     const size_t nl = fs.lights.size(), nm = fs.materials.size(), nx = fs.obj_xform.size();
     p.lights.ensure(nl ? nl : 1);
@@ -1082,13 +1092,17 @@ int rr_debug_bsdf_sample(rr_ctx* c, const float* mat12, const float* n3, const f
         set_device(c);
         hipStream_t st = c->stream;
         const size_t m = n > 0 ? (size_t)n : 1;
-        DevBuf<float> dm, du, dw, df, dp;
+        DevBuf<float> dm, du, dw, df, dp, dl;
         DevBuf<int32_t> dk;
+        float lut[kMatLutFloatsPerMat];
+        build_material_lut(mat12, lut);
+        dl.ensure(kMatLutFloatsPerMat);
+        RR_HIP(hipMemcpyAsync(dl.ptr, lut, sizeof lut, hipMemcpyHostToDevice, st));
         dm.ensure(RR_MAT_FLOATS);
         du.ensure(3 * m); dw.ensure(3 * m); df.ensure(3 * m); dp.ensure(m); dk.ensure(m);
         RR_HIP(hipMemcpyAsync(dm.ptr, mat12, RR_MAT_FLOATS * sizeof(float), hipMemcpyHostToDevice, st));
         if (n > 0) RR_HIP(hipMemcpyAsync(du.ptr, u, 3 * (size_t)n * sizeof(float), hipMemcpyHostToDevice, st));
-        bsdf_batch_device(dm.ptr, n3, wo3, n, du.ptr, dw.ptr, df.ptr, dp.ptr, dk.ptr, st);
+        bsdf_batch_device(dm.ptr, dl.ptr, n3, wo3, n, du.ptr, dw.ptr, df.ptr, dp.ptr, dk.ptr, st);
         if (n > 0) {
             RR_HIP(hipMemcpyAsync(wi3, dw.ptr, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));
             RR_HIP(hipMemcpyAsync(f3, df.ptr, 3 * (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));
@@ -1096,7 +1110,8 @@ int rr_debug_bsdf_sample(rr_ctx* c, const float* mat12, const float* n3, const f
             RR_HIP(hipMemcpyAsync(ok, dk.ptr, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         }
         RR_HIP(hipStreamSynchronize(st));
-        dm.release(); du.release(); dw.release(); df.release(); dp.release(); dk.release();
+        RR_HIP(hipStreamSynchronize(st));
+        dm.release(); du.release(); dw.release(); df.release(); dp.release(); dk.release(); dl.release();
         return RR_OK;
     });
 }

@@ -241,19 +241,27 @@ RR_HD bool slab(float3 o, float3 invd, float bx0, float by0, float bz0, float bx
     return tn <= tf;
 }
 
-// Moeller-Trumbore, two-sided. Returns t (and u, v) or false.
+// Moeller-Trumbore, two-sided, with the barycentric test done before the
+// division: with a = |det| and the numerators un = tv.pv, vn = d.qv taken with
+// det's sign, the ray meets the triangle iff 0 <= un <= a, vn >= 0, un + vn <= a
+// (no rounding in the sign flips); only then is 1/det computed for t, u, v.
+// Most leaf tests of a traversal miss, and they no longer divide.
+RR_HD bool bary_pass(float det, float un, float vn) {
+    const bool neg = det < 0.0f;
+    const float a = neg ? -det : det, su = neg ? -un : un, sv = neg ? -vn : vn;
+    return !(det == 0.0f) && !(su < 0.0f || su > a) && !(sv < 0.0f || su + sv > a);
+}
 RR_HD bool tri_test(float3 o, float3 d, float3 v0, float3 e1, float3 e2, float& t, float& u,
                     float& v) {
     const float3 pv = cross3(d, e2);
     const float det = dot3(e1, pv);
-    if (det == 0.0f) return false;
-    const float inv = 1.0f / det;
     const float3 tv = sub3(o, v0);
-    u = dot3(tv, pv) * inv;
-    if (u < 0.0f || u > 1.0f) return false;
     const float3 qv = cross3(tv, e1);
-    v = dot3(d, qv) * inv;
-    if (v < 0.0f || u + v > 1.0f) return false;
+    const float un = dot3(tv, pv), vn = dot3(d, qv);
+    if (!bary_pass(det, un, vn)) return false;
+    const float inv = 1.0f / det;
+    u = un * inv;
+    v = vn * inv;
     t = dot3(e2, qv) * inv;
     return true;
 }
@@ -540,6 +548,17 @@ RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float
 // (bsdf_microfacet.h, interpolate_fresnel_color / fresnel_dielectric_cos in
 // bsdf_util.h); Cycles is third-party and not in the reference tree, so this
 // restatement is unpinned against Cycles' own output.
+//
+// The two functions of a material that need a square root and two divisions
+// each — Cycles' Fresnel blend FH and the specular-lobe pick probability —
+// are tabulated per material on the host (build_material_lut, identical
+// double-precision construction in the oracle) and read by linear
+// interpolation: kMatLutN intervals over cos in [0, 1], FH against the cosine
+// of the half angle, the pick probability against the cosine of the view
+// angle (interpolation error below 4e-4 for specular IORs 1.2 .. 2).
+constexpr int kMatLutN = 128;
+constexpr int kMatLutStride = 260;  // floats per material: FH [0, 128], ps [129, 257], 2 pad
+
 struct Mat {
     float3 base;
     float metallic, specular, roughness, ior;
@@ -548,33 +567,16 @@ struct Mat {
     // per-material terms (mat_derive), evaluated once per material load
     float alpha, a2;   // GGX roughness alpha = max(roughness^2, 1e-3), alpha^2
     float3 cspec0;     // Cycles cspec0 = saturate(0.08 specular (1 - metallic) + base metallic)
-    float ior_s;       // specular IOR = 2 / (1 - sqrt(0.08 specular)) - 1
-    float f0d, f0n;    // F0 = fresnel_dielectric_cos(1, ior_s), 1 / (1 - F0)
-    float wd;          // diffuse closure sample weight = (1 - metallic) * average(base)
     float kd0;         // (1 - metallic) / pi
     int spec_on;       // the specular closure exists (specular or metallic > 1e-5)
 };
-
-// Cycles fresnel_dielectric_cos: reflectance of a dielectric of relative IOR
-// eta at incidence cosine cosi, without the refracted direction (1 under TIR).
-RR_HD float fresnel_dielectric_cos(float cosi, float eta) {
-    const float c = fabsf(cosi);
-    float g = eta * eta - 1.0f + c * c;
-    if (g > 0.0f) {
-        g = sqrtf(g);
-        const float A = (g - c) / (g + c);
-        const float B = (c * (g + c) - 1.0f) / (c * (g - c) + 1.0f);
-        return 0.5f * A * A * (1.0f + B * B);
-    }
-    return 1.0f;
-}
 
 RR_HD float saturatef_(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
 
 RR_HD void mat_derive(Mat& m) {
     // alpha floor 1e-3 (roughness 0.032): below it the float GGX terms break
-    // down (a2 - 1 rounds to -1, D = a2 / (pi tt^2) overflows at N.H = 1);
-    // Cycles switches to a singular mirror lobe below alpha^2 = 1e-7 instead
+    // down (a2 - 1 rounds to -1, D overflows at N.H = 1); Cycles switches to
+    // a singular mirror lobe below alpha^2 = 1e-7 instead
     float alpha = m.roughness * m.roughness;
     if (alpha < 1.0e-3f) alpha = 1.0e-3f;
     m.alpha = alpha;
@@ -582,10 +584,6 @@ RR_HD void mat_derive(Mat& m) {
     const float sm = m.specular * 0.08f * (1.0f - m.metallic);
     m.cspec0 = mk3(saturatef_(sm + m.base.x * m.metallic), saturatef_(sm + m.base.y * m.metallic),
                    saturatef_(sm + m.base.z * m.metallic));
-    m.ior_s = 2.0f / (1.0f - sqrtf(0.08f * m.specular)) - 1.0f;
-    m.f0d = fresnel_dielectric_cos(1.0f, m.ior_s);
-    m.f0n = 1.0f / (1.0f - m.f0d);
-    m.wd = (1.0f - m.metallic) * ((m.base.x + m.base.y + m.base.z) * 0.333333343f);
     m.kd0 = (1.0f - m.metallic) * 0.318309886183791f;
     m.spec_on = (m.specular > 1.0e-5f || m.metallic > 1.0e-5f) ? 1 : 0;
 }
@@ -597,10 +595,10 @@ RR_HD float schlick_w(float c) {
     return m2 * m2 * m;
 }
 
-// Cycles interpolate_fresnel_color: the dielectric Fresnel at cos, normalised
-// against its value at normal incidence, blends cspec0 towards white.
-RR_HD float fresnel_blend(const Mat& m, float cos_theta) {
-    return (fresnel_dielectric_cos(cos_theta, m.ior_s) - m.f0d) * m.f0n;
+// A material table channel at u in [0, 1] (t: global or LDS pointer).
+template <typename FloatP>
+RR_HD float lut_at(FloatP t, float u) {
+    return table_lerp(t, kMatLutN + 1, fminf(fmaxf(u, 0.0f), 1.0f));
 }
 
 // Terms of the view direction shared by every evaluation at one shading point
@@ -609,14 +607,19 @@ struct BsdfView {
     float cosV, ps, fv, g1v;
 };
 
-// f (cosine not included) and the combined one-sample-MIS pdf of the two
-// closures (Cycles surface_shader_bsdf_eval: every closure evaluated, pdfs
-// weighted by the closures' sample weights):
+// f * cosL (the BSDF times the cosine of the light direction, Cycles'
+// convention) and the combined one-sample-MIS pdf of the two closures (Cycles
+// surface_shader_bsdf_eval: every closure evaluated, pdfs weighted by the
+// closures' sample weights):
 //   diffuse  base (1 - metallic) / pi * [(1 - FV/2)(1 - FL/2) + RR (FL + FV + FL FV (RR - 1))],
 //            RR = roughness (L.V + 1)            (PRINCIPLED_DIFFUSE_FULL)
 //   specular F * D G1(V) G1(L) / (4 cosV cosL), GGX D, separable Smith G1,
-//            F = cspec0 (1 - FH) + FH, FH = fresnel_blend(L.H)
-RR_HD float3 bsdf_eval_v(const Mat& m, const BsdfView& vw, float3 N, float3 wo, float3 wi, float& pdf) {
+//            F = cspec0 (1 - FH) + FH, FH = the table at L.H
+// with |V + L|^2 = 2 + 2 L.V, so (N.H)^2 = (cosV + cosL)^2 / (2 + 2 L.V) and
+// (L.H)^2 = (1 + L.V) / 2 (no normalised half vector).
+// lut: this material's table (kMatLutStride floats).
+template <typename FloatP>
+RR_HD float3 bsdf_eval_v(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, float3 wo, float3 wi, float& pdf) {
     const float cosV = vw.cosV;
     const float cosL = dot3(N, wi);
     if (cosV <= 0.0f || cosL <= 0.0f) {
@@ -625,49 +628,37 @@ RR_HD float3 bsdf_eval_v(const Mat& m, const BsdfView& vw, float3 N, float3 wo, 
     }
     if (m.model == 1) {
         pdf = cosL * 0.318309886183791f;
-        return scl3(m.base, 0.318309886183791f);
+        return scl3(m.base, pdf);
     }
     const float ps = vw.ps;
-    const float3 H = norm3(add3(wo, wi));
-    const float cosD = dot3(wi, H);
-    const float NdotH = dot3(N, H);
+    const float lv = dot3(wi, wo);
     const float a2 = m.a2;
     // diffuse
     const float fl = schlick_w(cosL);
     const float fv = vw.fv;
-    const float rr = m.roughness * (dot3(wi, wo) + 1.0f);
-    const float kd = m.kd0 * ((1.0f - 0.5f * fv) * (1.0f - 0.5f * fl) + rr * (fl + fv + fl * fv * (rr - 1.0f)));
+    const float rr = m.roughness * (lv + 1.0f);
+    const float kd =
+        m.kd0 * ((1.0f - 0.5f * fv) * (1.0f - 0.5f * fl) + rr * (fl + fv + fl * fv * (rr - 1.0f))) * cosL;
     // specular
-    const float tt = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
-    const float D = a2 / (3.14159265358979f * tt * tt);
-    const float g1v = vw.g1v;
+    const float sv = cosV + cosL;
+    const float nh2 = sv * sv / (2.0f + 2.0f * lv);
+    const float tt = nh2 * (a2 - 1.0f) + 1.0f;
+    const float pdf_s = vw.g1v * a2 / (12.5663706143592f * tt * tt * cosV);  // D G1(V) / (4 cosV)
     const float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
-    const float fh = fresnel_blend(m, cosD);
-    const float ks = m.spec_on ? D * g1v * g1l / (4.0f * cosV * cosL) : 0.0f;
+    const float ks = m.spec_on ? pdf_s * g1l : 0.0f;  // D G1(V) G1(L) / (4 cosV cosL) * cosL
+    const float fh = lut_at(lut, sqrtf((1.0f + lv) * 0.5f));  // L.H = sqrt((1 + L.V) / 2)
     const float3 c0 = m.cspec0;
     const float3 F = mk3(c0.x * (1.0f - fh) + fh, c0.y * (1.0f - fh) + fh, c0.z * (1.0f - fh) + fh);
     const float pdf_d = cosL * 0.318309886183791f;
-    const float pdf_s = g1v * D / (4.0f * cosV);
     pdf = (1.0f - ps) * pdf_d + ps * pdf_s;
     return mk3(m.base.x * kd + F.x * ks, m.base.y * kd + F.y * ks, m.base.z * kd + F.z * ks);
 }
 
-// Probability of picking the specular lobe: the closures' sample weights
-// (Cycles bsdf_microfacet_fresnel_color: the specular weight times the
-// average Fresnel colour at the view angle; diffuse: average(base) (1 - metallic)).
-RR_HD float spec_prob(const Mat& m, float cosV) {
-    if (m.model == 1 || !m.spec_on) return 0.0f;
-    const float fh = fresnel_blend(m, cosV);
-    const float3 c0 = m.cspec0;
-    const float wsp = ((c0.x * (1.0f - fh) + fh) + (c0.y * (1.0f - fh) + fh) + (c0.z * (1.0f - fh) + fh)) * 0.333333343f;
-    const float tot = wsp + m.wd;
-    return tot > 0.0f ? wsp / tot : 1.0f;
-}
-
-RR_HD BsdfView bsdf_view(const Mat& m, float3 N, float3 wo) {
+template <typename FloatP>
+RR_HD BsdfView bsdf_view(const Mat& m, FloatP lut, float3 N, float3 wo) {
     BsdfView v;
     v.cosV = dot3(N, wo);
-    v.ps = spec_prob(m, v.cosV);
+    v.ps = lut_at(lut + (kMatLutN + 1), v.cosV);  // 0 for Lambert and without a specular closure
     v.fv = schlick_w(v.cosV);
     const float a2 = m.a2;
     v.g1v = 2.0f * v.cosV / (v.cosV + sqrtf(a2 + (1.0f - a2) * v.cosV * v.cosV));
@@ -675,40 +666,37 @@ RR_HD BsdfView bsdf_view(const Mat& m, float3 N, float3 wo) {
 }
 
 // The one-shot form (tests / inspection): same result as bsdf_eval_v with
-// bsdf_view(m, N, wo), except that the caller's ps is used.
-RR_HD float3 bsdf_eval(const Mat& m, float3 N, float3 wo, float3 wi, float ps, float& pdf) {
-    BsdfView v = bsdf_view(m, N, wo);
+// bsdf_view(m, lut, N, wo), except that the caller's ps is used.
+template <typename FloatP>
+RR_HD float3 bsdf_eval(const Mat& m, FloatP lut, float3 N, float3 wo, float3 wi, float ps, float& pdf) {
+    BsdfView v = bsdf_view(m, lut, N, wo);
     v.ps = ps;
-    return bsdf_eval_v(m, v, N, wo, wi, pdf);
+    return bsdf_eval_v(m, lut, v, N, wo, wi, pdf);
 }
 
-// GGX visible-normal sample (Heitz 2018) in the local frame (N = +z).
-// (dx, dy): concentric_disk(u1, u2), drawn by the caller (bsdf_sample shares
-// it between the lobes).
+// GGX visible-normal sample in the local frame (N = +z), by spherical caps
+// (Dupuy & Benyoub 2023): in the stretched configuration the visible normals
+// of the view vh are vh + c for c uniform on the cap z > -vh.z of the unit
+// sphere. (dx, dy): concentric_disk(u1, u2) (r^2 = dx^2 + dy^2 uniform, the
+// angle uniform), drawn by the caller (bsdf_sample shares it between the
+// lobes): z = 1 - r^2 (1 + vz), and (x, y) = (dx, dy) sqrt((1 + vz)(2 - r^2 (1 + vz)))
+// so that x^2 + y^2 = 1 - z^2, without a division.
 RR_HD float3 sample_vndf(float3 v, float alpha, float dx, float dy) {
     const float3 vh = norm3(mk3(alpha * v.x, alpha * v.y, v.z));
-    const float lensq = vh.x * vh.x + vh.y * vh.y;
-    float3 t1;
-    if (lensq > 0.0f) {
-        const float il = 1.0f / sqrtf(lensq);
-        t1 = mk3(-vh.y * il, vh.x * il, 0.0f);
-    } else {
-        t1 = mk3(1.0f, 0.0f, 0.0f);
-    }
-    const float3 t2 = cross3(vh, t1);
-    const float s = 0.5f * (1.0f + vh.z);
-    dy = (1.0f - s) * sqrtf(fmaxf(0.0f, 1.0f - dx * dx)) + s * dy;
-    const float nz = sqrtf(fmaxf(0.0f, 1.0f - dx * dx - dy * dy));
-    const float3 nh = mk3(dx * t1.x + dy * t2.x + nz * vh.x, dx * t1.y + dy * t2.y + nz * vh.y,
-                          dx * t1.z + dy * t2.z + nz * vh.z);
-    return norm3(mk3(alpha * nh.x, alpha * nh.y, fmaxf(0.0f, nh.z)));
+    const float r2 = dx * dx + dy * dy;
+    const float k = 1.0f + vh.z;
+    const float z = 1.0f - r2 * k;
+    const float s = sqrtf(fmaxf(0.0f, k * (2.0f - r2 * k)));
+    const float3 h = mk3(dx * s + vh.x, dy * s + vh.y, fmaxf(0.0f, z + vh.z));
+    return norm3(mk3(alpha * h.x, alpha * h.y, h.z));
 }
 
-// Sample a direction; returns false when the path must end. glossy: the
-// specular lobe was picked (Cycles LABEL_GLOSSY; else LABEL_DIFFUSE), which
-// decides the bounce counter the scatter advances.
-RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, float ul, float u1, float u2,
-                       float3& wi, float3& f, float& pdf, bool& glossy) {
+// Sample a direction; returns false when the path must end. f: f * cosL as
+// bsdf_eval_v. glossy: the specular lobe was picked (Cycles LABEL_GLOSSY;
+// else LABEL_DIFFUSE), which decides the bounce counter the scatter advances.
+template <typename FloatP>
+RR_HD bool bsdf_sample(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, float3 wo, float ul, float u1,
+                       float u2, float3& wi, float3& f, float& pdf, bool& glossy) {
     const float cosV = vw.cosV;
     if (cosV <= 0.0f) return false;
     const float ps = vw.ps;
@@ -728,7 +716,7 @@ RR_HD bool bsdf_sample(const Mat& m, const BsdfView& vw, float3 N, float3 wo, fl
         const float z = sqrtf(fmaxf(0.0f, 1.0f - x * x - y * y));
         wi = mk3(T.x * x + B.x * y + N.x * z, T.y * x + B.y * y + N.y * z, T.z * x + B.z * y + N.z * z);
     }
-    f = bsdf_eval_v(m, vw, N, wo, wi, pdf);
+    f = bsdf_eval_v(m, lut, vw, N, wo, wi, pdf);
     return pdf > 0.0f;
 }
 

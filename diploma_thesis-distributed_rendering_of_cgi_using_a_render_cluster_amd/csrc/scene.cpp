@@ -807,6 +807,50 @@ SceneDesc load_scene(const std::string& path) {
     return s;
 }
 
+namespace {
+// Cycles fresnel_dielectric_cos (bsdf_util.h), in double for the tables.
+double fresnel_dielectric_d(double cosi, double eta) {
+    const double c = std::fabs(cosi);
+    double g = eta * eta - 1.0 + c * c;
+    if (g > 0.0) {
+        g = std::sqrt(g);
+        const double A = (g - c) / (g + c);
+        const double B = (c * (g + c) - 1.0) / (c * (g - c) + 1.0);
+        return 0.5 * A * A * (1.0 + B * B);
+    }
+    return 1.0;
+}
+double clamp01(double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); }
+}  // namespace
+
+void build_material_lut(const float* m, float* out) {
+    const int N = kMatLutIntervals;
+    const double spec = m[4], met = m[3];
+    const double b[3] = {m[0], m[1], m[2]};
+    const int model = (int)m[10];
+    const bool spec_on = m[4] > 1.0e-5f || m[3] > 1.0e-5f;
+    // Cycles principled closure setup: ior = 2 / (1 - sqrt(0.08 specular)) - 1,
+    // cspec0 = 0.08 specular (1 - metallic) + base metallic (specular tint 0)
+    const double eta = 2.0 / (1.0 - std::sqrt(0.08 * spec)) - 1.0;
+    const double f0 = fresnel_dielectric_d(1.0, eta);
+    double c0[3];
+    for (int k = 0; k < 3; ++k) c0[k] = clamp01(spec * 0.08 * (1.0 - met) + b[k] * met);
+    const double wd = (1.0 - met) * ((b[0] + b[1] + b[2]) / 3.0);
+    for (int i = 0; i <= N; ++i) {
+        const double c = (double)i / N;  // cos of the half angle
+        out[i] = (float)((fresnel_dielectric_d(c, eta) - f0) / (1.0 - f0));
+    }
+    for (int i = 0; i <= N; ++i) {
+        const double c = (double)i / N;  // cos of the view angle
+        const double fh = (fresnel_dielectric_d(c, eta) - f0) / (1.0 - f0);
+        const double wsp = ((c0[0] * (1.0 - fh) + fh) + (c0[1] * (1.0 - fh) + fh) + (c0[2] * (1.0 - fh) + fh)) / 3.0;
+        double ps = 0.0;
+        if (model != 1 && spec_on) ps = wsp + wd > 0.0 ? wsp / (wsp + wd) : 1.0;
+        out[N + 1 + i] = (float)ps;
+    }
+    for (int i = 2 * (N + 1); i < kMatLutFloatsPerMat; ++i) out[i] = 0.0f;
+}
+
 FrameSetup setup_frame(const SceneDesc& s, int frame, const rr_render_params* p) {
     rr_render_params d;
     rr_render_params_default(&d);
@@ -899,6 +943,9 @@ FrameSetup setup_frame(const SceneDesc& s, int frame, const rr_render_params* p)
         for (int k = 0; k < 3; ++k) M[7 + k] = (float)(md.emission[k] * md.emission_strength);
         M[10] = (float)md.model;
         f.materials.insert(f.materials.end(), M, M + RR_MAT_FLOATS);
+        float lut[kMatLutFloatsPerMat];
+        build_material_lut(M, lut);
+        f.mat_lut.insert(f.mat_lut.end(), lut, lut + kMatLutFloatsPerMat);
     }
     for (int k = 0; k < 3; ++k) f.world[k] = (float)(s.world_color[k] * s.world_strength);
     // object transforms (row-major 3x4, float)

@@ -141,6 +141,7 @@ struct FrameSetup {
     float cam[RR_CAM_FLOATS] = {};
     std::vector<float> lights;     // n * RR_LIGHT_FLOATS
     std::vector<float> materials;  // n * RR_MAT_FLOATS
+    std::vector<float> mat_lut;    // n * kMatLutFloatsPerMat (build_material_lut)
     float world[3] = {0, 0, 0};
     std::vector<float> obj_xform;  // n_objects * 12 (3x4 row-major, float)
 };
@@ -159,6 +160,14 @@ FrameSetup setup_frame(const SceneDesc& s, int frame, const rr_render_params* p)
 constexpr int kFilterTableSize = 1024;
 constexpr int kSrgbLutSize = 4096;
 void build_filter_table(float width, float* table /* kFilterTableSize */);
+// Per-material tables of the Principled closures (rr_device.h kMatLutN,
+// kMatLutStride): Cycles' Fresnel blend FH against cos of the half angle and
+// the specular-lobe pick probability against cos of the view angle, in double
+// from the material's RR_MAT_FLOATS floats (oracle/rr_oracle.c builds them the
+// same way).
+constexpr int kMatLutIntervals = 128;
+constexpr int kMatLutFloatsPerMat = 260;
+void build_material_lut(const float* mat12, float* out /* kMatLutFloatsPerMat */);
 void build_srgb_lut(float* lut /* kSrgbLutSize + 1 */);
 
 }  // namespace rr

@@ -93,6 +93,7 @@ struct SceneView {
     NodeP nodes;
     TriP tris;
     FloatP mats, lights, filter;
+    FloatP lut;  // material tables (kMatLutStride floats per material, build_material_lut)
     lds_f4w* cam = nullptr;  // LDS scenes, camera kernels: 3 float4 per triangle (stage_camera)
     lds_f4w* nrm = nullptr;   // LDS scenes, shading kernels: unit geometric normal per triangle
 };
@@ -224,7 +225,9 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         return;
     }
     const TriPack tp = load_tri(v.tris, h.idx);
-    const Mat m = view_mat(v, f2i(tp.p1.w));
+    const int mid = f2i(tp.p1.w);
+    const Mat m = view_mat(v, mid);
+    const auto lut = v.lut + kMatLutStride * mid;
     const float t = h.t;
     const float3 P = mk3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
     float3 N;
@@ -240,7 +243,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         add_to(L, c);
     }
     if (path_capped(fc, bounce, lob)) return;
-    const BsdfView vw = bsdf_view(m, N, wo);
+    const BsdfView vw = bsdf_view(m, lut, N, wo);
     const uint32_t dim0 = 2u + (uint32_t)(kDimsPerBounce * bounce);
     const float3 Po = offset_ray(P, N);
     // next-event estimation toward one uniformly chosen light
@@ -269,9 +272,10 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
                 const float3 ts = sub3(sp, P);
                 const float ds2 = dot3(ts, ts);
                 dist = sqrtf(ds2);
-                wi = scl3(ts, 1.0f / dist);
+                const float id = 1.0f / dist;
+                wi = scl3(ts, id);
                 const float cl = fabsf(dot3(wl, wi));
-                Li = scl3(I, cl / ds2);
+                Li = scl3(I, cl * id * id);
             } else {
                 dist = sqrtf(dl2);
                 wi = scl3(tl, 1.0f / dist);
@@ -285,8 +289,8 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         const float cosN = dot3(N, wi);
         if (cosN > 0.0f) {
             float pdf;
-            const float3 f = bsdf_eval_v(m, vw, N, wo, wi, pdf);
-            const float k = cosN * (float)fc.n_lights;
+            const float3 f = bsdf_eval_v(m, lut, vw, N, wo, wi, pdf);  // f * cosN
+            const float k = (float)fc.n_lights;
             float3 c = mk3(T.x * f.x * k * Li.x, T.y * f.y * k * Li.y, T.z * f.z * k * Li.z);
             if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
             if (max3f(c) > 0.0f) {
@@ -302,18 +306,17 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     float3 wi, f;
     float pdf;
     bool glossy;
-    if (!bsdf_sample(m, vw, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f, pdf,
-                     glossy))
+    if (!bsdf_sample(m, lut, vw, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f,
+                     pdf, glossy))
         return;
-    const float cosL = dot3(N, wi);
-    if (!(cosL > 0.0f)) return;
-    const float k = cosL / pdf;
+    const float k = 1.0f / pdf;  // f = f * cosL already
     T = mk3(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
     if (!(max3f(T) > 0.0f)) return;
     if (bounce >= kRrStartBounce) {
         const float q = fminf(max3f(T), 1.0f);
         if (rng(key, dim0 + 6u) >= q) return;
-        T = mk3(T.x / q, T.y / q, T.z / q);
+        const float iq = 1.0f / q;
+        T = mk3(T.x * iq, T.y * iq, T.z * iq);
     }
     out.cont = true;
     out.o = Po;
@@ -448,16 +451,17 @@ RR_D void count_wave(uint32_t* __restrict__ ctr, bool pred) {
 }  // namespace
 struct SceneArgs {
     const BvhNode* nodes;
-    const Bvh4Node* nodes4;  // split path (large scenes)
+    const Bvh4Node* nodes4;  // BVH4 collapse (rr_debug_trace only)
     const TriPack* tris;
     const float* mats;
     const float* lights;
     const float* filter;
+    const float* mat_lut;    // kMatLutStride floats per material
     int n_nodes, n_tris, n_mats, n_lights;
 };
 
 namespace {
-RR_D GlobalView global_view(const SceneArgs& a) { return {a.nodes, a.tris, a.mats, a.lights, a.filter}; }
+RR_D GlobalView global_view(const SceneArgs& a) { return {a.nodes, a.tris, a.mats, a.lights, a.filter, a.mat_lut}; }
 
 RR_D void lds_copy(lds_f4w* dst, const float4* __restrict__ src, int n4) {
     const rr_f4v* s = reinterpret_cast<const rr_f4v*>(src);
@@ -558,7 +562,7 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
     v.tris = (lds_tri*)q;
     lds_copy(q, reinterpret_cast<const float4*>(a.tris), 3 * a.n_tris);
     q += 3 * a.n_tris;
-    v.mats = v.lights = v.filter = nullptr;
+    v.mats = v.lights = v.filter = v.lut = nullptr;
     if (shading) {
         v.mats = (lds_float*)q;
         lds_copy(q, reinterpret_cast<const float4*>(a.mats), 3 * a.n_mats);
@@ -569,6 +573,9 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
         v.filter = (lds_float*)q;
         lds_copy(q, reinterpret_cast<const float4*>(a.filter), kFilterN / 4);
         q += kFilterN / 4;
+        v.lut = (lds_float*)q;
+        lds_copy(q, reinterpret_cast<const float4*>(a.mat_lut), kMatLutStride / 4 * a.n_mats);
+        q += kMatLutStride / 4 * a.n_mats;
     }
     if (shading || cam_fc) __syncthreads();  // the copies above are visible
     if (shading) {  // per-triangle unit normals
@@ -620,19 +627,18 @@ RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float
             const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2), tv = xyz(ca), qv = xyz(cb);
             const float3 pv = cross3(d, e2);
             const float det = dot3(e1, pv);
-            const float inv = 1.0f / det;
-            const float u = dot3(tv, pv) * inv;
-            const float vv = dot3(d, qv) * inv;
-            const float t = ca.w * inv;
-            const int orig = f2i(tp.p0.w);
-            const bool ok = !(det == 0.0f) && !(u < 0.0f || u > 1.0f) && !(vv < 0.0f || u + vv > 1.0f) &&
-                            t > tmin && (t < h.t || (t == h.t && orig < h.orig));
-            if (ok) {
-                h.t = t;
-                h.u = u;
-                h.v = vv;
-                h.idx = i;
-                h.orig = orig;
+            const float un = dot3(tv, pv), vn = dot3(d, qv);
+            if (bary_pass(det, un, vn)) {  // tri_test's order: the division only for rays that meet it
+                const float inv = 1.0f / det;
+                const float u = un * inv, vv = vn * inv, t = ca.w * inv;
+                const int orig = f2i(tp.p0.w);
+                if (t > tmin && (t < h.t || (t == h.t && orig < h.orig))) {
+                    h.t = t;
+                    h.u = u;
+                    h.v = vv;
+                    h.idx = i;
+                    h.orig = orig;
+                }
             }
         }
     }
@@ -1313,6 +1319,8 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
 // and shading work, so the long tiles start early and the background tiles,
 // whose samples are all culled camera rays, fill the tail.
 constexpr int kTile = 8;  // 8x8 pixels = one wave
+constexpr int kTileShards = 8;      // k_tiles unit counters (one per block % 8)
+constexpr int kTileCtrStride = 32;  // words between them (128 B)
 
 struct TileOrder {
     int tx, n;               // tiles per row, tiles in the frame
@@ -1459,23 +1467,34 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     const TileOrder to = uniform_order(tile_order(fc, cull));
     const int lane = threadIdx.x & 63;
     // Work units: each tile of the screen-rectangle box is cut into sl.n slices,
-    // one per sample group (box tiles first), every other tile is one unit.
+    // one per sample group; every other tile is one unit whose samples are all
+    // culled (the world term). Those are dealt statically (wave w takes the
+    // tiles nb + w, nb + w + waves, ...: no atomics for the cheap units); the
+    // box slices come from n_shards = min(grid, kTileShards) counters, one per
+    // group of blocks with equal blockIdx % n_shards (blocks are dealt
+    // round-robin over the 8 XCDs, so a shard's atomics stay in one XCD's L2),
+    // shard g handing out slices g, g + n_shards, ... One counter for every
+    // unit serialised ~35k device-scope atomics on one address per 04vs frame.
     const int ng = (fc.spp_total + kFilmGroup - 1) / kFilmGroup;
     const int nb = to.bw * to.bh;
     const int n_sliced = nb * sl.n;
-    const int n_units = n_sliced + (to.n - nb);
+    const int nwaves = (int)(gridDim.x * kWavesPerBlock);
+    const int n_shards = min((int)gridDim.x, kTileShards);  // small frames launch fewer blocks than shards
+    const int shard = (int)blockIdx.x % n_shards;
+    int a_next = nb + (int)wave_id();  // this wave's next background tile (static)
     for (;;) {
-        int u = 0;
-        if (lane == 0) u = (int)atomicAdd(tile_ctr, 1u);
-        u = __builtin_amdgcn_readlane(u, 0);
-        if (u >= n_units) break;
         int t, k = 0, nk = 1;  // tile, slice, slices of this tile
-        if (u < n_sliced) {
+        if (a_next < to.n) {
+            t = a_next;
+            a_next += nwaves;
+        } else {
+            int u = 0;
+            if (lane == 0) u = (int)atomicAdd(tile_ctr + shard * kTileCtrStride, 1u);
+            u = __builtin_amdgcn_readlane(u, 0) * n_shards + shard;
+            if (u >= n_sliced) break;
             t = u / sl.n;
             k = u - t * sl.n;
             nk = sl.n;
-        } else {
-            t = u - n_sliced + nb;
         }
         int tx, ty;
         to.at(t, tx, ty);
@@ -1651,18 +1670,23 @@ __global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* 
 // orc_bsdf_sample): the material as the frame kernels load it (mat_derive),
 // the view terms once (bsdf_view), then bsdf_sample per (ul, u1, u2).
 // ok: 0 the path ends, 1 diffuse lobe, 2 glossy lobe.
-__global__ void k_debug_bsdf(const float* __restrict__ mat12, float3 N, float3 wo, int n, const float* __restrict__ u,
-                             float* __restrict__ wi3, float* __restrict__ f3, float* __restrict__ pdf,
-                             int32_t* __restrict__ ok) {
+// f3: the BSDF value f (f * cosL / cosL, as the oracle's export reports it).
+__global__ void k_debug_bsdf(const float* __restrict__ mat12, const float* __restrict__ lut, float3 N, float3 wo,
+                             int n, const float* __restrict__ u, float* __restrict__ wi3, float* __restrict__ f3,
+                             float* __restrict__ pdf, int32_t* __restrict__ ok) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     Mat m = load_mat(mat12, 0);
     mat_derive(m);
-    const BsdfView vw = bsdf_view(m, N, wo);
+    const BsdfView vw = bsdf_view(m, lut, N, wo);
     float3 wi = mk3(0.0f, 0.0f, 0.0f), f = wi;
     float p = 0.0f;
     bool glossy = false;
-    const bool good = bsdf_sample(m, vw, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], wi, f, p, glossy);
+    const bool good = bsdf_sample(m, lut, vw, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], wi, f, p, glossy);
+    if (good) {
+        const float cosL = dot3(N, wi);
+        f = mk3(f.x / cosL, f.y / cosL, f.z / cosL);
+    }
     wi3[3 * i] = wi.x; wi3[3 * i + 1] = wi.y; wi3[3 * i + 2] = wi.z;
     f3[3 * i] = f.x; f3[3 * i + 1] = f.y; f3[3 * i + 2] = f.z;
     pdf[i] = p;
@@ -1766,18 +1790,19 @@ int grid_for(K kernel, size_t dyn_lds) {
 // kernels take the LDS-resident variant: at most ~12 KB next to the 16 KB
 // traversal stack and the <= 8 KB segment prefix keeps 4 blocks of the
 // register-limited kernels per CU.
-constexpr size_t kLdsSceneMax = 12 * 1024;
+constexpr size_t kLdsSceneMax = 16 * 1024;
 size_t scene_budget_bytes(const FrameConsts& fc) {  // the residency test's measure (scene_in_lds)
     const int n_nodes = std::max(fc.n_tris - 1, 1);
-    return 16 * (4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris + 3 * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights +
-                 kFilterN / 4);
+    return 16 * (4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris + (3 + kMatLutStride / 4) * (size_t)fc.n_mats +
+                 3 * (size_t)fc.n_lights + kFilterN / 4);
 }
 // What stage_scene stages (without the camera data): + the normals (1 float4
 // per triangle) when shading.
 size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
     const int n_nodes = std::max(fc.n_tris - 1, 1);
     size_t f4 = 4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris;
-    if (shading) f4 += 3 * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4 + (size_t)fc.n_tris;
+    if (shading)
+        f4 += (3 + kMatLutStride / 4) * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4 + (size_t)fc.n_tris;
     return 16 * f4;
 }
 }  // namespace
@@ -1893,8 +1918,10 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
-    counters.release(); spill.release(); tile_slab.release(); film_part.release(); segs.release(); hits.release(); qctr.release();
+    counters.release(); tile_ctrs.release(); spill.release(); tile_slab.release(); film_part.release(); segs.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
+    mat_lut.release();
+    mat_lut_cached.clear();
     trav_counts.release();
     prof.release();
     cap = 0;
@@ -1987,7 +2014,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
             tc = p.trav_counts.ptr;
         }
         const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
-                           std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
+                           p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
         FrameConsts fc = base;
         fc.first_sample = 0;
         fc.spp_chunk = base.spp_total;
@@ -1999,7 +2026,9 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         }
         const int g = clamp_grid(tiles * 64, G.tiles);
         p.prof.begin(st, RR_K_TILES);
-        G.kx<<<g, kBlock, G.dyn_primary, st>>>(fc, sa, tot + 2 * (base.max_bounces + 1), p.film.ptr, p.srgb_lut.ptr,
+        p.tile_ctrs.ensure((size_t)kTileShards * kTileCtrStride);
+        RR_HIP(hipMemsetAsync(p.tile_ctrs.ptr, 0, sizeof(uint32_t) * kTileShards * kTileCtrStride, st));
+        G.kx<<<g, kBlock, G.dyn_primary, st>>>(fc, sa, p.tile_ctrs.ptr, p.film.ptr, p.srgb_lut.ptr,
                                                reinterpret_cast<uchar4*>(p.rgba8.ptr), tot, p.spill.ptr, tc, sl);
         if (sl.n > 1)
             k_tiles_fold<<<(int)std::min<long>((tiles + kWavesPerBlock - 1) / kWavesPerBlock, 2048), kBlock, 0, st>>>(
@@ -2025,7 +2054,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     KernelProfiler& pr = p.prof;
     const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
-                       std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
+                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
     if (!G.lds && base.n_tris > 0) {
         render_split(p, base, n_chunks, st, sa, tc, pq, sq);
         RR_HIP(hipGetLastError());
@@ -2083,10 +2112,10 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     RR_HIP(hipGetLastError());
 }
 
-void bsdf_batch_device(const float* d_mat12, const float n3[3], const float wo3[3], int n, const float* d_u,
-                       float* d_wi, float* d_f, float* d_pdf, int32_t* d_ok, hipStream_t st) {
+void bsdf_batch_device(const float* d_mat12, const float* d_lut, const float n3[3], const float wo3[3], int n,
+                       const float* d_u, float* d_wi, float* d_f, float* d_pdf, int32_t* d_ok, hipStream_t st) {
     if (n > 0)
-        k_debug_bsdf<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(d_mat12, mk3(n3[0], n3[1], n3[2]),
+        k_debug_bsdf<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(d_mat12, d_lut, mk3(n3[0], n3[1], n3[2]),
                                                                    mk3(wo3[0], wo3[1], wo3[2]), n, d_u, d_wi, d_f,
                                                                    d_pdf, d_ok);
     RR_HIP(hipGetLastError());

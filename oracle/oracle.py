@@ -44,6 +44,7 @@ def lib():
         L.orc_bsdf_sample.argtypes = [f, f, f, c_int, f, f, f, f, i32]
         L.orc_filter_table.argtypes = [ctypes.c_float, f]
         L.orc_srgb_lut.argtypes = [f]
+        L.orc_material_lut.argtypes = [f, f]
         L.orc_set_filmic.argtypes = [f, c_int, f, c_int, c_int, ctypes.c_float, ctypes.c_float]
         L.orc_filmic.argtypes = [c_int, f, u8]
         _lib = L
@@ -227,4 +228,12 @@ def filmic(rgb: np.ndarray) -> np.ndarray:
     rgb = _f32(rgb).reshape(-1, 3)
     out = np.zeros((rgb.shape[0], 3), np.uint8)
     lib().orc_filmic(rgb.shape[0], _p(rgb, ctypes.c_float), _p(out, ctypes.c_uint8))
+    return out
+
+
+def material_lut(mat12) -> np.ndarray:
+    """The material's table (Fresnel blend | lobe pick probability, 260 floats)."""
+    m = _f32(mat12)
+    out = np.zeros(260, np.float32)
+    lib().orc_material_lut(_p(m, ctypes.c_float), _p(out, ctypes.c_float))
     return out

@@ -496,18 +496,27 @@ static int slab_test(v3 o, v3 inv, const float* b, float tmin, float tmax, float
     return tn <= tf;
 }
 
+/* Moeller-Trumbore with the barycentric test before the division
+ * (csrc/rr_device.h bary_pass / tri_test): with a = |det| and the numerators
+ * taken with det's sign, the ray meets the triangle iff 0 <= un <= a, vn >= 0,
+ * un + vn <= a; only then t, u, v = numerators / det. */
+static int bary_pass(float det, float un, float vn) {
+    int neg = det < 0.0f;
+    float a = neg ? -det : det, su = neg ? -un : un, sv = neg ? -vn : vn;
+    return !(det == 0.0f) && !(su < 0.0f || su > a) && !(sv < 0.0f || su + sv > a);
+}
+
 static int mt_test(v3 o, v3 d, const float* t9, float* t, float* u, float* v) {
     v3 v0 = V(t9[0], t9[1], t9[2]), e1 = V(t9[3], t9[4], t9[5]), e2 = V(t9[6], t9[7], t9[8]);
     v3 pv = vcross(d, e2);
     float det = vdot(e1, pv);
-    if (det == 0.0f) return 0;
-    float inv = 1.0f / det;
     v3 tv = vsub(o, v0);
-    *u = vdot(tv, pv) * inv;
-    if (*u < 0.0f || *u > 1.0f) return 0;
     v3 qv = vcross(tv, e1);
-    *v = vdot(d, qv) * inv;
-    if (*v < 0.0f || *u + *v > 1.0f) return 0;
+    float un = vdot(tv, pv), vn = vdot(d, qv);
+    if (!bary_pass(det, un, vn)) return 0;
+    float inv = 1.0f / det;
+    *u = un * inv;
+    *v = vn * inv;
     *t = vdot(e2, qv) * inv;
     return 1;
 }
@@ -616,27 +625,66 @@ static int trace(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hit
  * with Fresnel of bsdf_microfacet.h (interpolate_fresnel_color,
  * fresnel_dielectric_cos of bsdf_util.h; sample weight scaled by the average
  * Fresnel colour at the view angle). Same float operations as
- * csrc/rr_device.h mat_derive / bsdf_eval_v / spec_prob. */
+ * csrc/rr_device.h mat_derive / bsdf_eval_v / bsdf_view / bsdf_sample; the
+ * Fresnel blend and the lobe pick probability are read from per-material
+ * tables built in double exactly as csrc/scene.cpp build_material_lut. */
 typedef struct { v3 base; float metallic, specular, roughness, ior; v3 emission; int model; } mat_t;
+
+#define ORC_LUT_N 128
+#define ORC_LUT_STRIDE 260
 
 static float sw(float c) { float m = 1.0f - c; if (m < 0.0f) m = 0.0f; float m2 = m * m; return m2 * m2 * m; }
 
-static float fresnel_dielectric_cos(float cosi, float eta) {
-    float c = fabsf(cosi);
-    float g = eta * eta - 1.0f + c * c;
-    if (g > 0.0f) {
-        g = sqrtf(g);
-        float A = (g - c) / (g + c);
-        float B = (c * (g + c) - 1.0f) / (c * (g - c) + 1.0f);
-        return 0.5f * A * A * (1.0f + B * B);
+static double fresnel_dielectric_d(double cosi, double eta) {
+    double c = fabs(cosi);
+    double g = eta * eta - 1.0 + c * c;
+    if (g > 0.0) {
+        g = sqrt(g);
+        double A = (g - c) / (g + c);
+        double B = (c * (g + c) - 1.0) / (c * (g - c) + 1.0);
+        return 0.5 * A * A * (1.0 + B * B);
     }
-    return 1.0f;
+    return 1.0;
+}
+
+static double clamp01d(double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); }
+
+/* FH(cos of the half angle) [0, 128] | spec pick probability(cos of the view) [129, 257] */
+void orc_material_lut(const float* m, float* out) {
+    const int N = ORC_LUT_N;
+    double spec = m[4], met = m[3];
+    double b[3] = {m[0], m[1], m[2]};
+    int model = (int)m[10];
+    int spec_on = m[4] > 1.0e-5f || m[3] > 1.0e-5f;
+    double eta = 2.0 / (1.0 - sqrt(0.08 * spec)) - 1.0;
+    double f0 = fresnel_dielectric_d(1.0, eta);
+    double c0[3];
+    for (int k = 0; k < 3; ++k) c0[k] = clamp01d(spec * 0.08 * (1.0 - met) + b[k] * met);
+    double wd = (1.0 - met) * ((b[0] + b[1] + b[2]) / 3.0);
+    for (int i = 0; i <= N; ++i) {
+        double c = (double)i / N;
+        out[i] = (float)((fresnel_dielectric_d(c, eta) - f0) / (1.0 - f0));
+    }
+    for (int i = 0; i <= N; ++i) {
+        double c = (double)i / N;
+        double fh = (fresnel_dielectric_d(c, eta) - f0) / (1.0 - f0);
+        double wsp = ((c0[0] * (1.0 - fh) + fh) + (c0[1] * (1.0 - fh) + fh) + (c0[2] * (1.0 - fh) + fh)) / 3.0;
+        double ps = 0.0;
+        if (model != 1 && spec_on) ps = wsp + wd > 0.0 ? wsp / (wsp + wd) : 1.0;
+        out[N + 1 + i] = (float)ps;
+    }
+    for (int i = 2 * (N + 1); i < ORC_LUT_STRIDE; ++i) out[i] = 0.0f;
+}
+
+static float lut_at(const float* t, float u) {
+    u = fminf(fmaxf(u, 0.0f), 1.0f);
+    return lerp_table(t, ORC_LUT_N + 1, u);
 }
 
 static float sat1(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
 
 /* terms Cycles derives at closure setup */
-typedef struct { float alpha, a2, ior_s, f0d, f0n, wd, kd0; v3 cspec0; int spec_on; } mterms;
+typedef struct { float alpha, a2, kd0; v3 cspec0; int spec_on; } mterms;
 
 static mterms mat_terms(const mat_t* m) {
     mterms t;
@@ -647,101 +695,80 @@ static mterms mat_terms(const mat_t* m) {
     float sm = m->specular * 0.08f * (1.0f - m->metallic);
     t.cspec0 = V(sat1(sm + m->base.x * m->metallic), sat1(sm + m->base.y * m->metallic),
                  sat1(sm + m->base.z * m->metallic));
-    t.ior_s = 2.0f / (1.0f - sqrtf(0.08f * m->specular)) - 1.0f;
-    t.f0d = fresnel_dielectric_cos(1.0f, t.ior_s);
-    t.f0n = 1.0f / (1.0f - t.f0d);
-    t.wd = (1.0f - m->metallic) * ((m->base.x + m->base.y + m->base.z) * 0.333333343f);
     t.kd0 = (1.0f - m->metallic) * 0.318309886183791f;
     t.spec_on = (m->specular > 1.0e-5f || m->metallic > 1.0e-5f) ? 1 : 0;
     return t;
 }
 
-static float fresnel_blend(const mterms* t, float c) { return (fresnel_dielectric_cos(c, t->ior_s) - t->f0d) * t->f0n; }
+static float g1_of(float a2, float c) { return 2.0f * c / (c + sqrtf(a2 + (1.0f - a2) * c * c)); }
 
-static v3 eval_bsdf(const mat_t* m, v3 N, v3 wo, v3 wi, float ps, float* pdf) {
+/* f * cosL and the combined pdf (csrc/rr_device.h bsdf_eval_v) */
+static v3 eval_bsdf(const mat_t* m, const float* lut, v3 N, v3 wo, v3 wi, float ps, float* pdf) {
     float cosV = vdot(N, wo), cosL = vdot(N, wi);
     if (cosV <= 0.0f || cosL <= 0.0f) { *pdf = 0.0f; return V(0.0f, 0.0f, 0.0f); }
     if (m->model == 1) { /* pure Lambert */
         *pdf = cosL * 0.318309886183791f;
-        return vscl(m->base, 0.318309886183791f);
+        return vscl(m->base, *pdf);
     }
     mterms T = mat_terms(m);
-    v3 H = vnorm(vadd(wo, wi));
-    float cosD = vdot(wi, H), NdotH = vdot(N, H);
+    float lv = vdot(wi, wo);
     float a2 = T.a2;
-    /* diffuse: (1 - FV/2)(1 - FL/2) + RR (FL + FV + FL FV (RR - 1)), RR = roughness (L.V + 1) */
     float fl = sw(cosL), fv = sw(cosV);
-    float rr = m->roughness * (vdot(wi, wo) + 1.0f);
-    float kd = T.kd0 * ((1.0f - 0.5f * fv) * (1.0f - 0.5f * fl) + rr * (fl + fv + fl * fv * (rr - 1.0f)));
-    /* GGX, separable Smith G1 */
-    float tt = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
-    float D = a2 / (3.14159265358979f * tt * tt);
-    float g1v = 2.0f * cosV / (cosV + sqrtf(a2 + (1.0f - a2) * cosV * cosV));
-    float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
-    float fh = fresnel_blend(&T, cosD);
-    float ks = T.spec_on ? D * g1v * g1l / (4.0f * cosV * cosL) : 0.0f;
+    float rr = m->roughness * (lv + 1.0f);
+    float kd = T.kd0 * ((1.0f - 0.5f * fv) * (1.0f - 0.5f * fl) + rr * (fl + fv + fl * fv * (rr - 1.0f))) * cosL;
+    float sv = cosV + cosL;
+    float nh2 = sv * sv / (2.0f + 2.0f * lv);
+    float tt = nh2 * (a2 - 1.0f) + 1.0f;
+    float g1v = g1_of(a2, cosV);
+    float pdf_s = g1v * a2 / (12.5663706143592f * tt * tt * cosV);
+    float g1l = g1_of(a2, cosL);
+    float ks = T.spec_on ? pdf_s * g1l : 0.0f;
+    float fh = lut_at(lut, sqrtf((1.0f + lv) * 0.5f));
     v3 c0 = T.cspec0;
     v3 F = V(c0.x * (1.0f - fh) + fh, c0.y * (1.0f - fh) + fh, c0.z * (1.0f - fh) + fh);
     float pdf_d = cosL * 0.318309886183791f;
-    float pdf_s = g1v * D / (4.0f * cosV);
     *pdf = (1.0f - ps) * pdf_d + ps * pdf_s;
     return V(m->base.x * kd + F.x * ks, m->base.y * kd + F.y * ks, m->base.z * kd + F.z * ks);
 }
 
-static float p_spec(const mat_t* m, float cosV) {
-    if (m->model == 1) return 0.0f;
-    mterms T = mat_terms(m);
-    if (!T.spec_on) return 0.0f;
-    float fh = fresnel_blend(&T, cosV);
-    v3 c0 = T.cspec0;
-    float wsp = ((c0.x * (1.0f - fh) + fh) + (c0.y * (1.0f - fh) + fh) + (c0.z * (1.0f - fh) + fh)) * 0.333333343f;
-    float tot = wsp + T.wd;
-    return tot > 0.0f ? wsp / tot : 1.0f;
-}
+static float p_spec(const float* lut, float cosV) { return lut_at(lut + ORC_LUT_N + 1, cosV); }
 
-static v3 vndf(v3 v, float alpha, float u1, float u2) {
+/* GGX visible normals by spherical caps (Dupuy & Benyoub 2023), csrc/rr_device.h sample_vndf */
+static v3 vndf(v3 v, float alpha, float dx, float dy) {
     v3 vh = vnorm(V(alpha * v.x, alpha * v.y, v.z));
-    float lensq = vh.x * vh.x + vh.y * vh.y;
-    v3 t1;
-    if (lensq > 0.0f) {
-        float il = 1.0f / sqrtf(lensq);
-        t1 = V(-vh.y * il, vh.x * il, 0.0f);
-    } else t1 = V(1.0f, 0.0f, 0.0f);
-    v3 t2 = vcross(vh, t1);
-    float dx, dy;
-    disk(u1, u2, &dx, &dy);
-    float s = 0.5f * (1.0f + vh.z);
-    dy = (1.0f - s) * sqrtf(fmaxf(0.0f, 1.0f - dx * dx)) + s * dy;
-    float nz = sqrtf(fmaxf(0.0f, 1.0f - dx * dx - dy * dy));
-    v3 nh = V(dx * t1.x + dy * t2.x + nz * vh.x, dx * t1.y + dy * t2.y + nz * vh.y, dx * t1.z + dy * t2.z + nz * vh.z);
-    return vnorm(V(alpha * nh.x, alpha * nh.y, fmaxf(0.0f, nh.z)));
+    float r2 = dx * dx + dy * dy;
+    float k = 1.0f + vh.z;
+    float z = 1.0f - r2 * k;
+    float s = sqrtf(fmaxf(0.0f, k * (2.0f - r2 * k)));
+    v3 h = V(dx * s + vh.x, dy * s + vh.y, fmaxf(0.0f, z + vh.z));
+    return vnorm(V(alpha * h.x, alpha * h.y, h.z));
 }
 
-/* glossy: the specular lobe was picked (Cycles LABEL_GLOSSY, else LABEL_DIFFUSE) */
-static int sample_bsdf(const mat_t* m, v3 N, v3 wo, float ul, float u1, float u2, v3* wi, v3* f, float* pdf,
-                       int* glossy) {
+/* glossy: the specular lobe was picked (Cycles LABEL_GLOSSY, else LABEL_DIFFUSE); f = f * cosL */
+static int sample_bsdf(const mat_t* m, const float* lut, v3 N, v3 wo, float ul, float u1, float u2, v3* wi, v3* f,
+                       float* pdf, int* glossy) {
     float cosV = vdot(N, wo);
     if (cosV <= 0.0f) return 0;
-    float ps = p_spec(m, cosV);
+    float ps = p_spec(lut, cosV);
     v3 T, B;
     onb(N, &T, &B);
+    float x, y;
+    disk(u1, u2, &x, &y);
     *glossy = ul < ps;
     if (ul < ps) {
         float alpha = m->roughness * m->roughness;
         if (alpha < 1.0e-3f) alpha = 1.0e-3f;
         v3 wl = V(vdot(wo, T), vdot(wo, B), cosV);
-        v3 hl = vndf(wl, alpha, u1, u2);
+        v3 hl = vndf(wl, alpha, x, y);
         v3 H = V(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,
                  T.z * hl.x + B.z * hl.y + N.z * hl.z);
         float k = 2.0f * vdot(wo, H);
         *wi = V(H.x * k - wo.x, H.y * k - wo.y, H.z * k - wo.z);
     } else {
-        float x, y;
-        disk(u1, u2, &x, &y);
         float z = sqrtf(fmaxf(0.0f, 1.0f - x * x - y * y));
         *wi = V(T.x * x + B.x * y + N.x * z, T.y * x + B.y * y + N.y * z, T.z * x + B.z * y + N.z * z);
     }
-    *f = eval_bsdf(m, N, wo, *wi, ps, pdf);
+    *f = eval_bsdf(m, lut, N, wo, *wi, ps, pdf);
     return *pdf > 0.0f;
 }
 
@@ -763,6 +790,7 @@ typedef struct {
     v3 world;
     int W, H, spp, max_bounces, view;
     int max_diffuse, max_glossy;  /* Cycles per-lobe bounce caps (>= 1) */
+    float* luts;                  /* ORC_LUT_STRIDE floats per material */
     uint32_t seed;
     float clamp, inv_w2, inv_h2;
     float filter[ORC_FILTER_N];
@@ -844,7 +872,9 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
         }
         const float* tp = S->bvh->tri + 9 * (size_t)h.idx;
         v3 e1 = V(tp[3], tp[4], tp[5]), e2 = V(tp[6], tp[7], tp[8]);
-        mat_t m = load_mat(S->mats, S->bvh->tri_mat[h.idx]);
+        const int mid = S->bvh->tri_mat[h.idx];
+        mat_t m = load_mat(S->mats, mid);
+        const float* lut = S->luts + ORC_LUT_STRIDE * (size_t)mid;
         float t = h.t;
         v3 P = V(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
         v3 N = vnorm(vcross(e1, e2));
@@ -887,9 +917,10 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
                     v3 ts = vsub(sp, P);
                     float ds2 = vdot(ts, ts);
                     dist = sqrtf(ds2);
-                    wi = vscl(ts, 1.0f / dist);
+                    float id = 1.0f / dist;
+                    wi = vscl(ts, id);
                     float cl = fabsf(vdot(wl, wi));
-                    Li = vscl(I, cl / ds2);
+                    Li = vscl(I, cl * id * id);
                 } else {
                     dist = sqrtf(dl2);
                     wi = vscl(tl, 1.0f / dist);
@@ -903,9 +934,9 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
             float cosN = vdot(N, wi);
             if (cosN > 0.0f) {
                 float pdf;
-                float ps = p_spec(&m, vdot(N, wo));
-                v3 f = eval_bsdf(&m, N, wo, wi, ps, &pdf);
-                float k = cosN * (float)S->n_lights;
+                float ps = p_spec(lut, vdot(N, wo));
+                v3 f = eval_bsdf(&m, lut, N, wo, wi, ps, &pdf); /* f * cosN */
+                float k = (float)S->n_lights;
                 v3 cc = V(T.x * f.x * k * Li.x, T.y * f.y * k * Li.y, T.z * f.z * k * Li.z);
                 if (b > 0) cc = clampc(cc, S->clamp);
                 if (vmax3(cc) > 0.0f) { shadow = 1; sh_dir = wi; sh_dist = dist; sh_c = cc; }
@@ -914,17 +945,17 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
         int alive = 0, glossy = 0;
         v3 wi, f;
         float pdf;
-        if (sample_bsdf(&m, N, wo, rnd(key, dim0 + 3u), rnd(key, dim0 + 4u), rnd(key, dim0 + 5u), &wi, &f, &pdf,
-                        &glossy)) {
-            float cosL = vdot(N, wi);
-            if (cosL > 0.0f) {
-                float k = cosL / pdf;
-                T = V(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
-                alive = vmax3(T) > 0.0f;
-                if (alive && b >= 3) {
-                    float q = fminf(vmax3(T), 1.0f);
-                    if (rnd(key, dim0 + 6u) >= q) alive = 0;
-                    else T = V(T.x / q, T.y / q, T.z / q);
+        if (sample_bsdf(&m, lut, N, wo, rnd(key, dim0 + 3u), rnd(key, dim0 + 4u), rnd(key, dim0 + 5u), &wi, &f,
+                        &pdf, &glossy)) {
+            float k = 1.0f / pdf; /* f = f * cosL */
+            T = V(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
+            alive = vmax3(T) > 0.0f;
+            if (alive && b >= 3) {
+                float q = fminf(vmax3(T), 1.0f);
+                if (rnd(key, dim0 + 6u) >= q) alive = 0;
+                else {
+                    float iq = 1.0f / q;
+                    T = V(T.x * iq, T.y * iq, T.z * iq);
                 }
             }
         }
@@ -1138,6 +1169,12 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     S->cam_all = ri[7] == 2;
     S->W = ri[0]; S->H = ri[1]; S->spp = ri[2]; S->max_bounces = ri[3]; S->seed = (uint32_t)ri[4]; S->view = ri[5];
     S->max_diffuse = ri[8]; S->max_glossy = ri[9];
+    {
+        int nm = 0; /* materials referenced by triangles (the product tables every scene material) */
+        for (int i = 0; i < n_tris; ++i) if (tri_mat[i] + 1 > nm) nm = tri_mat[i] + 1;
+        S->luts = (float*)calloc((size_t)(nm > 0 ? nm : 1) * ORC_LUT_STRIDE, sizeof(float));
+        for (int i = 0; i < nm; ++i) orc_material_lut(mats + 12 * (size_t)i, S->luts + ORC_LUT_STRIDE * (size_t)i);
+    }
     S->clamp = rf[0];
     S->inv_w2 = 2.0f / (float)S->W;
     S->inv_h2 = 2.0f / (float)S->H;
@@ -1197,6 +1234,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
             }
         }
     }
+    free(S->luts);
     free(S);
     lbvh_free(&B);
     return 0;
@@ -1215,16 +1253,24 @@ void orc_disk(int n, const float* u, float* xy) {
 /* BSDF sampling for the estimator tests (tests/test_oracle.py): n draws of
  * sample_bsdf at one shading point, u = n x (ul, u1, u2) -> wi (3), f (3),
  * pdf and ok per draw (ok = 0: the path ends, as in radiance()). */
+/* exports report the BSDF value f = (f * cosL) / cosL */
+static v3 f_of(v3 fcos, float cosL) { return cosL > 0.0f ? V(fcos.x / cosL, fcos.y / cosL, fcos.z / cosL) : fcos; }
+
 void orc_bsdf_sample(const float* mat12, const float* n3, const float* wo3, int n, const float* u, float* wi3,
                      float* f3, float* pdf, int32_t* ok) {
     mat_t m = load_mat(mat12, 0);
+    float lut[ORC_LUT_STRIDE];
+    orc_material_lut(mat12, lut);
     v3 N = V(n3[0], n3[1], n3[2]), wo = V(wo3[0], wo3[1], wo3[2]);
     for (int i = 0; i < n; ++i) {
         v3 wi = V(0.0f, 0.0f, 0.0f), f = wi;
         float p = 0.0f;
         int glossy = 0;
-        ok[i] = sample_bsdf(&m, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], &wi, &f, &p, &glossy);
-        if (ok[i]) ok[i] = 1 + glossy;  /* 1 diffuse lobe, 2 glossy lobe (rr_debug_bsdf_sample) */
+        ok[i] = sample_bsdf(&m, lut, N, wo, u[3 * i], u[3 * i + 1], u[3 * i + 2], &wi, &f, &p, &glossy);
+        if (ok[i]) {
+            ok[i] = 1 + glossy;  /* 1 diffuse lobe, 2 glossy lobe (rr_debug_bsdf_sample) */
+            f = f_of(f, vdot(N, wi));
+        }
         wi3[3 * i] = wi.x; wi3[3 * i + 1] = wi.y; wi3[3 * i + 2] = wi.z;
         f3[3 * i] = f.x; f3[3 * i + 1] = f.y; f3[3 * i + 2] = f.z;
         pdf[i] = p;
@@ -1235,10 +1281,13 @@ void orc_bsdf_sample(const float* mat12, const float* n3, const float* wo3, int 
 void orc_bsdf_eval_n(const float* mat12, const float* n3, const float* wo3, int n, const float* wi3, float* f3,
                      float* pdf) {
     mat_t m = load_mat(mat12, 0);
+    float lut[ORC_LUT_STRIDE];
+    orc_material_lut(mat12, lut);
     v3 N = V(n3[0], n3[1], n3[2]), wo = V(wo3[0], wo3[1], wo3[2]);
-    float ps = p_spec(&m, vdot(N, wo));
+    float ps = p_spec(lut, vdot(N, wo));
     for (int i = 0; i < n; ++i) {
-        v3 f = eval_bsdf(&m, N, wo, V(wi3[3 * i], wi3[3 * i + 1], wi3[3 * i + 2]), ps, &pdf[i]);
+        v3 wi = V(wi3[3 * i], wi3[3 * i + 1], wi3[3 * i + 2]);
+        v3 f = f_of(eval_bsdf(&m, lut, N, wo, wi, ps, &pdf[i]), vdot(N, wi));
         f3[3 * i] = f.x; f3[3 * i + 1] = f.y; f3[3 * i + 2] = f.z;
     }
 }
@@ -1246,8 +1295,10 @@ void orc_bsdf_eval_n(const float* mat12, const float* n3, const float* wo3, int 
 /* BSDF eval for known-answer tests: mat12, N, wo, wi -> f (3), pdf. */
 void orc_bsdf_eval(const float* mat12, const float* n3, const float* wo3, const float* wi3, float* f3, float* pdf) {
     mat_t m = load_mat(mat12, 0);
+    float lut[ORC_LUT_STRIDE];
+    orc_material_lut(mat12, lut);
     v3 N = V(n3[0], n3[1], n3[2]), wo = V(wo3[0], wo3[1], wo3[2]), wi = V(wi3[0], wi3[1], wi3[2]);
-    float ps = p_spec(&m, vdot(N, wo));
-    v3 f = eval_bsdf(&m, N, wo, wi, ps, pdf);
+    float ps = p_spec(lut, vdot(N, wo));
+    v3 f = f_of(eval_bsdf(&m, lut, N, wo, wi, ps, pdf), vdot(N, wi));
     f3[0] = f.x; f3[1] = f.y; f3[2] = f.z;
 }

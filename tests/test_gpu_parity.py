@@ -141,6 +141,8 @@ PATHS = {"tiles": 0, "wavefront": 4}
 @pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("frame,w,h,spp,chunk", [(1, 160, 90, 16, 0), (30, 96, 54, 8, 3), (60, 64, 36, 5, 1),
                                                  (600, 33, 17, 7, 2), (30, 1, 1, 9, 0), (45, 7, 130, 3, 0),
+                                                 # grids of 1..7 blocks (fewer than k_tiles' unit shards)
+                                                 (30, 8, 130, 3, 0), (45, 16, 24, 2, 0), (5, 40, 40, 33, 0),
                                                  # > kFilmGroup (32) samples: grouped film sum, k_tiles
                                                  # sample-group slices, groups straddling chunks
                                                  (5, 40, 24, 72, 20), (10, 48, 32, 128, 0), (20, 24, 16, 65, 7)])
