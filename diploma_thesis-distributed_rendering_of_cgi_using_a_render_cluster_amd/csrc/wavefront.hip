@@ -50,7 +50,10 @@ constexpr int kFilterN = 1024;
 // film (sum = 0; per group: sum += group). Frames of <= kFilmGroup samples
 // are the plain in-order sum. Groups let k_tiles split a tile's samples
 // across waves without changing a bit.
-constexpr int kFilmGroup = 32;
+#ifndef RR_FILM_GROUP
+#define RR_FILM_GROUP 32
+#endif
+constexpr int kFilmGroup = RR_FILM_GROUP;
 constexpr int kSrgbN = 4096;
 constexpr int kLightF = 12;
 constexpr int kMatF = 12;
@@ -212,10 +215,24 @@ RR_D void add_to(float3& L, float3 c) {
     L.z = L.z + c.z;
 }
 
+// Shadow rays of shade(): handed back in ShadeOut (queue kernels) ...
+struct EmitShadow {
+    static constexpr bool kInline = false;
+    RR_D bool operator()(float3, float3, float) const { return false; }
+};
+
 // K9: shade one path at `bounce` given its closest hit; L updated in place.
-template <typename View>
+// With an inline shadow tracer (Shadow::kInline: a functor returning whether
+// the ray (origin, direction, distance) is occluded) the NEE ray is traced as
+// soon as it exists and its contribution added, before the continuation is
+// sampled: the same radiance additions in the same order as emitting it
+// (emission, then NEE, then the next bounce), with the shadow-ray state dead
+// before the continuation's registers are needed. out.shadow still reports
+// that a shadow ray was traced.
+template <typename View, typename Shadow = EmitShadow>
 __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const View& v, float3 o, float3 d,
-                                      float3 T, uint32_t lob, const Hit& h, uint32_t key, float3& L, ShadeOut& out) {
+                                      float3 T, uint32_t lob, const Hit& h, uint32_t key, float3& L, ShadeOut& out,
+                                      const Shadow& trace_shadow = Shadow{}) {
     out.cont = false;
     out.shadow = false;
     if (h.idx < 0) {
@@ -295,10 +312,14 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
             if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
             if (max3f(c) > 0.0f) {
                 out.shadow = true;
-                out.so = Po;
-                out.sd = wi;
-                out.sdist = dist;
-                out.sc = c;
+                if constexpr (Shadow::kInline) {
+                    if (!trace_shadow(Po, wi, dist)) add_to(L, c);
+                } else {
+                    out.so = Po;
+                    out.sd = wi;
+                    out.sdist = dist;
+                    out.sc = c;
+                }
             }
         }
     }
@@ -1426,6 +1447,21 @@ RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint3
     }
 }
 
+// The tile kernel's shadow rays, traced inside shade() (any hit over the
+// LDS-resident LBVH).
+template <bool kCount>
+struct InlineShadow {
+    static constexpr bool kInline = true;
+    const LdsView& v;
+    int n_tris;
+    TravStack& st;
+    TravCount& cnt;
+    RR_D bool operator()(float3 so, float3 sd, float dist) const {
+        Hit hs;
+        return traverse<true, kCount>(v.nodes, v.tris, n_tris, so, sd, 0.0f, dist, st, hs, cnt);
+    }
+};
+
 // Active lanes of the wave whose predicate holds: the tile kernel's ray
 // counters are wave totals kept in scalar registers (no per-lane VGPRs live
 // across the unit loop).
@@ -1525,14 +1561,22 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         tile_mask(fc, v, fc.n_tris, (float)(tx * kTile), (float)(tx * kTile + kTile - 1), (float)(ty * kTile),
                   (float)(ty * kTile + kTile - 1), cm0, cm1);
         const uint32_t pk = pixel_key(fc.seed, (uint32_t)pix);
-        for (int s = s_lo; s < s_hi; ++s) {
+        // no triangle can be hit from this tile (wave-uniform): every sample is
+        // the world term, summed as the sample loop would (0 + world + ...)
+        const int s_run = (cm0 | cm1) != 0 ? s_hi : s_lo;
+        for (int s = s_run; s < s_hi; ++s) {
+            acc.x = acc.x + fc.world.x;
+            acc.y = acc.y + fc.world.y;
+            acc.z = acc.z + fc.world.z;
+        }
+        for (int s = s_lo; s < s_run; ++s) {
             const uint32_t key = sample_key(pk, (uint32_t)s);
             float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = mk3(1.0f, 1.0f, 1.0f), L = o;
             uint32_t lob = 0;
             float tmin = 0.0f, tmax = -1.0f;
             bool culled = true;
             if (valid) camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
-            n_t0 += wave_count(!culled && (cm0 | cm1) != 0);
+            n_t0 += wave_count(!culled);
             bool live = valid;
             for (int b = 0; b <= fc.max_bounces; ++b) {
                 if (!__any(live)) break;
@@ -1545,13 +1589,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     } else {
                         traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, ce);
                     }
-                    shade(fc, b, v, o, d, T, lob, h, key, L, so);
-                    if (so.shadow) {
-                        Hit hs;
-                        if (!traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs,
-                                                    cs))
-                            add_to(L, so.sc);
-                    }
+                    shade(fc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, fc.n_tris, st, cs});
                     if (b == 0) {
                         n_c0 += wave_count(so.cont);
                         n_s0 += wave_count(so.shadow);
