@@ -351,6 +351,20 @@ __global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restr
     }
 }
 
+// BVH4 collapse over a PLOC hierarchy: the child and parent links the
+// Karras build writes (children, node_parent = parent << 1 | side, root -1),
+// taken from the PLOC nodes.
+__global__ __launch_bounds__(kBlock) void k_ploc_links(int ni, const BvhNode* __restrict__ nodes,
+                                                       int2* __restrict__ children, int32_t* __restrict__ node_parent) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= ni) return;
+    const int4 d = nodes[i].d;
+    children[i] = make_int2(d.x, d.y);
+    if (d.x >= 0) node_parent[d.x] = 2 * i;
+    if (d.y >= 0) node_parent[d.y] = 2 * i + 1;
+    if (i == 0) node_parent[0] = -1;
+}
+
 // BVH4 collapse, step 1: depth parity of every internal node (walk to the
 // root through node_parent); flags[i] = 1 and rank[i] = 1 for even depth.
 __global__ __launch_bounds__(kBlock) void k_depth_parity(int ni, const int32_t* __restrict__ node_parent,
@@ -368,12 +382,15 @@ __global__ __launch_bounds__(kBlock) void k_depth_parity(int ni, const int32_t* 
 // BVH2 node i becomes BVH4 node rank[i]; its children, in slot order, are for
 // each side (left, right) either that leaf child, or both children of the
 // odd-depth internal child (leaf, or BVH4 node rank[grandchild]). Boxes come
-// from the parents' child boxes, so they are the BVH2 boxes bit for bit.
+// from the parents' child boxes (the BVH2 boxes), quantised on the node's
+// grid (rr_device.h QNode4): origin = the lo corner of the children's union,
+// per axis the smallest exponent that spans the union in 255 steps, lo
+// rounded down and hi up.
 __global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNode* __restrict__ nodes,
                                                       const int2* __restrict__ children,
                                                       const uint32_t* __restrict__ flags,
                                                       const uint32_t* __restrict__ rank,
-                                                      Bvh4Node* __restrict__ out) {
+                                                      QNode4* __restrict__ out) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= ni || !flags[i]) return;
     float lo[3][4], hi[3][4];
@@ -402,22 +419,32 @@ __global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNo
             put(cn, cc, 1);
         }
     }
-    for (; m < 4; ++m) {
-        for (int a = 0; a < 3; ++a) {
-            lo[a][m] = 0.0f;
-            hi[a][m] = 0.0f;
+    const int used = m;
+    float org[3];
+    uint32_t ql[3] = {0u, 0u, 0u}, qh[3] = {0u, 0u, 0u}, eb = 0u;
+    for (int a = 0; a < 3; ++a) {
+        float l = lo[a][0], h = hi[a][0];
+        for (int c = 1; c < used; ++c) {
+            l = fminf(l, lo[a][c]);
+            h = fmaxf(h, hi[a][c]);
         }
-        ref[m] = kEmpty4;
+        const int e = q4_exponent((double)h - (double)l);
+        org[a] = l;
+        eb |= (uint32_t)(e + 128) << (8 * a);
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t ql_c = c < used ? q4_quant(lo[a][c], l, e, false) : 255u;
+            const uint32_t qh_c = c < used ? q4_quant(hi[a][c], l, e, true) : 0u;
+            ql[a] |= ql_c << (8 * c);
+            qh[a] |= qh_c << (8 * c);
+        }
     }
-    Bvh4Node o;
-    o.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
-    o.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
-    o.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
-    o.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
-    o.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
-    o.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+    for (; m < 4; ++m) ref[m] = kEmpty4;
+    QNode4 o;
+    o.org = make_float4(org[0], org[1], org[2], i2f((int)eb));
     o.child = make_int4(ref[0], ref[1], ref[2], ref[3]);
-    o.pad = make_int4(0, 0, 0, 0);
+    o.q0 = make_uint4(ql[0], ql[1], ql[2], qh[0]);
+    o.q1 = make_uint2(qh[1], qh[2]);
+    o.pad = make_uint2(0u, 0u);
     out[rank[i]] = o;
 }
 
@@ -878,23 +905,21 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, b
         std::swap(s.keys[0], s.keys[1]);
         std::swap(s.vals[0], s.vals[1]);
     }
-    s.ploc = want_ploc && n > 2 && !want4;
+    s.ploc = want_ploc && n > 2;
     if (s.ploc) {
         build_ploc(s, st);
-        if (prof) prof->end(st);
-        RR_HIP(hipGetLastError());
-        s.has4 = false;
-        s.built = true;
-        return;
-    }
-    if (n > 1) {
+        if (want4)
+            k_ploc_links<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n - 1, s.nodes.ptr, s.children.ptr,
+                                                                  s.node_parent.ptr);
+    } else if (n > 1) {
         k_karras<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n, s.keys[0].ptr, s.children.ptr,
                                                           s.node_parent.ptr, s.leaf_parent.ptr, s.range.ptr);
         RR_HIP(hipMemsetAsync(s.flags.ptr, 0, (size_t)(n - 1) * sizeof(uint32_t), st));
     }
-    k_refit<<<nb, kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr, s.leaf_parent.ptr,
-                                   s.node_parent.ptr, s.children.ptr, s.flags.ptr, s.nodes.ptr,
-                                   s.tris.ptr);
+    if (!s.ploc)
+        k_refit<<<nb, kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr, s.leaf_parent.ptr,
+                                       s.node_parent.ptr, s.children.ptr, s.flags.ptr, s.nodes.ptr,
+                                       s.tris.ptr);
     if (want4) {  // BVH4 collapse (flags are free again once refit is done)
         const int ni = n > 1 ? n - 1 : 1;
         s.rank4.ensure((size_t)ni + 1);

@@ -70,7 +70,7 @@ struct DevScene {
     // acceleration structure consumed by traversal
     DevBuf<BvhNode> nodes;  // max(n-1, 1)
     DevBuf<TriPack> tris;   // n, leaf order
-    DevBuf<Bvh4Node> nodes4;   // BVH4 collapse of `nodes` (split path), <= n-1
+    DevBuf<QNode4> nodes4;     // quantised BVH4 collapse of `nodes` (split path), <= n-1
     DevBuf<uint32_t> rank4;    // BVH2 node -> BVH4 index (exclusive scan); [n-1] = BVH4 count
     bool has4 = false;
     // PLOC build (large scenes): cluster ping-pong, neighbours, scan flags, counters

@@ -197,14 +197,19 @@ void bind_scene(rr_ctx* c, rr_scene* s) {
 // `staging` (pinned, per frame slot) keeps the host-to-device copies
 // asynchronous, so a frame can be enqueued while the previous one still runs.
 // Hierarchy ids (render_ints[7] of rr_debug_frame_state, rr_debug_trace):
-// 2 = Karras LBVH (BVH2), 3 = PLOC (BVH2), 4 = LBVH collapsed to the BVH4.
+// 2 = Karras LBVH (BVH2), 3 = PLOC (BVH2), 4 = PLOC (LBVH below 3 triangles)
+// collapsed to the quantised BVH4 (rr_device.h QNode4).
 constexpr int kHierLbvh = 2, kHierPloc = 3, kHierBvh4 = 4;
 
 // The hierarchy the frame kernels walk: LDS-resident scenes the LBVH (fused
-// path), larger scenes PLOC (split path; or the BVH4 when built for it).
+// path), larger scenes the quantised BVH4 (split path).
 int frame_hier(int n_tris, int n_mats, int n_lights) {
     if (scene_in_lds(n_tris, n_mats, n_lights)) return kHierLbvh;
+#ifdef RR_SPLIT_BVH2
     return kHierPloc;
+#else
+    return kHierBvh4;
+#endif
 }
 
 // The view transform a frame on ctx is rendered with: Filmic needs the
@@ -254,7 +259,7 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     DevScene& d = s->dev;
     if (hier == 0) hier = frame_hier(d.n_tris, (int)(nm / RR_MAT_FLOATS), (int)(nl / RR_LIGHT_FLOATS));
     const bool want4 = hier == kHierBvh4;
-    const bool want_ploc = hier == kHierPloc && d.n_tris > 2;
+    const bool want_ploc = (hier == kHierPloc || hier == kHierBvh4) && d.n_tris > 2;
     const bool rebuild =
         !d.built || d.cached_xform != fs.obj_xform || (want4 && !d.has4) || (want_ploc != d.ploc);
     const bool upload_x = rebuild && d.n_tris > 0;
@@ -1002,7 +1007,7 @@ int rr_debug_bvh_hier(rr_ctx* c, rr_scene* s, int32_t frame, int32_t hier, uint3
     });
 }
 
-int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* children4, float* boxes4) {
+int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* children4, uint32_t* nodes16) {
     if (!c || !s || !n4) return fail(RR_EINVAL, "NULL ctx, scene or n4");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
@@ -1020,19 +1025,19 @@ int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* c
             RR_HIP(hipMemcpyAsync(&cnt, d.rank4.ptr + ni, sizeof cnt, hipMemcpyDeviceToHost, st));
             RR_HIP(hipStreamSynchronize(st));
             *n4 = (int32_t)cnt;
-            if (children4 || boxes4) {
-                std::vector<Bvh4Node> nodes(cnt);
-                RR_HIP(hipMemcpyAsync(nodes.data(), d.nodes4.ptr, cnt * sizeof(Bvh4Node), hipMemcpyDeviceToHost, st));
+            if (children4 || nodes16) {
+                std::vector<QNode4> nodes(cnt);
+                RR_HIP(hipMemcpyAsync(nodes.data(), d.nodes4.ptr, cnt * sizeof(QNode4), hipMemcpyDeviceToHost, st));
                 RR_HIP(hipStreamSynchronize(st));
                 for (uint32_t i = 0; i < cnt; ++i) {
-                    const Bvh4Node& q = nodes[i];
+                    const QNode4& q = nodes[i];
                     if (children4) {
                         children4[4 * i] = q.child.x;
                         children4[4 * i + 1] = q.child.y;
                         children4[4 * i + 2] = q.child.z;
                         children4[4 * i + 3] = q.child.w;
                     }
-                    if (boxes4) std::memcpy(boxes4 + 24 * (size_t)i, &q, 24 * sizeof(float));
+                    if (nodes16) std::memcpy(nodes16 + 16 * (size_t)i, &q, sizeof(QNode4));
                 }
             }
         }

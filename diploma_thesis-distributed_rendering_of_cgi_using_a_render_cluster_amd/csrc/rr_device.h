@@ -33,20 +33,46 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "node must be one 64-byte line");
 
-// 4-wide node for scenes traversed from HBM (split path): the
-// LBVH collapsed two levels at a time (every even-depth BVH2 node becomes one
-// node whose children are its grandchildren, or its leaf children). 128 B =
-// one L2/HBM line carries four child boxes (SoA, so the four slab tests
-// vectorise) and four child refs: >= 0 BVH4 node, < 0 ~leaf, kEmpty4 unused.
-// Per ray this halves the node fetches of the BVH2 walk, and each fetched
-// line is fully used (a BVH2 node used 64 B of its 128 B line).
-struct alignas(16) Bvh4Node {
-    float4 lox, loy, loz, hix, hiy, hiz;
+// Quantised 4-wide node, the hierarchy of scenes traversed from HBM (split
+// path): the PLOC BVH2 collapsed two levels at a time (every
+// even-depth BVH2 node becomes one node whose children are its grandchildren,
+// or its leaf children), with the four child boxes stored as 8-bit offsets on
+// a per-node grid: child lo/hi = org + q * 2^e per axis, q rounded outwards
+// (exactly, in double, at build time), so each quantised box contains the
+// child's box. 64 B per node: one BVH4 visit costs the bytes of one BVH2
+// visit and replaces up to three of them.
+//   org.xyz  grid origin = the node box's lo corner
+//   org.w    exponent bytes (ex + 128) | (ey + 128) << 8 | (ez + 128) << 16
+//   child    >= 0 node, < 0 ~leaf, kEmpty4 unused slot (q lo 255, hi 0)
+//   q0       lo x | lo y | lo z | hi x, q1: hi y | hi z (child c in byte c)
+struct alignas(16) QNode4 {
+    float4 org;
     int4 child;
-    int4 pad;
+    uint4 q0;
+    uint2 q1;
+    uint2 pad;
 };
-static_assert(sizeof(Bvh4Node) == 128, "BVH4 node must be one 128-byte line");
+static_assert(sizeof(QNode4) == 64, "quantised BVH4 node is 64 bytes");
 constexpr int kEmpty4 = 0x7fffffff;
+constexpr int kQExpMin = -64, kQExpMax = 100;
+
+// Smallest e in [kQExpMin, kQExpMax] with 255 * 2^e >= ext (ext >= 0).
+RR_HD int q4_exponent(double ext) {
+    if (!(ext > 0.0)) return kQExpMin;
+    int k;
+    (void)frexp(ext, &k);  // ext = m 2^k, 0.5 <= m < 1: 255 * 2^(k-8) < 2^k, 255 * 2^(k-7) >= 2^k
+    const int e = ldexp(255.0, k - 8) >= ext ? k - 8 : k - 7;
+    return e < kQExpMin ? kQExpMin : (e > kQExpMax ? kQExpMax : e);
+}
+// Grid coordinate of a box bound, rounded down (lo) or up (hi), in [0, 255].
+RR_HD uint32_t q4_quant(float v, float org, int e, bool up) {
+    const double x = ((double)v - (double)org) * ldexp(1.0, -e);
+    const double q = up ? ceil(x) : floor(x);
+    return q <= 0.0 ? 0u : (q >= 255.0 ? 255u : (uint32_t)q);
+}
+// Reciprocal for the quantised slab test: finite for zero components (a ray
+// parallel to an axis gets +-2^64, which keeps every plane distance finite).
+RR_HD float q4_rcp(float x) { return fabsf(x) < 0x1p-64f ? (x < 0.0f ? -0x1p64f : 0x1p64f) : 1.0f / x; }
 
 // Triangle in leaf order, 48 B: v0 | e1 = v1-v0 | e2 = v2-v0, with the original
 // triangle id and material id in the .w lanes.
@@ -433,18 +459,18 @@ struct TravState {
     }
 };
 
-RR_D Bvh4Node load_node4(const Bvh4Node* __restrict__ p, int i) { return p[i]; }
-
-RR_D float f4get(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 RR_D int i4get(const int4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
-// Resumable traversal of the BVH4 (same contract as TravState): leaf children
-// whose boxes pass are intersected at once in slot order; the nearest hit
-// internal child is visited next and the others are pushed in descending slot
-// order. oracle/rr_oracle.c trace4() is the same walk.
+// Resumable traversal of the quantised BVH4 (same contract as TravState).
+// Per node and axis: s = iq * 2^e (exact), o' = (org - o) * iq; a plane at grid
+// coordinate q lies at t = fma(q, s, o'). The near plane is lo for iq >= 0,
+// else hi (iq is never 0 or inf, so no NaN and no min/max per axis).
+// Leaf children whose boxes pass are intersected at once in slot order; the
+// nearest hit internal child is visited next and the others are pushed in
+// descending slot order. oracle/rr_oracle.c trace4() is the same walk.
 template <bool kAnyHit, bool kCount = false>
-struct TravState4 {
-    float3 o, d, invd;
+struct TravStateQ4 {
+    float3 o, d, iq;
     float tmin;
     Hit h;
     int node;
@@ -456,25 +482,43 @@ struct TravState4 {
         h.u = h.v = 0.0f;
         h.idx = -1;
         h.orig = -1;
-        invd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
         node = 0;
     }
     template <typename TriP, typename Stack>
-    RR_D bool step(const Bvh4Node* __restrict__ nodes, TriP tris, Stack& st, TravCount& cnt) {
+    RR_D bool step(const QNode4* __restrict__ nodes, TriP tris, Stack& st, TravCount& cnt) {
         if (kCount) ++cnt.nodes;
         const float tcur = h.t;
         float tn[4];
         int ref[4];
         uint32_t leaves = 0, inner = 0;
         {
-            const Bvh4Node nd = load_node4(nodes, node);
+            const QNode4* p = nodes + node;
+            const float4 org = p->org;
+            const int4 ch = p->child;
+            const uint4 q0 = p->q0;
+            const uint2 q1 = p->q1;
+            const uint32_t eb = (uint32_t)f2i(org.w);
+            const float sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
+            const float sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
+            const float sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
+            const float ox = (org.x - o.x) * iq.x, oy = (org.y - o.y) * iq.y, oz = (org.z - o.z) * iq.z;
+            const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
+            const uint32_t nx = px ? q0.x : q0.w, fx = px ? q0.w : q0.x;
+            const uint32_t ny = py ? q0.y : q1.x, fy = py ? q1.x : q0.y;
+            const uint32_t nz = pz ? q0.z : q1.y, fz = pz ? q1.y : q0.z;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                ref[c] = i4get(nd.child, c);
-                const bool hit = ref[c] != kEmpty4 &&
-                                 slab(o, invd, f4get(nd.lox, c), f4get(nd.loy, c), f4get(nd.loz, c),
-                                      f4get(nd.hix, c), f4get(nd.hiy, c), f4get(nd.hiz, c), tmin, tcur, tn[c]);
-                if (hit) {
+                ref[c] = i4get(ch, c);
+                const int sh = 8 * c;
+                const float t0 = fmaxf(fmaxf(fmaf((float)((nx >> sh) & 255u), sx, ox),
+                                             fmaf((float)((ny >> sh) & 255u), sy, oy)),
+                                       fmaxf(fmaf((float)((nz >> sh) & 255u), sz, oz), tmin));
+                const float t1 = fminf(fminf(fmaf((float)((fx >> sh) & 255u), sx, ox),
+                                             fmaf((float)((fy >> sh) & 255u), sy, oy)),
+                                       fminf(fmaf((float)((fz >> sh) & 255u), sz, oz), tcur));
+                tn[c] = t0;
+                if (ref[c] != kEmpty4 && t0 <= t1) {
                     if (ref[c] < 0) leaves |= 1u << c;
                     else inner |= 1u << c;
                 }

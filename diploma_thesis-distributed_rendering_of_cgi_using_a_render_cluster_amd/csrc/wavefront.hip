@@ -472,7 +472,7 @@ RR_D void count_wave(uint32_t* __restrict__ ctr, bool pred) {
 }  // namespace
 struct SceneArgs {
     const BvhNode* nodes;
-    const Bvh4Node* nodes4;  // BVH4 collapse (rr_debug_trace only)
+    const QNode4* nodes4;    // quantised BVH4 (split path)
     const TriPack* tris;
     const float* mats;
     const float* lights;
@@ -991,17 +991,22 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
 #define RR_TRACE_WAVES 7
 #endif
 constexpr int kRefillBelow = RR_REFILL_BELOW;
-// Hierarchy of the split path: the PLOC BVH2 (a BVH4 collapse measured
-// slower: VGPR spills in the trace kernels).
+// Hierarchy of the split path: the PLOC BVH2 collapsed to the quantised BVH4.
+#ifdef RR_SPLIT_BVH2
 template <bool kAnyHit, bool kCount>
 using SplitTrav = TravState<kAnyHit, kCount>;
 RR_D const BvhNode* split_nodes(const SceneArgs& sa) { return sa.nodes; }
+#else
+template <bool kAnyHit, bool kCount>
+using SplitTrav = TravStateQ4<kAnyHit, kCount>;
+RR_D const QNode4* split_nodes(const SceneArgs& sa) { return sa.nodes4; }
+#endif
 constexpr int kQGroups = 64;   // append groups per queue (one lane each in QueueMap)
 constexpr int kQStride = 32;   // words between group counters (128 B)
 
 // map(k) -> slot is called by every lane of the wave (converged: QueueMap
 // shuffles); ray_of(slot, ...) and done(k, slot, hit) per lane.
-// TS: TravState4<kAnyHit, kCount> (BVH4 nodes) or TravState (BVH2).
+// TS: TravStateQ4<kAnyHit, kCount> (quantised BVH4) or TravState (BVH2).
 template <typename TS, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack& st, TravCount& cnt, MapFn&& map,
                        RayFn&& ray_of, DoneFn&& done) {
@@ -1731,7 +1736,7 @@ __global__ void k_debug_bsdf(const float* __restrict__ mat12, const float* __res
     ok[i] = good ? (glossy ? 2 : 1) : 0;
 }
 
-__global__ void k_debug_trace4(const Bvh4Node* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
+__global__ void k_debug_trace4(const QNode4* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
                                int n, const float4* __restrict__ rays, float4* __restrict__ hits,
                                int32_t* __restrict__ prims, uint8_t* __restrict__ occ,
                                int32_t* __restrict__ spill) {
@@ -1742,7 +1747,7 @@ __global__ void k_debug_trace4(const Bvh4Node* __restrict__ nodes, const TriPack
     TravCount cnt;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
-        TravState4<false> ts;
+        TravStateQ4<false> ts;
         ts.start(xyz(o), xyz(d), o.w, d.w);
         st.sp = 0;
         if (n_tris > 0)
@@ -1750,7 +1755,7 @@ __global__ void k_debug_trace4(const Bvh4Node* __restrict__ nodes, const TriPack
             }
         hits[i] = make_float4(ts.h.t, ts.h.u, ts.h.v, 0.0f);
         prims[i] = ts.h.orig;
-        TravState4<true> ta;
+        TravStateQ4<true> ta;
         ta.start(xyz(o), xyz(d), o.w, d.w);
         st.sp = 0;
         if (n_tris > 0)

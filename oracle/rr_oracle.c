@@ -157,10 +157,10 @@ typedef struct {
     float* tri;       /* leaf order: v0 e1 e2 (9) */
     int* tri_orig;
     int* tri_mat;
-    int width;        /* hierarchy trace() walks: 2 (LBVH) or 4 (BVH4 collapse) */
+    int width;        /* hierarchy trace() walks: 2 (BVH2) or 4 (quantised BVH4 collapse) */
     int n4;           /* BVH4 nodes */
     int* child4;      /* 4 per node: >= 0 node, < 0 ~leaf, ORC_EMPTY4 unused */
-    float* box4;      /* 24 per node: lox[4] loy[4] loz[4] hix[4] hiy[4] hiz[4] */
+    uint32_t* q4;     /* 16 words per node, csrc/rr_device.h QNode4 */
 } lbvh;
 
 #define ORC_EMPTY4 0x7fffffff
@@ -209,7 +209,7 @@ static void subtree_box(const lbvh* B, const float* tris9, int c, float out[6]) 
 }
 
 static void lbvh_free(lbvh* B) {
-    free(B->child4); free(B->box4); free(B->child_lf); free(B->range);
+    free(B->child4); free(B->q4); free(B->child_lf); free(B->range);
     free(B->keys); free(B->order); free(B->child); free(B->box);
     free(B->tri); free(B->tri_orig); free(B->tri_mat);
     memset(B, 0, sizeof *B);
@@ -421,7 +421,50 @@ static void ploc_build(lbvh* B, const float* tris9) {
     free(ref); free(ref2); free(box); free(box2); free(nn);
 }
 
-/* BVH4 collapse of the LBVH, as csrc/bvh.hip k_depth_parity + k_collapse4:
+/* Quantisation of the BVH4 child boxes (csrc/rr_device.h q4_exponent /
+ * q4_quant, bvh.hip k_collapse4): per axis the smallest e in [-64, 100] with
+ * 255 * 2^e >= the extent of the children's union (in double, exact), grid
+ * origin = the union's lo corner, lo rounded down and hi up to [0, 255]. */
+#define ORC_QEXP_MIN (-64)
+#define ORC_QEXP_MAX 100
+static int q4_exponent(double ext) {
+    if (!(ext > 0.0)) return ORC_QEXP_MIN;
+    int k;
+    (void)frexp(ext, &k);
+    int e = ldexp(255.0, k - 8) >= ext ? k - 8 : k - 7;
+    return e < ORC_QEXP_MIN ? ORC_QEXP_MIN : (e > ORC_QEXP_MAX ? ORC_QEXP_MAX : e);
+}
+static uint32_t q4_quant(float v, float org, int e, int up) {
+    double x = ((double)v - (double)org) * ldexp(1.0, -e);
+    double q = up ? ceil(x) : floor(x);
+    return q <= 0.0 ? 0u : (q >= 255.0 ? 255u : (uint32_t)q);
+}
+/* finite reciprocal for the quantised slab test (rr_device.h q4_rcp) */
+static float q4_rcp(float x) { return fabsf(x) < 0x1p-64f ? (x < 0.0f ? -0x1p64f : 0x1p64f) : 1.0f / x; }
+
+static void q4_pack(const float lo[3][4], const float hi[3][4], const int ref[4], int used, uint32_t* o) {
+    uint32_t ql[3] = {0, 0, 0}, qh[3] = {0, 0, 0}, eb = 0;
+    float org[3];
+    for (int a = 0; a < 3; ++a) {
+        float l = lo[a][0], h = hi[a][0];
+        for (int c = 1; c < used; ++c) { l = fminf(l, lo[a][c]); h = fmaxf(h, hi[a][c]); }
+        int e = q4_exponent((double)h - (double)l);
+        org[a] = l;
+        eb |= (uint32_t)(e + 128) << (8 * a);
+        for (int c = 0; c < 4; ++c) {
+            ql[a] |= (c < used ? q4_quant(lo[a][c], l, e, 0) : 255u) << (8 * c);
+            qh[a] |= (c < used ? q4_quant(hi[a][c], l, e, 1) : 0u) << (8 * c);
+        }
+    }
+    memcpy(o, org, 3 * sizeof(float));
+    o[3] = eb;
+    for (int c = 0; c < 4; ++c) o[4 + c] = (uint32_t)ref[c];
+    o[8] = ql[0]; o[9] = ql[1]; o[10] = ql[2]; o[11] = qh[0]; o[12] = qh[1]; o[13] = qh[2];
+    o[14] = 0; o[15] = 0;
+}
+
+/* BVH4 collapse of the BVH2 (PLOC, or Karras below 3 triangles), as
+ * csrc/bvh.hip k_ploc_links + k_depth_parity + k_collapse4:
  * every even-depth internal node (root depth 0) becomes BVH4 node rank(i) =
  * number of even-depth nodes with a smaller index; its children in slot order
  * are, per side (left, right), the leaf child itself or both children of the
@@ -451,7 +494,7 @@ static void lbvh_collapse4(lbvh* B) {
     }
     B->n4 = n4;
     B->child4 = (int*)malloc(sizeof(int) * 4 * (size_t)n4);
-    B->box4 = (float*)malloc(sizeof(float) * 24 * (size_t)n4);
+    B->q4 = (uint32_t*)malloc(sizeof(uint32_t) * 16 * (size_t)n4);
     for (int i = 0; i < ni; ++i) {
         if (depth[i] & 1) continue;
         float lo[3][4], hi[3][4];
@@ -469,16 +512,13 @@ static void lbvh_collapse4(lbvh* B) {
                 ++m;
             }
         }
+        const int used = m;
         for (; m < 4; ++m) {
             for (int a = 0; a < 3; ++a) { lo[a][m] = 0.0f; hi[a][m] = 0.0f; }
             ref[m] = ORC_EMPTY4;
         }
-        float* o = B->box4 + 24 * (size_t)rank[i];
-        for (int c = 0; c < 4; ++c) {
-            o[c] = lo[0][c]; o[4 + c] = lo[1][c]; o[8 + c] = lo[2][c];
-            o[12 + c] = hi[0][c]; o[16 + c] = hi[1][c]; o[20 + c] = hi[2][c];
-            B->child4[4 * (size_t)rank[i] + c] = ref[c];
-        }
+        q4_pack((const float(*)[4])lo, (const float(*)[4])hi, ref, used, B->q4 + 16 * (size_t)rank[i]);
+        for (int c = 0; c < 4; ++c) B->child4[4 * (size_t)rank[i] + c] = ref[c];
     }
     free(depth); free(rank); free(stack);
 }
@@ -532,26 +572,45 @@ static void try_leaf(const lbvh* B, int leaf, v3 o, v3 d, float tmin, hitrec* h)
 
 typedef struct { float t; int slot, ref; } ckey;
 
-/* BVH4 walk of rr_device.h TravState4: the four slab tests against the box
- * test bound at node entry, passing leaf children intersected in slot order,
- * the nearest hit internal child (ties: lower slot) visited next, the other
- * hit internal children pushed in descending slot order. */
+/* Quantised BVH4 walk of rr_device.h TravStateQ4: per axis s = iq * 2^e,
+ * o' = (org - o) * iq, plane t = fma(q, s, o'), near plane lo for iq >= 0 else
+ * hi; the four box tests against the bound at node entry, passing leaf
+ * children intersected in slot order, the nearest hit internal child (ties:
+ * lower slot) visited next, the other hit internal children pushed in
+ * descending slot order. */
 static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hitrec* h) {
     h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
     if (B->n <= 0) return 0;
-    v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float iq[3] = {q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z)};
+    const float oo[3] = {o.x, o.y, o.z};
     int stack[ORC_MAXDEPTH];
     int sp = 0, node = 0;
     for (;;) {
-        const float* bx = B->box4 + 24 * (size_t)node;
+        const uint32_t* nd = B->q4 + 16 * (size_t)node;
         const int* ch = B->child4 + 4 * (size_t)node;
         const float tcur = h->t;
+        float sc[3], of[3];
+        uint32_t nq[3], fq[3];
+        for (int a = 0; a < 3; ++a) {
+            float org;
+            memcpy(&org, nd + a, sizeof org);
+            sc[a] = ldexpf(iq[a], (int)((nd[3] >> (8 * a)) & 255u) - 128);
+            of[a] = (org - oo[a]) * iq[a];
+            int pos = iq[a] >= 0.0f;
+            nq[a] = pos ? nd[8 + a] : nd[11 + a];
+            fq[a] = pos ? nd[11 + a] : nd[8 + a];
+        }
         ckey k[4];
         for (int c = 0; c < 4; ++c) {
             int ref = ch[c];
-            float b6[6] = {bx[c], bx[4 + c], bx[8 + c], bx[12 + c], bx[16 + c], bx[20 + c]};
-            float tn = 0.0f;
-            int hit = ref != ORC_EMPTY4 && slab_test(o, inv, b6, tmin, tcur, &tn);
+            int sh = 8 * c;
+            float tn = fmaxf(fmaxf(fmaf((float)((nq[0] >> sh) & 255u), sc[0], of[0]),
+                                   fmaf((float)((nq[1] >> sh) & 255u), sc[1], of[1])),
+                             fmaxf(fmaf((float)((nq[2] >> sh) & 255u), sc[2], of[2]), tmin));
+            float tf = fminf(fminf(fmaf((float)((fq[0] >> sh) & 255u), sc[0], of[0]),
+                                   fmaf((float)((fq[1] >> sh) & 255u), sc[1], of[1])),
+                             fminf(fmaf((float)((fq[2] >> sh) & 255u), sc[2], of[2]), tcur));
+            int hit = ref != ORC_EMPTY4 && tn <= tf;
             k[c].slot = c;
             k[c].ref = ref;
             k[c].t = (hit && ref >= 0) ? tn : INFINITY;
@@ -1111,14 +1170,15 @@ int orc_trace_brute(int n, const float* tris9, int n_rays, const float* rays, fl
     return 0;
 }
 
-/* BVH4 collapse (rr_debug_bvh4 layout): n4 nodes, 4 child refs, 24 floats each. */
-int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, float* boxes4) {
+/* Quantised BVH4 (rr_debug_bvh4 layout): n4 nodes, 4 child refs and the 16
+ * words of each node. */
+int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, uint32_t* nodes16) {
     lbvh B;
-    lbvh_build(&B, n, tris9, NULL, 4);
+    lbvh_build(&B, n, tris9, NULL, 3);
     lbvh_collapse4(&B);
     *n4 = B.n4;
     if (children4 && B.n4) memcpy(children4, B.child4, sizeof(int32_t) * 4 * (size_t)B.n4);
-    if (boxes4 && B.n4) memcpy(boxes4, B.box4, sizeof(float) * 24 * (size_t)B.n4);
+    if (nodes16 && B.n4) memcpy(nodes16, B.q4, sizeof(uint32_t) * 16 * (size_t)B.n4);
     lbvh_free(&B);
     return 0;
 }
@@ -1126,7 +1186,7 @@ int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, f
 int orc_trace_w(int n, const float* tris9, int width, int n_rays, const float* rays, float* hits, int32_t* prims,
                 uint8_t* occluded) {
     lbvh B;
-    lbvh_build(&B, n, tris9, NULL, width);
+    lbvh_build(&B, n, tris9, NULL, width == 4 ? 3 : width);
     if (width == 4) { lbvh_collapse4(&B); B.width = 4; }
     for (int r = 0; r < n_rays; ++r) {
         const float* R = rays + 8 * (size_t)r;
@@ -1157,7 +1217,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
                const float* lights, const float* mats, const float* world, const int32_t* ri, const float* rf,
                float* film, uint8_t* rgba8, int row_begin, int row_end, int threads) {
     lbvh B;
-    lbvh_build(&B, n_tris, tris9, tri_mat, ri[7] == 3 ? 3 : 2);  /* the hierarchy the product walks */
+    lbvh_build(&B, n_tris, tris9, tri_mat, (ri[7] == 3 || ri[7] == 4) ? 3 : 2);  /* the hierarchy the product walks */
     if (ri[7] == 4) { lbvh_collapse4(&B); B.width = 4; }
     scene_t* S = (scene_t*)calloc(1, sizeof(scene_t));
     S->bvh = &B;

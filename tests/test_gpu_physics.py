@@ -1,7 +1,8 @@
 """Parity of the HIP path with the CPU oracle on the large-scene configs:
 the C4 physics stand-ins (02/03: thousands of rigid bodies, hierarchy rebuilt
 every frame) and the C5 synthetic 10M-triangle scene. These
-scenes take the HBM (non-LDS) traversal path over a PLOC hierarchy. Integer work (Morton keys, radix order,
+scenes take the HBM (non-LDS) traversal path over a PLOC hierarchy collapsed
+to the quantised BVH4. Integer work (Morton keys, radix order,
 BVH topology, hit ids) and the float work are bit-exact (tolerance 0), as in
 test_gpu_parity.py. Full-size C5 is checked through size-independent
 properties: the whole 10M-triangle LBVH equals the oracle's, and a ray batch
@@ -54,14 +55,14 @@ def _camera_rays(st, n, rng):
 
 @pytest.mark.parametrize("frame", [1, 45, 170])
 def test_physics_bvh_bit_exact(ctx, s02, frame):
-    """The frame's hierarchy (PLOC over the Morton-sorted leaves for scenes
-    traversed from HBM) equals the oracle's build, node for node."""
+    """The frame's BVH2 (PLOC over the Morton-sorted leaves for scenes traversed
+    from HBM, before its collapse to the quantised BVH4) equals the oracle's
+    build, node for node."""
     st = ctx.frame_state(s02, frame)
     assert st.tris.shape[0] == 92002
-    hier = int(st.render_ints[7])
-    assert hier == 3
+    assert int(st.render_ints[7]) == 4
     keys, order, children, boxes = ctx.bvh(s02, frame)
-    ok, oo, oc, ob = O.build_lbvh(st.tris, hier=hier)
+    ok, oo, oc, ob = O.build_lbvh(st.tris, hier=3)
     assert np.array_equal(keys, ok)
     assert np.array_equal(order, oo)
     assert np.array_equal(children, oc)
@@ -82,8 +83,9 @@ def test_physics_rebuilds_every_frame(ctx, rr, s02):
 
 @pytest.mark.parametrize("hier", [3, 2, 4])
 def test_physics_trace_bit_exact(ctx, s02, hier):
-    """Ray batches through PLOC (the frame's hierarchy), the LBVH and its BVH4
-    collapse, each against the oracle's walk of the same hierarchy."""
+    """Ray batches through PLOC, the LBVH and the quantised BVH4 collapse of
+    PLOC (the frame's hierarchy), each against the oracle's walk of the same
+    hierarchy."""
     st = ctx.frame_state(s02, 90)
     rays = _camera_rays(st, 40000, np.random.default_rng(7))
     hits, prims, occ = ctx.trace(s02, 90, rays, width=hier)
@@ -141,7 +143,8 @@ def test_c5_full_size_bvh_bit_exact(ctx, sc5):
     n = st.tris.shape[0]
     assert n == 512 * 20480 + 2
     keys, order, children, boxes = ctx.bvh(sc5, 120)
-    ok, oo, oc, ob = O.build_lbvh(st.tris, hier=int(st.render_ints[7]))
+    assert int(st.render_ints[7]) == 4
+    ok, oo, oc, ob = O.build_lbvh(st.tris, hier=3)
     assert np.array_equal(keys, ok)
     assert np.array_equal(order, oo)
     assert np.array_equal(children, oc)

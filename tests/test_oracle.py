@@ -242,18 +242,54 @@ def test_04_frame_is_plausible():
     assert np.array_equal(f2[10:20], film[10:20]) and np.array_equal(r2[10:20], rgba[10:20])
 
 
+def _q4_child_boxes(node):
+    """Decoded child boxes of one quantised BVH4 node (rr_device.h QNode4), in
+    double: lo/hi = org + q * 2^e per axis, (4, 3) each."""
+    org = node[0:3].view(np.float32).astype(np.float64)
+    e = np.array([((int(node[3]) >> (8 * a)) & 255) - 128 for a in range(3)])
+    q = np.array([[(int(node[8 + k]) >> (8 * c)) & 255 for k in range(6)] for c in range(4)], np.float64)
+    return org + q[:, 0:3] * np.exp2(e), org + q[:, 3:6] * np.exp2(e)
+
+
+def _check_q4_contains(tris, ch, nodes):
+    """Every quantised child box contains the boxes of all triangles below it."""
+    sorted_tris = None
+
+    def walk(i):
+        lo4, hi4 = _q4_child_boxes(nodes[i])
+        under = []
+        for c in range(4):
+            r = int(ch[i, c])
+            if r == 0x7FFFFFFF:
+                continue
+            ids = [~r] if r < 0 else walk(r)
+            under += ids
+            t = sorted_tris[ids].reshape(-1, 3).astype(np.float64)
+            assert np.all(lo4[c] <= t.min(0)) and np.all(t.max(0) <= hi4[c]), (i, c)
+        return under
+
+    # leaf refs name sorted leaves: recover the Morton order from the LBVH build
+    _, order, _, _ = O.build_lbvh(tris, hier=3 if tris.shape[0] > 2 else 2)
+    sorted_tris = tris.reshape(-1, 9)[order].reshape(-1, 3, 3)
+    assert sorted(walk(0)) == list(range(tris.shape[0]))
+
+
 @pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (7, 2), (300, 3), (5000, 4)])
 def test_bvh4_collapse_and_walk_equal_brute_force(n, seed):
-    """BVH4 collapse: every leaf once, every node but the root once, boxes taken
-    from the LBVH; the BVH4 walk finds the brute-force closest hits."""
+    """Quantised BVH4 collapse of the PLOC hierarchy: every leaf once, every
+    node but the root once, quantised boxes containing their subtrees; the
+    BVH4 walk finds the brute-force closest hits."""
     rng = np.random.default_rng(seed)
     c = rng.uniform(-5, 5, (n, 1, 3))
     tris = (c + rng.normal(0, 0.6, (n, 3, 3))).astype(np.float32)
-    ch, bx = O.build_bvh4(tris)
+    ch, nodes = O.build_bvh4(tris)
+    assert np.array_equal(nodes[:, 4:8].view(np.int32), ch)
     leaves = -ch[ch < 0] - 1
     assert np.array_equal(np.sort(leaves), np.arange(n)) or (n == 1 and set(leaves) == {0})
     inner = ch[(ch >= 0) & (ch != 0x7FFFFFFF)]
     assert np.array_equal(np.sort(inner), np.arange(1, ch.shape[0]))
+    if n > 1:
+        _check_q4_contains(tris, ch, nodes)
     m = 4000
     rays = np.zeros((m, 8), np.float32)
     rays[:, 0:3] = rng.uniform(-8, 8, (m, 3))
@@ -266,6 +302,53 @@ def test_bvh4_collapse_and_walk_equal_brute_force(n, seed):
     assert np.array_equal(p4, bp) and np.array_equal(p2, bp)
     assert np.array_equal(h4[:, 0], bh[:, 0])
     assert np.array_equal(o4, o2)
+
+
+def test_bvh4_axis_aligned_geometry_and_rays():
+    """Flat boxes (an axis-aligned grid of quads and a cube) and rays with
+    exactly zero direction components: the finite reciprocal of the quantised
+    walk (q4_rcp) keeps every plane distance finite, and the hits still equal
+    brute force. Ray origins stay off the box planes: a ray parallel to a box
+    face and exactly on it is a boundary case both the BVH2 slab test (0 * inf)
+    and this walk may reject."""
+    quads = []
+    for i in range(8):
+        for j in range(8):
+            x0, z0 = i - 4.0, j - 4.0
+            a, b, c, d = (x0, 0, z0), (x0 + 1, 0, z0), (x0 + 1, 0, z0 + 1), (x0, 0, z0 + 1)
+            quads += [(a, b, c), (a, c, d)]
+    for ax in range(3):  # a unit cube's faces at +-0.5 around (0, 1, 0)
+        for s in (-0.5, 0.5):
+            p = [[0.0, 1.0, 0.0] for _ in range(4)]
+            u, v = (ax + 1) % 3, (ax + 2) % 3
+            for k, (du, dv) in enumerate(((-.5, -.5), (.5, -.5), (.5, .5), (-.5, .5))):
+                p[k][ax] += s
+                p[k][u] += du
+                p[k][v] += dv
+            quads += [(p[0], p[1], p[2]), (p[0], p[2], p[3])]
+    tris = np.array(quads, np.float32)
+    ch, nodes = O.build_bvh4(tris)
+    _check_q4_contains(tris, ch, nodes)
+    rng = np.random.default_rng(7)
+    rays = []
+    for _ in range(3000):
+        o = rng.uniform(-5, 5, 3).round(1) + 0.0123
+        o[1] = abs(o[1]) + 0.25
+        d = np.zeros(3)
+        axes = rng.choice(3, rng.integers(1, 3), replace=False)
+        d[axes] = rng.choice([-1.0, 1.0], len(axes)) * rng.uniform(0.2, 1.0, len(axes))
+        d /= np.linalg.norm(d)
+        rays.append([*o, 0.0, *d, 1e30])
+    for _ in range(1000):  # straight down onto the grid, straight across through the cube
+        x, z = rng.uniform(-4, 4, 2).round(2) + 0.0031
+        rays.append([x, 3.0, z, 0.0, 0.0, -1.0, 0.0, 1e30])
+        y, w = rng.uniform(0.5, 1.5), rng.uniform(-0.5, 0.5)
+        rays.append([-6.0, y, w, 0.0, 1.0, 0.0, 0.0, 1e30])
+    rays = np.array(rays, np.float32)
+    h4, p4, o4 = O.trace(tris, rays, width=4)
+    bh, bp = O.trace_brute(tris, rays)
+    assert np.count_nonzero(bp >= 0) > 2000
+    assert np.array_equal(p4, bp) and np.array_equal(h4[:, 0], bh[:, 0])
 
 
 @pytest.mark.parametrize("n,seed", [(3, 0), (50, 1), (2000, 2)])
