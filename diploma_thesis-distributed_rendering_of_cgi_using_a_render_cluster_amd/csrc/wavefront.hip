@@ -968,20 +968,20 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
 // and shading run as separate kernels so that the traversal kernels carry only
 // the ray + traversal state (≤ 64 VGPRs, 8 waves per SIMD to hide the
 // L2/MALL/HBM latency of the node fetches) and keep their lanes busy with
-// lane refill: each wave owns a contiguous range of the ray queue and, when
-// fewer than kRefillBelow of its lanes are still traversing, hands the idle
-// lanes the next rays of its range (ballot prefix, no atomics). Finished rays
-// write a hit record (t, leaf index) that the shading kernel consumes in queue
-// order.
+// lane refill: each wave owns a sequence of 64-ray chunks of the ray queue
+// (trace_refill) and, when fewer than kRefillBelow of its lanes are still
+// traversing, hands the idle lanes the next rays of its sequence (ballot
+// prefix, no atomics). Finished rays write a hit record (t, leaf index) at
+// their queue slot, which the shading kernel consumes in the same order.
 //
 // Queues here are GROUPED: a shading wave appends its ballot-compacted rays
 // to group g = wave % kQGroups with one atomicAdd on that group's counter
 // (counters 128 B apart). One counter per queue serialised the appends
 // (device-scope atomics on one address: ~11 ns each, measured as >80 % of the
 // shading kernels' time); 64 groups spread them over 64 lines. A consumer wave
-// scans the 64 group counts in registers (one load per lane + a 6-step shuffle
-// scan, no LDS, no barrier) and maps a dense index j to (group, offset) with a
-// 6-step shuffle binary search. Queue order may vary between runs; what each
+// reads the 64 group counts into registers (one load per lane, no LDS, no
+// barrier) and walks the groups in time order (QueueMap::slot_t, one shuffle
+// per position). Queue order may vary between runs; what each
 // path computes (and the per-path order of radiance additions) does not, so
 // images stay bit-identical to the fused kernels' and the oracle's.
 #ifndef RR_REFILL_BELOW
@@ -1007,24 +1007,35 @@ constexpr int kQStride = 32;   // words between group counters (128 B)
 // map(k) -> slot is called by every lane of the wave (converged: QueueMap
 // shuffles); ray_of(slot, ...) and done(k, slot, hit) per lane.
 // TS: TravStateQ4<kAnyHit, kCount> (quantised BVH4) or TravState (BVH2).
+// Positions 0..count-1 are dealt to the waves in chunks of 64, round-robin
+// (wave w: chunks w, w + waves, ...), so at any time the rays in flight on the
+// whole chip come from one window of about 64 x waves positions: for camera
+// rays one band of the image, for queued rays the entries the producer
+// kernel appended at about the same time (QueueMap::slot_t). Rays of one
+// window share most of the nodes they visit, and the window's working set
+// stays in L2 (measured on C5: a contiguous range per wave spread the rays in
+// flight over the whole frame). map(k) may return kNoSlot (a gap): that
+// position holds no ray.
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 template <typename TS, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack& st, TravCount& cnt, MapFn&& map,
                        RayFn&& ray_of, DoneFn&& done) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int nw = gridDim.x * kWavesPerBlock;
-    const int per = (count + nw - 1) / nw;
-    int next = (int)wave_id() * per;  // wave-uniform cursor into this wave's range
-    const int end = min(count, next + per);
+    const int w = (int)wave_id();
+    // position of the q-th ray of this wave's sequence
+    auto gpos = [&](int q) { return ((q >> 6) * nw + w) * 64 + (q & 63); };
+    int next = 0;  // wave-uniform cursor into this wave's sequence
     TS ts;
     int j = -1;
     uint32_t js = 0;  // queue slot of ray j
     for (;;) {
         const uint64_t idle = __ballot(j < 0);
-        if (next < end && idle) {  // wave-uniform
-            const int k = next + (int)__popcll(idle & below);
-            const uint32_t ks = map(k < end ? k : end - 1);
-            if (j < 0 && k < end) {
+        if (gpos(next) < count && idle) {  // wave-uniform
+            const int k = gpos(next + (int)__popcll(idle & below));
+            const uint32_t ks = map(k < count ? k : count - 1);
+            if (j < 0 && k < count && ks != kNoSlot) {
                 float3 o, d;
                 float tmin, tmax;
                 ray_of(ks, o, d, tmin, tmax);
@@ -1040,7 +1051,7 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack&
             next += (int)__popcll(idle);
         }
         if (!__ballot(j >= 0)) {
-            if (next >= end) break;
+            if (gpos(next) >= count) break;
             continue;
         }
         for (;;) {
@@ -1049,7 +1060,7 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack&
                 j = -1;
             }
             const int na = (int)__popcll(__ballot(j >= 0));
-            if (na == 0 || (next < end && na < kRefillBelow)) break;
+            if (na == 0 || (gpos(next) < count && na < kRefillBelow)) break;
         }
     }
 }
@@ -1071,33 +1082,41 @@ struct QueueIn {
     uint32_t* total;    // block 0 records the queue length (ray statistics), may be null
 };
 
-// Per-wave view of a grouped queue: lane g holds the exclusive prefix of the
-// group counts; slot(j) is a shuffle binary search (every lane of the wave
-// must call it, each with its own j).
+// Per-wave view of a grouped queue: lane g holds group g's count; slot_t(m)
+// maps a position to a queue slot with one shuffle (every lane of the wave
+// must call it, each with its own m).
 struct QueueMap {
-    int pre;     // this lane's group start in dense order
+    int cnt;     // this lane's group count
     int total;
+    int span;    // positions of slot_t: 64 groups x the largest group count rounded up to 64
     uint32_t cap;
     RR_D void init(const QueueIn& q) {
         const int lane = threadIdx.x & 63;
         const int c = (int)q.ctr[lane * kQStride];
-        int incl = c;
+        int sum = c, mx = c;
         for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
+            sum += __shfl_xor(sum, off);
+            mx = max(mx, __shfl_xor(mx, off));
         }
-        pre = incl - c;
-        total = __shfl(incl, 63);
+        cnt = c;
+        total = sum;
+        span = ((mx + 63) & ~63) * 64;
         cap = q.cap;
         if (q.total && blockIdx.x == 0 && threadIdx.x == 0) *q.total = (uint32_t)total;
     }
-    RR_D uint32_t slot(int j) const {
-        int g = 0;
-        for (int step = 32; step > 0; step >>= 1) {  // largest g with pre[g] <= j
-            const int cand = g + step;
-            if (__shfl(pre, cand) <= j) g = cand;
-        }
-        return (uint32_t)g * cap + (uint32_t)(j - __shfl(pre, g));
+    // Time order: chunks of 64 entries, chunk c = entries 64 (c / 64) ..
+    // 64 (c / 64) + 63 of group c % 64 (kNoSlot past that group's count).
+    // Every producer wave appends its batch to its group in one piece as it
+    // goes, so a chunk holds the rays of about one producer batch (coherent
+    // within the consumer wave), and equal offsets in different groups were
+    // appended at about the same time, by waves working on one window of their
+    // own input (measured on C5 at 16 spp: extend 53.7 -> 49.9 ms, shadow
+    // 42.8 -> 39.9 ms against each wave walking a contiguous range of the
+    // group-concatenated order).
+    RR_D uint32_t slot_t(int m) const {
+        const int c = m >> 6;
+        const int g = c & 63, off = ((c >> 6) << 6) + (m & 63);
+        return off < __shfl(cnt, g) ? (uint32_t)g * cap + (uint32_t)off : kNoSlot;
     }
 };
 
@@ -1190,7 +1209,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
     }
 }
 
-// Extension rays entering bounce b: closest hit -> hits[j] (j dense).
+// Extension rays entering bounce b: closest hit -> hits[slot].
 template <bool kCount>
 __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
                                                                          float2* __restrict__ hits,
@@ -1202,26 +1221,26 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_extend(SceneAr
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
-        split_nodes(sa), sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
+        split_nodes(sa), sa.tris, sa.n_tris, qm.span, st, cnt, [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
             tmin = 0.0f;
             tmax = kFltMax;
         },
-        [&](int j, uint32_t, const Hit& h) { hits[j] = pack_hit(h); });
+        [&](int, uint32_t i, const Hit& h) { hits[i] = pack_hit(h); });
     if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
 }
 
-// Bounce b: shade from hits[j]; appends the next path queue and this bounce's
-// shadow queue.
+// Bounce b: shade from hits[slot], in the queue's time order (slot_t); appends
+// the next path queue and this bounce's shadow queue.
 __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in,
                                                          QueueIn qi, const float2* __restrict__ hits,
                                                          Rad rad, PathQueue out, ShadowQueue sq,
                                                          QueueOut qo) {
     QueueMap qm;
     qm.init(qi);
-    const int count = qm.total;
+    const int count = qm.span;
     const GlobalView v = global_view(sa);
     const int stride = gridDim.x * kBlock;
     int pid = 0;
@@ -1229,11 +1248,11 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
         const int j = b0 + (int)threadIdx.x;
         ShadeOut so;
         so.cont = so.shadow = false;
-        const uint32_t i = qm.slot(j);  // all lanes (shuffles); used only when j < count
-        if (j < count) {
+        const uint32_t i = qm.slot_t(j < count ? j : count - 1);  // all lanes (shuffles)
+        if (j < count && i != kNoSlot) {
             const float4 a = in.o[i], b = in.d[i], c = in.t[i];
             pid = f2i(a.w);
-            const Hit h = unpack_hit(hits[j]);
+            const Hit h = unpack_hit(hits[i]);
             const int sl = (int)fc.div_npix.div((uint32_t)pid);
             const int pix = pid - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
@@ -1257,7 +1276,7 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_shadow_refill(SceneA
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
-        split_nodes(sa), sa.tris, sa.n_tris, qm.total, st, cnt, [&](int j) { return qm.slot(j); },
+        split_nodes(sa), sa.tris, sa.n_tris, qm.span, st, cnt, [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
