@@ -205,11 +205,7 @@ constexpr int kHierLbvh = 2, kHierPloc = 3, kHierBvh4 = 4;
 // path), larger scenes the quantised BVH4 (split path).
 int frame_hier(int n_tris, int n_mats, int n_lights) {
     if (scene_in_lds(n_tris, n_mats, n_lights)) return kHierLbvh;
-#ifdef RR_SPLIT_BVH2
-    return kHierPloc;
-#else
     return kHierBvh4;
-#endif
 }
 
 // The view transform a frame on ctx is rendered with: Filmic needs the

@@ -991,16 +991,12 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
 #define RR_TRACE_WAVES 7
 #endif
 constexpr int kRefillBelow = RR_REFILL_BELOW;
-// Hierarchy of the split path: the PLOC BVH2 collapsed to the quantised BVH4.
-#ifdef RR_SPLIT_BVH2
-template <bool kAnyHit, bool kCount>
-using SplitTrav = TravState<kAnyHit, kCount>;
-RR_D const BvhNode* split_nodes(const SceneArgs& sa) { return sa.nodes; }
-#else
+// Hierarchy of the split path: the PLOC BVH2 collapsed to the quantised BVH4
+// (measured against walking the PLOC BVH2 itself, C5 / 02 / 03 frames at 16 /
+// 64 / 64 spp: 191 -> 139, 174 -> 149, 192 -> 160 ms).
 template <bool kAnyHit, bool kCount>
 using SplitTrav = TravStateQ4<kAnyHit, kCount>;
 RR_D const QNode4* split_nodes(const SceneArgs& sa) { return sa.nodes4; }
-#endif
 constexpr int kQGroups = 64;   // append groups per queue (one lane each in QueueMap)
 constexpr int kQStride = 32;   // words between group counters (128 B)
 

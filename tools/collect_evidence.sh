@@ -4,7 +4,7 @@
 #   tools/collect_evidence.sh r1
 set -euo pipefail
 tag=${1:-r1}
-for p in "" _02 _c5; do
+for p in "" _01 _02 _03 _c5; do
     d=gpurun_out/prof_${tag}${p}
     cp $d/${tag}${p}_kernel_stats.md profiles/${tag}${p}_kernel_stats.md
     cp $d/trace/run_kernel_stats.csv profiles/${tag}${p}_kernel_stats.csv

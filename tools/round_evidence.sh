@@ -8,11 +8,14 @@ S=tools/gpu_steps.sh
 mkdir -p gpurun_out/ev
 $S 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread ::: \
    900 tools/profile_round.sh $tag ::: \
+   900 tools/profile_round.sh ${tag}_01 01 ::: \
    900 tools/profile_round.sh ${tag}_02 02 ::: \
+   900 tools/profile_round.sh ${tag}_03 03 ::: \
    900 tools/profile_round.sh ${tag}_c5 c5 "--spp 64" || exit $?
-cp gpurun_out/prof_$tag/${tag}_pmc.json profiles/r1_pmc.json
-cp gpurun_out/prof_${tag}_02/${tag}_02_pmc.json profiles/r1_pmc_02.json
-cp gpurun_out/prof_${tag}_c5/${tag}_c5_pmc.json profiles/r1_pmc_c5.json
+# the bench lines below price their roofline with these (bench.py newest_profile)
+cp gpurun_out/prof_$tag/${tag}_pmc.json profiles/${tag}_pmc.json
+for w in 01 02 03; do cp gpurun_out/prof_${tag}_$w/${tag}_${w}_pmc.json profiles/${tag}_pmc_$w.json; done
+cp gpurun_out/prof_${tag}_c5/${tag}_c5_pmc.json profiles/${tag}_pmc_c5.json
 for wl in 04vs 01 02 03 c5; do
     $S 600 python bench.py --workload $wl > gpurun_out/ev/bench_$wl.json || exit $?
 done
