@@ -65,19 +65,19 @@ WORKLOADS = {
            "metric": "job frames/sec at 1/2/4/8 MI355X (02_physics stand-in)", "steps": 10, "warmup": 2,
            "data": "synthetic: 02_physics stand-in (2,000 closed-form rigid bodies, 92,002 triangles; the 02 .blend "
                    "is missing from the reference), PNG written per frame",
-           "workload": "02-physics-standin, 1 frame per step: 1920x1080, 64 spp, max 8 bounces, full LBVH "
+           "workload": "02-physics-standin, 1 frame per step: 1920x1080, 64 spp, max 8 bounces, full hierarchy "
                        "rebuild every frame + wavefront path trace + PNG encode/write"},
     "03": {"job": os.path.join(ROOT, "jobs", "03_physics-2-standin_480f-8w_dynamic.toml"),
            "metric": "job frames/sec at 1/2/4/8 MI355X (03_physics-2 stand-in)", "steps": 10, "warmup": 2,
            "data": "synthetic: 03_physics-2 stand-in (3,000 closed-form rigid bodies, 412,002 triangles), JPEG q90",
-           "workload": "03-physics-2-standin, 1 frame per step: 1920x1080, 64 spp, max 8 bounces, full LBVH "
+           "workload": "03-physics-2-standin, 1 frame per step: 1920x1080, 64 spp, max 8 bounces, full hierarchy "
                        "rebuild every frame + wavefront path trace + JPEG q90 encode/write"},
     "c5": {"job": os.path.join(ROOT, "jobs", "c5_synthetic-10m_240f-8w_dynamic.toml"),
            "metric": "job frames/sec at 1/2/4/8 MI355X (C5 synthetic 10M triangles, 4K, 1024 spp)",
            "steps": 2, "warmup": 1,
            "data": "synthetic: 512 displaced icospheres x 20,480 triangles + ground (10,485,762 triangles), "
                    "per-instance rigid motion, JPEG q90",
-           "workload": "c5-synthetic-10m, 1 frame per step: 3840x2160, 1024 spp, max 4 bounces, full LBVH "
+           "workload": "c5-synthetic-10m, 1 frame per step: 3840x2160, 1024 spp, max 4 bounces, full hierarchy "
                        "rebuild every frame + wavefront path trace + JPEG q90 encode/write"},
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -86,6 +86,7 @@ MALL_BYTES = 256 << 20  # Infinity Cache (MALL) capacity
 # (MI355X_MICROARCH.md, wave scheduling), 4 SIMDs per CU, 256 CUs.
 VALU_ISSUE_PER_CLK_PER_SIMD = 0.5
 SIMDS = 256 * 4
+PEAK_CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def parse_args():
@@ -205,14 +206,17 @@ def pmc_valu(cls: str, path: str, avg_ms: float):
             if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
                 if "SQ_INSTS_VALU" not in v or "GRBM_GUI_ACTIVE" not in v:
                     return None
-                pmc_ms = v.get("avg_ms") or avg_ms
-                clk = v["GRBM_GUI_ACTIVE"] / 8.0 / (pmc_ms * 1e-3)
+                # the effective clock of the counting pass (GRBM_GUI_ACTIVE / 8 over the
+                # same dispatches' duration, tools/pmc_summary.py), at most the
+                # 2.4 GHz peak engine clock; without it the peak clock
+                clk_ghz = min(float(v.get("clock_ghz_pmc") or PEAK_CLOCK_GHZ), PEAK_CLOCK_GHZ)
                 achieved = v["SQ_INSTS_VALU"] / (avg_ms * 1e-3)  # wave-instructions/s at the bench's launch time
-                peak = VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * clk
+                peak = VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * clk_ghz * 1e9
                 return {"achieved": round(achieved / 1e9, 1), "peak": round(peak / 1e9, 1),
                         "unit": "G wave-instr/s", "frac": round(achieved / peak, 3),
-                        "clock_ghz": round(clk / 1e9, 3), "valu_per_launch": round(v["SQ_INSTS_VALU"]),
-                        "source": os.path.relpath(path, ROOT)}
+                        "clock_ghz": round(clk_ghz, 3),
+                        "clock_source": "PMC pass" if v.get("clock_ghz_pmc") else "peak engine clock",
+                        "valu_per_launch": round(v["SQ_INSTS_VALU"]), "source": os.path.relpath(path, ROOT)}
     return None
 
 
@@ -350,7 +354,8 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names):
                     **hbm, "hbm_frac": round(per_s(bytes_frame) / HBM_PEAK_GBS, 4),
                     "note": "VALU-issue bound (LDS-resident scene); no PMC summary to price it"}
         return {**base, "bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],
-                "frac": valu["frac"], "clock_ghz": valu["clock_ghz"], "valu_per_launch": valu["valu_per_launch"],
+                "frac": valu["frac"], "clock_ghz": valu["clock_ghz"], "clock_source": valu["clock_source"],
+                "valu_per_launch": valu["valu_per_launch"],
                 "valu_source": valu["source"], **hbm, "hbm_frac": round(per_s(bytes_frame) / HBM_PEAK_GBS, 4),
                 "note": "k_tiles: scene in LDS, bound by vector-instruction issue (SQ_INSTS_VALU per launch / launch "
                         "time vs 0.5 wave-instr/clk/SIMD x 1024 SIMDs); HBM sees only film + RGBA8 (hbm_frac)"}

@@ -65,12 +65,32 @@ def cmd_stats(a):
         print(f"| `{k}` | {v['calls']} | {v['total_ms']:.3f} | {v['avg_ms']:.4f} | {v['pct']:.2f} |")
 
 
+def pass_durations(d: str) -> dict:
+    """{kernel: mean dispatch ns} from the kernel trace of a --pmc pass run with
+    --kernel-trace (empty if the pass has none)."""
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    acc = defaultdict(list)
+    for f in files:
+        with open(f, newline="") as fh:
+            for r in csv.DictReader(fh):
+                acc[short_name(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
 def cmd_traffic(a):
     fetch, write = counters(a.fetch), counters(a.write)
-    extra = {}
+    extra, clocks = {}, {}
     for d in a.sq or []:
-        for k, cs in counters(d).items():
+        cs_d = counters(d)
+        dur = pass_durations(d)
+        for k, cs in cs_d.items():
             extra.setdefault(k, {}).update(cs)
+            # effective clock of the pass that counted GRBM_GUI_ACTIVE (summed over
+            # the 8 XCDs) over the same dispatches' duration (MI355X_MICROARCH.md,
+            # DVFS note)
+            if "GRBM_GUI_ACTIVE" in cs and k in dur:
+                g = sum(cs["GRBM_GUI_ACTIVE"]) / len(cs["GRBM_GUI_ACTIVE"])
+                clocks[k] = {"pmc_pass_avg_ms": dur[k] / 1e6, "clock_ghz_pmc": g / 8.0 / dur[k]}
     out = {"source": {"fetch": a.fetch, "write": a.write, "sq": a.sq or []},
            "units": "bytes per launch; fetch_bytes = 2 x FETCH_SIZE(KiB) x 1024 (gfx950 correction)",
            "kernels": {}}
@@ -84,6 +104,7 @@ def cmd_traffic(a):
              "traffic_bytes": 2.0 * fr + wr}
         for c, vals in extra.get(k, {}).items():
             e[c] = sum(vals) / max(len(vals), 1)
+        e.update(clocks.get(k, {}))
         out["kernels"][k] = e
     with open(a.o, "w") as fh:
         json.dump(out, fh, indent=1)
