@@ -351,101 +351,144 @@ __global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restr
     }
 }
 
-// BVH4 collapse over a PLOC hierarchy: the child and parent links the
-// Karras build writes (children, node_parent = parent << 1 | side, root -1),
-// taken from the PLOC nodes.
-__global__ __launch_bounds__(kBlock) void k_ploc_links(int ni, const BvhNode* __restrict__ nodes,
-                                                       int2* __restrict__ children, int32_t* __restrict__ node_parent) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= ni) return;
-    const int4 d = nodes[i].d;
-    children[i] = make_int2(d.x, d.y);
-    if (d.x >= 0) node_parent[d.x] = 2 * i;
-    if (d.y >= 0) node_parent[d.y] = 2 * i + 1;
-    if (i == 0) node_parent[0] = -1;
-}
-
-// BVH4 collapse, step 1: depth parity of every internal node (walk to the
-// root through node_parent); flags[i] = 1 and rank[i] = 1 for even depth.
-__global__ __launch_bounds__(kBlock) void k_depth_parity(int ni, const int32_t* __restrict__ node_parent,
-                                                         uint32_t* __restrict__ flags, uint32_t* __restrict__ rank) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= ni) return;
-    int depth = 0;
-    for (int p = node_parent[i]; p >= 0 && depth < 4096; p = node_parent[p >> 1]) ++depth;
-    const uint32_t even = (depth & 1) ? 0u : 1u;
-    flags[i] = even;
-    rank[i] = even;
-}
-
-// BVH4 collapse, step 2 (after an exclusive scan of rank): every even-depth
-// BVH2 node i becomes BVH4 node rank[i]; its children, in slot order, are for
-// each side (left, right) either that leaf child, or both children of the
-// odd-depth internal child (leaf, or BVH4 node rank[grandchild]). Boxes come
-// from the parents' child boxes (the BVH2 boxes), quantised on the node's
-// grid (rr_device.h QNode4): origin = the lo corner of the children's union,
-// per axis the smallest exponent that spans the union in 255 steps, lo
-// rounded down and hi up.
-__global__ __launch_bounds__(kBlock) void k_collapse4(int ni, int n, const BvhNode* __restrict__ nodes,
-                                                      const int2* __restrict__ children,
-                                                      const uint32_t* __restrict__ flags,
-                                                      const uint32_t* __restrict__ rank,
-                                                      QNode4* __restrict__ out) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= ni || !flags[i]) return;
-    float lo[3][4], hi[3][4];
+// ------------------------------------------------------- BVH4 collapse ---
+// The BVH2 (PLOC; Karras below 3 triangles) becomes the quantised BVH4 of the
+// split path (rr_device.h QNode4), top down, one level per launch pair:
+//  - children of the BVH4 node rooted at BVH2 node r: start from r's two
+//    children; while there are fewer than four, the internal entry with the
+//    largest box measure (dx*dy + dy*dz + dz*dx, ties: lowest slot) is opened
+//    (replaced by its left child, its right child appended);
+//  - nodes are numbered breadth first and the internal children of a node
+//    take consecutive indices in slot order (level frontier [lo, hi): node k
+//    counts its internal children, an exclusive scan gives each node its
+//    children's first index hi + prefix), so siblings share 128 B lines;
+//  - child boxes are quantised on the node's grid: origin = the lo corner of
+//    the children's union, per axis the smallest exponent that spans it in
+//    255 steps, lo rounded down and hi up (exactly, in double).
+// oracle/rr_oracle.c lbvh_collapse4 / q4_pack restate it.
+struct C4Set {
+    int m;
     int ref[4];
-    int m = 0;
-    auto put = [&](const BvhNode& nd, int2 ch, int side) {
+    float lo[3][4], hi[3][4];
+};
+
+__device__ __forceinline__ float c4_measure(const C4Set& S, int c) {
+    const float dx = S.hi[0][c] - S.lo[0][c], dy = S.hi[1][c] - S.lo[1][c], dz = S.hi[2][c] - S.lo[2][c];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+__device__ void c4_set(const BvhNode* __restrict__ nodes, int n, int r, C4Set& S) {
+    auto put = [&](int slot, const BvhNode& nd, int side) {
         const float* f = reinterpret_cast<const float*>(&nd) + 6 * side;
-        const int c = side ? ch.y : ch.x;
         for (int a = 0; a < 3; ++a) {
-            lo[a][m] = f[a];
-            hi[a][m] = f[3 + a];
+            S.lo[a][slot] = f[a];
+            S.hi[a][slot] = f[3 + a];
         }
-        ref[m] = c < 0 ? c : (int)rank[c];
-        ++m;
+        S.ref[slot] = n > 1 ? (side ? nd.d.y : nd.d.x) : ~0;  // one triangle: both slots are leaf 0
     };
-    const BvhNode nd = nodes[i];
-    const int2 ch = n > 1 ? children[i] : make_int2(~0, ~0);
-    for (int side = 0; side < 2; ++side) {
-        const int c = side ? ch.y : ch.x;
-        if (c < 0) {
-            put(nd, ch, side);
+    const BvhNode nd = nodes[r];
+    put(0, nd, 0);
+    put(1, nd, 1);
+    S.m = 2;
+    while (S.m < 4) {
+        int best = -1;
+        float ba = 0.0f;
+        for (int c = 0; c < S.m; ++c) {
+            if (S.ref[c] < 0) continue;
+            const float a = c4_measure(S, c);
+            if (best < 0 || a > ba) {
+                best = c;
+                ba = a;
+            }
+        }
+        if (best < 0) break;
+        const BvhNode cn = nodes[S.ref[best]];
+        put(S.m, cn, 1);
+        put(best, cn, 0);
+        ++S.m;
+    }
+}
+
+// Level start: frontier [0, 1) = the BVH2 root.
+__global__ void k_c4_init(int32_t* __restrict__ ctl, int32_t* __restrict__ src) {
+    ctl[0] = 0;
+    ctl[1] = 1;
+    src[0] = 0;
+}
+
+// cnt[k] = internal children of frontier node lo + k (0 past the frontier,
+// k <= bound: the scan's total lands in cnt[bound]).
+__global__ __launch_bounds__(kBlock) void k_c4_count(const int32_t* __restrict__ ctl, int bound, int n,
+                                                     const BvhNode* __restrict__ nodes,
+                                                     const int32_t* __restrict__ src, uint32_t* __restrict__ cnt) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k > bound) return;
+    const int lo = ctl[0], hi = ctl[1];
+    uint32_t c = 0;
+    if (k < bound && lo + k < hi) {
+        C4Set S;
+        c4_set(nodes, n, src[lo + k], S);
+        for (int j = 0; j < S.m; ++j) c += S.ref[j] >= 0 ? 1u : 0u;
+    }
+    cnt[k] = c;
+}
+
+// Node lo + k: children -> indices hi + cnt[k] .. (after the exclusive scan),
+// their BVH2 roots -> src, the quantised node -> out.
+__global__ __launch_bounds__(kBlock) void k_c4_emit(const int32_t* __restrict__ ctl, int bound, int n,
+                                                    const BvhNode* __restrict__ nodes, int32_t* __restrict__ src,
+                                                    const uint32_t* __restrict__ cnt, QNode4* __restrict__ out) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= bound) return;
+    const int lo = ctl[0], hi = ctl[1];
+    const int idx = lo + k;
+    if (idx >= hi) return;
+    C4Set S;
+    c4_set(nodes, n, src[idx], S);
+    int next = hi + (int)cnt[k];
+    int ref[4];
+    for (int c = 0; c < 4; ++c) {
+        if (c >= S.m) {
+            ref[c] = kEmpty4;
+        } else if (S.ref[c] >= 0) {
+            src[next] = S.ref[c];
+            ref[c] = next++;
         } else {
-            const BvhNode cn = nodes[c];
-            const int2 cc = children[c];
-            put(cn, cc, 0);
-            put(cn, cc, 1);
+            ref[c] = S.ref[c];
         }
     }
-    const int used = m;
     float org[3];
     uint32_t ql[3] = {0u, 0u, 0u}, qh[3] = {0u, 0u, 0u}, eb = 0u;
     for (int a = 0; a < 3; ++a) {
-        float l = lo[a][0], h = hi[a][0];
-        for (int c = 1; c < used; ++c) {
-            l = fminf(l, lo[a][c]);
-            h = fmaxf(h, hi[a][c]);
+        float l = S.lo[a][0], h = S.hi[a][0];
+        for (int c = 1; c < S.m; ++c) {
+            l = fminf(l, S.lo[a][c]);
+            h = fmaxf(h, S.hi[a][c]);
         }
         const int e = q4_exponent((double)h - (double)l);
         org[a] = l;
         eb |= (uint32_t)(e + 128) << (8 * a);
         for (int c = 0; c < 4; ++c) {
-            const uint32_t ql_c = c < used ? q4_quant(lo[a][c], l, e, false) : 255u;
-            const uint32_t qh_c = c < used ? q4_quant(hi[a][c], l, e, true) : 0u;
+            const uint32_t ql_c = c < S.m ? q4_quant(S.lo[a][c], l, e, false) : 255u;
+            const uint32_t qh_c = c < S.m ? q4_quant(S.hi[a][c], l, e, true) : 0u;
             ql[a] |= ql_c << (8 * c);
             qh[a] |= qh_c << (8 * c);
         }
     }
-    for (; m < 4; ++m) ref[m] = kEmpty4;
     QNode4 o;
     o.org = make_float4(org[0], org[1], org[2], i2f((int)eb));
     o.child = make_int4(ref[0], ref[1], ref[2], ref[3]);
     o.q0 = make_uint4(ql[0], ql[1], ql[2], qh[0]);
     o.q1 = make_uint2(qh[1], qh[2]);
     o.pad = make_uint2(0u, 0u);
-    out[rank[i]] = o;
+    out[idx] = o;
+}
+
+// Next level: [hi, hi + total).
+__global__ void k_c4_advance(int32_t* __restrict__ ctl, int bound, const uint32_t* __restrict__ cnt) {
+    const int hi = ctl[1];
+    ctl[0] = hi;
+    ctl[1] = hi + (int)cnt[bound];
 }
 
 // ------------------------------------------------------------------ PLOC ---
@@ -796,7 +839,7 @@ void DevScene::release() {
     tri_world.release(); bounds.release();
     for (int k = 0; k < 2; ++k) { keys[k].release(); vals[k].release(); }
     hist.release(); scan_part.release(); children.release(); node_parent.release();
-    leaf_parent.release(); flags.release(); nodes.release(); tris.release(); nodes4.release(); rank4.release();
+    leaf_parent.release(); flags.release(); nodes.release(); tris.release(); nodes4.release(); q4_src.release(); q4_cnt.release(); q4_ctl.release();
     range.release();
     for (int k = 0; k < 2; ++k) ploc_cl[k].release();
     ploc_nn.release(); ploc_keep.release(); ploc_mrg.release(); ploc_ctl.release();
@@ -846,6 +889,43 @@ void build_ploc(DevScene& s, hipStream_t st) {
         if (cnt >= bound || rounds > 4 * 64 + 2 * n) throw std::runtime_error("PLOC made no progress");
         bound = cnt;
     }
+}
+
+// Quantised BVH4 of the built BVH2 (kernels above): one count / scan / emit /
+// advance round per level; the host learns the frontier size every 4 levels
+// (one synchronisation) and sizes the next launches by it (a level has at
+// most 4x the nodes of the one before).
+void build_bvh4(DevScene& s, hipStream_t st) {
+    const int n = s.n_tris;
+    const int ni = n > 1 ? n - 1 : 1;
+    s.nodes4.ensure((size_t)ni);
+    s.q4_src.ensure((size_t)ni);
+    s.q4_cnt.ensure((size_t)ni + 1);
+    s.q4_ctl.ensure(2);
+    k_c4_init<<<1, 1, 0, st>>>(s.q4_ctl.ptr, s.q4_src.ptr);
+    long frontier = 1;  // bound on the current level's node count
+    for (int level = 0;; ++level) {
+        const int bound = (int)std::min<long>(frontier, ni);
+        k_c4_count<<<cdiv(bound + 1, kBlock), kBlock, 0, st>>>(s.q4_ctl.ptr, bound, n, s.nodes.ptr, s.q4_src.ptr,
+                                                                s.q4_cnt.ptr);
+        exclusive_scan(s, s.q4_cnt.ptr, bound + 1, st);
+        k_c4_emit<<<cdiv(bound, kBlock), kBlock, 0, st>>>(s.q4_ctl.ptr, bound, n, s.nodes.ptr, s.q4_src.ptr,
+                                                           s.q4_cnt.ptr, s.nodes4.ptr);
+        k_c4_advance<<<1, 1, 0, st>>>(s.q4_ctl.ptr, bound, s.q4_cnt.ptr);
+        frontier = std::min<long>(frontier * 4, ni);
+        if ((level & 3) == 3) {
+            int ctl[2];
+            RR_HIP(hipMemcpyAsync(ctl, s.q4_ctl.ptr, sizeof ctl, hipMemcpyDeviceToHost, st));
+            RR_HIP(hipStreamSynchronize(st));
+            if (ctl[0] == ctl[1]) {
+                s.n4 = ctl[1];
+                break;
+            }
+            frontier = ctl[1] - ctl[0];
+            if (level > 4 * 4096) throw std::runtime_error("BVH4 collapse made no progress");
+        }
+    }
+    s.has4 = true;
 }
 
 void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, bool want_ploc) {
@@ -908,9 +988,6 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, b
     s.ploc = want_ploc && n > 2;
     if (s.ploc) {
         build_ploc(s, st);
-        if (want4)
-            k_ploc_links<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n - 1, s.nodes.ptr, s.children.ptr,
-                                                                  s.node_parent.ptr);
     } else if (n > 1) {
         k_karras<<<cdiv(n - 1, kBlock), kBlock, 0, st>>>(n, s.keys[0].ptr, s.children.ptr,
                                                           s.node_parent.ptr, s.leaf_parent.ptr, s.range.ptr);
@@ -920,23 +997,7 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, b
         k_refit<<<nb, kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr, s.leaf_parent.ptr,
                                        s.node_parent.ptr, s.children.ptr, s.flags.ptr, s.nodes.ptr,
                                        s.tris.ptr);
-    if (want4) {  // BVH4 collapse (flags are free again once refit is done)
-        const int ni = n > 1 ? n - 1 : 1;
-        s.rank4.ensure((size_t)ni + 1);
-        s.nodes4.ensure((size_t)ni);
-        if (n > 1) {
-            k_depth_parity<<<cdiv(ni, kBlock), kBlock, 0, st>>>(ni, s.node_parent.ptr, s.flags.ptr, s.rank4.ptr);
-        } else {
-            const uint32_t one = 1u;
-            RR_HIP(hipMemcpyAsync(s.flags.ptr, &one, sizeof one, hipMemcpyHostToDevice, st));
-            RR_HIP(hipMemcpyAsync(s.rank4.ptr, &one, sizeof one, hipMemcpyHostToDevice, st));
-        }
-        RR_HIP(hipMemsetAsync(s.rank4.ptr + ni, 0, sizeof(uint32_t), st));
-        exclusive_scan(s, s.rank4.ptr, ni + 1, st);  // rank4[ni] = BVH4 node count
-        k_collapse4<<<cdiv(ni, kBlock), kBlock, 0, st>>>(ni, n, s.nodes.ptr, s.children.ptr, s.flags.ptr,
-                                                         s.rank4.ptr, s.nodes4.ptr);
-        s.has4 = true;
-    }
+    if (want4) build_bvh4(s, st);
     if (prof) prof->end(st);
     RR_HIP(hipGetLastError());
     s.built = true;

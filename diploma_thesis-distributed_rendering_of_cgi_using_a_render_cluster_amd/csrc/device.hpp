@@ -71,7 +71,10 @@ struct DevScene {
     DevBuf<BvhNode> nodes;  // max(n-1, 1)
     DevBuf<TriPack> tris;   // n, leaf order
     DevBuf<QNode4> nodes4;     // quantised BVH4 collapse of `nodes` (split path), <= n-1
-    DevBuf<uint32_t> rank4;    // BVH2 node -> BVH4 index (exclusive scan); [n-1] = BVH4 count
+    DevBuf<int32_t> q4_src;    // BVH4 node -> its BVH2 root (collapse scratch)
+    DevBuf<uint32_t> q4_cnt;   // per frontier node: internal children (scanned in place)
+    DevBuf<int32_t> q4_ctl;    // current level [lo, hi)
+    int n4 = 0;                // BVH4 nodes
     bool has4 = false;
     // PLOC build (large scenes): cluster ping-pong, neighbours, scan flags, counters
     DevBuf<float4> ploc_cl[2];

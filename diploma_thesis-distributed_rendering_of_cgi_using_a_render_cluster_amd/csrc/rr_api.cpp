@@ -1016,10 +1016,7 @@ int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* c
         const int n = d.n_tris;
         *n4 = 0;
         if (n > 0) {
-            const int ni = n > 1 ? n - 1 : 1;
-            uint32_t cnt = 0;
-            RR_HIP(hipMemcpyAsync(&cnt, d.rank4.ptr + ni, sizeof cnt, hipMemcpyDeviceToHost, st));
-            RR_HIP(hipStreamSynchronize(st));
+            const uint32_t cnt = (uint32_t)d.n4;
             *n4 = (int32_t)cnt;
             if (children4 || nodes16) {
                 std::vector<QNode4> nodes(cnt);

@@ -464,63 +464,66 @@ static void q4_pack(const float lo[3][4], const float hi[3][4], const int ref[4]
 }
 
 /* BVH4 collapse of the BVH2 (PLOC, or Karras below 3 triangles), as
- * csrc/bvh.hip k_ploc_links + k_depth_parity + k_collapse4:
- * every even-depth internal node (root depth 0) becomes BVH4 node rank(i) =
- * number of even-depth nodes with a smaller index; its children in slot order
- * are, per side (left, right), the leaf child itself or both children of the
- * odd-depth internal child; boxes are the parents' child boxes. */
+ * csrc/bvh.hip build_bvh4 (k_c4_count / k_c4_emit): breadth first from the
+ * root; a node's children start as its BVH2 root's two children, and while
+ * fewer than four, the internal entry with the largest box measure
+ * dx*dy + dy*dz + dz*dx (ties: lowest slot) is replaced by its left child and
+ * its right child appended; the internal children of a node get consecutive
+ * indices in slot order after every node of the current level (a FIFO
+ * numbering). Boxes are the BVH2 child boxes, quantised by q4_pack. */
+typedef struct { int m; int ref[4]; float lo[3][4], hi[3][4]; } c4set;
+
+static void c4_put(const lbvh* B, c4set* S, int slot, int node, int side) {
+    const float* f = B->box + 12 * (size_t)node + 6 * side;
+    for (int a = 0; a < 3; ++a) { S->lo[a][slot] = f[a]; S->hi[a][slot] = f[3 + a]; }
+    S->ref[slot] = B->n > 1 ? B->child_lf[2 * node + side] : ~0;
+}
+
+static void c4_set(const lbvh* B, int r, c4set* S) {
+    c4_put(B, S, 0, r, 0);
+    c4_put(B, S, 1, r, 1);
+    S->m = 2;
+    while (S->m < 4) {
+        int best = -1;
+        float ba = 0.0f;
+        for (int c = 0; c < S->m; ++c) {
+            if (S->ref[c] < 0) continue;
+            float dx = S->hi[0][c] - S->lo[0][c], dy = S->hi[1][c] - S->lo[1][c], dz = S->hi[2][c] - S->lo[2][c];
+            float a = dx * dy + dy * dz + dz * dx;
+            if (best < 0 || a > ba) { best = c; ba = a; }
+        }
+        if (best < 0) break;
+        int cn = S->ref[best];
+        c4_put(B, S, S->m, cn, 1);
+        c4_put(B, S, best, cn, 0);
+        ++S->m;
+    }
+}
+
 static void lbvh_collapse4(lbvh* B) {
     const int n = B->n;
     B->n4 = 0;
     if (n <= 0) return;
     const int ni = n > 1 ? n - 1 : 1;
-    int* depth = (int*)malloc(sizeof(int) * (size_t)ni);
-    int* rank = (int*)malloc(sizeof(int) * (size_t)ni);
-    int* stack = (int*)malloc(sizeof(int) * (size_t)ni + 16);
-    int sp = 0;
-    depth[0] = 0;
-    stack[sp++] = 0;
-    while (sp && n > 1) {
-        int v = stack[--sp];
-        for (int s = 0; s < 2; ++s) {
-            int c = B->child[2 * v + s];
-            if (c >= 0) { depth[c] = depth[v] + 1; stack[sp++] = c; }
+    int* src = (int*)malloc(sizeof(int) * (size_t)ni);
+    B->child4 = (int*)malloc(sizeof(int) * 4 * (size_t)ni);
+    B->q4 = (uint32_t*)malloc(sizeof(uint32_t) * 16 * (size_t)ni);
+    src[0] = 0;
+    int count = 1;
+    for (int idx = 0; idx < count; ++idx) {
+        c4set S;
+        c4_set(B, src[idx], &S);
+        int ref[4];
+        for (int c = 0; c < 4; ++c) {
+            if (c >= S.m) ref[c] = ORC_EMPTY4;
+            else if (S.ref[c] >= 0) { src[count] = S.ref[c]; ref[c] = count++; }
+            else ref[c] = S.ref[c];
         }
+        q4_pack((const float(*)[4])S.lo, (const float(*)[4])S.hi, ref, S.m, B->q4 + 16 * (size_t)idx);
+        for (int c = 0; c < 4; ++c) B->child4[4 * (size_t)idx + c] = ref[c];
     }
-    int n4 = 0;
-    for (int i = 0; i < ni; ++i) {
-        rank[i] = n4;
-        if ((depth[i] & 1) == 0) ++n4;
-    }
-    B->n4 = n4;
-    B->child4 = (int*)malloc(sizeof(int) * 4 * (size_t)n4);
-    B->q4 = (uint32_t*)malloc(sizeof(uint32_t) * 16 * (size_t)n4);
-    for (int i = 0; i < ni; ++i) {
-        if (depth[i] & 1) continue;
-        float lo[3][4], hi[3][4];
-        int ref[4], m = 0;
-        for (int side = 0; side < 2; ++side) {
-            int c = B->child[2 * i + side];
-            int par[2], sd[2], k = 0;
-            if (c < 0) { par[0] = i; sd[0] = side; k = 1; }
-            else { par[0] = c; sd[0] = 0; par[1] = c; sd[1] = 1; k = 2; }
-            for (int q = 0; q < k; ++q) {
-                const float* f = B->box + 12 * (size_t)par[q] + 6 * sd[q];
-                int cc = B->child[2 * par[q] + sd[q]];
-                for (int a = 0; a < 3; ++a) { lo[a][m] = f[a]; hi[a][m] = f[3 + a]; }
-                ref[m] = cc < 0 ? cc : rank[cc];
-                ++m;
-            }
-        }
-        const int used = m;
-        for (; m < 4; ++m) {
-            for (int a = 0; a < 3; ++a) { lo[a][m] = 0.0f; hi[a][m] = 0.0f; }
-            ref[m] = ORC_EMPTY4;
-        }
-        q4_pack((const float(*)[4])lo, (const float(*)[4])hi, ref, used, B->q4 + 16 * (size_t)rank[i]);
-        for (int c = 0; c < 4; ++c) B->child4[4 * (size_t)rank[i] + c] = ref[c];
-    }
-    free(depth); free(rank); free(stack);
+    B->n4 = count;
+    free(src);
 }
 
 /* ------------------------------------------------------------ tracing ---- */
