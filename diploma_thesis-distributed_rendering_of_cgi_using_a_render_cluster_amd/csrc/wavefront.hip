@@ -572,7 +572,11 @@ RR_D void stage_camera(lds_f4w* q, lds_tri* tris, int n_tris, const FrameConsts&
     }
 }
 
-// cam_fc: also stage the camera-ray data (stage_camera) after the scene.
+// kCam: also stage the camera-ray data (stage_camera, from *cam_fc) after the
+// scene. A compile-time switch, not a null test on cam_fc: comparing the
+// address of the kernel's FrameConsts argument with null kept the whole
+// struct in scratch (180 B per lane, every field read with a scratch load).
+template <bool kCam = false>
 RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& used,
                          const FrameConsts* cam_fc = nullptr) {
     lds_f4w* q = base;
@@ -598,7 +602,7 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
         lds_copy(q, reinterpret_cast<const float4*>(a.mat_lut), kMatLutStride / 4 * a.n_mats);
         q += kMatLutStride / 4 * a.n_mats;
     }
-    if (shading || cam_fc) __syncthreads();  // the copies above are visible
+    if (shading || kCam) __syncthreads();  // the copies above are visible
     if (shading) {  // per-triangle unit normals
         v.nrm = q;
         for (int i = threadIdx.x; i < a.n_tris; i += kBlock) {
@@ -610,7 +614,7 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
         }
         q += a.n_tris;
     }
-    if (cam_fc) {
+    if constexpr (kCam) {
         v.cam = q;
         stage_camera(q, v.tris, a.n_tris, *cam_fc);
         q += kCamF4 * a.n_tris;
@@ -751,7 +755,7 @@ __global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_primary(FrameConsts 
     if constexpr (kLds) {
         extern __shared__ float4 dyn4[];
         int used;
-        const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used, &fc);
+        const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
         primary_body<kCount>(fc, v, np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack, traced);
     } else {
         primary_body<kCount>(fc, global_view(sa), np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack, traced);
@@ -1019,7 +1023,12 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack&
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int nw = gridDim.x * kWavesPerBlock;
-    const int w = (int)wave_id();
+    // this wave's rank with the waves ordered XCD by XCD (blocks b and b + 8
+    // share an XCD, MI355X_MICROARCH.md): consecutive chunks go to one XCD, so
+    // each XCD's L2 serves one eighth of the window instead of all of it
+    const int G = (int)gridDim.x, bx = (int)blockIdx.x, xcd = bx & 7;
+    const int w = __builtin_amdgcn_readfirstlane((xcd * (G >> 3) + min(xcd, G & 7) + (bx >> 3)) * kWavesPerBlock +
+                                                 (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
     // position of the q-th ray of this wave's sequence
     auto gpos = [&](int q) { return ((q >> 6) * nw + w) * 64 + (q & 63); };
     int next = 0;  // wave-uniform cursor into this wave's sequence
@@ -1668,7 +1677,7 @@ __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(lds_stack);
     int used;
-    const LdsView v = stage_scene((lds_f4w*)dyn4, sa, true, used, &fc);
+    const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
     tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl);
 }
 
