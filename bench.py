@@ -517,6 +517,9 @@ def main():
                                      "2 frames in flight: frame N encoded + written while N+1 renders",
                        "view_transform_substituted": int(any(substituted))},
             "mrays_per_s_per_gpu": round(traced / elapsed / 1e6, 1),
+            # SURVEY 8(d)'s form: rays traced over the summed render-kernel time
+            "mrays_per_s_per_gpu_kernel_time": (round(traced / (sum(kernel_ms) * 1e-3) / 1e6, 1)
+                                                if sum(kernel_ms) > 0 else None),
             "rays_per_frame": {k: v // max(args.steps, 1) for k, v in rays.items()},
             "device_ms_per_frame": round(sum(kernel_ms) / max(args.steps, 1), 3),
             "kernels": per_class,
