@@ -461,11 +461,39 @@ struct TravState {
 
 RR_D int i4get(const int4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
-// Resumable traversal of the quantised BVH4 (same contract as TravState).
-// Per node and axis: s = iq * 2^e (exact), o' = (org - o) * iq; a plane at grid
-// coordinate q lies at t = fma(q, s, o'). The near plane is lo for iq >= 0,
-// else hi (iq is never 0 or inf, so no NaN and no min/max per axis).
-// Leaf children whose boxes pass are intersected at once in slot order; the
+// The four child box tests of a quantised node for one ray (iq: q4_rcp of the
+// direction): bit c set when child c exists and its box meets [tmin, tcur];
+// tn[c] = the entry distance. Per axis s = iq * 2^e (exact), o' = (org - o) *
+// iq; a plane at grid coordinate q lies at t = fma(q, s, o'); the near plane is
+// lo for iq >= 0, else hi (iq is never 0 or inf, so no NaN and no min/max per
+// axis). oracle/rr_oracle.c trace4() restates it.
+RR_D uint32_t q4_box_hits(const float4& org, const int4& ch, const uint4& q0, const uint2& q1, float3 o, float3 iq,
+                          float tmin, float tcur, float tn[4]) {
+    const uint32_t eb = (uint32_t)f2i(org.w);
+    const float sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
+    const float sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
+    const float sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
+    const float ox = (org.x - o.x) * iq.x, oy = (org.y - o.y) * iq.y, oz = (org.z - o.z) * iq.z;
+    const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
+    const uint32_t nx = px ? q0.x : q0.w, fx = px ? q0.w : q0.x;
+    const uint32_t ny = py ? q0.y : q1.x, fy = py ? q1.x : q0.y;
+    const uint32_t nz = pz ? q0.z : q1.y, fz = pz ? q1.y : q0.z;
+    uint32_t hits = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int sh = 8 * c;
+        const float t0 = fmaxf(fmaxf(fmaf((float)((nx >> sh) & 255u), sx, ox), fmaf((float)((ny >> sh) & 255u), sy, oy)),
+                               fmaxf(fmaf((float)((nz >> sh) & 255u), sz, oz), tmin));
+        const float t1 = fminf(fminf(fmaf((float)((fx >> sh) & 255u), sx, ox), fmaf((float)((fy >> sh) & 255u), sy, oy)),
+                               fminf(fmaf((float)((fz >> sh) & 255u), sz, oz), tcur));
+        tn[c] = t0;
+        if (i4get(ch, c) != kEmpty4 && t0 <= t1) hits |= 1u << c;
+    }
+    return hits;
+}
+
+// Resumable traversal of the quantised BVH4 (same contract as TravState), box
+// tests by q4_box_hits. Leaf children whose boxes pass are intersected at once in slot order; the
 // nearest hit internal child is visited next and the others are pushed in
 // descending slot order. oracle/rr_oracle.c trace4() is the same walk.
 template <bool kAnyHit, bool kCount = false>
@@ -494,31 +522,12 @@ struct TravStateQ4 {
         uint32_t leaves = 0, inner = 0;
         {
             const QNode4* p = nodes + node;
-            const float4 org = p->org;
             const int4 ch = p->child;
-            const uint4 q0 = p->q0;
-            const uint2 q1 = p->q1;
-            const uint32_t eb = (uint32_t)f2i(org.w);
-            const float sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
-            const float sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
-            const float sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
-            const float ox = (org.x - o.x) * iq.x, oy = (org.y - o.y) * iq.y, oz = (org.z - o.z) * iq.z;
-            const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
-            const uint32_t nx = px ? q0.x : q0.w, fx = px ? q0.w : q0.x;
-            const uint32_t ny = py ? q0.y : q1.x, fy = py ? q1.x : q0.y;
-            const uint32_t nz = pz ? q0.z : q1.y, fz = pz ? q1.y : q0.z;
+            const uint32_t hm = q4_box_hits(p->org, ch, p->q0, p->q1, o, iq, tmin, tcur, tn);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 ref[c] = i4get(ch, c);
-                const int sh = 8 * c;
-                const float t0 = fmaxf(fmaxf(fmaf((float)((nx >> sh) & 255u), sx, ox),
-                                             fmaf((float)((ny >> sh) & 255u), sy, oy)),
-                                       fmaxf(fmaf((float)((nz >> sh) & 255u), sz, oz), tmin));
-                const float t1 = fminf(fminf(fmaf((float)((fx >> sh) & 255u), sx, ox),
-                                             fmaf((float)((fy >> sh) & 255u), sy, oy)),
-                                       fminf(fmaf((float)((fz >> sh) & 255u), sz, oz), tcur));
-                tn[c] = t0;
-                if (ref[c] != kEmpty4 && t0 <= t1) {
+                if ((hm >> c) & 1u) {
                     if (ref[c] < 0) leaves |= 1u << c;
                     else inner |= 1u << c;
                 }

@@ -1017,18 +1017,21 @@ constexpr int kQStride = 32;   // words between group counters (128 B)
 // flight over the whole frame). map(k) may return kNoSlot (a gap): that
 // position holds no ray.
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+// This wave's rank with the waves ordered XCD by XCD (blocks b and b + 8 share
+// an XCD, MI355X_MICROARCH.md): consecutive chunks go to one XCD, so each
+// XCD's L2 serves one eighth of the window instead of all of it.
+RR_D int xcd_wave_rank() {
+    const int G = (int)gridDim.x, bx = (int)blockIdx.x, xcd = bx & 7;
+    return __builtin_amdgcn_readfirstlane((xcd * (G >> 3) + min(xcd, G & 7) + (bx >> 3)) * kWavesPerBlock +
+                                          (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
+}
 template <typename TS, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack& st, TravCount& cnt, MapFn&& map,
                        RayFn&& ray_of, DoneFn&& done) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int nw = gridDim.x * kWavesPerBlock;
-    // this wave's rank with the waves ordered XCD by XCD (blocks b and b + 8
-    // share an XCD, MI355X_MICROARCH.md): consecutive chunks go to one XCD, so
-    // each XCD's L2 serves one eighth of the window instead of all of it
-    const int G = (int)gridDim.x, bx = (int)blockIdx.x, xcd = bx & 7;
-    const int w = __builtin_amdgcn_readfirstlane((xcd * (G >> 3) + min(xcd, G & 7) + (bx >> 3)) * kWavesPerBlock +
-                                                 (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
+    const int w = xcd_wave_rank();
     // position of the q-th ray of this wave's sequence
     auto gpos = [&](int q) { return ((q >> 6) * nw + w) * 64 + (q & 63); };
     int next = 0;  // wave-uniform cursor into this wave's sequence
@@ -1184,6 +1187,127 @@ __global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary(FrameC
         [&](int p, uint32_t, const Hit& h) { hits[p] = pack_hit(h); });
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
     if ((threadIdx.x & 63) == 0 && n_traced) atomicAdd(traced, n_traced);
+    if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
+}
+
+// Packet traversal (camera rays of the split path, render_split decides): one wave walks the quantised BVH4 for the rays of its 64
+// lanes together, visiting the union of the nodes they need one node at a
+// time. The node index is wave-uniform, so the 64 B node (and every leaf
+// triangle) comes in through scalar loads, once per wave instead of once per
+// lane, and each lane runs the same box and triangle tests as its own walk
+// (q4_box_hits, leaf_test) against its own ray, with its own closest-hit bound.
+// A lane tests every leaf the wave visits whose box its ray passes, so it
+// meets every triangle its own walk would; the accept rule (smaller t, then
+// smaller original id) makes the closest hit the same. Children are visited
+// nearest first for the first lane that enters the node. For coherent rays
+// this trades extra node visits per ray for one memory request per visit
+// instead of 64 (measured per 02 / 03 frame at 64 spp: camera-ray traversal
+// 24.2 -> 14.6, 21.8 -> 15.0 ms). It loses where the rays of a tile part ways
+// early: C5, about one triangle per pixel, 23.6 -> 33.5 ms at 16 spp; and the
+// shadow rays of camera hits (per-lane 39.7 / 46.8 ms, packets 121 / 86 ms on
+// C5 / 02) are not coherent enough for it at all.
+// act: the lane has a ray; stk: this wave's kPacketStack LDS entries.
+constexpr int kPacketStack = 128;  // a node pushes <= 3: bounded by 3 x the BVH4 depth
+template <bool kCount>
+RR_D void packet_trace(const QNode4* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk, bool act,
+                       float3 o, float3 d, float tmin, Hit& h, TravCount& cnt) {
+    if (!__ballot(act)) return;
+    const float3 iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
+    int node = 0, sp = 0;
+    for (;;) {
+        const bool live = act;
+        const QNode4* p = nodes + node;
+        const int4 ch = p->child;
+        float tn[4];
+        const uint32_t hm = live ? q4_box_hits(p->org, ch, p->q0, p->q1, o, iq, tmin, h.t, tn) : 0u;
+        if (kCount && live) ++cnt.nodes;
+        // leaf children in slot order (a lane tests those its ray enters)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int r = i4get(ch, c);
+            if (r >= 0 || r == kEmpty4 || !__ballot((hm >> c) & 1u)) continue;
+            const int f = leaf_first(r), m = leaf_count(r);
+            for (int k = 0; k < m; ++k) {
+                const TriPack tp = load_tri(tris, f + k);
+                if ((hm >> c) & 1u) {
+                    if (kCount) ++cnt.tris;
+                    leaf_test(tp, f + k, o, d, tmin, h);
+                }
+            }
+        }
+        // internal children some lane enters: the representative lane's nearest next
+        uint32_t inner = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int r = i4get(ch, c);
+            if (r >= 0 && r != kEmpty4 && __ballot((hm >> c) & 1u)) inner |= 1u << c;
+        }
+        if (!inner) {
+            if (sp == 0) break;
+            node = __builtin_amdgcn_readfirstlane(stk[--sp]);
+            continue;
+        }
+        const uint64_t any = __ballot(hm != 0u);
+        const int rl = (int)__builtin_ctzll(any);
+        const uint32_t rh = (uint32_t)__builtin_amdgcn_readlane((int)hm, rl);
+        int best = -1;
+        float bt = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (!((inner >> c) & 1u)) continue;
+            const float tc = ((rh >> c) & 1u)
+                                 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tn[c]), rl))
+                                 : __builtin_huge_valf();
+            if (best < 0 || tc < bt) {
+                best = c;
+                bt = tc;
+            }
+        }
+#pragma unroll
+        for (int c = 3; c >= 0; --c)
+            if (c != best && ((inner >> c) & 1u) && sp < kPacketStack) stk[sp++] = i4get(ch, c);  // never full here
+        node = __builtin_amdgcn_readfirstlane(i4get(ch, best));
+    }
+}
+
+// Camera paths as packets: a wave traces the 64 camera rays of one 8x8 pixel
+// tile (one sample) with packet_trace. Tiles are dealt to the waves as
+// trace_refill deals chunks (round-robin over the XCD-ordered waves).
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, RR_TRACE_WAVES) void k_trace_primary_packet(
+    FrameConsts fc, SceneArgs sa, int np, float2* __restrict__ hits, int32_t* __restrict__,
+    unsigned long long* __restrict__ tc, uint32_t* __restrict__ traced) {
+    __shared__ int stack_all[kWavesPerBlock * kPacketStack];
+    lds_int* stk = lds_slot(stack_all) + (threadIdx.x >> 6) * kPacketStack;
+    TravCount cnt;
+    const ScreenCull cull = screen_cull(fc, sa.nodes);
+    const int lane = threadIdx.x & 63;
+    const int tiles_x = (fc.W + 7) >> 3, tiles_y = (fc.H + 7) >> 3;
+    const int ntiles = tiles_x * tiles_y;
+    const int npk = ntiles * (np / fc.npix);
+    const int nw = gridDim.x * kWavesPerBlock;
+    uint32_t n_traced = 0;
+    for (int q = xcd_wave_rank(); q < npk; q += nw) {
+        const int sl = q / ntiles, t = q - sl * ntiles;
+        const int ty = t / tiles_x, tx = t - ty * tiles_x;
+        const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
+        const bool valid = px < fc.W && py < fc.H;
+        const int pix = py * fc.W + px;
+        float3 o = mk3(0.0f, 0.0f, 0.0f), d = o;
+        float tmin = 0.0f, tmax = -1.0f;
+        bool culled = true;
+        if (valid) {
+            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
+            camera_ray_xy(fc, sa.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
+        }
+        n_traced += valid && !culled ? 1u : 0u;
+        Hit h;
+        set_miss(h, tmax);
+        packet_trace<kCount>(sa.nodes4, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt);
+        if (valid) hits[(size_t)sl * fc.npix + pix] = pack_hit(h);
+    }
+    for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
+    if (lane == 0 && n_traced) atomicAdd(traced, n_traced);
     if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
 }
 
@@ -1927,10 +2051,12 @@ struct SplitGrids {
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
+    void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
         kts = count ? k_shadow_refill<true> : k_shadow_refill<false>;
+        ktpk = count ? k_trace_primary_packet<true> : k_trace_primary_packet<false>;
         trace_p = grid_for(ktp, 0);
         trace_e = grid_for(kte, 0);
         shadow = grid_for(kts, 0);
@@ -2004,6 +2130,9 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
     const SplitGrids G(tc != nullptr);
     const int npix = base.npix;
     const int cpc = counters_per_chunk(base.max_bounces);
+    // camera rays as packets (packet_trace) when triangles are large on screen:
+    // at most one triangle per two pixels (02 / 03 yes, C5 no)
+    const bool packets = (long)base.n_tris * 2 <= (long)npix;
     // group counters: [chunk][bounce 0..max][path | shadow][kQGroups * kQStride]
     const size_t per_q = (size_t)kQGroups * kQStride;
     const size_t per_chunk = (size_t)(base.max_bounces + 1) * 2 * per_q;
@@ -2024,8 +2153,8 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         if ((size_t)std::max(cap_p, cap_e) * kQGroups > p.cap)
             throw std::runtime_error("queue capacity exceeded (split path)");
         pr.begin(st, RR_K_PRIMARY);
-        G.ktp<<<clamp_grid(np, G.trace_p), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc,
-                                                             tot + camera_traced_slot(base.max_bounces));
+        (packets ? G.ktpk : G.ktp)<<<clamp_grid(np, G.trace_p), kBlock, 0, st>>>(
+            fc, sa, np, p.hits.ptr, p.spill.ptr, tc, tot + camera_traced_slot(base.max_bounces));
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
         k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq,
