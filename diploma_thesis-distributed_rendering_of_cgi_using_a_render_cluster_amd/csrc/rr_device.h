@@ -2,8 +2,10 @@
 //
 // Every floating-point expression here is written in the exact operation order
 // of the CPU oracle (oracle/rr_oracle.c), compiled with contraction OFF on both
-// sides (-ffp-contract=off plus the pragma below), IEEE division/sqrt (hipcc's
-// default correctly rounded f32 div/sqrt), and no libm transcendentals on the
+// sides (-ffp-contract=off plus the pragma below): a fused multiply-add appears
+// only where the source spells fmaf() (v_fma_f32 here, the correctly rounded
+// fmaf of C99 in the oracle, the same single rounding), IEEE division/sqrt
+// (hipcc's default correctly rounded f32 div/sqrt), and no libm transcendentals on the
 // per-sample path (sin/cos by the fixed polynomial of sincos_small, sRGB by a
 // host-built table). That makes the GPU image reproducible bit for bit by the
 // oracle (tests/test_gpu_parity.py).
@@ -73,6 +75,21 @@ RR_HD uint32_t q4_quant(float v, float org, int e, bool up) {
 // Reciprocal for the quantised slab test: finite for zero components (a ray
 // parallel to an axis gets +-2^64, which keeps every plane distance finite).
 RR_HD float q4_rcp(float x) { return fabsf(x) < 0x1p-64f ? (x < 0.0f ? -0x1p64f : 0x1p64f) : 1.0f / x; }
+// Finite reciprocal of a ray direction for the slab tests (BVH2 and BVH4): one
+// division for the three components when their product is at least 2^-100
+// (then no component is below 2^-100 and nothing overflows), else q4_rcp per
+// component. Traversal only decides which boxes are opened; the hits come from
+// the triangle test, so the reciprocal's last bits never reach a pixel except
+// through the oracle's identical walk.
+RR_HD float3 rcp3(float3 d) {
+    const float p = d.x * d.y;
+    const float q = p * d.z;
+    if (fabsf(q) >= 0x1p-100f) {
+        const float r = 1.0f / q;
+        return make_float3(r * (d.y * d.z), r * (d.x * d.z), r * p);
+    }
+    return make_float3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
+}
 
 // Triangle in leaf order, 48 B: v0 | e1 = v1-v0 | e2 = v2-v0, with the original
 // triangle id and material id in the .w lanes.
@@ -105,9 +122,18 @@ RR_HD float3 add3(float3 a, float3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b
 RR_HD float3 sub3(float3 a, float3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
 RR_HD float3 mul3(float3 a, float3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
 RR_HD float3 scl3(float3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
-RR_HD float dot3(float3 a, float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// Products of the vector helpers accumulate through fmaf (one rounding per
+// multiply-add; dot: x first, then y, then z).
+RR_HD float dot3(float3 a, float3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 RR_HD float3 cross3(float3 a, float3 b) {
-    return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    return mk3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+// a + b s, per component
+RR_HD float3 madd3(float3 a, float3 b, float s) { return mk3(fmaf(b.x, s, a.x), fmaf(b.y, s, a.y), fmaf(b.z, s, a.z)); }
+// x t + y u + z w (a point of the frame t, u, w)
+RR_HD float3 frame3(float3 t, float3 u, float3 w, float x, float y, float z) {
+    return mk3(fmaf(w.x, z, fmaf(u.x, y, t.x * x)), fmaf(w.y, z, fmaf(u.y, y, t.y * x)),
+               fmaf(w.z, z, fmaf(u.z, y, t.z * x)));
 }
 RR_HD float3 norm3(float3 a) {
     const float inv = 1.0f / sqrtf(dot3(a, a));
@@ -167,9 +193,10 @@ RR_HD float rng(uint32_t key, uint32_t dim) {
 // sin/cos on |x| <= pi/4 (Cephes sinf/cosf kernels), fixed op order.
 RR_HD void sincos_small(float x, float& s, float& c) {
     const float z = x * x;
-    s = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x + x;
-    c = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z -
-        0.5f * z + 1.0f;
+    const float ps = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    s = fmaf(ps * z, x, x);
+    const float pc = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+    c = fmaf(pc * z, z, fmaf(-0.5f, z, 1.0f));
 }
 
 // Shirley-Chiu concentric square->disk map; angles stay in [-pi/4, pi/4].
@@ -178,8 +205,8 @@ RR_HD void sincos_small(float x, float& s, float& c) {
 // (pi/4) a/b, x = b sin, y = b cos; a = b = 0: the origin), but a wave whose
 // lanes fall in both cases pays for one division and one sincos, not two.
 RR_HD void concentric_disk(float u1, float u2, float& x, float& y) {
-    const float a = 2.0f * u1 - 1.0f;
-    const float b = 2.0f * u2 - 1.0f;
+    const float a = fmaf(2.0f, u1, -1.0f);
+    const float b = fmaf(2.0f, u2, -1.0f);
     const bool wide = fabsf(a) > fabsf(b);
     const float num = wide ? b : a, r = wide ? a : b;
     float s, c;
@@ -194,15 +221,15 @@ RR_HD void make_onb(float3 n, float3& b1, float3& b2) {
     const float sign = copysignf(1.0f, n.z);
     const float a = -1.0f / (sign + n.z);
     const float b = n.x * n.y * a;
-    b1 = mk3(1.0f + sign * n.x * n.x * a, sign * b, -sign * n.x);
-    b2 = mk3(b, sign + n.y * n.y * a, -n.y);
+    b1 = mk3(fmaf(sign * n.x * n.x, a, 1.0f), sign * b, -sign * n.x);
+    b2 = mk3(b, fmaf(n.y * n.y, a, sign), -n.y);
 }
 
 // Self-intersection-safe ray origin (Waechter & Binder, Ray Tracing Gems ch. 6).
 RR_HD float offset_axis(float p, float n) {
     const int of = (int)(256.0f * n);
     const float pi = i2f(f2i(p) + ((p < 0.0f) ? -of : of));
-    return fabsf(p) < 0.03125f ? p + 1.52587890625e-05f * n : pi;
+    return fabsf(p) < 0.03125f ? fmaf(1.52587890625e-05f, n, p) : pi;
 }
 RR_HD float3 offset_ray(float3 p, float3 n) {
     return mk3(offset_axis(p.x, n.x), offset_axis(p.y, n.y), offset_axis(p.z, n.z));
@@ -216,7 +243,7 @@ RR_HD float table_lerp(FloatP t, int n, float u) {
     if (i >= n - 1) return t[n - 1];
     if (i < 0) i = 0;
     const float fr = f - (float)i;
-    return t[i] + (t[i + 1] - t[i]) * fr;
+    return fmaf(t[i + 1] - t[i], fr, t[i]);
 }
 
 // ------------------------------------------------------- screen culling ---
@@ -256,11 +283,12 @@ RR_HD bool screen_rect(float3 pos, float3 right, float3 up, float3 back, float h
 // ---------------------------------------------------------- intersection ---
 // Slab test against [bmin,bmax]; inclusive so equal-t candidates survive (the
 // closest hit is then independent of traversal order, see closest_tri()).
-RR_HD bool slab(float3 o, float3 invd, float bx0, float by0, float bz0, float bx1, float by1,
+// Plane distances t = fmaf(b, invd, oi) with oi = -(o invd) per ray (rcp3).
+RR_HD bool slab(float3 oi, float3 invd, float bx0, float by0, float bz0, float bx1, float by1,
                 float bz1, float tmin, float tmax, float& tnear) {
-    const float tx0 = (bx0 - o.x) * invd.x, tx1 = (bx1 - o.x) * invd.x;
-    const float ty0 = (by0 - o.y) * invd.y, ty1 = (by1 - o.y) * invd.y;
-    const float tz0 = (bz0 - o.z) * invd.z, tz1 = (bz1 - o.z) * invd.z;
+    const float tx0 = fmaf(bx0, invd.x, oi.x), tx1 = fmaf(bx1, invd.x, oi.x);
+    const float ty0 = fmaf(by0, invd.y, oi.y), ty1 = fmaf(by1, invd.y, oi.y);
+    const float tz0 = fmaf(bz0, invd.z, oi.z), tz1 = fmaf(bz1, invd.z, oi.z);
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
     tnear = tn;
@@ -401,7 +429,7 @@ struct TravCount {
 // nodes / tris: global or LDS pointers (wavefront.hip SceneView).
 template <bool kAnyHit, bool kCount = false>
 struct TravState {
-    float3 o, d, invd;
+    float3 o, d, invd, oi;
     float tmin;
     Hit h;
     int node;
@@ -413,7 +441,8 @@ struct TravState {
         h.u = h.v = 0.0f;
         h.idx = -1;
         h.orig = -1;
-        invd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        invd = rcp3(d);
+        oi = mk3(-(o.x * invd.x), -(o.y * invd.y), -(o.z * invd.z));
         node = 0;
     }
     // One node visit; true when the ray is finished (any-hit: on the first hit).
@@ -422,8 +451,8 @@ struct TravState {
         const BvhNode nd = load_node(nodes, node);
         if (kCount) ++cnt.nodes;
         float tl, tr;
-        bool hl = slab(o, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
-        bool hr = slab(o, invd, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
+        bool hl = slab(oi, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
+        bool hr = slab(oi, invd, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
         const int cl = nd.d.x, cr = nd.d.y;
         // passing leaves (single triangles), left then right, one per
         // iteration: lanes with only a left and lanes with only a right leaf
@@ -510,7 +539,7 @@ struct TravStateQ4 {
         h.u = h.v = 0.0f;
         h.idx = -1;
         h.orig = -1;
-        iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
+        iq = rcp3(d);
         node = 0;
     }
     template <typename TriP, typename Stack>
@@ -657,7 +686,8 @@ RR_HD float lut_at(FloatP t, float u) {
 // Terms of the view direction shared by every evaluation at one shading point
 // (NEE and the sampled continuation): computed once per shading point.
 struct BsdfView {
-    float cosV, ps, fv, g1v;
+    float cosV, ps, fv;
+    float cv1;  // cosV + sqrt(a2 + (1 - a2) cosV^2): Smith G1(V) = 2 cosV / cv1
 };
 
 // f * cosL (the BSDF times the cosine of the light direction, Cycles'
@@ -669,7 +699,11 @@ struct BsdfView {
 //   specular F * D G1(V) G1(L) / (4 cosV cosL), GGX D, separable Smith G1,
 //            F = cspec0 (1 - FH) + FH, FH = the table at L.H
 // with |V + L|^2 = 2 + 2 L.V, so (N.H)^2 = (cosV + cosL)^2 / (2 + 2 L.V) and
-// (L.H)^2 = (1 + L.V) / 2 (no normalised half vector).
+// (L.H)^2 = (1 + L.V) / 2 (no normalised half vector). One division: with
+// den = 2 + 2 L.V, tt = (N.H)^2 (a2 - 1) + 1 = X / den, X = (cosV + cosL)^2
+// (a2 - 1) + den, and G1(c) = 2c / c1, c1 = c + sqrt(a2 + (1 - a2) c^2):
+//   D G1(V) / (4 cosV)           = a2 den^2 / (2 pi X^2 cv1)        (pdf_s)
+//   D G1(V) G1(L) / (4 cosV)     = a2 den^2 cosL / (pi X^2 cv1 cl1)  (ks)
 // lut: this material's table (kMatLutStride floats).
 template <typename FloatP>
 RR_HD float3 bsdf_eval_v(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, float3 wo, float3 wi, float& pdf) {
@@ -691,20 +725,23 @@ RR_HD float3 bsdf_eval_v(const Mat& m, FloatP lut, const BsdfView& vw, float3 N,
     const float fv = vw.fv;
     const float rr = m.roughness * (lv + 1.0f);
     const float kd =
-        m.kd0 * ((1.0f - 0.5f * fv) * (1.0f - 0.5f * fl) + rr * (fl + fv + fl * fv * (rr - 1.0f))) * cosL;
+        m.kd0 * fmaf(rr, fmaf(fl * fv, rr - 1.0f, fl + fv), fmaf(-0.5f, fv, 1.0f) * fmaf(-0.5f, fl, 1.0f)) * cosL;
     // specular
     const float sv = cosV + cosL;
-    const float nh2 = sv * sv / (2.0f + 2.0f * lv);
-    const float tt = nh2 * (a2 - 1.0f) + 1.0f;
-    const float pdf_s = vw.g1v * a2 / (12.5663706143592f * tt * tt * cosV);  // D G1(V) / (4 cosV)
-    const float g1l = 2.0f * cosL / (cosL + sqrtf(a2 + (1.0f - a2) * cosL * cosL));
-    const float ks = m.spec_on ? pdf_s * g1l : 0.0f;  // D G1(V) G1(L) / (4 cosV cosL) * cosL
-    const float fh = lut_at(lut, sqrtf((1.0f + lv) * 0.5f));  // L.H = sqrt((1 + L.V) / 2)
+    const float den = fmaf(2.0f, lv, 2.0f);
+    const float X = fmaf(sv * sv, a2 - 1.0f, den);
+    const float cl1 = cosL + sqrtf(fmaf((1.0f - a2) * cosL, cosL, a2));
+    const float q = a2 * den * den;
+    const float r = 1.0f / (3.14159265358979f * X * X * vw.cv1 * cl1);
+    const float pdf_s = q * cl1 * r * 0.5f;                 // D G1(V) / (4 cosV)
+    const float ks = m.spec_on ? q * cosL * r : 0.0f;       // D G1(V) G1(L) / (4 cosV cosL) * cosL
+    const float fh = lut_at(lut, sqrtf(fmaf(0.5f, lv, 0.5f)));  // L.H = sqrt((1 + L.V) / 2)
     const float3 c0 = m.cspec0;
-    const float3 F = mk3(c0.x * (1.0f - fh) + fh, c0.y * (1.0f - fh) + fh, c0.z * (1.0f - fh) + fh);
+    const float fh1 = 1.0f - fh;
+    const float3 F = mk3(fmaf(c0.x, fh1, fh), fmaf(c0.y, fh1, fh), fmaf(c0.z, fh1, fh));
     const float pdf_d = cosL * 0.318309886183791f;
-    pdf = (1.0f - ps) * pdf_d + ps * pdf_s;
-    return mk3(m.base.x * kd + F.x * ks, m.base.y * kd + F.y * ks, m.base.z * kd + F.z * ks);
+    pdf = fmaf(ps, pdf_s, (1.0f - ps) * pdf_d);
+    return mk3(fmaf(F.x, ks, m.base.x * kd), fmaf(F.y, ks, m.base.y * kd), fmaf(F.z, ks, m.base.z * kd));
 }
 
 template <typename FloatP>
@@ -714,7 +751,7 @@ RR_HD BsdfView bsdf_view(const Mat& m, FloatP lut, float3 N, float3 wo) {
     v.ps = lut_at(lut + (kMatLutN + 1), v.cosV);  // 0 for Lambert and without a specular closure
     v.fv = schlick_w(v.cosV);
     const float a2 = m.a2;
-    v.g1v = 2.0f * v.cosV / (v.cosV + sqrtf(a2 + (1.0f - a2) * v.cosV * v.cosV));
+    v.cv1 = v.cosV + sqrtf(fmaf((1.0f - a2) * v.cosV, v.cosV, a2));
     return v;
 }
 
@@ -736,11 +773,11 @@ RR_HD float3 bsdf_eval(const Mat& m, FloatP lut, float3 N, float3 wo, float3 wi,
 // so that x^2 + y^2 = 1 - z^2, without a division.
 RR_HD float3 sample_vndf(float3 v, float alpha, float dx, float dy) {
     const float3 vh = norm3(mk3(alpha * v.x, alpha * v.y, v.z));
-    const float r2 = dx * dx + dy * dy;
+    const float r2 = fmaf(dy, dy, dx * dx);
     const float k = 1.0f + vh.z;
-    const float z = 1.0f - r2 * k;
-    const float s = sqrtf(fmaxf(0.0f, k * (2.0f - r2 * k)));
-    const float3 h = mk3(dx * s + vh.x, dy * s + vh.y, fmaxf(0.0f, z + vh.z));
+    const float z = fmaf(-r2, k, 1.0f);
+    const float s = sqrtf(fmaxf(0.0f, k * fmaf(-r2, k, 2.0f)));
+    const float3 h = mk3(fmaf(dx, s, vh.x), fmaf(dy, s, vh.y), fmaxf(0.0f, z + vh.z));
     return norm3(mk3(alpha * h.x, alpha * h.y, h.z));
 }
 
@@ -761,13 +798,12 @@ RR_HD bool bsdf_sample(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, f
     if (glossy) {
         const float3 wl = mk3(dot3(wo, T), dot3(wo, B), cosV);
         const float3 hl = sample_vndf(wl, m.alpha, x, y);
-        const float3 H = mk3(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,
-                             T.z * hl.x + B.z * hl.y + N.z * hl.z);
+        const float3 H = frame3(T, B, N, hl.x, hl.y, hl.z);
         const float k = 2.0f * dot3(wo, H);
-        wi = mk3(H.x * k - wo.x, H.y * k - wo.y, H.z * k - wo.z);
+        wi = mk3(fmaf(H.x, k, -wo.x), fmaf(H.y, k, -wo.y), fmaf(H.z, k, -wo.z));
     } else {
-        const float z = sqrtf(fmaxf(0.0f, 1.0f - x * x - y * y));
-        wi = mk3(T.x * x + B.x * y + N.x * z, T.y * x + B.y * y + N.y * z, T.z * x + B.z * y + N.z * z);
+        const float z = sqrtf(fmaxf(0.0f, fmaf(-y, y, fmaf(-x, x, 1.0f))));
+        wi = frame3(T, B, N, x, y, z);
     }
     f = bsdf_eval_v(m, lut, vw, N, wo, wi, pdf);
     return pdf > 0.0f;

@@ -167,12 +167,12 @@ __device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt
             return;
         }
     }
-    const float sx = (fx * fc.inv_w2 - 1.0f) * fc.half_w;
-    const float sy = (1.0f - fy * fc.inv_h2) * fc.half_h;
-    const float len = sqrtf(sx * sx + sy * sy + 1.0f);
-    const float3 dw = mk3(fc.cam_right.x * sx + fc.cam_up.x * sy - fc.cam_back.x,
-                          fc.cam_right.y * sx + fc.cam_up.y * sy - fc.cam_back.y,
-                          fc.cam_right.z * sx + fc.cam_up.z * sy - fc.cam_back.z);
+    const float sx = fmaf(fx, fc.inv_w2, -1.0f) * fc.half_w;
+    const float sy = fmaf(-fy, fc.inv_h2, 1.0f) * fc.half_h;
+    const float len = sqrtf(fmaf(sy, sy, fmaf(sx, sx, 1.0f)));
+    const float3 dw = mk3(fmaf(fc.cam_up.x, sy, fmaf(fc.cam_right.x, sx, -fc.cam_back.x)),
+                          fmaf(fc.cam_up.y, sy, fmaf(fc.cam_right.y, sx, -fc.cam_back.y)),
+                          fmaf(fc.cam_up.z, sy, fmaf(fc.cam_right.z, sx, -fc.cam_back.z)));
     const float il = 1.0f / len;
     d = scl3(dw, il);
     o = fc.cam_pos;
@@ -246,7 +246,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     const Mat m = view_mat(v, mid);
     const auto lut = v.lut + kMatLutStride * mid;
     const float t = h.t;
-    const float3 P = mk3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+    const float3 P = madd3(o, d, t);
     float3 N;
     if constexpr (std::is_same<View, LdsView>::value)
         N = xyz(lds_ld4(v.nrm + h.idx));  // staged: norm3(cross3(e1, e2))
@@ -284,8 +284,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
                 concentric_disk(rng(key, dim0 + 1u), rng(key, dim0 + 2u), dx, dy);
                 dx = dx * radius;
                 dy = dy * radius;
-                const float3 sp = mk3(lp.x + b1.x * dx + b2.x * dy, lp.y + b1.y * dx + b2.y * dy,
-                                      lp.z + b1.z * dx + b2.z * dy);
+                const float3 sp = madd3(madd3(lp, b1, dx), b2, dy);
                 const float3 ts = sub3(sp, P);
                 const float ds2 = dot3(ts, ts);
                 dist = sqrtf(ds2);
@@ -1733,6 +1732,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             bool live = valid;
             for (int b = 0; b <= fc.max_bounces; ++b) {
                 if (!__any(live)) break;
+                bool cont = false, shadow = false;
                 if (live) {
                     ShadeOut so;
                     Hit h;
@@ -1743,13 +1743,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                         traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, ce);
                     }
                     shade(fc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, fc.n_tris, st, cs});
-                    if (b == 0) {
-                        n_c0 += wave_count(so.cont);
-                        n_s0 += wave_count(so.shadow);
-                    } else {
-                        n_c1 += wave_count(so.cont);
-                        n_s1 += wave_count(so.shadow);
-                    }
+                    cont = so.cont;
+                    shadow = so.shadow;
                     if (so.cont) {
                         o = so.o;
                         d = so.d;
@@ -1758,6 +1753,16 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     } else {
                         live = false;
                     }
+                }
+                // counted with the whole wave active: a ballot inside `if (live)`
+                // would land in the counters of live lanes only, and lane 0 (the
+                // one flush_rays reads) may be dead by then
+                if (b == 0) {
+                    n_c0 += wave_count(cont);
+                    n_s0 += wave_count(shadow);
+                } else {
+                    n_c1 += wave_count(cont);
+                    n_s1 += wave_count(shadow);
                 }
             }
             acc.x = acc.x + L.x;

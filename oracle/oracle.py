@@ -237,3 +237,14 @@ def material_lut(mat12) -> np.ndarray:
     out = np.zeros(260, np.float32)
     lib().orc_material_lut(_p(m, ctypes.c_float), _p(out, ctypes.c_float))
     return out
+
+
+def ray_counts():
+    """Ray statistics of the last render (test/debug): (continuations at bounce 0,
+    shadow rays at bounce 0, continuations later, shadow rays later) and the
+    first (pixel, sample) pairs whose path continued past bounce 1."""
+    out = np.zeros(4, np.int64)
+    late = np.zeros(32, np.int32)
+    n = ctypes.c_int(0)
+    lib().orc_ray_counts(_p(out, ctypes.c_longlong), _p(late, ctypes.c_int32), ctypes.byref(n))
+    return tuple(int(x) for x in out), [tuple(late[2 * k:2 * k + 2]) for k in range(n.value)]

@@ -23,9 +23,11 @@
  *    unit_float_to_uchar_clamp.
  *  - Written scalar, one path at a time, in the same IEEE single-precision
  *    operation order as the HIP kernels, without contraction (built with
- *    -ffp-contract=off; x86-64 SSE has no FMA by default) and without libm
- *    transcendentals on the per-sample path, so GPU and oracle agree bit for
- *    bit on identical inputs (tests/test_gpu_parity.py).
+ *    -ffp-contract=off): a fused multiply-add happens exactly where both
+ *    sides spell fmaf() (C99 fmaf is correctly rounded, as v_fma_f32 is; -mfma
+ *    makes it one instruction), and without libm transcendentals on the
+ *    per-sample path, so GPU and oracle agree bit for bit on identical inputs
+ *    (tests/test_gpu_parity.py).
  *  - Pinning of this oracle against analytic known answers (white furnace,
  *    point-light closed form, ray/triangle and LBVH vs brute force):
  *    tests/test_oracle.py.
@@ -49,8 +51,15 @@ static v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
 static v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 static v3 vmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
 static v3 vscl(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
-static float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-static v3 vcross(v3 a, v3 b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+/* products accumulate through fmaf (rr_device.h dot3 / cross3 / madd3 / frame3) */
+static float vdot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static v3 vcross(v3 a, v3 b) {
+    return V(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+static v3 vmadd(v3 a, v3 b, float s) { return V(fmaf(b.x, s, a.x), fmaf(b.y, s, a.y), fmaf(b.z, s, a.z)); }
+static v3 vframe(v3 t, v3 u, v3 w, float x, float y, float z) {
+    return V(fmaf(w.x, z, fmaf(u.x, y, t.x * x)), fmaf(w.y, z, fmaf(u.y, y, t.y * x)), fmaf(w.z, z, fmaf(u.z, y, t.z * x)));
+}
 static v3 vnorm(v3 a) { float inv = 1.0f / sqrtf(vdot(a, a)); return vscl(a, inv); }
 static float vmax3(v3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
 
@@ -95,7 +104,7 @@ static float lerp_table(const float* t, int n, float u) {
     if (i >= n - 1) return t[n - 1];
     if (i < 0) i = 0;
     float fr = f - (float)i;
-    return t[i] + (t[i + 1] - t[i]) * fr;
+    return fmaf(t[i + 1] - t[i], fr, t[i]);
 }
 
 /* --------------------------------------------------------------- RNG ---- */
@@ -114,12 +123,14 @@ static float rnd(uint32_t key, uint32_t dim) {
 /* ---------------------------------------------------------- sampling ---- */
 static void small_sincos(float x, float* s, float* c) {
     float z = x * x;
-    *s = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x + x;
-    *c = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z - 0.5f * z + 1.0f;
+    float ps = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    *s = fmaf(ps * z, x, x);
+    float pc = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+    *c = fmaf(pc * z, z, fmaf(-0.5f, z, 1.0f));
 }
 
 static void disk(float u1, float u2, float* x, float* y) {
-    float a = 2.0f * u1 - 1.0f, b = 2.0f * u2 - 1.0f, s, c;
+    float a = fmaf(2.0f, u1, -1.0f), b = fmaf(2.0f, u2, -1.0f), s, c;
     if (a == 0.0f && b == 0.0f) { *x = 0.0f; *y = 0.0f; return; }
     if (fabsf(a) > fabsf(b)) {
         small_sincos(0.785398163397448f * (b / a), &s, &c);
@@ -134,14 +145,14 @@ static void onb(v3 n, v3* b1, v3* b2) {
     float sign = copysignf(1.0f, n.z);
     float a = -1.0f / (sign + n.z);
     float b = n.x * n.y * a;
-    *b1 = V(1.0f + sign * n.x * n.x * a, sign * b, -sign * n.x);
-    *b2 = V(b, sign + n.y * n.y * a, -n.y);
+    *b1 = V(fmaf(sign * n.x * n.x, a, 1.0f), sign * b, -sign * n.x);
+    *b2 = V(b, fmaf(n.y * n.y, a, sign), -n.y);
 }
 
 static float off_axis(float p, float n) {
     int of = (int)(256.0f * n);
     float pi = ibits(fbits(p) + ((p < 0.0f) ? -of : of));
-    return fabsf(p) < 0.03125f ? p + 1.52587890625e-05f * n : pi;
+    return fabsf(p) < 0.03125f ? fmaf(1.52587890625e-05f, n, p) : pi;
 }
 static v3 offset_ray(v3 p, v3 n) { return V(off_axis(p.x, n.x), off_axis(p.y, n.y), off_axis(p.z, n.z)); }
 
@@ -441,6 +452,17 @@ static uint32_t q4_quant(float v, float org, int e, int up) {
 }
 /* finite reciprocal for the quantised slab test (rr_device.h q4_rcp) */
 static float q4_rcp(float x) { return fabsf(x) < 0x1p-64f ? (x < 0.0f ? -0x1p64f : 0x1p64f) : 1.0f / x; }
+/* slab-test reciprocal of a direction (rr_device.h rcp3): one division when
+ * the component product is at least 2^-100, else q4_rcp per component */
+static v3 rcp3(v3 d) {
+    float p = d.x * d.y;
+    float q = p * d.z;
+    if (fabsf(q) >= 0x1p-100f) {
+        float r = 1.0f / q;
+        return V(r * (d.y * d.z), r * (d.x * d.z), r * p);
+    }
+    return V(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
+}
 
 static void q4_pack(const float lo[3][4], const float hi[3][4], const int ref[4], int used, uint32_t* o) {
     uint32_t ql[3] = {0, 0, 0}, qh[3] = {0, 0, 0}, eb = 0;
@@ -529,10 +551,11 @@ static void lbvh_collapse4(lbvh* B) {
 /* ------------------------------------------------------------ tracing ---- */
 typedef struct { float t, u, v; int idx, orig; } hitrec;
 
-static int slab_test(v3 o, v3 inv, const float* b, float tmin, float tmax, float* tnear) {
-    float tx0 = (b[0] - o.x) * inv.x, tx1 = (b[3] - o.x) * inv.x;
-    float ty0 = (b[1] - o.y) * inv.y, ty1 = (b[4] - o.y) * inv.y;
-    float tz0 = (b[2] - o.z) * inv.z, tz1 = (b[5] - o.z) * inv.z;
+/* plane distances fmaf(b, inv, oi), oi = -(o inv) per ray (rr_device.h slab) */
+static int slab_test(v3 oi, v3 inv, const float* b, float tmin, float tmax, float* tnear) {
+    float tx0 = fmaf(b[0], inv.x, oi.x), tx1 = fmaf(b[3], inv.x, oi.x);
+    float ty0 = fmaf(b[1], inv.y, oi.y), ty1 = fmaf(b[4], inv.y, oi.y);
+    float tz0 = fmaf(b[2], inv.z, oi.z), tz1 = fmaf(b[5], inv.z, oi.z);
     float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
     float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
     *tnear = tn;
@@ -584,7 +607,8 @@ typedef struct { float t; int slot, ref; } ckey;
 static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hitrec* h) {
     h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
     if (B->n <= 0) return 0;
-    const float iq[3] = {q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z)};
+    const v3 iqv = rcp3(d);
+    const float iq[3] = {iqv.x, iqv.y, iqv.z};
     const float oo[3] = {o.x, o.y, o.z};
     int stack[ORC_MAXDEPTH];
     int sp = 0, node = 0;
@@ -647,14 +671,15 @@ static int trace(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hit
     if (B->width == 4) return trace4(B, o, d, tmin, tmax, any, h);
     h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
     if (B->n <= 0) return 0;
-    v3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    v3 inv = rcp3(d);
+    v3 oi = V(-(o.x * inv.x), -(o.y * inv.y), -(o.z * inv.z));
     int stack[ORC_MAXDEPTH];
     int sp = 0, node = 0;
     for (;;) {
         const float* bx = B->box + 12 * (size_t)node;
         float tl, tr;
-        int hl = slab_test(o, inv, bx, tmin, h->t, &tl);
-        int hr = slab_test(o, inv, bx + 6, tmin, h->t, &tr);
+        int hl = slab_test(oi, inv, bx, tmin, h->t, &tl);
+        int hr = slab_test(oi, inv, bx + 6, tmin, h->t, &tr);
         int cl = B->child_lf[2 * node], cr = B->child_lf[2 * node + 1];
         int nl = 0, nr = 0, fl = 0, fr = 0;
         if (hl && cl < 0) { fl = leaf_first(cl); nl = leaf_count(cl); hl = 0; }
@@ -762,9 +787,12 @@ static mterms mat_terms(const mat_t* m) {
     return t;
 }
 
-static float g1_of(float a2, float c) { return 2.0f * c / (c + sqrtf(a2 + (1.0f - a2) * c * c)); }
+/* c + sqrt(a2 + (1 - a2) c^2): Smith G1(c) = 2c / c1 */
+static float g1_den(float a2, float c) { return c + sqrtf(fmaf((1.0f - a2) * c, c, a2)); }
 
-/* f * cosL and the combined pdf (csrc/rr_device.h bsdf_eval_v) */
+/* f * cosL and the combined pdf (csrc/rr_device.h bsdf_eval_v, one division:
+ * den = 2 + 2 L.V, X = (cosV + cosL)^2 (a2 - 1) + den = tt den,
+ * pdf_s = a2 den^2 / (2 pi X^2 cv1), ks = a2 den^2 cosL / (pi X^2 cv1 cl1)) */
 static v3 eval_bsdf(const mat_t* m, const float* lut, v3 N, v3 wo, v3 wi, float ps, float* pdf) {
     float cosV = vdot(N, wo), cosL = vdot(N, wi);
     if (cosV <= 0.0f || cosL <= 0.0f) { *pdf = 0.0f; return V(0.0f, 0.0f, 0.0f); }
@@ -777,20 +805,22 @@ static v3 eval_bsdf(const mat_t* m, const float* lut, v3 N, v3 wo, v3 wi, float 
     float a2 = T.a2;
     float fl = sw(cosL), fv = sw(cosV);
     float rr = m->roughness * (lv + 1.0f);
-    float kd = T.kd0 * ((1.0f - 0.5f * fv) * (1.0f - 0.5f * fl) + rr * (fl + fv + fl * fv * (rr - 1.0f))) * cosL;
+    float kd = T.kd0 * fmaf(rr, fmaf(fl * fv, rr - 1.0f, fl + fv), fmaf(-0.5f, fv, 1.0f) * fmaf(-0.5f, fl, 1.0f)) * cosL;
     float sv = cosV + cosL;
-    float nh2 = sv * sv / (2.0f + 2.0f * lv);
-    float tt = nh2 * (a2 - 1.0f) + 1.0f;
-    float g1v = g1_of(a2, cosV);
-    float pdf_s = g1v * a2 / (12.5663706143592f * tt * tt * cosV);
-    float g1l = g1_of(a2, cosL);
-    float ks = T.spec_on ? pdf_s * g1l : 0.0f;
-    float fh = lut_at(lut, sqrtf((1.0f + lv) * 0.5f));
+    float den = fmaf(2.0f, lv, 2.0f);
+    float X = fmaf(sv * sv, a2 - 1.0f, den);
+    float cv1 = g1_den(a2, cosV), cl1 = g1_den(a2, cosL);
+    float q = a2 * den * den;
+    float r = 1.0f / (3.14159265358979f * X * X * cv1 * cl1);
+    float pdf_s = q * cl1 * r * 0.5f;
+    float ks = T.spec_on ? q * cosL * r : 0.0f;
+    float fh = lut_at(lut, sqrtf(fmaf(0.5f, lv, 0.5f)));
     v3 c0 = T.cspec0;
-    v3 F = V(c0.x * (1.0f - fh) + fh, c0.y * (1.0f - fh) + fh, c0.z * (1.0f - fh) + fh);
+    float fh1 = 1.0f - fh;
+    v3 F = V(fmaf(c0.x, fh1, fh), fmaf(c0.y, fh1, fh), fmaf(c0.z, fh1, fh));
     float pdf_d = cosL * 0.318309886183791f;
-    *pdf = (1.0f - ps) * pdf_d + ps * pdf_s;
-    return V(m->base.x * kd + F.x * ks, m->base.y * kd + F.y * ks, m->base.z * kd + F.z * ks);
+    *pdf = fmaf(ps, pdf_s, (1.0f - ps) * pdf_d);
+    return V(fmaf(F.x, ks, m->base.x * kd), fmaf(F.y, ks, m->base.y * kd), fmaf(F.z, ks, m->base.z * kd));
 }
 
 static float p_spec(const float* lut, float cosV) { return lut_at(lut + ORC_LUT_N + 1, cosV); }
@@ -798,11 +828,11 @@ static float p_spec(const float* lut, float cosV) { return lut_at(lut + ORC_LUT_
 /* GGX visible normals by spherical caps (Dupuy & Benyoub 2023), csrc/rr_device.h sample_vndf */
 static v3 vndf(v3 v, float alpha, float dx, float dy) {
     v3 vh = vnorm(V(alpha * v.x, alpha * v.y, v.z));
-    float r2 = dx * dx + dy * dy;
+    float r2 = fmaf(dy, dy, dx * dx);
     float k = 1.0f + vh.z;
-    float z = 1.0f - r2 * k;
-    float s = sqrtf(fmaxf(0.0f, k * (2.0f - r2 * k)));
-    v3 h = V(dx * s + vh.x, dy * s + vh.y, fmaxf(0.0f, z + vh.z));
+    float z = fmaf(-r2, k, 1.0f);
+    float s = sqrtf(fmaxf(0.0f, k * fmaf(-r2, k, 2.0f)));
+    v3 h = V(fmaf(dx, s, vh.x), fmaf(dy, s, vh.y), fmaxf(0.0f, z + vh.z));
     return vnorm(V(alpha * h.x, alpha * h.y, h.z));
 }
 
@@ -822,13 +852,12 @@ static int sample_bsdf(const mat_t* m, const float* lut, v3 N, v3 wo, float ul, 
         if (alpha < 1.0e-3f) alpha = 1.0e-3f;
         v3 wl = V(vdot(wo, T), vdot(wo, B), cosV);
         v3 hl = vndf(wl, alpha, x, y);
-        v3 H = V(T.x * hl.x + B.x * hl.y + N.x * hl.z, T.y * hl.x + B.y * hl.y + N.y * hl.z,
-                 T.z * hl.x + B.z * hl.y + N.z * hl.z);
+        v3 H = vframe(T, B, N, hl.x, hl.y, hl.z);
         float k = 2.0f * vdot(wo, H);
-        *wi = V(H.x * k - wo.x, H.y * k - wo.y, H.z * k - wo.z);
+        *wi = V(fmaf(H.x, k, -wo.x), fmaf(H.y, k, -wo.y), fmaf(H.z, k, -wo.z));
     } else {
-        float z = sqrtf(fmaxf(0.0f, 1.0f - x * x - y * y));
-        *wi = V(T.x * x + B.x * y + N.x * z, T.y * x + B.y * y + N.y * z, T.z * x + B.z * y + N.z * z);
+        float z = sqrtf(fmaxf(0.0f, fmaf(-y, y, fmaf(-x, x, 1.0f))));
+        *wi = vframe(T, B, N, x, y, z);
     }
     *f = eval_bsdf(m, lut, N, wo, *wi, ps, pdf);
     return *pdf > 0.0f;
@@ -895,16 +924,23 @@ static mat_t load_mat(const float* mats, int id) {
     return r;
 }
 
+/* Ray statistics of the last orc_render (orc_ray_counts): continuations and
+ * shadow rays created at bounce 0 / at later bounces, as rr_frame_stats counts
+ * them, and the first (pixel, sample) pairs whose path continued past bounce 1. */
+static long long g_rays[4];
+static int g_late[32], g_n_late;
+
 static v3 radiance(const scene_t* S, int pix, int sample) {
     const float* c = S->cam;
     uint32_t key = pkey(S->seed, (uint32_t)pix, (uint32_t)sample);
     int px = pix % S->W, py = pix / S->W;
     float fx = (float)px + 0.5f + lerp_table(S->filter, ORC_FILTER_N, rnd(key, 0));
     float fy = (float)py + 0.5f + lerp_table(S->filter, ORC_FILTER_N, rnd(key, 1));
-    float sx = (fx * S->inv_w2 - 1.0f) * c[12];
-    float sy = (1.0f - fy * S->inv_h2) * c[13];
-    float len = sqrtf(sx * sx + sy * sy + 1.0f);
-    v3 dw = V(c[3] * sx + c[6] * sy - c[9], c[4] * sx + c[7] * sy - c[10], c[5] * sx + c[8] * sy - c[11]);
+    float sx = fmaf(fx, S->inv_w2, -1.0f) * c[12];
+    float sy = fmaf(-fy, S->inv_h2, 1.0f) * c[13];
+    float len = sqrtf(fmaf(sy, sy, fmaf(sx, sx, 1.0f)));
+    v3 dw = V(fmaf(c[6], sy, fmaf(c[3], sx, -c[9])), fmaf(c[7], sy, fmaf(c[4], sx, -c[10])),
+              fmaf(c[8], sy, fmaf(c[5], sx, -c[11])));
     float il = 1.0f / len;
     v3 d = vscl(dw, il);
     v3 o = V(c[0], c[1], c[2]);
@@ -938,7 +974,7 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
         mat_t m = load_mat(S->mats, mid);
         const float* lut = S->luts + ORC_LUT_STRIDE * (size_t)mid;
         float t = h.t;
-        v3 P = V(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+        v3 P = vmadd(o, d, t);
         v3 N = vnorm(vcross(e1, e2));
         if (vdot(N, d) > 0.0f) N = V(-N.x, -N.y, -N.z);
         v3 wo = V(-d.x, -d.y, -d.z);
@@ -975,7 +1011,7 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
                     disk(rnd(key, dim0 + 1u), rnd(key, dim0 + 2u), &dx, &dy);
                     dx = dx * radius;
                     dy = dy * radius;
-                    v3 sp = V(lp.x + b1.x * dx + b2.x * dy, lp.y + b1.y * dx + b2.y * dy, lp.z + b1.z * dx + b2.z * dy);
+                    v3 sp = vmadd(vmadd(lp, b1, dx), b2, dy);
                     v3 ts = vsub(sp, P);
                     float ds2 = vdot(ts, ts);
                     dist = sqrtf(ds2);
@@ -1019,6 +1055,17 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
                     float iq = 1.0f / q;
                     T = V(T.x * iq, T.y * iq, T.z * iq);
                 }
+            }
+        }
+        {
+            const int kb = b == 0 ? 0 : 2;
+#pragma omp atomic
+            g_rays[kb] += alive;
+#pragma omp atomic
+            g_rays[kb + 1] += shadow;
+            if (b > 0 && alive) {
+#pragma omp critical(orc_late)
+                if (g_n_late < 16) { g_late[2 * g_n_late] = pix; g_late[2 * g_n_late + 1] = sample; ++g_n_late; }
             }
         }
         if (shadow) {
@@ -1216,9 +1263,17 @@ int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* h
  * frame can be timed. threads <= 0: OpenMP default. */
 #define ORC_FILM_GROUP 32
 
+void orc_ray_counts(long long* out4, int* late32, int* n_late) {
+    for (int k = 0; k < 4; ++k) out4[k] = g_rays[k];
+    for (int k = 0; k < 2 * g_n_late; ++k) late32[k] = g_late[k];
+    *n_late = g_n_late;
+}
+
 int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const float* cam, int n_lights,
                const float* lights, const float* mats, const float* world, const int32_t* ri, const float* rf,
                float* film, uint8_t* rgba8, int row_begin, int row_end, int threads) {
+    memset(g_rays, 0, sizeof g_rays);
+    g_n_late = 0;
     lbvh B;
     lbvh_build(&B, n_tris, tris9, tri_mat, (ri[7] == 3 || ri[7] == 4) ? 3 : 2);  /* the hierarchy the product walks */
     if (ri[7] == 4) { lbvh_collapse4(&B); B.width = 4; }
