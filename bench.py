@@ -192,11 +192,14 @@ def pmc_traffic(cls: str, path: str):
     return None
 
 
-def pmc_valu(cls: str, path: str, avg_ms: float):
-    """VALU issue utilisation of the class's timed kernel from the committed PMC
-    summary: SQ_INSTS_VALU wave-instructions per launch over the launch time,
-    against 0.5 per clock per SIMD at the clock the counters saw
-    (GRBM_GUI_ACTIVE / 8 XCDs / launch time, MI355X_MICROARCH.md DVFS note)."""
+def pmc_valu(cls: str, path: str, avg_ms: float, kernel_clock_ghz: float = 0.0):
+    """VALU issue of the class's timed kernel from the committed PMC summary:
+    SQ_INSTS_VALU wave-instructions per launch over the launch time, against
+    0.5 per clock per SIMD x 1024 SIMDs at the 2.4 GHz peak engine clock (the
+    roofline peak; `frac`), and at the clock the kernel itself measured
+    (`kernel_clock_ghz`, shader-clock over real-time ticks inside k_tiles'
+    counting launch, MI355X_MICROARCH.md DVFS item 6; `issue_util_at_kernel_clock`):
+    the chip holds its clock well under 2.4 GHz under this load."""
     if not os.path.exists(path):
         return None
     with open(path) as fh:
@@ -206,17 +209,17 @@ def pmc_valu(cls: str, path: str, avg_ms: float):
             if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
                 if "SQ_INSTS_VALU" not in v or "GRBM_GUI_ACTIVE" not in v:
                     return None
-                # the effective clock of the counting pass (GRBM_GUI_ACTIVE / 8 over the
-                # same dispatches' duration, tools/pmc_summary.py), at most the
-                # 2.4 GHz peak engine clock; without it the peak clock
-                clk_ghz = min(float(v.get("clock_ghz_pmc") or PEAK_CLOCK_GHZ), PEAK_CLOCK_GHZ)
                 achieved = v["SQ_INSTS_VALU"] / (avg_ms * 1e-3)  # wave-instructions/s at the bench's launch time
-                peak = VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * clk_ghz * 1e9
-                return {"achieved": round(achieved / 1e9, 1), "peak": round(peak / 1e9, 1),
-                        "unit": "G wave-instr/s", "frac": round(achieved / peak, 3),
-                        "clock_ghz": round(clk_ghz, 3),
-                        "clock_source": "PMC pass" if v.get("clock_ghz_pmc") else "peak engine clock",
-                        "valu_per_launch": round(v["SQ_INSTS_VALU"]), "source": os.path.relpath(path, ROOT)}
+                peak = VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * PEAK_CLOCK_GHZ * 1e9
+                out = {"achieved": round(achieved / 1e9, 1), "peak": round(peak / 1e9, 1),
+                       "unit": "G wave-instr/s", "frac": round(achieved / peak, 3), "clock_ghz": PEAK_CLOCK_GHZ,
+                       "clock_source": "peak engine clock (MI355X_MICROARCH.md)",
+                       "valu_per_launch": round(v["SQ_INSTS_VALU"]), "source": os.path.relpath(path, ROOT)}
+                if kernel_clock_ghz > 0:
+                    out["kernel_clock_ghz"] = round(kernel_clock_ghz, 3)
+                    out["issue_util_at_kernel_clock"] = round(
+                        achieved / (VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * kernel_clock_ghz * 1e9), 3)
+                return out
     return None
 
 
@@ -339,7 +342,7 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names):
     wl_key = "" if args.workload == "04vs" else f"_{args.workload}"
     pmc = args.pmc_summary or newest_profile("%s_pmc" + wl_key + ".json")
     tr = pmc_traffic(cls, pmc) if pmc else None
-    valu = pmc_valu(cls, pmc, avg_ms) if pmc else None
+    valu = pmc_valu(cls, pmc, avg_ms, float(getattr(cstats, "kernel_clock_ghz", 0.0))) if pmc else None
     hbm = {"hbm_algorithmic_gbs": round(per_s(survey_frame if split else bytes_frame), 2),
            "hbm_compulsory_gbs": round(per_s(bytes_frame), 2),
            "hbm_survey_formula_gbs": round(per_s(survey_frame), 2),
@@ -356,6 +359,7 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names):
         return {**base, "bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],
                 "frac": valu["frac"], "clock_ghz": valu["clock_ghz"], "clock_source": valu["clock_source"],
                 "valu_per_launch": valu["valu_per_launch"],
+                **{k: valu[k] for k in ("kernel_clock_ghz", "issue_util_at_kernel_clock") if k in valu},
                 "valu_source": valu["source"], **hbm, "hbm_frac": round(per_s(bytes_frame) / HBM_PEAK_GBS, 4),
                 "note": "k_tiles: scene in LDS, bound by vector-instruction issue (SQ_INSTS_VALU per launch / launch "
                         "time vs 0.5 wave-instr/clk/SIMD x 1024 SIMDs); HBM sees only film + RGBA8 (hbm_frac)"}

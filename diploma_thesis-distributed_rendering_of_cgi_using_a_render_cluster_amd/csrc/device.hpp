@@ -151,7 +151,7 @@ struct DevPaths {
     DevBuf<float> lights, materials;
     DevBuf<float> mat_lut;             // material tables (build_material_lut), uploaded when they change
     std::vector<float> mat_lut_cached;
-    DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: 6 totals
+    DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: 6 totals + 2 clock tick sums
     KernelProfiler prof;
     bool count_traversal = false;
     bool force_wavefront = false;  // RR_FLAG_WAVEFRONT: LDS-resident scenes skip k_tiles

@@ -79,7 +79,7 @@ struct FrameRun {
     std::vector<int32_t> counters;
     double kernel_ms[RR_K_CLASSES];
     int32_t kernel_launches[RR_K_CLASSES];
-    unsigned long long trav[6];
+    unsigned long long trav[8];  // 6 traversal totals + k_tiles clock ticks (shader, real time)
 };
 
 // One frame between rr_frame_submit and rr_frame_complete: its host-side
@@ -525,6 +525,10 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
     for (int k = 0; k < 3; ++k) {
         st->trav_nodes[k] = r.trav[2 * k];
         st->trav_tris[k] = r.trav[2 * k + 1];
+    }
+    {
+        // k_tiles<count>: sum over waves of shader-clock and 100 MHz real-time ticks
+        st->kernel_clock_ghz = r.trav[7] ? 0.1 * (double)r.trav[6] / (double)r.trav[7] : 0.0;
     }
     st->build_ms = r.rebuilt ? r.build_ms : 0.0;
     st->trace_ms = r.trace_ms;

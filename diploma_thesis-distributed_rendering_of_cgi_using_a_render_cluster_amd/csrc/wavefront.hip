@@ -241,17 +241,21 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         add_to(L, c);
         return;
     }
-    const TriPack tp = load_tri(v.tris, h.idx);
-    const int mid = f2i(tp.p1.w);
+    int mid;
+    float3 N;
+    if constexpr (std::is_same<View, LdsView>::value) {
+        const float4 nm = lds_ld4(v.nrm + h.idx);  // staged: norm3(cross3(e1, e2)), material id
+        N = xyz(nm);
+        mid = f2i(nm.w);
+    } else {
+        const TriPack tp = load_tri(v.tris, h.idx);
+        mid = f2i(tp.p1.w);
+        N = norm3(cross3(xyz(tp.p1), xyz(tp.p2)));
+    }
     const Mat m = view_mat(v, mid);
     const auto lut = v.lut + kMatLutStride * mid;
     const float t = h.t;
     const float3 P = madd3(o, d, t);
-    float3 N;
-    if constexpr (std::is_same<View, LdsView>::value)
-        N = xyz(lds_ld4(v.nrm + h.idx));  // staged: norm3(cross3(e1, e2))
-    else
-        N = norm3(cross3(xyz(tp.p1), xyz(tp.p2)));
     if (dot3(N, d) > 0.0f) N = mk3(-N.x, -N.y, -N.z);
     const float3 wo = mk3(-d.x, -d.y, -d.z);
     if (m.emission.x != 0.0f || m.emission.y != 0.0f || m.emission.z != 0.0f) {
@@ -602,13 +606,13 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
         q += kMatLutStride / 4 * a.n_mats;
     }
     if (shading || kCam) __syncthreads();  // the copies above are visible
-    if (shading) {  // per-triangle unit normals
+    if (shading) {  // per-triangle unit normals and material ids (shade() reads no TriPack)
         v.nrm = q;
         for (int i = threadIdx.x; i < a.n_tris; i += kBlock) {
             const TriPack tp = load_tri(v.tris, i);
             const float3 n = norm3(cross3(xyz(tp.p1), xyz(tp.p2)));
             rr_f4v x;
-            x.x = n.x; x.y = n.y; x.z = n.z; x.w = 0.0f;
+            x.x = n.x; x.y = n.y; x.z = n.z; x.w = tp.p1.w;
             q[i] = x;
         }
         q += a.n_tris;
@@ -1644,6 +1648,14 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
                      const TileSlices sl) {
     const int stride = gridDim.x * kBlock;
+    // counting instantiation only: the wave's shader-clock and real-time
+    // counters at start and end give the clock the kernel ran at (read-only
+    // counters; the timed instantiation executes none of this)
+    unsigned long long clk0 = 0, rt0 = 0;
+    if (kCount) {
+        clk0 = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+    }
     TravStack st{stack, spill, stride, 0};
     TravCount cp, ce, cs;
     uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0, n_t0 = 0;
@@ -1786,6 +1798,11 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         flush_counts(tc, 0, cp.nodes, cp.tris);
         flush_counts(tc, 2, ce.nodes, ce.tris);
         flush_counts(tc, 4, cs.nodes, cs.tris);
+        const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&tc[6], clk1 - clk0);
+            atomicAdd(&tc[7], rt1 - rt0);
+        }
     }
 }
 
@@ -2210,8 +2227,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * n_ctr, st));
         unsigned long long* tc = nullptr;
         if (p.count_traversal) {
-            p.trav_counts.ensure(6);
-            RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 6 * sizeof(unsigned long long), st));
+            p.trav_counts.ensure(8);
+            RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 8 * sizeof(unsigned long long), st));
             tc = p.trav_counts.ptr;
         }
         const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
@@ -2247,8 +2264,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
     unsigned long long* tc = nullptr;
     if (p.count_traversal) {
-        p.trav_counts.ensure(6);
-        RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 6 * sizeof(unsigned long long), st));
+        p.trav_counts.ensure(8);
+        RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 8 * sizeof(unsigned long long), st));
         tc = p.trav_counts.ptr;
     }
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 2
+#define RR_ABI_VERSION 3
 
 /* error codes (negative errno values) */
 #define RR_OK 0
@@ -133,6 +133,11 @@ typedef struct rr_frame_stats {
     uint64_t camera_rays_traced;
     int32_t view_transform;            /* RR_VIEW_* the frame was rendered with */
     int32_t view_transform_substituted;/* 1: the scene asked for Filmic, no LUTs were configured, Standard used */
+    /* RR_FLAG_COUNT_TRAVERSAL, LDS-resident scenes: the shader clock the tile
+     * kernel ran at, in GHz, measured inside it (shader-clock ticks over the
+     * 100 MHz real-time counter across each wave's lifetime, summed over waves);
+     * 0 when not measured */
+    double kernel_clock_ghz;
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */

@@ -930,7 +930,7 @@ static mat_t load_mat(const float* mats, int id) {
 static long long g_rays[4];
 static int g_late[32], g_n_late;
 
-static v3 radiance(const scene_t* S, int pix, int sample) {
+static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
     const float* c = S->cam;
     uint32_t key = pkey(S->seed, (uint32_t)pix, (uint32_t)sample);
     int px = pix % S->W, py = pix / S->W;
@@ -1059,10 +1059,8 @@ static v3 radiance(const scene_t* S, int pix, int sample) {
         }
         {
             const int kb = b == 0 ? 0 : 2;
-#pragma omp atomic
-            g_rays[kb] += alive;
-#pragma omp atomic
-            g_rays[kb + 1] += shadow;
+            rays[kb] += alive;  /* per row, summed after the row (orc_render) */
+            rays[kb + 1] += shadow;
             if (b > 0 && alive) {
 #pragma omp critical(orc_late)
                 if (g_n_late < 16) { g_late[2 * g_n_late] = pix; g_late[2 * g_n_late + 1] = sample; ++g_n_late; }
@@ -1313,6 +1311,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
 #pragma omp parallel for schedule(dynamic, 1)
 #endif
     for (int y = row_begin; y < row_end; ++y) {
+        long long rays[4] = {0, 0, 0, 0};
         for (int x = 0; x < S->W; ++x) {
             int pix = y * S->W + x;
             /* film sum order (the product's kFilmGroup, csrc/wavefront.hip): in
@@ -1322,7 +1321,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
                 v3 P = V(0.0f, 0.0f, 0.0f);
                 const int g1 = g0 + ORC_FILM_GROUP < S->spp ? g0 + ORC_FILM_GROUP : S->spp;
                 for (int s = g0; s < g1; ++s) {
-                    v3 L = radiance(S, pix, s);
+                    v3 L = radiance(S, pix, s, rays);
                     P.x = P.x + L.x;
                     P.y = P.y + L.y;
                     P.z = P.z + L.z;
@@ -1350,6 +1349,10 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
                 }
                 rgba8[4 * (size_t)pix + 3] = 255;
             }
+        }
+        for (int k = 0; k < 4; ++k) {
+#pragma omp atomic
+            g_rays[k] += rays[k];
         }
     }
     free(S->luts);
