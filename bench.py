@@ -360,6 +360,7 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names):
                 "frac": valu["frac"], "clock_ghz": valu["clock_ghz"], "clock_source": valu["clock_source"],
                 "valu_per_launch": valu["valu_per_launch"],
                 **{k: valu[k] for k in ("kernel_clock_ghz", "issue_util_at_kernel_clock") if k in valu},
+                "wave_fill": round(float(getattr(cstats, "kernel_wave_fill", 0.0)), 3),
                 "valu_source": valu["source"], **hbm, "hbm_frac": round(per_s(bytes_frame) / HBM_PEAK_GBS, 4),
                 "note": "k_tiles: scene in LDS, bound by vector-instruction issue (SQ_INSTS_VALU per launch / launch "
                         "time vs 0.5 wave-instr/clk/SIMD x 1024 SIMDs); HBM sees only film + RGBA8 (hbm_frac)"}

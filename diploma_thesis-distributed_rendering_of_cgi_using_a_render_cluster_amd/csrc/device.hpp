@@ -151,7 +151,7 @@ struct DevPaths {
     DevBuf<float> lights, materials;
     DevBuf<float> mat_lut;             // material tables (build_material_lut), uploaded when they change
     std::vector<float> mat_lut_cached;
-    DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: 6 totals + 2 clock tick sums
+    DevBuf<unsigned long long> trav_counts;  // RR_FLAG_COUNT_TRAVERSAL: kTravWords
     KernelProfiler prof;
     bool count_traversal = false;
     bool force_wavefront = false;  // RR_FLAG_WAVEFRONT: LDS-resident scenes skip k_tiles
@@ -195,6 +195,11 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof = nullptr, boo
 // behind posted writes): measured 112 us per frame on 04vs. Kernel arguments
 // are written by the host into device memory, so nothing waits.
 constexpr int kUploadMax = 720;
+// RR_FLAG_COUNT_TRAVERSAL words: [0..5] traversal totals (nodes, triangles per
+// class); k_tiles' counting launch: [6] shader-clock ticks and [7] real-time
+// ticks after the scene staging, [8] waves, [9] real-time ticks from entry,
+// [10] ~first entry, [11] last end (rr_api.cpp fill_stats)
+constexpr int kTravWords = 12;
 struct UploadSeg {
     float* dst;
     int n;

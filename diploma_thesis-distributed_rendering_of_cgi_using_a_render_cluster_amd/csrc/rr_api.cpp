@@ -79,7 +79,7 @@ struct FrameRun {
     std::vector<int32_t> counters;
     double kernel_ms[RR_K_CLASSES];
     int32_t kernel_launches[RR_K_CLASSES];
-    unsigned long long trav[8];  // 6 traversal totals + k_tiles clock ticks (shader, real time)
+    unsigned long long trav[kTravWords];
 };
 
 // One frame between rr_frame_submit and rr_frame_complete: its host-side
@@ -527,8 +527,11 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
         st->trav_tris[k] = r.trav[2 * k + 1];
     }
     {
-        // k_tiles<count>: sum over waves of shader-clock and 100 MHz real-time ticks
-        st->kernel_clock_ghz = r.trav[7] ? 0.1 * (double)r.trav[6] / (double)r.trav[7] : 0.0;
+        // k_tiles<count>: sums over waves of shader-clock and 100 MHz real-time ticks
+        const unsigned long long* w = r.trav;
+        st->kernel_clock_ghz = w[7] ? 0.1 * (double)w[6] / (double)w[7] : 0.0;
+        const unsigned long long t0 = ~w[10], t1 = w[11];
+        st->kernel_wave_fill = (w[8] && t1 > t0) ? (double)w[9] / (double)w[8] / (double)(t1 - t0) : 0.0;
     }
     st->build_ms = r.rebuilt ? r.build_ms : 0.0;
     st->trace_ms = r.trace_ms;

@@ -1646,7 +1646,7 @@ template <bool kCount>
 RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
                      const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
-                     const TileSlices sl) {
+                     const TileSlices sl, unsigned long long rt_entry) {
     const int stride = gridDim.x * kBlock;
     // counting instantiation only: the wave's shader-clock and real-time
     // counters at start and end give the clock the kernel ran at (read-only
@@ -1799,9 +1799,13 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         flush_counts(tc, 2, ce.nodes, ce.tris);
         flush_counts(tc, 4, cs.nodes, cs.tris);
         const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-        if ((threadIdx.x & 63) == 0) {
+        if ((threadIdx.x & 63) == 0) {  // device.hpp kTravWords
             atomicAdd(&tc[6], clk1 - clk0);
             atomicAdd(&tc[7], rt1 - rt0);
+            atomicAdd(&tc[8], 1ull);
+            atomicAdd(&tc[9], rt1 - rt_entry);
+            atomicMax(&tc[10], ~rt_entry);  // the first entry, complemented (the words start at 0)
+            atomicMax(&tc[11], rt1);
         }
     }
 }
@@ -1819,12 +1823,13 @@ __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc
                                                                   int32_t* __restrict__ spill,
                                                                   unsigned long long* __restrict__ tc,
                                                                   TileSlices sl) {
+    const unsigned long long rt_entry = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ int lds_stack[kLdsStack * kBlock];
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(lds_stack);
     int used;
     const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
-    tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl);
+    tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry);
 }
 
 #endif  // RR_TILES_TU
@@ -2227,8 +2232,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * n_ctr, st));
         unsigned long long* tc = nullptr;
         if (p.count_traversal) {
-            p.trav_counts.ensure(8);
-            RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 8 * sizeof(unsigned long long), st));
+            p.trav_counts.ensure(kTravWords);
+            RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, kTravWords * sizeof(unsigned long long), st));
             tc = p.trav_counts.ptr;
         }
         const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
@@ -2264,8 +2269,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
     unsigned long long* tc = nullptr;
     if (p.count_traversal) {
-        p.trav_counts.ensure(8);
-        RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, 8 * sizeof(unsigned long long), st));
+        p.trav_counts.ensure(kTravWords);
+        RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, kTravWords * sizeof(unsigned long long), st));
         tc = p.trav_counts.ptr;
     }
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};

@@ -58,7 +58,8 @@ class FrameStats(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double * 8), ("kernel_launches", ctypes.c_int32 * 8),
                 ("trav_nodes", ctypes.c_uint64 * 3), ("trav_tris", ctypes.c_uint64 * 3),
                 ("camera_rays_traced", ctypes.c_uint64), ("view_transform", ctypes.c_int32),
-                ("view_transform_substituted", ctypes.c_int32), ("kernel_clock_ghz", ctypes.c_double)]
+                ("view_transform_substituted", ctypes.c_int32), ("kernel_clock_ghz", ctypes.c_double),
+                ("kernel_wave_fill", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         out = {}

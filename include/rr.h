@@ -138,6 +138,10 @@ typedef struct rr_frame_stats {
      * 100 MHz real-time counter across each wave's lifetime, summed over waves);
      * 0 when not measured */
     double kernel_clock_ghz;
+    /* same launch: the waves' mean lifetime over the launch's span (first wave
+     * start to last wave end), i.e. how full the persistent grid stayed; 0
+     * when not measured */
+    double kernel_wave_fill;
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */
