@@ -145,6 +145,8 @@ struct DevPaths {
     DevBuf<float4> film_part;  // open sample group's partial sum between chunks (k_accumulate)
     DevBuf<float> tile_slab;   // k_tiles: per sliced tile, one group sum plane per sample group
     DevBuf<uint32_t> tile_ctrs;  // k_tiles: work-unit counters, one 128-B line per shard
+    DevBuf<uint32_t> tile_cost;  // k_tiles: per screen tile, the real-time ticks its units took (last launch)
+    DevBuf<int32_t> tile_order;  // k_tiles: box tiles by descending tile_cost (k_tile_order)
     DevBuf<uint8_t> rgba8;
     DevBuf<float> filter_table;
     DevBuf<float> srgb_lut;

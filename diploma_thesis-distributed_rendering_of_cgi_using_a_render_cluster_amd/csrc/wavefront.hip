@@ -1634,6 +1634,8 @@ struct TileSlices {
     int n;             // slices per box tile = sample groups (1: no slicing)
     size_t floats;     // slab floats per tile: 192 * groups
     float* slab;
+    const int32_t* order;  // box tiles in hand-out order (k_tile_order)
+    uint32_t* cost;        // per screen tile: real-time ticks of its units, for the next launch's order
 };
 using TilesFn = void (*)(FrameConsts, SceneArgs, uint32_t*, float4*, const float*, uchar4*, uint32_t*, int32_t*,
                          unsigned long long*, TileSlices);
@@ -1678,24 +1680,24 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     const int ng = (fc.spp_total + kFilmGroup - 1) / kFilmGroup;
     const int nb = to.bw * to.bh;
     const int n_sliced = nb * sl.n;
-    const int nwaves = (int)(gridDim.x * kWavesPerBlock);
+    const int n_units = n_sliced + (to.n - nb);  // box slices, then one unit per background tile
     const int n_shards = min((int)gridDim.x, kTileShards);  // small frames launch fewer blocks than shards
     const int shard = (int)blockIdx.x % n_shards;
-    int a_next = nb + (int)wave_id();  // this wave's next background tile (static)
     for (;;) {
         int t, k = 0, nk = 1;  // tile, slice, slices of this tile
-        if (a_next < to.n) {
-            t = a_next;
-            a_next += nwaves;
-        } else {
-            int u = 0;
-            if (lane == 0) u = (int)atomicAdd(tile_ctr + shard * kTileCtrStride, 1u);
-            u = __builtin_amdgcn_readlane(u, 0) * n_shards + shard;
-            if (u >= n_sliced) break;
-            t = u / sl.n;
-            k = u - t * sl.n;
+        int u = 0;
+        if (lane == 0) u = (int)atomicAdd(tile_ctr + shard * kTileCtrStride, 1u);
+        u = __builtin_amdgcn_readlane(u, 0) * n_shards + shard;
+        if (u >= n_units) break;
+        if (u < n_sliced) {  // box tiles in the order of k_tile_order (the heaviest first)
+            const int j = u / sl.n;
+            k = u - j * sl.n;
             nk = sl.n;
+            t = uniform_i(sl.order[j]);
+        } else {  // background tiles (the world term) fill the end of the launch
+            t = nb + (u - n_sliced);
         }
+        const unsigned long long u_start = __builtin_amdgcn_s_memrealtime();
         int tx, ty;
         to.at(t, tx, ty);
         const int px = tx * kTile + (lane & (kTile - 1)), py = ty * kTile + (lane >> 3);
@@ -1786,12 +1788,12 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             slab[lane] = acc.x;
             slab[64 + lane] = acc.y;
             slab[128 + lane] = acc.z;
-            continue;
-        }
-        if (valid) {
+        } else if (valid) {
             film[pix] = acc;
             out[pix] = tonemap(fc, acc, srgb);
         }
+        if (lane == 0)  // this unit's time, for the next launch's hand-out order (k_tile_order)
+            atomicAdd(&sl.cost[ty * to.tx + tx], (uint32_t)(__builtin_amdgcn_s_memrealtime() - u_start));
     }
     flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tot + camera_traced_slot(fc.max_bounces), n_t0);
     if (kCount) {
@@ -1833,6 +1835,60 @@ __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc
 }
 
 #endif  // RR_TILES_TU
+
+// Hand-out order of k_tiles' box tiles (longest processing time first): the
+// tiles of this frame's box sorted by the time their units took in the
+// previous launch at the same screen tile (descending, over 128 log-spaced
+// buckets; the order inside a bucket is arbitrary), so the heaviest units start
+// first and the light rim and background units fill the end of the launch. On
+// 04vs the heaviest tiles lie on the box's rim rows (the lit faces), which the
+// box's row order handed out last, and the launch ended with those units
+// running on a nearly empty chip. Scheduling only: every unit computes the
+// same bits in any order. The same single-workgroup launch zeroes the costs
+// for the coming launch, the unit counters and the ray counters.
+constexpr int kOrderBuckets = 128;
+constexpr int kOrderThreads = 1024;
+RR_D int cost_bucket(uint32_t c) {
+    if (c < 4u) return (int)c;
+    const int e = 31 - __builtin_clz(c);
+    return min(kOrderBuckets - 1, 4 * e + (int)((c >> (e - 2)) & 3u));
+}
+__global__ __launch_bounds__(kOrderThreads) void k_tile_order(FrameConsts fc, const BvhNode* __restrict__ nodes,
+                                                              uint32_t* __restrict__ cost, int32_t* __restrict__ order,
+                                                              uint32_t* __restrict__ tile_ctr,
+                                                              uint32_t* __restrict__ ray_ctr, int n_ray_ctr) {
+    __shared__ uint32_t cnt[kOrderBuckets];
+    const int tid = threadIdx.x;
+    const ScreenCull cull = screen_cull(fc, nodes);
+    const TileOrder to = tile_order(fc, cull);
+    const int nb = to.bw * to.bh;
+    for (int i = tid; i < kOrderBuckets; i += kOrderThreads) cnt[i] = 0u;
+    for (int i = tid; i < kTileShards * kTileCtrStride; i += kOrderThreads) tile_ctr[i] = 0u;
+    for (int i = tid; i < n_ray_ctr; i += kOrderThreads) ray_ctr[i] = 0u;
+    __syncthreads();
+    for (int t = tid; t < nb; t += kOrderThreads) {
+        int x, y;
+        to.at(t, x, y);
+        atomicAdd(&cnt[cost_bucket(cost[y * to.tx + x])], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {  // bucket starts, the heaviest bucket first
+        uint32_t run = 0;
+        for (int b = kOrderBuckets - 1; b >= 0; --b) {
+            const uint32_t c = cnt[b];
+            cnt[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < nb; t += kOrderThreads) {
+        int x, y;
+        to.at(t, x, y);
+        order[atomicAdd(&cnt[cost_bucket(cost[y * to.tx + x])], 1u)] = t;
+    }
+    __syncthreads();
+    for (int i = tid; i < to.n; i += kOrderThreads) cost[i] = 0u;
+}
 
 // Film of the sliced tiles: the group sums of each box tile that is not
 // culled, added in group order (the same box and culling test as k_tiles,
@@ -2138,7 +2194,7 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
-    counters.release(); tile_ctrs.release(); spill.release(); tile_slab.release(); film_part.release(); segs.release(); hits.release(); qctr.release();
+    counters.release(); tile_ctrs.release(); tile_cost.release(); tile_order.release(); spill.release(); tile_slab.release(); film_part.release(); segs.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     mat_lut.release();
     mat_lut_cached.clear();
@@ -2228,8 +2284,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         const int cpc = counters_per_chunk(base.max_bounces);
         const long tiles = (long)((base.W + 7) / 8) * ((base.H + 7) / 8);
         const size_t n_ctr = (size_t)cpc * n_chunks;
-        p.counters.ensure(n_ctr);
-        RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * n_ctr, st));
+        p.counters.ensure(n_ctr);  // zeroed by k_tile_order
         unsigned long long* tc = nullptr;
         if (p.count_traversal) {
             p.trav_counts.ensure(kTravWords);
@@ -2242,7 +2297,13 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         fc.first_sample = 0;
         fc.spp_chunk = base.spp_total;
         uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr);
-        TileSlices sl{film_groups(base.spp_total), (size_t)192 * film_groups(base.spp_total), nullptr};
+        if (p.tile_cost.cap < (size_t)tiles) {  // costs of a new size start at 0 (the first order is the box's)
+            p.tile_cost.ensure((size_t)tiles);
+            RR_HIP(hipMemsetAsync(p.tile_cost.ptr, 0, sizeof(uint32_t) * tiles, st));
+        }
+        p.tile_order.ensure((size_t)tiles);
+        TileSlices sl{film_groups(base.spp_total), (size_t)192 * film_groups(base.spp_total), nullptr,
+                      p.tile_order.ptr, p.tile_cost.ptr};
         if (sl.n > 1) {
             p.tile_slab.ensure(sl.floats * (size_t)tiles);
             sl.slab = p.tile_slab.ptr;
@@ -2250,7 +2311,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         const int g = clamp_grid(tiles * 64, G.tiles);
         p.prof.begin(st, RR_K_TILES);
         p.tile_ctrs.ensure((size_t)kTileShards * kTileCtrStride);
-        RR_HIP(hipMemsetAsync(p.tile_ctrs.ptr, 0, sizeof(uint32_t) * kTileShards * kTileCtrStride, st));
+        k_tile_order<<<1, kOrderThreads, 0, st>>>(fc, s.nodes.ptr, p.tile_cost.ptr, p.tile_order.ptr, p.tile_ctrs.ptr,
+                                                  reinterpret_cast<uint32_t*>(p.counters.ptr), (int)n_ctr);
         G.kx<<<g, kBlock, G.dyn_primary, st>>>(fc, sa, p.tile_ctrs.ptr, p.film.ptr, p.srgb_lut.ptr,
                                                reinterpret_cast<uchar4*>(p.rgba8.ptr), tot, p.spill.ptr, tc, sl);
         if (sl.n > 1)
