@@ -11,8 +11,10 @@ write. Frames are independent; each rank (one per GPU) renders its own frames
 Timed region: barrier + device sync on both sides, max over ranks (the only
 cross-rank exchange, over gloo: frames are independent, there is no data-path
 collective and no RCCL). Per-kernel device times come from HIP events recorded
-by the library on its own stream around every launch during the timed steps
-(RR_FLAG_PROFILE_KERNELS). Traversal counts for the algorithmic-byte model
+by the library on its own stream around every launch (RR_FLAG_PROFILE_KERNELS):
+during the timed steps, or — when consecutive k_tiles frames overlap on the
+device in the timed steps — over frames rendered one at a time right after it
+(roofline.launch_timing says which). Traversal counts for the algorithmic-byte model
 come from one extra counting frame after the timed region
 (RR_FLAG_COUNT_TRAVERSAL).
 
@@ -317,7 +319,11 @@ def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin 
                       f"{t_used:.1f} s, extrapolated to whole frames; render only (no encode)"}
 
 
-def roofline_line(args, cls, cstats, kernel_ms, launches, names):
+def names_idx(cls: str, rr) -> int:
+    return list(rr.native.KERNEL_CLASSES).index(cls)
+
+
+def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps):
     """The dominant kernel class against the roofline that actually bounds it
     (DESIGN.md §6):
       * LDS-resident scenes (k_tiles, 04vs / 01): VALU issue. The scene lives
@@ -336,7 +342,7 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names):
     scene_bytes = 64.0 * max(n - 1, 1) + 48.0 * n
     split = launches[5] > 0
     bytes_frame, survey_frame = algorithmic_bytes(cls, cstats, scene_bytes, split)
-    launches_frame = max(launches[dom] / max(args.steps, 1), 1)
+    launches_frame = max(launches[dom] / max(steps, 1), 1)
     avg_ms = kernel_ms[dom] / max(launches[dom], 1)
     per_s = lambda b: b / launches_frame / (avg_ms * 1e-3) / 1e9  # noqa: E731
     wl_key = "" if args.workload == "04vs" else f"_{args.workload}"
@@ -478,6 +484,24 @@ def main():
     last_stats = runner.last_stats
     t_max = reduce_max_seconds(elapsed, dist)
 
+    # Per-launch kernel times for the roofline. When consecutive k_tiles frames
+    # overlap on the device (the two frame slots' streams, rr_api.cpp
+    # enqueue_frame), an event pair around a launch also spans the wait for the
+    # CUs the previous frame still holds; so those frames are timed again one at
+    # a time after the timed region (rr_render_frame: nothing else in flight),
+    # the same HIP events around the same launches. Frames of other paths never
+    # overlap, and their timed-region events are used as they are.
+    solo = not args.serial and launches[names_idx("tiles", rr)] > 0
+    roof_ms, roof_launches, roof_steps = kernel_ms, launches, args.steps
+    if solo:
+        roof_ms, roof_launches = [0.0] * 8, [0] * 8
+        roof_steps = min(args.steps, 10)
+        for i in range(roof_steps):  # spread over the timed steps' frames
+            runner.render_frame(job, frame_of(args.warmup + i * args.steps // roof_steps))
+            for k in range(8):
+                roof_ms[k] += runner.last_stats.kernel_ms[k]
+                roof_launches[k] += runner.last_stats.kernel_launches[k]
+
     # traversal counts for the byte model: one counting frame, outside the timed region
     scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, ROOT))
     f_count = frame_of(args.warmup)
@@ -489,10 +513,18 @@ def main():
         value = total_frames / t_max
         names = rr.native.KERNEL_CLASSES
         per_class = {names[k]: {"ms_total": kernel_ms[k], "launches": launches[k]} for k in range(len(names))}
+        if solo:
+            per_class = {names[k]: {"ms_total": roof_ms[k], "launches": roof_launches[k],
+                                    "timed_region_event_ms_total": kernel_ms[k]} for k in range(len(names))}
         roofline = None
         if not args.no_profile:
-            dom = max(range(len(names)), key=lambda k: kernel_ms[k])
-            roofline = roofline_line(args, names[dom], cstats, kernel_ms, launches, names)
+            dom = max(range(len(names)), key=lambda k: roof_ms[k])
+            roofline = roofline_line(args, names[dom], cstats, roof_ms, roof_launches, names, roof_steps)
+            roofline["launch_timing"] = (
+                f"HIP events around each launch on the library's stream, {roof_steps} frames rendered one at a "
+                "time after the timed region (in the timed region consecutive k_tiles frames overlap on the "
+                "device, and an event pair would also span the wait for the previous frame's CUs)" if solo else
+                "HIP events around each launch on the library's stream over the timed region")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -523,10 +555,12 @@ def main():
                        "view_transform_substituted": int(any(substituted))},
             "mrays_per_s_per_gpu": round(traced / elapsed / 1e6, 1),
             # SURVEY 8(d)'s form: rays traced over the summed render-kernel time
-            "mrays_per_s_per_gpu_kernel_time": (round(traced / (sum(kernel_ms) * 1e-3) / 1e6, 1)
-                                                if sum(kernel_ms) > 0 else None),
+            # (kernels timed alone, see roofline.launch_timing)
+            "mrays_per_s_per_gpu_kernel_time": (
+                round(traced / args.steps / (sum(roof_ms) / max(roof_steps, 1) * 1e-3) / 1e6, 1)
+                if sum(roof_ms) > 0 else None),
             "rays_per_frame": {k: v // max(args.steps, 1) for k, v in rays.items()},
-            "device_ms_per_frame": round(sum(kernel_ms) / max(args.steps, 1), 3),
+            "device_ms_per_frame": round(sum(roof_ms) / max(roof_steps, 1), 3),
             "kernels": per_class,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -212,6 +212,11 @@ bool upload_by_kernarg(const float* src, const UploadSeg* segs, int nseg, hipStr
 // scene of these sizes; otherwise the split path over the BVH4 in HBM.
 bool scene_in_lds(int n_tris, int n_mats, int n_lights);
 
+// Whether render_frame_device renders this frame with k_tiles (one launch over
+// all samples; LDS-resident scene). Such a frame touches only per-frame-slot
+// buffers and read-only tables, so it may run beside the other slot's frame.
+bool frame_uses_tiles(const FrameConsts& base, bool force_wavefront);
+
 // Render all chunks of one frame: film accumulate + tonemap to rgba8.
 // counters_per_chunk receives the device counter layout for stats.
 void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int n_chunks,

@@ -115,10 +115,43 @@ struct FrameSlot {
     rr_frame_timing tm{};
     double anim_ms = 0.0;
     std::chrono::steady_clock::time_point t_call;
+    // Device state private to this slot, swapped in while its frame is enqueued
+    // (SlotSwap), so that a k_tiles frame can run on the GPU beside the other
+    // slot's frame: the slot's own stream, the small per-frame buffers of
+    // DevPaths and of the JPEG coder, and the per-frame products of its scene's
+    // hierarchy build (`alt`: everything in DevScene but the uploaded
+    // triangles, for the scene `alt_scene`).
+    hipStream_t stream = nullptr;
+    bool tiles = false;  // this frame renders with k_tiles (may overlap its neighbours)
+    DevBuf<float> lights, materials, tile_slab;
+    DevBuf<uint32_t> tile_ctrs, tile_cost;
+    DevBuf<int32_t> tile_order, spill;
+    DevBuf<unsigned long long> trav_counts;
+    DevBuf<uint32_t> jpeg_blk, jpeg_scratch;
+    DevScene alt;
+    const rr_scene* alt_scene = nullptr;
+    void release_private() {
+        lights.release();
+        materials.release();
+        tile_slab.release();
+        tile_ctrs.release();
+        tile_cost.release();
+        tile_order.release();
+        spill.release();
+        trav_counts.release();
+        jpeg_blk.release();
+        jpeg_scratch.release();
+        alt.release();
+        alt = DevScene{};
+        alt_scene = nullptr;
+    }
 };
 
 struct rr_ctx {
     int device = 0;
+    // the compute stream the device code enqueues on: slot 0's stream outside
+    // frames (inspection entry points), the frame slot's stream while a frame is
+    // enqueued (enqueue_frame SlotSwap)
     hipStream_t stream = nullptr;
     // device-to-host copies of a frame's outputs run here, so the next frame's
     // kernels on `stream` do not wait for them (the output buffers are per
@@ -138,6 +171,7 @@ struct rr_ctx {
     FrameSlot slots[RR_MAX_FRAMES_IN_FLIGHT];
     uint64_t next_ticket = 1;     // tickets are issued in submission order
     uint64_t next_complete = 1;   // the ticket rr_frame_complete expects next
+    FrameSlot* last_enqueued = nullptr;  // the slot of the frame enqueued last (its ev[2]: device work done)
     // UNIX-time estimate of when the compute stream finished the last completed
     // frame (rr_frame_complete): the next frame's device work cannot start before
     double gpu_free_at = 0.0;
@@ -168,6 +202,36 @@ int guarded(F&& f) {
 }
 
 void set_device(rr_ctx* c) { RR_HIP(hipSetDevice(c->device)); }
+
+// Waits for every compute stream of the context (the home stream and both
+// slots'; while a frame is enqueued its slot stream sits in c->stream). Called
+// before a table that all frames read (filter, sRGB, material, JPEG, Filmic)
+// is rewritten, since a frame of the other slot may still be reading it.
+void quiesce(rr_ctx* c) {
+    RR_HIP(hipStreamSynchronize(c->stream));
+    for (auto& sl : c->slots)
+        if (sl.stream) RR_HIP(hipStreamSynchronize(sl.stream));
+}
+
+// Frames of the two slots overlap on the device when both render with k_tiles
+// (RR_TUNE_OVERLAP=0: every frame waits for the one before, as on one stream).
+bool overlap_enabled() {
+    static const bool on = !(getenv("RR_TUNE_OVERLAP") && atoi(getenv("RR_TUNE_OVERLAP")) == 0);
+    return on;
+}
+
+// Exchanges the per-frame products of a scene's hierarchy build (transforms,
+// world triangles, build scratch, nodes, packed triangles, cache state) between
+// the scene and a slot's private set; the uploaded object-space triangles stay.
+void swap_products(DevScene& home, DevScene& alt) {
+    std::swap(home, alt);
+    std::swap(home.tri_local, alt.tri_local);
+    std::swap(home.tri_obj, alt.tri_obj);
+    std::swap(home.tri_mat, alt.tri_mat);
+    std::swap(home.n_tris, alt.n_tris);
+    std::swap(home.n_objs, alt.n_objs);
+    std::swap(home.uploaded, alt.uploaded);
+}
 
 // One-time upload of the scene's object-space triangles.
 void upload_scene(rr_ctx* c, rr_scene* s) {
@@ -223,6 +287,7 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     DevPaths& p = c->paths;
     // tables (built on the host once; identical construction in the oracle)
     if (c->filter_width_cached != fs.filter_width) {
+        quiesce(c);
         c->filter_cache.assign(kFilterTableSize, 0.f);
         build_filter_table(fs.filter_width, c->filter_cache.data());
         p.filter_table.ensure(kFilterTableSize);
@@ -231,6 +296,7 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
         c->filter_width_cached = fs.filter_width;
     }
     if (!c->srgb_uploaded) {
+        quiesce(c);
         std::vector<float> lut(kSrgbLutSize + 1);
         build_srgb_lut(lut.data());
         p.srgb_lut.ensure(lut.size());
@@ -238,6 +304,7 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
         c->srgb_uploaded = true;
     }
     if (p.mat_lut_cached != fs.mat_lut) {  // material tables: static per scene, uploaded when they change
+        quiesce(c);
         p.mat_lut.ensure(fs.mat_lut.size());
         RR_HIP(hipMemcpyAsync(p.mat_lut.ptr, fs.mat_lut.data(), fs.mat_lut.size() * sizeof(float),
                               hipMemcpyHostToDevice, st));
@@ -338,6 +405,7 @@ bool device_entropy_enabled() {
 // Huffman coding) into the slot's pinned stream buffer, on the context stream.
 void enqueue_jpeg_device(rr_ctx* c, FrameSlot& sl, const uint8_t* d_rgba, int W, int H, const float* d_tab) {
     if (!c->jpeg_huff.ptr) {
+        quiesce(c);
         uint32_t h[4 * 256];
         jpeg_huff_tables(h);
         c->jpeg_huff.ensure(4 * 256);
@@ -380,9 +448,47 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     r = FrameRun{};
     r.W = fs.W;
     r.H = fs.H;
-    hipStream_t st = c->stream;
     for (auto& e : sl.ev)
         if (!e) RR_HIP(hipEventCreate(&e));
+    if (sl.alt_scene != s) {  // products of another scene (or none): start this scene's set afresh
+        sl.alt.release();
+        sl.alt = DevScene{};
+        sl.alt_scene = s;
+    }
+    // This frame runs on its slot's stream with the slot's private buffers
+    // swapped in (the other slot's frame may still be running). A k_tiles frame
+    // following a k_tiles frame does not wait for it: k_tiles and its helper
+    // kernels touch only slot buffers and read-only tables, so frame N+1's
+    // build and launch fill the CUs that frame N's tail and its JPEG kernels
+    // leave idle. Any other frame shares the wavefront queues of DevPaths and
+    // waits for the previous frame's device work.
+    struct SlotSwap {
+        rr_ctx* c;
+        FrameSlot& sl;
+        void swap() {
+            DevPaths& p = c->paths;
+            std::swap(c->stream, sl.stream);
+            std::swap(p.lights, sl.lights);
+            std::swap(p.materials, sl.materials);
+            std::swap(p.tile_slab, sl.tile_slab);
+            std::swap(p.tile_ctrs, sl.tile_ctrs);
+            std::swap(p.tile_cost, sl.tile_cost);
+            std::swap(p.tile_order, sl.tile_order);
+            std::swap(p.spill, sl.spill);
+            std::swap(p.trav_counts, sl.trav_counts);
+            std::swap(c->jpeg_blk, sl.jpeg_blk);
+            std::swap(c->jpeg_scratch, sl.jpeg_scratch);
+            swap_products(sl.scene->dev, sl.alt);
+        }
+        SlotSwap(rr_ctx* c_, FrameSlot& s_) : c(c_), sl(s_) { swap(); }
+        ~SlotSwap() { swap(); }
+    } slot_swap(c, sl);
+    hipStream_t st = c->stream;
+    sl.tiles = frame_uses_tiles(make_consts(fs, s->dev.n_tris), (fs.flags & RR_FLAG_WAVEFRONT) != 0);
+    FrameSlot* prev = c->last_enqueued;
+    if (prev && prev != &sl && !(overlap_enabled() && sl.tiles && prev->tiles))
+        RR_HIP(hipStreamWaitEvent(st, prev->ev[2], 0));
+    c->last_enqueued = &sl;
     sl.prof.reset((fs.flags & RR_FLAG_PROFILE_KERNELS) != 0);
     struct ProfSwap {  // the device code records into paths.prof; swapped back on every exit
         KernelProfiler &a, &b;
@@ -426,6 +532,7 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     const size_t npix = (size_t)fs.W * fs.H;
     if (sl.jpeg) {
         if (c->jpeg_tab_quality != sl.quality) {
+            quiesce(c);
             JpegTables t;
             jpeg_tables(sl.quality, t);
             float tab[192];
@@ -603,6 +710,7 @@ int rr_set_ocio_config(rr_ctx* c, const char* dir) {
     if (!c) return fail(RR_EINVAL, "NULL ctx");
     return guarded([&] {
         set_device(c);
+        quiesce(c);
         c->filmic.release();
         if (!dir || !*dir) return RR_OK;
         FilmicLuts l;
@@ -625,7 +733,13 @@ int rr_create(int device_ordinal, rr_ctx** out) {
         std::unique_ptr<rr_ctx> c(new rr_ctx());
         c->device = device_ordinal;
         set_device(c.get());
-        RR_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        // The slots' streams first, so that each gets a hardware queue of its
+        // own (GPU_MAX_HW_QUEUES is 4, and the process's null stream holds
+        // one): streams created beyond that share a queue, and a queue runs
+        // its kernels in order, so frames of two slots on one queue cannot
+        // overlap. The home stream (inspection calls) is slot 0's.
+        for (auto& sl : c->slots) RR_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        c->stream = c->slots[0].stream;
         RR_HIP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
         if (const char* d = getenv("RR_OCIO_DIR")) {
             // a broken LUT directory does not fail the context: Filmic frames fall
@@ -644,6 +758,8 @@ void rr_destroy(rr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& sl : c->slots)
+        if (sl.stream) (void)hipStreamSynchronize(sl.stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     c->paths.release();
     c->filmic.release();
@@ -657,9 +773,10 @@ void rr_destroy(rr_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         sl.prof.release();
     }
-    if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     for (auto& sl : c->slots) {
+        if (sl.stream) (void)hipStreamDestroy(sl.stream);  // c->stream is slot 0's
+        sl.release_private();
         sl.counters.release();
         sl.film.release();
         sl.rgba8.release();
@@ -690,9 +807,17 @@ int rr_scene_load(rr_ctx* c, const char* path, rr_scene** out) {
 
 void rr_scene_free(rr_scene* s) {
     if (!s) return;
-    if (s->ctx) {
-        (void)hipSetDevice(s->ctx->device);
-        if (s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
+    if (rr_ctx* c = s->ctx) {
+        (void)hipSetDevice(c->device);
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        for (auto& sl : c->slots) {
+            if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+            if (sl.alt_scene == s) {  // the slot's build products of this scene
+                sl.alt.release();
+                sl.alt = DevScene{};
+                sl.alt_scene = nullptr;
+            }
+        }
     }
     s->dev.release();
     delete s;
@@ -829,7 +954,7 @@ int rr_synchronize(rr_ctx* c) {
     if (!c) return fail(RR_EINVAL, "NULL ctx");
     return guarded([&] {
         set_device(c);
-        RR_HIP(hipStreamSynchronize(c->stream));
+        quiesce(c);
         RR_HIP(hipStreamSynchronize(c->copy_stream));
         return RR_OK;
     });

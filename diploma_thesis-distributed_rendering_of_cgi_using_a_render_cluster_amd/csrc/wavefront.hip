@@ -2090,6 +2090,12 @@ bool scene_in_lds(int n_tris, int n_mats, int n_lights) {
     return n_tris > 0 && n_tris <= 128 && scene_budget_bytes(fc) <= kLdsSceneMax;  // 128: camera_hit's mask
 }
 
+bool frame_uses_tiles(const FrameConsts& base, bool force_wavefront) {
+    const long n_tiles = (long)((base.W + 7) / 8) * ((base.H + 7) / 8);
+    return scene_in_lds(base.n_tris, base.n_mats, base.n_lights) && tiles_enabled() && !force_wavefront &&
+           tile_slab_bytes(base.spp_total, n_tiles) <= kTileSlabMax;
+}
+
 namespace {
 // Launch geometry of one frame's path kernels.
 struct Grids {
@@ -2275,9 +2281,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     const int npix = base.npix;
     const size_t npaths = (size_t)npix * base.spp_chunk;
     const Grids G(base, p.count_traversal);
-    const long n_tiles = (long)((base.W + 7) / 8) * ((base.H + 7) / 8);
-    if (G.lds && base.n_tris > 0 && tiles_enabled() && !p.force_wavefront &&
-        tile_slab_bytes(base.spp_total, n_tiles) <= kTileSlabMax) {  // one launch: all samples of every tile
+    if (frame_uses_tiles(base, p.force_wavefront)) {  // one launch: all samples of every tile
         p.ensure_tiles();
         p.film.ensure((size_t)npix);
         p.rgba8.ensure((size_t)npix * 4);

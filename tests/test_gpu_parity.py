@@ -410,6 +410,38 @@ def test_pipelined_frames_match_serial(ctx, rr, tmp_path, s04):
     ctx.render_frame(s04, 6, p, str(tmp_path / "s6"), "JPEG", 90)
 
 
+def test_overlapped_frames_match_serial_across_paths(ctx, rr, tmp_path, s04):
+    """Two k_tiles frames in flight run side by side on the slots' streams
+    (each with its own hierarchy build, tile buffers and JPEG scratch); a
+    split-path frame (02 stand-in, 92k triangles) in between waits for its
+    predecessor. Every file equals the serial render byte for byte, also when
+    consecutive tile frames of different resolutions and sample counts share
+    the device."""
+    s02 = ctx.load_scene(scene_path("02_physics-standin.rrscene"))
+    try:
+        plan = [(s04, 5, rr.default_params(width=480, height=270, spp=64)),
+                (s04, 9, rr.default_params(width=320, height=180, spp=40)),
+                (s02, 60, rr.default_params(width=160, height=90, spp=4)),
+                (s04, 2, rr.default_params(width=480, height=270, spp=64)),
+                (s04, 60, rr.default_params(width=480, height=270, spp=64)),
+                (s04, 30, rr.default_params(width=480, height=270, spp=64))]
+        serial = []
+        for i, (s, f, p) in enumerate(plan):
+            ctx.render_frame(s, f, p, str(tmp_path / f"s{i}"), "JPEG", 90)
+            serial.append((tmp_path / f"s{i}.jpg").read_bytes())
+        pending = []
+        for i, (s, f, p) in enumerate(plan):
+            if len(pending) == 2:
+                ctx.complete_frame(pending.pop(0))
+            pending.append(ctx.submit_frame(s, f, p, str(tmp_path / f"p{i}"), "JPEG", 90))
+        for t in pending:
+            ctx.complete_frame(t)
+        for i in range(len(plan)):
+            assert (tmp_path / f"p{i}.jpg").read_bytes() == serial[i], f"frame {i} of the plan differs"
+    finally:
+        s02.close()
+
+
 def test_backend_runner_render_frames_pipelined(rr, tmp_path):
     """BackendRunner.render_frames: every frame written, traced once, in order."""
     import json
