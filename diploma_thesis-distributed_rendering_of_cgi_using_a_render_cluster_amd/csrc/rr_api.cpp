@@ -1213,6 +1213,22 @@ int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int
     });
 }
 
+int rr_debug_sqrt_check(rr_ctx* c, uint32_t lo, uint64_t n, uint64_t* counts3) {
+    if (!c || !counts3 || n > (1ull << 32) - lo) return fail(RR_EINVAL, "bad arguments");
+    return guarded([&] {
+        if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
+        set_device(c);
+        hipStream_t st = c->stream;
+        DevBuf<unsigned long long> d;
+        d.ensure(3);
+        sqrt_check_device(lo, n, d.ptr, st);
+        RR_HIP(hipMemcpyAsync(counts3, d.ptr, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        RR_HIP(hipStreamSynchronize(st));
+        d.release();
+        return RR_OK;
+    });
+}
+
 int rr_debug_bsdf_sample(rr_ctx* c, const float* mat12, const float* n3, const float* wo3, int32_t n,
                          const float* u, float* wi3, float* f3, float* pdf, int32_t* ok) {
     if (!c || !mat12 || !n3 || !wo3 || n < 0 || (n > 0 && (!u || !wi3 || !f3 || !pdf || !ok)))

@@ -139,6 +139,37 @@ RR_HD float3 norm3(float3 a) {
     const float inv = 1.0f / sqrtf(dot3(a, a));
     return scl3(a, inv);
 }
+
+// IEEE square root (the bits of sqrtf, which the oracle calls) for x = +-0 or
+// x in [2^-96, FLT_MAX]. hipcc's correctly rounded sqrtf is v_sqrt_f32 (within
+// 1 ulp) plus a correction that tries the neighbours s -+ 1 ulp by their
+// residuals, wrapped in a 2^32 pre-scale for x < 2^-96 and a class test for
+// zero / infinity; here the wrapping is left out (16 -> 9 instructions), which
+// returns the same bits over that range: rr_debug_sqrt_check compares all
+// 2^32 inputs with sqrtf on the device, 0 mismatches (tests/test_gpu_math.py). Every call site states
+// why its argument is in range; sqrt_any handles the rest.
+RR_HD float sqrt_rn(float x) {
+#if __HIP_DEVICE_COMPILE__
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
+    const float rm = fmaf(-sm, s, x), rp = fmaf(-sp, s, x);
+    const float r = rm <= 0.0f ? sm : s;
+    return rp > 0.0f ? sp : r;
+#else
+    return sqrtf(x);
+#endif
+}
+// Any x: sqrt_rn when every active lane's argument is in its range (one
+// wave-uniform test), else the full sqrtf.
+RR_HD float sqrt_any(float x) {
+#if __HIP_DEVICE_COMPILE__
+    if (__all((x >= 0x1p-96f && x <= 3.40282347e38f) || x == 0.0f)) return sqrt_rn(x);
+#endif
+    return sqrtf(x);
+}
+// norm3 for |a|^2 in [2^-96, FLT_MAX] (sqrt_rn; same bits as norm3)
+RR_HD float3 norm3_rn(float3 a) { return scl3(a, 1.0f / sqrt_rn(dot3(a, a))); }
+RR_HD float3 norm3_any(float3 a) { return scl3(a, 1.0f / sqrt_any(dot3(a, a))); }
 RR_HD float max3f(float3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
 RR_HD float3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
 
@@ -730,12 +761,16 @@ RR_HD float3 bsdf_eval_v(const Mat& m, FloatP lut, const BsdfView& vw, float3 N,
     const float sv = cosV + cosL;
     const float den = fmaf(2.0f, lv, 2.0f);
     const float X = fmaf(sv * sv, a2 - 1.0f, den);
-    const float cl1 = cosL + sqrtf(fmaf((1.0f - a2) * cosL, cosL, a2));
+    // sqrt_rn arguments: a2 + (1 - a2) c^2 with c in (0, 1] lies between a2 >= 1e-6
+    // (alpha floor) and 1; (1 + L.V) / 2 of unit vectors is 0, a multiple of
+    // 2^-26 or a rounding below 0 (NaN on both sides, clamped to the table's
+    // first entry by lut_at)
+    const float cl1 = cosL + sqrt_rn(fmaf((1.0f - a2) * cosL, cosL, a2));
     const float q = a2 * den * den;
     const float r = 1.0f / (3.14159265358979f * X * X * vw.cv1 * cl1);
     const float pdf_s = q * cl1 * r * 0.5f;                 // D G1(V) / (4 cosV)
     const float ks = m.spec_on ? q * cosL * r : 0.0f;       // D G1(V) G1(L) / (4 cosV cosL) * cosL
-    const float fh = lut_at(lut, sqrtf(fmaf(0.5f, lv, 0.5f)));  // L.H = sqrt((1 + L.V) / 2)
+    const float fh = lut_at(lut, sqrt_rn(fmaf(0.5f, lv, 0.5f)));  // L.H = sqrt((1 + L.V) / 2)
     const float3 c0 = m.cspec0;
     const float fh1 = 1.0f - fh;
     const float3 F = mk3(fmaf(c0.x, fh1, fh), fmaf(c0.y, fh1, fh), fmaf(c0.z, fh1, fh));
@@ -751,7 +786,7 @@ RR_HD BsdfView bsdf_view(const Mat& m, FloatP lut, float3 N, float3 wo) {
     v.ps = lut_at(lut + (kMatLutN + 1), v.cosV);  // 0 for Lambert and without a specular closure
     v.fv = schlick_w(v.cosV);
     const float a2 = m.a2;
-    v.cv1 = v.cosV + sqrtf(fmaf((1.0f - a2) * v.cosV, v.cosV, a2));
+    v.cv1 = v.cosV + sqrt_rn(fmaf((1.0f - a2) * v.cosV, v.cosV, a2));  // >= a2 >= 1e-6 (as cl1)
     return v;
 }
 
@@ -772,13 +807,17 @@ RR_HD float3 bsdf_eval(const Mat& m, FloatP lut, float3 N, float3 wo, float3 wi,
 // lobes): z = 1 - r^2 (1 + vz), and (x, y) = (dx, dy) sqrt((1 + vz)(2 - r^2 (1 + vz)))
 // so that x^2 + y^2 = 1 - z^2, without a division.
 RR_HD float3 sample_vndf(float3 v, float alpha, float dx, float dy) {
-    const float3 vh = norm3(mk3(alpha * v.x, alpha * v.y, v.z));
+    // |vh|^2 >= min(alpha^2, 1) |v|^2 with v a unit vector: sqrt_rn's range;
+    // s^2 is 0 or a product of k >= 1 and a difference of 2 and an exact
+    // product of floats of at most 2 (a multiple of 2^-48); the final h can
+    // vanish at the cap's rim (sqrt_any)
+    const float3 vh = norm3_rn(mk3(alpha * v.x, alpha * v.y, v.z));
     const float r2 = fmaf(dy, dy, dx * dx);
     const float k = 1.0f + vh.z;
     const float z = fmaf(-r2, k, 1.0f);
-    const float s = sqrtf(fmaxf(0.0f, k * fmaf(-r2, k, 2.0f)));
+    const float s = sqrt_rn(fmaxf(0.0f, k * fmaf(-r2, k, 2.0f)));
     const float3 h = mk3(fmaf(dx, s, vh.x), fmaf(dy, s, vh.y), fmaxf(0.0f, z + vh.z));
-    return norm3(mk3(alpha * h.x, alpha * h.y, h.z));
+    return norm3_any(mk3(alpha * h.x, alpha * h.y, h.z));
 }
 
 // Sample a direction; returns false when the path must end. f: f * cosL as
@@ -802,7 +841,8 @@ RR_HD bool bsdf_sample(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, f
         const float k = 2.0f * dot3(wo, H);
         wi = mk3(fmaf(H.x, k, -wo.x), fmaf(H.y, k, -wo.y), fmaf(H.z, k, -wo.z));
     } else {
-        const float z = sqrtf(fmaxf(0.0f, fmaf(-y, y, fmaf(-x, x, 1.0f))));
+        // 1 - x^2 - y^2 of a disk point: 0 or at least 2^-70 (sqrt_rn's range)
+        const float z = sqrt_rn(fmaxf(0.0f, fmaf(-y, y, fmaf(-x, x, 1.0f))));
         wi = frame3(T, B, N, x, y, z);
     }
     f = bsdf_eval_v(m, lut, vw, N, wo, wi, pdf);

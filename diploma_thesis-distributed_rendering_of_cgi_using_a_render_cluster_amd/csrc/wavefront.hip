@@ -169,7 +169,7 @@ __device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt
     }
     const float sx = fmaf(fx, fc.inv_w2, -1.0f) * fc.half_w;
     const float sy = fmaf(-fy, fc.inv_h2, 1.0f) * fc.half_h;
-    const float len = sqrtf(fmaf(sy, sy, fmaf(sx, sx, 1.0f)));
+    const float len = sqrt_rn(fmaf(sy, sy, fmaf(sx, sx, 1.0f)));  // >= 1
     const float3 dw = mk3(fmaf(fc.cam_up.x, sy, fmaf(fc.cam_right.x, sx, -fc.cam_back.x)),
                           fmaf(fc.cam_up.y, sy, fmaf(fc.cam_right.y, sx, -fc.cam_back.y)),
                           fmaf(fc.cam_up.z, sy, fmaf(fc.cam_right.z, sx, -fc.cam_back.z)));
@@ -281,7 +281,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
             const float3 tl = sub3(lp, P);
             const float dl2 = dot3(tl, tl);
             if (radius > 0.0f) {
-                const float3 wl = scl3(tl, 1.0f / sqrtf(dl2));
+                const float3 wl = scl3(tl, 1.0f / sqrt_any(dl2));
                 float3 b1, b2;
                 make_onb(wl, b1, b2);
                 float dx, dy;
@@ -291,13 +291,13 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
                 const float3 sp = madd3(madd3(lp, b1, dx), b2, dy);
                 const float3 ts = sub3(sp, P);
                 const float ds2 = dot3(ts, ts);
-                dist = sqrtf(ds2);
+                dist = sqrt_any(ds2);
                 const float id = 1.0f / dist;
                 wi = scl3(ts, id);
                 const float cl = fabsf(dot3(wl, wi));
                 Li = scl3(I, cl * id * id);
             } else {
-                dist = sqrtf(dl2);
+                dist = sqrt_any(dl2);
                 wi = scl3(tl, 1.0f / dist);
                 Li = scl3(I, 1.0f / dl2);
             }
@@ -2397,6 +2397,37 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, p.film_part.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
                                             p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
         pr.end(st);
+    }
+    RR_HIP(hipGetLastError());
+}
+
+namespace {
+// sqrt_rn / sqrt_any against the device's correctly rounded sqrtf over the
+// float bit patterns [lo, lo + n): counts[0] = sqrt_rn mismatches with the
+// argument in its range (+-0 or [2^-96, FLT_MAX]), counts[1] = sqrt_rn
+// mismatches outside it, counts[2] = sqrt_any mismatches anywhere (NaN equals
+// NaN). Each lane checks 16 patterns.
+__global__ void k_debug_sqrt(uint32_t lo, uint64_t n, unsigned long long* __restrict__ counts) {
+    unsigned long long c[3] = {0, 0, 0};
+    const uint64_t first = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 16;
+    for (uint64_t k = first; k < first + 16 && k < n; ++k) {
+        const float x = __uint_as_float((uint32_t)(lo + k));
+        const float ref = sqrtf(x), a = sqrt_rn(x), b = sqrt_any(x);
+        const bool in = (x >= 0x1p-96f && x <= 3.40282347e38f) || x == 0.0f;
+        if (!(__float_as_uint(a) == __float_as_uint(ref) || (a != a && ref != ref))) ++c[in ? 0 : 1];
+        if (!(__float_as_uint(b) == __float_as_uint(ref) || (b != b && ref != ref))) ++c[2];
+    }
+    for (int i = 0; i < 3; ++i)
+        if (c[i]) atomicAdd(&counts[i], c[i]);
+}
+}  // namespace
+
+void sqrt_check_device(uint32_t lo, uint64_t n, unsigned long long* d_counts, hipStream_t st) {
+    RR_HIP(hipMemsetAsync(d_counts, 0, 3 * sizeof(unsigned long long), st));
+    const uint64_t per_block = (uint64_t)kBlock * 16;
+    for (uint64_t off = 0; off < n; off += per_block << 16) {  // <= 65536 blocks per launch
+        const uint64_t m = std::min<uint64_t>(n - off, per_block << 16);
+        k_debug_sqrt<<<(unsigned)((m + per_block - 1) / per_block), kBlock, 0, st>>>((uint32_t)(lo + off), m, d_counts);
     }
     RR_HIP(hipGetLastError());
 }
