@@ -78,13 +78,13 @@ struct Rad {
 // Dense queue state (SoA, ping-pong per bounce).
 struct PathQueue {
     float4* o;  // origin.xyz, path id (int bits)
-    float4* d;  // direction.xyz, 0
-    float4* t;  // throughput.xyz, 0
+    float4* d;  // direction.xyz, lobe bounce counters (int bits)
+    float4* t;  // throughput.xyz, 1 when the ray leaves a hull side of its triangle (hull_flags), else 0
 };
 struct ShadowQueue {
     float4* o;  // origin.xyz, path id (int bits)
     float4* d;  // direction.xyz, tmax
-    float4* c;  // contribution.xyz, 0
+    float4* c;  // contribution.xyz, hull escape flag as in PathQueue::t
 };
 
 // Read-only scene data of the path kernels: in HBM (GlobalView) or, for
@@ -187,8 +187,12 @@ __device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, i
     camera_ray_xy(fc, filt, pix - py * fc.W, py, key, o, d, tmin, tmax, cull, culled);
 }
 
+// Staged material word of LDS-resident scenes: material id | hull_flags << kHullShift.
+constexpr int kHullShift = 30;
+
 struct ShadeOut {
     bool cont, shadow;
+    bool esc;                // the rays leave a hull side of the hit triangle (hull_flags): they meet nothing
     float3 o, d, T;          // continuation ray + throughput
     uint32_t lob;            // continuation's lobe bounce counters (lobe_counts)
     float3 so, sd, sc;       // shadow ray + pending contribution
@@ -235,6 +239,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
                                       const Shadow& trace_shadow = Shadow{}) {
     out.cont = false;
     out.shadow = false;
+    out.esc = false;
     if (h.idx < 0) {
         float3 c = mul3(T, fc.world);
         if (bounce > 0) c = clamp_contrib(c, fc.clamp_indirect);
@@ -243,10 +248,12 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     }
     int mid;
     float3 N;
+    uint32_t hull = 0;  // hull_flags of the hit triangle (LDS-resident scenes)
     if constexpr (std::is_same<View, LdsView>::value) {
-        const float4 nm = lds_ld4(v.nrm + h.idx);  // staged: norm3(cross3(e1, e2)), material id
+        const float4 nm = lds_ld4(v.nrm + h.idx);  // staged: norm3(cross3(e1, e2)), material id | hull flags
         N = xyz(nm);
-        mid = f2i(nm.w);
+        mid = f2i(nm.w) & ((1 << kHullShift) - 1);
+        hull = (uint32_t)f2i(nm.w) >> kHullShift;
     } else {
         const TriPack tp = load_tri(v.tris, h.idx);
         mid = f2i(tp.p1.w);
@@ -256,7 +263,11 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     const auto lut = v.lut + kMatLutStride * mid;
     const float t = h.t;
     const float3 P = madd3(o, d, t);
-    if (dot3(N, d) > 0.0f) N = mk3(-N.x, -N.y, -N.z);
+    const bool flip = dot3(N, d) > 0.0f;
+    if (flip) N = mk3(-N.x, -N.y, -N.z);
+    // shadow and continuation rays leave on N's side: the front side unless flipped
+    const bool esc = ((hull >> (flip ? 1 : 0)) & 1u) != 0u;
+    out.esc = esc;
     const float3 wo = mk3(-d.x, -d.y, -d.z);
     if (m.emission.x != 0.0f || m.emission.y != 0.0f || m.emission.z != 0.0f) {
         float3 c = mul3(T, m.emission);
@@ -316,7 +327,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
             if (max3f(c) > 0.0f) {
                 out.shadow = true;
                 if constexpr (Shadow::kInline) {
-                    if (!trace_shadow(Po, wi, dist)) add_to(L, c);
+                    if (esc || !trace_shadow(Po, wi, dist)) add_to(L, c);
                 } else {
                     out.so = Po;
                     out.sd = wi;
@@ -375,13 +386,13 @@ __device__ __forceinline__ void emit(const ShadeOut& so, int pid, PathQueue out,
         const uint32_t s1 = seg_base + cur.c + (uint32_t)__popcll(mc & below);
         out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
         out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, i2f((int)so.lob));
-        out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, 0.0f);
+        out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, so.esc ? 1.0f : 0.0f);
     }
     if (so.shadow) {
         const uint32_t s2 = seg_base + cur.s + (uint32_t)__popcll(ms & below);
         sq.o[s2] = make_float4(so.so.x, so.so.y, so.so.z, i2f(pid));
         sq.d[s2] = make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist);
-        sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, 0.0f);
+        sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, so.esc ? 1.0f : 0.0f);
     }
     cur.c += (uint32_t)__popcll(mc);
     cur.s += (uint32_t)__popcll(ms);
@@ -491,6 +502,36 @@ RR_D void lds_copy(lds_f4w* dst, const float4* __restrict__ src, int n4) {
     const rr_f4v* s = reinterpret_cast<const rr_f4v*>(src);
     for (int i = threadIdx.x; i < n4; i += kBlock) dst[i] = s[i];
 }
+// Hull flags of an LDS-resident scene's triangle i (oracle/rr_oracle.c
+// tri_hull, the same float operations): bit 0 when every vertex of every
+// triangle lies behind triangle i's plane on its front side (the cross(e1, e2)
+// direction), up to 2^-12 of the vertex's distance from v0 times |n|_1; bit 1
+// the same for the back side. A ray leaving the triangle on a side whose bit is
+// set moves away from a plane the whole scene lies behind: it meets nothing, so
+// its continuation misses and its shadow ray is unoccluded without a traversal
+// (the tests skipped could only report rounding-level grazing hits). On 04vs /
+// 01 (a cube) every face is such a side: no secondary ray is traversed. Kept in
+// bits kHullShift.. of the staged material word (shade() reads that word anyway).
+RR_D uint32_t hull_flags(lds_tri* tris, int n_tris, int i) {
+    const TriPack s = load_tri(tris, i);
+    const float3 v0 = xyz(s.p0), n = cross3(xyz(s.p1), xyz(s.p2));
+    const float an = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
+    bool front = true, back = true;
+    for (int j = 0; j < n_tris; ++j) {
+        const TriPack e = load_tri(tris, j);
+        const float3 w0 = xyz(e.p0);
+        const float3 w[3] = {w0, add3(w0, xyz(e.p1)), add3(w0, xyz(e.p2))};
+        for (int k = 0; k < 3; ++k) {
+            const float3 r = sub3(w[k], v0);
+            const float h = dot3(n, r);
+            const float lim = an * (fabsf(r.x) + fabsf(r.y) + fabsf(r.z)) * 0x1p-12f;
+            front = front && h <= lim;
+            back = back && -h <= lim;
+        }
+    }
+    return (front ? 1u : 0u) | (back ? 2u : 0u);
+}
+
 // Stages the scene at the start of dynamic LDS (all threads call; ends with a
 // barrier). `shading`: also materials, lights and the filter table. Returns the
 // view; `used` receives the float4 slots taken (LDS layout: scene_lds_f4()).
@@ -606,13 +647,14 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
         q += kMatLutStride / 4 * a.n_mats;
     }
     if (shading || kCam) __syncthreads();  // the copies above are visible
-    if (shading) {  // per-triangle unit normals and material ids (shade() reads no TriPack)
+    if (shading) {  // per-triangle unit normals, material ids and hull flags (shade() reads no TriPack)
         v.nrm = q;
         for (int i = threadIdx.x; i < a.n_tris; i += kBlock) {
             const TriPack tp = load_tri(v.tris, i);
             const float3 n = norm3(cross3(xyz(tp.p1), xyz(tp.p2)));
             rr_f4v x;
-            x.x = n.x; x.y = n.y; x.z = n.z; x.w = tp.p1.w;
+            x.x = n.x; x.y = n.y; x.z = n.z;
+            x.w = i2f(f2i(tp.p1.w) | (int)(hull_flags(v.tris, a.n_tris, i) << kHullShift));
             q[i] = x;
         }
         q += a.n_tris;
@@ -799,7 +841,8 @@ RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueu
             pid = f2i(a.w);
             const float3 o = xyz(a), d = xyz(b);
             Hit h;
-            traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
+            if (c.w != 0.0f) set_miss(h, kFltMax);  // left a hull side (hull_flags)
+            else traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
             const int sl = (int)fc.div_npix.div((uint32_t)pid);
             const int pix = pid - sl * fc.npix;
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
@@ -858,6 +901,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
         float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = o, L = o;
         uint32_t key = 0, lob = 0;
         int pid = 0;
+        bool esc = false;
         if (live) {
             const uint32_t i = ix.slot((uint32_t)j);
             const float4 a = in.o[i], b = in.d[i], c = in.t[i];
@@ -865,6 +909,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
             o = xyz(a);
             d = xyz(b);
             T = xyz(c);
+            esc = c.w != 0.0f;
             lob = (uint32_t)f2i(b.w);
             const int sl = (int)fc.div_npix.div((uint32_t)pid);
             const int pix = pid - sl * fc.npix;
@@ -877,11 +922,12 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
             so.cont = so.shadow = false;
             if (live) {
                 Hit h;
-                traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cc);
+                if (esc) set_miss(h, kFltMax);
+                else traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cc);
                 shade(fc, b, v, o, d, T, lob, h, key, L, so);
                 if (so.shadow) {
                     Hit hs;
-                    if (!traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs, cs)) {
+                    if (so.esc || !traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs, cs)) {
                         L.x = L.x + so.sc.x;
                         L.y = L.y + so.sc.y;
                         L.z = L.z + so.sc.z;
@@ -892,6 +938,7 @@ RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue
                     d = so.d;
                     T = so.T;
                     lob = so.lob;
+                    esc = so.esc;
                 } else {
                     live = false;
                 }
@@ -938,11 +985,11 @@ RR_D void shadow_body(NodeP nodes, TriP tris, int n_tris, ShadowQueue sq, const 
     TravCount cnt;
     for (int j = gtid; j < count; j += stride) {
         const uint32_t i = ix.slot((uint32_t)j);
-        const float4 a = sq.o[i], b = sq.d[i];
+        const float4 a = sq.o[i], b = sq.d[i], c = sq.c[i];
         Hit h;
-        if (!traverse<true, kCount>(nodes, tris, n_tris, xyz(a), xyz(b), 0.0f, b.w, st, h, cnt)) {
+        // c.w: the ray leaves a hull side of its triangle (hull_flags)
+        if (c.w != 0.0f || !traverse<true, kCount>(nodes, tris, n_tris, xyz(a), xyz(b), 0.0f, b.w, st, h, cnt)) {
             const int pid = f2i(a.w);
-            const float4 c = sq.c[i];
             float3 L = rad.get(pid);
             L.x = L.x + c.x;
             L.y = L.y + c.y;
@@ -1155,13 +1202,13 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
         const uint32_t s1 = bc + (uint32_t)__popcll(mc & below);
         out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
         out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, i2f((int)so.lob));
-        out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, 0.0f);
+        out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, so.esc ? 1.0f : 0.0f);
     }
     if (so.shadow) {
         const uint32_t s2 = bs + (uint32_t)__popcll(ms & below);
         sq.o[s2] = make_float4(so.so.x, so.so.y, so.so.z, i2f(pid));
         sq.d[s2] = make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist);
-        sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, 0.0f);
+        sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, so.esc ? 1.0f : 0.0f);
     }
 }
 
@@ -1740,7 +1787,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = mk3(1.0f, 1.0f, 1.0f), L = o;
             uint32_t lob = 0;
             float tmin = 0.0f, tmax = -1.0f;
-            bool culled = true;
+            bool culled = true, esc = false;
             if (valid) camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
             n_t0 += wave_count(!culled);
             bool live = valid;
@@ -1753,6 +1800,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     if (b == 0) {  // the camera ray against the tile's triangles (wave-uniform masks)
                         set_miss(h, tmax);
                         if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);
+                    } else if (esc) {  // left a hull side of its triangle (hull_flags): meets nothing
+                        set_miss(h, kFltMax);
                     } else {
                         traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, ce);
                     }
@@ -1764,6 +1813,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                         d = so.d;
                         T = so.T;
                         lob = so.lob;
+                        esc = so.esc;
                     } else {
                         live = false;
                     }

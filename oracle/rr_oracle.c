@@ -887,6 +887,7 @@ typedef struct {
     float filter[ORC_FILTER_N];
     float srgb[ORC_SRGB_N + 1];
     int cam_all;          /* camera rays test every triangle (LDS-resident scenes, render_ints[7] == 2) */
+    unsigned char* hull;  /* LDS-resident scenes: per leaf, bit 0 / 1 = the scene lies behind its front / back side (tri_hull) */
     int cull_on;          /* screen_rect() succeeded */
     float cull[4];        /* x0 x1 y0 y1 in subpixel coordinates */
 } scene_t;
@@ -927,6 +928,36 @@ static mat_t load_mat(const float* mats, int id) {
 /* Ray statistics of the last orc_render (orc_ray_counts): continuations and
  * shadow rays created at bounce 0 / at later bounces, as rr_frame_stats counts
  * them, and the first (pixel, sample) pairs whose path continued past bounce 1. */
+/* Hull flags of an LDS-resident scene's triangle (csrc/wavefront.hip
+ * stage_scene, hull_flags; same float operations): bit 0 when every vertex of
+ * every triangle lies behind the triangle's plane on its front side (the
+ * cross(e1, e2) direction), up to 2^-12 of the vertex's distance times |n|_1,
+ * bit 1 the same for the back side. A ray that leaves the triangle on a side
+ * whose bit is set moves away from a plane the whole scene lies behind, so it
+ * meets nothing: the continuation misses and the shadow ray is unoccluded
+ * without a traversal (the skipped tests could only report rounding-level
+ * grazing hits). */
+static unsigned tri_hull(const lbvh* B, int i) {
+    const float* s = B->tri + 9 * (size_t)i;
+    const v3 v0 = V(s[0], s[1], s[2]);
+    const v3 n = vcross(V(s[3], s[4], s[5]), V(s[6], s[7], s[8]));
+    const float an = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
+    int front = 1, back = 1;
+    for (int j = 0; j < B->n; ++j) {
+        const float* e = B->tri + 9 * (size_t)j;
+        const v3 w0 = V(e[0], e[1], e[2]);
+        const v3 w[3] = {w0, vadd(w0, V(e[3], e[4], e[5])), vadd(w0, V(e[6], e[7], e[8]))};
+        for (int k = 0; k < 3; ++k) {
+            const v3 r = vsub(w[k], v0);
+            const float h = vdot(n, r);
+            const float lim = an * (fabsf(r.x) + fabsf(r.y) + fabsf(r.z)) * 0x1p-12f;
+            front = front && h <= lim;
+            back = back && -h <= lim;
+        }
+    }
+    return (unsigned)front | (unsigned)back << 1;
+}
+
 static long long g_rays[4];
 static int g_late[32], g_n_late;
 
@@ -947,6 +978,7 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
     float tmin = c[14] * len, tmax = c[15] * len;
     v3 L = V(0.0f, 0.0f, 0.0f), T = V(1.0f, 1.0f, 1.0f);
     int nd = 0, ng = 0;  /* diffuse / glossy scatters so far (Cycles path_state_next) */
+    int esc = 0;         /* the ray leaves a hull side of its triangle (tri_hull): it meets nothing */
     const int culled = S->cull_on && (fx < S->cull[0] || fx > S->cull[1] || fy < S->cull[2] || fy > S->cull[3]);
     for (int b = 0; b <= S->max_bounces; ++b) {
         hitrec h;
@@ -959,6 +991,8 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
              * is order-independent, so the result is the same) */
             h.t = tmax; h.u = h.v = 0.0f; h.idx = -1; h.orig = -1;
             for (int i = 0; i < S->bvh->n; ++i) try_leaf(S->bvh, i, o, d, tmin, &h);
+        } else if (esc) {
+            h.t = tmax; h.u = h.v = 0.0f; h.idx = -1; h.orig = -1;
         } else {
             trace(S->bvh, o, d, tmin, tmax, 0, &h);
         }
@@ -976,7 +1010,10 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
         float t = h.t;
         v3 P = vmadd(o, d, t);
         v3 N = vnorm(vcross(e1, e2));
-        if (vdot(N, d) > 0.0f) N = V(-N.x, -N.y, -N.z);
+        const int flip = vdot(N, d) > 0.0f;
+        if (flip) N = V(-N.x, -N.y, -N.z);
+        /* rays leaving this point go to N's side: the front side unless flipped */
+        const int leave_esc = S->hull ? (int)((S->hull[h.idx] >> flip) & 1u) : 0;
         v3 wo = V(-d.x, -d.y, -d.z);
         if (m.emission.x != 0.0f || m.emission.y != 0.0f || m.emission.z != 0.0f) {
             v3 cc = vmul(T, m.emission);
@@ -1068,11 +1105,12 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
         }
         if (shadow) {
             hitrec hs;
-            if (!trace(S->bvh, Po, sh_dir, 0.0f, sh_dist, 1, &hs)) L = vadd(L, sh_c);
+            if (leave_esc || !trace(S->bvh, Po, sh_dir, 0.0f, sh_dist, 1, &hs)) L = vadd(L, sh_c);
         }
         if (!alive) break;
         if (glossy) ++ng; else ++nd;
         o = Po; d = wi; tmin = 0.0f; tmax = 3.402823466e+38f;
+        esc = leave_esc;
     }
     return L;
 }
@@ -1283,6 +1321,10 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     S->mats = mats;
     S->world = V(world[0], world[1], world[2]);
     S->cam_all = ri[7] == 2;
+    if (S->cam_all && n_tris > 0) {
+        S->hull = (unsigned char*)malloc((size_t)n_tris);
+        for (int i = 0; i < n_tris; ++i) S->hull[i] = (unsigned char)tri_hull(&B, i);
+    }
     S->W = ri[0]; S->H = ri[1]; S->spp = ri[2]; S->max_bounces = ri[3]; S->seed = (uint32_t)ri[4]; S->view = ri[5];
     S->max_diffuse = ri[8]; S->max_glossy = ri[9];
     {
@@ -1356,6 +1398,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
         }
     }
     free(S->luts);
+    free(S->hull);
     free(S);
     lbvh_free(&B);
     return 0;

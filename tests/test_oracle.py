@@ -242,6 +242,31 @@ def test_04_frame_is_plausible():
     assert np.array_equal(f2[10:20], film[10:20]) and np.array_equal(r2[10:20], rgba[10:20])
 
 
+@pytest.mark.parametrize("frame,ground", [(1, False), (30, False), (60, True), (5, True)])
+def test_hull_escape_changes_no_pixel(frame, ground):
+    """LDS-resident scenes (render_ints[7] == 2) skip the traversal of a
+    secondary ray that leaves a triangle on a side the whole scene lies behind
+    (tri_hull). Such a ray meets nothing, so the frame equals the one rendered
+    with every secondary ray traversed (render_ints[7] == 3: PLOC hierarchy,
+    no hull rule) bit for bit — on the cube, where every face is a hull side,
+    and with a ground quad under it, where the side faces are not."""
+    scene = HO.load_scene(scene_path("04_very-simple-standin.rrscene"))
+    fc = HO.frame_constants(scene, frame, 64, 36)
+    tris, mats = world_tris(scene, frame)
+    if ground:
+        g = np.array([[[-6, -6, -1.5], [6, -6, -1.5], [6, 6, -1.5]], [[-6, -6, -1.5], [6, 6, -1.5], [-6, 6, -1.5]]],
+                     np.float32)
+        tris, mats = np.concatenate([tris, g]), np.concatenate([mats, mats[:2]])
+    rf = np.array([10.0, 1.5, 1.0, 0], np.float32)
+    films = []
+    for hier in (2, 3):
+        ri = np.array([64, 36, 16, 12, 0, 0, 0, hier, 4, 4], np.int32)
+        f, _ = O.render(tris, mats, fc["camera"], fc["lights"], fc["materials"], fc["world"], ri, rf, threads=4)
+        films.append(f)
+    assert films[0][..., 0].max() > 0.3
+    assert np.array_equal(films[0], films[1])
+
+
 def _q4_child_boxes(node):
     """Decoded child boxes of one quantised BVH4 node (rr_device.h QNode4), in
     double: lo/hi = org + q * 2^e per axis, (4, 3) each."""
