@@ -230,9 +230,10 @@ void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, f
 void bsdf_batch_device(const float* d_mat12, const float* d_lut, const float n3[3], const float wo3[3], int n,
                        const float* d_u, float* d_wi, float* d_f, float* d_pdf, int32_t* d_ok, hipStream_t st);
 
-// sqrt_rn / sqrt_any (rr_device.h) against sqrtf over the float bit patterns
-// [lo, lo + n) on the device; d_counts: 3 words (rr_debug_sqrt_check).
-void sqrt_check_device(uint32_t lo, uint64_t n, unsigned long long* d_counts, hipStream_t st);
+// sqrt_rn / sqrt_any / rcp_rn (rr_device.h) against sqrtf and 1.0f / x over
+// the float bit patterns [lo, lo + n) on the device; d_counts: 5 words
+// (rr_debug_fastmath_check).
+void fastmath_check_device(uint32_t lo, uint64_t n, unsigned long long* d_counts, hipStream_t st);
 
 // Device JPEG forward transform (jpeg.hip); tab = dct | qinv luma | qinv chroma.
 void jpeg_fdct_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, int16_t* d_out, hipStream_t st);

@@ -1213,16 +1213,16 @@ int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int
     });
 }
 
-int rr_debug_sqrt_check(rr_ctx* c, uint32_t lo, uint64_t n, uint64_t* counts3) {
-    if (!c || !counts3 || n > (1ull << 32) - lo) return fail(RR_EINVAL, "bad arguments");
+int rr_debug_fastmath_check(rr_ctx* c, uint32_t lo, uint64_t n, uint64_t* counts5) {
+    if (!c || !counts5 || n > (1ull << 32) - lo) return fail(RR_EINVAL, "bad arguments");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         set_device(c);
         hipStream_t st = c->stream;
         DevBuf<unsigned long long> d;
-        d.ensure(3);
-        sqrt_check_device(lo, n, d.ptr, st);
-        RR_HIP(hipMemcpyAsync(counts3, d.ptr, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        d.ensure(5);
+        fastmath_check_device(lo, n, d.ptr, st);
+        RR_HIP(hipMemcpyAsync(counts5, d.ptr, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         RR_HIP(hipStreamSynchronize(st));
         d.release();
         return RR_OK;

@@ -145,7 +145,7 @@ RR_HD float3 norm3(float3 a) {
 // 1 ulp) plus a correction that tries the neighbours s -+ 1 ulp by their
 // residuals, wrapped in a 2^32 pre-scale for x < 2^-96 and a class test for
 // zero / infinity; here the wrapping is left out (16 -> 9 instructions), which
-// returns the same bits over that range: rr_debug_sqrt_check compares all
+// returns the same bits over that range: rr_debug_fastmath_check compares all
 // 2^32 inputs with sqrtf on the device, 0 mismatches (tests/test_gpu_math.py). Every call site states
 // why its argument is in range; sqrt_any handles the rest.
 RR_HD float sqrt_rn(float x) {
@@ -167,8 +167,25 @@ RR_HD float sqrt_any(float x) {
 #endif
     return sqrtf(x);
 }
+// IEEE reciprocal (the bits of 1.0f / b) for |b| in [2^-60, 2^60]. hipcc's
+// correctly rounded division is v_rcp_f32 refined by fused multiply-adds,
+// between v_div_scale (which rescales operands near the exponent limits) and
+// v_div_fixup (infinities, zeros, NaNs): 11 instructions. In that range
+// neither wrapper changes anything, and the refinement alone (7 instructions)
+// returns the same bits: rr_debug_fastmath_check compares every float with
+// 1.0f / b on the device (tests/test_gpu_math.py).
+RR_HD float rcp_rn(float b) {
+#if __HIP_DEVICE_COMPILE__
+    float r = __builtin_amdgcn_rcpf(b);
+    r = fmaf(fmaf(-b, r, 1.0f), r, r);
+    float q = fmaf(fmaf(-b, r, 1.0f), r, r);
+    return fmaf(fmaf(-b, q, 1.0f), r, q);
+#else
+    return 1.0f / b;
+#endif
+}
 // norm3 for |a|^2 in [2^-96, FLT_MAX] (sqrt_rn; same bits as norm3)
-RR_HD float3 norm3_rn(float3 a) { return scl3(a, 1.0f / sqrt_rn(dot3(a, a))); }
+RR_HD float3 norm3_rn(float3 a) { return scl3(a, rcp_rn(sqrt_rn(dot3(a, a)))); }
 RR_HD float3 norm3_any(float3 a) { return scl3(a, 1.0f / sqrt_any(dot3(a, a))); }
 RR_HD float max3f(float3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
 RR_HD float3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
@@ -250,7 +267,7 @@ RR_HD void concentric_disk(float u1, float u2, float& x, float& y) {
 // Orthonormal basis (Duff et al. 2017, branchless).
 RR_HD void make_onb(float3 n, float3& b1, float3& b2) {
     const float sign = copysignf(1.0f, n.z);
-    const float a = -1.0f / (sign + n.z);
+    const float a = -rcp_rn(sign + n.z);  // |sign + n.z| in [1, 2] for a unit n; -1/x == -(1/x)
     const float b = n.x * n.y * a;
     b1 = mk3(fmaf(sign * n.x * n.x, a, 1.0f), sign * b, -sign * n.x);
     b2 = mk3(b, fmaf(n.y * n.y, a, sign), -n.y);

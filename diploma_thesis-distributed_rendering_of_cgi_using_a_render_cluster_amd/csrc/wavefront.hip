@@ -173,7 +173,7 @@ __device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt
     const float3 dw = mk3(fmaf(fc.cam_up.x, sy, fmaf(fc.cam_right.x, sx, -fc.cam_back.x)),
                           fmaf(fc.cam_up.y, sy, fmaf(fc.cam_right.y, sx, -fc.cam_back.y)),
                           fmaf(fc.cam_up.z, sy, fmaf(fc.cam_right.z, sx, -fc.cam_back.z)));
-    const float il = 1.0f / len;
+    const float il = rcp_rn(len);  // len in [1, 2^60]: the camera's half extents are finite
     d = scl3(dw, il);
     o = fc.cam_pos;
     tmin = fc.clip_start * len;
@@ -2452,32 +2452,37 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
 }
 
 namespace {
-// sqrt_rn / sqrt_any against the device's correctly rounded sqrtf over the
-// float bit patterns [lo, lo + n): counts[0] = sqrt_rn mismatches with the
-// argument in its range (+-0 or [2^-96, FLT_MAX]), counts[1] = sqrt_rn
-// mismatches outside it, counts[2] = sqrt_any mismatches anywhere (NaN equals
-// NaN). Each lane checks 16 patterns.
-__global__ void k_debug_sqrt(uint32_t lo, uint64_t n, unsigned long long* __restrict__ counts) {
-    unsigned long long c[3] = {0, 0, 0};
+// sqrt_rn / sqrt_any / rcp_rn against the device's correctly rounded sqrtf
+// and 1.0f / x over the float bit patterns [lo, lo + n): counts[0] = sqrt_rn
+// mismatches with the argument in its range (+-0 or [2^-96, FLT_MAX]),
+// counts[1] = sqrt_rn mismatches outside it, counts[2] = sqrt_any mismatches
+// anywhere, counts[3] = rcp_rn mismatches with |x| in [2^-60, 2^60],
+// counts[4] = rcp_rn mismatches outside (NaN equals NaN). 16 patterns a lane.
+__global__ void k_debug_fastmath(uint32_t lo, uint64_t n, unsigned long long* __restrict__ counts) {
+    unsigned long long c[5] = {0, 0, 0, 0, 0};
     const uint64_t first = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 16;
+    auto same = [](float a, float b) { return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b); };
     for (uint64_t k = first; k < first + 16 && k < n; ++k) {
         const float x = __uint_as_float((uint32_t)(lo + k));
-        const float ref = sqrtf(x), a = sqrt_rn(x), b = sqrt_any(x);
+        const float ref = sqrtf(x);
         const bool in = (x >= 0x1p-96f && x <= 3.40282347e38f) || x == 0.0f;
-        if (!(__float_as_uint(a) == __float_as_uint(ref) || (a != a && ref != ref))) ++c[in ? 0 : 1];
-        if (!(__float_as_uint(b) == __float_as_uint(ref) || (b != b && ref != ref))) ++c[2];
+        if (!same(sqrt_rn(x), ref)) ++c[in ? 0 : 1];
+        if (!same(sqrt_any(x), ref)) ++c[2];
+        const bool rin = fabsf(x) >= 0x1p-60f && fabsf(x) <= 0x1p60f;
+        if (!same(rcp_rn(x), 1.0f / x)) ++c[rin ? 3 : 4];
     }
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 5; ++i)
         if (c[i]) atomicAdd(&counts[i], c[i]);
 }
 }  // namespace
 
-void sqrt_check_device(uint32_t lo, uint64_t n, unsigned long long* d_counts, hipStream_t st) {
-    RR_HIP(hipMemsetAsync(d_counts, 0, 3 * sizeof(unsigned long long), st));
+void fastmath_check_device(uint32_t lo, uint64_t n, unsigned long long* d_counts, hipStream_t st) {
+    RR_HIP(hipMemsetAsync(d_counts, 0, 5 * sizeof(unsigned long long), st));
     const uint64_t per_block = (uint64_t)kBlock * 16;
     for (uint64_t off = 0; off < n; off += per_block << 16) {  // <= 65536 blocks per launch
         const uint64_t m = std::min<uint64_t>(n - off, per_block << 16);
-        k_debug_sqrt<<<(unsigned)((m + per_block - 1) / per_block), kBlock, 0, st>>>((uint32_t)(lo + off), m, d_counts);
+        k_debug_fastmath<<<(unsigned)((m + per_block - 1) / per_block), kBlock, 0, st>>>((uint32_t)(lo + off), m,
+                                                                                      d_counts);
     }
     RR_HIP(hipGetLastError());
 }

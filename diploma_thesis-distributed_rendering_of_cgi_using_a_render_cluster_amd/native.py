@@ -81,7 +81,7 @@ EXPORTS = [
     "rr_last_warning", "rr_set_ocio_config", "rr_synchronize",
     "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
     "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_bvh4", "rr_debug_bvh_hier", "rr_debug_jpeg_device",
-    "rr_debug_bsdf_sample", "rr_debug_sqrt_check",
+    "rr_debug_bsdf_sample", "rr_debug_fastmath_check",
 ]
 
 _lib = None
@@ -136,7 +136,7 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_uint64)]),
         "rr_debug_object_matrix": (c_int, [P, i32, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
         "rr_debug_bsdf_sample": (c_int, [P, f32p, f32p, f32p, i32, f32p, f32p, f32p, f32p, i32p]),
-        "rr_debug_sqrt_check": (c_int, [P, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+        "rr_debug_fastmath_check": (c_int, [P, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -384,10 +384,11 @@ class RenderContext:
                                           _ptr(pdf, ctypes.c_float), _ptr(ok, ctypes.c_int32)), self.handle)
         return wi, f, pdf, ok
 
-    def sqrt_check(self, lo: int = 0, n: int = 1 << 32):
-        """rr_debug_sqrt_check: (sqrt_rn mismatches in range, outside range, sqrt_any mismatches)."""
-        out = (ctypes.c_uint64 * 3)()
-        _check(lib().rr_debug_sqrt_check(self.handle, int(lo), int(n), out), self.handle)
+    def fastmath_check(self, lo: int = 0, n: int = 1 << 32):
+        """rr_debug_fastmath_check: mismatches of (sqrt_rn in range, sqrt_rn outside, sqrt_any,
+        rcp_rn in range, rcp_rn outside)."""
+        out = (ctypes.c_uint64 * 5)()
+        _check(lib().rr_debug_fastmath_check(self.handle, int(lo), int(n), out), self.handle)
         return tuple(int(v) for v in out)
 
     def trace(self, scene: Scene, frame: int, rays: np.ndarray, width: int = 0):

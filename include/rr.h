@@ -307,13 +307,15 @@ int rr_debug_trace(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t bv
 int rr_debug_bsdf_sample(rr_ctx* ctx, const float* mat12, const float* n3, const float* wo3, int32_t n,
                          const float* u, float* wi3, float* f3, float* pdf, int32_t* ok);
 
-/* The per-sample path's square roots (rr_device.h sqrt_rn / sqrt_any)
- * against the device's correctly rounded sqrtf, over the float bit patterns
- * lo .. lo + n - 1: counts3[0] = sqrt_rn mismatches with the argument in its
- * range (+-0 or [2^-96, FLT_MAX]; must be 0), [1] = sqrt_rn mismatches outside
- * it (not called there), [2] = sqrt_any mismatches (must be 0). Test
+/* The per-sample path's square roots and reciprocals (rr_device.h sqrt_rn /
+ * sqrt_any / rcp_rn) against the device's correctly rounded sqrtf and
+ * 1.0f / x, over the float bit patterns lo .. lo + n - 1: counts5[0] =
+ * sqrt_rn mismatches with the argument in its range (+-0 or [2^-96, FLT_MAX];
+ * must be 0), [1] = sqrt_rn mismatches outside it (not called there), [2] =
+ * sqrt_any mismatches (must be 0), [3] = rcp_rn mismatches with |x| in
+ * [2^-60, 2^60] (must be 0), [4] = rcp_rn mismatches outside it. Test
  * infrastructure for the bit-exactness claim; no reference counterpart. */
-int rr_debug_sqrt_check(rr_ctx* ctx, uint32_t lo, uint64_t n, uint64_t* counts3);
+int rr_debug_fastmath_check(rr_ctx* ctx, uint32_t lo, uint64_t n, uint64_t* counts5);
 
 /* Host animation evaluation: object_to_world matrix (row-major 4x4, f64) of
  * object `object_index` at (possibly fractional) frame. */
