@@ -551,7 +551,7 @@ def main():
                        "resolution": f"{int(last_stats.width)}x{int(last_stats.height)}", "spp": int(last_stats.spp),
                        "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)",
                        "pipelining": "serial (rr_render_frame per frame)" if args.serial else
-                                     "2 frames in flight: frame N encoded + written while N+1 renders",
+                                     "3 frames in flight: frame N encoded + written while N+1 renders and N+2 waits on its stream",
                        "view_transform_substituted": int(any(substituted))},
             "mrays_per_s_per_gpu": round(traced / elapsed / 1e6, 1),
             # SURVEY 8(d)'s form: rays traced over the summed render-kernel time

@@ -28,7 +28,7 @@ bool encode_jpeg_coeffs(const int16_t* coeffs, int W, int H, int quality, std::v
 void jpeg_header_bytes(int W, int H, int quality, std::vector<uint8_t>& out);
 void jpeg_huff_tables(uint32_t out[4 * 256]);
 bool encode_jpeg(const uint8_t* rgba, int W, int H, int quality, std::vector<uint8_t>& out, int threads = 0);
-bool encode_png(const uint8_t* rgba, int W, int H, std::vector<uint8_t>& out, int level = 1);
+bool encode_png(const uint8_t* rgba, int W, int H, std::vector<uint8_t>& out, int level = 1, int threads = 0);
 bool write_file(const std::string& path, const std::vector<uint8_t>& data);
 
 }  // namespace rr

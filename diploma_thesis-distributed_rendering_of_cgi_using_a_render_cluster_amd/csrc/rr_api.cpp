@@ -84,17 +84,17 @@ struct FrameRun {
 
 // One frame between rr_frame_submit and rr_frame_complete: its host-side
 // outputs (pinned, so the device-to-host copies stay asynchronous), events,
-// kernel profiler and the request. Two slots = the next queued frame renders
+// kernel profiler and the request. Several slots = the next queued frames render
 // while the host encodes and writes the previous one.
 struct FrameSlot {
     bool busy = false;
     uint64_t ticket = 0;
     // 0 start, 1 built, 4 image done (before the device JPEG coder), 2 stream
-    // work done, 3 outputs on the host (copy stream)
+    // work done, 3 outputs on the host (after their copies)
     hipEvent_t ev[5] = {};
     DevBuf<int32_t> counters;  // this frame's ray counters (swapped into DevPaths while enqueuing)
     // this frame's device outputs (swapped into DevPaths / rr_ctx while enqueuing):
-    // the copy stream reads them while the next frame's kernels write the other
+    // their copies to the host run while the next frames' kernels write the other
     // slot's, so no frame waits for its predecessor's device-to-host copies
     DevBuf<float4> film;
     DevBuf<uint8_t> rgba8;
@@ -153,10 +153,6 @@ struct rr_ctx {
     // frames (inspection entry points), the frame slot's stream while a frame is
     // enqueued (enqueue_frame SlotSwap)
     hipStream_t stream = nullptr;
-    // device-to-host copies of a frame's outputs run here, so the next frame's
-    // kernels on `stream` do not wait for them (the output buffers are per
-    // frame slot, FrameSlot::film / rgba8 / coeffs)
-    hipStream_t copy_stream = nullptr;
     DevPaths paths;
     // device JPEG transform (jpeg.hip): tables for the last quality, coefficients
     DevBuf<float> jpeg_tab;
@@ -213,7 +209,7 @@ void quiesce(rr_ctx* c) {
         if (sl.stream) RR_HIP(hipStreamSynchronize(sl.stream));
 }
 
-// Frames of the two slots overlap on the device when both render with k_tiles
+// Frames of different slots overlap on the device when both render with k_tiles
 // (RR_TUNE_OVERLAP=0: every frame waits for the one before, as on one stream).
 bool overlap_enabled() {
     static const bool on = !(getenv("RR_TUNE_OVERLAP") && atoi(getenv("RR_TUNE_OVERLAP")) == 0);
@@ -495,7 +491,7 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
         ProfSwap(KernelProfiler& x, KernelProfiler& y) : a(x), b(y) { std::swap(a, b); }
         ~ProfSwap() { std::swap(a, b); }
     } prof_swap(c->paths.prof, sl.prof);
-    struct CtrSwap {  // per-slot counters: the copy stream may still read the previous frame's
+    struct CtrSwap {  // per-slot counters: the previous frame's may still be on their way to the host
         DevBuf<int32_t>&a, &b;
         CtrSwap(DevBuf<int32_t>& x, DevBuf<int32_t>& y) : a(x), b(y) { std::swap(a, b); }
         ~CtrSwap() { std::swap(a, b); }
@@ -550,8 +546,9 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
         else jpeg_fdct_device(c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr, c->jpeg_coeffs.ptr, st);
     }
     RR_HIP(hipEventRecord(sl.ev[2], st));
-    hipStream_t cs = c->copy_stream;
-    RR_HIP(hipStreamWaitEvent(cs, sl.ev[2], 0));
+    // the outputs' device-to-host copies follow on the slot's own stream: the
+    // next frames run on the other slots' streams, so nothing waits for them
+    hipStream_t cs = st;
     if (sl.jpeg && !sl.jpeg_dev) {
         const size_t nc = jpeg_coeff_count(fs.W, fs.H);
         sl.host_coeffs.ensure(nc * sizeof(int16_t));
@@ -733,14 +730,15 @@ int rr_create(int device_ordinal, rr_ctx** out) {
         std::unique_ptr<rr_ctx> c(new rr_ctx());
         c->device = device_ordinal;
         set_device(c.get());
-        // The slots' streams first, so that each gets a hardware queue of its
-        // own (GPU_MAX_HW_QUEUES is 4, and the process's null stream holds
-        // one): streams created beyond that share a queue, and a queue runs
-        // its kernels in order, so frames of two slots on one queue cannot
-        // overlap. The home stream (inspection calls) is slot 0's.
+        // One stream per slot and no other, so that each gets a hardware queue
+        // of its own (GPU_MAX_HW_QUEUES is 4, and the process's null stream
+        // holds one): streams created beyond that share a queue, and a queue
+        // runs its kernels in order, so frames of two slots on one queue
+        // cannot overlap. The home stream (inspection calls) is slot 0's;
+        // with RR_MAX_FRAMES_IN_FLIGHT = 3 the three slots and the null stream
+        // take the four queues.
         for (auto& sl : c->slots) RR_HIP(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
         c->stream = c->slots[0].stream;
-        RR_HIP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
         if (const char* d = getenv("RR_OCIO_DIR")) {
             // a broken LUT directory does not fail the context: Filmic frames fall
             // back to Standard and carry the reason in rr_last_warning
@@ -760,7 +758,6 @@ void rr_destroy(rr_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& sl : c->slots)
         if (sl.stream) (void)hipStreamSynchronize(sl.stream);
-    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     c->paths.release();
     c->filmic.release();
     c->jpeg_tab.release();
@@ -773,7 +770,6 @@ void rr_destroy(rr_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         sl.prof.release();
     }
-    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     for (auto& sl : c->slots) {
         if (sl.stream) (void)hipStreamDestroy(sl.stream);  // c->stream is slot 0's
         sl.release_private();
@@ -955,7 +951,6 @@ int rr_synchronize(rr_ctx* c) {
     return guarded([&] {
         set_device(c);
         quiesce(c);
-        RR_HIP(hipStreamSynchronize(c->copy_stream));
         return RR_OK;
     });
 }

@@ -137,9 +137,9 @@ class BackendRunner:
         return frt, stats
 
     def render_frames(self, job: BlenderJob, frame_indices, on_frame=None) -> list:
-        """Render a worker's queued frames in order with frame N+1's device
-        work in flight while frame N is encoded and written (SURVEY.md §8f
-        rank 2). Every frame still gets its own file, FrameRenderTime and
+        """Render a worker's queued frames in order with frames N+1 and N+2's
+        device work in flight while frame N is encoded and written (SURVEY.md
+        §8f rank 2; RR_MAX_FRAMES_IN_FLIGHT pending at most). Every frame still gets its own file, FrameRenderTime and
         trace entry, exactly as render_frame would produce them; on_frame
         (frame_index, frt, stats) is called as each one completes."""
         frames = list(frame_indices)
@@ -219,7 +219,8 @@ class WorkerAutomaticQueue:
     Two differences, neither visible in the protocol:
       * no 100 ms poll (queue.rs:81): queue_frame wakes the loop through a
         condition variable, so a GPU frame of a few ms is not padded to 100 ms;
-      * up to `frames_in_flight` (2) frames render at once: frame N+1 is
+      * up to `frames_in_flight` (default 2, at most RR_MAX_FRAMES_IN_FLIGHT)
+        frames render at once: frame N+1 is
         submitted before frame N is completed, so N's encode and file write
         overlap N+1's device work. N+1 is marked RENDERING when it is
         SUBMITTED (under the queue lock, before the device call), so a steal
@@ -229,7 +230,7 @@ class WorkerAutomaticQueue:
     trace counters (trace_new_frame_queued, trace_frame_stolen_from_queue).
     """
 
-    def __init__(self, runner, on_finished=None, frames_in_flight: int = RR_MAX_FRAMES_IN_FLIGHT, logger=None):
+    def __init__(self, runner, on_finished=None, frames_in_flight: int = 2, logger=None):
         if not 1 <= frames_in_flight <= RR_MAX_FRAMES_IN_FLIGHT:
             raise ValueError(f"frames_in_flight must be 1..{RR_MAX_FRAMES_IN_FLIGHT}")
         self.runner = runner

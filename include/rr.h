@@ -43,7 +43,7 @@ extern "C" {
 #define RR_EBUSY (-16)   /* rr_frame_submit with RR_MAX_FRAMES_IN_FLIGHT frames pending */
 
 /* Frames a context keeps between rr_frame_submit and rr_frame_complete. */
-#define RR_MAX_FRAMES_IN_FLIGHT 2
+#define RR_MAX_FRAMES_IN_FLIGHT 3
 
 typedef struct rr_ctx rr_ctx;
 typedef struct rr_scene rr_scene;
@@ -187,6 +187,10 @@ int rr_render_frame(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,
  * intended loop is submit(N+1), complete(N): the host encodes and writes
  * frame N while the GPU renders N+1. At most RR_MAX_FRAMES_IN_FLIGHT frames
  * may be pending (RR_EBUSY otherwise); they complete in submission order.
+ * Each pending frame has its own stream: with three pending, frame N+2's
+ * device work is queued while N+1 renders, and starts on the CUs N+1 leaves
+ * idle before N's JPEG kernels (waiting behind N+1) have let the host
+ * complete N.
  * rr_render_frame == submit + complete. Same arguments and errors as
  * rr_render_frame; a failed complete still retires its ticket. */
 int rr_frame_submit(rr_ctx* ctx, rr_scene* scene, int32_t frame_index,

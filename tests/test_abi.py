@@ -112,13 +112,23 @@ def _test_image(w=67, h=45):
     return img
 
 
-def test_png_encoder_is_lossless(rr, tmp_path):
-    img = _test_image()
+@pytest.mark.parametrize("w,h", [(67, 45), (1, 1), (33, 17), (1920, 1080), (300, 1000)])
+def test_png_encoder_is_lossless(rr, tmp_path, w, h):
+    """Band-parallel deflate (one band below 32 rows, up to 16 bands): one
+    valid zlib stream whose pixels decode exactly (zlib and PIL check the
+    Adler-32 and the stored/final block structure)."""
+    import zlib
+    img = _test_image(w, h)
     n = rr.encode_image(img, str(tmp_path / "frame"), "PNG")
     path = tmp_path / "frame.png"
     assert path.is_file() and path.stat().st_size == n
     back = np.asarray(Image.open(path).convert("RGBA"))
     assert np.array_equal(back, img)
+    data = path.read_bytes()
+    i = data.index(b"IDAT")
+    ln = int.from_bytes(data[i - 4:i], "big")
+    raw = zlib.decompress(data[i + 4:i + 4 + ln])  # raises on a bad checksum or stream
+    assert len(raw) == (4 * w + 1) * h
 
 
 @pytest.mark.parametrize("w,h", [(67, 45), (16, 16), (1, 1), (1920, 1080)])

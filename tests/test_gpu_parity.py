@@ -386,12 +386,14 @@ def test_pipelined_frames_match_serial(ctx, rr, tmp_path, s04):
     byte-identical files to rr_render_frame, in submission order."""
     p = rr.default_params(width=160, height=90, spp=4)
     serial = {}
-    for f in (3, 4, 5):
+    for f in (3, 4, 5, 7):
         ctx.render_frame(s04, f, p, str(tmp_path / f"s{f}"), "JPEG", 90)
         serial[f] = (tmp_path / f"s{f}.jpg").read_bytes()
     t3 = ctx.submit_frame(s04, 3, p, str(tmp_path / "p3"), "JPEG", 90)
     t4 = ctx.submit_frame(s04, 4, p, str(tmp_path / "p4"), "JPEG", 90)
-    with pytest.raises(rr.RRError) as e:  # a third frame in flight
+    t7 = ctx.submit_frame(s04, 7, p, str(tmp_path / "p7"), "JPEG", 90)
+    assert rr.native.RR_MAX_FRAMES_IN_FLIGHT == 3
+    with pytest.raises(rr.RRError) as e:  # a fourth frame in flight
         ctx.submit_frame(s04, 5, p, str(tmp_path / "p5"), "JPEG", 90)
     assert e.value.code == rr.native.RR_EBUSY
     with pytest.raises(rr.RRError):  # out of order
@@ -399,9 +401,11 @@ def test_pipelined_frames_match_serial(ctx, rr, tmp_path, s04):
     tm3, st3 = ctx.complete_frame(t3)
     t5 = ctx.submit_frame(s04, 5, p, str(tmp_path / "p5"), "PNG", 90)
     tm4, _ = ctx.complete_frame(t4)
+    ctx.complete_frame(t7)
     tm5, _ = ctx.complete_frame(t5)
     assert (tmp_path / "p3.jpg").read_bytes() == serial[3]
     assert (tmp_path / "p4.jpg").read_bytes() == serial[4]
+    assert (tmp_path / "p7.jpg").read_bytes() == serial[7]
     assert (tmp_path / "p5.png").is_file()
     for tm in (tm3, tm4, tm5):
         assert tm.loaded_at <= tm.started_rendering_at <= tm.finished_rendering_at <= tm.file_saving_finished_at
@@ -431,7 +435,7 @@ def test_overlapped_frames_match_serial_across_paths(ctx, rr, tmp_path, s04):
             serial.append((tmp_path / f"s{i}.jpg").read_bytes())
         pending = []
         for i, (s, f, p) in enumerate(plan):
-            if len(pending) == 2:
+            if len(pending) == rr.native.RR_MAX_FRAMES_IN_FLIGHT:
                 ctx.complete_frame(pending.pop(0))
             pending.append(ctx.submit_frame(s, f, p, str(tmp_path / f"p{i}"), "JPEG", 90))
         for t in pending:

@@ -133,7 +133,7 @@ def test_serial_depth_and_failed_frame(rr, tmp_path):
         q.cancel()
         q.join(5)
     with pytest.raises(ValueError):
-        rr.WorkerAutomaticQueue(runner, frames_in_flight=3)
+        rr.WorkerAutomaticQueue(runner, frames_in_flight=rr.native.RR_MAX_FRAMES_IN_FLIGHT + 1)
 
 
 def test_cancel_stops_taking_frames(rr, tmp_path):
