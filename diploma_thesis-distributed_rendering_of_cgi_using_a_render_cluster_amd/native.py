@@ -21,7 +21,7 @@ RR_OK, RR_ENOENT, RR_EIO, RR_ENOMEM, RR_ENODEV, RR_EINVAL, RR_ENOTSUP = 0, -2, -
 RR_EBUSY = -16
 RR_MAX_FRAMES_IN_FLIGHT = 3
 RR_VIEW_SCENE, RR_VIEW_STANDARD, RR_VIEW_RAW, RR_VIEW_FILMIC = -1, 0, 1, 2
-RR_ABI_VERSION = 3
+RR_ABI_VERSION = 4
 RR_CAM_FLOATS, RR_LIGHT_FLOATS, RR_MAT_FLOATS, RR_RENDER_INTS, RR_RENDER_FLOATS = 16, 12, 12, 10, 4
 
 

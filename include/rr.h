@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 3
+#define RR_ABI_VERSION 4
 
 /* error codes (negative errno values) */
 #define RR_OK 0
