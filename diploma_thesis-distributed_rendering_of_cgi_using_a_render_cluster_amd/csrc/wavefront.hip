@@ -1787,7 +1787,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = mk3(1.0f, 1.0f, 1.0f), L = o;
             uint32_t lob = 0;
             float tmin = 0.0f, tmax = -1.0f;
-            bool culled = true, esc = false;
+            bool culled = true;
             if (valid) camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
             n_t0 += wave_count(!culled);
             bool live = valid;
@@ -1800,20 +1800,24 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     if (b == 0) {  // the camera ray against the tile's triangles (wave-uniform masks)
                         set_miss(h, tmax);
                         if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);
-                    } else if (esc) {  // left a hull side of its triangle (hull_flags): meets nothing
-                        set_miss(h, kFltMax);
                     } else {
                         traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, ce);
                     }
                     shade(fc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, fc.n_tris, st, cs});
                     cont = so.cont;
                     shadow = so.shadow;
-                    if (so.cont) {
+                    if (so.cont && so.esc) {
+                        // the continuation leaves a hull side of its triangle
+                        // (hull_flags): its next hit is the world, added here as
+                        // bounce b + 1's shade() would add it (T x world, clamped),
+                        // and the path ends without that iteration
+                        add_to(L, clamp_contrib(mul3(so.T, fc.world), fc.clamp_indirect));
+                        live = false;
+                    } else if (so.cont) {
                         o = so.o;
                         d = so.d;
                         T = so.T;
                         lob = so.lob;
-                        esc = so.esc;
                     } else {
                         live = false;
                     }
