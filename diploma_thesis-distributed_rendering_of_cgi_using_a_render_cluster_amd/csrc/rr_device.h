@@ -167,7 +167,7 @@ RR_HD float sqrt_any(float x) {
 #endif
     return sqrtf(x);
 }
-// IEEE reciprocal (the bits of 1.0f / b) for |b| in [2^-60, 2^60]. hipcc's
+// IEEE reciprocal (the bits of 1.0f / b) for |b| in [2^-126, 2^126). hipcc's
 // correctly rounded division is v_rcp_f32 refined by fused multiply-adds,
 // between v_div_scale (which rescales operands near the exponent limits) and
 // v_div_fixup (infinities, zeros, NaNs): 11 instructions. In that range
@@ -184,9 +184,27 @@ RR_HD float rcp_rn(float b) {
     return 1.0f / b;
 #endif
 }
+// sqrt(x) and 1 / sqrt(x) (the bits of sqrtf and of 1.0f / sqrtf): sqrt_rn
+// and rcp_rn when every active lane's x is in [2^-96, FLT_MAX] (the root then
+// lies in [2^-48, 2^64], inside rcp_rn's range), else the IEEE operations.
+RR_HD void sqrt_rcp_any(float x, float& s, float& r) {
+#if __HIP_DEVICE_COMPILE__
+    if (__all(x >= 0x1p-96f && x <= 3.40282347e38f)) {
+        s = sqrt_rn(x);
+        r = rcp_rn(s);
+        return;
+    }
+#endif
+    s = sqrtf(x);
+    r = 1.0f / s;
+}
 // norm3 for |a|^2 in [2^-96, FLT_MAX] (sqrt_rn; same bits as norm3)
 RR_HD float3 norm3_rn(float3 a) { return scl3(a, rcp_rn(sqrt_rn(dot3(a, a)))); }
-RR_HD float3 norm3_any(float3 a) { return scl3(a, 1.0f / sqrt_any(dot3(a, a))); }
+RR_HD float3 norm3_any(float3 a) {
+    float s, r;
+    sqrt_rcp_any(dot3(a, a), s, r);
+    return scl3(a, r);
+}
 RR_HD float max3f(float3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
 RR_HD float3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
 

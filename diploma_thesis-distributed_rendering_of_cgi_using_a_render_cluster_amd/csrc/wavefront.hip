@@ -292,7 +292,9 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
             const float3 tl = sub3(lp, P);
             const float dl2 = dot3(tl, tl);
             if (radius > 0.0f) {
-                const float3 wl = scl3(tl, 1.0f / sqrt_any(dl2));
+                float sl, rl;
+                sqrt_rcp_any(dl2, sl, rl);
+                const float3 wl = scl3(tl, rl);
                 float3 b1, b2;
                 make_onb(wl, b1, b2);
                 float dx, dy;
@@ -302,14 +304,15 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
                 const float3 sp = madd3(madd3(lp, b1, dx), b2, dy);
                 const float3 ts = sub3(sp, P);
                 const float ds2 = dot3(ts, ts);
-                dist = sqrt_any(ds2);
-                const float id = 1.0f / dist;
+                float id;
+                sqrt_rcp_any(ds2, dist, id);
                 wi = scl3(ts, id);
                 const float cl = fabsf(dot3(wl, wi));
                 Li = scl3(I, cl * id * id);
             } else {
-                dist = sqrt_any(dl2);
-                wi = scl3(tl, 1.0f / dist);
+                float id;
+                sqrt_rcp_any(dl2, dist, id);
+                wi = scl3(tl, id);
                 Li = scl3(I, 1.0f / dl2);
             }
         } else {  // sun: delta direction, irradiance
@@ -2460,7 +2463,7 @@ namespace {
 // and 1.0f / x over the float bit patterns [lo, lo + n): counts[0] = sqrt_rn
 // mismatches with the argument in its range (+-0 or [2^-96, FLT_MAX]),
 // counts[1] = sqrt_rn mismatches outside it, counts[2] = sqrt_any mismatches
-// anywhere, counts[3] = rcp_rn mismatches with |x| in [2^-60, 2^60],
+// anywhere, counts[3] = rcp_rn mismatches with |x| in [2^-126, 2^126),
 // counts[4] = rcp_rn mismatches outside (NaN equals NaN). 16 patterns a lane.
 __global__ void k_debug_fastmath(uint32_t lo, uint64_t n, unsigned long long* __restrict__ counts) {
     unsigned long long c[5] = {0, 0, 0, 0, 0};
@@ -2472,7 +2475,7 @@ __global__ void k_debug_fastmath(uint32_t lo, uint64_t n, unsigned long long* __
         const bool in = (x >= 0x1p-96f && x <= 3.40282347e38f) || x == 0.0f;
         if (!same(sqrt_rn(x), ref)) ++c[in ? 0 : 1];
         if (!same(sqrt_any(x), ref)) ++c[2];
-        const bool rin = fabsf(x) >= 0x1p-60f && fabsf(x) <= 0x1p60f;
+        const bool rin = fabsf(x) >= 0x1p-126f && fabsf(x) < 0x1p126f;
         if (!same(rcp_rn(x), 1.0f / x)) ++c[rin ? 3 : 4];
     }
     for (int i = 0; i < 5; ++i)

@@ -317,7 +317,7 @@ int rr_debug_bsdf_sample(rr_ctx* ctx, const float* mat12, const float* n3, const
  * sqrt_rn mismatches with the argument in its range (+-0 or [2^-96, FLT_MAX];
  * must be 0), [1] = sqrt_rn mismatches outside it (not called there), [2] =
  * sqrt_any mismatches (must be 0), [3] = rcp_rn mismatches with |x| in
- * [2^-60, 2^60] (must be 0), [4] = rcp_rn mismatches outside it. Test
+ * [2^-126, 2^126) (must be 0), [4] = rcp_rn mismatches outside it. Test
  * infrastructure for the bit-exactness claim; no reference counterpart. */
 int rr_debug_fastmath_check(rr_ctx* ctx, uint32_t lo, uint64_t n, uint64_t* counts5);
 

@@ -14,7 +14,8 @@ def test_fast_sqrt_and_reciprocal_match_ieee_on_every_float(ctx):
           f"rcp_rn: {rc_in} in range, {rc_out} outside")
     assert sq_in == 0  # +-0 and [2^-96, FLT_MAX]: every call site of sqrt_rn stays in there
     assert sq_any == 0  # the guarded form is exact everywhere
-    assert rc_in == 0  # |x| in [2^-60, 2^60]: every call site of rcp_rn stays in there
+    assert rc_in == 0  # |x| in [2^-126, 2^126): every call site of rcp_rn stays in there
+    assert rc_out > 0  # subnormals, zero and |x| >= 2^126 need the division's wrappers
     assert sq_out > 0  # the range restriction is real (subnormals, tiny normals, inf)
 
 
