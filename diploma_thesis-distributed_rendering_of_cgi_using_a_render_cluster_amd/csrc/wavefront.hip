@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
 // path computes (and the per-path order of radiance additions) does not, so
 // images stay bit-identical to the fused kernels' and the oracle's.
 #ifndef RR_REFILL_BELOW
-#define RR_REFILL_BELOW 44
+#define RR_REFILL_BELOW 52
 #endif
 constexpr int kRefillBelow = RR_REFILL_BELOW;
 // Waves per SIMD of the trace kernels (their launch bounds; ≤ 64 VGPRs at 8,
