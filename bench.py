@@ -290,33 +290,46 @@ def spawn_ranks(args) -> int:
     return max(abs(p.wait()) for p in procs)
 
 
-def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin frame 1"):
+def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin frame 1", spp_scale: float = 1.0):
     """Oracle (C restatement, OpenMP) on the host cores: 4-row bands of the same
     frame, taken in an order spread over the image, until the budget is spent or
-    the frame is done; extrapolated to frames/s. Threads: OMP_NUM_THREADS when
-    the environment sets it (the GPU box gives one GPU's job a 16-core share
-    and sets it; nproc there counts the whole machine), else every core this
-    process may run on."""
+    the frame is done; extrapolated to frames/s with ONE hierarchy build per
+    frame (each band call rebuilds it; its build time, orc_last_build_seconds,
+    is taken out of the band's time and counted once). Threads: OMP_NUM_THREADS
+    when the environment sets it (the GPU box gives one GPU's job a 16-core
+    share and sets it; nproc there counts the whole machine), else every core
+    this process may run on. spp_scale: the frame's samples over the samples
+    rendered (render time is linear in spp; the build is not)."""
     H = int(state.render_ints[1])
     usable, nproc, model = host_cpu()
     threads = int(os.environ.get("OMP_NUM_THREADS") or usable)
     bands = list(range(0, H, 4))
-    done_rows, t_used = 0, 0.0
+    done_rows, t_used, t_render, builds = 0, 0.0, 0.0, []
     order = [b for k in range(16) for b in bands[k::16]]
     for b in order:
         t0 = time.perf_counter()
         oracle_mod.render_state(state, rows=(b, min(b + 4, H)), threads=threads, film=False)
-        t_used += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        tb = min(oracle_mod.last_build_seconds(), dt)
+        builds.append(tb)
+        t_used += dt
+        t_render += dt - tb
         done_rows += min(b + 4, H) - b
         if t_used >= budget_s:
             break
     frac = done_rows / H
-    return {"value": frac / t_used, "unit": "frames/s", "cores": threads, "kind": "port",
+    t_build = sum(builds) / len(builds)
+    t_frame = t_build + t_render / frac * spp_scale
+    return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads, "kind": "port",
             "host": {"nproc": nproc, "affinity_cores": usable, "cpu_model": model,
                      "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
             "sample": f"{done_rows} of {H} rows (4-row bands spread over the frame) of {label} "
                       f"at {int(state.render_ints[0])}x{H}, {int(state.render_ints[2])} spp, "
-                      f"{t_used:.1f} s, extrapolated to whole frames; render only (no encode)"}
+                      f"{t_used:.1f} s in {len(builds)} band calls; frame time = one hierarchy build "
+                      f"({t_build:.3f} s) + the bands' render time extrapolated to the whole frame; "
+                      f"render only (no encode)"
+                      + (f"; rendered at {int(state.render_ints[2])} spp, render time scaled by {spp_scale:g}"
+                         if spp_scale != 1.0 else "")}
 
 
 def names_idx(cls: str, rr) -> int:
@@ -534,11 +547,8 @@ def main():
                 spp_full = int(last_stats.spp)
                 spp_cpu = min(spp_full, 128)
                 state = runner.ctx.frame_state(scene, f_count, rr.default_params(spp=spp_cpu))
-                cpu = cpu_baseline(O, state, args.cpu_seconds,
-                                   f"{args.workload} frame {f_count} (each band call includes the oracle's BVH build)")
-                if spp_cpu != spp_full:
-                    cpu["value"] = cpu["value"] * spp_cpu / spp_full
-                    cpu["sample"] += f"; rendered at {spp_cpu} spp and scaled to {spp_full} spp"
+                cpu = cpu_baseline(O, state, args.cpu_seconds, f"{args.workload} frame {f_count}",
+                                   spp_scale=spp_full / spp_cpu)
             except Exception as e:  # baseline is reported, never the target
                 cpu = {"value": None, "unit": "frames/s", "error": str(e)}
         traced = rays["camera_traced"] + rays["extension"] + rays["shadow"]

@@ -239,6 +239,13 @@ def material_lut(mat12) -> np.ndarray:
     return out
 
 
+def last_build_seconds() -> float:
+    """Wall seconds the last render() spent building its hierarchy."""
+    L = lib()
+    L.orc_last_build_seconds.restype = ctypes.c_double
+    return float(L.orc_last_build_seconds())
+
+
 def ray_counts():
     """Ray statistics of the last render (test/debug): (continuations at bounce 0,
     shadow rays at bounce 0, continuations later, shadow rays later) and the

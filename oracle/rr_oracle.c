@@ -36,6 +36,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -959,6 +960,14 @@ static unsigned tri_hull(const lbvh* B, int i) {
 }
 
 static long long g_rays[4];
+/* wall seconds of the last orc_render's hierarchy build (orc_last_build_seconds):
+ * the CPU baseline counts one build per frame, not one per rendered band */
+static double g_build_s;
+static double wall_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 static int g_late[32], g_n_late;
 
 static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
@@ -1299,6 +1308,8 @@ int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* h
  * frame can be timed. threads <= 0: OpenMP default. */
 #define ORC_FILM_GROUP 32
 
+double orc_last_build_seconds(void) { return g_build_s; }
+
 void orc_ray_counts(long long* out4, int* late32, int* n_late) {
     for (int k = 0; k < 4; ++k) out4[k] = g_rays[k];
     for (int k = 0; k < 2 * g_n_late; ++k) late32[k] = g_late[k];
@@ -1311,8 +1322,10 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     memset(g_rays, 0, sizeof g_rays);
     g_n_late = 0;
     lbvh B;
+    const double t_build = wall_s();
     lbvh_build(&B, n_tris, tris9, tri_mat, (ri[7] == 3 || ri[7] == 4) ? 3 : 2);  /* the hierarchy the product walks */
     if (ri[7] == 4) { lbvh_collapse4(&B); B.width = 4; }
+    g_build_s = wall_s() - t_build;
     scene_t* S = (scene_t*)calloc(1, sizeof(scene_t));
     S->bvh = &B;
     S->cam = cam;
