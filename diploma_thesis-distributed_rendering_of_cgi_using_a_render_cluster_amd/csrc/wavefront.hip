@@ -1045,14 +1045,11 @@ __global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq,
 #define RR_REFILL_BELOW 52
 #endif
 constexpr int kRefillBelow = RR_REFILL_BELOW;
-// Waves per SIMD of the trace kernels (their launch bounds; ≤ 64 VGPRs at 8,
-// ≤ 72 at 7): hierarchies that stay in the caches (02 / 03: 92k / 412k
-// triangles) trace faster with more rays in flight (8 against 7: 02 / 03
-// frames at 64 spp −3.7 %), the 10.5M-triangle C5 slower (8 spp 102 -> 113 ms:
-// more rays in flight thrash L2/MALL), so the choice follows the triangle
-// count (render_split).
-constexpr int kTraceWavesLarge = 7, kTraceWavesCached = 8;
-constexpr int kTraceCachedTris = 2000000;
+// Waves per SIMD of the trace kernels (their launch bounds: <= 64 VGPRs):
+// 8 against 7 measured 02 / 03 frames at 64 spp -3.7 / -3.8 %, C5 at 16 spp
+// -2.7 % (with the quantised BVH4 and windowed ray order; over round 1's
+// BVH2 walk C5 had been slower at 8, 102 -> 113 ms).
+constexpr int kTraceWaves = 8;
 // Hierarchy of the split path: the PLOC BVH2 collapsed to the quantised BVH4
 // (measured against walking the PLOC BVH2 itself, C5 / 02 / 03 frames at 16 /
 // 64 / 64 spp: 191 -> 139, 174 -> 149, 192 -> 160 ms).
@@ -1221,8 +1218,8 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
 }
 
 // Camera paths: raygen + closest hit -> hits[p].
-template <bool kCount, int kWaves>
-__global__ __launch_bounds__(kBlock, kWaves) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
                                                                           float2* __restrict__ hits,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc,
@@ -1331,8 +1328,8 @@ RR_D void packet_trace(const QNode4* __restrict__ nodes, const TriPack* __restri
 // Camera paths as packets: a wave traces the 64 camera rays of one 8x8 pixel
 // tile (one sample) with packet_trace. Tiles are dealt to the waves as
 // trace_refill deals chunks (round-robin over the XCD-ordered waves).
-template <bool kCount, int kWaves>
-__global__ __launch_bounds__(kBlock, kWaves) void k_trace_primary_packet(
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
     FrameConsts fc, SceneArgs sa, int np, float2* __restrict__ hits, int32_t* __restrict__,
     unsigned long long* __restrict__ tc, uint32_t* __restrict__ traced) {
     __shared__ int stack_all[kWavesPerBlock * kPacketStack];
@@ -1397,8 +1394,8 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
 }
 
 // Extension rays entering bounce b: closest hit -> hits[slot].
-template <bool kCount, int kWaves>
-__global__ __launch_bounds__(kBlock, kWaves) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
                                                                          float2* __restrict__ hits,
                                                                          int32_t* __restrict__ spill,
                                                                          unsigned long long* __restrict__ tc) {
@@ -1452,8 +1449,8 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
 }
 
 // Shadow rays with lane refill: unoccluded -> radiance += contribution.
-template <bool kCount, int kWaves>
-__global__ __launch_bounds__(kBlock, kWaves) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
+template <bool kCount>
+__global__ __launch_bounds__(kBlock, kTraceWaves) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
                                                                           Rad rad,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc) {
@@ -2203,16 +2200,11 @@ struct SplitGrids {
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
     void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
-    template <int kW>
-    void pick(bool count) {
-        ktp = count ? k_trace_primary<true, kW> : k_trace_primary<false, kW>;
-        kte = count ? k_trace_extend<true, kW> : k_trace_extend<false, kW>;
-        kts = count ? k_shadow_refill<true, kW> : k_shadow_refill<false, kW>;
-        ktpk = count ? k_trace_primary_packet<true, kW> : k_trace_primary_packet<false, kW>;
-    }
-    SplitGrids(bool count, int n_tris) {
-        if (n_tris <= kTraceCachedTris) pick<kTraceWavesCached>(count);
-        else pick<kTraceWavesLarge>(count);
+    explicit SplitGrids(bool count) {
+        ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
+        kte = count ? k_trace_extend<true> : k_trace_extend<false>;
+        kts = count ? k_shadow_refill<true> : k_shadow_refill<false>;
+        ktpk = count ? k_trace_primary_packet<true> : k_trace_primary_packet<false>;
         trace_p = grid_for(ktp, 0);
         trace_e = grid_for(kte, 0);
         shadow = grid_for(kts, 0);
@@ -2283,7 +2275,7 @@ namespace {
 void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_t st, const SceneArgs& sa,
                   unsigned long long* tc, PathQueue pq[2], const ShadowQueue& sq) {
     KernelProfiler& pr = p.prof;
-    const SplitGrids G(tc != nullptr, base.n_tris);
+    const SplitGrids G(tc != nullptr);
     const int npix = base.npix;
     const int cpc = counters_per_chunk(base.max_bounces);
     // camera rays as packets (packet_trace) when triangles are large on screen:
