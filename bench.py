@@ -533,10 +533,19 @@ def main():
         if not args.no_profile:
             dom = max(range(len(names)), key=lambda k: roof_ms[k])
             roofline = roofline_line(args, names[dom], cstats, roof_ms, roof_launches, names, roof_steps)
+            if roofline.get("bound") == "valu" and roofline.get("valu_per_launch") and solo:
+                # the same VALU work issued over the timed region's wall time (frames
+                # overlapping, work units not cut by sample group when a frame overlaps
+                # a pending one): a lower bound of the issue rate the kernel sustains there
+                k = names_idx("tiles", rr)
+                rate = roofline["valu_per_launch"] * launches[k] / t_max / 1e9
+                roofline["achieved_timed_region"] = round(rate, 1)
+                roofline["frac_timed_region"] = round(rate / roofline["peak"], 3)
             roofline["launch_timing"] = (
                 f"HIP events around each launch on the library's stream, {roof_steps} frames rendered one at a "
                 "time after the timed region (in the timed region consecutive k_tiles frames overlap on the "
-                "device, and an event pair would also span the wait for the previous frame's CUs)" if solo else
+                "device, and an event pair would also span the wait for the previous frame's CUs; a frame "
+                "rendered alone cuts its tiles into sample-group units, an overlapping one does not)" if solo else
                 "HIP events around each launch on the library's stream over the timed region")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

@@ -157,6 +157,7 @@ struct DevPaths {
     KernelProfiler prof;
     bool count_traversal = false;
     bool force_wavefront = false;  // RR_FLAG_WAVEFRONT: LDS-resident scenes skip k_tiles
+    bool tile_whole = false;       // k_tiles: one work unit per tile (the frame overlaps a pending one)
     int grid_blocks = 0;  // persistent grid for path kernels
     void ensure_paths(size_t n);
     void ensure_tiles();  // k_tiles: only the traversal stack spill area

@@ -485,6 +485,14 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     if (prev && prev != &sl && !(overlap_enabled() && sl.tiles && prev->tiles))
         RR_HIP(hipStreamWaitEvent(st, prev->ev[2], 0));
     c->last_enqueued = &sl;
+    // a k_tiles frame enqueued while another k_tiles frame is pending overlaps
+    // it: whole-tile work units (render_frame_device); a frame rendered alone
+    // (rr_render_frame, the first of a batch) slices its tiles by sample group.
+    // Scheduling only: both give the same bits.
+    bool pending_tiles = false;
+    for (auto& o : c->slots)
+        if (&o != &sl && o.busy && o.tiles) pending_tiles = true;
+    c->paths.tile_whole = overlap_enabled() && sl.tiles && pending_tiles;
     sl.prof.reset((fs.flags & RR_FLAG_PROFILE_KERNELS) != 0);
     struct ProfSwap {  // the device code records into paths.prof; swapped back on every exit
         KernelProfiler &a, &b;

@@ -1782,10 +1782,20 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         // no triangle can be hit from this tile (wave-uniform): every sample is
         // the world term, summed as the sample loop would (0 + world + ...)
         const int s_run = (cm0 | cm1) != 0 ? s_hi : s_lo;
+        // film sum order: in order within groups of kFilmGroup samples, the
+        // group sums in order (one group per unit when tiles are sliced)
+        float3 P = mk3(0.0f, 0.0f, 0.0f);
+        auto group_end = [&](int s) {
+            if ((s + 1) % kFilmGroup == 0 || s + 1 == s_hi) {
+                acc.x = acc.x + P.x;
+                acc.y = acc.y + P.y;
+                acc.z = acc.z + P.z;
+                P = mk3(0.0f, 0.0f, 0.0f);
+            }
+        };
         for (int s = s_run; s < s_hi; ++s) {
-            acc.x = acc.x + fc.world.x;
-            acc.y = acc.y + fc.world.y;
-            acc.z = acc.z + fc.world.z;
+            add_to(P, fc.world);
+            group_end(s);
         }
         for (int s = s_lo; s < s_run; ++s) {
             const uint32_t key = sample_key(pk, (uint32_t)s);
@@ -1838,9 +1848,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     n_s1 += wave_count(shadow);
                 }
             }
-            acc.x = acc.x + L.x;
-            acc.y = acc.y + L.y;
-            acc.z = acc.z + L.z;
+            add_to(P, L);
+            group_end(s);
         }
         if (nk > 1) {  // one group of a sliced tile: its sum goes to the slab, k_tiles_fold adds them up
             float* const slab = sl.slab + (size_t)t * sl.floats + (size_t)k * 192;
@@ -2365,7 +2374,12 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
             RR_HIP(hipMemsetAsync(p.tile_cost.ptr, 0, sizeof(uint32_t) * tiles, st));
         }
         p.tile_order.ensure((size_t)tiles);
-        TileSlices sl{film_groups(base.spp_total), (size_t)192 * film_groups(base.spp_total), nullptr,
+        // units: one per (box tile, sample group) when the frame runs alone, so
+        // the heaviest tiles do not finish the launch on a nearly empty chip;
+        // one per tile (every group of it, summed in order in the unit) when
+        // the frame overlaps a pending one (p.tile_whole): the other frame's
+        // waves fill the tail, and the slab writes and the fold launch go
+        TileSlices sl{p.tile_whole ? 1 : film_groups(base.spp_total), (size_t)192 * film_groups(base.spp_total), nullptr,
                       p.tile_order.ptr, p.tile_cost.ptr};
         if (sl.n > 1) {
             p.tile_slab.ensure(sl.floats * (size_t)tiles);
