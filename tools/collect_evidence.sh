@@ -10,6 +10,11 @@ for p in "" _01 _02 _03 _c5; do
     cp $d/trace/run_kernel_stats.csv profiles/${tag}${p}_kernel_stats.csv
     cp $d/${tag}${p}_pmc.json profiles/${tag}_pmc${p}.json
     grep '^{' $d/trace_bench.json > profiles/${tag}${p}_bench_under_rocprof.json
+    if [ -f $d/${tag}${p}_serial_kernel_stats.md ]; then
+        cp $d/${tag}${p}_serial_kernel_stats.md profiles/${tag}${p}_serial_kernel_stats.md
+        cp $d/trace_serial/run_kernel_stats.csv profiles/${tag}${p}_serial_kernel_stats.csv
+        grep '^{' $d/trace_serial_bench.json > profiles/${tag}${p}_serial_bench_under_rocprof.json
+    fi
 done
 for wl in 04vs 01 02 03 c5 04vs_serial; do
     grep '^{' gpurun_out/ev/bench_$wl.json > profiles/${tag}_bench_$wl.json

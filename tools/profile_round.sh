@@ -15,11 +15,25 @@ mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 
 if [ "$wl" == "c5" ]; then steps="--steps 2 --warmup 1"; psteps="--steps 1 --warmup 1"; else steps="--steps 10 --warmup 2"; psteps="--steps 3 --warmup 1"; fi
-B="bench.py --workload $wl $psteps --no-cpu-baseline --no-profile $extra"
+# LDS-tile workloads (04vs, 01): frames overlap in the pipelined bench, so
+# launches run as whole-tile units that share the chip with their neighbours
+# and a traced launch's span is not its own cost. The counter passes and a
+# second trace therefore run the frames serially (sample-group units, one
+# launch on the chip at a time): the same launches the bench's solo pass
+# times for the roofline, so the per-launch VALU count and that trace's
+# average duration describe one kernel configuration.
+ser=""
+if [ "$wl" == "04vs" ] || [ "$wl" == "01" ]; then ser="--serial"; fi
+B="bench.py --workload $wl $psteps --no-cpu-baseline --no-profile $ser $extra"
 
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
     -- python3 bench.py --workload $wl $steps --no-cpu-baseline $extra > "$out/trace_bench.json"
 echo "trace done"
+if [ -n "$ser" ]; then
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace_serial" -o run \
+        -- python3 bench.py --workload $wl $steps --no-cpu-baseline --serial $extra > "$out/trace_serial_bench.json"
+    echo "serial trace done"
+fi
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- python3 $B > /dev/null
 echo "fetch done"
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- python3 $B > /dev/null
@@ -33,5 +47,8 @@ timeout -s KILL 240 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WA
     --output-format csv -d "$out/sq2" -o run -- python3 $B > /dev/null
 echo "sq2 done"
 python3 tools/pmc_summary.py stats "$out/trace" > "$out/${tag}_kernel_stats.md"
+if [ -n "$ser" ]; then
+    python3 tools/pmc_summary.py stats "$out/trace_serial" > "$out/${tag}_serial_kernel_stats.md"
+fi
 python3 tools/pmc_summary.py traffic --fetch "$out/fetch" --write "$out/write" --sq "$out/sq1" --sq "$out/sq2" \
     -o "$out/${tag}_pmc.json"
