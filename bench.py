@@ -268,11 +268,131 @@ def host_cpu():
     return usable, os.cpu_count() or 1, model
 
 
+def _read_sysfs(path: str):
+    try:
+        with open(path) as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
+
+
+def parse_cpulist(s: str | None) -> set:
+    """sysfs cpulist ("0-3,8,10-11") -> set of CPU ids."""
+    out = set()
+    for part in (s or "").split(","):
+        part = part.strip()
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def gpu_numa_nodes(sysfs: str = "/sys") -> list:
+    """NUMA node of every GPU in HIP's enumeration order — the GPU nodes of the
+    KFD topology in node order — read from sysfs without touching a GPU:
+    the node's PCI address (properties domain / location_id = bus << 8 |
+    device << 3 | function) -> /sys/bus/pci/devices/<bdf>/numa_node. -1 where
+    unknown; [] without a KFD topology (CPU containers)."""
+    base = os.path.join(sysfs, "class/kfd/kfd/topology/nodes")
+    try:
+        ids = sorted(int(x) for x in os.listdir(base) if x.isdigit())
+    except OSError:
+        return []
+    out = []
+    for i in ids:
+        props = _read_sysfs(os.path.join(base, str(i), "properties")) or ""
+        kv = dict(ln.split()[:2] for ln in props.splitlines() if len(ln.split()) >= 2)
+        if int(kv.get("simd_count", "0")) <= 0:
+            continue  # a CPU node
+        loc, dom = int(kv.get("location_id", "0")), int(kv.get("domain", "0"))
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
+        node = _read_sysfs(os.path.join(sysfs, "bus/pci/devices", bdf, "numa_node"))
+        out.append(int(node) if node not in (None, "") else -1)
+    return out
+
+
+def gpu_placement(devices: list, allowed: set, numa: list, node_cpus) -> list:
+    """Host CPUs per rank (rank r drives GPU devices[r]): the CPUs of its GPU's
+    NUMA node that this process may use, split into disjoint contiguous
+    shares among the ranks whose GPUs sit on that node; ranks whose GPU's
+    node is unknown (or has none of the allowed CPUs) share what is left of
+    `allowed` the same way. One worker pinned per GPU as the reference pins
+    one per node slot (scripts/arnes/queue-batch_04vs_14400f-10w_dynamic.sh:
+    6-10,59). node_cpus(n) -> set of CPU ids of NUMA node n."""
+    groups: dict = {}
+    for r, d in enumerate(devices):
+        n = numa[d] if 0 <= d < len(numa) else -1
+        if n < 0 or not (node_cpus(n) & allowed):
+            n = None
+        groups.setdefault(n, []).append(r)
+    plan: list = [set() for _ in devices]
+    used = set()
+    for n in sorted((k for k in groups if k is not None)):
+        pool = sorted(node_cpus(n) & allowed)
+        used.update(pool)
+        _split(pool, groups[n], plan)
+    if None in groups:
+        rest = sorted(allowed - used) or sorted(allowed)
+        _split(rest, groups[None], plan)
+    return plan
+
+
+def _split(pool: list, ranks: list, plan: list):
+    k = len(ranks)
+    for j, r in enumerate(ranks):
+        share = pool[j * len(pool) // k:(j + 1) * len(pool) // k]
+        plan[r] = set(share) if share else {pool[j % len(pool)]}
+
+
+def rank_placement(local_rank: int, devices: list) -> dict:
+    """This rank's CPU set and GPU NUMA node (computed identically by every
+    local rank, so the sets are disjoint)."""
+    numa = gpu_numa_nodes()
+    allowed = set(os.sched_getaffinity(0))
+    plan = gpu_placement(devices, allowed, numa,
+                         lambda n: parse_cpulist(_read_sysfs(f"/sys/devices/system/node/node{n}/cpulist")))
+    d = devices[local_rank]
+    return {"device": d, "numa_node": numa[d] if 0 <= d < len(numa) else -1, "cpus": sorted(plan[local_rank])}
+
+
+def pin_rank(place: dict):
+    """Pins this process (before any GPU call) to its CPU share and caps the
+    host threads of the oracle / OpenMP to it; librr's encoders size their
+    pools from the affinity mask (image_io.cpp encoder_threads)."""
+    os.sched_setaffinity(0, place["cpus"])
+    cap = len(place["cpus"])
+    omp = int(os.environ.get("OMP_NUM_THREADS") or cap)
+    os.environ["OMP_NUM_THREADS"] = str(max(1, min(omp, cap)))
+
+
+def cpuset_str(cpus) -> str:
+    """[0, 1, 2, 5] -> "0-2,5"."""
+    cpus, out = sorted(cpus), []
+    i = 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def physical_devices(n: int) -> list:
+    """GPU indices (HIP's enumeration of the whole machine) of local ranks 0..n-1:
+    the parent's HIP_VISIBLE_DEVICES list when set, else 0..n-1."""
+    visible = os.environ.get("HIP_VISIBLE_DEVICES")
+    devs = visible.split(",") if visible else [str(i) for i in range(n)]
+    return [int(x) if x.strip().isdigit() else i for i, x in enumerate(devs[:n])]
+
+
 def spawn_ranks(args) -> int:
     """--gpus N with no launcher: N child processes of this script, rank i on
-    GPU i (HIP_VISIBLE_DEVICES, mapped through the parent's own list), gloo
-    rendezvous on 127.0.0.1. Started before this process touches a GPU; the
-    children's rank 0 prints the line. Returns the worst exit code."""
+    GPU i (HIP_VISIBLE_DEVICES, mapped through the parent's own list), each
+    pinned to its GPU's NUMA node share (gpu_placement), gloo rendezvous on
+    127.0.0.1. Started before this process touches a GPU; the children's
+    rank 0 prints the line. Returns the worst exit code."""
     with socket.socket() as s_:
         s_.bind(("127.0.0.1", 0))
         port = s_.getsockname()[1]
@@ -281,11 +401,14 @@ def spawn_ranks(args) -> int:
     if len(devs) < args.gpus:
         print(f"bench.py: --gpus {args.gpus} but HIP_VISIBLE_DEVICES lists {len(devs)}", file=sys.stderr)
         return 2
+    phys = physical_devices(args.gpus)
     procs = []
     for r in range(args.gpus):
+        place = rank_placement(r, phys)
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(args.gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HIP_VISIBLE_DEVICES=devs[r], RR_BENCH_DEVICE="0",
-                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+                   RR_BENCH_PLACEMENT=json.dumps(place))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     return max(abs(p.wait()) for p in procs)
 
@@ -407,6 +530,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = int(os.environ.get("RR_BENCH_DEVICE", local))
+    placement = None
+    if world > 1:  # one worker pinned per GPU, before any GPU call (spawn_ranks or torchrun)
+        if "RR_BENCH_PLACEMENT" in os.environ:
+            placement = json.loads(os.environ["RR_BENCH_PLACEMENT"])
+        else:
+            n_local = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+            phys = ([device] * n_local if "RR_BENCH_DEVICE" in os.environ else physical_devices(n_local))
+            placement = rank_placement(local, phys)
+        pin_rank(placement)
+        placement = {**placement, "cpus": cpuset_str(placement["cpus"]),
+                     "omp_num_threads": int(os.environ["OMP_NUM_THREADS"])}
     import torch  # first, as in every bench run so far: the HIP runtime librr binds to is torch's
     gpu = torch.cuda.is_available()
     if gpu:
@@ -441,10 +575,11 @@ def main():
         mine = [frame_of(args.warmup + s) for s in range(args.steps)]
         barrier()
         t_max = reduce_max_seconds(time.perf_counter() - t0, dist)
-        by_rank = [mine]
+        by_rank, places = [mine], [placement]
         if dist is not None:
-            by_rank = [None] * world
+            by_rank, places = [None] * world, [None] * world
             dist.all_gather_object(by_rank, mine)
+            dist.all_gather_object(places, placement)
         if rank == 0:
             print(json.dumps({"metric": wl["metric"], "value": None, "unit": "frames/s", "n_gpus": world,
                               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 6),
@@ -452,7 +587,7 @@ def main():
                               "data": "dry run: no frames rendered", "dry_run": True,
                               "config": {"workload": wl["workload"], "job": os.path.basename(wl["job"]),
                                          "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)"},
-                              "frames_by_rank": by_rank}), flush=True)
+                              "frames_by_rank": by_rank, "placement_by_rank": places}), flush=True)
         shutil.rmtree(outdir, ignore_errors=True)
         if dist is not None:
             dist.destroy_process_group()
@@ -496,6 +631,10 @@ def main():
     elapsed = time.perf_counter() - t0
     last_stats = runner.last_stats
     t_max = reduce_max_seconds(elapsed, dist)
+    places = [placement]
+    if dist is not None:
+        places = [None] * world
+        dist.all_gather_object(places, placement)
 
     # Per-launch kernel times for the roofline. When consecutive k_tiles frames
     # overlap on the device (the two frame slots' streams, rr_api.cpp
@@ -571,7 +710,8 @@ def main():
                        "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)",
                        "pipelining": "serial (rr_render_frame per frame)" if args.serial else
                                      "3 frames in flight: frame N encoded + written while N+1 renders and N+2 waits on its stream",
-                       "view_transform_substituted": int(any(substituted))},
+                       "view_transform_substituted": int(any(substituted)),
+                       "placement_by_rank": places},
             "mrays_per_s_per_gpu": round(traced / elapsed / 1e6, 1),
             # SURVEY 8(d)'s form: rays traced over the summed render-kernel time
             # (kernels timed alone, see roofline.launch_timing)

@@ -800,11 +800,6 @@ __global__ __launch_bounds__(kBlock) void k_upload(UploadArgs a) {
     }
 }
 
-bool small_build_enabled() {
-    static const bool on = !(getenv("RR_TUNE_SMALL_BUILD") && atoi(getenv("RR_TUNE_SMALL_BUILD")) == 0);
-    return on;
-}
-
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 void exclusive_scan(DevScene& s, uint32_t* data, int m, hipStream_t st) {
@@ -818,8 +813,7 @@ void exclusive_scan(DevScene& s, uint32_t* data, int m, hipStream_t st) {
 }  // namespace
 
 bool upload_by_kernarg(const float* src, const UploadSeg* segs, int nseg, hipStream_t st) {
-    static const bool on = !(getenv("RR_TUNE_KERNARG_UPLOAD") && atoi(getenv("RR_TUNE_KERNARG_UPLOAD")) == 0);
-    if (!on || nseg > 3) return false;
+    if (nseg > 3) return false;
     UploadArgs a{};
     int total = 0;
     for (int k = 0; k < nseg; ++k) total += segs[k].n;
@@ -951,7 +945,7 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, b
     s.flags.ensure((size_t)(n > 1 ? n - 1 : 1));
     s.range.ensure((size_t)(n > 1 ? n - 1 : 1));
 
-    if (n <= kSmallBuild && !want4 && !(want_ploc && n > 2) && small_build_enabled()) {
+    if (n <= kSmallBuild && !want4 && !(want_ploc && n > 2)) {
         k_build_small<<<1, kSmallBuild, 0, st>>>(n, s.tri_local.ptr, s.tri_obj.ptr, s.obj_xform.ptr, s.tri_mat.ptr,
                                                  s.tri_world.ptr, s.bounds.ptr, s.keys[0].ptr, s.vals[0].ptr,
                                                  s.children.ptr, s.node_parent.ptr, s.leaf_parent.ptr, s.range.ptr,

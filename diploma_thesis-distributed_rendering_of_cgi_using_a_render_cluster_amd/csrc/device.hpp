@@ -158,6 +158,7 @@ struct DevPaths {
     bool count_traversal = false;
     bool force_wavefront = false;  // RR_FLAG_WAVEFRONT: LDS-resident scenes skip k_tiles
     bool tile_whole = false;       // k_tiles: one work unit per tile (the frame overlaps a pending one)
+    int last_tile_slices = 0;      // render_frame_device: k_tiles units per box tile of the last frame (0: not k_tiles)
     int grid_blocks = 0;  // persistent grid for path kernels
     void ensure_paths(size_t n);
     void ensure_tiles();  // k_tiles: only the traversal stack spill area
@@ -236,10 +237,8 @@ void bsdf_batch_device(const float* d_mat12, const float* d_lut, const float n3[
 // (rr_debug_fastmath_check).
 void fastmath_check_device(uint32_t lo, uint64_t n, unsigned long long* d_counts, hipStream_t st);
 
-// Device JPEG forward transform (jpeg.hip); tab = dct | qinv luma | qinv chroma.
-void jpeg_fdct_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, int16_t* d_out, hipStream_t st);
-
-// Device JPEG encode (jpeg.hip): the forward transform above + Huffman coding
+// Device JPEG encode (jpeg.hip): the forward transform (tab = dct | qinv luma |
+// qinv chroma) + Huffman coding
 // of the coefficients into the entropy-coded segment of the file (rows, RSTn
 // markers, EOI), written to pinned host memory as [uint64 length][8 B pad]
 // [bytes]. d_huff: 4 x 256 packed code | len << 16 (DC luma, AC luma, DC

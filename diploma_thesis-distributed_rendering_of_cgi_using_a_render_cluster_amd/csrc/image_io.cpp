@@ -16,12 +16,21 @@
 #include <cstring>
 #include <thread>
 
+#include <sched.h>
+
 namespace rr {
 
+// Host threads of the encoders: the CPUs this process may run on (a worker
+// pinned to its GPU's NUMA node — bench.py gpu_placement — gets that share,
+// not the machine's count), at most 16.
 int encoder_threads() {
-    unsigned n = std::thread::hardware_concurrency();
-    if (n == 0) n = 4;
-    return (int)std::min(n, 16u);
+    int n = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    if (n <= 0) n = 4;
+    return std::min(n, 16);
 }
 
 namespace {

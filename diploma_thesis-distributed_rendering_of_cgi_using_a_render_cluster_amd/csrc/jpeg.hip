@@ -69,11 +69,6 @@ __device__ __forceinline__ int fdct_block(const uchar4* __restrict__ rgba, int W
     }
 }
 
-__global__ __launch_bounds__(64) void k_jpeg_fdct(const uchar4* __restrict__ rgba, int W, int H, int mcux,
-                                                  const float* __restrict__ tab, int16_t* __restrict__ out) {
-    (void)fdct_block(rgba, W, H, mcux, tab, out, blockIdx.x % 6);
-}
-
 // ------------------------------------------------------ entropy coding ---
 // Baseline Huffman coding of the quantised coefficients on the device, byte for
 // byte the host coder's output (image_io.cpp entropy_mcu_row + join_rows): one
@@ -159,7 +154,7 @@ __device__ uint32_t wg_scan(uint32_t& v, uint32_t* lds_waves) {
     return total;
 }
 
-// k_jpeg_fdct + the AC bit count of the block (acbits[block]).
+// The forward transform of one block (fdct_block) + its AC bit count (acbits[block]).
 __global__ __launch_bounds__(64) void k_jpeg_fdct_bits(const uchar4* __restrict__ rgba, int W, int H, int mcux,
                                                        const float* __restrict__ tab,
                                                        const uint32_t* __restrict__ huff,
@@ -378,12 +373,6 @@ void jpeg_encode_device(const uint8_t* d_rgba, int W, int H, const float* d_tab,
     k_jpeg_emit<<<(nblocks + 3) / 4, kJpegThreads, 0, st>>>(d_coeffs, mcux, nblocks, d_huff, b.blk_off, b.row_bits,
                                                              b.scratch, sw);
     k_jpeg_finish<<<mcuy, kJpegThreads, 0, st>>>(b.row_bits, b.scratch, sw, b.ready, mcuy, host_out);
-    RR_HIP(hipGetLastError());
-}
-
-void jpeg_fdct_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, int16_t* d_out, hipStream_t st) {
-    const int mcux = (W + 15) / 16, mcuy = (H + 15) / 16;
-    k_jpeg_fdct<<<mcux * mcuy * 6, 64, 0, st>>>(reinterpret_cast<const uchar4*>(d_rgba), W, H, mcux, d_tab, d_out);
     RR_HIP(hipGetLastError());
 }
 

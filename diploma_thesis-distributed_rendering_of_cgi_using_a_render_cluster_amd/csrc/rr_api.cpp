@@ -72,7 +72,7 @@ struct PinnedBuf {
 }  // namespace
 
 struct FrameRun {
-    int W, H, chunks, spp_chunk;
+    int W, H, chunks, spp_chunk, tile_slices;
     bool rebuilt;
     float build_ms, trace_ms, readback_ms;
     float render_ms, device_ms;  // ev0 -> ev4 (build + trace + view transform), ev0 -> ev2 (+ device JPEG)
@@ -100,12 +100,13 @@ struct FrameSlot {
     DevBuf<uint8_t> rgba8;
     DevBuf<int16_t> coeffs;
     KernelProfiler prof;
-    PinnedBuf host_rgba, host_coeffs, host_counters, host_upload;
+    PinnedBuf host_rgba, host_counters, host_upload;
     PinnedBuf host_jpeg;   // device-coded JPEG stream: [uint64 length][pad][bytes]
-    bool jpeg_dev = false;  // this frame's entropy coding runs on the device
     FrameSetup fs;
-    bool view_substituted = false;  // Filmic asked for, no LUTs: rendered with Standard
+    bool view_substituted = false;  // the scene's view settings not applied in full (view_warning says what)
+    std::string view_warning;
     double submit_at = 0.0;         // UNIX time when the device work was enqueued
+    bool anchor = false;            // submitted to an idle context: its device start is submit_at
     rr_scene* scene = nullptr;
     std::string out_path, format;
     int quality = 0;
@@ -118,12 +119,17 @@ struct FrameSlot {
     // Device state private to this slot, swapped in while its frame is enqueued
     // (SlotSwap), so that a k_tiles frame can run on the GPU beside the other
     // slot's frame: the slot's own stream, the small per-frame buffers of
-    // DevPaths and of the JPEG coder, and the per-frame products of its scene's
+    // DevPaths (lights, materials, material tables) and of the JPEG coder, and
+    // — for k_tiles frames only — the per-frame products of its scene's
     // hierarchy build (`alt`: everything in DevScene but the uploaded
-    // triangles, for the scene `alt_scene`).
+    // triangles, for the scene `alt_scene`). Frames of the split path never
+    // overlap their predecessor, so they use the scene's own copy: a large
+    // scene is held once, not once per slot.
     hipStream_t stream = nullptr;
     bool tiles = false;  // this frame renders with k_tiles (may overlap its neighbours)
     DevBuf<float> lights, materials, tile_slab;
+    DevBuf<float> mat_lut;  // material tables of this slot's frames (uploaded when they change)
+    std::vector<float> mat_lut_cached;
     DevBuf<uint32_t> tile_ctrs, tile_cost;
     DevBuf<int32_t> tile_order, spill;
     DevBuf<unsigned long long> trav_counts;
@@ -133,6 +139,8 @@ struct FrameSlot {
     void release_private() {
         lights.release();
         materials.release();
+        mat_lut.release();
+        mat_lut_cached.clear();
         tile_slab.release();
         tile_ctrs.release();
         tile_cost.release();
@@ -168,11 +176,23 @@ struct rr_ctx {
     uint64_t next_ticket = 1;     // tickets are issued in submission order
     uint64_t next_complete = 1;   // the ticket rr_frame_complete expects next
     FrameSlot* last_enqueued = nullptr;  // the slot of the frame enqueued last (its ev[2]: device work done)
+    bool in_slot = false;  // a frame is being enqueued: the slot's private buffers are swapped in
     // UNIX-time estimate of when the compute stream finished the last completed
     // frame (rr_frame_complete): the next frame's device work cannot start before
     double gpu_free_at = 0.0;
     FilmicDev filmic;             // RR_VIEW_FILMIC LUTs (rr_set_ocio_config / RR_OCIO_DIR)
-    std::string warning;          // rr_last_warning
+    // rr_last_warning = the context's warning (a broken RR_OCIO_DIR, kept for
+    // the context's lifetime) + the last completed frame's
+    std::string ctx_warning, frame_warning, warning;
+    // Device start times of completed frames (rr_frame_complete): every frame
+    // also records its start on start_ring[ticket % kStartRing], which outlives
+    // the frame slot's own events by a few frames, so the next frame's start is
+    // the previous one's plus the device clock's difference between the two.
+    static constexpr int kStartRing = 8;
+    hipEvent_t start_ring[kStartRing] = {};
+    uint64_t chain_ticket = 0;   // last completed frame whose device start is known (0: none)
+    double chain_unix = 0.0;     // its device start, UNIX seconds
+    double last_render_end = 0.0;  // finished_rendering_at of the last completed frame
 };
 
 struct rr_scene {
@@ -207,13 +227,6 @@ void quiesce(rr_ctx* c) {
     RR_HIP(hipStreamSynchronize(c->stream));
     for (auto& sl : c->slots)
         if (sl.stream) RR_HIP(hipStreamSynchronize(sl.stream));
-}
-
-// Frames of different slots overlap on the device when both render with k_tiles
-// (RR_TUNE_OVERLAP=0: every frame waits for the one before, as on one stream).
-bool overlap_enabled() {
-    static const bool on = !(getenv("RR_TUNE_OVERLAP") && atoi(getenv("RR_TUNE_OVERLAP")) == 0);
-    return on;
 }
 
 // Exchanges the per-frame products of a scene's hierarchy build (transforms,
@@ -269,11 +282,18 @@ int frame_hier(int n_tris, int n_mats, int n_lights) {
 }
 
 // The view transform a frame on ctx is rendered with: Filmic needs the
-// context's LUTs; without them Standard, and the caller is told (returns true).
-bool resolve_view(const rr_ctx* c, FrameSetup& fs) {
-    if (fs.view_transform != VIEW_FILMIC || (c && c->filmic.ready)) return false;
-    fs.view_transform = VIEW_STANDARD;
-    return true;
+// context's LUTs, without them Standard. Returns what of the scene's view
+// settings the frame does not apply ("" if nothing): that fallback, and the
+// scene's own notes (FrameSetup::view_note: an unsupported view transform,
+// look or display gamma).
+std::string resolve_view(const rr_ctx* c, FrameSetup& fs) {
+    std::string w = fs.view_note;
+    if (fs.view_transform == VIEW_FILMIC && !(c && c->filmic.ready)) {
+        fs.view_transform = VIEW_STANDARD;
+        w = "scene view transform Filmic rendered as Standard: no OCIO LUTs configured "
+            "(rr_set_ocio_config / RR_OCIO_DIR)" + (w.empty() ? "" : "; " + w);
+    }
+    return w;
 }
 
 // hier: 0 = the frame's hierarchy, else a kHier* id (inspection entry points).
@@ -300,7 +320,10 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
         c->srgb_uploaded = true;
     }
     if (p.mat_lut_cached != fs.mat_lut) {  // material tables: static per scene, uploaded when they change
-        quiesce(c);
+        // a frame slot's own table is read only by that slot's frames (the
+        // slot's previous frame has completed); the context's table, used by
+        // the inspection calls, may be read by any stream
+        if (!c->in_slot) quiesce(c);
         p.mat_lut.ensure(fs.mat_lut.size());
         RR_HIP(hipMemcpyAsync(p.mat_lut.ptr, fs.mat_lut.data(), fs.mat_lut.size() * sizeof(float),
                               hipMemcpyHostToDevice, st));
@@ -380,21 +403,14 @@ int choose_spp_chunk(const FrameSetup& fs) {
     if (fs.spp_per_chunk > 0) return std::min(fs.spp_per_chunk, fs.spp);
     // Paths in flight per chunk: the SoA path state is 160 B/path (radiance
     // record 16 B, two path-queue slots 2 x 48 B, shadow slot 48 B), so the
-    // default 256M paths take ~43 GB of the 288 GB HBM (a 1080p 128 spp frame is one chunk). RR_TUNE_CHUNK_MPATHS
-    // overrides it (A/B knob); np stays below 2^31 for 32-bit queue indices.
-    static const long mpaths = getenv("RR_TUNE_CHUNK_MPATHS") ? atol(getenv("RR_TUNE_CHUNK_MPATHS")) : 256;
-    const long target = std::min<long>(std::max<long>(mpaths, 1) << 20, (1L << 31) - 1);
+    // default 256M paths take ~43 GB of the 288 GB HBM (a 1080p 128 spp frame
+    // is one chunk); np stays below 2^31 for 32-bit queue indices.
+    constexpr long kChunkPaths = 256L << 20;
+    const long target = kChunkPaths;
     long c = target / std::max(1, fs.W * fs.H);
     if (c < 1) c = 1;
     if (c > fs.spp) c = fs.spp;
     return (int)c;
-}
-
-// Entropy coding on the device (jpeg.hip) unless RR_TUNE_DEVICE_ENTROPY=0
-// (then the coefficients are copied back and Huffman-coded on host threads).
-bool device_entropy_enabled() {
-    static const bool on = !(getenv("RR_TUNE_DEVICE_ENTROPY") && atoi(getenv("RR_TUNE_DEVICE_ENTROPY")) == 0);
-    return on;
 }
 
 // Device JPEG encode of an RGBA8 frame (transform into c->jpeg_coeffs +
@@ -466,6 +482,8 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
             std::swap(c->stream, sl.stream);
             std::swap(p.lights, sl.lights);
             std::swap(p.materials, sl.materials);
+            std::swap(p.mat_lut, sl.mat_lut);
+            std::swap(p.mat_lut_cached, sl.mat_lut_cached);
             std::swap(p.tile_slab, sl.tile_slab);
             std::swap(p.tile_ctrs, sl.tile_ctrs);
             std::swap(p.tile_cost, sl.tile_cost);
@@ -474,15 +492,17 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
             std::swap(p.trav_counts, sl.trav_counts);
             std::swap(c->jpeg_blk, sl.jpeg_blk);
             std::swap(c->jpeg_scratch, sl.jpeg_scratch);
-            swap_products(sl.scene->dev, sl.alt);
+            if (sl.tiles) swap_products(sl.scene->dev, sl.alt);
+            c->in_slot = !c->in_slot;
         }
         SlotSwap(rr_ctx* c_, FrameSlot& s_) : c(c_), sl(s_) { swap(); }
         ~SlotSwap() { swap(); }
-    } slot_swap(c, sl);
-    hipStream_t st = c->stream;
+    };
     sl.tiles = frame_uses_tiles(make_consts(fs, s->dev.n_tris), (fs.flags & RR_FLAG_WAVEFRONT) != 0);
+    SlotSwap slot_swap(c, sl);
+    hipStream_t st = c->stream;
     FrameSlot* prev = c->last_enqueued;
-    if (prev && prev != &sl && !(overlap_enabled() && sl.tiles && prev->tiles))
+    if (prev && prev != &sl && !(sl.tiles && prev->tiles))
         RR_HIP(hipStreamWaitEvent(st, prev->ev[2], 0));
     c->last_enqueued = &sl;
     // a k_tiles frame enqueued while another k_tiles frame is pending overlaps
@@ -492,7 +512,7 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     bool pending_tiles = false;
     for (auto& o : c->slots)
         if (&o != &sl && o.busy && o.tiles) pending_tiles = true;
-    c->paths.tile_whole = overlap_enabled() && sl.tiles && pending_tiles;
+    c->paths.tile_whole = sl.tiles && pending_tiles;
     sl.prof.reset((fs.flags & RR_FLAG_PROFILE_KERNELS) != 0);
     struct ProfSwap {  // the device code records into paths.prof; swapped back on every exit
         KernelProfiler &a, &b;
@@ -515,11 +535,15 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
         OutSwap(rr_ctx* c_, FrameSlot& s_) : c(c_), sl(s_) { swap(); }
         ~OutSwap() { swap(); }
     } out_swap(c, sl);
-    sl.jpeg_dev = false;
     sl.count = (fs.flags & RR_FLAG_COUNT_TRAVERSAL) != 0;
     c->paths.count_traversal = sl.count;
     c->paths.force_wavefront = (fs.flags & RR_FLAG_WAVEFRONT) != 0;
     RR_HIP(hipEventRecord(sl.ev[0], st));
+    {
+        hipEvent_t& se = c->start_ring[sl.ticket % rr_ctx::kStartRing];
+        if (!se) RR_HIP(hipEventCreate(&se));
+        RR_HIP(hipEventRecord(se, st));
+    }
     r.rebuilt = prepare_frame(c, s, fs, sl.host_upload);
     RR_HIP(hipEventRecord(sl.ev[1], st));
     FrameConsts k = make_consts(fs, s->dev.n_tris);
@@ -527,6 +551,7 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     r.chunks = (fs.spp + r.spp_chunk - 1) / r.spp_chunk;
     k.spp_chunk = r.spp_chunk;
     render_frame_device(s->dev, c->paths, k, r.chunks, st);
+    r.tile_slices = c->paths.last_tile_slices;
     if (fs.view_transform == VIEW_FILMIC) {  // film -> Filmic -> rgba8 (overwrites the kernels' tonemap)
         c->paths.prof.begin(st, RR_K_ACCUM);
         view_filmic_device(c->filmic, k, c->paths.film.ptr, reinterpret_cast<uchar4*>(c->paths.rgba8.ptr), st);
@@ -547,22 +572,12 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
             RR_HIP(hipMemcpy(c->jpeg_tab.ptr, tab, sizeof tab, hipMemcpyHostToDevice));
             c->jpeg_tab_quality = sl.quality;
         }
-        const size_t nc = jpeg_coeff_count(fs.W, fs.H);
-        c->jpeg_coeffs.ensure(nc);
-        sl.jpeg_dev = device_entropy_enabled();
-        if (sl.jpeg_dev) enqueue_jpeg_device(c, sl, c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr);
-        else jpeg_fdct_device(c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr, c->jpeg_coeffs.ptr, st);
+        enqueue_jpeg_device(c, sl, c->paths.rgba8.ptr, fs.W, fs.H, c->jpeg_tab.ptr);
     }
     RR_HIP(hipEventRecord(sl.ev[2], st));
     // the outputs' device-to-host copies follow on the slot's own stream: the
     // next frames run on the other slots' streams, so nothing waits for them
     hipStream_t cs = st;
-    if (sl.jpeg && !sl.jpeg_dev) {
-        const size_t nc = jpeg_coeff_count(fs.W, fs.H);
-        sl.host_coeffs.ensure(nc * sizeof(int16_t));
-        RR_HIP(hipMemcpyAsync(sl.host_coeffs.ptr, c->jpeg_coeffs.ptr, nc * sizeof(int16_t), hipMemcpyDeviceToHost,
-                              cs));
-    }
     if (sl.want_rgba) {
         sl.host_rgba.ensure(npix * 4);
         RR_HIP(hipMemcpyAsync(sl.host_rgba.ptr, c->paths.rgba8.ptr, npix * 4, hipMemcpyDeviceToHost, cs));
@@ -649,6 +664,7 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
     st->trace_ms = r.trace_ms;
     st->readback_ms = r.readback_ms;
     st->bvh_rebuilt = r.rebuilt ? 1 : 0;
+    st->tile_slices = r.tile_slices;
     st->n_triangles = n_tris;
 }
 
@@ -709,7 +725,12 @@ int32_t rr_abi_version(void) { return RR_ABI_VERSION; }
 
 const char* rr_last_error(rr_ctx*) { return g_err.c_str(); }
 
-const char* rr_last_warning(rr_ctx* c) { return c ? c->warning.c_str() : ""; }
+const char* rr_last_warning(rr_ctx* c) {
+    if (!c) return "";
+    c->warning = c->ctx_warning;
+    if (!c->frame_warning.empty()) c->warning += (c->warning.empty() ? "" : "; ") + c->frame_warning;
+    return c->warning.c_str();
+}
 
 int rr_set_ocio_config(rr_ctx* c, const char* dir) {
     if (!c) return fail(RR_EINVAL, "NULL ctx");
@@ -717,6 +738,7 @@ int rr_set_ocio_config(rr_ctx* c, const char* dir) {
         set_device(c);
         quiesce(c);
         c->filmic.release();
+        c->ctx_warning.clear();  // an RR_OCIO_DIR problem is superseded by this call
         if (!dir || !*dir) return RR_OK;
         FilmicLuts l;
         std::string err;
@@ -753,7 +775,7 @@ int rr_create(int device_ordinal, rr_ctx** out) {
             FilmicLuts l;
             std::string err;
             if (*d && load_filmic_luts(d, l, err)) c->filmic.upload(l, d);
-            else if (*d) c->warning = "RR_OCIO_DIR: " + err;
+            else if (*d) c->ctx_warning = "RR_OCIO_DIR: " + err;
         }
         *out = c.release();
         return RR_OK;
@@ -778,6 +800,8 @@ void rr_destroy(rr_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         sl.prof.release();
     }
+    for (auto& e : c->start_ring)
+        if (e) (void)hipEventDestroy(e);
     for (auto& sl : c->slots) {
         if (sl.stream) (void)hipStreamDestroy(sl.stream);  // c->stream is slot 0's
         sl.release_private();
@@ -858,7 +882,8 @@ int rr_frame_submit(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_param
         sl->tm.loaded_at = unix_now();
         const auto t_anim = std::chrono::steady_clock::now();
         sl->fs = setup_frame(s->desc, frame, params);
-        sl->view_substituted = resolve_view(c, sl->fs);
+        sl->view_warning = resolve_view(c, sl->fs);
+        sl->view_substituted = !sl->view_warning.empty();
         sl->anim_ms = ms_since(t_anim);
         sl->tm.started_rendering_at = unix_now();
         sl->scene = s;
@@ -868,10 +893,12 @@ int rr_frame_submit(rr_ctx* c, rr_scene* s, int32_t frame, const rr_render_param
         sl->jpeg = jpeg;
         sl->want_rgba = out_path && !jpeg;
         sl->film_out = nullptr;
+        sl->anchor = idle(c);
         sl->submit_at = unix_now();
+        sl->ticket = c->next_ticket;
         enqueue_frame(c, *sl);
         sl->busy = true;
-        sl->ticket = c->next_ticket++;
+        ++c->next_ticket;
         *ticket = sl->ticket;
         return RR_OK;
     });
@@ -891,33 +918,40 @@ int rr_frame_complete(rr_ctx* c, uint64_t ticket, rr_frame_timing* timing, rr_fr
         const FrameSetup& fs = sl->fs;
         const FrameRun& r = sl->r;
         const double t_sync = unix_now();
-        // Render span from the device's own clock: the frame's work starts when
-        // it was enqueued or when the stream finished the previous frame,
-        // whichever is later, and lasts ev0 -> ev4 (build, trace, view
-        // transform); the device JPEG coder, the copies and the file write
-        // after ev4 are "saving" (Blender's write_still). Host times when
-        // complete happens to be called (possibly long after the device
-        // finished) do not enter the span.
-        const double gpu_start = std::max(sl->submit_at, c->gpu_free_at);
-        sl->tm.started_rendering_at = std::min(std::max(sl->tm.started_rendering_at, gpu_start), t_sync);
+        // Render span from the device's own clock. The frame's device work
+        // starts at its start event: for a frame submitted to an idle context
+        // that is the submit time; otherwise the previous completed frame's
+        // device start plus the device clock's difference between the two
+        // start events (start_ring). Frames in flight together overlap on the
+        // device, but the worker's records are consecutive (traces.py
+        // not_before, performance.rs): the render span starts when the
+        // previous frame's ended, or at the device start if later, and ends
+        // at the frame's own end event (ev4: build, trace, view transform),
+        // so the spans of overlapped frames add up to at most the wall time
+        // they took. The device JPEG coder, the copies and the file write
+        // after ev4 are "saving" (Blender's write_still).
+        constexpr int K = rr_ctx::kStartRing;
+        double dev_start = std::max(sl->submit_at, c->gpu_free_at);
+        if (!sl->anchor && c->chain_ticket && c->chain_ticket + 1 == ticket && c->start_ring[ticket % K]) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, c->start_ring[c->chain_ticket % K], c->start_ring[ticket % K]) == hipSuccess)
+                dev_start = c->chain_unix + ms * 1e-3;
+        }
+        dev_start = std::min(std::max(dev_start, sl->submit_at), t_sync);
+        c->chain_ticket = ticket;
+        c->chain_unix = dev_start;
+        sl->tm.started_rendering_at = std::min(std::max(dev_start, c->last_render_end), t_sync);
         sl->tm.finished_rendering_at =
-            std::min(std::max(gpu_start + r.render_ms * 1e-3, sl->tm.started_rendering_at), t_sync);
+            std::min(std::max(dev_start + r.render_ms * 1e-3, sl->tm.started_rendering_at), t_sync);
         sl->tm.file_saving_started_at = sl->tm.finished_rendering_at;
-        c->gpu_free_at = std::min(gpu_start + r.device_ms * 1e-3, t_sync);
+        c->last_render_end = sl->tm.finished_rendering_at;
+        c->gpu_free_at = std::min(dev_start + r.device_ms * 1e-3, t_sync);
         uint64_t bytes = 0;
         const auto t_enc = std::chrono::steady_clock::now();
-        if (sl->jpeg && sl->jpeg_dev) {
+        if (sl->jpeg) {  // JFIF headers + the device-coded stream
             const std::string path = sl->out_path + ".jpg";
             if (!write_device_jpeg(*sl, path, &bytes))
                 return fail(RR_EIO, "cannot write " + path + ": " + std::strerror(errno));
-        } else if (sl->jpeg) {
-            std::vector<uint8_t> data;
-            if (!encode_jpeg_coeffs(reinterpret_cast<const int16_t*>(sl->host_coeffs.ptr), fs.W, fs.H, sl->quality,
-                                    data))
-                return fail(RR_EINVAL, "JPEG encode failed");
-            const std::string path = sl->out_path + ".jpg";
-            if (!write_file(path, data)) return fail(RR_EIO, "cannot write " + path + ": " + std::strerror(errno));
-            bytes = data.size();
         } else if (!sl->out_path.empty()) {
             const int e = do_encode(sl->host_rgba.ptr, fs.W, fs.H, sl->out_path.c_str(), sl->format.c_str(),
                                     sl->quality, &bytes);
@@ -926,10 +960,7 @@ int rr_frame_complete(rr_ctx* c, uint64_t ticket, rr_frame_timing* timing, rr_fr
         const double enc_ms = ms_since(t_enc);
         sl->tm.file_saving_finished_at = unix_now();
         if (timing) *timing = sl->tm;
-        c->warning = sl->view_substituted
-                         ? "scene view transform Filmic rendered as Standard: no OCIO LUTs configured "
-                           "(rr_set_ocio_config / RR_OCIO_DIR)"
-                         : "";
+        c->frame_warning = sl->view_warning;
         if (stats) {
             fill_stats(stats, fs, r, sl->scene->dev.n_tris);
             stats->view_transform_substituted = sl->view_substituted ? 1 : 0;
@@ -972,18 +1003,21 @@ int rr_render_frame_to_memory(rr_ctx* c, rr_scene* s, int32_t frame, const rr_re
     return guarded([&] {
         sl->t_call = std::chrono::steady_clock::now();
         sl->fs = setup_frame(s->desc, frame, params);
-        sl->view_substituted = resolve_view(c, sl->fs);
+        sl->view_warning = resolve_view(c, sl->fs);
+        sl->view_substituted = !sl->view_warning.empty();
         sl->scene = s;
         sl->out_path.clear();
         sl->format.clear();
         sl->jpeg = false;
         sl->want_rgba = true;
         sl->film_out = film;
+        sl->ticket = c->next_ticket;
         enqueue_frame(c, *sl);
         finish_frame(c, *sl);
         sl->film_out = nullptr;
         const FrameSetup& fs = sl->fs;
         if (rgba8) std::memcpy(rgba8, sl->host_rgba.ptr, (size_t)fs.W * fs.H * 4);
+        c->frame_warning = sl->view_warning;
         if (stats) {
             fill_stats(stats, fs, sl->r, s->dev.n_tris);
             stats->view_transform_substituted = sl->view_substituted ? 1 : 0;

@@ -646,11 +646,23 @@ SceneDesc load_scene(const std::string& path) {
         d.view_transform_name = r.get_str("view_transform", "Standard");
         // "Filmic" is applied through Blender's OCIO LUTs when the context has
         // them (rr_set_ocio_config); otherwise the frame falls back to Standard
-        // and says so (rr_frame_stats.view_transform_substituted).
+        // and says so (rr_frame_stats.view_transform_substituted). Any other
+        // Blender 3.6 view ("Filmic Log", "False Color", "Standard" looks, ...)
+        // renders as Standard with the same flag and a warning naming it, as
+        // does a look or a display gamma the renderer does not apply: the job
+        // still renders, and the substitution is never silent.
         if (d.view_transform_name == "Standard") d.view_transform = VIEW_STANDARD;
         else if (d.view_transform_name == "Raw") d.view_transform = VIEW_RAW;
         else if (d.view_transform_name == "Filmic") d.view_transform = VIEW_FILMIC;
-        else throw std::runtime_error("unsupported view transform: " + d.view_transform_name);
+        else {
+            d.view_transform = VIEW_STANDARD;
+            d.view_note = "view transform '" + d.view_transform_name + "' is not supported, rendered as Standard";
+        }
+        const std::string look = r.get_str("look", "None");
+        auto note = [&](const std::string& m) { d.view_note += (d.view_note.empty() ? "" : "; ") + m; };
+        if (look != "None" && !look.empty()) note("look '" + look + "' ignored");
+        const double gamma = r.get_num("gamma", 1.0);
+        if (gamma != 1.0) note("display gamma " + std::to_string(gamma) + " ignored");
     }
     if (s.render.resx <= 0 || s.render.resy <= 0 || s.render.percent <= 0)
         throw std::runtime_error("invalid resolution");
@@ -876,6 +888,7 @@ FrameSetup setup_frame(const SceneDesc& s, int frame, const rr_render_params* p)
     f.clamp_indirect = (float)(p->clamp_indirect >= 0.f ? p->clamp_indirect : r.clamp_indirect);
     f.seed = p->use_scene_seed ? r.seed : p->seed;
     f.view_transform = p->view_transform >= 0 ? p->view_transform : r.view_transform;
+    if (p->view_transform < 0) f.view_note = r.view_note;
     if (f.view_transform != VIEW_STANDARD && f.view_transform != VIEW_RAW && f.view_transform != VIEW_FILMIC)
         throw std::runtime_error("unsupported view transform");
     f.spp_per_chunk = p->spp_per_chunk > 0 ? p->spp_per_chunk : r.spp_per_chunk;

@@ -112,6 +112,11 @@ struct RenderDesc {
     double clamp_indirect = 10.0, filter_width = 1.5, exposure = 0.0;
     int view_transform = VIEW_STANDARD;
     std::string view_transform_name = "Standard";
+    // What of the scene's colour management a frame does not apply, for the
+    // frame's warning ("" when all of it is applied): a view transform other
+    // than Standard / Raw / Filmic (rendered as Standard), a look other than
+    // None, a display gamma other than 1 (both ignored).
+    std::string view_note;
     uint32_t seed = 0;
     int spp_per_chunk = 0;
 };
@@ -136,6 +141,7 @@ struct SceneDesc {
 struct FrameSetup {
     int32_t W = 0, H = 0, spp = 0, max_bounces = 0, view_transform = 0, spp_per_chunk = 0, flags = 0;
     int32_t max_diffuse = 4, max_glossy = 4;
+    std::string view_note;  // RenderDesc::view_note when the view comes from the scene
     uint32_t seed = 0;
     float clamp_indirect = 0.f, filter_width = 1.5f, exposure_scale = 1.f;
     float cam[RR_CAM_FLOATS] = {};

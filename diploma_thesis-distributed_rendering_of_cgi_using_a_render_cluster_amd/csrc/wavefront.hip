@@ -2094,8 +2094,8 @@ using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, Pa
 using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, Rad, int32_t*, unsigned long long*);
 using TailFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, uint32_t*, int32_t*,
                         unsigned long long*);
-// LDS-resident scenes render through k_tiles (default) or, with RR_TUNE_TILES=0,
-// through the wavefront kernels (A/B and parity of both paths).
+// LDS-resident scenes render through k_tiles (RR_FLAG_WAVEFRONT: through the
+// wavefront kernels, the parity tests' second path).
 // k_tiles slices a box tile into its sample groups: one unit per group, the
 // group sums handed to the slice finishing last through a slab of one plane
 // (3 x 64 floats) per group.
@@ -2105,10 +2105,6 @@ size_t tile_slab_bytes(int spp, long tiles) {
     return ng > 1 ? (size_t)192 * sizeof(float) * ng * (size_t)tiles : 0;
 }
 constexpr size_t kTileSlabMax = (size_t)16 << 30;
-bool tiles_enabled() {
-    static const bool on = !(getenv("RR_TUNE_TILES") && atoi(getenv("RR_TUNE_TILES")) == 0);
-    return on;
-}
 // Persistent grid = resident blocks: CUs x blocks per CU the kernel's register
 // and LDS budget admits (a grid-stride loop over more blocks than fit would
 // only queue the surplus behind the first wave of blocks).
@@ -2160,7 +2156,7 @@ bool scene_in_lds(int n_tris, int n_mats, int n_lights) {
 
 bool frame_uses_tiles(const FrameConsts& base, bool force_wavefront) {
     const long n_tiles = (long)((base.W + 7) / 8) * ((base.H + 7) / 8);
-    return scene_in_lds(base.n_tris, base.n_mats, base.n_lights) && tiles_enabled() && !force_wavefront &&
+    return scene_in_lds(base.n_tris, base.n_mats, base.n_lights) && !force_wavefront &&
            tile_slab_bytes(base.spp_total, n_tiles) <= kTileSlabMax;
 }
 
@@ -2349,6 +2345,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     const int npix = base.npix;
     const size_t npaths = (size_t)npix * base.spp_chunk;
     const Grids G(base, p.count_traversal);
+    p.last_tile_slices = 0;
     if (frame_uses_tiles(base, p.force_wavefront)) {  // one launch: all samples of every tile
         p.ensure_tiles();
         p.film.ensure((size_t)npix);
@@ -2381,6 +2378,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         // waves fill the tail, and the slab writes and the fold launch go
         TileSlices sl{p.tile_whole ? 1 : film_groups(base.spp_total), (size_t)192 * film_groups(base.spp_total), nullptr,
                       p.tile_order.ptr, p.tile_cost.ptr};
+        p.last_tile_slices = sl.n;
         if (sl.n > 1) {
             p.tile_slab.ensure(sl.floats * (size_t)tiles);
             sl.slab = p.tile_slab.ptr;

@@ -157,10 +157,20 @@ def parse_with_base_directory_prefix(path: str, base: str | os.PathLike | None) 
     return Path(path)
 
 
-def scene_path_for_project(project_file: Path) -> Path:
-    """The exported scene of a project: <stem>.rrscene next to the .blend
-    (tools/blend_export.py writes it once per project)."""
+def scene_path_for_project(project_file: Path, scene_dirs=()) -> Path:
+    """The exported scene of a project (tools/blend_export.py writes it once per
+    project): <stem>.rrscene next to the .blend, else the first
+    <dir>/<stem>.rrscene of scene_dirs that exists (BackendRunner passes the
+    base directory's scenes/, where this repository keeps its exports). A
+    .rrscene project names itself."""
     p = Path(project_file)
     if p.suffix == ".rrscene":
         return p
-    return p.with_suffix(".rrscene")
+    here = p.with_suffix(".rrscene")
+    if here.is_file():
+        return here
+    for d in scene_dirs:
+        q = Path(d) / (p.stem + ".rrscene")
+        if q.is_file():
+            return q
+    return here

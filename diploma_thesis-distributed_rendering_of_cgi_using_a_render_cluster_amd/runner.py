@@ -65,7 +65,7 @@ class BackendRunner:
         key = str(project)
         s = self._scenes.get(key)
         if s is None:
-            scene_file = scene_path_for_project(project)
+            scene_file = scene_path_for_project(project, [self.base_directory_path / "scenes"])
             if not scene_file.is_file():
                 raise RenderError(f"No exported scene for project {project!s}: expected {scene_file!s} "
                                   "(export it once with tools/blend_export.py)")

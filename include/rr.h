@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 4
+#define RR_ABI_VERSION 5
 
 /* error codes (negative errno values) */
 #define RR_OK 0
@@ -142,6 +142,13 @@ typedef struct rr_frame_stats {
      * start to last wave end), i.e. how full the persistent grid stayed; 0
      * when not measured */
     double kernel_wave_fill;
+    /* LDS-resident scenes (k_tiles): work units per tile of the scene's
+     * screen box — 1 when the frame overlapped another k_tiles frame in flight
+     * (whole tiles, every sample group of a tile in one unit), the number of
+     * 32-sample groups when it ran alone (one unit per group); 0 for frames of
+     * the other paths. Scheduling only: both give the same bits. */
+    int32_t tile_slices;
+    int32_t reserved0;
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */

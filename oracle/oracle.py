@@ -47,6 +47,7 @@ def lib():
         L.orc_material_lut.argtypes = [f, f]
         L.orc_set_filmic.argtypes = [f, c_int, f, c_int, c_int, ctypes.c_float, ctypes.c_float]
         L.orc_filmic.argtypes = [c_int, f, u8]
+        L.orc_set_rules.argtypes = [c_int, c_int]
         _lib = L
     return _lib
 
@@ -128,6 +129,22 @@ def render(tris, tri_mat, camera, lights, materials, world, render_ints, render_
                      _p(world, ctypes.c_float), _p(ri, ctypes.c_int32), _p(rf, ctypes.c_float),
                      _p(f, ctypes.c_float), _p(r, ctypes.c_uint8), r0, r1, threads)
     return f, r
+
+
+class rules:
+    """Context manager: orc_render's shortcuts switched for a block (test use),
+    e.g. `with O.rules(cull=False): ...`. Both are restored to on afterwards."""
+
+    def __init__(self, cull: bool = True, hull: bool = True):
+        self.cull, self.hull = cull, hull
+
+    def __enter__(self):
+        lib().orc_set_rules(int(self.cull), int(self.hull))
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_rules(1, 1)
+        return False
 
 
 def render_state(state, **kw):

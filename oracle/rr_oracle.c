@@ -1310,6 +1310,17 @@ int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* h
 
 double orc_last_build_seconds(void) { return g_build_s; }
 
+/* The two shortcuts orc_render shares with the product, switchable so the
+ * tests can show that neither changes a pixel (tests/test_oracle.py):
+ *  cull: camera rays outside the scene's screen rectangle (screen_rect) are
+ *        misses without a traversal (csrc/wavefront.hip camera_ray_xy);
+ *  hull: on LDS-resident scenes (render_ints[7] == 2) a secondary ray leaving
+ *        a hull side of its triangle (tri_hull) is a miss / unoccluded without
+ *        a traversal (csrc/wavefront.hip hull_flags).
+ * Both are on by default (what the product does). */
+static int g_rule_cull = 1, g_rule_hull = 1;
+void orc_set_rules(int cull, int hull) { g_rule_cull = cull; g_rule_hull = hull; }
+
 void orc_ray_counts(long long* out4, int* late32, int* n_late) {
     for (int k = 0; k < 4; ++k) out4[k] = g_rays[k];
     for (int k = 0; k < 2 * g_n_late; ++k) late32[k] = g_late[k];
@@ -1334,7 +1345,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     S->mats = mats;
     S->world = V(world[0], world[1], world[2]);
     S->cam_all = ri[7] == 2;
-    if (S->cam_all && n_tris > 0) {
+    if (S->cam_all && n_tris > 0 && g_rule_hull) {
         S->hull = (unsigned char*)malloc((size_t)n_tris);
         for (int i = 0; i < n_tris; ++i) S->hull[i] = (unsigned char)tri_hull(&B, i);
     }
@@ -1355,7 +1366,7 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
         const float* r = B.box; /* root: two child boxes */
         float lo[3] = {fminf(r[0], r[6]), fminf(r[1], r[7]), fminf(r[2], r[8])};
         float hi[3] = {fmaxf(r[3], r[9]), fmaxf(r[4], r[10]), fmaxf(r[5], r[11])};
-        S->cull_on = screen_rect(cam, (float)S->W, (float)S->H, lo, hi, S->cull);
+        S->cull_on = g_rule_cull ? screen_rect(cam, (float)S->W, (float)S->H, lo, hi, S->cull) : 0;
     }
     const float exposure = rf[2];
     const float inv_spp = 1.0f / (float)S->spp;

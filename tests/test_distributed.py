@@ -120,3 +120,53 @@ def test_bench_spawns_one_rank_per_gpu_dry_run():
     assert line["n_gpus"] == 2 and line["value"] is None and line["dry_run"]
     a, b = line["frames_by_rank"]
     assert not set(a) & set(b) and sorted(a + b) == JOB_FRAMES
+    # each rank pinned to its own non-empty CPU share before any GPU call
+    pa, pb = line["placement_by_rank"]
+    print(pa, pb)
+    assert (pa["device"], pb["device"]) == (0, 1)
+    ca, cb = _bench().parse_cpulist(pa["cpus"]), _bench().parse_cpulist(pb["cpus"])
+    assert ca and cb and not ca & cb
+    assert 1 <= pa["omp_num_threads"] <= len(ca) and 1 <= pb["omp_num_threads"] <= len(cb)
+
+
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_gpu_placement_follows_numa_nodes(tmp_path):
+    """gpu_placement on an 8-GPU, 2-socket topology written as sysfs files: the
+    KFD topology (CPU nodes first, then GPUs in HIP's order) gives each GPU's
+    PCI address, the PCI device its NUMA node; each rank gets a disjoint,
+    non-empty share of its own GPU's node, and ranks of one node split it."""
+    b = _bench()
+    topo = tmp_path / "class/kfd/kfd/topology/nodes"
+    numa_of = [0, 0, 0, 0, 1, 1, 1, 1]
+    for i in range(2):  # CPU nodes
+        (topo / str(i)).mkdir(parents=True)
+        (topo / str(i) / "properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
+    for g in range(8):
+        bus = 0x10 + 0x10 * g
+        (topo / str(2 + g)).mkdir(parents=True)
+        (topo / str(2 + g) / "properties").write_text(f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+        dev = tmp_path / "bus/pci/devices" / f"0000:{bus:02x}:00.0"
+        dev.mkdir(parents=True)
+        (dev / "numa_node").write_text(f"{numa_of[g]}\n")
+    numa = b.gpu_numa_nodes(str(tmp_path))
+    assert numa == numa_of
+    node_cpus = {0: set(range(0, 64)) | set(range(128, 192)), 1: set(range(64, 128)) | set(range(192, 256))}
+    allowed = set(range(256))
+    plan = b.gpu_placement(list(range(8)), allowed, numa, lambda n: node_cpus[n])
+    for r, cpus in enumerate(plan):
+        assert len(cpus) == 32 and cpus <= node_cpus[numa_of[r]]
+    assert len(set().union(*plan)) == 256  # disjoint
+    # two ranks on one GPU (the one-GPU rehearsal) split that GPU's node
+    p2 = b.gpu_placement([5, 5], allowed, numa, lambda n: node_cpus[n])
+    assert p2[0] and p2[1] and not p2[0] & p2[1] and p2[0] | p2[1] == node_cpus[1]
+    # no topology (CPU containers): the allowed set split evenly
+    p3 = b.gpu_placement([0, 1], {0, 1, 2, 3, 4, 5, 6, 7}, [], lambda n: set())
+    assert p3 == [{0, 1, 2, 3}, {4, 5, 6, 7}]
+    assert b.cpuset_str([0, 1, 2, 5, 7, 8]) == "0-2,5,7-8" and b.parse_cpulist("0-2,5,7-8") == {0, 1, 2, 5, 7, 8}

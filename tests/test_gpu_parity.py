@@ -455,6 +455,100 @@ def test_backend_runner_render_frames_pipelined(rr, tmp_path):
     runner = rr.BackendRunner(root, params=rr.default_params(width=96, height=54, spp=2))
     seen = []
     frts = runner.render_frames(job, job.frames(), on_frame=lambda f, frt, st: seen.append(f))
-    runner.close()
     assert seen == job.frames() and len(frts) == len(seen)
     assert sorted(os.listdir(tmp_path)) == [f"{f:06d}.jpg" for f in job.frames()]
+    # render spans from the device clock (rr_api.cpp rr_frame_complete): frames
+    # overlap on the device, yet the spans are consecutive and together cover
+    # no more than the wall time the frames took (timings straight from the
+    # library, before traces.py's clamping)
+    import time
+    p = rr.default_params(width=480, height=270, spp=64)
+    scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, root))
+    t0 = time.time()
+    pending, timings = [], []
+    for f in range(1, 13):
+        if len(pending) == rr.native.RR_MAX_FRAMES_IN_FLIGHT:
+            timings.append(runner.ctx.complete_frame(pending.pop(0))[0])
+        pending.append(runner.ctx.submit_frame(scene, f, p, str(tmp_path / f"span{f}"), "JPEG", 90))
+    timings += [runner.ctx.complete_frame(t)[0] for t in pending]
+    wall = time.time() - t0
+    runner.close()
+    spans = [(t.started_rendering_at, t.finished_rendering_at) for t in timings]
+    assert all(a <= b for a, b in spans)
+    assert all(spans[i][1] <= spans[i + 1][0] for i in range(len(spans) - 1)), spans
+    total = sum(b - a for a, b in spans)
+    print(f"12 overlapped frames: render spans {total * 1e3:.1f} ms of {wall * 1e3:.1f} ms wall")
+    assert t0 <= spans[0][0] and spans[-1][1] <= t0 + wall and 0 < total <= wall
+
+
+@pytest.mark.parametrize("seed", [0, 3, 6, 7, 11, 14])
+def test_random_soups_bit_exact_against_traversed_oracle(ctx, rr, tmp_path, seed):
+    """Random non-convex LDS-resident soups (tests/soups.py, <= 60 triangles):
+    k_tiles (tile-binned camera rays, hull rule, screen culling) equals the
+    oracle rendering the same frame with every camera ray and every
+    secondary ray traversed, bit for bit."""
+    import soups
+    path = str(tmp_path / f"soup{seed}.rrscene")
+    tris = soups.soup_scene(S04, seed, path)
+    s = ctx.load_scene(path)
+    try:
+        frame = 1 + (3 * seed) % 30
+        p = rr.default_params(width=160, height=90, spp=24)
+        film, rgba, stats = ctx.render_to_memory(s, frame, p)
+        st = ctx.frame_state(s, frame, p)
+        assert int(st.render_ints[7]) == 2  # LDS-resident: k_tiles
+        with O.rules(cull=False, hull=False):
+            of, orgba = O.render_state(st)
+        print(f"soup {seed}: {len(tris)} triangles, {soups.hull_sides(tris)} hull sides, "
+              f"{stats.camera_rays_traced} camera rays traced")
+        assert np.array_equal(film, of), f"{np.count_nonzero(film != of)} film mismatches"
+        assert np.array_equal(rgba, orgba)
+    finally:
+        s.close()
+
+
+def _cube_bands_8bit(rgba, n):
+    """n 4-row bands spread over the rows whose 8-bit pixels differ from the
+    background (the corner pixel), each with its cube-pixel count."""
+    bg = rgba[-1, 0, :3]
+    hit = np.any(rgba[..., :3] != bg[None, None, :], axis=-1)
+    rows = np.nonzero(hit.sum(axis=1) > 0)[0]
+    assert len(rows) >= 4 * n, len(rows)
+    starts = np.linspace(rows[0], rows[-1] - 3, n).astype(int)
+    return [(int(r), int(hit[r:r + 4].sum())) for r in starts]
+
+
+@pytest.mark.parametrize("job_name,frames", [("04_very-simple_demo_10f-1w.toml", list(range(1, 11))),
+                                             ("01_simple-animation_600f-8w_dynamic.toml", [1, 20, 60, 61])])
+def test_timed_configuration_bands_bit_exact(rr, tmp_path, job_name, frames):
+    """The bench's timed configuration under the oracle: BackendRunner.render_frames
+    exactly as bench.py times it (scene defaults 1920x1080 x 128 spp, three
+    frames in flight, so every k_tiles frame after the first overlaps a pending
+    one and runs as whole-tile work units, tile_slices == 1), one write_still
+    per frame (render-timing-script.py:90) under the worker's queue loop
+    (queue.rs:79-118), PNG so the written file is lossless. Four 4-row bands
+    through the cube per frame, decoded from the written file, equal the
+    oracle's pixels bit for bit."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    job = rr.BlenderJob.load_from_file(os.path.join(root, "jobs", job_name))
+    job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": str(tmp_path),
+                                   "output_file_format": "PNG"})
+    runner = rr.BackendRunner(root, params=rr.default_params())
+    slices = {}
+    try:
+        runner.render_frames(job, frames, on_frame=lambda f, frt, st: slices.__setitem__(f, int(st.tile_slices)))
+        print(f"{job_name}: tile_slices per frame {slices}")
+        assert slices[frames[0]] == 4 and all(slices[f] == 1 for f in frames[1:])
+        scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, root))
+        for f in frames:
+            img = np.asarray(Image.open(tmp_path / f"{f:06d}.png").convert("RGBA"))
+            assert img.shape == (1080, 1920, 4)
+            st = runner.ctx.frame_state(scene, f)
+            for r0, n_hit in _cube_bands_8bit(img, 4):
+                _, orgba = O.render_state(st, rows=(r0, r0 + 4), film=False)
+                print(f"  frame {f} rows {r0}..{r0 + 3}: {n_hit} cube pixels")
+                assert n_hit > 0
+                nbad = int(np.count_nonzero(img[r0:r0 + 4] != orgba[r0:r0 + 4]))
+                assert nbad == 0, f"frame {f} rows {r0}..{r0 + 3}: {nbad} mismatches"
+    finally:
+        runner.close()

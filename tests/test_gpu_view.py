@@ -108,3 +108,54 @@ def test_bounce_caps_bit_exact_and_known_answer(ctx, rr, name, caps, hits):
         assert st.extension_rays == pytest.approx(st.camera_rays * (hits - 1), rel=2e-3)
     finally:
         s.close()
+
+
+def test_unsupported_view_settings_render_standard_and_say_so(ctx, rr, tmp_path):
+    """A Blender 3.6 view the renderer does not implement ('Filmic Log') and a
+    look ('Medium Contrast') do not fail the job: the frame renders with
+    Standard, bit-identical to the Standard scene, is flagged
+    (view_transform_substituted) and the warning names both."""
+    import json
+    with open(scene_path("04_very-simple-standin.rrscene")) as f:
+        sc = json.load(f)
+    sc["render"]["view_transform"] = "Filmic Log"
+    sc["render"]["look"] = "Medium Contrast"
+    path = str(tmp_path / "filmic_log.rrscene")
+    with open(path, "w") as f:
+        json.dump(sc, f)
+    p = rr.default_params(width=96, height=54, spp=4)
+    s_log, s_std = ctx.load_scene(path), ctx.load_scene(scene_path("04_very-simple-standin.rrscene"))
+    try:
+        film, rgba, st = ctx.render_to_memory(s_log, 12, p)
+        w = ctx.last_warning()
+        assert st.view_transform_substituted == 1 and st.view_transform == 0
+        assert "Filmic Log" in w and "Medium Contrast" in w, w
+        film2, rgba2, st2 = ctx.render_to_memory(s_std, 12, p)
+        assert st2.view_transform_substituted == 0 and ctx.last_warning() == ""
+        assert np.array_equal(film, film2) and np.array_equal(rgba, rgba2)
+        # the oracle's Standard render of the same frame
+        _, orgba = O.render_state(ctx.frame_state(s_log, 12, p))
+        assert np.array_equal(rgba, orgba)
+    finally:
+        s_log.close()
+        s_std.close()
+
+
+def test_context_warning_survives_frames(rr, tmp_path, monkeypatch):
+    """A broken RR_OCIO_DIR is reported by rr_last_warning for the context's
+    lifetime, next to each frame's own warning, not only until the first frame."""
+    monkeypatch.setenv("RR_OCIO_DIR", str(tmp_path / "no_such_dir"))
+    c = rr.RenderContext(0)
+    try:
+        assert "RR_OCIO_DIR" in c.last_warning()
+        s = c.load_scene(scene_path("01_simple-animation.rrscene"))
+        _, _, st = c.render_to_memory(s, 5, rr.default_params(width=64, height=36, spp=2))
+        w = c.last_warning()
+        assert st.view_transform_substituted == 1
+        assert "RR_OCIO_DIR" in w and "Filmic rendered as Standard" in w, w
+        c.set_ocio_config(None)  # superseded: only the frame's warning is left
+        _, _, _ = c.render_to_memory(s, 5, rr.default_params(width=64, height=36, spp=2))
+        assert "RR_OCIO_DIR" not in c.last_warning()
+        s.close()
+    finally:
+        c.close()

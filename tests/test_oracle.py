@@ -267,6 +267,65 @@ def test_hull_escape_changes_no_pixel(frame, ground):
     assert np.array_equal(films[0], films[1])
 
 
+def _soup_frame(tmp_path, seed, frame, W=128, H=72):
+    """Frame inputs of random soup `seed` (tests/soups.py) in the 04vs stand-in."""
+    import soups
+    path = str(tmp_path / f"soup{seed}.rrscene")
+    soups.soup_scene(scene_path("04_very-simple-standin.rrscene"), seed, path)
+    scene = HO.load_scene(path)
+    tris, mats = world_tris(scene, frame)
+    return HO.frame_constants(scene, frame, W, H), tris, mats
+
+
+@pytest.mark.parametrize("seed", list(range(20)))
+def test_hull_rule_random_soups(tmp_path, seed):
+    """The hull rule (tri_hull) on 20 random non-convex LDS-resident soups of
+    <= 60 triangles (star-shaped closed blobs, free shards, half with a ground
+    quad): frames with the rule equal frames with every secondary ray
+    traversed, bit for bit, on the same hierarchy (render_ints[7] == 2)."""
+    import soups
+    fc, tris, mats = _soup_frame(tmp_path, seed, 1 + (3 * seed) % 30)
+    n_sides = soups.hull_sides(tris)
+    rf = np.array([10.0, 1.5, 1.0, 0], np.float32)
+    ri = np.array([128, 72, 16, 12, 0, 0, 0, 2, 4, 4], np.int32)
+    args = (tris, mats, fc["camera"], fc["lights"], fc["materials"], fc["world"], ri, rf)
+    f_rule, r_rule = O.render(*args, threads=4)
+    with O.rules(hull=False):
+        f_all, r_all = O.render(*args, threads=4)
+    print(f"soup {seed}: {len(tris)} triangles, {n_sides} hull sides")
+    assert len(tris) <= 60 and n_sides > 0
+    assert np.any(np.abs(f_rule[..., :3] - fc["world"][None, None, :]) > 1e-3)  # the soup is on screen
+    assert np.array_equal(f_rule, f_all), f"{np.count_nonzero(f_rule != f_all)} film mismatches"
+    assert np.array_equal(r_rule, r_all)
+
+
+@pytest.mark.parametrize("case", ["04vs-1", "04vs-30", "04vs-60", "soup-3", "soup-6", "soup-11"])
+@pytest.mark.parametrize("hier", [2, 3])
+def test_screen_cull_changes_no_pixel(tmp_path, case, hier):
+    """Camera rays outside the scene's projected bounding rectangle (screen_rect,
+    one pixel of slack) are misses without a traversal. Rendering with the
+    rule and with every camera ray traced gives the same film bit for bit, on
+    the LBVH (LDS-resident path, camera rays against every triangle) and on
+    the PLOC hierarchy."""
+    kind, k = case.split("-")
+    if kind == "04vs":
+        scene = HO.load_scene(scene_path("04_very-simple-standin.rrscene"))
+        fc = HO.frame_constants(scene, int(k), 96, 54)
+        tris, mats = world_tris(scene, int(k))
+    else:
+        fc, tris, mats = _soup_frame(tmp_path, int(k), 20, 96, 54)
+    rf = np.array([10.0, 1.5, 1.0, 0], np.float32)
+    ri = np.array([96, 54, 8, 12, 0, 0, 0, hier, 4, 4], np.int32)
+    args = (tris, mats, fc["camera"], fc["lights"], fc["materials"], fc["world"], ri, rf)
+    f_cull, _ = O.render(*args, threads=4)
+    with O.rules(cull=False):
+        f_all, _ = O.render(*args, threads=4)
+    bg = np.all(np.abs(f_cull[..., :3] - fc["world"][None, None, :]) <= 1e-7, axis=-1)
+    print(f"{case} hier {hier}: {int(bg.sum())} of {bg.size} pixels background")
+    assert 0 < bg.sum() < bg.size  # the rectangle leaves background pixels to cull
+    assert np.array_equal(f_cull, f_all), f"{np.count_nonzero(f_cull != f_all)} film mismatches"
+
+
 def _q4_child_boxes(node):
     """Decoded child boxes of one quantised BVH4 node (rr_device.h QNode4), in
     double: lo/hi = org + q * 2^e per axis, (4, 3) each."""

@@ -2,12 +2,19 @@
 
 The jobs under jobs/ point `render_script_path` here. The MI355X backend does
 not execute it (frames are rendered in-process through include/rr.h); it exists
-so the same job TOMLs can drive the REFERENCE worker with a real Blender 3.6
-(`--blenderBinary /path/to/blender`) when one is available, with Cycles pinned
-to the settings the MI355X renderer implements (SURVEY.md §7 hard parts b-d):
-engine CYCLES on the CPU, fixed samples (no adaptive sampling, no denoiser),
-bounce limit, indirect clamp, Blackman-Harris 1.5 px filter, Standard view
-transform, seed.
+so the 04 and 01 job TOMLs can drive the REFERENCE worker with a real Blender
+3.6 (`--blenderBinary /path/to/blender`) when one is available: their
+project_file_path names a .blend (blender-projects/01_simple-animation/
+01_simple-animation.blend, the reference's own; blender-projects/04_very-simple/
+04_very-simple-standin.blend, written by tools/make_standin_blend.py), which
+the worker hands to Blender as the project (worker/src/rendering/runner/
+mod.rs:140-146). Cycles is pinned to the settings the MI355X renderer
+implements (SURVEY.md §7 hard parts b-d): engine CYCLES on the CPU, fixed
+samples (no adaptive sampling, no denoiser), bounce limit, indirect clamp,
+Blackman-Harris 1.5 px filter, seed, no dithering. Resolution, frame range and
+the view transform are the .blend's own (1920x1080 at 100 % in both; the 04
+stand-in is Standard, 01 is Filmic, as the GPU backend renders them when the
+context has Blender's OCIO LUTs).
 
 CLI (after the last "--"), stdout protocol and timing semantics are those the
 reference worker parses (worker/src/rendering/runner/utilities.rs:105-203):
@@ -62,9 +69,7 @@ def main():
     cy.seed = int(os.environ.get("RR_SEED", "0"))
     cy.pixel_filter_type = "BLACKMAN_HARRIS"
     cy.filter_width = 1.5
-    scene.view_settings.view_transform = "Standard"
-    scene.view_settings.look = "None"
-    scene.render.dither_intensity = 0.0
+    scene.render.dither_intensity = 0.0  # the GPU backend does not dither
     scene.frame_set(frame)
     scene.render.filepath = hash_substitute(a["render-output"], frame)
     scene.render.image_settings.file_format = a["render-format"]
