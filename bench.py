@@ -179,50 +179,30 @@ KERNEL_OF_CLASS = {"build": [], "primary": ["k_primary", "k_trace_primary"],
                    "tiles": ["k_tiles"]}
 
 
-def pmc_traffic(cls: str, path: str):
-    """HBM bytes per launch of the class's timed kernel (not the counting
-    instantiation) from a committed rocprofv3 PMC summary (tools/pmc_summary.py
-    traffic), or None when absent."""
-    if not os.path.exists(path):
-        return None
+def pmc_kernels(path: str | None) -> dict:
+    """Per-kernel entries of a committed rocprofv3 PMC summary
+    (tools/pmc_summary.py traffic), {} when absent."""
+    if not path or not os.path.exists(path):
+        return {}
     with open(path) as fh:
-        ks = json.load(fh)["kernels"]
-    for name in KERNEL_OF_CLASS.get(cls, []):
-        for k, v in ks.items():
-            if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
-                return {"bytes": v["traffic_bytes"], "source": os.path.relpath(path, ROOT), "kernel": k}
-    return None
+        return json.load(fh)["kernels"]
 
 
-def pmc_valu(cls: str, path: str, avg_ms: float, kernel_clock_ghz: float = 0.0):
-    """VALU issue of the class's timed kernel from the committed PMC summary:
-    SQ_INSTS_VALU wave-instructions per launch over the launch time, against
-    0.5 per clock per SIMD x 1024 SIMDs at the 2.4 GHz peak engine clock (the
-    roofline peak; `frac`), and at the clock the kernel itself measured
-    (`kernel_clock_ghz`, shader-clock over real-time ticks inside k_tiles'
-    counting launch, MI355X_MICROARCH.md DVFS item 6; `issue_util_at_kernel_clock`):
-    the chip holds its clock well under 2.4 GHz under this load."""
-    if not os.path.exists(path):
-        return None
-    with open(path) as fh:
-        ks = json.load(fh)["kernels"]
+def pmc_entry(ks: dict, cls: str, variant: str | None = None):
+    """(name, entry) of the class's timed kernel (not the counting
+    instantiation) in a PMC summary: `variant` = the template arguments after
+    kCount (k_tiles: "true" whole-tile units, "false" sample-group slices)."""
     for name in KERNEL_OF_CLASS.get(cls, []):
         for k, v in ks.items():
-            if k.split("<")[0] == name and ("<" not in k or k.split("<")[1].startswith("false")):
-                if "SQ_INSTS_VALU" not in v or "GRBM_GUI_ACTIVE" not in v:
-                    return None
-                achieved = v["SQ_INSTS_VALU"] / (avg_ms * 1e-3)  # wave-instructions/s at the bench's launch time
-                peak = VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * PEAK_CLOCK_GHZ * 1e9
-                out = {"achieved": round(achieved / 1e9, 1), "peak": round(peak / 1e9, 1),
-                       "unit": "G wave-instr/s", "frac": round(achieved / peak, 3), "clock_ghz": PEAK_CLOCK_GHZ,
-                       "clock_source": "peak engine clock (MI355X_MICROARCH.md)",
-                       "valu_per_launch": round(v["SQ_INSTS_VALU"]), "source": os.path.relpath(path, ROOT)}
-                if kernel_clock_ghz > 0:
-                    out["kernel_clock_ghz"] = round(kernel_clock_ghz, 3)
-                    out["issue_util_at_kernel_clock"] = round(
-                        achieved / (VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * kernel_clock_ghz * 1e9), 3)
-                return out
-    return None
+            if k.split("<")[0] != name:
+                continue
+            targs = k.split("<")[1].rstrip(">").split(",") if "<" in k else []
+            if targs and targs[0] != "false":
+                continue  # the counting instantiation
+            if variant is not None and (len(targs) < 2 or targs[1] != variant):
+                continue
+            return k, v
+    return None, None
 
 
 def frame_partition(frames, step: int, rank: int, world: int):
@@ -459,17 +439,26 @@ def names_idx(cls: str, rr) -> int:
     return list(rr.native.KERNEL_CLASSES).index(cls)
 
 
-def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps):
+def valu_peak_per_s() -> float:
+    return VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * PEAK_CLOCK_GHZ * 1e9
+
+
+def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=None):
     """The dominant kernel class against the roofline that actually bounds it
     (DESIGN.md §6):
       * LDS-resident scenes (k_tiles, 04vs / 01): VALU issue. The scene lives
-        in LDS; HBM sees only the film, so the HBM fraction is an honest small
-        number (kept as hbm_frac) and the bound is vector-instruction issue:
-        SQ_INSTS_VALU per launch over the launch time against 0.5 wave-
-        instructions per clock per SIMD.
-      * split path over a hierarchy that fits in L2 / MALL (02 / 03): HBM from
-        the PMC counters (FETCH_SIZE + WRITE_SIZE per launch over the launch
-        time); SURVEY §8(d)'s per-visit byte formula over-counts cache hits.
+        in LDS; HBM sees only the film (hbm_frac) and the bound is vector-
+        instruction issue: SQ_INSTS_VALU wave-instructions against 0.5 per
+        clock per SIMD x 1024 SIMDs at the 2.4 GHz peak clock. Headline = the
+        TIMED REGION: the launches the timed frames ran (whole-tile units for
+        every frame that overlapped a pending one, sample-group slices for a
+        frame alone; each kind priced by its own PMC count) over the timed
+        region's wall time; avg_launch_ms = that wall time per launch (<=
+        ms_per_step). The same launches timed alone by HIP events after the
+        timed region are the secondary `solo` figure.
+      * split path over a hierarchy that fits in L2 / MALL (02 / 03): bound by
+        memory latency (L2 hits waited on), reported as l2_hit_rate and
+        wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES beside the PMC HBM rate.
       * split path over a hierarchy far above MALL (C5): HBM, SURVEY §8(d)'s
         algorithmic bytes (64 B per node visit, 48 B per triangle test + the
         ray / hit stream); the PMC traffic beside it."""
@@ -480,43 +469,88 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps):
     bytes_frame, survey_frame = algorithmic_bytes(cls, cstats, scene_bytes, split)
     launches_frame = max(launches[dom] / max(steps, 1), 1)
     avg_ms = kernel_ms[dom] / max(launches[dom], 1)
-    per_s = lambda b: b / launches_frame / (avg_ms * 1e-3) / 1e9  # noqa: E731
     wl_key = "" if args.workload == "04vs" else f"_{args.workload}"
-    pmc = args.pmc_summary or newest_profile("%s_pmc" + wl_key + ".json")
-    tr = pmc_traffic(cls, pmc) if pmc else None
-    valu = pmc_valu(cls, pmc, avg_ms, float(getattr(cstats, "kernel_clock_ghz", 0.0))) if pmc else None
+    pmc_path = args.pmc_summary or newest_profile("%s_pmc" + wl_key + ".json")
+    ks = pmc_kernels(pmc_path)
+    src = os.path.relpath(pmc_path, ROOT) if ks else None
+    if cls == "tiles" and not split:
+        _, e_sl = pmc_entry(ks, cls, "false")
+        _, e_wh = pmc_entry(ks, cls, "true")
+        if e_sl is None:  # a summary from before the whole-tile variant (k_tiles<false>)
+            _, e_sl = pmc_entry(ks, cls)
+        v_sl = e_sl.get("SQ_INSTS_VALU") if e_sl else None
+        v_wh = e_wh.get("SQ_INSTS_VALU") if e_wh else None
+        peak = valu_peak_per_s()
+        out = {"kernel": cls, "bound": "valu", "unit": "G wave-instr/s", "peak": round(peak / 1e9, 1),
+               "clock_ghz": PEAK_CLOCK_GHZ, "clock_source": "peak engine clock (MI355X_MICROARCH.md)",
+               "valu_source": src, "launches_per_frame": launches_frame,
+               "bytes_per_launch_algorithmic": round(bytes_frame / launches_frame)}
+        if timed is not None:
+            n_wh, n_sl, t_s = timed["whole"], timed["sliced"], timed["elapsed"]
+            eff_ms = t_s / max(n_wh + n_sl, 1) * 1e3
+            out["avg_launch_ms"] = round(eff_ms, 4)
+            out["launch_timing"] = (f"timed region: {n_wh + n_sl} k_tiles launches ({n_wh} whole-tile, {n_sl} "
+                                    f"sample-group sliced) over {t_s * 1e3:.2f} ms of wall time; consecutive "
+                                    "frames overlap on the device, so this is the time per launch the timed "
+                                    "frames sustained")
+            if v_sl is not None and (v_wh is not None or n_wh == 0):
+                valu = (n_wh * (v_wh or 0.0) + n_sl * v_sl) / max(n_wh + n_sl, 1)
+                ach = valu / (eff_ms * 1e-3)
+                out.update({"achieved": round(ach / 1e9, 1), "frac": round(ach / peak, 3),
+                            "valu_per_launch": round(valu),
+                            "valu_per_launch_whole": round(v_wh) if v_wh is not None else None,
+                            "valu_per_launch_sliced": round(v_sl)})
+            else:
+                out.update({"achieved": None, "frac": None, "valu_per_launch": None,
+                            "note_valu": "no PMC count for the timed launches' kernel variant"})
+        if v_sl is not None:
+            out["solo"] = {"avg_launch_ms": round(avg_ms, 4), "valu_per_launch": round(v_sl),
+                           "achieved": round(v_sl / (avg_ms * 1e-3) / 1e9, 1),
+                           "frac": round(v_sl / (avg_ms * 1e-3) / peak, 3),
+                           "launch_timing": f"HIP events around each launch, {steps} frames rendered one at a "
+                                            "time after the timed region (sample-group slices)"}
+        kc = float(getattr(cstats, "kernel_clock_ghz", 0.0))
+        if kc > 0 and out.get("achieved"):
+            out["kernel_clock_ghz"] = round(kc, 3)
+            out["issue_util_at_kernel_clock"] = round(out["achieved"] * 1e9 /
+                                                      (VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * kc * 1e9), 3)
+        out["wave_fill_solo"] = round(float(getattr(cstats, "kernel_wave_fill", 0.0)), 3)
+        t_ms = out.get("avg_launch_ms", avg_ms)
+        comp = bytes_frame / launches_frame / (t_ms * 1e-3) / 1e9
+        tr = e_wh if (e_wh and timed and timed["whole"]) else e_sl
+        out.update({"hbm_compulsory_gbs": round(comp, 2), "hbm_frac": round(comp / HBM_PEAK_GBS, 4),
+                    "hbm_survey_formula_gbs": round(survey_frame / launches_frame / (t_ms * 1e-3) / 1e9, 2),
+                    "traffic": round(tr["traffic_bytes"]) if tr else None,
+                    "traffic_gbs": round(tr["traffic_bytes"] / (t_ms * 1e-3) / 1e9, 1) if tr else None,
+                    "traffic_source": src if tr else None,
+                    "note": "k_tiles: scene in LDS, bound by vector-instruction issue (SQ_INSTS_VALU per launch / "
+                            "launch time vs 0.5 wave-instr/clk/SIMD x 1024 SIMDs at 2.4 GHz); HBM sees only the "
+                            "film + RGBA8 (hbm_frac)"})
+        return out
+    per_s = lambda b: b / launches_frame / (avg_ms * 1e-3) / 1e9  # noqa: E731
+    _, e = pmc_entry(ks, cls)
     hbm = {"hbm_algorithmic_gbs": round(per_s(survey_frame if split else bytes_frame), 2),
            "hbm_compulsory_gbs": round(per_s(bytes_frame), 2),
            "hbm_survey_formula_gbs": round(per_s(survey_frame), 2),
-           "traffic": round(tr["bytes"]) if tr else None,
-           "traffic_gbs": round(tr["bytes"] / (avg_ms * 1e-3) / 1e9, 1) if tr else None,
-           "traffic_source": tr["source"] if tr else None}
+           "traffic": round(e["traffic_bytes"]) if e else None,
+           "traffic_gbs": round(e["traffic_bytes"] / (avg_ms * 1e-3) / 1e9, 1) if e else None,
+           "traffic_source": src if e else None,
+           "launch_timing": "HIP events around each launch on the library's stream over the timed region"}
     base = {"kernel": cls, "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": launches_frame,
             "bytes_per_launch_algorithmic": round((survey_frame if split else bytes_frame) / launches_frame)}
-    if not split:
-        if valu is None:
-            return {**base, "bound": "valu", "achieved": None, "peak": None, "unit": "G wave-instr/s", "frac": None,
-                    **hbm, "hbm_frac": round(per_s(bytes_frame) / HBM_PEAK_GBS, 4),
-                    "note": "VALU-issue bound (LDS-resident scene); no PMC summary to price it"}
-        return {**base, "bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"], "unit": valu["unit"],
-                "frac": valu["frac"], "clock_ghz": valu["clock_ghz"], "clock_source": valu["clock_source"],
-                "valu_per_launch": valu["valu_per_launch"],
-                **{k: valu[k] for k in ("kernel_clock_ghz", "issue_util_at_kernel_clock") if k in valu},
-                "wave_fill": round(float(getattr(cstats, "kernel_wave_fill", 0.0)), 3),
-                "valu_source": valu["source"], **hbm, "hbm_frac": round(per_s(bytes_frame) / HBM_PEAK_GBS, 4),
-                "note": "k_tiles: scene in LDS, bound by vector-instruction issue (SQ_INSTS_VALU per launch / launch "
-                        "time vs 0.5 wave-instr/clk/SIMD x 1024 SIMDs); HBM sees only film + RGBA8 (hbm_frac)"}
+    lat = {k: round(e[k], 3) for k in ("l2_hit_rate", "wait_frac") if e and k in e}
     resident = n * (64.0 + 48.0) < MALL_BYTES  # hierarchy + triangles fit in the 256 MB MALL
-    if resident and tr is not None:
-        ach = tr["bytes"] / (avg_ms * 1e-3) / 1e9
-        return {**base, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), **hbm,
-                "note": "hierarchy + triangles fit in L2/MALL: achieved = PMC HBM traffic (FETCH_SIZE x2 + WRITE_SIZE, "
-                        "MI355X_MICROARCH.md) per launch / launch time; the SURVEY 8(d) per-visit formula "
-                        "(hbm_survey_formula_gbs) counts cache hits as HBM bytes"}
+    if resident and e is not None:
+        ach = e["traffic_bytes"] / (avg_ms * 1e-3) / 1e9
+        return {**base, "bound": "latency", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), **lat, **hbm,
+                "note": "hierarchy + triangles fit in L2/MALL: the kernel waits on cache-hit latency, not HBM "
+                        "bandwidth (l2_hit_rate, wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES from the PMC passes); "
+                        "achieved / frac are its PMC HBM rate (FETCH_SIZE x2 + WRITE_SIZE per launch / launch "
+                        "time) for reference only"}
     ach = per_s(survey_frame)
     return {**base, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), **hbm,
+            "frac": round(ach / HBM_PEAK_GBS, 4), **lat, **hbm,
             "note": "hierarchy above MALL: achieved = SURVEY 8(d) algorithmic bytes (64 B per node visit, 48 B per "
                     "triangle test + ray/hit stream) per launch / launch time; traffic = PMC HBM bytes per launch "
                     "(FETCH_SIZE counts Infinity-Cache hits, so it is an upper bound on HBM reads)"}
@@ -605,6 +639,7 @@ def main():
     launches = [0] * 8
     rays = {"camera": 0, "camera_traced": 0, "extension": 0, "shadow": 0}
     substituted = []
+    tile_modes = {"whole": 0, "sliced": 0}
 
     def account(st):
         for k in range(8):
@@ -615,6 +650,10 @@ def main():
         rays["extension"] += st.extension_rays
         rays["shadow"] += st.shadow_rays
         substituted.append(st.view_transform_substituted)
+        if st.tile_slices == 1:
+            tile_modes["whole"] += 1
+        elif st.tile_slices > 1:
+            tile_modes["sliced"] += 1
 
     barrier(runner.ctx)
     t0 = time.perf_counter()
@@ -671,21 +710,8 @@ def main():
         roofline = None
         if not args.no_profile:
             dom = max(range(len(names)), key=lambda k: roof_ms[k])
-            roofline = roofline_line(args, names[dom], cstats, roof_ms, roof_launches, names, roof_steps)
-            if roofline.get("bound") == "valu" and roofline.get("valu_per_launch") and solo:
-                # the same VALU work issued over the timed region's wall time (frames
-                # overlapping, work units not cut by sample group when a frame overlaps
-                # a pending one): a lower bound of the issue rate the kernel sustains there
-                k = names_idx("tiles", rr)
-                rate = roofline["valu_per_launch"] * launches[k] / t_max / 1e9
-                roofline["achieved_timed_region"] = round(rate, 1)
-                roofline["frac_timed_region"] = round(rate / roofline["peak"], 3)
-            roofline["launch_timing"] = (
-                f"HIP events around each launch on the library's stream, {roof_steps} frames rendered one at a "
-                "time after the timed region (in the timed region consecutive k_tiles frames overlap on the "
-                "device, and an event pair would also span the wait for the previous frame's CUs; a frame "
-                "rendered alone cuts its tiles into sample-group units, an overlapping one does not)" if solo else
-                "HIP events around each launch on the library's stream over the timed region")
+            timed = ({**tile_modes, "elapsed": elapsed} if names[dom] == "tiles" and sum(tile_modes.values()) else None)
+            roofline = roofline_line(args, names[dom], cstats, roof_ms, roof_launches, names, roof_steps, timed)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -711,6 +737,7 @@ def main():
                        "pipelining": "serial (rr_render_frame per frame)" if args.serial else
                                      "3 frames in flight: frame N encoded + written while N+1 renders and N+2 waits on its stream",
                        "view_transform_substituted": int(any(substituted)),
+                       "k_tiles_units": tile_modes,
                        "placement_by_rank": places},
             "mrays_per_s_per_gpu": round(traced / elapsed / 1e6, 1),
             # SURVEY 8(d)'s form: rays traced over the summed render-kernel time

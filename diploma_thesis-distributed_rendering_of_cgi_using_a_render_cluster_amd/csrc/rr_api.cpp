@@ -32,7 +32,7 @@
 
 using namespace rr;
 
-static_assert(kMatLutIntervals == kMatLutN && kMatLutFloatsPerMat == kMatLutStride,
+static_assert(kMatLutIntervals == kMatLutN && kMatLutFloatsPerMat == kMatLutStride && kMatLutPsOffset == kMatLutPs,
               "scene.hpp material-table layout must match rr_device.h");
 
 namespace {

@@ -311,6 +311,18 @@ RR_HD float table_lerp(FloatP t, int n, float u) {
     const float fr = f - (float)i;
     return fmaf(t[i + 1] - t[i], fr, t[i]);
 }
+// The same read without the two range branches (each a divergent branch with
+// its exec-mask bookkeeping on the per-sample path), for u in [0, 1] and a
+// table whose entry t[n] repeats t[n - 1] (or u < 1): then i lies in
+// [0, n - 1], and at i = n - 1 (u = 1) the lerp returns fmaf(0, 0, t[n - 1])
+// = t[n - 1], the bits table_lerp returns.
+template <typename FloatP>
+RR_HD float table_lerp_padded(FloatP t, int n, float u) {
+    const float f = u * (float)(n - 1);
+    const int i = (int)f;
+    const float fr = f - (float)i;
+    return fmaf(t[i + 1] - t[i], fr, t[i]);
+}
 
 // ------------------------------------------------------- screen culling ---
 // Screen-space bounds of the scene box [lo, hi] for the pinhole camera of
@@ -705,7 +717,8 @@ RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float
 // of the half angle, the pick probability against the cosine of the view
 // angle (interpolation error below 4e-4 for specular IORs 1.2 .. 2).
 constexpr int kMatLutN = 128;
-constexpr int kMatLutStride = 260;  // floats per material: FH [0, 128], ps [129, 257], 2 pad
+constexpr int kMatLutStride = 260;  // floats per material: FH [0, 128] + repeat, ps [130, 258] + repeat
+constexpr int kMatLutPs = 130;      // offset of the pick-probability channel
 
 struct Mat {
     float3 base;
@@ -743,10 +756,12 @@ RR_HD float schlick_w(float c) {
     return m2 * m2 * m;
 }
 
-// A material table channel at u in [0, 1] (t: global or LDS pointer).
+// A material table channel at u in [0, 1] (t: global or LDS pointer); each
+// channel's last entry is repeated (build_material_lut), so the branch-free
+// read applies.
 template <typename FloatP>
 RR_HD float lut_at(FloatP t, float u) {
-    return table_lerp(t, kMatLutN + 1, fminf(fmaxf(u, 0.0f), 1.0f));
+    return table_lerp_padded(t, kMatLutN + 1, fminf(fmaxf(u, 0.0f), 1.0f));
 }
 
 // Terms of the view direction shared by every evaluation at one shading point
@@ -818,7 +833,7 @@ template <typename FloatP>
 RR_HD BsdfView bsdf_view(const Mat& m, FloatP lut, float3 N, float3 wo) {
     BsdfView v;
     v.cosV = dot3(N, wo);
-    v.ps = lut_at(lut + (kMatLutN + 1), v.cosV);  // 0 for Lambert and without a specular closure
+    v.ps = lut_at(lut + kMatLutPs, v.cosV);  // 0 for Lambert and without a specular closure
     v.fv = schlick_w(v.cosV);
     const float a2 = m.a2;
     v.cv1 = v.cosV + sqrt_rn(fmaf((1.0f - a2) * v.cosV, v.cosV, a2));  // >= a2 >= 1e-6 (as cl1)

@@ -858,9 +858,12 @@ void build_material_lut(const float* m, float* out) {
         const double wsp = ((c0[0] * (1.0 - fh) + fh) + (c0[1] * (1.0 - fh) + fh) + (c0[2] * (1.0 - fh) + fh)) / 3.0;
         double ps = 0.0;
         if (model != 1 && spec_on) ps = wsp + wd > 0.0 ? wsp / (wsp + wd) : 1.0;
-        out[N + 1 + i] = (float)ps;
+        out[kMatLutPsOffset + i] = (float)ps;
     }
-    for (int i = 2 * (N + 1); i < kMatLutFloatsPerMat; ++i) out[i] = 0.0f;
+    // each channel's last entry repeated once: the device reads the tables with
+    // a branch-free lerp that touches t[i + 1] also at u = 1 (rr_device.h lut_at)
+    out[N + 1] = out[N];
+    out[kMatLutPsOffset + N + 1] = out[kMatLutPsOffset + N];
 }
 
 FrameSetup setup_frame(const SceneDesc& s, int frame, const rr_render_params* p) {

@@ -173,6 +173,8 @@ void build_filter_table(float width, float* table /* kFilterTableSize */);
 // same way).
 constexpr int kMatLutIntervals = 128;
 constexpr int kMatLutFloatsPerMat = 260;
+// layout: FH [0, 128] + a repeat of [128] at 129 | ps [130, 258] + a repeat at 259
+constexpr int kMatLutPsOffset = 130;
 void build_material_lut(const float* mat12, float* out /* kMatLutFloatsPerMat */);
 void build_srgb_lut(float* lut /* kSrgbLutSize + 1 */);
 

@@ -155,8 +155,9 @@ template <typename FloatP>
 __device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt, int px, int py,
                                               uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
                                               const ScreenCull* cull = nullptr, bool* culled = nullptr) {
-    const float fx = (float)px + 0.5f + table_lerp(filt, kFilterN, rng(key, 0));
-    const float fy = (float)py + 0.5f + table_lerp(filt, kFilterN, rng(key, 1));
+    // rng() < 1: the filter table is read without its range branches
+    const float fx = (float)px + 0.5f + table_lerp_padded(filt, kFilterN, rng(key, 0));
+    const float fy = (float)py + 0.5f + table_lerp_padded(filt, kFilterN, rng(key, 1));
     if (cull) {
         *culled = cull->outside(fx, fy);
         if (*culled) {  // a miss: no direction needed (shade() of a miss reads only T and the world)
@@ -1691,12 +1692,15 @@ struct TileSlices {
 };
 using TilesFn = void (*)(FrameConsts, SceneArgs, uint32_t*, float4*, const float*, uchar4*, uint32_t*, int32_t*,
                          unsigned long long*, TileSlices);
-// k_tiles<count> of tiles.hip: this file compiled again with RR_TILES_TU and
-// without SLP vectorisation (see the Makefile).
-TilesFn tiles_kernel(bool count);
+// k_tiles<count, whole> of tiles.hip: this file compiled again with
+// RR_TILES_TU and without SLP vectorisation (see the Makefile). whole: one
+// work unit per box tile (the frame overlaps a pending k_tiles frame,
+// TileSlices.n == 1), a variant of its own so that the slab code is compiled
+// out and a counter pass tells its launches from the sliced ones by name.
+TilesFn tiles_kernel(bool count, bool whole);
 namespace {
 
-template <bool kCount>
+template <bool kCount, bool kWhole>
 RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
                      const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
@@ -1731,7 +1735,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     // unit serialised ~35k device-scope atomics on one address per 04vs frame.
     const int ng = (fc.spp_total + kFilmGroup - 1) / kFilmGroup;
     const int nb = to.bw * to.bh;
-    const int n_sliced = nb * sl.n;
+    const int n_slices = kWhole ? 1 : sl.n;
+    const int n_sliced = nb * n_slices;
     const int n_units = n_sliced + (to.n - nb);  // box slices, then one unit per background tile
     const int n_shards = min((int)gridDim.x, kTileShards);  // small frames launch fewer blocks than shards
     const int shard = (int)blockIdx.x % n_shards;
@@ -1742,9 +1747,9 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         u = __builtin_amdgcn_readlane(u, 0) * n_shards + shard;
         if (u >= n_units) break;
         if (u < n_sliced) {  // box tiles in the order of k_tile_order (the heaviest first)
-            const int j = u / sl.n;
-            k = u - j * sl.n;
-            nk = sl.n;
+            const int j = kWhole ? u : u / n_slices;
+            k = kWhole ? 0 : u - j * n_slices;
+            nk = n_slices;
             t = uniform_i(sl.order[j]);
         } else {  // background tiles (the world term) fill the end of the launch
             t = nb + (u - n_sliced);
@@ -1851,7 +1856,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             add_to(P, L);
             group_end(s);
         }
-        if (nk > 1) {  // one group of a sliced tile: its sum goes to the slab, k_tiles_fold adds them up
+        if (!kWhole && nk > 1) {  // one group of a sliced tile: its sum goes to the slab, k_tiles_fold adds them up
             float* const slab = sl.slab + (size_t)t * sl.floats + (size_t)k * 192;
             slab[lane] = acc.x;
             slab[64 + lane] = acc.y;
@@ -1884,7 +1889,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
 #ifndef RR_TILES_WAVES
 #define RR_TILES_WAVES 4  // waves per SIMD the register budget must admit (<= 128 VGPRs)
 #endif
-template <bool kCount>
+template <bool kCount, bool kWhole>
 __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc, SceneArgs sa,
                                                                   uint32_t* __restrict__ tile_ctr,
                                                                   float4* __restrict__ film,
@@ -1899,7 +1904,7 @@ __global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc
     lds_int* stack = lds_slot(lds_stack);
     int used;
     const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
-    tiles_body<kCount>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry);
+    tiles_body<kCount, kWhole>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry);
 }
 
 #endif  // RR_TILES_TU
@@ -2067,7 +2072,10 @@ __global__ void k_debug_trace4(const QNode4* __restrict__ nodes, const TriPack* 
 }  // namespace
 
 #if RR_TILES_TU
-TilesFn tiles_kernel(bool count) { return count ? k_tiles<true> : k_tiles<false>; }
+TilesFn tiles_kernel(bool count, bool whole) {
+    return count ? (whole ? k_tiles<true, true> : k_tiles<true, false>)
+                 : (whole ? k_tiles<false, true> : k_tiles<false, false>);
+}
 #else
 int device_cu_count() {
     static int cus = 0;
@@ -2172,7 +2180,7 @@ struct Grids {
     TailFn kt;
     TilesFn kx;
     int tiles;
-    Grids(const FrameConsts& fc, bool count) {
+    Grids(const FrameConsts& fc, bool count, bool whole) {
         lds = scene_in_lds(fc.n_tris, fc.n_mats, fc.n_lights);
         kp = lds ? (count ? k_primary<true, true> : k_primary<false, true>)
                  : (count ? k_primary<true, false> : k_primary<false, false>);
@@ -2194,7 +2202,7 @@ struct Grids {
         extend = grid_for(ke, dyn_extend);
         shadow = grid_for(ks, dyn_shadow);
         tail = grid_for(kt, dyn_extend);
-        kx = tiles_kernel(count);
+        kx = tiles_kernel(count, whole);
         tiles = lds ? grid_for(kx, dyn_primary) : 0;
     }
 };
@@ -2344,7 +2352,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
 void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_t st) {
     const int npix = base.npix;
     const size_t npaths = (size_t)npix * base.spp_chunk;
-    const Grids G(base, p.count_traversal);
+    const Grids G(base, p.count_traversal, p.tile_whole);
     p.last_tile_slices = 0;
     if (frame_uses_tiles(base, p.force_wavefront)) {  // one launch: all samples of every tile
         p.ensure_tiles();

@@ -737,7 +737,9 @@ static double fresnel_dielectric_d(double cosi, double eta) {
 
 static double clamp01d(double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); }
 
-/* FH(cos of the half angle) [0, 128] | spec pick probability(cos of the view) [129, 257] */
+/* FH(cos of the half angle) [0, 128] + [128] repeated | spec pick probability(cos of
+ * the view) [130, 258] + [258] repeated (csrc/scene.cpp build_material_lut) */
+#define ORC_LUT_PS 130
 void orc_material_lut(const float* m, float* out) {
     const int N = ORC_LUT_N;
     double spec = m[4], met = m[3];
@@ -759,9 +761,10 @@ void orc_material_lut(const float* m, float* out) {
         double wsp = ((c0[0] * (1.0 - fh) + fh) + (c0[1] * (1.0 - fh) + fh) + (c0[2] * (1.0 - fh) + fh)) / 3.0;
         double ps = 0.0;
         if (model != 1 && spec_on) ps = wsp + wd > 0.0 ? wsp / (wsp + wd) : 1.0;
-        out[N + 1 + i] = (float)ps;
+        out[ORC_LUT_PS + i] = (float)ps;
     }
-    for (int i = 2 * (N + 1); i < ORC_LUT_STRIDE; ++i) out[i] = 0.0f;
+    out[N + 1] = out[N];
+    out[ORC_LUT_PS + N + 1] = out[ORC_LUT_PS + N];
 }
 
 static float lut_at(const float* t, float u) {
@@ -824,7 +827,7 @@ static v3 eval_bsdf(const mat_t* m, const float* lut, v3 N, v3 wo, v3 wi, float 
     return V(fmaf(F.x, ks, m->base.x * kd), fmaf(F.y, ks, m->base.y * kd), fmaf(F.z, ks, m->base.z * kd));
 }
 
-static float p_spec(const float* lut, float cosV) { return lut_at(lut + ORC_LUT_N + 1, cosV); }
+static float p_spec(const float* lut, float cosV) { return lut_at(lut + ORC_LUT_PS, cosV); }
 
 /* GGX visible normals by spherical caps (Dupuy & Benyoub 2023), csrc/rr_device.h sample_vndf */
 static v3 vndf(v3 v, float alpha, float dx, float dy) {

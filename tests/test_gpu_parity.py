@@ -541,7 +541,8 @@ def test_timed_configuration_bands_bit_exact(rr, tmp_path, job_name, frames):
         assert slices[frames[0]] == 4 and all(slices[f] == 1 for f in frames[1:])
         scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, root))
         for f in frames:
-            img = np.asarray(Image.open(tmp_path / f"{f:06d}.png").convert("RGBA"))
+            out = rr.naming.output_path_without_extension(str(tmp_path), job.output_file_name_format, f)
+            img = np.asarray(Image.open(out + ".png").convert("RGBA"))
             assert img.shape == (1080, 1920, 4)
             st = runner.ctx.frame_state(scene, f)
             for r0, n_hit in _cube_bands_8bit(img, 4):

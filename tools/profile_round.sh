@@ -15,16 +15,19 @@ mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 
 if [ "$wl" == "c5" ]; then steps="--steps 2 --warmup 1"; psteps="--steps 1 --warmup 1"; else steps="--steps 10 --warmup 2"; psteps="--steps 3 --warmup 1"; fi
-# LDS-tile workloads (04vs, 01): frames overlap in the pipelined bench, so
-# launches run as whole-tile units that share the chip with their neighbours
-# and a traced launch's span is not its own cost. The counter passes and a
-# second trace therefore run the frames serially (sample-group units, one
-# launch on the chip at a time): the same launches the bench's solo pass
-# times for the roofline, so the per-launch VALU count and that trace's
-# average duration describe one kernel configuration.
+# LDS-tile workloads (04vs, 01): frames overlap in the pipelined bench, and
+# every frame that overlaps a pending one runs k_tiles<false, true> (whole-
+# tile units); a frame alone runs k_tiles<false, false> (sample-group
+# slices). The counter passes run the pipelined bench, so the summary holds
+# a per-launch count for both variants (the profiler serialises dispatches,
+# so each count is the launch's own); bench.py prices the timed region's
+# launches with them. A second kernel trace runs the frames serially (one
+# launch on the chip at a time): the solo launches of the roofline's
+# secondary figure.
 ser=""
 if [ "$wl" == "04vs" ] || [ "$wl" == "01" ]; then ser="--serial"; fi
-B="bench.py --workload $wl $psteps --no-cpu-baseline --no-profile $ser $extra"
+if [ "$wl" == "c5" ]; then psteps="--steps 1 --warmup 1"; else psteps="--steps 6 --warmup 1"; fi
+B="bench.py --workload $wl $psteps --no-cpu-baseline --no-profile $extra"
 
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
     -- python3 bench.py --workload $wl $steps --no-cpu-baseline $extra > "$out/trace_bench.json"
