@@ -22,6 +22,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "device.hpp"
@@ -193,6 +194,9 @@ struct rr_ctx {
     uint64_t chain_ticket = 0;   // last completed frame whose device start is known (0: none)
     double chain_unix = 0.0;     // its device start, UNIX seconds
     double last_render_end = 0.0;  // finished_rendering_at of the last completed frame
+    // scenes bound to this context: rr_destroy releases their device buffers
+    // and unbinds them, so a scene freed after its context touches no freed state
+    std::unordered_set<rr_scene*> scenes;
 };
 
 struct rr_scene {
@@ -263,6 +267,7 @@ void upload_scene(rr_ctx* c, rr_scene* s) {
 void bind_scene(rr_ctx* c, rr_scene* s) {
     if (s->ctx && s->ctx != c) throw std::runtime_error("scene belongs to another context");
     s->ctx = c;
+    c->scenes.insert(s);
     upload_scene(c, s);
 }
 
@@ -802,6 +807,10 @@ void rr_destroy(rr_ctx* c) {
     }
     for (auto& e : c->start_ring)
         if (e) (void)hipEventDestroy(e);
+    for (rr_scene* s : c->scenes) {  // still-open scenes: back to host-only handles
+        s->dev.release();
+        s->ctx = nullptr;
+    }
     for (auto& sl : c->slots) {
         if (sl.stream) (void)hipStreamDestroy(sl.stream);  // c->stream is slot 0's
         sl.release_private();
@@ -823,11 +832,10 @@ int rr_scene_load(rr_ctx* c, const char* path, rr_scene** out) {
     }
     return guarded([&] {
         std::unique_ptr<rr_scene> s(new rr_scene());
-        s->ctx = c;  // NULL: host-only handle, bound to a context at its first render
         s->desc = load_scene(path);
         s->dev.n_tris = (int)s->desc.tri_obj.size();
         s->dev.n_objs = (int)s->desc.objects.size();
-        if (c) upload_scene(c, s.get());
+        if (c) bind_scene(c, s.get());  // NULL: host-only handle, bound to a context at its first render
         *out = s.release();
         return RR_OK;
     });
@@ -846,6 +854,7 @@ void rr_scene_free(rr_scene* s) {
                 sl.alt_scene = nullptr;
             }
         }
+        c->scenes.erase(s);
     }
     s->dev.release();
     delete s;
