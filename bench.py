@@ -393,7 +393,8 @@ def spawn_ranks(args) -> int:
     return max(abs(p.wait()) for p in procs)
 
 
-def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin frame 1", spp_scale: float = 1.0):
+def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin frame 1", spp_scale: float = 1.0,
+                 threads: int | None = None):
     """Oracle (C restatement, OpenMP) on the host cores: 4-row bands of the same
     frame, taken in an order spread over the image, until the budget is spent or
     the frame is done; extrapolated to frames/s with ONE hierarchy build per
@@ -405,7 +406,8 @@ def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin 
     rendered (render time is linear in spp; the build is not)."""
     H = int(state.render_ints[1])
     usable, nproc, model = host_cpu()
-    threads = int(os.environ.get("OMP_NUM_THREADS") or usable)
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS") or usable)
     bands = list(range(0, H, 4))
     done_rows, t_used, t_render, builds = 0, 0.0, 0.0, []
     order = [b for k in range(16) for b in bands[k::16]]
@@ -723,6 +725,11 @@ def main():
                 state = runner.ctx.frame_state(scene, f_count, rr.default_params(spp=spp_cpu))
                 cpu = cpu_baseline(O, state, args.cpu_seconds, f"{args.workload} frame {f_count}",
                                    spp_scale=spp_full / spp_cpu)
+                # the thesis' own single-worker point: one worker with 4 CPU cores
+                # (scripts/arnes/queue-batch_04vs_14400f-1w.sh:6-7)
+                w1 = cpu_baseline(O, state, args.cpu_seconds / 2, f"{args.workload} frame {f_count}",
+                                  spp_scale=spp_full / spp_cpu, threads=4)
+                cpu["thesis_point_w1_t4"] = {k: w1[k] for k in ("value", "unit", "cores", "sample")}
             except Exception as e:  # baseline is reported, never the target
                 cpu = {"value": None, "unit": "frames/s", "error": str(e)}
         traced = rays["camera_traced"] + rays["extension"] + rays["shadow"]
