@@ -1656,6 +1656,26 @@ RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint3
     }
 }
 
+// The tile kernel's secondary traversals as out-of-line functions: on the
+// scenes it renders they are rare (04vs / 01: a cube, every face a hull side,
+// so no shadow or continuation ray is traversed but for the odd path through
+// an edge crack), and inlined, their registers and control flow weighed on the
+// whole sample loop (A/B, 40 pipelined frames: 04vs 886 -> 907, 01 901 -> 923
+// frames/s; solo launches -1 %). Their state goes through the call's stack
+// frame; the register budget stays at 4 waves per SIMD (5 measured slower
+// solo, +-0 pipelined).
+template <bool kCount>
+__device__ __noinline__ bool shadow_trace(const LdsView& v, int n_tris, float3 so, float3 sd, float dist, TravStack& st,
+                                          TravCount& cnt) {
+    Hit hs;
+    return traverse<true, kCount>(v.nodes, v.tris, n_tris, so, sd, 0.0f, dist, st, hs, cnt);
+}
+template <bool kCount>
+__device__ __noinline__ Hit ext_trace(const LdsView& v, int n_tris, float3 o, float3 d, TravStack& st, TravCount& cnt) {
+    Hit h;
+    traverse<false, kCount>(v.nodes, v.tris, n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
+    return h;
+}
 // The tile kernel's shadow rays, traced inside shade() (any hit over the
 // LDS-resident LBVH).
 template <bool kCount>
@@ -1666,8 +1686,7 @@ struct InlineShadow {
     TravStack& st;
     TravCount& cnt;
     RR_D bool operator()(float3 so, float3 sd, float dist) const {
-        Hit hs;
-        return traverse<true, kCount>(v.nodes, v.tris, n_tris, so, sd, 0.0f, dist, st, hs, cnt);
+        return shadow_trace<kCount>(v, n_tris, so, sd, dist, st, cnt);
     }
 };
 
@@ -1821,7 +1840,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                         set_miss(h, tmax);
                         if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);
                     } else {
-                        traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, ce);
+                        h = ext_trace<kCount>(v, fc.n_tris, o, d, st, ce);
                     }
                     shade(fc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, fc.n_tris, st, cs});
                     cont = so.cont;
