@@ -172,9 +172,9 @@ def algorithmic_bytes(cls: str, stats, scene_bytes: float, split: bool) -> tuple
     return stream + min(trav, scene_bytes), stream + trav
 
 
-# kernel names per class: fused (LDS scenes) and split (large scenes) paths
-KERNEL_OF_CLASS = {"build": [], "primary": ["k_primary", "k_trace_primary"],
-                   "extend": ["k_extend", "k_trace_extend"], "shadow": ["k_shadow", "k_shadow_refill"],
+# kernel names per class: the split path (large scenes) and k_tiles (LDS-resident scenes)
+KERNEL_OF_CLASS = {"build": [], "primary": ["k_trace_primary", "k_trace_primary_packet"],
+                   "extend": ["k_trace_extend"], "shadow": ["k_shadow_refill"],
                    "shade": ["k_shade_extend", "k_shade_primary"], "accumulate": ["k_accumulate"],
                    "tiles": ["k_tiles"]}
 

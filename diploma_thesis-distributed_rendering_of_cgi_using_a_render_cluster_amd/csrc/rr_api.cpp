@@ -279,11 +279,13 @@ void bind_scene(rr_ctx* c, rr_scene* s) {
 // collapsed to the quantised BVH4 (rr_device.h QNode4).
 constexpr int kHierLbvh = 2, kHierPloc = 3, kHierBvh4 = 4;
 
-// The hierarchy the frame kernels walk: LDS-resident scenes the LBVH (fused
-// path), larger scenes the quantised BVH4 (split path).
-int frame_hier(int n_tris, int n_mats, int n_lights) {
-    if (scene_in_lds(n_tris, n_mats, n_lights)) return kHierLbvh;
-    return kHierBvh4;
+FrameConsts make_consts(const FrameSetup& fs, int n_tris);
+
+// The hierarchy the frame kernels walk: the LBVH for frames k_tiles renders
+// (LDS-resident scenes), the quantised BVH4 for the split path (larger scenes,
+// and LDS-resident ones under RR_FLAG_WAVEFRONT).
+int frame_hier(const FrameSetup& fs, int n_tris) {
+    return frame_uses_tiles(make_consts(fs, n_tris), (fs.flags & RR_FLAG_WAVEFRONT) != 0) ? kHierLbvh : kHierBvh4;
 }
 
 // The view transform a frame on ctx is rendered with: Filmic needs the
@@ -344,7 +346,7 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     std::memcpy(up + nl, fs.materials.data(), nm * sizeof(float));
     std::memcpy(up + nl + nm, fs.obj_xform.data(), nx * sizeof(float));
     DevScene& d = s->dev;
-    if (hier == 0) hier = frame_hier(d.n_tris, (int)(nm / RR_MAT_FLOATS), (int)(nl / RR_LIGHT_FLOATS));
+    if (hier == 0) hier = frame_hier(fs, d.n_tris);
     const bool want4 = hier == kHierBvh4;
     const bool want_ploc = (hier == kHierPloc || hier == kHierBvh4) && d.n_tris > 2;
     const bool rebuild =
@@ -697,10 +699,7 @@ int do_encode(const uint8_t* rgba, int W, int H, const char* out_path, const cha
 
 // BVH width the frame kernels traverse for this scene (2: LDS-resident fused
 // path, 4: split path from HBM).
-int frame_hier_of(rr_scene* s, const FrameSetup& fs) {
-    return frame_hier(s->dev.n_tris, (int)(fs.materials.size() / RR_MAT_FLOATS),
-                      (int)(fs.lights.size() / RR_LIGHT_FLOATS));
-}
+int frame_hier_of(rr_scene* s, const FrameSetup& fs) { return frame_hier(fs, s->dev.n_tris); }
 
 FrameSlot* slot_for(rr_ctx* c, uint64_t ticket) { return &c->slots[ticket % RR_MAX_FRAMES_IN_FLIGHT]; }
 

@@ -364,106 +364,10 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     out.lob = lob + (glossy ? kGlossyOne : 1u);
 }
 
-// K8: segmented queues, no atomics, no barriers. Each producer WAVE owns
-// segment [wave * seg_cap, +seg_cap) of each output queue (wave = blockIdx.x *
-// kWavesPerBlock + wave in block) and appends to it in order: a lane's slot is
-// the wave's running cursor + its ballot prefix. At exit the wave publishes its
-// two segment lengths. seg_cap = ceil(input count / grid threads) * 64 bounds
-// what one wave can emit. A consumer turns a dense index j into a slot with
-// the prefix over the producer's segment lengths (SegIndex below), so queue
-// order is deterministic, no global counter is contended and waves of a block
-// never wait for each other.
 constexpr int kWavesPerBlock = kBlock / 64;
-constexpr int kMaxBlocksPerCu = 8;  // grid cap per CU (segment arrays are sized for it)
-struct SegCursor {
-    uint32_t c = 0, s = 0;  // items this wave has appended (wave-uniform)
-};
+constexpr int kMaxBlocksPerCu = 8;  // grid cap per CU
 
 RR_D uint32_t wave_id() { return blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); }
-
-__device__ __forceinline__ void emit(const ShadeOut& so, int pid, PathQueue out, ShadowQueue sq, uint32_t seg_base,
-                                     SegCursor& cur) {
-    const uint64_t mc = __ballot(so.cont), ms = __ballot(so.shadow);
-    const int lane = threadIdx.x & 63;
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    if (so.cont) {
-        const uint32_t s1 = seg_base + cur.c + (uint32_t)__popcll(mc & below);
-        out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
-        out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, i2f((int)so.lob));
-        out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, so.esc ? 1.0f : 0.0f);
-    }
-    if (so.shadow) {
-        const uint32_t s2 = seg_base + cur.s + (uint32_t)__popcll(ms & below);
-        sq.o[s2] = make_float4(so.so.x, so.so.y, so.so.z, i2f(pid));
-        sq.d[s2] = make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist);
-        sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, so.esc ? 1.0f : 0.0f);
-    }
-    cur.c += (uint32_t)__popcll(mc);
-    cur.s += (uint32_t)__popcll(ms);
-}
-
-// Producer epilogue: publish this wave's segment lengths.
-__device__ __forceinline__ void publish(const SegCursor& cur, uint32_t* __restrict__ seg_c,
-                                        uint32_t* __restrict__ seg_s) {
-    if ((threadIdx.x & 63) == 0) {
-        seg_c[wave_id()] = cur.c;
-        seg_s[wave_id()] = cur.s;
-    }
-}
-
-// Consumer side: exclusive prefix of the producer's nseg (= waves) segment
-// lengths in LDS (dynamic shared memory, nseg + 1 words), then dense index ->
-// slot.
-struct SegIndex {
-    lds_uint* pre;
-    int nseg;
-    uint32_t cap;
-    __device__ __forceinline__ uint32_t slot(uint32_t j) const {
-        int lo = 0, hi = nseg - 1;  // largest s with pre[s] <= j
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (pre[mid] <= j) lo = mid;
-            else hi = mid - 1;
-        }
-        return (uint32_t)lo * cap + (j - pre[lo]);
-    }
-};
-
-// Builds the prefix (all threads of the block must call it) and returns the
-// total; block 0 records the total for the host's ray statistics.
-__device__ __forceinline__ uint32_t seg_prefix(const uint32_t* __restrict__ seg, int nseg, lds_uint* pre,
-                                               uint32_t* __restrict__ total_out) {
-    __shared__ uint32_t wsum[kWavesPerBlock];
-    const int per = (nseg + kBlock - 1) / kBlock;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int first = t * per;
-    uint32_t local = 0;
-    for (int k = 0; k < per; ++k)
-        if (first + k < nseg) local += seg[first + k];
-    // inclusive wave scan of the per-thread sums
-    uint32_t incl = local;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
-        if (lane >= off) incl += v;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    uint32_t wbase = 0, total = 0;
-    for (int k = 0; k < kWavesPerBlock; ++k) {
-        if (k < w) wbase += wsum[k];
-        total += wsum[k];
-    }
-    uint32_t run = wbase + incl - local;
-    for (int k = 0; k < per; ++k)
-        if (first + k < nseg) {
-            pre[first + k] = run;
-            run += seg[first + k];
-        }
-    if (t == 0) pre[nseg] = total;
-    if (blockIdx.x == 0 && t == 0 && total_out) *total_out = total;
-    __syncthreads();
-    return total;
-}
 
 // Traversal-count reduction (RR_FLAG_COUNT_TRAVERSAL only).
 __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc, int slot, uint32_t nv,
@@ -479,14 +383,6 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
     }
 }
 
-// Adds the number of active lanes whose predicate holds (one atomic per wave).
-RR_D void count_wave(uint32_t* __restrict__ ctr, bool pred) {
-    const uint64_t m = __ballot(pred);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(ctr, (uint32_t)__popcll(m));
-}
-
-// K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
-// Scene data as kernel arguments (global pointers + counts).
 }  // namespace
 struct SceneArgs {
     const BvhNode* nodes;
@@ -743,282 +639,6 @@ RR_D void tile_mask(const FrameConsts& fc, const LdsView& v, int n_tris, float x
          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
     m1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32)) << 32) |
          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
-}
-
-// K-primary: raygen + closest hit + shade of bounce 0 for every camera path.
-// Outputs: segment seg_cap per block of the path queue (bounce 1) and the
-// shadow queue (bounce 0), lengths published in seg_c / seg_s.
-template <bool kCount, typename View>
-RR_D void primary_body(const FrameConsts& fc, const View& v, int np, Rad rad, PathQueue out,
-                       ShadowQueue sq, uint32_t seg_cap, uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
-                       int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
-                       uint32_t* __restrict__ traced) {
-    const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill, stride, 0};
-    TravCount cnt;
-    SegCursor cur;
-    const uint32_t seg_base = wave_id() * seg_cap;
-    const ScreenCull cull = screen_cull(fc, v.nodes);
-    const uint64_t cm0 = fc.n_tris >= 64 ? ~0ull : (1ull << fc.n_tris) - 1ull;
-    const uint64_t cm1 = fc.n_tris <= 64 ? 0ull : fc.n_tris >= 128 ? ~0ull : (1ull << (fc.n_tris - 64)) - 1ull;
-    for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {  // block-uniform trip count
-        const int p = b0 + (int)threadIdx.x;
-        ShadeOut so;
-        so.cont = so.shadow = false;
-        bool culled = true;
-        if (p < np) {
-            const int sl = (int)fc.div_npix.div((uint32_t)p);
-            const int pix = p - sl * fc.npix;
-            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            float3 o, d;
-            float tmin, tmax;
-            camera_ray(fc, v.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
-            Hit h;
-            if constexpr (std::is_same<View, LdsView>::value) {  // LDS scenes: every triangle (camera_hit)
-                set_miss(h, tmax);
-                if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cnt);  // wave-uniform masks
-            } else
-                traverse<false, kCount>(v.nodes, v.tris, culled ? 0 : fc.n_tris, o, d, tmin, tmax, st, h, cnt);
-            float3 L = mk3(0.0f, 0.0f, 0.0f);
-            shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), 0u, h, key, L, so);
-            rad.put(p, L);
-        }
-        count_wave(traced, !culled && fc.n_tris > 0);
-        emit(so, p, out, sq, seg_base, cur);
-    }
-    publish(cur, seg_c, seg_s);
-    if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
-}
-
-#ifndef RR_FUSED_WAVES
-#define RR_FUSED_WAVES 1
-#endif
-template <bool kCount, bool kLds>
-__global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_primary(FrameConsts fc, SceneArgs sa, int np, Rad rad,
-                                                    PathQueue out, ShadowQueue sq, uint32_t seg_cap,
-                                                    uint32_t* __restrict__ seg_c, uint32_t* __restrict__ seg_s,
-                                                    int32_t* __restrict__ spill,
-                                                    unsigned long long* __restrict__ tc, uint32_t* __restrict__ traced) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
-    lds_int* stack = lds_slot(lds_stack);
-    if constexpr (kLds) {
-        extern __shared__ float4 dyn4[];
-        int used;
-        const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
-        primary_body<kCount>(fc, v, np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack, traced);
-    } else {
-        primary_body<kCount>(fc, global_view(sa), np, rad, out, sq, seg_cap, seg_c, seg_s, spill, tc, stack, traced);
-    }
-}
-
-// K-extend: closest hit + shade of bounce b >= 1 over the path queue of the
-// previous bounce (segments in_seg[0..in_nseg) of capacity in_cap).
-struct SegIn {
-    const uint32_t* seg;
-    int nseg;
-    uint32_t cap;
-    uint32_t* total;  // block 0 records the queue length here (ray statistics)
-};
-struct SegOut {
-    uint32_t cap;
-    uint32_t* seg_c;
-    uint32_t* seg_s;
-};
-
-template <bool kCount, typename View>
-RR_D void extend_body(const FrameConsts& fc, int bounce, const View& v, PathQueue in, const SegIndex& ix, int count,
-                      Rad rad, PathQueue out, ShadowQueue sq, const SegOut& so_seg,
-                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack) {
-    const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill, stride, 0};
-    TravCount cnt;
-    SegCursor cur;
-    const uint32_t seg_base = wave_id() * so_seg.cap;
-    int pid = 0;
-    for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
-        const int j = b0 + (int)threadIdx.x;
-        ShadeOut so;
-        so.cont = so.shadow = false;
-        if (j < count) {
-            const uint32_t i = ix.slot((uint32_t)j);
-            const float4 a = in.o[i], b = in.d[i], c = in.t[i];
-            pid = f2i(a.w);
-            const float3 o = xyz(a), d = xyz(b);
-            Hit h;
-            if (c.w != 0.0f) set_miss(h, kFltMax);  // left a hull side (hull_flags)
-            else traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
-            const int sl = (int)fc.div_npix.div((uint32_t)pid);
-            const int pix = pid - sl * fc.npix;
-            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            float3 L = rad.get(pid);
-            shade(fc, bounce, v, o, d, xyz(c), (uint32_t)f2i(b.w), h, key, L, so);
-            rad.put(pid, L);
-        }
-        emit(so, pid, out, sq, seg_base, cur);
-    }
-    publish(cur, so_seg.seg_c, so_seg.seg_s);
-    if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
-}
-
-template <bool kCount, bool kLds>
-__global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in, SegIn si,
-                                                   Rad rad, PathQueue out, ShadowQueue sq,
-                                                   SegOut sg, int32_t* __restrict__ spill,
-                                                   unsigned long long* __restrict__ tc) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
-    extern __shared__ float4 dyn4[];
-    lds_int* stack = lds_slot(lds_stack);
-    int used = 0;
-    LdsView lv;
-    if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, true, used);
-    const SegIndex ix{(lds_uint*)((lds_f4w*)dyn4 + used), si.nseg, si.cap};
-    const int count = (int)seg_prefix(si.seg, si.nseg, ix.pre, si.total);
-    if constexpr (kLds)
-        extend_body<kCount>(fc, bounce, lv, in, ix, count, rad, out, sq, sg, spill, tc, stack);
-    else
-        extend_body<kCount>(fc, bounce, global_view(sa), in, ix, count, rad, out, sq, sg, spill, tc, stack);
-}
-
-// K-tail (fused path): bounces b_first..max_bounces of every path still alive,
-// each path run to completion by one thread — closest hit, shade, its shadow
-// ray, continue — instead of two launches per bounce. After Russian roulette
-// starts the late bounces carry few paths, and per bounce a launch pair cost
-// ~35 us of fixed work (segment prefix, launch gap) for ~1 us of rays. The
-// radiance additions of a path keep their order (emission(b), NEE(b),
-// emission(b+1), ...), so results are bit-identical to the per-bounce kernels.
-#ifndef RR_TAIL_BOUNCE
-#define RR_TAIL_BOUNCE 2
-#endif
-constexpr int kTailBounce = RR_TAIL_BOUNCE;
-
-
-template <bool kCount, typename View>
-RR_D void tail_body(const FrameConsts& fc, int b_first, const View& v, PathQueue in, const SegIndex& ix, int count,
-                    Rad rad, uint32_t* __restrict__ tot, int32_t* __restrict__ spill,
-                    unsigned long long* __restrict__ tc, lds_int* stack) {
-    const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill, stride, 0};
-    TravCount cc, cs;
-    for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
-        const int j = b0 + (int)threadIdx.x;
-        bool live = j < count;
-        float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = o, L = o;
-        uint32_t key = 0, lob = 0;
-        int pid = 0;
-        bool esc = false;
-        if (live) {
-            const uint32_t i = ix.slot((uint32_t)j);
-            const float4 a = in.o[i], b = in.d[i], c = in.t[i];
-            pid = f2i(a.w);
-            o = xyz(a);
-            d = xyz(b);
-            T = xyz(c);
-            esc = c.w != 0.0f;
-            lob = (uint32_t)f2i(b.w);
-            const int sl = (int)fc.div_npix.div((uint32_t)pid);
-            const int pix = pid - sl * fc.npix;
-            key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            L = rad.get(pid);
-        }
-        for (int b = b_first; b <= fc.max_bounces; ++b) {
-            if (!__any(live)) break;
-            ShadeOut so;
-            so.cont = so.shadow = false;
-            if (live) {
-                Hit h;
-                if (esc) set_miss(h, kFltMax);
-                else traverse<false, kCount>(v.nodes, v.tris, fc.n_tris, o, d, 0.0f, kFltMax, st, h, cc);
-                shade(fc, b, v, o, d, T, lob, h, key, L, so);
-                if (so.shadow) {
-                    Hit hs;
-                    if (so.esc || !traverse<true, kCount>(v.nodes, v.tris, fc.n_tris, so.so, so.sd, 0.0f, so.sdist, st, hs, cs)) {
-                        L.x = L.x + so.sc.x;
-                        L.y = L.y + so.sc.y;
-                        L.z = L.z + so.sc.z;
-                    }
-                }
-                if (so.cont) {
-                    o = so.o;
-                    d = so.d;
-                    T = so.T;
-                    lob = so.lob;
-                    esc = so.esc;
-                } else {
-                    live = false;
-                }
-            }
-            count_wave(tot + 2 * b, so.cont);        // paths entering b + 1
-            count_wave(tot + 2 * b + 1, so.shadow);  // shadow rays of bounce b
-        }
-        if (j < count) rad.put(pid, L);
-    }
-    if (kCount) {
-        flush_counts(tc, 2, cc.nodes, cc.tris);
-        flush_counts(tc, 4, cs.nodes, cs.tris);
-    }
-}
-
-template <bool kCount, bool kLds>
-__global__ __launch_bounds__(kBlock, RR_FUSED_WAVES) void k_tail(FrameConsts fc, int b_first, SceneArgs sa,
-                                                                 PathQueue in, SegIn si, Rad rad,
-                                                                 uint32_t* __restrict__ tot,
-                                                                 int32_t* __restrict__ spill,
-                                                                 unsigned long long* __restrict__ tc) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
-    extern __shared__ float4 dyn4[];
-    lds_int* stack = lds_slot(lds_stack);
-    int used = 0;
-    LdsView lv;
-    if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, true, used);
-    const SegIndex ix{(lds_uint*)((lds_f4w*)dyn4 + used), si.nseg, si.cap};
-    const int count = (int)seg_prefix(si.seg, si.nseg, ix.pre, si.total);
-    if constexpr (kLds)
-        tail_body<kCount>(fc, b_first, lv, in, ix, count, rad, tot, spill, tc, stack);
-    else
-        tail_body<kCount>(fc, b_first, global_view(sa), in, ix, count, rad, tot, spill, tc, stack);
-}
-
-// K10: shadow rays of one bounce; unoccluded -> radiance += contribution.
-template <bool kCount, typename NodeP, typename TriP>
-RR_D void shadow_body(NodeP nodes, TriP tris, int n_tris, ShadowQueue sq, const SegIndex& ix, int count,
-                      Rad rad, int32_t* __restrict__ spill, unsigned long long* __restrict__ tc,
-                      lds_int* stack) {
-    const int gtid = blockIdx.x * kBlock + threadIdx.x;
-    const int stride = gridDim.x * kBlock;
-    TravStack st{stack, spill, stride, 0};
-    TravCount cnt;
-    for (int j = gtid; j < count; j += stride) {
-        const uint32_t i = ix.slot((uint32_t)j);
-        const float4 a = sq.o[i], b = sq.d[i], c = sq.c[i];
-        Hit h;
-        // c.w: the ray leaves a hull side of its triangle (hull_flags)
-        if (c.w != 0.0f || !traverse<true, kCount>(nodes, tris, n_tris, xyz(a), xyz(b), 0.0f, b.w, st, h, cnt)) {
-            const int pid = f2i(a.w);
-            float3 L = rad.get(pid);
-            L.x = L.x + c.x;
-            L.y = L.y + c.y;
-            L.z = L.z + c.z;
-            rad.put(pid, L);
-        }
-    }
-    if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
-}
-
-template <bool kCount, bool kLds>
-__global__ __launch_bounds__(kBlock) void k_shadow(SceneArgs sa, ShadowQueue sq, SegIn si, Rad rad,
-                                                   int32_t* __restrict__ spill, unsigned long long* __restrict__ tc) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
-    extern __shared__ float4 dyn4[];
-    lds_int* stack = lds_slot(lds_stack);
-    int used = 0;
-    LdsView lv;
-    if constexpr (kLds) lv = stage_scene((lds_f4w*)dyn4, sa, false, used);
-    const SegIndex ix{(lds_uint*)((lds_f4w*)dyn4 + used), si.nseg, si.cap};
-    const int count = (int)seg_prefix(si.seg, si.nseg, ix.pre, si.total);
-    if constexpr (kLds)
-        shadow_body<kCount>(lv.nodes, lv.tris, sa.n_tris, sq, ix, count, rad, spill, tc, stack);
-    else
-        shadow_body<kCount>(sa.nodes, sa.tris, sa.n_tris, sq, ix, count, rad, spill, tc, stack);
 }
 
 // ------------------------------------------------------------------------
@@ -1531,6 +1151,29 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
             part[pix] = P;
         }
         film[pix] = acc;
+    }
+}
+
+// Scenes without triangles: every camera sample misses, its radiance is the
+// world term (T = 1 at bounce 0, no clamp); the film is that term summed in
+// the grouped order (in order within groups of kFilmGroup, the group sums in
+// order), then tonemapped: what the oracle's radiance() gives for an empty
+// hierarchy.
+__global__ __launch_bounds__(kBlock) void k_world(FrameConsts fc, float4* __restrict__ film,
+                                                  const float* __restrict__ srgb, uchar4* __restrict__ out) {
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int g0 = 0; g0 < fc.spp_total; g0 += kFilmGroup) {
+        float3 P = mk3(0.0f, 0.0f, 0.0f);
+        const int g1 = min(fc.spp_total, g0 + kFilmGroup);
+        for (int s = g0; s < g1; ++s) add_to(P, fc.world);
+        acc.x = acc.x + P.x;
+        acc.y = acc.y + P.y;
+        acc.z = acc.z + P.z;
+    }
+    const uchar4 px = tonemap(fc, acc, srgb);
+    for (int pix = blockIdx.x * kBlock + threadIdx.x; pix < fc.npix; pix += gridDim.x * kBlock) {
+        film[pix] = acc;
+        out[pix] = px;
     }
 }
 
@@ -2114,15 +1757,8 @@ int device_cu_count() {
 int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2) + 2; }
 
 namespace {
-using PrimaryFn = void (*)(FrameConsts, SceneArgs, int, Rad, PathQueue, ShadowQueue, uint32_t, uint32_t*,
-                           uint32_t*, int32_t*, unsigned long long*, uint32_t*);
-using ExtendFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, PathQueue, ShadowQueue, SegOut,
-                          int32_t*, unsigned long long*);
-using ShadowFn = void (*)(SceneArgs, ShadowQueue, SegIn, Rad, int32_t*, unsigned long long*);
-using TailFn = void (*)(FrameConsts, int, SceneArgs, PathQueue, SegIn, Rad, uint32_t*, int32_t*,
-                        unsigned long long*);
 // LDS-resident scenes render through k_tiles (RR_FLAG_WAVEFRONT: through the
-// wavefront kernels, the parity tests' second path).
+// split trace / shade kernels of large scenes, the parity tests' second path).
 // k_tiles slices a box tile into its sample groups: one unit per group, the
 // group sums handed to the slice finishing last through a slab of one plane
 // (3 x 64 floats) per group.
@@ -2188,41 +1824,16 @@ bool frame_uses_tiles(const FrameConsts& base, bool force_wavefront) {
 }
 
 namespace {
-// Launch geometry of one frame's path kernels.
-struct Grids {
-    bool lds;
-    int primary, extend, shadow, tail;
-    size_t dyn_primary, dyn_extend, dyn_shadow;
-    PrimaryFn kp;
-    ExtendFn ke;
-    ShadowFn ks;
-    TailFn kt;
+// Launch geometry of k_tiles: the scene and the camera data staged in dynamic
+// LDS (stage_scene, stage_camera), the resident grid for it.
+struct TileGrid {
     TilesFn kx;
-    int tiles;
-    Grids(const FrameConsts& fc, bool count, bool whole) {
-        lds = scene_in_lds(fc.n_tris, fc.n_mats, fc.n_lights);
-        kp = lds ? (count ? k_primary<true, true> : k_primary<false, true>)
-                 : (count ? k_primary<true, false> : k_primary<false, false>);
-        ke = lds ? (count ? k_extend<true, true> : k_extend<false, true>)
-                 : (count ? k_extend<true, false> : k_extend<false, false>);
-        ks = lds ? (count ? k_shadow<true, true> : k_shadow<false, true>)
-                 : (count ? k_shadow<true, false> : k_shadow<false, false>);
-        kt = lds ? (count ? k_tail<true, true> : k_tail<false, true>)
-                 : (count ? k_tail<true, false> : k_tail<false, false>);
-        const size_t sp = lds ? scene_lds_bytes(fc, true) : 0, ss = lds ? scene_lds_bytes(fc, false) : 0;
-        dyn_primary = sp + (lds ? 16 * kCamF4 * (size_t)fc.n_tris : 0);  // + stage_camera's float4s per triangle
-        primary = grid_for(kp, dyn_primary);
-        // consumers hold the producer's segment prefix after the scene: one word
-        // per producer block + 1; more LDS can only shrink k_extend's grid, so
-        // the bound taken without the prefix covers the grid taken with it.
-        const size_t pre = sizeof(uint32_t) * (size_t)(kWavesPerBlock * std::max(primary, grid_for(ke, sp)) + 1);
-        dyn_extend = sp + pre;
-        dyn_shadow = ss + pre;
-        extend = grid_for(ke, dyn_extend);
-        shadow = grid_for(ks, dyn_shadow);
-        tail = grid_for(kt, dyn_extend);
+    size_t dyn;
+    int grid;
+    TileGrid(const FrameConsts& fc, bool count, bool whole) {
+        dyn = scene_lds_bytes(fc, true) + 16 * kCamF4 * (size_t)fc.n_tris;
         kx = tiles_kernel(count, whole);
-        tiles = lds ? grid_for(kx, dyn_primary) : 0;
+        grid = grid_for(kx, dyn);
     }
 };
 // Launch geometry of the split (trace / shade) path of large scenes.
@@ -2260,18 +1871,11 @@ inline int clamp_grid(long work, int resident) {
     const long g = (work + kBlock - 1) / kBlock;
     return (int)std::max<long>(1, std::min<long>(g, resident));
 }
-// Segment capacity of a producer launched with `grid` blocks over at most
-// `work` items: the most any one wave can emit.
-inline uint32_t seg_cap(long work, int grid) {
-    const long stride = (long)grid * kBlock;
-    return (uint32_t)(((work + stride - 1) / stride) * 64);
-}
 }  // namespace
 
 void DevPaths::ensure_paths(size_t n) {
     if (grid_blocks == 0) grid_blocks = device_cu_count() * kMaxBlocksPerCu;
-    n += (size_t)grid_blocks * kBlock + n / 64;  // segment / group round-up slack (seg_cap, group_cap)
-    segs.ensure((size_t)4 * grid_blocks * kWavesPerBlock);
+    n += (size_t)grid_blocks * kBlock + n / 64;  // group round-up slack (group_cap)
     if (n > cap) {
         for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                                   &sh_c})
@@ -2291,7 +1895,7 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
-    counters.release(); tile_ctrs.release(); tile_cost.release(); tile_order.release(); spill.release(); tile_slab.release(); film_part.release(); segs.release(); hits.release(); qctr.release();
+    counters.release(); tile_ctrs.release(); tile_cost.release(); tile_order.release(); spill.release(); tile_slab.release(); film_part.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     mat_lut.release();
     mat_lut_cached.clear();
@@ -2371,9 +1975,9 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
 void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_t st) {
     const int npix = base.npix;
     const size_t npaths = (size_t)npix * base.spp_chunk;
-    const Grids G(base, p.count_traversal, p.tile_whole);
     p.last_tile_slices = 0;
     if (frame_uses_tiles(base, p.force_wavefront)) {  // one launch: all samples of every tile
+        const TileGrid G(base, p.count_traversal, p.tile_whole);
         p.ensure_tiles();
         p.film.ensure((size_t)npix);
         p.rgba8.ensure((size_t)npix * 4);
@@ -2410,12 +2014,12 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
             p.tile_slab.ensure(sl.floats * (size_t)tiles);
             sl.slab = p.tile_slab.ptr;
         }
-        const int g = clamp_grid(tiles * 64, G.tiles);
+        const int g = clamp_grid(tiles * 64, G.grid);
         p.prof.begin(st, RR_K_TILES);
         p.tile_ctrs.ensure((size_t)kTileShards * kTileCtrStride);
         k_tile_order<<<1, kOrderThreads, 0, st>>>(fc, s.nodes.ptr, p.tile_cost.ptr, p.tile_order.ptr, p.tile_ctrs.ptr,
                                                   reinterpret_cast<uint32_t*>(p.counters.ptr), (int)n_ctr);
-        G.kx<<<g, kBlock, G.dyn_primary, st>>>(fc, sa, p.tile_ctrs.ptr, p.film.ptr, p.srgb_lut.ptr,
+        G.kx<<<g, kBlock, G.dyn, st>>>(fc, sa, p.tile_ctrs.ptr, p.film.ptr, p.srgb_lut.ptr,
                                                reinterpret_cast<uchar4*>(p.rgba8.ptr), tot, p.spill.ptr, tc, sl);
         if (sl.n > 1)
             k_tiles_fold<<<(int)std::min<long>((tiles + kWavesPerBlock - 1) / kWavesPerBlock, 2048), kBlock, 0, st>>>(
@@ -2424,13 +2028,21 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         RR_HIP(hipGetLastError());
         return;
     }
-    p.ensure_paths(npaths);
     p.film.ensure((size_t)npix);
-    if (n_chunks > 1) p.film_part.ensure((size_t)npix);
     p.rgba8.ensure((size_t)npix * 4);
     const int cpc = counters_per_chunk(base.max_bounces);
     p.counters.ensure((size_t)cpc * n_chunks);
     RR_HIP(hipMemsetAsync(p.counters.ptr, 0, sizeof(int32_t) * cpc * n_chunks, st));
+    if (base.n_tris <= 0) {  // nothing to hit: every sample is the world term
+        p.prof.begin(st, RR_K_ACCUM);
+        k_world<<<clamp_grid(npix, accum_grid()), kBlock, 0, st>>>(base, p.film.ptr, p.srgb_lut.ptr,
+                                                                   reinterpret_cast<uchar4*>(p.rgba8.ptr));
+        p.prof.end(st);
+        RR_HIP(hipGetLastError());
+        return;
+    }
+    p.ensure_paths(npaths);
+    if (n_chunks > 1) p.film_part.ensure((size_t)npix);
     unsigned long long* tc = nullptr;
     if (p.count_traversal) {
         p.trav_counts.ensure(kTravWords);
@@ -2439,63 +2051,9 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     }
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
-    KernelProfiler& pr = p.prof;
     const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
                        p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
-    if (!G.lds && base.n_tris > 0) {
-        render_split(p, base, n_chunks, st, sa, tc, pq, sq);
-        RR_HIP(hipGetLastError());
-        return;
-    }
-    for (int c = 0; c < n_chunks; ++c) {
-        FrameConsts fc = base;
-        fc.first_sample = c * base.spp_chunk;
-        fc.spp_chunk = base.spp_chunk;
-        if (fc.first_sample + fc.spp_chunk > base.spp_total) fc.spp_chunk = base.spp_total - fc.first_sample;
-        const int np = npix * fc.spp_chunk;
-        // segment lengths, ping-pong by bounce parity: [parity][path | shadow][grid]
-        auto seg = [&](int b, int q) {
-            return p.segs.ptr + ((size_t)(b & 1) * 2 + q) * p.grid_blocks * kWavesPerBlock;
-        };
-        uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr + (size_t)cpc * c);
-        const int gp = clamp_grid(np, G.primary), ge = clamp_grid(np, G.extend), gs = clamp_grid(np, G.shadow);
-        const uint32_t cap_p = seg_cap(np, gp), cap_e = seg_cap(np, ge);
-        pr.begin(st, RR_K_PRIMARY);
-        G.kp<<<gp, kBlock, G.dyn_primary, st>>>(fc, sa, np, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq, cap_p, seg(0, 0), seg(0, 1),
-                                                p.spill.ptr, tc, tot + camera_traced_slot(base.max_bounces));
-        pr.end(st);
-        int g_prev = gp;  // grid of the producer of the current queues
-        uint32_t cap_prev = cap_p;
-        for (int b = 0; b <= base.max_bounces; ++b) {
-            if (b >= kTailBounce) {  // the remaining bounces in one launch
-                pr.begin(st, RR_K_EXTEND);
-                G.kt<<<clamp_grid(np, G.tail), kBlock, G.dyn_extend, st>>>(
-                    fc, b, sa, pq[b & 1], SegIn{seg(b - 1, 0), g_prev * kWavesPerBlock, cap_prev, tot + 2 * (b - 1)},
-                    Rad{reinterpret_cast<float*>(p.rad.ptr)}, tot, p.spill.ptr, tc);
-                pr.end(st);
-                break;
-            }
-            if (b > 0) {
-                pr.begin(st, RR_K_EXTEND);
-                G.ke<<<ge, kBlock, G.dyn_extend, st>>>(fc, b, sa, pq[b & 1],
-                                                       SegIn{seg(b - 1, 0), g_prev * kWavesPerBlock, cap_prev, tot + 2 * (b - 1)},
-                                                       Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[(b + 1) & 1], sq,
-                                                       SegOut{cap_e, seg(b, 0), seg(b, 1)}, p.spill.ptr, tc);
-                pr.end(st);
-                g_prev = ge;
-                cap_prev = cap_e;
-            }
-            pr.begin(st, RR_K_SHADOW);
-            G.ks<<<gs, kBlock, G.dyn_shadow, st>>>(sa, sq, SegIn{seg(b, 1), g_prev * kWavesPerBlock, cap_prev, tot + 2 * b + 1},
-                                                   Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.spill.ptr, tc);
-            pr.end(st);
-        }
-        const int ga = clamp_grid(npix, accum_grid());
-        pr.begin(st, RR_K_ACCUM);
-        k_accumulate<<<ga, kBlock, 0, st>>>(fc, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.film.ptr, p.film_part.ptr, c == 0 ? 1 : 0, c == n_chunks - 1 ? 1 : 0,
-                                            p.srgb_lut.ptr, reinterpret_cast<uchar4*>(p.rgba8.ptr));
-        pr.end(st);
-    }
+    render_split(p, base, n_chunks, st, sa, tc, pq, sq);
     RR_HIP(hipGetLastError());
 }
 

@@ -78,7 +78,8 @@ typedef struct rr_render_params {
 /* Measurement flags (rr_render_params.flags). */
 #define RR_FLAG_PROFILE_KERNELS 1  /* HIP events around every launch -> stats.kernel_ms[] */
 #define RR_FLAG_COUNT_TRAVERSAL 2  /* count BVH nodes visited / triangles tested -> stats */
-#define RR_FLAG_WAVEFRONT 4        /* LDS-resident scenes: wavefront kernels instead of k_tiles (A/B, parity) */
+#define RR_FLAG_WAVEFRONT 4        /* LDS-resident scenes: the split trace/shade kernels of large scenes
+                                    * (quantised BVH4 from HBM) instead of k_tiles (parity: both paths) */
 
 /* Kernel classes of rr_frame_stats.kernel_ms / kernel_launches. */
 #define RR_K_BUILD 0     /* world transform + Morton + radix sort + Karras + refit */

@@ -133,8 +133,10 @@ def test_trace_edge_cases(ctx, s04):
     assert len(p0) == 0
 
 
-# "tiles": k_tiles (default for LDS-resident scenes); "wavefront": the queue
-# kernels (RR_FLAG_WAVEFRONT), the path large scenes take.
+# "tiles": k_tiles (default for LDS-resident scenes); "wavefront": the split
+# trace / shade kernels over the quantised BVH4 (RR_FLAG_WAVEFRONT), the path
+# large scenes take (frame_state reports render_ints[7] == 4 for it, so the
+# oracle walks the same hierarchy without the hull rule).
 PATHS = {"tiles": 0, "wavefront": 4}
 
 
@@ -553,3 +555,27 @@ def test_timed_configuration_bands_bit_exact(rr, tmp_path, job_name, frames):
                 assert nbad == 0, f"frame {f} rows {r0}..{r0 + 3}: {nbad} mismatches"
     finally:
         runner.close()
+
+
+def test_empty_scene_is_the_world(ctx, rr, tmp_path):
+    """A scene without triangles (k_world): every sample is the world term, the
+    film its grouped sum, equal to the oracle's frame of an empty hierarchy."""
+    import json
+    with open(S04) as f:
+        sc = json.load(f)
+    m = sc["meshes"][0]
+    m["vertices"], m["triangles"], m["material_indices"], m["smooth"] = [], [], [], []
+    path = str(tmp_path / "empty.rrscene")
+    with open(path, "w") as f:
+        json.dump(sc, f)
+    s = ctx.load_scene(path)
+    try:
+        p = rr.default_params(width=40, height=24, spp=40)
+        film, rgba, st = ctx.render_to_memory(s, 3, p)
+        fs = ctx.frame_state(s, 3, p)
+        assert s.counts()["triangles"] == 0 and st.camera_rays_traced == 0 and st.extension_rays == 0
+        of, orgba = O.render_state(fs)
+        assert np.array_equal(film, of) and np.array_equal(rgba, orgba)
+        np.testing.assert_allclose(film[..., :3], np.broadcast_to(fs.world, (24, 40, 3)), rtol=1e-6)
+    finally:
+        s.close()
