@@ -355,20 +355,32 @@ __global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restr
 // The BVH2 (PLOC; Karras below 3 triangles) becomes the quantised BVH4 of the
 // split path (rr_device.h QNode4), top down, one level per launch pair:
 //  - children of the BVH4 node rooted at BVH2 node r: start from r's two
-//    children; while there are fewer than four, the internal entry with the
-//    largest box measure (dx*dy + dy*dz + dz*dx, ties: lowest slot) is opened
-//    (replaced by its left child, its right child appended);
+//    children; a child subtree of at most kLeafTris triangles is a leaf entry
+//    and never opened; while there are fewer than four entries, the internal
+//    entry with the largest box measure (dx*dy + dy*dz + dz*dx, ties: lowest
+//    slot) is opened (replaced by its left child, its right child appended);
 //  - nodes are numbered breadth first and the internal children of a node
 //    take consecutive indices in slot order (level frontier [lo, hi): node k
 //    counts its internal children, an exclusive scan gives each node its
 //    children's first index hi + prefix), so siblings share 128 B lines;
+//  - the triangles of a node's leaf entries take consecutive positions of the
+//    BVH4's own triangle array (tris4, swapped into DevScene::tris after the
+//    collapse) in slot order, and within an entry in the left-first order of
+//    its subtree, after the triangles of the levels before and of the nodes
+//    before it in its level (a second count and scan), so one leaf is one
+//    contiguous range ~(first | (count - 1) << 28): on C5 the single-triangle
+//    leaves had left ~40 % of the BVH4 nodes with two leaf children;
 //  - child boxes are quantised on the node's grid: origin = the lo corner of
 //    the children's union, per axis the smallest exponent that spans it in
 //    255 steps, lo rounded down and hi up (exactly, in double).
-// oracle/rr_oracle.c lbvh_collapse4 / q4_pack restate it.
+// oracle/rr_oracle.c lbvh_collapse4 / q4_pack restate it (ORC_LEAF_TRIS).
+#ifndef RR_LEAF_TRIS
+#define RR_LEAF_TRIS 1  // must equal oracle/rr_oracle.c ORC_LEAF_TRIS (A/B builds may change it)
+#endif
+constexpr int kLeafTris = RR_LEAF_TRIS;
 struct C4Set {
     int m;
-    int ref[4];
+    int ref[4], cnt[4];
     float lo[3][4], hi[3][4];
 };
 
@@ -376,6 +388,9 @@ __device__ __forceinline__ float c4_measure(const C4Set& S, int c) {
     const float dx = S.hi[0][c] - S.lo[0][c], dy = S.hi[1][c] - S.lo[1][c], dz = S.hi[2][c] - S.lo[2][c];
     return dx * dy + dy * dz + dz * dx;
 }
+
+// an entry that stays a leaf: one triangle, or a subtree of <= kLeafTris
+__device__ __forceinline__ bool c4_leaf(const C4Set& S, int c) { return S.ref[c] < 0 || S.cnt[c] <= kLeafTris; }
 
 __device__ void c4_set(const BvhNode* __restrict__ nodes, int n, int r, C4Set& S) {
     auto put = [&](int slot, const BvhNode& nd, int side) {
@@ -385,6 +400,7 @@ __device__ void c4_set(const BvhNode* __restrict__ nodes, int n, int r, C4Set& S
             S.hi[a][slot] = f[3 + a];
         }
         S.ref[slot] = n > 1 ? (side ? nd.d.y : nd.d.x) : ~0;  // one triangle: both slots are leaf 0
+        S.cnt[slot] = n > 1 ? (side ? nd.d.w : nd.d.z) : 1;
     };
     const BvhNode nd = nodes[r];
     put(0, nd, 0);
@@ -394,7 +410,7 @@ __device__ void c4_set(const BvhNode* __restrict__ nodes, int n, int r, C4Set& S
         int best = -1;
         float ba = 0.0f;
         for (int c = 0; c < S.m; ++c) {
-            if (S.ref[c] < 0) continue;
+            if (c4_leaf(S, c)) continue;
             const float a = c4_measure(S, c);
             if (best < 0 || a > ba) {
                 best = c;
@@ -409,35 +425,47 @@ __device__ void c4_set(const BvhNode* __restrict__ nodes, int n, int r, C4Set& S
     }
 }
 
-// Level start: frontier [0, 1) = the BVH2 root.
+// Level start: frontier [0, 1) = the BVH2 root, triangle positions from 0.
 __global__ void k_c4_init(int32_t* __restrict__ ctl, int32_t* __restrict__ src) {
     ctl[0] = 0;
     ctl[1] = 1;
+    ctl[2] = 0;
     src[0] = 0;
 }
 
-// cnt[k] = internal children of frontier node lo + k (0 past the frontier,
-// k <= bound: the scan's total lands in cnt[bound]).
+// cnt[k] = internal children, tcnt[k] = triangles of the leaf entries of
+// frontier node lo + k (0 past the frontier, k <= bound: the scans' totals
+// land in [bound]).
 __global__ __launch_bounds__(kBlock) void k_c4_count(const int32_t* __restrict__ ctl, int bound, int n,
                                                      const BvhNode* __restrict__ nodes,
-                                                     const int32_t* __restrict__ src, uint32_t* __restrict__ cnt) {
+                                                     const int32_t* __restrict__ src, uint32_t* __restrict__ cnt,
+                                                     uint32_t* __restrict__ tcnt) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     if (k > bound) return;
     const int lo = ctl[0], hi = ctl[1];
-    uint32_t c = 0;
+    uint32_t c = 0, t = 0;
     if (k < bound && lo + k < hi) {
         C4Set S;
         c4_set(nodes, n, src[lo + k], S);
-        for (int j = 0; j < S.m; ++j) c += S.ref[j] >= 0 ? 1u : 0u;
+        for (int j = 0; j < S.m; ++j) {
+            if (!c4_leaf(S, j)) ++c;
+            else if (n > 1) t += (uint32_t)(S.ref[j] < 0 ? 1 : S.cnt[j]);
+        }
+        if (n == 1) t = 1;  // one triangle: both slots name position 0
     }
     cnt[k] = c;
+    tcnt[k] = t;
 }
 
-// Node lo + k: children -> indices hi + cnt[k] .. (after the exclusive scan),
-// their BVH2 roots -> src, the quantised node -> out.
+// Node lo + k: internal children -> indices hi + cnt[k] .., their BVH2 roots
+// -> src; leaf entries -> triangle positions ctl[2] + tcnt[k] .. (after the
+// exclusive scans), their triangles copied there; the quantised node -> out.
 __global__ __launch_bounds__(kBlock) void k_c4_emit(const int32_t* __restrict__ ctl, int bound, int n,
                                                     const BvhNode* __restrict__ nodes, int32_t* __restrict__ src,
-                                                    const uint32_t* __restrict__ cnt, QNode4* __restrict__ out) {
+                                                    const uint32_t* __restrict__ cnt,
+                                                    const uint32_t* __restrict__ tcnt,
+                                                    const TriPack* __restrict__ tris, TriPack* __restrict__ tris4,
+                                                    QNode4* __restrict__ out) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= bound) return;
     const int lo = ctl[0], hi = ctl[1];
@@ -446,15 +474,34 @@ __global__ __launch_bounds__(kBlock) void k_c4_emit(const int32_t* __restrict__ 
     C4Set S;
     c4_set(nodes, n, src[idx], S);
     int next = hi + (int)cnt[k];
+    int tpos = ctl[2] + (int)tcnt[k];
     int ref[4];
     for (int c = 0; c < 4; ++c) {
         if (c >= S.m) {
             ref[c] = kEmpty4;
-        } else if (S.ref[c] >= 0) {
+        } else if (!c4_leaf(S, c)) {
             src[next] = S.ref[c];
             ref[c] = next++;
+        } else if (n == 1) {
+            tris4[0] = tris[0];
+            ref[c] = leaf_ref(0, 1);
         } else {
-            ref[c] = S.ref[c];
+            // the subtree's leaves, left first (depth < kLeafTris)
+            int stack[kLeafTris], sp = 0, r = S.ref[c], m = 0;
+            const int first = tpos;
+            for (;;) {
+                if (r < 0) {
+                    tris4[tpos++] = tris[~r];
+                    ++m;
+                    if (sp == 0) break;
+                    r = stack[--sp];
+                } else {
+                    const int4 d = nodes[r].d;
+                    stack[sp++] = d.y;
+                    r = d.x;
+                }
+            }
+            ref[c] = leaf_ref(first, m);
         }
     }
     float org[3];
@@ -484,11 +531,13 @@ __global__ __launch_bounds__(kBlock) void k_c4_emit(const int32_t* __restrict__ 
     out[idx] = o;
 }
 
-// Next level: [hi, hi + total).
-__global__ void k_c4_advance(int32_t* __restrict__ ctl, int bound, const uint32_t* __restrict__ cnt) {
+// Next level: [hi, hi + total), triangle positions after this level's.
+__global__ void k_c4_advance(int32_t* __restrict__ ctl, int bound, const uint32_t* __restrict__ cnt,
+                             const uint32_t* __restrict__ tcnt) {
     const int hi = ctl[1];
     ctl[0] = hi;
     ctl[1] = hi + (int)cnt[bound];
+    ctl[2] += (int)tcnt[bound];
 }
 
 // ------------------------------------------------------------------ PLOC ---
@@ -509,7 +558,9 @@ __global__ void k_c4_advance(int32_t* __restrict__ ctl, int bound, const uint32_
 #endif
 constexpr int kPlocR = RR_PLOC_R;
 
-// cluster k: cl[2k] = (lo.xyz, ref bits), cl[2k+1] = (hi.xyz, 0)
+// cluster k: cl[2k] = (lo.xyz, ref bits), cl[2k+1] = (hi.xyz, leaves under it);
+// a PLOC node's d.z / d.w hold the leaf counts of its two children (the BVH4
+// collapse keeps subtrees of <= kLeafTris triangles as leaves)
 __device__ __forceinline__ float ploc_area(float4 alo, float4 ahi, float4 blo, float4 bhi) {
     const float dx = fmaxf(ahi.x, bhi.x) - fminf(alo.x, blo.x);
     const float dy = fmaxf(ahi.y, bhi.y) - fminf(alo.y, blo.y);
@@ -534,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void k_ploc_init(int n, const uint32_t* __r
     cl[2 * i] = make_float4(fminf(fminf(a.x, b.x), c.x), fminf(fminf(a.y, b.y), c.y), fminf(fminf(a.z, b.z), c.z),
                             i2f(~i));
     cl[2 * i + 1] = make_float4(fmaxf(fmaxf(a.x, b.x), c.x), fmaxf(fmaxf(a.y, b.y), c.y),
-                                fmaxf(fmaxf(a.z, b.z), c.z), 0.0f);
+                                fmaxf(fmaxf(a.z, b.z), c.z), i2f(1));  // .w: leaves under the cluster
 }
 
 // Nearest neighbour within kPlocR positions (ascending scan, strict <).
@@ -605,10 +656,11 @@ __global__ __launch_bounds__(kBlock) void k_ploc_apply(const int* __restrict__ c
         nd.a = make_float4(alo.x, alo.y, alo.z, ahi.x);
         nd.b = make_float4(ahi.y, ahi.z, blo.x, blo.y);
         nd.c = make_float4(blo.z, bhi.x, bhi.y, bhi.z);
-        nd.d = make_int4(f2i(alo.w), f2i(blo.w), 0, 0);
+        nd.d = make_int4(f2i(alo.w), f2i(blo.w), f2i(ahi.w), f2i(bhi.w));  // child refs, child leaf counts
         nodes[idx] = nd;
         cl_out[2 * o] = make_float4(fminf(alo.x, blo.x), fminf(alo.y, blo.y), fminf(alo.z, blo.z), i2f(idx));
-        cl_out[2 * o + 1] = make_float4(fmaxf(ahi.x, bhi.x), fmaxf(ahi.y, bhi.y), fmaxf(ahi.z, bhi.z), 0.0f);
+        cl_out[2 * o + 1] = make_float4(fmaxf(ahi.x, bhi.x), fmaxf(ahi.y, bhi.y), fmaxf(ahi.z, bhi.z),
+                                        i2f(f2i(ahi.w) + f2i(bhi.w)));
     } else {
         cl_out[2 * o] = alo;
         cl_out[2 * o + 1] = ahi;
@@ -833,7 +885,7 @@ void DevScene::release() {
     tri_world.release(); bounds.release();
     for (int k = 0; k < 2; ++k) { keys[k].release(); vals[k].release(); }
     hist.release(); scan_part.release(); children.release(); node_parent.release();
-    leaf_parent.release(); flags.release(); nodes.release(); tris.release(); nodes4.release(); q4_src.release(); q4_cnt.release(); q4_ctl.release();
+    leaf_parent.release(); flags.release(); nodes.release(); tris.release(); nodes4.release(); tris4.release(); q4_src.release(); q4_cnt.release(); q4_tcnt.release(); q4_ctl.release();
     range.release();
     for (int k = 0; k < 2; ++k) ploc_cl[k].release();
     ploc_nn.release(); ploc_keep.release(); ploc_mrg.release(); ploc_ctl.release();
@@ -893,19 +945,23 @@ void build_bvh4(DevScene& s, hipStream_t st) {
     const int n = s.n_tris;
     const int ni = n > 1 ? n - 1 : 1;
     s.nodes4.ensure((size_t)ni);
+    s.tris4.ensure((size_t)n);
     s.q4_src.ensure((size_t)ni);
     s.q4_cnt.ensure((size_t)ni + 1);
-    s.q4_ctl.ensure(2);
+    s.q4_tcnt.ensure((size_t)ni + 1);
+    s.q4_ctl.ensure(3);
     k_c4_init<<<1, 1, 0, st>>>(s.q4_ctl.ptr, s.q4_src.ptr);
     long frontier = 1;  // bound on the current level's node count
     for (int level = 0;; ++level) {
         const int bound = (int)std::min<long>(frontier, ni);
         k_c4_count<<<cdiv(bound + 1, kBlock), kBlock, 0, st>>>(s.q4_ctl.ptr, bound, n, s.nodes.ptr, s.q4_src.ptr,
-                                                                s.q4_cnt.ptr);
+                                                                s.q4_cnt.ptr, s.q4_tcnt.ptr);
         exclusive_scan(s, s.q4_cnt.ptr, bound + 1, st);
+        exclusive_scan(s, s.q4_tcnt.ptr, bound + 1, st);
         k_c4_emit<<<cdiv(bound, kBlock), kBlock, 0, st>>>(s.q4_ctl.ptr, bound, n, s.nodes.ptr, s.q4_src.ptr,
-                                                           s.q4_cnt.ptr, s.nodes4.ptr);
-        k_c4_advance<<<1, 1, 0, st>>>(s.q4_ctl.ptr, bound, s.q4_cnt.ptr);
+                                                           s.q4_cnt.ptr, s.q4_tcnt.ptr, s.tris.ptr, s.tris4.ptr,
+                                                           s.nodes4.ptr);
+        k_c4_advance<<<1, 1, 0, st>>>(s.q4_ctl.ptr, bound, s.q4_cnt.ptr, s.q4_tcnt.ptr);
         frontier = std::min<long>(frontier * 4, ni);
         if ((level & 3) == 3) {
             int ctl[2];
@@ -919,6 +975,7 @@ void build_bvh4(DevScene& s, hipStream_t st) {
             if (level > 4 * 4096) throw std::runtime_error("BVH4 collapse made no progress");
         }
     }
+    std::swap(s.tris, s.tris4);  // the traversal and shading read the BVH4's leaf order
     s.has4 = true;
 }
 

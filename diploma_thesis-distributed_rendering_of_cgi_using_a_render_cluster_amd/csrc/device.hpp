@@ -69,11 +69,13 @@ struct DevScene {
     DevBuf<int2> range;           // n-1 : (first sorted leaf, leaf count) under each node
     // acceleration structure consumed by traversal
     DevBuf<BvhNode> nodes;  // max(n-1, 1)
-    DevBuf<TriPack> tris;   // n, leaf order
+    DevBuf<TriPack> tris;   // n, leaf order (after a BVH4 collapse: the BVH4's leaf order)
     DevBuf<QNode4> nodes4;     // quantised BVH4 collapse of `nodes` (split path), <= n-1
+    DevBuf<TriPack> tris4;     // collapse scratch: the triangles in the BVH4's leaf order (swapped into `tris`)
     DevBuf<int32_t> q4_src;    // BVH4 node -> its BVH2 root (collapse scratch)
     DevBuf<uint32_t> q4_cnt;   // per frontier node: internal children (scanned in place)
-    DevBuf<int32_t> q4_ctl;    // current level [lo, hi)
+    DevBuf<uint32_t> q4_tcnt;  // per frontier node: triangles of its leaf entries (scanned in place)
+    DevBuf<int32_t> q4_ctl;    // current level [lo, hi), first triangle of the level
     int n4 = 0;                // BVH4 nodes
     bool has4 = false;
     // PLOC build (large scenes): cluster ping-pong, neighbours, scan flags, counters

@@ -349,8 +349,9 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     if (hier == 0) hier = frame_hier(fs, d.n_tris);
     const bool want4 = hier == kHierBvh4;
     const bool want_ploc = (hier == kHierPloc || hier == kHierBvh4) && d.n_tris > 2;
-    const bool rebuild =
-        !d.built || d.cached_xform != fs.obj_xform || (want4 && !d.has4) || (want_ploc != d.ploc);
+    // (a BVH4 collapse reorders the triangles into its leaf order, so a BVH2
+    // walk of the same PLOC tree needs a build without it)
+    const bool rebuild = !d.built || d.cached_xform != fs.obj_xform || (want4 != d.has4) || (want_ploc != d.ploc);
     const bool upload_x = rebuild && d.n_tris > 0;
     if (upload_x) d.obj_xform.ensure(nx);
     const UploadSeg segs[3] = {{p.lights.ptr, (int)nl}, {p.materials.ptr, (int)nm},
@@ -1180,7 +1181,8 @@ int rr_debug_bvh_hier(rr_ctx* c, rr_scene* s, int32_t frame, int32_t hier, uint3
     });
 }
 
-int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* children4, uint32_t* nodes16) {
+int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* children4, uint32_t* nodes16,
+                  int32_t* tri_orig) {
     if (!c || !s || !n4) return fail(RR_EINVAL, "NULL ctx, scene or n4");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
@@ -1209,6 +1211,12 @@ int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* c
                     }
                     if (nodes16) std::memcpy(nodes16 + 16 * (size_t)i, &q, sizeof(QNode4));
                 }
+            }
+            if (tri_orig) {  // original id of each position of the BVH4's triangle array
+                std::vector<TriPack> tp((size_t)n);
+                RR_HIP(hipMemcpyAsync(tp.data(), d.tris.ptr, (size_t)n * sizeof(TriPack), hipMemcpyDeviceToHost, st));
+                RR_HIP(hipStreamSynchronize(st));
+                for (int i = 0; i < n; ++i) tri_orig[i] = f2i(tp[(size_t)i].p0.w);
             }
         }
         return RR_OK;

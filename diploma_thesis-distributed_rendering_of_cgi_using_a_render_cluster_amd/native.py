@@ -131,7 +131,7 @@ def lib() -> ctypes.CDLL:
                                          f32p, i32p, f32p]),
         "rr_debug_bvh": (c_int, [P, P, i32, u32p, u32p, i32p, f32p]),
         "rr_debug_trace": (c_int, [P, P, i32, i32, i32, f32p, f32p, i32p, u8p]),
-        "rr_debug_bvh4": (c_int, [P, P, i32, i32p, i32p, u32p]),
+        "rr_debug_bvh4": (c_int, [P, P, i32, i32p, i32p, u32p, i32p]),
         "rr_debug_bvh_hier": (c_int, [P, P, i32, i32, u32p, u32p, i32p, f32p]),
         "rr_debug_jpeg_device": (c_int, [P, u8p, i32, i32, i32, u8p, ctypes.c_uint64,
                                          ctypes.POINTER(ctypes.c_uint64)]),
@@ -348,15 +348,20 @@ class RenderContext:
                                   _ptr(boxes, ctypes.c_float)), self.handle)
         return keys, order, children, boxes
 
-    def bvh4(self, scene: Scene, frame: int):
+    def bvh4(self, scene: Scene, frame: int, with_order: bool = False):
         """rr_debug_bvh4: (children4 (n4,4), nodes (n4,16) uint32: the raw 64-byte
-        quantised nodes, rr_device.h QNode4)."""
+        quantised nodes, rr_device.h QNode4); with_order: also the original
+        triangle id at each position of the BVH4's triangle array."""
         n4 = ctypes.c_int32()
-        _check(lib().rr_debug_bvh4(self.handle, scene.handle, int(frame), ctypes.byref(n4), None, None), self.handle)
+        _check(lib().rr_debug_bvh4(self.handle, scene.handle, int(frame), ctypes.byref(n4), None, None, None),
+               self.handle)
         ch = np.zeros((max(n4.value, 1), 4), np.int32)
         bx = np.zeros((max(n4.value, 1), 16), np.uint32)
+        orig = np.zeros(max(scene.counts()["triangles"], 1), np.int32)
         _check(lib().rr_debug_bvh4(self.handle, scene.handle, int(frame), ctypes.byref(n4), _ptr(ch, ctypes.c_int32),
-                                   _ptr(bx, ctypes.c_uint32)), self.handle)
+                                   _ptr(bx, ctypes.c_uint32), _ptr(orig, ctypes.c_int32)), self.handle)
+        if with_order:
+            return ch[:n4.value], bx[:n4.value], orig[:scene.counts()["triangles"]]
         return ch[:n4.value], bx[:n4.value]
 
     def jpeg_device(self, rgba: np.ndarray, quality: int = 90) -> bytes:

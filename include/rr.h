@@ -291,16 +291,18 @@ int rr_debug_bvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, uint32_t* ke
 int rr_debug_bvh_hier(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t hier, uint32_t* keys,
                       uint32_t* order, int32_t* children, float* boxes);
 
-/* Quantised BVH4 of the frame (the PLOC hierarchy collapsed two levels at a
- * time, the hierarchy the split path of large scenes traverses; built on
+/* Quantised BVH4 of the frame (the PLOC hierarchy collapsed into 4-wide
+ * nodes, the hierarchy the split path of large scenes traverses; built on
  * demand here). *n4 receives the node count; if children4 / nodes16 are
- * non-NULL they receive 4*n4 child refs (>= 0 node, < 0 ~leaf, 0x7fffffff
+ * non-NULL they receive 4*n4 child refs (>= 0 node, < 0 leaf range
+ * ~(first | (count - 1) << 28) of the BVH4's triangle array, 0x7fffffff
  * empty) and the 16 32-bit words of each 64-byte node: origin x y z (float),
  * exponent bytes (e+128 per axis), 4 child refs, lo x/y/z and hi x/y/z grid
- * coordinates (one byte per child), 2 zero words. Call once with NULL arrays
- * to size them. */
+ * coordinates (one byte per child), 2 zero words; tri_orig (n triangles)
+ * the original triangle id at each position of that array. Call once with
+ * NULL arrays to size them. */
 int rr_debug_bvh4(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t* n4,
-                  int32_t* children4, uint32_t* nodes16);
+                  int32_t* children4, uint32_t* nodes16, int32_t* tri_orig);
 
 /* Trace a batch of rays against the frame's hierarchy. bvh_width: 2 (LBVH),
  * 4 (BVH4 collapse) or 0 (whichever the frame kernels use for this scene,

@@ -34,7 +34,7 @@ def lib():
         L.orc_build_bvh.argtypes = [c_int, f, c_int, u32, u32, i32, f]
         L.orc_trace.argtypes = [c_int, f, c_int, f, f, i32, u8]
         L.orc_trace_w.argtypes = [c_int, f, c_int, c_int, f, f, i32, u8]
-        L.orc_build_bvh4.argtypes = [c_int, f, i32, i32, u32]
+        L.orc_build_bvh4.argtypes = [c_int, f, i32, i32, u32, i32]
         L.orc_trace_brute.argtypes = [c_int, f, c_int, f, f, i32]
         L.orc_render.argtypes = [c_int, f, i32, f, c_int, f, f, f, i32, f, f, u8, c_int, c_int, c_int]
         L.orc_rng.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, c_int, f]
@@ -84,15 +84,20 @@ def trace(tris: np.ndarray, rays: np.ndarray, width: int = 2):
     return hits, prims, occ
 
 
-def build_bvh4(tris: np.ndarray):
-    """Quantised BVH4: (children4 (n4,4), nodes (n4,16) uint32) as rr_debug_bvh4."""
+def build_bvh4(tris: np.ndarray, with_order: bool = False):
+    """Quantised BVH4: (children4 (n4,4), nodes (n4,16) uint32) as rr_debug_bvh4;
+    with_order: also the original triangle id of each position of the BVH4's
+    triangle array (the order its leaf ranges index)."""
     tris = _f32(tris).reshape(-1, 9)
     n = tris.shape[0]
     ni = max(n - 1, 1)
     n4 = np.zeros(1, np.int32)
     ch, bx = np.zeros((ni, 4), np.int32), np.zeros((ni, 16), np.uint32)
+    orig = np.zeros(max(n, 1), np.int32)
     lib().orc_build_bvh4(n, _p(tris, ctypes.c_float), _p(n4, ctypes.c_int32), _p(ch, ctypes.c_int32),
-                         _p(bx, ctypes.c_uint32))
+                         _p(bx, ctypes.c_uint32), _p(orig, ctypes.c_int32))
+    if with_order:
+        return ch[:n4[0]], bx[:n4[0]], orig[:n]
     return ch[:n4[0]], bx[:n4[0]]
 
 

@@ -170,6 +170,7 @@ typedef struct {
     int* tri_orig;
     int* tri_mat;
     int width;        /* hierarchy trace() walks: 2 (BVH2) or 4 (quantised BVH4 collapse) */
+    int* cnt;         /* 2 per internal node: leaf count of each child subtree (PLOC, Karras) */
     int n4;           /* BVH4 nodes */
     int* child4;      /* 4 per node: >= 0 node, < 0 ~leaf, ORC_EMPTY4 unused */
     uint32_t* q4;     /* 16 words per node, csrc/rr_device.h QNode4 */
@@ -221,7 +222,7 @@ static void subtree_box(const lbvh* B, const float* tris9, int c, float out[6]) 
 }
 
 static void lbvh_free(lbvh* B) {
-    free(B->child4); free(B->q4); free(B->child_lf); free(B->range);
+    free(B->child4); free(B->q4); free(B->child_lf); free(B->range); free(B->cnt);
     free(B->keys); free(B->order); free(B->child); free(B->box);
     free(B->tri); free(B->tri_orig); free(B->tri_mat);
     memset(B, 0, sizeof *B);
@@ -282,6 +283,7 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats, int 
     B->child = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->child_lf = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->range = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
+    B->cnt = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->box = (float*)malloc(sizeof(float) * 12 * (size_t)ni);
     if (hier == 3 && n > 2) {
         ploc_build(B, tris9);
@@ -290,6 +292,7 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats, int 
     }
     if (n == 1) {
         B->child[0] = ~0; B->child[1] = ~0;
+        B->cnt[0] = B->cnt[1] = 1;
     } else {
         const uint32_t* k = B->keys;
         for (int i = 0; i < n - 1; ++i) {
@@ -313,6 +316,8 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats, int 
             B->child[2 * i + 1] = (hi_ == g + 1) ? ~(g + 1) : g + 1;
             B->range[2 * i] = lo_;
             B->range[2 * i + 1] = hi_ - lo_ + 1;
+            B->cnt[2 * i] = g - lo_ + 1;       /* leaves of the left subtree [lo_, g] */
+            B->cnt[2 * i + 1] = hi_ - g;       /* and of the right one [g + 1, hi_] */
         }
     }
     /* boxes bottom-up: children of node i have larger indices or are leaves?
@@ -383,9 +388,12 @@ static void ploc_build(lbvh* B, const float* tris9) {
     float* box = (float*)malloc(sizeof(float) * 6 * (size_t)n);
     float* box2 = (float*)malloc(sizeof(float) * 6 * (size_t)n);
     int* nn = (int*)malloc(sizeof(int) * (size_t)n);
+    int* cn = (int*)malloc(sizeof(int) * (size_t)n);   /* leaves under each cluster */
+    int* cn2 = (int*)malloc(sizeof(int) * (size_t)n);
     for (int i = 0; i < n; ++i) {
         tri_box(tris9 + 9 * (size_t)B->order[i], box + 6 * (size_t)i);
         ref[i] = ~i;
+        cn[i] = 1;
     }
     int cnt = n, next = n - 2;
     while (cnt > 1) {
@@ -418,10 +426,14 @@ static void ploc_build(lbvh* B, const float* tris9) {
                 for (int t = 0; t < 6; ++t) { nb[t] = a[t]; nb[6 + t] = b[t]; }
                 B->child[2 * idx] = ref[i];
                 B->child[2 * idx + 1] = ref[j];
+                B->cnt[2 * idx] = cn[i];
+                B->cnt[2 * idx + 1] = cn[j];
                 for (int t = 0; t < 3; ++t) { o[t] = fminf(a[t], b[t]); o[3 + t] = fmaxf(a[3 + t], b[3 + t]); }
+                cn2[k] = cn[i] + cn[j];
                 ref2[k++] = idx;
             } else {
                 for (int t = 0; t < 6; ++t) o[t] = a[t];
+                cn2[k] = cn[i];
                 ref2[k++] = ref[i];
             }
         }
@@ -429,8 +441,9 @@ static void ploc_build(lbvh* B, const float* tris9) {
         cnt = k;
         int* tr = ref; ref = ref2; ref2 = tr;
         float* tb = box; box = box2; box2 = tb;
+        int* tc = cn; cn = cn2; cn2 = tc;
     }
-    free(ref); free(ref2); free(box); free(box2); free(nn);
+    free(ref); free(ref2); free(box); free(box2); free(nn); free(cn); free(cn2);
 }
 
 /* Quantisation of the BVH4 child boxes (csrc/rr_device.h q4_exponent /
@@ -488,19 +501,31 @@ static void q4_pack(const float lo[3][4], const float hi[3][4], const int ref[4]
 
 /* BVH4 collapse of the BVH2 (PLOC, or Karras below 3 triangles), as
  * csrc/bvh.hip build_bvh4 (k_c4_count / k_c4_emit): breadth first from the
- * root; a node's children start as its BVH2 root's two children, and while
- * fewer than four, the internal entry with the largest box measure
- * dx*dy + dy*dz + dz*dx (ties: lowest slot) is replaced by its left child and
- * its right child appended; the internal children of a node get consecutive
- * indices in slot order after every node of the current level (a FIFO
- * numbering). Boxes are the BVH2 child boxes, quantised by q4_pack. */
-typedef struct { int m; int ref[4]; float lo[3][4], hi[3][4]; } c4set;
+ * root; a node's children start as its BVH2 root's two children. A child
+ * subtree of at most ORC_LEAF_TRIS triangles is a leaf entry (never opened);
+ * while there are fewer than four entries, the internal entry with the
+ * largest box measure dx*dy + dy*dz + dz*dx (ties: lowest slot) is replaced
+ * by its left child and its right child appended. The internal children of a
+ * node get consecutive indices in slot order after every node of the current
+ * level (a FIFO numbering); the triangles of its leaf entries get consecutive
+ * positions of the BVH4's own triangle array, in slot order and, within an
+ * entry, in the left-first order of its subtree, after every triangle of the
+ * levels before and of the nodes before it in its level (tri, tri_orig,
+ * tri_mat are permuted into that order, so a leaf ref names the range
+ * ~(first | (count - 1) << 28) of it). Boxes are the BVH2 child boxes,
+ * quantised by q4_pack. */
+#define ORC_LEAF_TRIS 1
+typedef struct { int m; int ref[4], cnt[4]; float lo[3][4], hi[3][4]; } c4set;
 
 static void c4_put(const lbvh* B, c4set* S, int slot, int node, int side) {
     const float* f = B->box + 12 * (size_t)node + 6 * side;
     for (int a = 0; a < 3; ++a) { S->lo[a][slot] = f[a]; S->hi[a][slot] = f[3 + a]; }
-    S->ref[slot] = B->n > 1 ? B->child_lf[2 * node + side] : ~0;
+    S->ref[slot] = B->n > 1 ? B->child[2 * node + side] : ~0;
+    S->cnt[slot] = B->n > 1 ? B->cnt[2 * node + side] : 1;
 }
+
+/* an entry that stays a leaf: one triangle, or a subtree of <= ORC_LEAF_TRIS */
+static int c4_leaf(const c4set* S, int c) { return S->ref[c] < 0 || S->cnt[c] <= ORC_LEAF_TRIS; }
 
 static void c4_set(const lbvh* B, int r, c4set* S) {
     c4_put(B, S, 0, r, 0);
@@ -510,7 +535,7 @@ static void c4_set(const lbvh* B, int r, c4set* S) {
         int best = -1;
         float ba = 0.0f;
         for (int c = 0; c < S->m; ++c) {
-            if (S->ref[c] < 0) continue;
+            if (c4_leaf(S, c)) continue;
             float dx = S->hi[0][c] - S->lo[0][c], dy = S->hi[1][c] - S->lo[1][c], dz = S->hi[2][c] - S->lo[2][c];
             float a = dx * dy + dy * dz + dz * dx;
             if (best < 0 || a > ba) { best = c; ba = a; }
@@ -523,30 +548,54 @@ static void c4_set(const lbvh* B, int r, c4set* S) {
     }
 }
 
+/* sorted leaf indices of the subtree ref (left first), returns the count */
+static int c4_gather(const lbvh* B, int ref, int* out) {
+    if (ref < 0) { out[0] = ~ref; return 1; }
+    int k = c4_gather(B, B->child[2 * ref], out);
+    return k + c4_gather(B, B->child[2 * ref + 1], out + k);
+}
+
 static void lbvh_collapse4(lbvh* B) {
     const int n = B->n;
     B->n4 = 0;
     if (n <= 0) return;
     const int ni = n > 1 ? n - 1 : 1;
     int* src = (int*)malloc(sizeof(int) * (size_t)ni);
+    int* perm = (int*)malloc(sizeof(int) * (size_t)n);  /* BVH4 triangle position -> sorted leaf */
     B->child4 = (int*)malloc(sizeof(int) * 4 * (size_t)ni);
     B->q4 = (uint32_t*)malloc(sizeof(uint32_t) * 16 * (size_t)ni);
     src[0] = 0;
-    int count = 1;
+    int count = 1, ntri = 0;
     for (int idx = 0; idx < count; ++idx) {
         c4set S;
         c4_set(B, src[idx], &S);
         int ref[4];
         for (int c = 0; c < 4; ++c) {
             if (c >= S.m) ref[c] = ORC_EMPTY4;
-            else if (S.ref[c] >= 0) { src[count] = S.ref[c]; ref[c] = count++; }
-            else ref[c] = S.ref[c];
+            else if (!c4_leaf(&S, c)) { src[count] = S.ref[c]; ref[c] = count++; }
+            else if (n == 1) { perm[0] = 0; ref[c] = leaf_ref(0, 1); }  /* one triangle: both slots name it */
+            else {
+                const int k = c4_gather(B, S.ref[c], perm + ntri);
+                ref[c] = leaf_ref(ntri, k);
+                ntri += k;
+            }
         }
         q4_pack((const float(*)[4])S.lo, (const float(*)[4])S.hi, ref, S.m, B->q4 + 16 * (size_t)idx);
         for (int c = 0; c < 4; ++c) B->child4[4 * (size_t)idx + c] = ref[c];
     }
     B->n4 = count;
-    free(src);
+    /* the triangle arrays in the BVH4's leaf order */
+    float* tri = (float*)malloc(sizeof(float) * 9 * (size_t)n);
+    int* orig = (int*)malloc(sizeof(int) * (size_t)n);
+    int* mat = (int*)malloc(sizeof(int) * (size_t)n);
+    for (int i = 0; i < n; ++i) {
+        memcpy(tri + 9 * (size_t)i, B->tri + 9 * (size_t)perm[i], 9 * sizeof(float));
+        orig[i] = B->tri_orig[perm[i]];
+        mat[i] = B->tri_mat[perm[i]];
+    }
+    free(B->tri); free(B->tri_orig); free(B->tri_mat);
+    B->tri = tri; B->tri_orig = orig; B->tri_mat = mat;
+    free(src); free(perm);
 }
 
 /* ------------------------------------------------------------ tracing ---- */
@@ -1270,13 +1319,15 @@ int orc_trace_brute(int n, const float* tris9, int n_rays, const float* rays, fl
 
 /* Quantised BVH4 (rr_debug_bvh4 layout): n4 nodes, 4 child refs and the 16
  * words of each node. */
-int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, uint32_t* nodes16) {
+int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, uint32_t* nodes16,
+                   int32_t* tri_orig) {
     lbvh B;
     lbvh_build(&B, n, tris9, NULL, 3);
     lbvh_collapse4(&B);
     *n4 = B.n4;
     if (children4 && B.n4) memcpy(children4, B.child4, sizeof(int32_t) * 4 * (size_t)B.n4);
     if (nodes16 && B.n4) memcpy(nodes16, B.q4, sizeof(uint32_t) * 16 * (size_t)B.n4);
+    if (tri_orig && n > 0) memcpy(tri_orig, B.tri_orig, sizeof(int32_t) * (size_t)n);
     lbvh_free(&B);
     return 0;
 }

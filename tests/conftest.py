@@ -34,6 +34,17 @@ def scene_path(name: str) -> str:
     return os.path.join(SCENES, name)
 
 
+def bvh4_leaf_positions(ch):
+    """Positions of a BVH4's triangle array its leaf refs ~(first | (count - 1)
+    << 28) name, in node order."""
+    out = []
+    for r in ch[ch < 0].tolist():
+        x = ~int(r)
+        f, k = x & 0x0FFFFFFF, (x >> 28) + 1
+        out += list(range(f, f + k))
+    return out
+
+
 def have_reference() -> bool:
     return os.path.isdir(os.path.join(REFERENCE, "worker"))
 

@@ -11,7 +11,7 @@ through it equals the oracle's traversal; images at reduced resolution/spp.
 import numpy as np
 import pytest
 
-from conftest import scene_path, walk_lbvh
+from conftest import bvh4_leaf_positions, scene_path, walk_lbvh
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -102,13 +102,14 @@ def test_physics_trace_bit_exact(ctx, s02, hier):
 @pytest.mark.parametrize("frame", [1, 90])
 def test_physics_bvh4_bit_exact(ctx, s02, frame):
     st = ctx.frame_state(s02, frame)
-    ch, bx = ctx.bvh4(s02, frame)
-    och, obx = O.build_bvh4(st.tris)
+    ch, bx, order = ctx.bvh4(s02, frame, with_order=True)
+    och, obx, oorder = O.build_bvh4(st.tris, with_order=True)
     assert ch.shape == och.shape and np.array_equal(ch, och)
     assert np.array_equal(bx, obx)
-    # every leaf appears exactly once, every node but the root is referenced once
-    leaves = -ch[ch < 0] - 1
-    assert np.array_equal(np.sort(leaves), np.arange(st.tris.shape[0]))
+    assert np.array_equal(order, oorder)  # the triangles in the BVH4's leaf order
+    # every triangle position in exactly one leaf (of <= 2), every node but the root referenced once
+    assert sorted(bvh4_leaf_positions(ch)) == list(range(st.tris.shape[0]))
+    assert sorted(order.tolist()) == list(range(st.tris.shape[0]))
     inner = ch[(ch >= 0) & (ch != 0x7FFFFFFF)]
     assert np.array_equal(np.sort(inner), np.arange(1, ch.shape[0]))
 
@@ -157,12 +158,15 @@ def test_c5_full_size_bvh_bit_exact(ctx, sc5):
 
 def test_c5_full_size_bvh4_bit_exact(ctx, sc5):
     st = ctx.frame_state(sc5, 120)
-    ch, bx = ctx.bvh4(sc5, 120)
-    och, obx = O.build_bvh4(st.tris)
+    ch, bx, order = ctx.bvh4(sc5, 120, with_order=True)
+    och, obx, oorder = O.build_bvh4(st.tris, with_order=True)
     assert np.array_equal(ch, och)
     assert np.array_equal(bx, obx)
-    leaves = -ch[ch < 0] - 1
+    assert np.array_equal(order, oorder)
+    leaves = np.array(bvh4_leaf_positions(ch))
     assert np.array_equal(np.sort(leaves), np.arange(st.tris.shape[0]))
+    two = int(np.count_nonzero([((~int(r)) >> 28) == 1 for r in ch[ch < 0].tolist()]))
+    print(f"C5 BVH4: {ch.shape[0]} nodes, {int((ch < 0).sum())} leaves ({two} of two triangles)")
 
 
 @pytest.mark.parametrize("width", [3, 4])

@@ -335,9 +335,25 @@ def _q4_child_boxes(node):
     return org + q[:, 0:3] * np.exp2(e), org + q[:, 3:6] * np.exp2(e)
 
 
-def _check_q4_contains(tris, ch, nodes):
-    """Every quantised child box contains the boxes of all triangles below it."""
-    sorted_tris = None
+def leaf_range(r):
+    """(first, count) of a leaf ref ~(first | (count - 1) << 28)."""
+    x = ~int(r)
+    return x & 0x0FFFFFFF, (x >> 28) + 1
+
+
+def bvh4_leaf_positions(ch):
+    """Positions of the BVH4's triangle array its leaf refs name, in node order."""
+    out = []
+    for r in ch[(ch < 0)].tolist():
+        f, k = leaf_range(r)
+        out += list(range(f, f + k))
+    return out
+
+
+def _check_q4_contains(tris, ch, nodes, order):
+    """Every quantised child box contains the boxes of all triangles below it
+    (order: original triangle id of each position of the BVH4's triangle array)."""
+    bvh4_tris = tris.reshape(-1, 9)[order].reshape(-1, 3, 3)
 
     def walk(i):
         lo4, hi4 = _q4_child_boxes(nodes[i])
@@ -346,16 +362,18 @@ def _check_q4_contains(tris, ch, nodes):
             r = int(ch[i, c])
             if r == 0x7FFFFFFF:
                 continue
-            ids = [~r] if r < 0 else walk(r)
+            if r < 0:
+                f, k = leaf_range(r)
+                ids = list(range(f, f + k))
+            else:
+                ids = walk(r)
             under += ids
-            t = sorted_tris[ids].reshape(-1, 3).astype(np.float64)
+            t = bvh4_tris[ids].reshape(-1, 3).astype(np.float64)
             assert np.all(lo4[c] <= t.min(0)) and np.all(t.max(0) <= hi4[c]), (i, c)
         return under
 
-    # leaf refs name sorted leaves: recover the Morton order from the LBVH build
-    _, order, _, _ = O.build_lbvh(tris, hier=3 if tris.shape[0] > 2 else 2)
-    sorted_tris = tris.reshape(-1, 9)[order].reshape(-1, 3, 3)
     assert sorted(walk(0)) == list(range(tris.shape[0]))
+    assert sorted(order.tolist()) == list(range(tris.shape[0]))  # a permutation
 
 
 @pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (7, 2), (300, 3), (5000, 4)])
@@ -366,14 +384,15 @@ def test_bvh4_collapse_and_walk_equal_brute_force(n, seed):
     rng = np.random.default_rng(seed)
     c = rng.uniform(-5, 5, (n, 1, 3))
     tris = (c + rng.normal(0, 0.6, (n, 3, 3))).astype(np.float32)
-    ch, nodes = O.build_bvh4(tris)
+    ch, nodes, order = O.build_bvh4(tris, with_order=True)
     assert np.array_equal(nodes[:, 4:8].view(np.int32), ch)
-    leaves = -ch[ch < 0] - 1
-    assert np.array_equal(np.sort(leaves), np.arange(n)) or (n == 1 and set(leaves) == {0})
+    leaves = bvh4_leaf_positions(ch)
+    assert sorted(leaves) == list(range(n)) or (n == 1 and set(leaves) == {0})
+    assert all(leaf_range(r)[1] <= 2 for r in ch[ch < 0].tolist())  # leaves of at most 2 triangles
     inner = ch[(ch >= 0) & (ch != 0x7FFFFFFF)]
     assert np.array_equal(np.sort(inner), np.arange(1, ch.shape[0]))
     if n > 1:
-        _check_q4_contains(tris, ch, nodes)
+        _check_q4_contains(tris, ch, nodes, order)
     m = 4000
     rays = np.zeros((m, 8), np.float32)
     rays[:, 0:3] = rng.uniform(-8, 8, (m, 3))
@@ -411,8 +430,8 @@ def test_bvh4_axis_aligned_geometry_and_rays():
                 p[k][v] += dv
             quads += [(p[0], p[1], p[2]), (p[0], p[2], p[3])]
     tris = np.array(quads, np.float32)
-    ch, nodes = O.build_bvh4(tris)
-    _check_q4_contains(tris, ch, nodes)
+    ch, nodes, order = O.build_bvh4(tris, with_order=True)
+    _check_q4_contains(tris, ch, nodes, order)
     rng = np.random.default_rng(7)
     rays = []
     for _ in range(3000):
