@@ -111,8 +111,16 @@ RR_HD int leaf_count(int ref) { return ((~ref) >> 28) + 1; }
 
 constexpr int kMaxLights = 64;
 constexpr int kBlock = 256;         // threads per block for all path kernels
-constexpr int kLdsStack = 16;       // traversal stack entries kept in LDS per lane
-constexpr int kSpillStack = 64;     // further entries in the per-thread HBM spill area
+// Traversal stack per lane: kLdsStack entries in LDS, the rest (up to the
+// oracle's ORC_MAXDEPTH = 80 in all) in a per-thread HBM spill area. 12 LDS
+// entries (12 KB per 256-thread block) leave room for the split-path trace
+// kernels' top-of-tree node copy (wavefront.hip stage_top) at 8 blocks per CU;
+// 16 entries with half the node copy measured 1-1.5 % slower on C5.
+#ifndef RR_LDS_STACK
+#define RR_LDS_STACK 12
+#endif
+constexpr int kLdsStack = RR_LDS_STACK;
+constexpr int kSpillStack = 80 - kLdsStack;
 constexpr int kDimsPerBounce = 8;   // RNG dimensions consumed per bounce
 constexpr int kRrStartBounce = 3;   // Russian roulette from this bounce on
 
@@ -599,6 +607,36 @@ RR_D uint32_t q4_box_hits(const float4& org, const int4& ch, const uint4& q0, co
     return hits;
 }
 
+// Node fetch of the BVH4 walk. The split-path trace kernels keep a copy of
+// the first n_top nodes in LDS (Q4Nodes): nodes are numbered breadth first,
+// so those are the top levels of the tree, which every ray visits — each of
+// those visits becomes a ds_read instead of an L2 round trip. Which copy a
+// node comes from changes no bit of it.
+RR_D void q4_load(const QNode4* __restrict__ nodes, int i, float4& org, int4& ch, uint4& q0, uint2& q1) {
+    const QNode4* p = nodes + i;
+    org = p->org;
+    ch = p->child;
+    q0 = p->q0;
+    q1 = p->q1;
+}
+struct Q4Nodes {
+    const QNode4* __restrict__ g;
+    lds_f4w* top;  // nodes [0, n_top): 4 float4 each (QNode4 layout)
+    int n_top;
+};
+RR_D void q4_load(const Q4Nodes& n, int i, float4& org, int4& ch, uint4& q0, uint2& q1) {
+    if (i < n.n_top) {
+        const lds_f4w* q = n.top + 4 * i;
+        org = lds_ld4(q);
+        const float4 c = lds_ld4(q + 1), a = lds_ld4(q + 2), b = lds_ld4(q + 3);
+        ch = make_int4(f2i(c.x), f2i(c.y), f2i(c.z), f2i(c.w));
+        q0 = make_uint4((uint32_t)f2i(a.x), (uint32_t)f2i(a.y), (uint32_t)f2i(a.z), (uint32_t)f2i(a.w));
+        q1 = make_uint2((uint32_t)f2i(b.x), (uint32_t)f2i(b.y));
+    } else {
+        q4_load(n.g, i, org, ch, q0, q1);
+    }
+}
+
 // Resumable traversal of the quantised BVH4 (same contract as TravState), box
 // tests by q4_box_hits. Leaf children whose boxes pass are intersected at once in slot order; the
 // nearest hit internal child is visited next and the others are pushed in
@@ -620,17 +658,20 @@ struct TravStateQ4 {
         iq = rcp3(d);
         node = 0;
     }
-    template <typename TriP, typename Stack>
-    RR_D bool step(const QNode4* __restrict__ nodes, TriP tris, Stack& st, TravCount& cnt) {
+    template <typename NodeSrc, typename TriP, typename Stack>
+    RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
         if (kCount) ++cnt.nodes;
         const float tcur = h.t;
         float tn[4];
         int ref[4];
         uint32_t leaves = 0, inner = 0;
         {
-            const QNode4* p = nodes + node;
-            const int4 ch = p->child;
-            const uint32_t hm = q4_box_hits(p->org, ch, p->q0, p->q1, o, iq, tmin, tcur, tn);
+            float4 org;
+            int4 ch;
+            uint4 q0;
+            uint2 q1;
+            q4_load(nodes, node, org, ch, q0, q1);
+            const uint32_t hm = q4_box_hits(org, ch, q0, q1, o, iq, tmin, tcur, tn);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 ref[c] = i4get(ch, c);

@@ -255,6 +255,10 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         N = xyz(nm);
         mid = f2i(nm.w) & ((1 << kHullShift) - 1);
         hull = (uint32_t)f2i(nm.w) >> kHullShift;
+        // an LDS-resident scene holds a handful of materials (scene_lds_f4): the
+        // table offsets become 24-bit multiplies (full rate) instead of
+        // v_mul_lo_u32 / v_mad_u64_u32
+        __builtin_assume(mid >= 0 && mid < 4096);
     } else {
         const TriPack tp = load_tri(v.tris, h.idx);
         mid = f2i(tp.p1.w);
@@ -283,6 +287,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     if (fc.n_lights > 0) {
         int li = (int)(rng(key, dim0) * (float)fc.n_lights);
         if (li > fc.n_lights - 1) li = fc.n_lights - 1;
+        __builtin_assume(li >= 0 && li < kMaxLights);  // rng >= 0, n_lights <= kMaxLights (setup_frame)
         const auto lt = v.lights + kLightF * li;
         float3 wi, Li;  // Li: radiance x cos_light / pdf (solid angle), i.e. I*cos/d^2
         float dist;
@@ -393,6 +398,7 @@ struct SceneArgs {
     const float* filter;
     const float* mat_lut;    // kMatLutStride floats per material
     int n_nodes, n_tris, n_mats, n_lights;
+    int n_nodes4;            // quantised BVH4 nodes (split path)
 };
 
 namespace {
@@ -676,7 +682,6 @@ constexpr int kTraceWaves = 8;
 // 64 / 64 spp: 191 -> 139, 174 -> 149, 192 -> 160 ms).
 template <bool kAnyHit, bool kCount>
 using SplitTrav = TravStateQ4<kAnyHit, kCount>;
-RR_D const QNode4* split_nodes(const SceneArgs& sa) { return sa.nodes4; }
 constexpr int kQGroups = 64;   // append groups per queue (one lane each in QueueMap)
 constexpr int kQStride = 32;   // words between group counters (128 B)
 
@@ -700,6 +705,26 @@ RR_D int xcd_wave_rank() {
     const int G = (int)gridDim.x, bx = (int)blockIdx.x, xcd = bx & 7;
     return __builtin_amdgcn_readfirstlane((xcd * (G >> 3) + min(xcd, G & 7) + (bx >> 3)) * kWavesPerBlock +
                                           (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
+}
+// Top of the quantised BVH4 in LDS for the trace kernels (Q4Nodes): the
+// first kTopNodes nodes (breadth-first numbering: the four top levels, 85
+// nodes, and part of the fifth), copied by the block at launch. 128 nodes =
+// 8 KB beside the 12 KB traversal stack (kLdsStack) keeps 8 blocks of 256
+// threads (8 waves per SIMD) per CU. Measured per frame slice against no copy
+// (C5 at 16 spp / 02 / 03 at 64 spp): 105.8 -> 101.4, 110.5 -> 107.0, 118.2 ->
+// 115.9 ms (extension and shadow traversal -3 to -7 %); 64 nodes with a
+// 16-entry stack 103.3, 192 with 8 entries 103.4 ms on C5.
+#ifndef RR_TOP_NODES
+#define RR_TOP_NODES 128
+#endif
+constexpr int kTopNodes = RR_TOP_NODES;
+RR_D Q4Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
+    lds_f4w* top = (lds_f4w*)top_shared;
+    const int n = kTopNodes > 0 ? min(sa.n_nodes4, kTopNodes) : 0;
+    const rr_f4v* src = reinterpret_cast<const rr_f4v*>(sa.nodes4);
+    for (int i = threadIdx.x; i < 4 * n; i += kBlock) top[i] = src[i];
+    __syncthreads();
+    return Q4Nodes{sa.nodes4, top, n};
 }
 template <typename TS, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack& st, TravCount& cnt, MapFn&& map,
@@ -846,12 +871,14 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameCons
                                                                           unsigned long long* __restrict__ tc,
                                                                           uint32_t* __restrict__ traced) {
     __shared__ int lds_stack[kLdsStack * kBlock];
+    __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
+    const Q4Nodes nodes = stage_top(sa, top_nodes);
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
     trace_refill<SplitTrav<false, kCount>>(
-        split_nodes(sa), sa.tris, sa.n_tris, np, st, cnt, [](int p) { return (uint32_t)p; },
+        nodes, sa.tris, sa.n_tris, np, st, cnt, [](int p) { return (uint32_t)p; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
             const int sl = (int)fc.div_npix.div(p);
             const int pix = (int)p - sl * fc.npix;
@@ -1021,12 +1048,14 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_extend(SceneArgs 
                                                                          int32_t* __restrict__ spill,
                                                                          unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
+    __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
+    const Q4Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
-        split_nodes(sa), sa.tris, sa.n_tris, qm.span, st, cnt, [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
@@ -1076,12 +1105,14 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_shadow_refill(SceneArgs
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
+    __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
+    const Q4Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
-        split_nodes(sa), sa.tris, sa.n_tris, qm.span, st, cnt, [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
@@ -1402,6 +1433,21 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     const int n_units = n_sliced + (to.n - nb);  // box slices, then one unit per background tile
     const int n_shards = min((int)gridDim.x, kTileShards);  // small frames launch fewer blocks than shards
     const int shard = (int)blockIdx.x % n_shards;
+    // Film value and 8-bit pixel of a background tile: every sample is the
+    // world term, summed in the grouped order, the same bits for every pixel,
+    // so the wave computes them once (wave-uniform, SGPRs) instead of per tile
+    // (128 x 3 adds and a tonemap with its sRGB table reads per background tile).
+    float4 bg = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int g = 0; g < ng; ++g) {
+        float3 P = mk3(0.0f, 0.0f, 0.0f);
+        const int s_end = min(fc.spp_total, (g + 1) * kFilmGroup);
+        for (int s = g * kFilmGroup; s < s_end; ++s) add_to(P, fc.world);
+        bg.x = bg.x + P.x;
+        bg.y = bg.y + P.y;
+        bg.z = bg.z + P.z;
+    }
+    bg = make_float4(uniform_f(bg.x), uniform_f(bg.y), uniform_f(bg.z), 0.0f);
+    const uchar4 bg_px = __builtin_bit_cast(uchar4, uniform_i(__builtin_bit_cast(int, tonemap(fc, bg, srgb))));
     for (;;) {
         int t, k = 0, nk = 1;  // tile, slice, slices of this tile
         int u = 0;
@@ -1423,19 +1469,11 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         const bool valid = px < fc.W && py < fc.H;
         const int pix = py * fc.W + px;
         float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (tile_culled(fc, cull, tx, ty)) {  // background tile: film = the world term, grouped sum
+        if (tile_culled(fc, cull, tx, ty)) {  // background tile: film = the world term, grouped sum (bg)
             if (k != 0) continue;             // (slice 0 does the whole tile)
-            for (int g = 0; g < ng; ++g) {
-                float3 P = mk3(0.0f, 0.0f, 0.0f);
-                const int s_end = min(fc.spp_total, (g + 1) * kFilmGroup);
-                for (int s = g * kFilmGroup; s < s_end; ++s) add_to(P, fc.world);
-                acc.x = acc.x + P.x;
-                acc.y = acc.y + P.y;
-                acc.z = acc.z + P.z;
-            }
             if (valid) {
-                film[pix] = acc;
-                out[pix] = tonemap(fc, acc, srgb);
+                film[pix] = bg;
+                out[pix] = bg_px;
             }
             continue;
         }
@@ -1992,7 +2030,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
             tc = p.trav_counts.ptr;
         }
         const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
-                           p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
+                           p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.n4};
         FrameConsts fc = base;
         fc.first_sample = 0;
         fc.spp_chunk = base.spp_total;
@@ -2052,7 +2090,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
-                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights};
+                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.n4};
     render_split(p, base, n_chunks, st, sa, tc, pq, sq);
     RR_HIP(hipGetLastError());
 }
