@@ -19,7 +19,9 @@ def main():
     scene_path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "scenes", "04_very-simple-standin.rrscene")
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     out = tempfile.mkdtemp(prefix="rr_host_timing_")
-    params = rr.default_params(flags=rr.native.RR_FLAG_PROFILE_KERNELS)
+    prof = os.environ.get("RR_HOST_TIMING_PROFILE", "0") == "1"
+    params = rr.default_params(flags=rr.native.RR_FLAG_PROFILE_KERNELS if prof else 0)
+    depth = rr.native.RR_MAX_FRAMES_IN_FLIGHT
     rows = []
     with rr.RenderContext(0) as ctx:
         s = ctx.load_scene(scene_path)
@@ -34,7 +36,7 @@ def main():
             tk = ctx.submit_frame(s, f, params, os.path.join(out, f"{i:06d}"), "JPEG", 90)
             t_sub = time.perf_counter() - t0
             pending.append((tk, t_sub))
-            if len(pending) >= 2:
+            if len(pending) >= depth:
                 tk0, ts0 = pending.pop(0)
                 t1 = time.perf_counter()
                 _, st = ctx.complete_frame(tk0)
@@ -51,6 +53,7 @@ def main():
     k = len(rows)
     avg = [sum(r[j] for r in rows) / k * 1e3 for j in range(6)]
     print(f"frames {k}, wall {wall / k * 1e3:.3f} ms/frame ({k / wall:.1f} frames/s)")
+    print(f"{depth} frames in flight, per-kernel events {'on' if prof else 'off'}")
     print(f"submit {avg[0]:.3f} ms | complete {avg[1]:.3f} ms (encode+write {avg[2]:.3f}) | "
           f"device trace {avg[3]:.3f} ms, kernels {avg[4]:.3f} ms | anim {avg[5]:.3f} ms")
 
