@@ -43,6 +43,7 @@
 
 #define ORC_FILTER_N 1024
 #define ORC_SRGB_N 4096
+#define ORC_SEG 64       /* pixels per OpenMP work item of orc_render */
 #define ORC_MAXDEPTH 80 /* = the GPU traversal stack (kLdsStack + kSpillStack, rr_device.h) */
 
 typedef struct { float x, y, z; } v3;
@@ -1426,13 +1427,21 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     const float inv_spp = 1.0f / (float)S->spp;
     if (row_end <= 0 || row_end > S->H) row_end = S->H;
     if (row_begin < 0) row_begin = 0;
+    /* work items of ORC_SEG pixels of one row, so that a band of a few rows
+     * still spreads over every thread (per-pixel results do not depend on the
+     * split) */
+    const int nseg = (S->W + ORC_SEG - 1) / ORC_SEG;
+    const long n_items = (long)(row_end - row_begin) * nseg;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 1)
 #endif
-    for (int y = row_begin; y < row_end; ++y) {
+    for (long it = 0; it < n_items; ++it) {
+        const int y = row_begin + (int)(it / nseg);
+        const int x0 = (int)(it % nseg) * ORC_SEG;
+        const int x1 = x0 + ORC_SEG < S->W ? x0 + ORC_SEG : S->W;
         long long rays[4] = {0, 0, 0, 0};
-        for (int x = 0; x < S->W; ++x) {
+        for (int x = x0; x < x1; ++x) {
             int pix = y * S->W + x;
             /* film sum order (the product's kFilmGroup, csrc/wavefront.hip): in
              * order within groups of ORC_FILM_GROUP samples, group sums in order */
