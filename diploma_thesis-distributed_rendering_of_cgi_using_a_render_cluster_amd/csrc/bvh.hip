@@ -351,67 +351,59 @@ __global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restr
     }
 }
 
-// ------------------------------------------------------- BVH4 collapse ---
-// The BVH2 (PLOC; Karras below 3 triangles) becomes the quantised BVH4 of the
-// split path (rr_device.h QNode4), top down, one level per launch pair:
-//  - children of the BVH4 node rooted at BVH2 node r: start from r's two
-//    children; a child subtree of at most kLeafTris triangles is a leaf entry
-//    and never opened; while there are fewer than four entries, the internal
-//    entry with the largest box measure (dx*dy + dy*dz + dz*dx, ties: lowest
-//    slot) is opened (replaced by its left child, its right child appended);
+// ------------------------------------------------ 6-wide collapse ---
+// The BVH2 (PLOC; Karras below 3 triangles) becomes the quantised 6-wide
+// hierarchy of the split path (rr_device.h QNode6), top down, one level per
+// launch pair:
+//  - children of the node rooted at BVH2 node r: start from r's two children
+//    (one slot for a one-triangle scene); a child that is a single triangle is
+//    a leaf entry; while there are fewer than six entries, the internal entry
+//    with the largest box measure (dx*dy + dy*dz + dz*dx, ties: lowest slot)
+//    is opened (replaced by its left child, its right child appended);
 //  - nodes are numbered breadth first and the internal children of a node
 //    take consecutive indices in slot order (level frontier [lo, hi): node k
 //    counts its internal children, an exclusive scan gives each node its
-//    children's first index hi + prefix), so siblings share 128 B lines;
+//    children's first index hi + prefix), so siblings share 128 B lines and a
+//    node stores only the first index;
 //  - the triangles of a node's leaf entries take consecutive positions of the
-//    BVH4's own triangle array (tris4, swapped into DevScene::tris after the
-//    collapse) in slot order, and within an entry in the left-first order of
-//    its subtree, after the triangles of the levels before and of the nodes
-//    before it in its level (a second count and scan), so one leaf is one
-//    contiguous range ~(first | (count - 1) << 28): on C5 the single-triangle
-//    leaves had left ~40 % of the BVH4 nodes with two leaf children;
+//    hierarchy's own triangle array (qtris, swapped into DevScene::tris after
+//    the collapse) in slot order, after the triangles of the levels before and
+//    of the nodes before it in its level (a second count and scan), so a node
+//    stores only the first position and the mask of its internal slots;
 //  - child boxes are quantised on the node's grid: origin = the lo corner of
 //    the children's union, per axis the smallest exponent that spans it in
 //    255 steps, lo rounded down and hi up (exactly, in double).
-// oracle/rr_oracle.c lbvh_collapse4 / q4_pack restate it (ORC_LEAF_TRIS).
-#ifndef RR_LEAF_TRIS
-#define RR_LEAF_TRIS 1  // must equal oracle/rr_oracle.c ORC_LEAF_TRIS (A/B builds may change it)
-#endif
-constexpr int kLeafTris = RR_LEAF_TRIS;
-struct C4Set {
+// oracle/rr_oracle.c lbvh_collapse4 / q4_pack restate it.
+struct QwSet {
     int m;
-    int ref[4], cnt[4];
-    float lo[3][4], hi[3][4];
+    int ref[kQWidth];
+    float lo[3][kQWidth], hi[3][kQWidth];
 };
 
-__device__ __forceinline__ float c4_measure(const C4Set& S, int c) {
+__device__ __forceinline__ float qw_measure(const QwSet& S, int c) {
     const float dx = S.hi[0][c] - S.lo[0][c], dy = S.hi[1][c] - S.lo[1][c], dz = S.hi[2][c] - S.lo[2][c];
     return dx * dy + dy * dz + dz * dx;
 }
 
-// an entry that stays a leaf: one triangle, or a subtree of <= kLeafTris
-__device__ __forceinline__ bool c4_leaf(const C4Set& S, int c) { return S.ref[c] < 0 || S.cnt[c] <= kLeafTris; }
-
-__device__ void c4_set(const BvhNode* __restrict__ nodes, int n, int r, C4Set& S) {
+__device__ void qw_set(const BvhNode* __restrict__ nodes, int n, int r, QwSet& S) {
     auto put = [&](int slot, const BvhNode& nd, int side) {
         const float* f = reinterpret_cast<const float*>(&nd) + 6 * side;
         for (int a = 0; a < 3; ++a) {
             S.lo[a][slot] = f[a];
             S.hi[a][slot] = f[3 + a];
         }
-        S.ref[slot] = n > 1 ? (side ? nd.d.y : nd.d.x) : ~0;  // one triangle: both slots are leaf 0
-        S.cnt[slot] = n > 1 ? (side ? nd.d.w : nd.d.z) : 1;
+        S.ref[slot] = n > 1 ? (side ? nd.d.y : nd.d.x) : ~0;
     };
     const BvhNode nd = nodes[r];
     put(0, nd, 0);
     put(1, nd, 1);
-    S.m = 2;
-    while (S.m < 4) {
+    S.m = n > 1 ? 2 : 1;  // one triangle: one leaf slot
+    while (S.m < kQWidth) {
         int best = -1;
         float ba = 0.0f;
         for (int c = 0; c < S.m; ++c) {
-            if (c4_leaf(S, c)) continue;
-            const float a = c4_measure(S, c);
+            if (S.ref[c] < 0) continue;
+            const float a = qw_measure(S, c);
             if (best < 0 || a > ba) {
                 best = c;
                 ba = a;
@@ -426,17 +418,17 @@ __device__ void c4_set(const BvhNode* __restrict__ nodes, int n, int r, C4Set& S
 }
 
 // Level start: frontier [0, 1) = the BVH2 root, triangle positions from 0.
-__global__ void k_c4_init(int32_t* __restrict__ ctl, int32_t* __restrict__ src) {
+__global__ void k_qw_init(int32_t* __restrict__ ctl, int32_t* __restrict__ src) {
     ctl[0] = 0;
     ctl[1] = 1;
     ctl[2] = 0;
     src[0] = 0;
 }
 
-// cnt[k] = internal children, tcnt[k] = triangles of the leaf entries of
+// cnt[k] = internal children, tcnt[k] = leaf children (one triangle each) of
 // frontier node lo + k (0 past the frontier, k <= bound: the scans' totals
 // land in [bound]).
-__global__ __launch_bounds__(kBlock) void k_c4_count(const int32_t* __restrict__ ctl, int bound, int n,
+__global__ __launch_bounds__(kBlock) void k_qw_count(const int32_t* __restrict__ ctl, int bound, int n,
                                                      const BvhNode* __restrict__ nodes,
                                                      const int32_t* __restrict__ src, uint32_t* __restrict__ cnt,
                                                      uint32_t* __restrict__ tcnt) {
@@ -445,13 +437,12 @@ __global__ __launch_bounds__(kBlock) void k_c4_count(const int32_t* __restrict__
     const int lo = ctl[0], hi = ctl[1];
     uint32_t c = 0, t = 0;
     if (k < bound && lo + k < hi) {
-        C4Set S;
-        c4_set(nodes, n, src[lo + k], S);
+        QwSet S;
+        qw_set(nodes, n, src[lo + k], S);
         for (int j = 0; j < S.m; ++j) {
-            if (!c4_leaf(S, j)) ++c;
-            else if (n > 1) t += (uint32_t)(S.ref[j] < 0 ? 1 : S.cnt[j]);
+            if (S.ref[j] >= 0) ++c;
+            else ++t;
         }
-        if (n == 1) t = 1;  // one triangle: both slots name position 0
     }
     cnt[k] = c;
     tcnt[k] = t;
@@ -460,52 +451,39 @@ __global__ __launch_bounds__(kBlock) void k_c4_count(const int32_t* __restrict__
 // Node lo + k: internal children -> indices hi + cnt[k] .., their BVH2 roots
 // -> src; leaf entries -> triangle positions ctl[2] + tcnt[k] .. (after the
 // exclusive scans), their triangles copied there; the quantised node -> out.
-__global__ __launch_bounds__(kBlock) void k_c4_emit(const int32_t* __restrict__ ctl, int bound, int n,
+__global__ __launch_bounds__(kBlock) void k_qw_emit(const int32_t* __restrict__ ctl, int bound, int n,
                                                     const BvhNode* __restrict__ nodes, int32_t* __restrict__ src,
                                                     const uint32_t* __restrict__ cnt,
                                                     const uint32_t* __restrict__ tcnt,
-                                                    const TriPack* __restrict__ tris, TriPack* __restrict__ tris4,
-                                                    QNode4* __restrict__ out) {
+                                                    const TriPack* __restrict__ tris, TriPack* __restrict__ qtris,
+                                                    QNode6* __restrict__ out) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= bound) return;
     const int lo = ctl[0], hi = ctl[1];
     const int idx = lo + k;
     if (idx >= hi) return;
-    C4Set S;
-    c4_set(nodes, n, src[idx], S);
-    int next = hi + (int)cnt[k];
-    int tpos = ctl[2] + (int)tcnt[k];
-    int ref[4];
-    for (int c = 0; c < 4; ++c) {
-        if (c >= S.m) {
-            ref[c] = kEmpty4;
-        } else if (!c4_leaf(S, c)) {
-            src[next] = S.ref[c];
-            ref[c] = next++;
-        } else if (n == 1) {
-            tris4[0] = tris[0];
-            ref[c] = leaf_ref(0, 1);
+    QwSet S;
+    qw_set(nodes, n, src[idx], S);
+    const int inner_base = hi + (int)cnt[k], tri_base = ctl[2] + (int)tcnt[k];
+    int next = inner_base, tpos = tri_base;
+    uint32_t inner = 0u;
+    for (int c = 0; c < S.m; ++c) {
+        if (S.ref[c] >= 0) {
+            src[next++] = S.ref[c];
+            inner |= 1u << c;
         } else {
-            // the subtree's leaves, left first (depth < kLeafTris)
-            int stack[kLeafTris], sp = 0, r = S.ref[c], m = 0;
-            const int first = tpos;
-            for (;;) {
-                if (r < 0) {
-                    tris4[tpos++] = tris[~r];
-                    ++m;
-                    if (sp == 0) break;
-                    r = stack[--sp];
-                } else {
-                    const int4 d = nodes[r].d;
-                    stack[sp++] = d.y;
-                    r = d.x;
-                }
-            }
-            ref[c] = leaf_ref(first, m);
+            qtris[tpos++] = tris[~S.ref[c]];
         }
     }
+    // quantised child boxes: children 0..3 one byte per word, 4 and 5 in byte
+    // pairs (rr_device.h QNode6)
+    uint32_t w[9] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // lo x, lo y, lo z, hi x, hi y, hi z; pairs
+    auto set_q = [&](int which, int c, uint32_t v) {
+        if (c < 4) w[which] |= v << (8 * c);
+        else w[6 + which / 2] |= v << (16 * (which & 1) + 8 * (c - 4));
+    };
     float org[3];
-    uint32_t ql[3] = {0u, 0u, 0u}, qh[3] = {0u, 0u, 0u}, eb = 0u;
+    uint32_t eb = 0u;
     for (int a = 0; a < 3; ++a) {
         float l = S.lo[a][0], h = S.hi[a][0];
         for (int c = 1; c < S.m; ++c) {
@@ -515,24 +493,21 @@ __global__ __launch_bounds__(kBlock) void k_c4_emit(const int32_t* __restrict__ 
         const int e = q4_exponent((double)h - (double)l);
         org[a] = l;
         eb |= (uint32_t)(e + 128) << (8 * a);
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t ql_c = c < S.m ? q4_quant(S.lo[a][c], l, e, false) : 255u;
-            const uint32_t qh_c = c < S.m ? q4_quant(S.hi[a][c], l, e, true) : 0u;
-            ql[a] |= ql_c << (8 * c);
-            qh[a] |= qh_c << (8 * c);
+        for (int c = 0; c < kQWidth; ++c) {
+            set_q(a, c, c < S.m ? q4_quant(S.lo[a][c], l, e, false) : 255u);
+            set_q(3 + a, c, c < S.m ? q4_quant(S.hi[a][c], l, e, true) : 0u);
         }
     }
-    QNode4 o;
-    o.org = make_float4(org[0], org[1], org[2], i2f((int)eb));
-    o.child = make_int4(ref[0], ref[1], ref[2], ref[3]);
-    o.q0 = make_uint4(ql[0], ql[1], ql[2], qh[0]);
-    o.q1 = make_uint2(qh[1], qh[2]);
-    o.pad = make_uint2(0u, 0u);
+    QNode6 o;
+    o.org = make_float4(org[0], org[1], org[2], i2f((int)(eb | inner << 24)));
+    o.a = make_uint4((uint32_t)inner_base, (uint32_t)tri_base, w[0], w[1]);
+    o.b = make_uint4(w[2], w[3], w[4], w[5]);
+    o.c = make_uint4(w[6], w[7], w[8], 0u);
     out[idx] = o;
 }
 
 // Next level: [hi, hi + total), triangle positions after this level's.
-__global__ void k_c4_advance(int32_t* __restrict__ ctl, int bound, const uint32_t* __restrict__ cnt,
+__global__ void k_qw_advance(int32_t* __restrict__ ctl, int bound, const uint32_t* __restrict__ cnt,
                              const uint32_t* __restrict__ tcnt) {
     const int hi = ctl[1];
     ctl[0] = hi;
@@ -560,7 +535,7 @@ constexpr int kPlocR = RR_PLOC_R;
 
 // cluster k: cl[2k] = (lo.xyz, ref bits), cl[2k+1] = (hi.xyz, leaves under it);
 // a PLOC node's d.z / d.w hold the leaf counts of its two children (the BVH4
-// collapse keeps subtrees of <= kLeafTris triangles as leaves)
+// collapse of an older round kept small subtrees as leaves; unused now)
 __device__ __forceinline__ float ploc_area(float4 alo, float4 ahi, float4 blo, float4 bhi) {
     const float dx = fmaxf(ahi.x, bhi.x) - fminf(alo.x, blo.x);
     const float dy = fmaxf(ahi.y, bhi.y) - fminf(alo.y, blo.y);
@@ -885,7 +860,7 @@ void DevScene::release() {
     tri_world.release(); bounds.release();
     for (int k = 0; k < 2; ++k) { keys[k].release(); vals[k].release(); }
     hist.release(); scan_part.release(); children.release(); node_parent.release();
-    leaf_parent.release(); flags.release(); nodes.release(); tris.release(); nodes4.release(); tris4.release(); q4_src.release(); q4_cnt.release(); q4_tcnt.release(); q4_ctl.release();
+    leaf_parent.release(); flags.release(); nodes.release(); tris.release(); qnodes.release(); qtris.release(); q_src.release(); q_cnt.release(); q_tcnt.release(); q_ctl.release();
     range.release();
     for (int k = 0; k < 2; ++k) ploc_cl[k].release();
     ploc_nn.release(); ploc_keep.release(); ploc_mrg.release(); ploc_ctl.release();
@@ -937,45 +912,45 @@ void build_ploc(DevScene& s, hipStream_t st) {
     }
 }
 
-// Quantised BVH4 of the built BVH2 (kernels above): one count / scan / emit /
+// Quantised 6-wide hierarchy of the built BVH2 (kernels above): one count / scan / emit /
 // advance round per level; the host learns the frontier size every 4 levels
 // (one synchronisation) and sizes the next launches by it (a level has at
-// most 4x the nodes of the one before).
-void build_bvh4(DevScene& s, hipStream_t st) {
+// most kQWidth x the nodes of the one before).
+void build_qbvh(DevScene& s, hipStream_t st) {
     const int n = s.n_tris;
     const int ni = n > 1 ? n - 1 : 1;
-    s.nodes4.ensure((size_t)ni);
-    s.tris4.ensure((size_t)n);
-    s.q4_src.ensure((size_t)ni);
-    s.q4_cnt.ensure((size_t)ni + 1);
-    s.q4_tcnt.ensure((size_t)ni + 1);
-    s.q4_ctl.ensure(3);
-    k_c4_init<<<1, 1, 0, st>>>(s.q4_ctl.ptr, s.q4_src.ptr);
+    s.qnodes.ensure((size_t)ni);
+    s.qtris.ensure((size_t)n);
+    s.q_src.ensure((size_t)ni);
+    s.q_cnt.ensure((size_t)ni + 1);
+    s.q_tcnt.ensure((size_t)ni + 1);
+    s.q_ctl.ensure(3);
+    k_qw_init<<<1, 1, 0, st>>>(s.q_ctl.ptr, s.q_src.ptr);
     long frontier = 1;  // bound on the current level's node count
     for (int level = 0;; ++level) {
         const int bound = (int)std::min<long>(frontier, ni);
-        k_c4_count<<<cdiv(bound + 1, kBlock), kBlock, 0, st>>>(s.q4_ctl.ptr, bound, n, s.nodes.ptr, s.q4_src.ptr,
-                                                                s.q4_cnt.ptr, s.q4_tcnt.ptr);
-        exclusive_scan(s, s.q4_cnt.ptr, bound + 1, st);
-        exclusive_scan(s, s.q4_tcnt.ptr, bound + 1, st);
-        k_c4_emit<<<cdiv(bound, kBlock), kBlock, 0, st>>>(s.q4_ctl.ptr, bound, n, s.nodes.ptr, s.q4_src.ptr,
-                                                           s.q4_cnt.ptr, s.q4_tcnt.ptr, s.tris.ptr, s.tris4.ptr,
-                                                           s.nodes4.ptr);
-        k_c4_advance<<<1, 1, 0, st>>>(s.q4_ctl.ptr, bound, s.q4_cnt.ptr, s.q4_tcnt.ptr);
-        frontier = std::min<long>(frontier * 4, ni);
+        k_qw_count<<<cdiv(bound + 1, kBlock), kBlock, 0, st>>>(s.q_ctl.ptr, bound, n, s.nodes.ptr, s.q_src.ptr,
+                                                                s.q_cnt.ptr, s.q_tcnt.ptr);
+        exclusive_scan(s, s.q_cnt.ptr, bound + 1, st);
+        exclusive_scan(s, s.q_tcnt.ptr, bound + 1, st);
+        k_qw_emit<<<cdiv(bound, kBlock), kBlock, 0, st>>>(s.q_ctl.ptr, bound, n, s.nodes.ptr, s.q_src.ptr,
+                                                           s.q_cnt.ptr, s.q_tcnt.ptr, s.tris.ptr, s.qtris.ptr,
+                                                           s.qnodes.ptr);
+        k_qw_advance<<<1, 1, 0, st>>>(s.q_ctl.ptr, bound, s.q_cnt.ptr, s.q_tcnt.ptr);
+        frontier = std::min<long>(frontier * kQWidth, ni);  // a level has at most kQWidth x the nodes of the one before
         if ((level & 3) == 3) {
             int ctl[2];
-            RR_HIP(hipMemcpyAsync(ctl, s.q4_ctl.ptr, sizeof ctl, hipMemcpyDeviceToHost, st));
+            RR_HIP(hipMemcpyAsync(ctl, s.q_ctl.ptr, sizeof ctl, hipMemcpyDeviceToHost, st));
             RR_HIP(hipStreamSynchronize(st));
             if (ctl[0] == ctl[1]) {
-                s.n4 = ctl[1];
+                s.nq = ctl[1];
                 break;
             }
             frontier = ctl[1] - ctl[0];
-            if (level > 4 * 4096) throw std::runtime_error("BVH4 collapse made no progress");
+            if (level > 4 * 4096) throw std::runtime_error("6-wide collapse made no progress");
         }
     }
-    std::swap(s.tris, s.tris4);  // the traversal and shading read the BVH4's leaf order
+    std::swap(s.tris, s.qtris);  // the traversal and shading read the 6-wide hierarchy's leaf order
     s.has4 = true;
 }
 
@@ -1048,7 +1023,7 @@ void build_lbvh(DevScene& s, hipStream_t st, KernelProfiler* prof, bool want4, b
         k_refit<<<nb, kBlock, 0, st>>>(n, s.vals[0].ptr, s.tri_world.ptr, s.tri_mat.ptr, s.leaf_parent.ptr,
                                        s.node_parent.ptr, s.children.ptr, s.flags.ptr, s.nodes.ptr,
                                        s.tris.ptr);
-    if (want4) build_bvh4(s, st);
+    if (want4) build_qbvh(s, st);
     if (prof) prof->end(st);
     RR_HIP(hipGetLastError());
     s.built = true;

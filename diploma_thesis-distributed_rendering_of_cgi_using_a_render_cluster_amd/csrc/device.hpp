@@ -70,13 +70,13 @@ struct DevScene {
     // acceleration structure consumed by traversal
     DevBuf<BvhNode> nodes;  // max(n-1, 1)
     DevBuf<TriPack> tris;   // n, leaf order (after a BVH4 collapse: the BVH4's leaf order)
-    DevBuf<QNode4> nodes4;     // quantised BVH4 collapse of `nodes` (split path), <= n-1
-    DevBuf<TriPack> tris4;     // collapse scratch: the triangles in the BVH4's leaf order (swapped into `tris`)
-    DevBuf<int32_t> q4_src;    // BVH4 node -> its BVH2 root (collapse scratch)
-    DevBuf<uint32_t> q4_cnt;   // per frontier node: internal children (scanned in place)
-    DevBuf<uint32_t> q4_tcnt;  // per frontier node: triangles of its leaf entries (scanned in place)
-    DevBuf<int32_t> q4_ctl;    // current level [lo, hi), first triangle of the level
-    int n4 = 0;                // BVH4 nodes
+    DevBuf<QNode6> qnodes;     // quantised 6-wide collapse of `nodes` (split path), <= n-1
+    DevBuf<TriPack> qtris;     // collapse scratch: the triangles in the collapse's leaf order (swapped into `tris`)
+    DevBuf<int32_t> q_src;     // wide node -> its BVH2 root (collapse scratch)
+    DevBuf<uint32_t> q_cnt;    // per frontier node: internal children (scanned in place)
+    DevBuf<uint32_t> q_tcnt;   // per frontier node: leaf children (scanned in place)
+    DevBuf<int32_t> q_ctl;     // current level [lo, hi), first triangle of the level
+    int nq = 0;                // wide nodes
     bool has4 = false;
     // PLOC build (large scenes): cluster ping-pong, neighbours, scan flags, counters
     DevBuf<float4> ploc_cl[2];

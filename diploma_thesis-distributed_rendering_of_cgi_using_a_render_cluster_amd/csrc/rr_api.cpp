@@ -276,8 +276,8 @@ void bind_scene(rr_ctx* c, rr_scene* s) {
 // asynchronous, so a frame can be enqueued while the previous one still runs.
 // Hierarchy ids (render_ints[7] of rr_debug_frame_state, rr_debug_trace):
 // 2 = Karras LBVH (BVH2), 3 = PLOC (BVH2), 4 = PLOC (LBVH below 3 triangles)
-// collapsed to the quantised BVH4 (rr_device.h QNode4).
-constexpr int kHierLbvh = 2, kHierPloc = 3, kHierBvh4 = 4;
+// collapsed to the quantised 6-wide hierarchy (rr_device.h QNode6).
+constexpr int kHierLbvh = 2, kHierPloc = 3, kHierQWide = 4;  // 4: the quantised 6-wide collapse (ABI value kept)
 
 FrameConsts make_consts(const FrameSetup& fs, int n_tris);
 
@@ -285,7 +285,7 @@ FrameConsts make_consts(const FrameSetup& fs, int n_tris);
 // (LDS-resident scenes), the quantised BVH4 for the split path (larger scenes,
 // and LDS-resident ones under RR_FLAG_WAVEFRONT).
 int frame_hier(const FrameSetup& fs, int n_tris) {
-    return frame_uses_tiles(make_consts(fs, n_tris), (fs.flags & RR_FLAG_WAVEFRONT) != 0) ? kHierLbvh : kHierBvh4;
+    return frame_uses_tiles(make_consts(fs, n_tris), (fs.flags & RR_FLAG_WAVEFRONT) != 0) ? kHierLbvh : kHierQWide;
 }
 
 // The view transform a frame on ctx is rendered with: Filmic needs the
@@ -347,8 +347,8 @@ bool prepare_frame(rr_ctx* c, rr_scene* s, const FrameSetup& fs, PinnedBuf& stag
     std::memcpy(up + nl + nm, fs.obj_xform.data(), nx * sizeof(float));
     DevScene& d = s->dev;
     if (hier == 0) hier = frame_hier(fs, d.n_tris);
-    const bool want4 = hier == kHierBvh4;
-    const bool want_ploc = (hier == kHierPloc || hier == kHierBvh4) && d.n_tris > 2;
+    const bool want4 = hier == kHierQWide;
+    const bool want_ploc = (hier == kHierPloc || hier == kHierQWide) && d.n_tris > 2;
     // (a BVH4 collapse reorders the triangles into its leaf order, so a BVH2
     // walk of the same PLOC tree needs a build without it)
     const bool rebuild = !d.built || d.cached_xform != fs.obj_xform || (want4 != d.has4) || (want_ploc != d.ploc);
@@ -1181,38 +1181,41 @@ int rr_debug_bvh_hier(rr_ctx* c, rr_scene* s, int32_t frame, int32_t hier, uint3
     });
 }
 
-int rr_debug_bvh4(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* n4, int32_t* children4, uint32_t* nodes16,
+int rr_debug_qbvh(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* nq, int32_t* children, uint32_t* nodes16,
                   int32_t* tri_orig) {
-    if (!c || !s || !n4) return fail(RR_EINVAL, "NULL ctx, scene or n4");
+    if (!c || !s || !nq) return fail(RR_EINVAL, "NULL ctx, scene or nq");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
         PinnedBuf staging;
-        prepare_frame(c, s, fs, staging, kHierBvh4);
+        prepare_frame(c, s, fs, staging, kHierQWide);
         DevScene& d = s->dev;
         hipStream_t st = c->stream;
         const int n = d.n_tris;
-        *n4 = 0;
+        *nq = 0;
         if (n > 0) {
-            const uint32_t cnt = (uint32_t)d.n4;
-            *n4 = (int32_t)cnt;
-            if (children4 || nodes16) {
-                std::vector<QNode4> nodes(cnt);
-                RR_HIP(hipMemcpyAsync(nodes.data(), d.nodes4.ptr, cnt * sizeof(QNode4), hipMemcpyDeviceToHost, st));
+            const uint32_t cnt = (uint32_t)d.nq;
+            *nq = (int32_t)cnt;
+            if (children || nodes16) {
+                std::vector<QNode6> nodes(cnt);
+                RR_HIP(hipMemcpyAsync(nodes.data(), d.qnodes.ptr, cnt * sizeof(QNode6), hipMemcpyDeviceToHost, st));
                 RR_HIP(hipStreamSynchronize(st));
                 for (uint32_t i = 0; i < cnt; ++i) {
-                    const QNode4& q = nodes[i];
-                    if (children4) {
-                        children4[4 * i] = q.child.x;
-                        children4[4 * i + 1] = q.child.y;
-                        children4[4 * i + 2] = q.child.z;
-                        children4[4 * i + 3] = q.child.w;
+                    const QNode6& q = nodes[i];
+                    if (children) {  // the implicit references, spelled out (unused slots: 0x7fffffff)
+                        const uint32_t eb = (uint32_t)f2i(q.org.w);
+                        for (int k = 0; k < kQWidth; ++k) {
+                            const uint32_t lox = k < 4 ? (q.a.z >> (8 * k)) & 255u : (q.c.x >> (8 * (k - 4))) & 255u;
+                            const uint32_t hix = k < 4 ? (q.b.y >> (8 * k)) & 255u : (q.c.y >> (16 + 8 * (k - 4))) & 255u;
+                            const bool unused = lox == 255u && hix == 0u && !((eb >> (24 + k)) & 1u);
+                            children[kQWidth * (size_t)i + k] = unused ? 0x7fffffff : q6_ref(q, k);
+                        }
                     }
-                    if (nodes16) std::memcpy(nodes16 + 16 * (size_t)i, &q, sizeof(QNode4));
+                    if (nodes16) std::memcpy(nodes16 + 16 * (size_t)i, &q, sizeof(QNode6));
                 }
             }
-            if (tri_orig) {  // original id of each position of the BVH4's triangle array
+            if (tri_orig) {  // original id of each position of the hierarchy's triangle array
                 std::vector<TriPack> tp((size_t)n);
                 RR_HIP(hipMemcpyAsync(tp.data(), d.tris.ptr, (size_t)n * sizeof(TriPack), hipMemcpyDeviceToHost, st));
                 RR_HIP(hipStreamSynchronize(st));
@@ -1235,7 +1238,7 @@ int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int
         PinnedBuf staging;
         const int hier = bvh_width ? bvh_width : frame_hier_of(s, fs);
         prepare_frame(c, s, fs, staging, hier);
-        const int width = hier == kHierBvh4 ? 4 : 2;
+        const int width = hier == kHierQWide ? 4 : 2;
         hipStream_t st = c->stream;
         DevBuf<float4> dr, dh;
         DevBuf<int32_t> dp;

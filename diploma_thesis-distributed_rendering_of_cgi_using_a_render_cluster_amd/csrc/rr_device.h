@@ -35,27 +35,38 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "node must be one 64-byte line");
 
-// Quantised 4-wide node, the hierarchy of scenes traversed from HBM (split
-// path): the PLOC BVH2 collapsed two levels at a time (every
-// even-depth BVH2 node becomes one node whose children are its grandchildren,
-// or its leaf children), with the four child boxes stored as 8-bit offsets on
-// a per-node grid: child lo/hi = org + q * 2^e per axis, q rounded outwards
+// Quantised 6-wide node, the hierarchy of scenes traversed from HBM (split
+// path): the PLOC BVH2 collapsed top down (each node's children
+// start as its BVH2 root's two children and the largest internal one is opened
+// until there are six), with the six child boxes stored as 8-bit offsets on a
+// per-node grid: child lo/hi = org + q * 2^e per axis, q rounded outwards
 // (exactly, in double, at build time), so each quantised box contains the
-// child's box. 64 B per node: one BVH4 visit costs the bytes of one BVH2
-// visit and replaces up to three of them.
+// child's box. Child references are implicit: the internal children of a node
+// are consecutive nodes (breadth-first numbering) and its leaf children are
+// consecutive triangles of the hierarchy's own triangle array (one triangle
+// per leaf), both in slot order, so a node stores two bases and a mask and
+// six children fit one 64-byte line (a 4-wide node with explicit links did
+// too; six children per fetch take about a quarter fewer node visits per ray).
 //   org.xyz  grid origin = the node box's lo corner
-//   org.w    exponent bytes (ex + 128) | (ey + 128) << 8 | (ez + 128) << 16
-//   child    >= 0 node, < 0 ~leaf, kEmpty4 unused slot (q lo 255, hi 0)
-//   q0       lo x | lo y | lo z | hi x, q1: hi y | hi z (child c in byte c)
-struct alignas(16) QNode4 {
+//   org.w    exponent bytes (ex + 128) | (ey + 128) << 8 | (ez + 128) << 16 | inner mask << 24
+//   a        x: first internal child's node index, y: first leaf child's
+//            triangle position, z / w: lo x / lo y of children 0..3 (byte c)
+//   b        lo z, hi x, hi y, hi z of children 0..3 (byte c)
+//   c        children 4, 5 as byte pairs: x (lo x, lo y), y (lo z, hi x), z (hi y, hi z), w 0
+// An unused slot has lo 255 and hi 0 on every axis: its box test always
+// fails. oracle/rr_oracle.c q4_pack / trace4 restate the layout and the walk.
+constexpr int kQWidth = 6;
+struct alignas(16) QNode6 {
     float4 org;
-    int4 child;
-    uint4 q0;
-    uint2 q1;
-    uint2 pad;
+    uint4 a, b, c;
 };
-static_assert(sizeof(QNode4) == 64, "quantised BVH4 node is 64 bytes");
-constexpr int kEmpty4 = 0x7fffffff;
+static_assert(sizeof(QNode6) == 64, "quantised 6-wide node is 64 bytes");
+RR_HD uint32_t q6_inner(const QNode6& n) { return (uint32_t)__builtin_bit_cast(int, n.org.w) >> 24; }
+// child c's reference: >= 0 internal node, < 0 ~triangle position
+RR_HD int q6_ref(const QNode6& n, int c) {
+    const uint32_t inner = q6_inner(n), below = inner & ((1u << c) - 1u);
+    return ((inner >> c) & 1u) ? (int)n.a.x + __builtin_popcount(below) : ~((int)n.a.y + (c - __builtin_popcount(below)));
+}
 constexpr int kQExpMin = -64, kQExpMax = 100;
 
 // Smallest e in [kQExpMin, kQExpMax] with 255 * 2^e >= ext (ext >= 0).
@@ -574,75 +585,79 @@ struct TravState {
     }
 };
 
-RR_D int i4get(const int4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
-
-// The four child box tests of a quantised node for one ray (iq: q4_rcp of the
-// direction): bit c set when child c exists and its box meets [tmin, tcur];
-// tn[c] = the entry distance. Per axis s = iq * 2^e (exact), o' = (org - o) *
-// iq; a plane at grid coordinate q lies at t = fma(q, s, o'); the near plane is
-// lo for iq >= 0, else hi (iq is never 0 or inf, so no NaN and no min/max per
-// axis). oracle/rr_oracle.c trace4() restates it.
-RR_D uint32_t q4_box_hits(const float4& org, const int4& ch, const uint4& q0, const uint2& q1, float3 o, float3 iq,
-                          float tmin, float tcur, float tn[4]) {
-    const uint32_t eb = (uint32_t)f2i(org.w);
+// The six child box tests of a quantised node for one ray (iq: q4_rcp of the
+// direction): bit c set when child c's box meets [tmin, tcur] (never for an
+// unused slot); tn[c] = the entry distance. Per axis s = iq * 2^e (exact),
+// o' = (org - o) * iq; a plane at grid coordinate q lies at t = fma(q, s, o');
+// the near plane is lo for iq >= 0, else hi (iq is never 0 or inf, so no NaN
+// and no min/max per axis). oracle/rr_oracle.c trace4() restates it.
+RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, float tn[kQWidth]) {
+    const uint32_t eb = (uint32_t)f2i(n.org.w);
     const float sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
     const float sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
     const float sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
-    const float ox = (org.x - o.x) * iq.x, oy = (org.y - o.y) * iq.y, oz = (org.z - o.z) * iq.z;
+    const float ox = (n.org.x - o.x) * iq.x, oy = (n.org.y - o.y) * iq.y, oz = (n.org.z - o.z) * iq.z;
     const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
-    const uint32_t nx = px ? q0.x : q0.w, fx = px ? q0.w : q0.x;
-    const uint32_t ny = py ? q0.y : q1.x, fy = py ? q1.x : q0.y;
-    const uint32_t nz = pz ? q0.z : q1.y, fz = pz ? q1.y : q0.z;
+    // children 0..3: one byte each of the near / far words per axis
+    const uint32_t nx = px ? n.a.z : n.b.y, fx = px ? n.b.y : n.a.z;
+    const uint32_t ny = py ? n.a.w : n.b.z, fy = py ? n.b.z : n.a.w;
+    const uint32_t nz = pz ? n.b.x : n.b.w, fz = pz ? n.b.w : n.b.x;
+    // children 4, 5: the byte pairs in the low / high halves of c.x .. c.z
+    const uint32_t lox = n.c.x & 0xffffu, loy = n.c.x >> 16, loz = n.c.y & 0xffffu;
+    const uint32_t hix = n.c.y >> 16, hiy = n.c.z & 0xffffu, hiz = n.c.z >> 16;
+    const uint32_t nx2 = px ? lox : hix, fx2 = px ? hix : lox;
+    const uint32_t ny2 = py ? loy : hiy, fy2 = py ? hiy : loy;
+    const uint32_t nz2 = pz ? loz : hiz, fz2 = pz ? hiz : loz;
     uint32_t hits = 0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int sh = 8 * c;
-        const float t0 = fmaxf(fmaxf(fmaf((float)((nx >> sh) & 255u), sx, ox), fmaf((float)((ny >> sh) & 255u), sy, oy)),
-                               fmaxf(fmaf((float)((nz >> sh) & 255u), sz, oz), tmin));
-        const float t1 = fminf(fminf(fmaf((float)((fx >> sh) & 255u), sx, ox), fmaf((float)((fy >> sh) & 255u), sy, oy)),
-                               fminf(fmaf((float)((fz >> sh) & 255u), sz, oz), tcur));
+    for (int c = 0; c < kQWidth; ++c) {
+        const int sh = c < 4 ? 8 * c : 8 * (c - 4);
+        const uint32_t qnx = c < 4 ? nx : nx2, qny = c < 4 ? ny : ny2, qnz = c < 4 ? nz : nz2;
+        const uint32_t qfx = c < 4 ? fx : fx2, qfy = c < 4 ? fy : fy2, qfz = c < 4 ? fz : fz2;
+        const float t0 = fmaxf(fmaxf(fmaf((float)((qnx >> sh) & 255u), sx, ox), fmaf((float)((qny >> sh) & 255u), sy, oy)),
+                               fmaxf(fmaf((float)((qnz >> sh) & 255u), sz, oz), tmin));
+        const float t1 = fminf(fminf(fmaf((float)((qfx >> sh) & 255u), sx, ox), fmaf((float)((qfy >> sh) & 255u), sy, oy)),
+                               fminf(fmaf((float)((qfz >> sh) & 255u), sz, oz), tcur));
         tn[c] = t0;
-        if (i4get(ch, c) != kEmpty4 && t0 <= t1) hits |= 1u << c;
+        if (t0 <= t1) hits |= 1u << c;
     }
     return hits;
 }
 
-// Node fetch of the BVH4 walk. The split-path trace kernels keep a copy of
-// the first n_top nodes in LDS (Q4Nodes): nodes are numbered breadth first,
+// Node fetch of the 6-wide walk. The split-path trace kernels keep a copy of
+// the first n_top nodes in LDS (Q6Nodes): nodes are numbered breadth first,
 // so those are the top levels of the tree, which every ray visits — each of
 // those visits becomes a ds_read instead of an L2 round trip. Which copy a
 // node comes from changes no bit of it.
-RR_D void q4_load(const QNode4* __restrict__ nodes, int i, float4& org, int4& ch, uint4& q0, uint2& q1) {
-    const QNode4* p = nodes + i;
-    org = p->org;
-    ch = p->child;
-    q0 = p->q0;
-    q1 = p->q1;
-}
-struct Q4Nodes {
-    const QNode4* __restrict__ g;
-    lds_f4w* top;  // nodes [0, n_top): 4 float4 each (QNode4 layout)
+RR_D QNode6 q6_load(const QNode6* __restrict__ nodes, int i) { return nodes[i]; }
+struct Q6Nodes {
+    const QNode6* __restrict__ g;
+    lds_f4w* top;  // nodes [0, n_top): 4 float4 each (QNode6 layout)
     int n_top;
 };
-RR_D void q4_load(const Q4Nodes& n, int i, float4& org, int4& ch, uint4& q0, uint2& q1) {
+RR_D uint4 f4_bits(float4 v) {
+    return make_uint4((uint32_t)f2i(v.x), (uint32_t)f2i(v.y), (uint32_t)f2i(v.z), (uint32_t)f2i(v.w));
+}
+RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
     if (i < n.n_top) {
         const lds_f4w* q = n.top + 4 * i;
-        org = lds_ld4(q);
-        const float4 c = lds_ld4(q + 1), a = lds_ld4(q + 2), b = lds_ld4(q + 3);
-        ch = make_int4(f2i(c.x), f2i(c.y), f2i(c.z), f2i(c.w));
-        q0 = make_uint4((uint32_t)f2i(a.x), (uint32_t)f2i(a.y), (uint32_t)f2i(a.z), (uint32_t)f2i(a.w));
-        q1 = make_uint2((uint32_t)f2i(b.x), (uint32_t)f2i(b.y));
-    } else {
-        q4_load(n.g, i, org, ch, q0, q1);
+        QNode6 r;
+        r.org = lds_ld4(q);
+        r.a = f4_bits(lds_ld4(q + 1));
+        r.b = f4_bits(lds_ld4(q + 2));
+        r.c = f4_bits(lds_ld4(q + 3));
+        return r;
     }
+    return q6_load(n.g, i);
 }
 
-// Resumable traversal of the quantised BVH4 (same contract as TravState), box
-// tests by q4_box_hits. Leaf children whose boxes pass are intersected at once in slot order; the
-// nearest hit internal child is visited next and the others are pushed in
-// descending slot order. oracle/rr_oracle.c trace4() is the same walk.
+// Resumable traversal of the quantised 6-wide hierarchy (same contract as
+// TravState), box tests by q6_box_hits. Leaf children whose boxes pass are
+// intersected at once in slot order; the nearest hit internal child is
+// visited next and the others are pushed in descending slot order.
+// oracle/rr_oracle.c trace4() is the same walk.
 template <bool kAnyHit, bool kCount = false>
-struct TravStateQ4 {
+struct TravStateQ6 {
     float3 o, d, iq;
     float tmin;
     Hit h;
@@ -662,37 +677,21 @@ struct TravStateQ4 {
     RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
         if (kCount) ++cnt.nodes;
         const float tcur = h.t;
-        float tn[4];
-        int ref[4];
-        uint32_t leaves = 0, inner = 0;
-        {
-            float4 org;
-            int4 ch;
-            uint4 q0;
-            uint2 q1;
-            q4_load(nodes, node, org, ch, q0, q1);
-            const uint32_t hm = q4_box_hits(org, ch, q0, q1, o, iq, tmin, tcur, tn);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                ref[c] = i4get(ch, c);
-                if ((hm >> c) & 1u) {
-                    if (ref[c] < 0) leaves |= 1u << c;
-                    else inner |= 1u << c;
-                }
-            }
-        }
+        float tn[kQWidth];
+        const QNode6 nd = q6_load(nodes, node);
+        const uint32_t hm = q6_box_hits(nd, o, iq, tmin, tcur, tn);
+        const uint32_t imask = q6_inner(nd);
+        uint32_t leaves = hm & ~imask;
+        const uint32_t inner = hm & imask;
         // passing leaves in slot order; the loop runs as often as the lane with
-        // the most leaves needs (usually once), not once per slot
+        // the most leaves needs, not once per slot
         while (leaves) {
             const int c = __builtin_ctz(leaves);
             leaves &= leaves - 1;
-            const int r = c == 0 ? ref[0] : c == 1 ? ref[1] : c == 2 ? ref[2] : ref[3];
-            const int f = leaf_first(r), m = leaf_count(r);
-            for (int q = 0; q < m; ++q) {
-                if (kCount) ++cnt.tris;
-                leaf_test(load_tri(tris, f + q), f + q, o, d, tmin, h);
-                if (kAnyHit && h.idx >= 0) return true;
-            }
+            const int ti = (int)nd.a.y + c - __builtin_popcount(imask & ((1u << c) - 1u));
+            if (kCount) ++cnt.tris;
+            leaf_test(load_tri(tris, ti), ti, o, d, tmin, h);
+            if (kAnyHit && h.idx >= 0) return true;
         }
         if (!inner) {
             if (st.sp == 0) return true;
@@ -702,19 +701,22 @@ struct TravStateQ4 {
         // nearest hit child next (ties: lower slot); the other hit children are
         // pushed in descending slot order (so they pop in slot order)
         int best = __builtin_ctz(inner);
-        float bt = tn[best == 0 ? 0 : best == 1 ? 1 : best == 2 ? 2 : 3];
+        float bt = tn[0];
 #pragma unroll
-        for (int c = 1; c < 4; ++c)
-            if (((inner >> c) & 1u) && tn[c] < bt) {
+        for (int c = 1; c < kQWidth; ++c)
+            if (best == c) bt = tn[c];
+#pragma unroll
+        for (int c = 1; c < kQWidth; ++c)
+            if (((inner >> c) & 1u) && c > best && tn[c] < bt) {
                 bt = tn[c];
                 best = c;
             }
         const uint32_t rest = inner & ~(1u << best);
-        if (rest & 8u) st.push(ref[3]);
-        if (rest & 4u) st.push(ref[2]);
-        if (rest & 2u) st.push(ref[1]);
-        if (rest & 1u) st.push(ref[0]);
-        node = best == 0 ? ref[0] : best == 1 ? ref[1] : best == 2 ? ref[2] : ref[3];
+        const int base = (int)nd.a.x;
+#pragma unroll
+        for (int c = kQWidth - 1; c >= 0; --c)
+            if ((rest >> c) & 1u) st.push(base + __builtin_popcount(imask & ((1u << c) - 1u)));
+        node = base + __builtin_popcount(imask & ((1u << best) - 1u));
         return false;
     }
 };

@@ -391,14 +391,14 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
 }  // namespace
 struct SceneArgs {
     const BvhNode* nodes;
-    const QNode4* nodes4;    // quantised BVH4 (split path)
+    const QNode6* qnodes;    // quantised 6-wide hierarchy (split path)
     const TriPack* tris;
     const float* mats;
     const float* lights;
     const float* filter;
     const float* mat_lut;    // kMatLutStride floats per material
     int n_nodes, n_tris, n_mats, n_lights;
-    int n_nodes4;            // quantised BVH4 nodes (split path)
+    int n_qnodes;            // its node count
 };
 
 namespace {
@@ -676,18 +676,21 @@ constexpr int kRefillBelow = RR_REFILL_BELOW;
 // 8 against 7 measured 02 / 03 frames at 64 spp -3.7 / -3.8 %, C5 at 16 spp
 // -2.7 % (with the quantised BVH4 and windowed ray order; over round 1's
 // BVH2 walk C5 had been slower at 8, 102 -> 113 ms).
-constexpr int kTraceWaves = 8;
+#ifndef RR_TRACE_WAVES
+#define RR_TRACE_WAVES 8
+#endif
+constexpr int kTraceWaves = RR_TRACE_WAVES;
 // Hierarchy of the split path: the PLOC BVH2 collapsed to the quantised BVH4
 // (measured against walking the PLOC BVH2 itself, C5 / 02 / 03 frames at 16 /
 // 64 / 64 spp: 191 -> 139, 174 -> 149, 192 -> 160 ms).
 template <bool kAnyHit, bool kCount>
-using SplitTrav = TravStateQ4<kAnyHit, kCount>;
+using SplitTrav = TravStateQ6<kAnyHit, kCount>;
 constexpr int kQGroups = 64;   // append groups per queue (one lane each in QueueMap)
 constexpr int kQStride = 32;   // words between group counters (128 B)
 
 // map(k) -> slot is called by every lane of the wave (converged: QueueMap
 // shuffles); ray_of(slot, ...) and done(k, slot, hit) per lane.
-// TS: TravStateQ4<kAnyHit, kCount> (quantised BVH4) or TravState (BVH2).
+// TS: TravStateQ6<kAnyHit, kCount> (quantised 6-wide hierarchy) or TravState (BVH2).
 // Positions 0..count-1 are dealt to the waves in chunks of 64, round-robin
 // (wave w: chunks w, w + waves, ...), so at any time the rays in flight on the
 // whole chip come from one window of about 64 x waves positions: for camera
@@ -706,7 +709,7 @@ RR_D int xcd_wave_rank() {
     return __builtin_amdgcn_readfirstlane((xcd * (G >> 3) + min(xcd, G & 7) + (bx >> 3)) * kWavesPerBlock +
                                           (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
 }
-// Top of the quantised BVH4 in LDS for the trace kernels (Q4Nodes): the
+// Top of the quantised hierarchy in LDS for the trace kernels (Q6Nodes): the
 // first kTopNodes nodes (breadth-first numbering: the four top levels, 85
 // nodes, and part of the fifth), copied by the block at launch. 128 nodes =
 // 8 KB beside the 12 KB traversal stack (kLdsStack) keeps 8 blocks of 256
@@ -718,13 +721,13 @@ RR_D int xcd_wave_rank() {
 #define RR_TOP_NODES 128
 #endif
 constexpr int kTopNodes = RR_TOP_NODES;
-RR_D Q4Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
+RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
     lds_f4w* top = (lds_f4w*)top_shared;
-    const int n = kTopNodes > 0 ? min(sa.n_nodes4, kTopNodes) : 0;
-    const rr_f4v* src = reinterpret_cast<const rr_f4v*>(sa.nodes4);
+    const int n = kTopNodes > 0 ? min(sa.n_qnodes, kTopNodes) : 0;
+    const rr_f4v* src = reinterpret_cast<const rr_f4v*>(sa.qnodes);
     for (int i = threadIdx.x; i < 4 * n; i += kBlock) top[i] = src[i];
     __syncthreads();
-    return Q4Nodes{sa.nodes4, top, n};
+    return Q6Nodes{sa.qnodes, top, n};
 }
 template <typename TS, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack& st, TravCount& cnt, MapFn&& map,
@@ -872,7 +875,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameCons
                                                                           uint32_t* __restrict__ traced) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const Q4Nodes nodes = stage_top(sa, top_nodes);
+    const Q6Nodes nodes = stage_top(sa, top_nodes);
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
@@ -910,41 +913,36 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameCons
 // shadow rays of camera hits (per-lane 39.7 / 46.8 ms, packets 121 / 86 ms on
 // C5 / 02) are not coherent enough for it at all.
 // act: the lane has a ray; stk: this wave's kPacketStack LDS entries.
-constexpr int kPacketStack = 128;  // a node pushes <= 3: bounded by 3 x the BVH4 depth
+constexpr int kPacketStack = 128;  // a node pushes <= 5: bounded by 5 x the hierarchy depth
 template <bool kCount>
-RR_D void packet_trace(const QNode4* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk, bool act,
+RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk, bool act,
                        float3 o, float3 d, float tmin, Hit& h, TravCount& cnt) {
     if (!__ballot(act)) return;
     const float3 iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
     int node = 0, sp = 0;
     for (;;) {
         const bool live = act;
-        const QNode4* p = nodes + node;
-        const int4 ch = p->child;
-        float tn[4];
-        const uint32_t hm = live ? q4_box_hits(p->org, ch, p->q0, p->q1, o, iq, tmin, h.t, tn) : 0u;
+        const QNode6 nd = nodes[node];  // wave-uniform: scalar loads
+        const uint32_t imask = q6_inner(nd);
+        float tn[kQWidth];
+        const uint32_t hm = live ? q6_box_hits(nd, o, iq, tmin, h.t, tn) : 0u;
         if (kCount && live) ++cnt.nodes;
         // leaf children in slot order (a lane tests those its ray enters)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int r = i4get(ch, c);
-            if (r >= 0 || r == kEmpty4 || !__ballot((hm >> c) & 1u)) continue;
-            const int f = leaf_first(r), m = leaf_count(r);
-            for (int k = 0; k < m; ++k) {
-                const TriPack tp = load_tri(tris, f + k);
-                if ((hm >> c) & 1u) {
-                    if (kCount) ++cnt.tris;
-                    leaf_test(tp, f + k, o, d, tmin, h);
-                }
+        for (int c = 0; c < kQWidth; ++c) {
+            if (((imask >> c) & 1u) || !__ballot((hm >> c) & 1u)) continue;
+            const int ti = (int)nd.a.y + c - __builtin_popcount(imask & ((1u << c) - 1u));
+            const TriPack tp = load_tri(tris, ti);
+            if ((hm >> c) & 1u) {
+                if (kCount) ++cnt.tris;
+                leaf_test(tp, ti, o, d, tmin, h);
             }
         }
         // internal children some lane enters: the representative lane's nearest next
         uint32_t inner = 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int r = i4get(ch, c);
-            if (r >= 0 && r != kEmpty4 && __ballot((hm >> c) & 1u)) inner |= 1u << c;
-        }
+        for (int c = 0; c < kQWidth; ++c)
+            if (((imask >> c) & 1u) && __ballot((hm >> c) & 1u)) inner |= 1u << c;
         if (!inner) {
             if (sp == 0) break;
             node = __builtin_amdgcn_readfirstlane(stk[--sp]);
@@ -956,7 +954,7 @@ RR_D void packet_trace(const QNode4* __restrict__ nodes, const TriPack* __restri
         int best = -1;
         float bt = 0.0f;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < kQWidth; ++c) {
             if (!((inner >> c) & 1u)) continue;
             const float tc = ((rh >> c) & 1u)
                                  ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tn[c]), rl))
@@ -966,10 +964,12 @@ RR_D void packet_trace(const QNode4* __restrict__ nodes, const TriPack* __restri
                 bt = tc;
             }
         }
+        const int base = (int)nd.a.x;
 #pragma unroll
-        for (int c = 3; c >= 0; --c)
-            if (c != best && ((inner >> c) & 1u) && sp < kPacketStack) stk[sp++] = i4get(ch, c);  // never full here
-        node = __builtin_amdgcn_readfirstlane(i4get(ch, best));
+        for (int c = kQWidth - 1; c >= 0; --c)
+            if (c != best && ((inner >> c) & 1u) && sp < kPacketStack)  // never full here
+                stk[sp++] = base + __builtin_popcount(imask & ((1u << c) - 1u));
+        node = __builtin_amdgcn_readfirstlane(base + __builtin_popcount(imask & ((1u << best) - 1u)));
     }
 }
 
@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         n_traced += valid && !culled ? 1u : 0u;
         Hit h;
         set_miss(h, tmax);
-        packet_trace<kCount>(sa.nodes4, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt);
+        packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt);
         if (valid) hits[(size_t)sl * fc.npix + pix] = pack_hit(h);
     }
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_extend(SceneArgs 
                                                                          unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const Q4Nodes nodes = stage_top(sa, top_nodes);
+    const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_shadow_refill(SceneArgs
                                                                           unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const Q4Nodes nodes = stage_top(sa, top_nodes);
+    const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
@@ -1740,7 +1740,7 @@ __global__ void k_debug_bsdf(const float* __restrict__ mat12, const float* __res
     ok[i] = good ? (glossy ? 2 : 1) : 0;
 }
 
-__global__ void k_debug_trace4(const QNode4* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
+__global__ void k_debug_trace4(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
                                int n, const float4* __restrict__ rays, float4* __restrict__ hits,
                                int32_t* __restrict__ prims, uint8_t* __restrict__ occ,
                                int32_t* __restrict__ spill) {
@@ -1751,7 +1751,7 @@ __global__ void k_debug_trace4(const QNode4* __restrict__ nodes, const TriPack* 
     TravCount cnt;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
-        TravStateQ4<false> ts;
+        TravStateQ6<false> ts;
         ts.start(xyz(o), xyz(d), o.w, d.w);
         st.sp = 0;
         if (n_tris > 0)
@@ -1759,7 +1759,7 @@ __global__ void k_debug_trace4(const QNode4* __restrict__ nodes, const TriPack* 
             }
         hits[i] = make_float4(ts.h.t, ts.h.u, ts.h.v, 0.0f);
         prims[i] = ts.h.orig;
-        TravStateQ4<true> ta;
+        TravStateQ6<true> ta;
         ta.start(xyz(o), xyz(d), o.w, d.w);
         st.sp = 0;
         if (n_tris > 0)
@@ -1954,7 +1954,10 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
     const int cpc = counters_per_chunk(base.max_bounces);
     // camera rays as packets (packet_trace) when triangles are large on screen:
     // at most one triangle per two pixels (02 / 03 yes, C5 no)
-    const bool packets = (long)base.n_tris * 2 <= (long)npix;
+#ifndef RR_PACKET_TRIS_PER_PIXEL_HALF
+#define RR_PACKET_TRIS_PER_PIXEL_HALF 1
+#endif
+    const bool packets = RR_PACKET_TRIS_PER_PIXEL_HALF && (long)base.n_tris * 2 <= (long)npix;
     // group counters: [chunk][bounce 0..max][path | shadow][kQGroups * kQStride]
     const size_t per_q = (size_t)kQGroups * kQStride;
     const size_t per_chunk = (size_t)(base.max_bounces + 1) * 2 * per_q;
@@ -2029,8 +2032,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
             RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, kTravWords * sizeof(unsigned long long), st));
             tc = p.trav_counts.ptr;
         }
-        const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
-                           p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.n4};
+        const SceneArgs sa{s.nodes.ptr, s.qnodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
+                           p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.nq};
         FrameConsts fc = base;
         fc.first_sample = 0;
         fc.spp_chunk = base.spp_total;
@@ -2089,8 +2092,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     }
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
-    const SceneArgs sa{s.nodes.ptr, s.nodes4.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
-                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.n4};
+    const SceneArgs sa{s.nodes.ptr, s.qnodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
+                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.nq};
     render_split(p, base, n_chunks, st, sa, tc, pq, sq);
     RR_HIP(hipGetLastError());
 }
@@ -2147,7 +2150,7 @@ void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, f
     if (width == 4) {
         if (!s.has4) throw std::runtime_error("BVH4 not built");
         if (n > 0)
-            k_debug_trace4<<<g, kBlock, 0, st>>>(s.nodes4.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,
+            k_debug_trace4<<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,
                                                  p.spill.ptr);
     } else if (n > 0)
         k_debug_trace<<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,

@@ -21,7 +21,8 @@ RR_OK, RR_ENOENT, RR_EIO, RR_ENOMEM, RR_ENODEV, RR_EINVAL, RR_ENOTSUP = 0, -2, -
 RR_EBUSY = -16
 RR_MAX_FRAMES_IN_FLIGHT = 3
 RR_VIEW_SCENE, RR_VIEW_STANDARD, RR_VIEW_RAW, RR_VIEW_FILMIC = -1, 0, 1, 2
-RR_ABI_VERSION = 5
+RR_ABI_VERSION = 6
+QWIDTH = 6  # children per quantised node of the split path (rr_device.h kQWidth)
 RR_CAM_FLOATS, RR_LIGHT_FLOATS, RR_MAT_FLOATS, RR_RENDER_INTS, RR_RENDER_FLOATS = 16, 12, 12, 10, 4
 
 
@@ -81,7 +82,7 @@ EXPORTS = [
     "rr_render_frame_to_memory", "rr_scene_resolution", "rr_encode_image", "rr_last_error",
     "rr_last_warning", "rr_set_ocio_config", "rr_synchronize",
     "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
-    "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_bvh4", "rr_debug_bvh_hier", "rr_debug_jpeg_device",
+    "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_qbvh", "rr_debug_bvh_hier", "rr_debug_jpeg_device",
     "rr_debug_bsdf_sample", "rr_debug_fastmath_check",
 ]
 
@@ -131,7 +132,7 @@ def lib() -> ctypes.CDLL:
                                          f32p, i32p, f32p]),
         "rr_debug_bvh": (c_int, [P, P, i32, u32p, u32p, i32p, f32p]),
         "rr_debug_trace": (c_int, [P, P, i32, i32, i32, f32p, f32p, i32p, u8p]),
-        "rr_debug_bvh4": (c_int, [P, P, i32, i32p, i32p, u32p, i32p]),
+        "rr_debug_qbvh": (c_int, [P, P, i32, i32p, i32p, u32p, i32p]),
         "rr_debug_bvh_hier": (c_int, [P, P, i32, i32, u32p, u32p, i32p, f32p]),
         "rr_debug_jpeg_device": (c_int, [P, u8p, i32, i32, i32, u8p, ctypes.c_uint64,
                                          ctypes.POINTER(ctypes.c_uint64)]),
@@ -348,21 +349,22 @@ class RenderContext:
                                   _ptr(boxes, ctypes.c_float)), self.handle)
         return keys, order, children, boxes
 
-    def bvh4(self, scene: Scene, frame: int, with_order: bool = False):
-        """rr_debug_bvh4: (children4 (n4,4), nodes (n4,16) uint32: the raw 64-byte
-        quantised nodes, rr_device.h QNode4); with_order: also the original
-        triangle id at each position of the BVH4's triangle array."""
-        n4 = ctypes.c_int32()
-        _check(lib().rr_debug_bvh4(self.handle, scene.handle, int(frame), ctypes.byref(n4), None, None, None),
+    def qbvh(self, scene: Scene, frame: int, with_order: bool = False):
+        """rr_debug_qbvh: (children (nq, QWIDTH) with the implicit references
+        spelled out, nodes (nq, 16) uint32: the raw 64-byte quantised nodes,
+        rr_device.h QNode6); with_order: also the original triangle id at each
+        position of the hierarchy's triangle array."""
+        nq = ctypes.c_int32()
+        _check(lib().rr_debug_qbvh(self.handle, scene.handle, int(frame), ctypes.byref(nq), None, None, None),
                self.handle)
-        ch = np.zeros((max(n4.value, 1), 4), np.int32)
-        bx = np.zeros((max(n4.value, 1), 16), np.uint32)
+        ch = np.zeros((max(nq.value, 1), QWIDTH), np.int32)
+        bx = np.zeros((max(nq.value, 1), 16), np.uint32)
         orig = np.zeros(max(scene.counts()["triangles"], 1), np.int32)
-        _check(lib().rr_debug_bvh4(self.handle, scene.handle, int(frame), ctypes.byref(n4), _ptr(ch, ctypes.c_int32),
+        _check(lib().rr_debug_qbvh(self.handle, scene.handle, int(frame), ctypes.byref(nq), _ptr(ch, ctypes.c_int32),
                                    _ptr(bx, ctypes.c_uint32), _ptr(orig, ctypes.c_int32)), self.handle)
         if with_order:
-            return ch[:n4.value], bx[:n4.value], orig[:scene.counts()["triangles"]]
-        return ch[:n4.value], bx[:n4.value]
+            return ch[:nq.value], bx[:nq.value], orig[:scene.counts()["triangles"]]
+        return ch[:nq.value], bx[:nq.value]
 
     def jpeg_device(self, rgba: np.ndarray, quality: int = 90) -> bytes:
         """rr_debug_jpeg_device: the JPEG file bytes of an (H, W, 4) uint8 image

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 5
+#define RR_ABI_VERSION 6
 
 /* error codes (negative errno values) */
 #define RR_OK 0
@@ -291,21 +291,23 @@ int rr_debug_bvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, uint32_t* ke
 int rr_debug_bvh_hier(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t hier, uint32_t* keys,
                       uint32_t* order, int32_t* children, float* boxes);
 
-/* Quantised BVH4 of the frame (the PLOC hierarchy collapsed into 4-wide
- * nodes, the hierarchy the split path of large scenes traverses; built on
- * demand here). *n4 receives the node count; if children4 / nodes16 are
- * non-NULL they receive 4*n4 child refs (>= 0 node, < 0 leaf range
- * ~(first | (count - 1) << 28) of the BVH4's triangle array, 0x7fffffff
- * empty) and the 16 32-bit words of each 64-byte node: origin x y z (float),
- * exponent bytes (e+128 per axis), 4 child refs, lo x/y/z and hi x/y/z grid
- * coordinates (one byte per child), 2 zero words; tri_orig (n triangles)
- * the original triangle id at each position of that array. Call once with
- * NULL arrays to size them. */
-int rr_debug_bvh4(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t* n4,
-                  int32_t* children4, uint32_t* nodes16, int32_t* tri_orig);
+/* Quantised 6-wide hierarchy of the frame (the PLOC hierarchy collapsed into
+ * 6-wide nodes, the hierarchy the split path of large scenes traverses; built
+ * on demand here). *nq receives the node count; if children / nodes16 are
+ * non-NULL they receive 6*nq child refs (>= 0 node, < 0 ~position in the
+ * hierarchy's triangle array, 0x7fffffff unused slot — spelled out from the
+ * node's implicit references) and the 16 32-bit words of each 64-byte node:
+ * origin x y z (float), exponent bytes (e+128 per axis) | internal-slot mask
+ * << 24, first internal child, first leaf triangle, lo x / lo y / lo z / hi x /
+ * hi y / hi z grid coordinates of children 0..3 (one byte each), children 4
+ * and 5 as byte pairs (lo x, lo y), (lo z, hi x), (hi y, hi z), one zero word;
+ * tri_orig (n triangles) the original triangle id at each position of that
+ * array. Call once with NULL arrays to size them. */
+int rr_debug_qbvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t* nq,
+                  int32_t* children, uint32_t* nodes16, int32_t* tri_orig);
 
 /* Trace a batch of rays against the frame's hierarchy. bvh_width: 2 (LBVH),
- * 4 (BVH4 collapse) or 0 (whichever the frame kernels use for this scene,
+ * 4 (the quantised 6-wide collapse) or 0 (whichever the frame kernels use for this scene,
  * render_ints[7] of rr_debug_frame_state). rays: n*8 floats
  * (o.xyz, tmin, d.xyz, tmax). hits: n*4 floats (t, u, v, 0), prims: n original
  * triangle ids (-1 miss), occluded: n bytes (any-hit result). */

@@ -13,6 +13,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liboracle.so")
+QW = 6  # child slots per quantised wide node (rr_oracle.c ORC_QW_MAX, rr_device.h kQWidth)
 
 _lib = None
 
@@ -34,7 +35,7 @@ def lib():
         L.orc_build_bvh.argtypes = [c_int, f, c_int, u32, u32, i32, f]
         L.orc_trace.argtypes = [c_int, f, c_int, f, f, i32, u8]
         L.orc_trace_w.argtypes = [c_int, f, c_int, c_int, f, f, i32, u8]
-        L.orc_build_bvh4.argtypes = [c_int, f, i32, i32, u32, i32]
+        L.orc_build_qbvh.argtypes = [c_int, f, i32, i32, u32, i32]
         L.orc_trace_brute.argtypes = [c_int, f, c_int, f, f, i32]
         L.orc_render.argtypes = [c_int, f, i32, f, c_int, f, f, f, i32, f, f, u8, c_int, c_int, c_int]
         L.orc_rng.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, c_int, f]
@@ -74,7 +75,7 @@ def build_lbvh(tris: np.ndarray, hier: int = 2):
 
 
 def trace(tris: np.ndarray, rays: np.ndarray, width: int = 2):
-    """Closest + any hit through the LBVH (2), PLOC (3) or the LBVH's BVH4 collapse (4)."""
+    """Closest + any hit through the LBVH (2), PLOC (3) or PLOC's quantised 6-wide collapse (4)."""
     tris = _f32(tris).reshape(-1, 9)
     rays = _f32(rays).reshape(-1, 8)
     n = rays.shape[0]
@@ -84,17 +85,17 @@ def trace(tris: np.ndarray, rays: np.ndarray, width: int = 2):
     return hits, prims, occ
 
 
-def build_bvh4(tris: np.ndarray, with_order: bool = False):
-    """Quantised BVH4: (children4 (n4,4), nodes (n4,16) uint32) as rr_debug_bvh4;
+def build_qbvh(tris: np.ndarray, with_order: bool = False):
+    """Quantised wide BVH: (children (n, QW), nodes (n, 16) uint32) as rr_debug_bvh4;
     with_order: also the original triangle id of each position of the BVH4's
     triangle array (the order its leaf ranges index)."""
     tris = _f32(tris).reshape(-1, 9)
     n = tris.shape[0]
     ni = max(n - 1, 1)
     n4 = np.zeros(1, np.int32)
-    ch, bx = np.zeros((ni, 4), np.int32), np.zeros((ni, 16), np.uint32)
+    ch, bx = np.zeros((ni, QW), np.int32), np.zeros((ni, 16), np.uint32)
     orig = np.zeros(max(n, 1), np.int32)
-    lib().orc_build_bvh4(n, _p(tris, ctypes.c_float), _p(n4, ctypes.c_int32), _p(ch, ctypes.c_int32),
+    lib().orc_build_qbvh(n, _p(tris, ctypes.c_float), _p(n4, ctypes.c_int32), _p(ch, ctypes.c_int32),
                          _p(bx, ctypes.c_uint32), _p(orig, ctypes.c_int32))
     if with_order:
         return ch[:n4[0]], bx[:n4[0]], orig[:n]

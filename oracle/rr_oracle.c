@@ -170,11 +170,11 @@ typedef struct {
     float* tri;       /* leaf order: v0 e1 e2 (9) */
     int* tri_orig;
     int* tri_mat;
-    int width;        /* hierarchy trace() walks: 2 (BVH2) or 4 (quantised BVH4 collapse) */
+    int width;        /* hierarchy trace() walks: 2 (BVH2) or 4 (the quantised wide collapse, ORC_QW children) */
     int* cnt;         /* 2 per internal node: leaf count of each child subtree (PLOC, Karras) */
-    int n4;           /* BVH4 nodes */
-    int* child4;      /* 4 per node: >= 0 node, < 0 ~leaf, ORC_EMPTY4 unused */
-    uint32_t* q4;     /* 16 words per node, csrc/rr_device.h QNode4 */
+    int n4;           /* quantised wide nodes */
+    int* child4;      /* ORC_QW per node (derived from the node, for tests): >= 0 node, < 0 ~leaf, ORC_EMPTY4 unused */
+    uint32_t* q4;     /* 16 words per node, csrc/rr_device.h QNode6 */
 } lbvh;
 
 #define ORC_EMPTY4 0x7fffffff
@@ -479,25 +479,48 @@ static v3 rcp3(v3 d) {
     return V(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
 }
 
-static void q4_pack(const float lo[3][4], const float hi[3][4], const int ref[4], int used, uint32_t* o) {
-    uint32_t ql[3] = {0, 0, 0}, qh[3] = {0, 0, 0}, eb = 0;
+/* Quantised wide node (csrc/rr_device.h QNode6), 16 words = 64 B, up to six
+ * children:
+ *   w0..2  grid origin (float bits)   w3  exponent bytes (e + 128) per axis | inner mask << 24
+ *   w4     index of the first internal child (the others follow in slot order)
+ *   w5     position of the first leaf child's triangle (the others follow)
+ *   w6..11 children 0..3: lo x, lo y, lo z, hi x, hi y, hi z (byte c = child c)
+ *   w12..14 children 4, 5: (lo x, lo y), (lo z, hi x), (hi y, hi z) as byte pairs
+ *   w15    0
+ * An unused slot has lo 255, hi 0 on every axis: its box test always fails. */
+#define ORC_QW_MAX 6
+#ifndef ORC_QW
+#define ORC_QW 6 /* children per node (<= ORC_QW_MAX; rr_device.h kQWidth) */
+#endif
+/* grid coordinate `which` (0..2 lo x/y/z, 3..5 hi x/y/z) of child c */
+static uint32_t qn_byte(const uint32_t* w, int which, int c) {
+    if (c < 4) return (w[6 + which] >> (8 * c)) & 255u;
+    return (w[12 + which / 2] >> (16 * (which & 1) + 8 * (c - 4))) & 255u;
+}
+static void qn_set_byte(uint32_t* w, int which, int c, uint32_t v) {
+    if (c < 4) w[6 + which] |= v << (8 * c);
+    else w[12 + which / 2] |= v << (16 * (which & 1) + 8 * (c - 4));
+}
+static void q4_pack(const float lo[3][ORC_QW_MAX], const float hi[3][ORC_QW_MAX], int used, uint32_t inner,
+                    uint32_t inner_base, uint32_t tri_base, uint32_t* o) {
+    uint32_t eb = 0;
     float org[3];
+    memset(o, 0, 16 * sizeof(uint32_t));
     for (int a = 0; a < 3; ++a) {
         float l = lo[a][0], h = hi[a][0];
         for (int c = 1; c < used; ++c) { l = fminf(l, lo[a][c]); h = fmaxf(h, hi[a][c]); }
         int e = q4_exponent((double)h - (double)l);
         org[a] = l;
         eb |= (uint32_t)(e + 128) << (8 * a);
-        for (int c = 0; c < 4; ++c) {
-            ql[a] |= (c < used ? q4_quant(lo[a][c], l, e, 0) : 255u) << (8 * c);
-            qh[a] |= (c < used ? q4_quant(hi[a][c], l, e, 1) : 0u) << (8 * c);
+        for (int c = 0; c < ORC_QW_MAX; ++c) {
+            qn_set_byte(o, a, c, c < used ? q4_quant(lo[a][c], l, e, 0) : 255u);
+            qn_set_byte(o, 3 + a, c, c < used ? q4_quant(hi[a][c], l, e, 1) : 0u);
         }
     }
     memcpy(o, org, 3 * sizeof(float));
-    o[3] = eb;
-    for (int c = 0; c < 4; ++c) o[4 + c] = (uint32_t)ref[c];
-    o[8] = ql[0]; o[9] = ql[1]; o[10] = ql[2]; o[11] = qh[0]; o[12] = qh[1]; o[13] = qh[2];
-    o[14] = 0; o[15] = 0;
+    o[3] = eb | inner << 24;
+    o[4] = inner_base;
+    o[5] = tri_base;
 }
 
 /* BVH4 collapse of the BVH2 (PLOC, or Karras below 3 triangles), as
@@ -516,7 +539,7 @@ static void q4_pack(const float lo[3][4], const float hi[3][4], const int ref[4]
  * ~(first | (count - 1) << 28) of it). Boxes are the BVH2 child boxes,
  * quantised by q4_pack. */
 #define ORC_LEAF_TRIS 1
-typedef struct { int m; int ref[4], cnt[4]; float lo[3][4], hi[3][4]; } c4set;
+typedef struct { int m; int ref[ORC_QW_MAX], cnt[ORC_QW_MAX]; float lo[3][ORC_QW_MAX], hi[3][ORC_QW_MAX]; } c4set;
 
 static void c4_put(const lbvh* B, c4set* S, int slot, int node, int side) {
     const float* f = B->box + 12 * (size_t)node + 6 * side;
@@ -531,8 +554,8 @@ static int c4_leaf(const c4set* S, int c) { return S->ref[c] < 0 || S->cnt[c] <=
 static void c4_set(const lbvh* B, int r, c4set* S) {
     c4_put(B, S, 0, r, 0);
     c4_put(B, S, 1, r, 1);
-    S->m = 2;
-    while (S->m < 4) {
+    S->m = B->n > 1 ? 2 : 1; /* one triangle: one leaf slot */
+    while (S->m < ORC_QW) {
         int best = -1;
         float ba = 0.0f;
         for (int c = 0; c < S->m; ++c) {
@@ -563,26 +586,29 @@ static void lbvh_collapse4(lbvh* B) {
     const int ni = n > 1 ? n - 1 : 1;
     int* src = (int*)malloc(sizeof(int) * (size_t)ni);
     int* perm = (int*)malloc(sizeof(int) * (size_t)n);  /* BVH4 triangle position -> sorted leaf */
-    B->child4 = (int*)malloc(sizeof(int) * 4 * (size_t)ni);
+    B->child4 = (int*)malloc(sizeof(int) * ORC_QW_MAX * (size_t)ni);
     B->q4 = (uint32_t*)malloc(sizeof(uint32_t) * 16 * (size_t)ni);
     src[0] = 0;
     int count = 1, ntri = 0;
     for (int idx = 0; idx < count; ++idx) {
         c4set S;
         c4_set(B, src[idx], &S);
-        int ref[4];
-        for (int c = 0; c < 4; ++c) {
+        int ref[ORC_QW_MAX];
+        uint32_t inner = 0;
+        const int inner_base = count, tri_base = ntri;
+        for (int c = 0; c < ORC_QW_MAX; ++c) {
             if (c >= S.m) ref[c] = ORC_EMPTY4;
-            else if (!c4_leaf(&S, c)) { src[count] = S.ref[c]; ref[c] = count++; }
-            else if (n == 1) { perm[0] = 0; ref[c] = leaf_ref(0, 1); }  /* one triangle: both slots name it */
-            else {
-                const int k = c4_gather(B, S.ref[c], perm + ntri);
-                ref[c] = leaf_ref(ntri, k);
-                ntri += k;
+            else if (!c4_leaf(&S, c)) { src[count] = S.ref[c]; ref[c] = count++; inner |= 1u << c; }
+            else if (n == 1) { perm[0] = 0; ref[c] = leaf_ref(0, 1); ntri = 1; }
+            else { /* a leaf entry is one triangle (ORC_LEAF_TRIS 1): position ntri */
+                c4_gather(B, S.ref[c], perm + ntri);
+                ref[c] = leaf_ref(ntri, 1);
+                ntri += 1;
             }
         }
-        q4_pack((const float(*)[4])S.lo, (const float(*)[4])S.hi, ref, S.m, B->q4 + 16 * (size_t)idx);
-        for (int c = 0; c < 4; ++c) B->child4[4 * (size_t)idx + c] = ref[c];
+        q4_pack((const float(*)[ORC_QW_MAX])S.lo, (const float(*)[ORC_QW_MAX])S.hi, S.m, inner, (uint32_t)inner_base,
+                (uint32_t)tri_base, B->q4 + 16 * (size_t)idx);
+        for (int c = 0; c < ORC_QW_MAX; ++c) B->child4[ORC_QW_MAX * (size_t)idx + c] = ref[c];
     }
     B->n4 = count;
     /* the triangle arrays in the BVH4's leaf order */
@@ -649,12 +675,15 @@ static void try_leaf(const lbvh* B, int leaf, v3 o, v3 d, float tmin, hitrec* h)
 
 typedef struct { float t; int slot, ref; } ckey;
 
-/* Quantised BVH4 walk of rr_device.h TravStateQ4: per axis s = iq * 2^e,
+/* Quantised wide walk of rr_device.h TravStateQW: per axis s = iq * 2^e,
  * o' = (org - o) * iq, plane t = fma(q, s, o'), near plane lo for iq >= 0 else
- * hi; the four box tests against the bound at node entry, passing leaf
- * children intersected in slot order, the nearest hit internal child (ties:
- * lower slot) visited next, the other hit internal children pushed in
- * descending slot order. */
+ * hi; the ORC_QW_MAX box tests against the bound at node entry (unused slots
+ * always fail), passing leaf children intersected in slot order, the nearest
+ * hit internal child (ties: lower slot) visited next, the other hit internal
+ * children pushed in descending slot order. Child refs are implicit: internal
+ * child c is node w4 + (internal slots before c), leaf child c is triangle
+ * w5 + (leaf slots before c). */
+long long g_node_visits; /* traversal statistics (test use) */
 static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hitrec* h) {
     h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
     if (B->n <= 0) return 0;
@@ -665,51 +694,52 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
     int sp = 0, node = 0;
     for (;;) {
         const uint32_t* nd = B->q4 + 16 * (size_t)node;
-        const int* ch = B->child4 + 4 * (size_t)node;
+        const uint32_t inner = nd[3] >> 24;
         const float tcur = h->t;
         float sc[3], of[3];
-        uint32_t nq[3], fq[3];
+        int pos[3];
         for (int a = 0; a < 3; ++a) {
             float org;
             memcpy(&org, nd + a, sizeof org);
             sc[a] = ldexpf(iq[a], (int)((nd[3] >> (8 * a)) & 255u) - 128);
             of[a] = (org - oo[a]) * iq[a];
-            int pos = iq[a] >= 0.0f;
-            nq[a] = pos ? nd[8 + a] : nd[11 + a];
-            fq[a] = pos ? nd[11 + a] : nd[8 + a];
+            pos[a] = iq[a] >= 0.0f;
         }
-        ckey k[4];
-        for (int c = 0; c < 4; ++c) {
-            int ref = ch[c];
-            int sh = 8 * c;
-            float tn = fmaxf(fmaxf(fmaf((float)((nq[0] >> sh) & 255u), sc[0], of[0]),
-                                   fmaf((float)((nq[1] >> sh) & 255u), sc[1], of[1])),
-                             fmaxf(fmaf((float)((nq[2] >> sh) & 255u), sc[2], of[2]), tmin));
-            float tf = fminf(fminf(fmaf((float)((fq[0] >> sh) & 255u), sc[0], of[0]),
-                                   fmaf((float)((fq[1] >> sh) & 255u), sc[1], of[1])),
-                             fminf(fmaf((float)((fq[2] >> sh) & 255u), sc[2], of[2]), tcur));
-            int hit = ref != ORC_EMPTY4 && tn <= tf;
+        ckey k[ORC_QW_MAX];
+        int n_in = 0, n_lf = 0;
+        for (int c = 0; c < ORC_QW_MAX; ++c) {
+            float tn = tmin, tf = tcur, p0[3], p1[3];
+            for (int a = 0; a < 3; ++a) {
+                const uint32_t ql = qn_byte(nd, a, c), qh = qn_byte(nd, 3 + a, c);
+                p0[a] = fmaf((float)(pos[a] ? ql : qh), sc[a], of[a]);
+                p1[a] = fmaf((float)(pos[a] ? qh : ql), sc[a], of[a]);
+            }
+            tn = fmaxf(fmaxf(p0[0], p0[1]), fmaxf(p0[2], tmin));
+            tf = fminf(fminf(p1[0], p1[1]), fminf(p1[2], tcur));
+            const int is_inner = (inner >> c) & 1u;
+            const int ref = is_inner ? (int)nd[4] + n_in : ~((int)nd[5] + n_lf);
+            if (is_inner) ++n_in; else ++n_lf;
+            const int hit = tn <= tf;
             k[c].slot = c;
             k[c].ref = ref;
-            k[c].t = (hit && ref >= 0) ? tn : INFINITY;
-            if (hit && ref < 0) {
-                for (int q = 0; q < leaf_count(ref); ++q) {
-                    try_leaf(B, leaf_first(ref) + q, o, d, tmin, h);
-                    if (any && h->idx >= 0) return 1;
-                }
+            k[c].t = (hit && is_inner) ? tn : INFINITY;
+            if (hit && !is_inner) {
+                try_leaf(B, ~ref, o, d, tmin, h);
+                if (any && h->idx >= 0) { ++g_node_visits; return 1; }
             }
         }
+        ++g_node_visits;
         /* nearest hit internal child next (ties: lower slot); the others are
          * pushed in descending slot order */
         int best = -1;
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < ORC_QW_MAX; ++c)
             if (k[c].t != INFINITY && (best < 0 || k[c].t < k[best].t)) best = c;
         if (best < 0) {
             if (sp == 0) break;
             node = stack[--sp];
             continue;
         }
-        for (int c = 3; c >= 0; --c)
+        for (int c = ORC_QW_MAX - 1; c >= 0; --c)
             if (c != best && k[c].t != INFINITY && sp < ORC_MAXDEPTH) stack[sp++] = k[c].ref;
         node = k[best].ref;
     }
@@ -1318,15 +1348,15 @@ int orc_trace_brute(int n, const float* tris9, int n_rays, const float* rays, fl
     return 0;
 }
 
-/* Quantised BVH4 (rr_debug_bvh4 layout): n4 nodes, 4 child refs and the 16
+/* Quantised wide BVH (rr_debug_bvh4 layout): n4 nodes, ORC_QW_MAX child refs and the 16
  * words of each node. */
-int orc_build_bvh4(int n, const float* tris9, int32_t* n4, int32_t* children4, uint32_t* nodes16,
+int orc_build_qbvh(int n, const float* tris9, int32_t* n4, int32_t* children4, uint32_t* nodes16,
                    int32_t* tri_orig) {
     lbvh B;
     lbvh_build(&B, n, tris9, NULL, 3);
     lbvh_collapse4(&B);
     *n4 = B.n4;
-    if (children4 && B.n4) memcpy(children4, B.child4, sizeof(int32_t) * 4 * (size_t)B.n4);
+    if (children4 && B.n4) memcpy(children4, B.child4, sizeof(int32_t) * ORC_QW_MAX * (size_t)B.n4);
     if (nodes16 && B.n4) memcpy(nodes16, B.q4, sizeof(uint32_t) * 16 * (size_t)B.n4);
     if (tri_orig && n > 0) memcpy(tri_orig, B.tri_orig, sizeof(int32_t) * (size_t)n);
     lbvh_free(&B);

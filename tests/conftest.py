@@ -34,9 +34,10 @@ def scene_path(name: str) -> str:
     return os.path.join(SCENES, name)
 
 
-def bvh4_leaf_positions(ch):
-    """Positions of a BVH4's triangle array its leaf refs ~(first | (count - 1)
-    << 28) name, in node order."""
+def qbvh_leaf_positions(ch):
+    """Positions of the quantised hierarchy's triangle array its leaf refs
+    ~(first | (count - 1) << 28) name (one triangle each: ~position), in node
+    order."""
     out = []
     for r in ch[ch < 0].tolist():
         x = ~int(r)

@@ -99,8 +99,8 @@ def test_trace_batches_bit_exact(ctx, s04):
     assert np.array_equal(bh[:, 0], oh[:, 0])
 
 
-def test_trace_bvh4_small_scene(ctx, s04):
-    """The BVH4 walk on the 12-triangle scene (forced; frames use the LDS BVH2)."""
+def test_trace_qbvh_small_scene(ctx, s04):
+    """The quantised 6-wide walk on the 12-triangle scene (forced; frames use the LDS BVH2)."""
     rng = np.random.default_rng(99)
     st = ctx.frame_state(s04, 45)
     assert int(st.render_ints[7]) == 2
@@ -109,8 +109,8 @@ def test_trace_bvh4_small_scene(ctx, s04):
     hits, prims, occ = ctx.trace(s04, 45, rays, width=4)
     oh, op, oo = O.trace(st.tris, rays, width=4)
     assert np.array_equal(prims, op) and np.array_equal(hits, oh) and np.array_equal(occ, oo)
-    ch, bx, order = ctx.bvh4(s04, 45, with_order=True)
-    och, obx, oorder = O.build_bvh4(st.tris, with_order=True)
+    ch, bx, order = ctx.qbvh(s04, 45, with_order=True)
+    och, obx, oorder = O.build_qbvh(st.tris, with_order=True)
     assert np.array_equal(ch, och) and np.array_equal(bx, obx) and np.array_equal(order, oorder)
 
 
@@ -134,7 +134,7 @@ def test_trace_edge_cases(ctx, s04):
 
 
 # "tiles": k_tiles (default for LDS-resident scenes); "wavefront": the split
-# trace / shade kernels over the quantised BVH4 (RR_FLAG_WAVEFRONT), the path
+# trace / shade kernels over the quantised 6-wide hierarchy (RR_FLAG_WAVEFRONT), the path
 # large scenes take (frame_state reports render_ints[7] == 4 for it, so the
 # oracle walks the same hierarchy without the hull rule).
 PATHS = {"tiles": 0, "wavefront": 4}
@@ -168,7 +168,7 @@ def test_tiles_equal_wavefront_full_resolution(ctx, rr, s04):
     (test_full_frame_bit_exact); against each other they may differ where a
     camera ray grazes a cube edge: k_tiles tests camera rays against every
     triangle of their tile (brute force), the split path walks the quantised
-    BVH4, whose float slab test can reject a box whose triangle the
+    6-wide hierarchy, whose float slab test can reject a box whose triangle the
     barycentric test would accept exactly on its edge (the oracle reproduces
     both: 6 film values of 04vs frame 7 at 40 spp, tools-free check in
     DESIGN.md §5)."""

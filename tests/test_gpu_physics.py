@@ -2,7 +2,7 @@
 the C4 physics stand-ins (02/03: thousands of rigid bodies, hierarchy rebuilt
 every frame) and the C5 synthetic 10M-triangle scene. These
 scenes take the HBM (non-LDS) traversal path over a PLOC hierarchy collapsed
-to the quantised BVH4. Integer work (Morton keys, radix order,
+to the quantised 6-wide hierarchy. Integer work (Morton keys, radix order,
 BVH topology, hit ids) and the float work are bit-exact (tolerance 0), as in
 test_gpu_parity.py. Full-size C5 is checked through size-independent
 properties: the whole 10M-triangle LBVH equals the oracle's, and a ray batch
@@ -11,7 +11,7 @@ through it equals the oracle's traversal; images at reduced resolution/spp.
 import numpy as np
 import pytest
 
-from conftest import bvh4_leaf_positions, scene_path, walk_lbvh
+from conftest import qbvh_leaf_positions, scene_path, walk_lbvh
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -56,7 +56,7 @@ def _camera_rays(st, n, rng):
 @pytest.mark.parametrize("frame", [1, 45, 170])
 def test_physics_bvh_bit_exact(ctx, s02, frame):
     """The frame's BVH2 (PLOC over the Morton-sorted leaves for scenes traversed
-    from HBM, before its collapse to the quantised BVH4) equals the oracle's
+    from HBM, before its collapse to the quantised 6-wide hierarchy) equals the oracle's
     build, node for node."""
     st = ctx.frame_state(s02, frame)
     assert st.tris.shape[0] == 92002
@@ -83,7 +83,7 @@ def test_physics_rebuilds_every_frame(ctx, rr, s02):
 
 @pytest.mark.parametrize("hier", [3, 2, 4])
 def test_physics_trace_bit_exact(ctx, s02, hier):
-    """Ray batches through PLOC, the LBVH and the quantised BVH4 collapse of
+    """Ray batches through PLOC, the LBVH and the quantised 6-wide hierarchy collapse of
     PLOC (the frame's hierarchy), each against the oracle's walk of the same
     hierarchy."""
     st = ctx.frame_state(s02, 90)
@@ -100,15 +100,15 @@ def test_physics_trace_bit_exact(ctx, s02, hier):
 
 
 @pytest.mark.parametrize("frame", [1, 90])
-def test_physics_bvh4_bit_exact(ctx, s02, frame):
+def test_physics_qbvh_bit_exact(ctx, s02, frame):
     st = ctx.frame_state(s02, frame)
-    ch, bx, order = ctx.bvh4(s02, frame, with_order=True)
-    och, obx, oorder = O.build_bvh4(st.tris, with_order=True)
+    ch, bx, order = ctx.qbvh(s02, frame, with_order=True)
+    och, obx, oorder = O.build_qbvh(st.tris, with_order=True)
     assert ch.shape == och.shape and np.array_equal(ch, och)
     assert np.array_equal(bx, obx)
-    assert np.array_equal(order, oorder)  # the triangles in the BVH4's leaf order
-    # every triangle position in exactly one leaf (of <= 2), every node but the root referenced once
-    assert sorted(bvh4_leaf_positions(ch)) == list(range(st.tris.shape[0]))
+    assert np.array_equal(order, oorder)  # the triangles in the hierarchy's leaf order
+    # every triangle position in exactly one leaf, every node but the root referenced once
+    assert sorted(qbvh_leaf_positions(ch)) == list(range(st.tris.shape[0]))
     assert sorted(order.tolist()) == list(range(st.tris.shape[0]))
     inner = ch[(ch >= 0) & (ch != 0x7FFFFFFF)]
     assert np.array_equal(np.sort(inner), np.arange(1, ch.shape[0]))
@@ -156,17 +156,17 @@ def test_c5_full_size_bvh_bit_exact(ctx, sc5):
     assert len(set(inner)) == len(inner)
 
 
-def test_c5_full_size_bvh4_bit_exact(ctx, sc5):
+def test_c5_full_size_qbvh_bit_exact(ctx, sc5):
     st = ctx.frame_state(sc5, 120)
-    ch, bx, order = ctx.bvh4(sc5, 120, with_order=True)
-    och, obx, oorder = O.build_bvh4(st.tris, with_order=True)
+    ch, bx, order = ctx.qbvh(sc5, 120, with_order=True)
+    och, obx, oorder = O.build_qbvh(st.tris, with_order=True)
     assert np.array_equal(ch, och)
     assert np.array_equal(bx, obx)
     assert np.array_equal(order, oorder)
-    leaves = np.array(bvh4_leaf_positions(ch))
+    leaves = np.array(qbvh_leaf_positions(ch))
     assert np.array_equal(np.sort(leaves), np.arange(st.tris.shape[0]))
-    two = int(np.count_nonzero([((~int(r)) >> 28) == 1 for r in ch[ch < 0].tolist()]))
-    print(f"C5 BVH4: {ch.shape[0]} nodes, {int((ch < 0).sum())} leaves ({two} of two triangles)")
+    print(f"C5 6-wide hierarchy: {ch.shape[0]} nodes, {int((ch < 0).sum())} leaves, "
+          f"{np.mean((ch != 0x7FFFFFFF).sum(1)):.2f} children per node")
 
 
 @pytest.mark.parametrize("width", [3, 4])

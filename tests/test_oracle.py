@@ -326,13 +326,39 @@ def test_screen_cull_changes_no_pixel(tmp_path, case, hier):
     assert np.array_equal(f_cull, f_all), f"{np.count_nonzero(f_cull != f_all)} film mismatches"
 
 
-def _q4_child_boxes(node):
-    """Decoded child boxes of one quantised BVH4 node (rr_device.h QNode4), in
-    double: lo/hi = org + q * 2^e per axis, (4, 3) each."""
+def _q6_child_boxes(node):
+    """Decoded child boxes of one quantised 6-wide node (rr_device.h QNode6),
+    in double: lo/hi = org + q * 2^e per axis, (6, 3) each."""
     org = node[0:3].view(np.float32).astype(np.float64)
     e = np.array([((int(node[3]) >> (8 * a)) & 255) - 128 for a in range(3)])
-    q = np.array([[(int(node[8 + k]) >> (8 * c)) & 255 for k in range(6)] for c in range(4)], np.float64)
+    q = np.zeros((6, 6), np.float64)  # [child, lo x lo y lo z hi x hi y hi z]
+    for c in range(6):
+        for k in range(6):
+            if c < 4:
+                q[c, k] = (int(node[6 + k]) >> (8 * c)) & 255
+            else:
+                q[c, k] = (int(node[12 + k // 2]) >> (16 * (k & 1) + 8 * (c - 4))) & 255
     return org + q[:, 0:3] * np.exp2(e), org + q[:, 3:6] * np.exp2(e)
+
+
+def _q6_refs(node):
+    """The implicit child references of a node, spelled out as rr_debug_qbvh
+    does: internal slot c -> first internal child + internal slots before c,
+    leaf slot -> ~(first leaf triangle + leaf slots before c), unused
+    (lo 255 / hi 0) -> 0x7fffffff."""
+    inner = int(node[3]) >> 24
+    out = []
+    for c in range(6):
+        below = bin(inner & ((1 << c) - 1)).count("1")
+        lox = (int(node[6]) >> (8 * c)) & 255 if c < 4 else (int(node[12]) >> (8 * (c - 4))) & 255
+        hix = (int(node[9]) >> (8 * c)) & 255 if c < 4 else (int(node[13]) >> (16 + 8 * (c - 4))) & 255
+        if (inner >> c) & 1:
+            out.append(int(node[4]) + below)
+        elif lox == 255 and hix == 0:
+            out.append(0x7FFFFFFF)
+        else:
+            out.append(~(int(node[5]) + c - below))
+    return out
 
 
 def leaf_range(r):
@@ -341,8 +367,8 @@ def leaf_range(r):
     return x & 0x0FFFFFFF, (x >> 28) + 1
 
 
-def bvh4_leaf_positions(ch):
-    """Positions of the BVH4's triangle array its leaf refs name, in node order."""
+def qbvh_leaf_positions(ch):
+    """Positions of the hierarchy's triangle array its leaf refs name, in node order."""
     out = []
     for r in ch[(ch < 0)].tolist():
         f, k = leaf_range(r)
@@ -352,13 +378,13 @@ def bvh4_leaf_positions(ch):
 
 def _check_q4_contains(tris, ch, nodes, order):
     """Every quantised child box contains the boxes of all triangles below it
-    (order: original triangle id of each position of the BVH4's triangle array)."""
+    (order: original triangle id of each position of the hierarchy's triangle array)."""
     bvh4_tris = tris.reshape(-1, 9)[order].reshape(-1, 3, 3)
 
     def walk(i):
-        lo4, hi4 = _q4_child_boxes(nodes[i])
+        lo4, hi4 = _q6_child_boxes(nodes[i])
         under = []
-        for c in range(4):
+        for c in range(6):
             r = int(ch[i, c])
             if r == 0x7FFFFFFF:
                 continue
@@ -377,18 +403,20 @@ def _check_q4_contains(tris, ch, nodes, order):
 
 
 @pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (7, 2), (300, 3), (5000, 4)])
-def test_bvh4_collapse_and_walk_equal_brute_force(n, seed):
-    """Quantised BVH4 collapse of the PLOC hierarchy: every leaf once, every
-    node but the root once, quantised boxes containing their subtrees; the
-    BVH4 walk finds the brute-force closest hits."""
+def test_qbvh_collapse_and_walk_equal_brute_force(n, seed):
+    """Quantised 6-wide collapse of the PLOC hierarchy: every leaf once, every
+    node but the root once, quantised boxes containing their subtrees, the
+    implicit child references as spelled out; the wide walk finds the
+    brute-force closest hits."""
     rng = np.random.default_rng(seed)
     c = rng.uniform(-5, 5, (n, 1, 3))
     tris = (c + rng.normal(0, 0.6, (n, 3, 3))).astype(np.float32)
-    ch, nodes, order = O.build_bvh4(tris, with_order=True)
-    assert np.array_equal(nodes[:, 4:8].view(np.int32), ch)
-    leaves = bvh4_leaf_positions(ch)
-    assert sorted(leaves) == list(range(n)) or (n == 1 and set(leaves) == {0})
-    assert all(leaf_range(r)[1] <= 2 for r in ch[ch < 0].tolist())  # leaves of at most 2 triangles
+    ch, nodes, order = O.build_qbvh(tris, with_order=True)
+    assert np.array_equal(np.array([_q6_refs(x) for x in nodes], np.int32).reshape(ch.shape), ch)
+    leaves = qbvh_leaf_positions(ch)
+    assert sorted(leaves) == list(range(n))
+    assert all(leaf_range(r)[1] == 1 for r in ch[ch < 0].tolist())  # one triangle per leaf
+    assert n < 300 or np.mean((ch != 0x7FFFFFFF).sum(1)) > 3.5  # (nodes over two single-triangle leaves stay 2-wide)
     inner = ch[(ch >= 0) & (ch != 0x7FFFFFFF)]
     assert np.array_equal(np.sort(inner), np.arange(1, ch.shape[0]))
     if n > 1:
@@ -407,7 +435,7 @@ def test_bvh4_collapse_and_walk_equal_brute_force(n, seed):
     assert np.array_equal(o4, o2)
 
 
-def test_bvh4_axis_aligned_geometry_and_rays():
+def test_qbvh_axis_aligned_geometry_and_rays():
     """Flat boxes (an axis-aligned grid of quads and a cube) and rays with
     exactly zero direction components: the finite reciprocal of the quantised
     walk (q4_rcp) keeps every plane distance finite, and the hits still equal
@@ -430,7 +458,7 @@ def test_bvh4_axis_aligned_geometry_and_rays():
                 p[k][v] += dv
             quads += [(p[0], p[1], p[2]), (p[0], p[2], p[3])]
     tris = np.array(quads, np.float32)
-    ch, nodes, order = O.build_bvh4(tris, with_order=True)
+    ch, nodes, order = O.build_qbvh(tris, with_order=True)
     _check_q4_contains(tris, ch, nodes, order)
     rng = np.random.default_rng(7)
     rays = []
