@@ -710,13 +710,14 @@ RR_D int xcd_wave_rank() {
                                           (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
 }
 // Top of the quantised hierarchy in LDS for the trace kernels (Q6Nodes): the
-// first kTopNodes nodes (breadth-first numbering: the four top levels, 85
-// nodes, and part of the fifth), copied by the block at launch. 128 nodes =
-// 8 KB beside the 12 KB traversal stack (kLdsStack) keeps 8 blocks of 256
-// threads (8 waves per SIMD) per CU. Measured per frame slice against no copy
-// (C5 at 16 spp / 02 / 03 at 64 spp): 105.8 -> 101.4, 110.5 -> 107.0, 118.2 ->
-// 115.9 ms (extension and shadow traversal -3 to -7 %); 64 nodes with a
-// 16-entry stack 103.3, 192 with 8 entries 103.4 ms on C5.
+// first kTopNodes nodes (breadth-first numbering: the three top levels of the
+// 6-wide hierarchy, 43 nodes, and most of the fourth), copied by the block at
+// launch. 128 nodes = 8 KB beside the 12 KB traversal stack (kLdsStack) keeps
+// 8 blocks of 256 threads (8 waves per SIMD) per CU. Measured on the 4-wide
+// hierarchy per frame slice against no copy (C5 at 16 spp / 02 / 03 at 64
+// spp): 105.8 -> 101.4, 110.5 -> 107.0, 118.2 -> 115.9 ms (extension and
+// shadow traversal -3 to -7 %); on the 6-wide one, 64 nodes with a 16-entry
+// stack measured the same as 128 with 12 (C5 95.0 / 94.7 ms).
 #ifndef RR_TOP_NODES
 #define RR_TOP_NODES 128
 #endif
@@ -1953,11 +1954,10 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
     const int npix = base.npix;
     const int cpc = counters_per_chunk(base.max_bounces);
     // camera rays as packets (packet_trace) when triangles are large on screen:
-    // at most one triangle per two pixels (02 / 03 yes, C5 no)
-#ifndef RR_PACKET_TRIS_PER_PIXEL_HALF
-#define RR_PACKET_TRIS_PER_PIXEL_HALF 1
-#endif
-    const bool packets = RR_PACKET_TRIS_PER_PIXEL_HALF && (long)base.n_tris * 2 <= (long)npix;
+    // at most one triangle per two pixels (02 / 03 yes, C5 no; on the 6-wide
+    // hierarchy packets against per-lane walks: 02 / 03 camera rays at 64 spp
+    // 12.6 / 12.4 against 16.9 / 15.0 ms)
+    const bool packets = (long)base.n_tris * 2 <= (long)npix;
     // group counters: [chunk][bounce 0..max][path | shadow][kQGroups * kQStride]
     const size_t per_q = (size_t)kQGroups * kQStride;
     const size_t per_chunk = (size_t)(base.max_bounces + 1) * 2 * per_q;
