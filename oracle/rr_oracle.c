@@ -492,11 +492,7 @@ static v3 rcp3(v3 d) {
 #ifndef ORC_QW
 #define ORC_QW 6 /* children per node (<= ORC_QW_MAX; rr_device.h kQWidth) */
 #endif
-/* grid coordinate `which` (0..2 lo x/y/z, 3..5 hi x/y/z) of child c */
-static uint32_t qn_byte(const uint32_t* w, int which, int c) {
-    if (c < 4) return (w[6 + which] >> (8 * c)) & 255u;
-    return (w[12 + which / 2] >> (16 * (which & 1) + 8 * (c - 4))) & 255u;
-}
+/* sets grid coordinate `which` (0..2 lo x/y/z, 3..5 hi x/y/z) of child c */
 static void qn_set_byte(uint32_t* w, int which, int c, uint32_t v) {
     if (c < 4) w[6 + which] |= v << (8 * c);
     else w[12 + which / 2] |= v << (16 * (which & 1) + 8 * (c - 4));
@@ -683,7 +679,6 @@ typedef struct { float t; int slot, ref; } ckey;
  * children pushed in descending slot order. Child refs are implicit: internal
  * child c is node w4 + (internal slots before c), leaf child c is triangle
  * w5 + (leaf slots before c). */
-long long g_node_visits; /* traversal statistics (test use) */
 static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hitrec* h) {
     h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
     if (B->n <= 0) return 0;
@@ -705,17 +700,28 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             of[a] = (org - oo[a]) * iq[a];
             pos[a] = iq[a] >= 0.0f;
         }
+        /* near / far grid coordinates per axis: children 0..3 one byte of a
+         * word, 4 and 5 a byte pair */
+        uint32_t nw[3], fw[3], nw2[3], fw2[3];
+        for (int a = 0; a < 3; ++a) {
+            const uint32_t lo = nd[6 + a], hi = nd[9 + a];
+            const uint32_t lo2 = (nd[12 + a / 2] >> (16 * (a & 1))) & 0xffffu;
+            const uint32_t hi2 = (nd[12 + (3 + a) / 2] >> (16 * ((3 + a) & 1))) & 0xffffu;
+            nw[a] = pos[a] ? lo : hi; fw[a] = pos[a] ? hi : lo;
+            nw2[a] = pos[a] ? lo2 : hi2; fw2[a] = pos[a] ? hi2 : lo2;
+        }
         ckey k[ORC_QW_MAX];
         int n_in = 0, n_lf = 0;
         for (int c = 0; c < ORC_QW_MAX; ++c) {
-            float tn = tmin, tf = tcur, p0[3], p1[3];
+            float p0[3], p1[3];
             for (int a = 0; a < 3; ++a) {
-                const uint32_t ql = qn_byte(nd, a, c), qh = qn_byte(nd, 3 + a, c);
-                p0[a] = fmaf((float)(pos[a] ? ql : qh), sc[a], of[a]);
-                p1[a] = fmaf((float)(pos[a] ? qh : ql), sc[a], of[a]);
+                const uint32_t qn = c < 4 ? (nw[a] >> (8 * c)) & 255u : (nw2[a] >> (8 * (c - 4))) & 255u;
+                const uint32_t qf = c < 4 ? (fw[a] >> (8 * c)) & 255u : (fw2[a] >> (8 * (c - 4))) & 255u;
+                p0[a] = fmaf((float)qn, sc[a], of[a]);
+                p1[a] = fmaf((float)qf, sc[a], of[a]);
             }
-            tn = fmaxf(fmaxf(p0[0], p0[1]), fmaxf(p0[2], tmin));
-            tf = fminf(fminf(p1[0], p1[1]), fminf(p1[2], tcur));
+            const float tn = fmaxf(fmaxf(p0[0], p0[1]), fmaxf(p0[2], tmin));
+            const float tf = fminf(fminf(p1[0], p1[1]), fminf(p1[2], tcur));
             const int is_inner = (inner >> c) & 1u;
             const int ref = is_inner ? (int)nd[4] + n_in : ~((int)nd[5] + n_lf);
             if (is_inner) ++n_in; else ++n_lf;
@@ -725,10 +731,9 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             k[c].t = (hit && is_inner) ? tn : INFINITY;
             if (hit && !is_inner) {
                 try_leaf(B, ~ref, o, d, tmin, h);
-                if (any && h->idx >= 0) { ++g_node_visits; return 1; }
+                if (any && h->idx >= 0) return 1;
             }
         }
-        ++g_node_visits;
         /* nearest hit internal child next (ties: lower slot); the others are
          * pushed in descending slot order */
         int best = -1;
