@@ -273,6 +273,17 @@ RR_HD uint32_t path_key(uint32_t seed, uint32_t pixel, uint32_t sample) {
 RR_HD float rng(uint32_t key, uint32_t dim) {
     return (float)(hash_u32(key + (dim + 1u) * 0x9E3779B9u) >> 8) * 5.9604644775390625e-08f;
 }
+// Two uniforms in [0, 1) from one hash, 16 bits each: the dimension pairs of
+// a sample (camera subpixel; light pick + lobe choice; disk point; BSDF
+// direction), half the hashes of one draw per dimension (each hash is two
+// v_mul_lo_u32, quarter rate: a timing build with one multiply per hash was
+// 2.3 % faster on 04vs). 2^-16 steps are far below the filter table's and the
+// samplers' resolution.
+RR_HD void rng2(uint32_t key, uint32_t dim, float& a, float& b) {
+    const uint32_t h = hash_u32(key + (dim + 1u) * 0x9E3779B9u);
+    a = (float)(h >> 16) * 1.52587890625e-05f;
+    b = (float)(h & 0xffffu) * 1.52587890625e-05f;
+}
 
 // ------------------------------------------------------------- sampling ---
 // sin/cos on |x| <= pi/4 (Cephes sinf/cosf kernels), fixed op order.

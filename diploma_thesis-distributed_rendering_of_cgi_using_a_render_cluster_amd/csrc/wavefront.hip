@@ -155,9 +155,11 @@ template <typename FloatP>
 __device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt, int px, int py,
                                               uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
                                               const ScreenCull* cull = nullptr, bool* culled = nullptr) {
-    // rng() < 1: the filter table is read without its range branches
-    const float fx = (float)px + 0.5f + table_lerp_padded(filt, kFilterN, rng(key, 0));
-    const float fy = (float)py + 0.5f + table_lerp_padded(filt, kFilterN, rng(key, 1));
+    // rng2() < 1: the filter table is read without its range branches
+    float ux, uy;
+    rng2(key, 0, ux, uy);
+    const float fx = (float)px + 0.5f + table_lerp_padded(filt, kFilterN, ux);
+    const float fy = (float)py + 0.5f + table_lerp_padded(filt, kFilterN, uy);
     if (cull) {
         *culled = cull->outside(fx, fy);
         if (*culled) {  // a miss: no direction needed (shade() of a miss reads only T and the world)
@@ -282,10 +284,15 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     if (path_capped(fc, bounce, lob)) return;
     const BsdfView vw = bsdf_view(m, lut, N, wo);
     const uint32_t dim0 = 2u + (uint32_t)(kDimsPerBounce * bounce);
+    // dimension pairs of this bounce (rng2): (light pick, lobe choice) at
+    // dim0, the disk point at dim0 + 1, the BSDF direction at dim0 + 4;
+    // Russian roulette keeps dim0 + 6 (oracle/rr_oracle.c radiance)
+    float u_light, u_lobe;
+    rng2(key, dim0, u_light, u_lobe);
     const float3 Po = offset_ray(P, N);
     // next-event estimation toward one uniformly chosen light
     if (fc.n_lights > 0) {
-        int li = (int)(rng(key, dim0) * (float)fc.n_lights);
+        int li = (int)(u_light * (float)fc.n_lights);
         if (li > fc.n_lights - 1) li = fc.n_lights - 1;
         __builtin_assume(li >= 0 && li < kMaxLights);  // rng >= 0, n_lights <= kMaxLights (setup_frame)
         const auto lt = v.lights + kLightF * li;
@@ -304,7 +311,9 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
                 float3 b1, b2;
                 make_onb(wl, b1, b2);
                 float dx, dy;
-                concentric_disk(rng(key, dim0 + 1u), rng(key, dim0 + 2u), dx, dy);
+                float u1, u2;
+                rng2(key, dim0 + 1u, u1, u2);
+                concentric_disk(u1, u2, dx, dy);
                 dx = dx * radius;
                 dy = dy * radius;
                 const float3 sp = madd3(madd3(lp, b1, dx), b2, dy);
@@ -350,9 +359,9 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     float3 wi, f;
     float pdf;
     bool glossy;
-    if (!bsdf_sample(m, lut, vw, N, wo, rng(key, dim0 + 3u), rng(key, dim0 + 4u), rng(key, dim0 + 5u), wi, f,
-                     pdf, glossy))
-        return;
+    float u_b1, u_b2;
+    rng2(key, dim0 + 4u, u_b1, u_b2);
+    if (!bsdf_sample(m, lut, vw, N, wo, u_lobe, u_b1, u_b2, wi, f, pdf, glossy)) return;
     const float k = 1.0f / pdf;  // f = f * cosL already
     T = mk3(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
     if (!(max3f(T) > 0.0f)) return;

@@ -121,6 +121,14 @@ static uint32_t pkey(uint32_t seed, uint32_t pixel, uint32_t sample) {
 static float rnd(uint32_t key, uint32_t dim) {
     return (float)(hash32(key + (dim + 1u) * 0x9E3779B9u) >> 8) * 5.9604644775390625e-08f;
 }
+/* two uniforms of one hash, 16 bits each (csrc/rr_device.h rng2): the
+ * dimension pairs of a sample (camera subpixel, light pick + lobe choice,
+ * disk point, BSDF direction) */
+static void rnd2(uint32_t key, uint32_t dim, float* a, float* b) {
+    const uint32_t h = hash32(key + (dim + 1u) * 0x9E3779B9u);
+    *a = (float)(h >> 16) * 1.52587890625e-05f;
+    *b = (float)(h & 0xffffu) * 1.52587890625e-05f;
+}
 
 /* ---------------------------------------------------------- sampling ---- */
 static void small_sincos(float x, float* s, float* c) {
@@ -1062,8 +1070,10 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
     const float* c = S->cam;
     uint32_t key = pkey(S->seed, (uint32_t)pix, (uint32_t)sample);
     int px = pix % S->W, py = pix / S->W;
-    float fx = (float)px + 0.5f + lerp_table(S->filter, ORC_FILTER_N, rnd(key, 0));
-    float fy = (float)py + 0.5f + lerp_table(S->filter, ORC_FILTER_N, rnd(key, 1));
+    float ux, uy;
+    rnd2(key, 0, &ux, &uy);
+    float fx = (float)px + 0.5f + lerp_table(S->filter, ORC_FILTER_N, ux);
+    float fy = (float)py + 0.5f + lerp_table(S->filter, ORC_FILTER_N, uy);
     float sx = fmaf(fx, S->inv_w2, -1.0f) * c[12];
     float sy = fmaf(-fy, S->inv_h2, 1.0f) * c[13];
     float len = sqrtf(fmaf(sy, sy, fmaf(sx, sx, 1.0f)));
@@ -1121,12 +1131,17 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
          * glossy_bounce to its cap ends the path at the next hit (emission only) */
         if (b >= S->max_bounces || nd >= S->max_diffuse || ng >= S->max_glossy) break;
         uint32_t dim0 = 2u + 8u * (uint32_t)b;
+        /* dimension pairs of this bounce: (light pick, lobe choice) at dim0,
+         * the disk point at dim0 + 1, the BSDF direction at dim0 + 4; the
+         * Russian-roulette test keeps its own dimension dim0 + 6 */
+        float u_light, u_lobe;
+        rnd2(key, dim0, &u_light, &u_lobe);
         v3 Po = offset_ray(P, N);
         int shadow = 0;
         v3 sh_dir = V(0, 0, 0), sh_c = V(0, 0, 0);
         float sh_dist = 0.0f;
         if (S->n_lights > 0) {
-            int li = (int)(rnd(key, dim0) * (float)S->n_lights);
+            int li = (int)(u_light * (float)S->n_lights);
             if (li > S->n_lights - 1) li = S->n_lights - 1;
             const float* lt = S->lights + 12 * li;
             v3 wi, Li;
@@ -1142,7 +1157,9 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
                     v3 b1, b2;
                     onb(wl, &b1, &b2);
                     float dx, dy;
-                    disk(rnd(key, dim0 + 1u), rnd(key, dim0 + 2u), &dx, &dy);
+                    float u1, u2;
+                    rnd2(key, dim0 + 1u, &u1, &u2);
+                    disk(u1, u2, &dx, &dy);
                     dx = dx * radius;
                     dy = dy * radius;
                     v3 sp = vmadd(vmadd(lp, b1, dx), b2, dy);
@@ -1177,7 +1194,9 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
         int alive = 0, glossy = 0;
         v3 wi, f;
         float pdf;
-        if (sample_bsdf(&m, lut, N, wo, rnd(key, dim0 + 3u), rnd(key, dim0 + 4u), rnd(key, dim0 + 5u), &wi, &f,
+        float u_b1, u_b2;
+        rnd2(key, dim0 + 4u, &u_b1, &u_b2);
+        if (sample_bsdf(&m, lut, N, wo, u_lobe, u_b1, u_b2, &wi, &f,
                         &pdf, &glossy)) {
             float k = 1.0f / pdf; /* f = f * cosL */
             T = V(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
