@@ -155,9 +155,10 @@ template <typename FloatP>
 __device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt, int px, int py,
                                               uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
                                               const ScreenCull* cull = nullptr, bool* culled = nullptr) {
-    // rng2() < 1: the filter table is read without its range branches
-    float ux, uy;
-    rng2(key, 0, ux, uy);
+    // the subpixel pair: the 16-bit halves of the path key itself (a hash
+    // output, so no hash of its own; the other dimensions hash key + offset);
+    // both < 1: the filter table is read without its range branches
+    const float ux = (float)(key >> 16) * 1.52587890625e-05f, uy = (float)(key & 0xffffu) * 1.52587890625e-05f;
     const float fx = (float)px + 0.5f + table_lerp_padded(filt, kFilterN, ux);
     const float fy = (float)py + 0.5f + table_lerp_padded(filt, kFilterN, uy);
     if (cull) {

@@ -1070,8 +1070,9 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
     const float* c = S->cam;
     uint32_t key = pkey(S->seed, (uint32_t)pix, (uint32_t)sample);
     int px = pix % S->W, py = pix / S->W;
-    float ux, uy;
-    rnd2(key, 0, &ux, &uy);
+    /* the camera subpixel pair: the 16-bit halves of the path key itself (a
+     * hash output; csrc/wavefront.hip camera_ray_xy) */
+    const float ux = (float)(key >> 16) * 1.52587890625e-05f, uy = (float)(key & 0xffffu) * 1.52587890625e-05f;
     float fx = (float)px + 0.5f + lerp_table(S->filter, ORC_FILTER_N, ux);
     float fy = (float)py + 0.5f + lerp_table(S->filter, ORC_FILTER_N, uy);
     float sx = fmaf(fx, S->inv_w2, -1.0f) * c[12];

@@ -198,13 +198,13 @@ def test_tiles_equal_wavefront_full_resolution(ctx, rr, s04):
 def test_ray_counts_match_oracle(ctx, rr, s04, path):
     """rr_frame_stats' ray counts equal the oracle's on a frame where paths
     leak into the cube through an edge crack and bounce inside it (04vs frame
-    22, 1920x1080 x 4 spp: two paths past bounce 1, found by the oracle).
+    6, 1920x1080 x 4 spp: a path past bounce 1, found by the oracle).
     k_tiles once counted its ballots inside the live-lane branch, which lost
     bounces run while the wave's lane 0 was already dead, without changing a
     pixel."""
     p = rr.default_params(spp=4, flags=PATHS[path])
-    film, _, st = ctx.render_to_memory(s04, 22, p)
-    of, _ = O.render_state(ctx.frame_state(s04, 22, rr.default_params(spp=4)))
+    film, _, st = ctx.render_to_memory(s04, 6, p)
+    of, _ = O.render_state(ctx.frame_state(s04, 6, rr.default_params(spp=4)))
     assert np.array_equal(film, of)
     (c0, s0, c1, s1), late = O.ray_counts()
     print(f"{path}: oracle continuations {c0} + {c1}, shadow rays {s0} + {s1}, late paths {late[:3]}")
