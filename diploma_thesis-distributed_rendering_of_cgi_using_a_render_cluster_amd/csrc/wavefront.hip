@@ -99,6 +99,7 @@ struct SceneView {
     FloatP lut;  // material tables (kMatLutStride floats per material, build_material_lut)
     lds_f4w* cam = nullptr;  // LDS scenes, camera kernels: 3 float4 per triangle (stage_camera)
     lds_f4w* nrm = nullptr;   // LDS scenes, shading kernels: unit geometric normal per triangle
+    lds_f4w* matd = nullptr;  // LDS scenes, shading kernels: each material with its derived terms (kMatDF4)
 };
 using GlobalView = SceneView<const BvhNode*, const TriPack*, const float*>;
 using LdsView = SceneView<lds_node*, lds_tri*, lds_float*>;
@@ -117,12 +118,32 @@ __device__ __forceinline__ Mat load_mat(FloatP mats, int id) {
     return r;
 }
 
-// Material `id` with its derived BSDF terms (mat_derive at load: staging them
-// in LDS measured slower — 2 more LDS reads and more live registers).
+// Material `id` with its derived BSDF terms: LDS-resident scenes stage them
+// per material (stage_scene: load_mat + mat_derive once per block, the same
+// operations, so the same bits), 4 float4 a shading point reads instead of
+// deriving them per sample; scenes in HBM derive at load.
+constexpr int kMatDF4 = 4;
+//   [0] base.xyz, roughness  [1] emission.xyz, model  [2] alpha, a2, kd0, spec_on  [3] cspec0.xyz, 0
 template <typename View>
 RR_D Mat view_mat(const View& v, int id) {
-    Mat m = load_mat(v.mats, id);
-    mat_derive(m);
+    Mat m;
+    if constexpr (std::is_same<View, LdsView>::value) {
+        const lds_f4w* q = v.matd + kMatDF4 * id;
+        const float4 a = lds_ld4(q), b = lds_ld4(q + 1), c = lds_ld4(q + 2), d = lds_ld4(q + 3);
+        m.base = xyz(a);
+        m.roughness = a.w;
+        m.emission = xyz(b);
+        m.model = f2i(b.w);
+        m.alpha = c.x;
+        m.a2 = c.y;
+        m.kd0 = c.z;
+        m.spec_on = f2i(c.w);
+        m.cspec0 = xyz(d);
+        m.metallic = m.specular = m.ior = 0.0f;  // used by mat_derive only
+    } else {
+        m = load_mat(v.mats, id);
+        mat_derive(m);
+    }
     return m;
 }
 
@@ -574,6 +595,21 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
             q[i] = x;
         }
         q += a.n_tris;
+        v.matd = q;  // derived material records (view_mat)
+        for (int i = threadIdx.x; i < a.n_mats; i += kBlock) {
+            Mat m = load_mat(v.mats, i);
+            mat_derive(m);
+            rr_f4v r0, r1, r2, r3;
+            r0.x = m.base.x; r0.y = m.base.y; r0.z = m.base.z; r0.w = m.roughness;
+            r1.x = m.emission.x; r1.y = m.emission.y; r1.z = m.emission.z; r1.w = i2f(m.model);
+            r2.x = m.alpha; r2.y = m.a2; r2.z = m.kd0; r2.w = i2f(m.spec_on);
+            r3.x = m.cspec0.x; r3.y = m.cspec0.y; r3.z = m.cspec0.z; r3.w = 0.0f;
+            q[kMatDF4 * i] = r0;
+            q[kMatDF4 * i + 1] = r1;
+            q[kMatDF4 * i + 2] = r2;
+            q[kMatDF4 * i + 3] = r3;
+        }
+        q += kMatDF4 * a.n_mats;
     }
     if constexpr (kCam) {
         v.cam = q;
@@ -1847,12 +1883,13 @@ size_t scene_budget_bytes(const FrameConsts& fc) {  // the residency test's meas
                  3 * (size_t)fc.n_lights + kFilterN / 4);
 }
 // What stage_scene stages (without the camera data): + the normals (1 float4
-// per triangle) when shading.
+// per triangle) and the derived material records when shading.
 size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
     const int n_nodes = std::max(fc.n_tris - 1, 1);
     size_t f4 = 4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris;
     if (shading)
-        f4 += (3 + kMatLutStride / 4) * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4 + (size_t)fc.n_tris;
+        f4 += (3 + kMatDF4 + kMatLutStride / 4) * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4 +
+              (size_t)fc.n_tris;
     return 16 * f4;
 }
 }  // namespace
