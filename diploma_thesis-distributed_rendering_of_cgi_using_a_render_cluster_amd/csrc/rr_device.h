@@ -927,14 +927,14 @@ RR_HD float3 sample_vndf(float3 v, float alpha, float dx, float dy) {
 // Sample a direction; returns false when the path must end. f: f * cosL as
 // bsdf_eval_v. glossy: the specular lobe was picked (Cycles LABEL_GLOSSY;
 // else LABEL_DIFFUSE), which decides the bounce counter the scatter advances.
+// (T, B): make_onb(N), which LDS-resident scenes stage per triangle side
+// (wavefront.hip stage_scene) instead of computing it per sample.
 template <typename FloatP>
-RR_HD bool bsdf_sample(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, float3 wo, float ul, float u1,
-                       float u2, float3& wi, float3& f, float& pdf, bool& glossy) {
+RR_HD bool bsdf_sample_onb(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, float3 T, float3 B, float3 wo,
+                           float ul, float u1, float u2, float3& wi, float3& f, float& pdf, bool& glossy) {
     const float cosV = vw.cosV;
     if (cosV <= 0.0f) return false;
     const float ps = vw.ps;
-    float3 T, B;
-    make_onb(N, T, B);
     float x, y;  // the disk sample both lobes start from
     concentric_disk(u1, u2, x, y);
     glossy = ul < ps;
@@ -951,6 +951,14 @@ RR_HD bool bsdf_sample(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, f
     }
     f = bsdf_eval_v(m, lut, vw, N, wo, wi, pdf);
     return pdf > 0.0f;
+}
+template <typename FloatP>
+RR_HD bool bsdf_sample(const Mat& m, FloatP lut, const BsdfView& vw, float3 N, float3 wo, float ul, float u1,
+                       float u2, float3& wi, float3& f, float& pdf, bool& glossy) {
+    if (vw.cosV <= 0.0f) return false;
+    float3 T, B;
+    make_onb(N, T, B);
+    return bsdf_sample_onb(m, lut, vw, N, T, B, wo, ul, u1, u2, wi, f, pdf, glossy);
 }
 
 RR_HD float3 clamp_contrib(float3 c, float clamp) {

@@ -100,6 +100,7 @@ struct SceneView {
     lds_f4w* cam = nullptr;  // LDS scenes, camera kernels: 3 float4 per triangle (stage_camera)
     lds_f4w* nrm = nullptr;   // LDS scenes, shading kernels: unit geometric normal per triangle
     lds_f4w* matd = nullptr;  // LDS scenes, shading kernels: each material with its derived terms (kMatDF4)
+    lds_f4w* onb = nullptr;   // LDS scenes, shading kernels: make_onb of both sides' normals (kOnbF4 per triangle)
 };
 using GlobalView = SceneView<const BvhNode*, const TriPack*, const float*>;
 using LdsView = SceneView<lds_node*, lds_tri*, lds_float*>;
@@ -214,6 +215,7 @@ __device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, i
 
 // Staged material word of LDS-resident scenes: material id | hull_flags << kHullShift.
 constexpr int kHullShift = 30;
+constexpr int kOnbF4 = 4;  // staged shading frames per triangle (stage_scene)
 
 struct ShadeOut {
     bool cont, shadow;
@@ -383,7 +385,16 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     bool glossy;
     float u_b1, u_b2;
     rng2(key, dim0 + 4u, u_b1, u_b2);
-    if (!bsdf_sample(m, lut, vw, N, wo, u_lobe, u_b1, u_b2, wi, f, pdf, glossy)) return;
+    bool sampled;
+    if constexpr (std::is_same<View, LdsView>::value) {  // the staged frame of the hit side
+        const lds_f4w* fr = v.onb + kOnbF4 * h.idx + (flip ? 2 : 0);
+        const float4 tb = lds_ld4(fr), bb = lds_ld4(fr + 1);
+        sampled = bsdf_sample_onb(m, lut, vw, N, xyz(tb), mk3(tb.w, bb.x, bb.y), wo, u_lobe, u_b1, u_b2, wi, f, pdf,
+                                  glossy);
+    } else {
+        sampled = bsdf_sample(m, lut, vw, N, wo, u_lobe, u_b1, u_b2, wi, f, pdf, glossy);
+    }
+    if (!sampled) return;
     const float k = 1.0f / pdf;  // f = f * cosL already
     T = mk3(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
     if (!(max3f(T) > 0.0f)) return;
@@ -610,6 +621,25 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
             q[kMatDF4 * i + 3] = r3;
         }
         q += kMatDF4 * a.n_mats;
+        // the shading frame (T, B) = make_onb(N) of both sides of each
+        // triangle, computed here once instead of per sample (the same
+        // operations, so the same bits): side s at [kOnbF4 i + 2 s] = (T, B.x),
+        // [kOnbF4 i + 2 s + 1] = (B.y, B.z, -, -)
+        v.onb = q;
+        __syncthreads();  // the normals above are visible
+        for (int j = threadIdx.x; j < 2 * a.n_tris; j += kBlock) {
+            const int i = j >> 1, side = j & 1;
+            const float4 nm = lds_ld4(v.nrm + i);
+            const float3 n = side ? mk3(-nm.x, -nm.y, -nm.z) : xyz(nm);
+            float3 t, b;
+            make_onb(n, t, b);
+            rr_f4v x, y;
+            x.x = t.x; x.y = t.y; x.z = t.z; x.w = b.x;
+            y.x = b.y; y.y = b.z; y.z = 0.0f; y.w = 0.0f;
+            q[kOnbF4 * i + 2 * side] = x;
+            q[kOnbF4 * i + 2 * side + 1] = y;
+        }
+        q += kOnbF4 * a.n_tris;
     }
     if constexpr (kCam) {
         v.cam = q;
@@ -1889,7 +1919,7 @@ size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
     size_t f4 = 4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris;
     if (shading)
         f4 += (3 + kMatDF4 + kMatLutStride / 4) * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4 +
-              (size_t)fc.n_tris;
+              (size_t)(1 + kOnbF4) * fc.n_tris;
     return 16 * f4;
 }
 }  // namespace
