@@ -86,7 +86,7 @@ def trace(tris: np.ndarray, rays: np.ndarray, width: int = 2):
 
 
 def build_qbvh(tris: np.ndarray, with_order: bool = False):
-    """Quantised wide BVH: (children (n, QW), nodes (n, 16) uint32) as rr_debug_bvh4;
+    """Quantised 6-wide hierarchy: (children (n, QW), nodes (n, 16) uint32) as rr_debug_qbvh;
     with_order: also the original triangle id of each position of the BVH4's
     triangle array (the order its leaf ranges index)."""
     tris = _f32(tris).reshape(-1, 9)
