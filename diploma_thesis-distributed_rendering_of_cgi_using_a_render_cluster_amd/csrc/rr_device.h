@@ -938,16 +938,23 @@ RR_HD bool bsdf_sample_onb(const Mat& m, FloatP lut, const BsdfView& vw, float3 
     float x, y;  // the disk sample both lobes start from
     concentric_disk(u1, u2, x, y);
     glossy = ul < ps;
+    // the lobe's direction in the local frame: the GGX half vector (glossy)
+    // or the cosine-weighted point (diffuse); one frame3 for both, so a wave
+    // whose lanes picked both lobes runs it once
+    float3 l;
     if (glossy) {
         const float3 wl = mk3(dot3(wo, T), dot3(wo, B), cosV);
-        const float3 hl = sample_vndf(wl, m.alpha, x, y);
-        const float3 H = frame3(T, B, N, hl.x, hl.y, hl.z);
-        const float k = 2.0f * dot3(wo, H);
-        wi = mk3(fmaf(H.x, k, -wo.x), fmaf(H.y, k, -wo.y), fmaf(H.z, k, -wo.z));
+        l = sample_vndf(wl, m.alpha, x, y);
     } else {
         // 1 - x^2 - y^2 of a disk point: 0 or at least 2^-70 (sqrt_rn's range)
-        const float z = sqrt_rn(fmaxf(0.0f, fmaf(-y, y, fmaf(-x, x, 1.0f))));
-        wi = frame3(T, B, N, x, y, z);
+        l = mk3(x, y, sqrt_rn(fmaxf(0.0f, fmaf(-y, y, fmaf(-x, x, 1.0f)))));
+    }
+    const float3 W = frame3(T, B, N, l.x, l.y, l.z);
+    if (glossy) {  // reflect wo about the half vector
+        const float k = 2.0f * dot3(wo, W);
+        wi = mk3(fmaf(W.x, k, -wo.x), fmaf(W.y, k, -wo.y), fmaf(W.z, k, -wo.z));
+    } else {
+        wi = W;
     }
     f = bsdf_eval_v(m, lut, vw, N, wo, wi, pdf);
     return pdf > 0.0f;
