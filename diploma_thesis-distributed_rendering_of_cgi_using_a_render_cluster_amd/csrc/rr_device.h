@@ -635,6 +635,46 @@ RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, floa
     return hits;
 }
 
+// q6_box_hits that keeps only the nearest hit internal child (ties: lower
+// slot) instead of every entry distance: six fewer live registers in the
+// per-lane walk (TravStateQ6); best = -1 when no internal child is hit.
+RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, uint32_t imask, int& best) {
+    const uint32_t eb = (uint32_t)f2i(n.org.w);
+    const float sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
+    const float sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
+    const float sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
+    const float ox = (n.org.x - o.x) * iq.x, oy = (n.org.y - o.y) * iq.y, oz = (n.org.z - o.z) * iq.z;
+    const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
+    const uint32_t nx = px ? n.a.z : n.b.y, fx = px ? n.b.y : n.a.z;
+    const uint32_t ny = py ? n.a.w : n.b.z, fy = py ? n.b.z : n.a.w;
+    const uint32_t nz = pz ? n.b.x : n.b.w, fz = pz ? n.b.w : n.b.x;
+    const uint32_t lox = n.c.x & 0xffffu, loy = n.c.x >> 16, loz = n.c.y & 0xffffu;
+    const uint32_t hix = n.c.y >> 16, hiy = n.c.z & 0xffffu, hiz = n.c.z >> 16;
+    const uint32_t nx2 = px ? lox : hix, fx2 = px ? hix : lox;
+    const uint32_t ny2 = py ? loy : hiy, fy2 = py ? hiy : loy;
+    const uint32_t nz2 = pz ? loz : hiz, fz2 = pz ? hiz : loz;
+    uint32_t hits = 0;
+    best = -1;
+    float bt = 0.0f;
+#pragma unroll
+    for (int c = 0; c < kQWidth; ++c) {
+        const int sh = c < 4 ? 8 * c : 8 * (c - 4);
+        const uint32_t qnx = c < 4 ? nx : nx2, qny = c < 4 ? ny : ny2, qnz = c < 4 ? nz : nz2;
+        const uint32_t qfx = c < 4 ? fx : fx2, qfy = c < 4 ? fy : fy2, qfz = c < 4 ? fz : fz2;
+        const float t0 = fmaxf(fmaxf(fmaf((float)((qnx >> sh) & 255u), sx, ox), fmaf((float)((qny >> sh) & 255u), sy, oy)),
+                               fmaxf(fmaf((float)((qnz >> sh) & 255u), sz, oz), tmin));
+        const float t1 = fminf(fminf(fmaf((float)((qfx >> sh) & 255u), sx, ox), fmaf((float)((qfy >> sh) & 255u), sy, oy)),
+                               fminf(fmaf((float)((qfz >> sh) & 255u), sz, oz), tcur));
+        const bool hit = t0 <= t1;
+        if (hit) hits |= 1u << c;
+        if (hit && ((imask >> c) & 1u) && (best < 0 || t0 < bt)) {
+            best = c;
+            bt = t0;
+        }
+    }
+    return hits;
+}
+
 // Node fetch of the 6-wide walk. The split-path trace kernels keep a copy of
 // the first n_top nodes in LDS (Q6Nodes): nodes are numbered breadth first,
 // so those are the top levels of the tree, which every ray visits — each of
@@ -688,10 +728,10 @@ struct TravStateQ6 {
     RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
         if (kCount) ++cnt.nodes;
         const float tcur = h.t;
-        float tn[kQWidth];
         const QNode6 nd = q6_load(nodes, node);
-        const uint32_t hm = q6_box_hits(nd, o, iq, tmin, tcur, tn);
         const uint32_t imask = q6_inner(nd);
+        int best;
+        const uint32_t hm = q6_box_best(nd, o, iq, tmin, tcur, imask, best);
         uint32_t leaves = hm & ~imask;
         const uint32_t inner = hm & imask;
         // passing leaves in slot order; the loop runs as often as the lane with
@@ -709,19 +749,8 @@ struct TravStateQ6 {
             node = st.pop();
             return false;
         }
-        // nearest hit child next (ties: lower slot); the other hit children are
-        // pushed in descending slot order (so they pop in slot order)
-        int best = __builtin_ctz(inner);
-        float bt = tn[0];
-#pragma unroll
-        for (int c = 1; c < kQWidth; ++c)
-            if (best == c) bt = tn[c];
-#pragma unroll
-        for (int c = 1; c < kQWidth; ++c)
-            if (((inner >> c) & 1u) && c > best && tn[c] < bt) {
-                bt = tn[c];
-                best = c;
-            }
+        // nearest hit child next (ties: lower slot, q6_box_best); the other hit
+        // children are pushed in descending slot order (so they pop in slot order)
         const uint32_t rest = inner & ~(1u << best);
         const int base = (int)nd.a.x;
 #pragma unroll
