@@ -742,11 +742,12 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
                 if (any && h->idx >= 0) return 1;
             }
         }
-        /* nearest hit internal child next (ties: lower slot); the others are
-         * pushed in descending slot order */
+        /* nearest hit internal child next (ties: lower slot; any-hit rays:
+         * the lowest hit internal slot); the others are pushed in descending
+         * slot order */
         int best = -1;
         for (int c = 0; c < ORC_QW_MAX; ++c)
-            if (k[c].t != INFINITY && (best < 0 || k[c].t < k[best].t)) best = c;
+            if (k[c].t != INFINITY && (best < 0 || (!any && k[c].t < k[best].t))) best = c;
         if (best < 0) {
             if (sp == 0) break;
             node = stack[--sp];
