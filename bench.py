@@ -395,11 +395,12 @@ def spawn_ranks(args) -> int:
 
 def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin frame 1", spp_scale: float = 1.0,
                  threads: int | None = None):
-    """Oracle (C restatement, OpenMP) on the host cores: 4-row bands of the same
-    frame, taken in an order spread over the image, until the budget is spent or
-    the frame is done; extrapolated to frames/s with ONE hierarchy build per
-    frame (each band call rebuilds it; its build time, orc_last_build_seconds,
-    is taken out of the band's time and counted once). Threads: OMP_NUM_THREADS
+    """Oracle (C restatement, OpenMP) on the host cores: bands of the same
+    frame (4 rows, or more where each call's hierarchy build outweighs a 4-row
+    band's render), taken in an order spread over the image, until the budget
+    is spent or the frame is done; extrapolated to frames/s with ONE hierarchy
+    build per frame (each band call rebuilds it; its build time,
+    orc_last_build_seconds, is taken out of the band's time and counted once). Threads: OMP_NUM_THREADS
     when the environment sets it (the GPU box gives one GPU's job a 16-core
     share and sets it; nproc there counts the whole machine), else every core
     this process may run on. spp_scale: the frame's samples over the samples
@@ -408,27 +409,40 @@ def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin 
     usable, nproc, model = host_cpu()
     if threads is None:
         threads = int(os.environ.get("OMP_NUM_THREADS") or usable)
-    bands = list(range(0, H, 4))
     done_rows, t_used, t_render, builds = 0, 0.0, 0.0, []
-    order = [b for k in range(16) for b in bands[k::16]]
-    for b in order:
+    band_h = 4
+
+    def band(b, h):
+        nonlocal done_rows, t_used, t_render
         t0 = time.perf_counter()
-        oracle_mod.render_state(state, rows=(b, min(b + 4, H)), threads=threads, film=False)
+        oracle_mod.render_state(state, rows=(b, min(b + h, H)), threads=threads, film=False)
         dt = time.perf_counter() - t0
         tb = min(oracle_mod.last_build_seconds(), dt)
         builds.append(tb)
         t_used += dt
         t_render += dt - tb
-        done_rows += min(b + 4, H) - b
+        done_rows += min(b + h, H) - b
+        return tb, dt - tb
+
+    # the first 4-row band measures the per-call hierarchy build against the
+    # render; where the build dominates (C5: ~3.5 s a call), later bands grow
+    # to about the build's cost in rows, so the budget renders more rows
+    tb0, tr0 = band(0, 4)
+    if tr0 > 0.0:
+        band_h = 4 * max(1, min(16, int(round(tb0 / tr0))))
+    bands = list(range(band_h, H, band_h)) if band_h > 4 else list(range(4, H, 4))
+    order = [b for k in range(16) for b in bands[k::16]]
+    for b in order:
         if t_used >= budget_s:
             break
+        band(b, band_h)
     frac = done_rows / H
     t_build = sum(builds) / len(builds)
     t_frame = t_build + t_render / frac * spp_scale
     return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads, "kind": "port",
             "host": {"nproc": nproc, "affinity_cores": usable, "cpu_model": model,
                      "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
-            "sample": f"{done_rows} of {H} rows (4-row bands spread over the frame) of {label} "
+            "sample": f"{done_rows} of {H} rows ({band_h}-row bands spread over the frame after a first 4-row band) of {label} "
                       f"at {int(state.render_ints[0])}x{H}, {int(state.render_ints[2])} spp, "
                       f"{t_used:.1f} s in {len(builds)} band calls; frame time = one hierarchy build "
                       f"({t_build:.3f} s) + the bands' render time extrapolated to the whole frame; "
