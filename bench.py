@@ -426,29 +426,65 @@ def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin 
 
     # the first 4-row band measures the per-call hierarchy build against the
     # render; where the build dominates (C5: ~3.5 s a call), later bands grow
-    # to about the build's cost in rows, so the budget renders more rows
+    # to about the build's cost in rows, so the budget renders more rows. The
+    # later bands tile rows 4.. H and are taken in an order spread over the
+    # frame; the extrapolation uses them alone (the first band is always the
+    # top rows, usually background) unless the frame gets done whole.
     tb0, tr0 = band(0, 4)
     if tr0 > 0.0:
         band_h = 4 * max(1, min(16, int(round(tb0 / tr0))))
-    bands = list(range(band_h, H, band_h)) if band_h > 4 else list(range(4, H, 4))
+    first = (done_rows, t_render)
+    bands = list(range(4, H, band_h))
     order = [b for k in range(16) for b in bands[k::16]]
     for b in order:
         if t_used >= budget_s:
             break
         band(b, band_h)
-    frac = done_rows / H
+    if done_rows < H and done_rows > first[0]:  # a sample: the spread bands only
+        frac = (done_rows - first[0]) / H
+        rendered = t_render - first[1]
+    else:
+        frac, rendered = done_rows / H, t_render
     t_build = sum(builds) / len(builds)
-    t_frame = t_build + t_render / frac * spp_scale
+    t_frame = t_build + rendered / frac * spp_scale
     return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads, "kind": "port",
             "host": {"nproc": nproc, "affinity_cores": usable, "cpu_model": model,
                      "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
-            "sample": f"{done_rows} of {H} rows ({band_h}-row bands spread over the frame after a first 4-row band) of {label} "
+            "sample": f"{done_rows} of {H} rows ({band_h}-row bands spread over rows 4..{H} after a first 4-row band "
+                      f"that sizes them and is left out of the extrapolation) of {label} "
                       f"at {int(state.render_ints[0])}x{H}, {int(state.render_ints[2])} spp, "
                       f"{t_used:.1f} s in {len(builds)} band calls; frame time = one hierarchy build "
                       f"({t_build:.3f} s) + the bands' render time extrapolated to the whole frame; "
                       f"render only (no encode)"
                       + (f"; rendered at {int(state.render_ints[2])} spp, render time scaled by {spp_scale:g}"
                          if spp_scale != 1.0 else "")}
+
+
+# The reference master's frame-dispatch loops (master/src/cluster/strategies.rs):
+# each pass tops the workers' queues up and then sleeps, so a worker receives at
+# most `per_pass` frames per sleep period whatever its render speed.
+DISPATCH = {"naive-fine": {"sleep_ms": 50, "source": "strategies.rs:20-64 (one frame to an empty queue, 50 ms sleep)"},
+            "eager-naive-coarse": {"sleep_ms": 100,
+                                   "source": "strategies.rs:70-146 (queue topped up to target_queue_size, 100 ms sleep)"},
+            "dynamic": {"sleep_ms": 50,
+                        "source": "strategies.rs:171-401 (queue topped up to target_queue_size, 50 ms sleep)"}}
+
+
+def dispatch_ceiling(job_dict: dict, workers: int) -> dict:
+    """Upper bound on the whole-job frames/s of BASELINE's metric (frames over
+    the master trace's job_finish_time - job_start_time, master/src/cluster/
+    mod.rs:590,666-668) set by the unchanged master's dispatch cadence alone
+    (no message latency, instant renders): workers x frames per pass / sleep."""
+    strat = job_dict.get("frame_distribution_strategy") or {}
+    kind = strat.get("strategy_type", "naive-fine")
+    d = DISPATCH.get(kind, DISPATCH["naive-fine"])
+    per_pass = 1 if kind == "naive-fine" else int(strat.get("target_queue_size", 1))
+    return {"value": round(workers * per_pass * 1000.0 / d["sleep_ms"], 1), "unit": "frames/s",
+            "strategy": kind, "frames_per_pass_per_worker": per_pass, "sleep_ms": d["sleep_ms"], "workers": workers,
+            "source": "/root/reference/master/src/cluster/" + d["source"],
+            "note": "what the reference master can dispatch to this many workers; bench.py's value times the "
+                    "worker's render loop with its queue kept full (no master in the loop), i.e. the renderer's "
+                    "rate: under the unchanged master the job runs at most min(value, this ceiling)"}
 
 
 def names_idx(cls: str, rr) -> int:
@@ -744,6 +780,20 @@ def main():
                 w1 = cpu_baseline(O, state, args.cpu_seconds / 2, f"{args.workload} frame {f_count}",
                                   spp_scale=spp_full / spp_cpu, threads=4)
                 cpu["thesis_point_w1_t4"] = {k: w1[k] for k in ("value", "unit", "cores", "sample")}
+                # BASELINE.md §2 times W x T = nproc; this job may use a 16-core
+                # share of the box (OMP_NUM_THREADS), so the whole host is a
+                # projection from the measured points, never a measurement
+                usable, nproc, _ = host_cpu()
+                if cpu.get("value") and w1.get("value") and cpu["cores"] > w1["cores"]:
+                    eff = (cpu["value"] / w1["value"]) / (cpu["cores"] / w1["cores"])
+                    cpu["whole_host_projection"] = {
+                        "value": round(cpu["value"] * nproc / cpu["cores"], 4), "unit": "frames/s", "cores": nproc,
+                        "kind": "projection",
+                        "scaling_eff_measured": round(eff, 3),
+                        "note": f"linear in threads from the {cpu['cores']}-thread point to nproc = {nproc} "
+                                f"(an upper bound: {w1['cores']} -> {cpu['cores']} threads scaled at {eff:.2f} of "
+                                f"linear); not run: the job's CPU share on the GPU box is OMP_NUM_THREADS = "
+                                f"{os.environ.get('OMP_NUM_THREADS')} of {usable} usable"}
             except Exception as e:  # baseline is reported, never the target
                 cpu = {"value": None, "unit": "frames/s", "error": str(e)}
         traced = rays["camera_traced"] + rays["extension"] + rays["shadow"]
@@ -767,6 +817,11 @@ def main():
                 round(traced / args.steps / (sum(roof_ms) / max(roof_steps, 1) * 1e-3) / 1e6, 1)
                 if sum(roof_ms) > 0 else None),
             "rays_per_frame": {k: v // max(args.steps, 1) for k, v in rays.items()},
+            "rays_note": "camera = W x H x spp samples; camera_traced = those tested against a triangle (the rest "
+                         "lie outside the scene's screen rectangle or meet no triangle of their tile and are "
+                         "resolved as background without a ray); mrays_per_s_per_gpu counts traced rays only",
+            "whole_job_ceiling_frames_s": dispatch_ceiling(job.to_dict(), world),
+            "value_under_reference_master_max": round(min(value, dispatch_ceiling(job.to_dict(), world)["value"]), 4),
             "device_ms_per_frame": round(sum(roof_ms) / max(roof_steps, 1), 3),
             "kernels": per_class,
             "roofline": roofline,

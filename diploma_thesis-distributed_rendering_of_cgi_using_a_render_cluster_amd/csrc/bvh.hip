@@ -316,8 +316,8 @@ __global__ __launch_bounds__(kBlock) void k_refit(int n, const uint32_t* __restr
     const float4 a = world[3 * orig], b = world[3 * orig + 1], c = world[3 * orig + 2];
     TriPack tp;
     tp.p0 = make_float4(a.x, a.y, a.z, i2f(orig));
-    tp.p1 = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, i2f(tri_mat[orig]));
-    tp.p2 = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.0f);
+    tp.p1 = make_float4(b.x, b.y, b.z, i2f(tri_mat[orig]));
+    tp.p2 = make_float4(c.x, c.y, c.z, 0.0f);
     tris[i] = tp;
     float bx[6] = {fminf(fminf(a.x, b.x), c.x), fminf(fminf(a.y, b.y), c.y), fminf(fminf(a.z, b.z), c.z),
                    fmaxf(fmaxf(a.x, b.x), c.x), fmaxf(fmaxf(a.y, b.y), c.y), fmaxf(fmaxf(a.z, b.z), c.z)};
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kBlock) void k_qw_emit(const int32_t* __restrict__ 
     o.org = make_float4(org[0], org[1], org[2], i2f((int)(eb | inner << 24)));
     o.a = make_uint4((uint32_t)inner_base, (uint32_t)tri_base, w[0], w[1]);
     o.b = make_uint4(w[2], w[3], w[4], w[5]);
-    o.c = make_uint4(w[6], w[7], w[8], 0u);
+    o.c = make_uint4(w[6], w[7], w[8], (1u << S.m) - 1u);  // used slots
     out[idx] = o;
 }
 
@@ -554,8 +554,8 @@ __global__ __launch_bounds__(kBlock) void k_ploc_init(int n, const uint32_t* __r
     const float4 a = world[3 * orig], b = world[3 * orig + 1], c = world[3 * orig + 2];
     TriPack tp;
     tp.p0 = make_float4(a.x, a.y, a.z, i2f(orig));
-    tp.p1 = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, i2f(tri_mat[orig]));
-    tp.p2 = make_float4(c.x - a.x, c.y - a.y, c.z - a.z, 0.0f);
+    tp.p1 = make_float4(b.x, b.y, b.z, i2f(tri_mat[orig]));
+    tp.p2 = make_float4(c.x, c.y, c.z, 0.0f);
     tris[i] = tp;
     cl[2 * i] = make_float4(fminf(fminf(a.x, b.x), c.x), fminf(fminf(a.y, b.y), c.y), fminf(fminf(a.z, b.z), c.z),
                             i2f(~i));
@@ -722,8 +722,8 @@ __global__ __launch_bounds__(kSmallBuild) void k_build_small(
         const float3 a = wv[i][0], b = wv[i][1], e = wv[i][2];
         TriPack tp;
         tp.p0 = make_float4(a.x, a.y, a.z, i2f(i));
-        tp.p1 = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, i2f(tri_mat[i]));
-        tp.p2 = make_float4(e.x - a.x, e.y - a.y, e.z - a.z, 0.0f);
+        tp.p1 = make_float4(b.x, b.y, b.z, i2f(tri_mat[i]));
+        tp.p2 = make_float4(e.x, e.y, e.z, 0.0f);
         tris[r] = tp;
         lbox[r][0] = fminf(fminf(a.x, b.x), e.x);
         lbox[r][1] = fminf(fminf(a.y, b.y), e.y);

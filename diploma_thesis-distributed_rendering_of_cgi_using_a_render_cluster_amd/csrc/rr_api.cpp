@@ -668,6 +668,7 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
         const unsigned long long t0 = ~w[10], t1 = w[11];
         st->kernel_wave_fill = (w[8] && t1 > t0) ? (double)w[9] / (double)w[8] / (double)(t1 - t0) : 0.0;
     }
+    st->stack_drops = (int32_t)std::min<unsigned long long>(r.trav[kTravDropWord], 0x7fffffffull);
     st->build_ms = r.rebuilt ? r.build_ms : 0.0;
     st->trace_ms = r.trace_ms;
     st->readback_ms = r.readback_ms;
@@ -1082,6 +1083,17 @@ int rr_debug_jpeg_device(rr_ctx* c, const uint8_t* rgba8, int32_t w, int32_t h, 
         dtab.release();
         return RR_OK;
     });
+}
+
+int rr_debug_scene_mesh(rr_scene* s, float* tri_local9, int32_t* tri_object) {
+    if (!s) return fail(RR_EINVAL, "scene is NULL");
+    const size_t n = s->desc.tri_obj.size();
+    if (tri_local9)
+        for (size_t i = 0; i < n; ++i)
+            for (int k = 0; k < 3; ++k)
+                for (int a = 0; a < 3; ++a) tri_local9[9 * i + 3 * k + a] = s->desc.tri_local[12 * i + 4 * k + a];
+    if (tri_object && n) std::memcpy(tri_object, s->desc.tri_obj.data(), n * sizeof(int32_t));
+    return RR_OK;
 }
 
 int rr_debug_counts(rr_scene* s, int32_t* nt, int32_t* nl, int32_t* nm, int32_t* no) {

@@ -52,9 +52,11 @@ static_assert(sizeof(BvhNode) == 64, "node must be one 64-byte line");
 //   a        x: first internal child's node index, y: first leaf child's
 //            triangle position, z / w: lo x / lo y of children 0..3 (byte c)
 //   b        lo z, hi x, hi y, hi z of children 0..3 (byte c)
-//   c        children 4, 5 as byte pairs: x (lo x, lo y), y (lo z, hi x), z (hi y, hi z), w 0
-// An unused slot has lo 255 and hi 0 on every axis: its box test always
-// fails. oracle/rr_oracle.c q4_pack / trace4 restate the layout and the walk.
+//   c        children 4, 5 as byte pairs: x (lo x, lo y), y (lo z, hi x), z (hi y, hi z),
+//            w: mask of the used slots
+// An unused slot has lo 255 and hi 0 on every axis, and its bit of c.w is 0:
+// its box test always fails. oracle/rr_oracle.c q4_pack / trace4 restate the
+// layout and the walk.
 constexpr int kQWidth = 6;
 struct alignas(16) QNode6 {
     float4 org;
@@ -102,12 +104,16 @@ RR_HD float3 rcp3(float3 d) {
     return make_float3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
 }
 
-// Triangle in leaf order, 48 B: v0 | e1 = v1-v0 | e2 = v2-v0, with the original
-// triangle id and material id in the .w lanes.
+// Triangle in leaf order, 48 B: the three world vertices as the transform
+// wrote them, with the original triangle id and material id in the .w lanes.
+// The vertices themselves (not v0 and two edge vectors) so that triangles
+// sharing a vertex see the same bits of it: the watertight test (woop_test)
+// needs that. The edges e1 = v1 - v0, e2 = v2 - v0 of the shading normal are
+// the same subtractions the build used to store (the same bits).
 struct alignas(16) TriPack {
     float4 p0;  // v0.xyz, orig id (int bits)
-    float4 p1;  // e1.xyz, material (int bits)
-    float4 p2;  // e2.xyz, 0
+    float4 p1;  // v1.xyz, material (int bits)
+    float4 p2;  // v2.xyz, 0
 };
 static_assert(sizeof(TriPack) == 48, "tri pack is 48 bytes");
 
@@ -389,43 +395,134 @@ RR_HD bool screen_rect(float3 pos, float3 right, float3 up, float3 back, float h
 }
 
 // ---------------------------------------------------------- intersection ---
+// Watertight traversal. The triangle test (woop_test) decides a hit exactly in
+// a 2D projection of the ray's own, so a ray never slips through the shared
+// edge or vertex of two triangles; the box tests must then open every box that
+// holds a triangle the test accepts. Their plane distances are rounded, so each
+// test widens the box by a margin that covers the rounding of both tests:
+// 2^-19 (32 units in the last place) of the larger of the coordinates involved
+// (the box's distance from the ray origin plus its extent, per axis; the
+// triangle test's projected vertices are exact to about 8 ulp of their distance
+// from the origin, the plane distances to about 13). The margin is a distance
+// along an axis; in t it is margin * |1/d| on that axis, subtracted from the
+// near planes and added to the far ones. oracle/rr_oracle.c restates both.
+constexpr float kBoxMargin = 0x1p-19f;
+
 // Slab test against [bmin,bmax]; inclusive so equal-t candidates survive (the
 // closest hit is then independent of traversal order, see closest_tri()).
-// Plane distances t = fmaf(b, invd, oi) with oi = -(o invd) per ray (rcp3).
-RR_HD bool slab(float3 oi, float3 invd, float bx0, float by0, float bz0, float bx1, float by1,
+// Plane distances t = fmaf(b, invd, oi) with oi = -(o invd) per ray (rcp3),
+// each axis widened by its margin em (slab_margin).
+RR_HD bool slab(float3 oi, float3 invd, float3 em, float bx0, float by0, float bz0, float bx1, float by1,
                 float bz1, float tmin, float tmax, float& tnear) {
     const float tx0 = fmaf(bx0, invd.x, oi.x), tx1 = fmaf(bx1, invd.x, oi.x);
     const float ty0 = fmaf(by0, invd.y, oi.y), ty1 = fmaf(by1, invd.y, oi.y);
     const float tz0 = fmaf(bz0, invd.z, oi.z), tz1 = fmaf(bz1, invd.z, oi.z);
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1) - em.x, fminf(ty0, ty1) - em.y), fmaxf(fminf(tz0, tz1) - em.z, tmin));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1) + em.x, fmaxf(ty0, ty1) + em.y), fminf(fmaxf(tz0, tz1) + em.z, tmax));
     tnear = tn;
     return tn <= tf;
 }
-
-// Moeller-Trumbore, two-sided, with the barycentric test done before the
-// division: with a = |det| and the numerators un = tv.pv, vn = d.qv taken with
-// det's sign, the ray meets the triangle iff 0 <= un <= a, vn >= 0, un + vn <= a
-// (no rounding in the sign flips); only then is 1/det computed for t, u, v.
-// Most leaf tests of a traversal miss, and they no longer divide.
-RR_HD bool bary_pass(float det, float un, float vn) {
-    const bool neg = det < 0.0f;
-    const float a = neg ? -det : det, su = neg ? -un : un, sv = neg ? -vn : vn;
-    return !(det == 0.0f) && !(su < 0.0f || su > a) && !(sv < 0.0f || su + sv > a);
+// The BVH2 walk's margins in t for one ray: kBoxMargin * (|o|_inf + r) * |1/d|
+// per axis, r = the largest |coordinate| of the scene box (every node box and
+// vertex lies within it, so |b - o| <= |o|_inf + r bounds the rounding of every
+// plane distance and projected vertex of the walk).
+RR_HD float3 slab_margin(float3 o, float3 invd, float r) {
+    const float m = (fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + r) * kBoxMargin;
+    return mk3(m * fabsf(invd.x), m * fabsf(invd.y), m * fabsf(invd.z));
 }
-RR_HD bool tri_test(float3 o, float3 d, float3 v0, float3 e1, float3 e2, float& t, float& u,
-                    float& v) {
-    const float3 pv = cross3(d, e2);
-    const float det = dot3(e1, pv);
-    const float3 tv = sub3(o, v0);
-    const float3 qv = cross3(tv, e1);
-    const float un = dot3(tv, pv), vn = dot3(d, qv);
-    if (!bary_pass(det, un, vn)) return false;
+
+// Watertight ray/triangle test (Woop, Benthin & Wald, JCGT 2(1) 2013). Per ray
+// (make_shear): kz = the axis of the largest |d| component, kx, ky the next two
+// cyclically, sx = d[kx] / d[kz], sy = d[ky] / d[kz], sz = 1 / d[kz]. Per
+// triangle: the vertices relative to the origin, permuted to (kx, ky, kz)
+// (rot3), sheared to 2D: x = a[kx] - sx a[kz], y = a[ky] - sy a[kz] — the
+// projection along d, the same bits of a vertex for every triangle that shares
+// it. The 2D edge functions U = cx by - cy bx, V = ax cy - ay cx, W = bx ay - by ax
+// (no fused multiply-add, so an edge shared by two triangles gives exactly
+// opposite values) decide the hit: inside iff U, V, W have no two opposite
+// signs. One that rounds to 0 is recomputed exactly (edge_exact: the paper's
+// double-precision fallback, done with two fused multiply-adds). So the projected
+// triangles of a closed mesh cover the plane with no gap: a ray that meets the
+// mesh hits at least one of its triangles, also on an edge or a vertex. Then
+// det = U + V + W, t = (U az + V bz + W cz) sz / det (the kz coordinates scaled
+// by sz), u = V / det and v = W / det (the weights of v1 and v2); the division
+// only for rays that pass.
+struct Shear {
+    float sx, sy, sz;
+    int kz;
+};
+// 1 / x: rcp_rn when every active lane's |x| is in [2^-126, 2^126) (one
+// wave-uniform test), else the IEEE division.
+RR_HD float rcp_any(float x) {
+#if __HIP_DEVICE_COMPILE__
+    if (__all(fabsf(x) >= 0x1p-126f && fabsf(x) < 0x1p126f)) return rcp_rn(x);
+#endif
+    return 1.0f / x;
+}
+// (a[kx], a[ky], a[kz]) for (kx, ky, kz) = (kz + 1, kz + 2, kz) mod 3.
+RR_HD float3 rot3(float3 a, int kz) {
+    const bool k0 = kz == 0, k1 = kz == 1;
+    return mk3(k0 ? a.y : (k1 ? a.z : a.x), k0 ? a.z : (k1 ? a.x : a.y), k0 ? a.x : (k1 ? a.y : a.z));
+}
+RR_HD Shear make_shear(float3 d) {
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    Shear s;
+    s.kz = ax >= ay ? (ax >= az ? 0 : 2) : (ay >= az ? 1 : 2);
+    const float3 r = rot3(d, s.kz);
+    s.sz = rcp_any(r.z);
+    s.sx = r.x * s.sz;
+    s.sy = r.y * s.sz;
+    return s;
+}
+// An edge function a b - c d that rounded to 0 (e = 0): then the products
+// p = a b and q = c d are equal floats, the exact value is the difference of
+// their rounding errors fma(a, b, -p) - fma(c, d, -q) (each exact without
+// underflow, and their difference is 0 only when the exact value is), which is
+// also what the same difference in double rounds to; the swapped edge
+// c d - a b of the neighbouring triangle gets exactly its negation. Other
+// values pass through.
+RR_HD float edge_exact(float a, float b, float c, float d, float e) {
+    if (e != 0.0f) return e;
+    return fmaf(a, b, -(a * b)) - fmaf(c, d, -(c * d));
+}
+// make_shear for a unit direction (camera rays): its largest component is at
+// least 1/sqrt(3) in magnitude, inside rcp_rn's range, so no range test.
+RR_HD Shear make_shear_unit(float3 d) {
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    Shear s;
+    s.kz = ax >= ay ? (ax >= az ? 0 : 2) : (ay >= az ? 1 : 2);
+    const float3 r = rot3(d, s.kz);
+    s.sz = rcp_rn(r.z);
+    s.sx = r.x * s.sz;
+    s.sy = r.y * s.sz;
+    return s;
+}
+// The test from the vertices relative to the origin, already permuted (a, b, c
+// = rot3(v - o, kz)).
+RR_HD bool woop_core(const Shear& s, float3 a, float3 b, float3 c, float& t, float& u, float& v) {
+    const float ax = fmaf(-s.sx, a.z, a.x), ay = fmaf(-s.sy, a.z, a.y);
+    const float bx = fmaf(-s.sx, b.z, b.x), by = fmaf(-s.sy, b.z, b.y);
+    const float cx = fmaf(-s.sx, c.z, c.x), cy = fmaf(-s.sy, c.z, c.y);
+    float U = cx * by - cy * bx;
+    float V = ax * cy - ay * cx;
+    float W = bx * ay - by * ax;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        U = edge_exact(cx, by, cy, bx, U);
+        V = edge_exact(ax, cy, ay, cx, V);
+        W = edge_exact(bx, ay, by, ax, W);
+    }
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+    const float det = U + V + W;
+    if (det == 0.0f) return false;
+    const float T = fmaf(W, s.sz * c.z, fmaf(V, s.sz * b.z, U * (s.sz * a.z)));
     const float inv = 1.0f / det;
-    u = un * inv;
-    v = vn * inv;
-    t = dot3(e2, qv) * inv;
+    t = T * inv;
+    u = V * inv;
+    v = W * inv;
     return true;
+}
+RR_HD bool woop_test(const Shear& s, float3 o, float3 v0, float3 v1, float3 v2, float& t, float& u, float& v) {
+    return woop_core(s, rot3(sub3(v0, o), s.kz), rot3(sub3(v1, o), s.kz), rot3(sub3(v2, o), s.kz), t, u, v);
 }
 
 struct Hit {
@@ -436,9 +533,9 @@ struct Hit {
 
 // Accept rule making the closest hit order-independent: smaller t wins; equal t
 // -> smaller original id wins.
-RR_HD void closest_tri(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
+RR_HD void closest_tri(const TriPack& tp, int idx, const Shear& s, float3 o, float tmin, Hit& h) {
     float t, u, v;
-    if (!tri_test(o, d, xyz(tp.p0), xyz(tp.p1), xyz(tp.p2), t, u, v)) return;
+    if (!woop_test(s, o, xyz(tp.p0), xyz(tp.p1), xyz(tp.p2), t, u, v)) return;
     const int orig = f2i(tp.p0.w);
     if (t > tmin && (t < h.t || (t == h.t && orig < h.orig))) {
         h.t = t;
@@ -449,8 +546,8 @@ RR_HD void closest_tri(const TriPack& tp, int idx, float3 o, float3 d, float tmi
     }
 }
 
-RR_HD void leaf_test(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
-    closest_tri(tp, idx, o, d, tmin, h);
+RR_HD void leaf_test(const TriPack& tp, int idx, const Shear& s, float3 o, float tmin, Hit& h) {
+    closest_tri(tp, idx, s, o, tmin, h);
 }
 
 // Traversal stack: kLdsStack entries in LDS ([entry][thread] -> conflict-free
@@ -499,15 +596,19 @@ struct TravStack {
     int* spill;     // spill_base: lane slot spill[(sp - kLdsStack) * stride + global thread]
     int spill_stride;
     int sp;
-    // A push beyond kLdsStack + kSpillStack entries is dropped (never reached
-    // by the LBVH/BVH4 depths of the test and bench scenes); the oracle's stack
-    // has the same capacity and the same rule (ORC_MAXDEPTH).
+    // pushes dropped for want of room (the counting kernels report them:
+    // rr_frame_stats / kTravWords, tests assert 0 on every bench scene)
+    uint32_t dropped = 0;
+    // A push beyond kLdsStack + kSpillStack entries is dropped (a missed
+    // subtree); the oracle's stack has the same capacity and the same rule
+    // (ORC_MAXDEPTH) and counts its drops too (orc_stack_drops).
     RR_D void push(int x) {
         if (sp < kLdsStack) {
             lds[sp * kBlock + (int)threadIdx.x] = x;
         } else if (sp < kLdsStack + kSpillStack) {
             spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kBlock + threadIdx.x)] = x;
         } else {
+            ++dropped;
             return;
         }
         ++sp;
@@ -535,22 +636,34 @@ struct TravCount {
 // step() with lane refill (wavefront.hip trace_refill), which changes only the
 // schedule, never the visited nodes, so the hits are identical.
 // nodes / tris: global or LDS pointers (wavefront.hip SceneView).
+// The largest |coordinate| of a BVH2's scene box (its root's two child boxes).
+RR_D float scene_radius(const BvhNode& r) {
+    const float a = fmaxf(fmaxf(fmaxf(fabsf(r.a.x), fabsf(r.a.y)), fmaxf(fabsf(r.a.z), fabsf(r.a.w))),
+                          fmaxf(fabsf(r.b.x), fabsf(r.b.y)));
+    const float b = fmaxf(fmaxf(fmaxf(fabsf(r.b.z), fabsf(r.b.w)), fmaxf(fabsf(r.c.x), fabsf(r.c.y))),
+                          fmaxf(fabsf(r.c.z), fabsf(r.c.w)));
+    return fmaxf(a, b);
+}
+
 template <bool kAnyHit, bool kCount = false>
 struct TravState {
-    float3 o, d, invd, oi;
+    float3 o, invd, oi, em;
+    Shear sh;
     float tmin;
     Hit h;
     int node;
-    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_) {
+    // r: scene_radius of the hierarchy walked (the box margins, slab_margin)
+    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_, float r) {
         o = o_;
-        d = d_;
+        sh = make_shear(d_);
         tmin = tmin_;
         h.t = tmax_;
         h.u = h.v = 0.0f;
         h.idx = -1;
         h.orig = -1;
-        invd = rcp3(d);
+        invd = rcp3(d_);
         oi = mk3(-(o.x * invd.x), -(o.y * invd.y), -(o.z * invd.z));
+        em = slab_margin(o, invd, r);
         node = 0;
     }
     // One node visit; true when the ray is finished (any-hit: on the first hit).
@@ -559,8 +672,8 @@ struct TravState {
         const BvhNode nd = load_node(nodes, node);
         if (kCount) ++cnt.nodes;
         float tl, tr;
-        bool hl = slab(oi, invd, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
-        bool hr = slab(oi, invd, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
+        bool hl = slab(oi, invd, em, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, tmin, h.t, tl);
+        bool hr = slab(oi, invd, em, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, tmin, h.t, tr);
         const int cl = nd.d.x, cr = nd.d.y;
         // passing leaves (single triangles), left then right, one per
         // iteration: lanes with only a left and lanes with only a right leaf
@@ -577,7 +690,7 @@ struct TravState {
         for (int k = 0; k < nl + nr; ++k) {
             const int ti = k < nl ? ~cl : ~cr;
             if (kCount) ++cnt.tris;
-            leaf_test(load_tri(tris, ti), ti, o, d, tmin, h);
+            leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
         }
         if (hl && hr) {
@@ -596,18 +709,47 @@ struct TravState {
     }
 };
 
-// The six child box tests of a quantised node for one ray (iq: q4_rcp of the
-// direction): bit c set when child c's box meets [tmin, tcur] (never for an
-// unused slot); tn[c] = the entry distance. Per axis s = iq * 2^e (exact),
-// o' = (org - o) * iq; a plane at grid coordinate q lies at t = fma(q, s, o');
-// the near plane is lo for iq >= 0, else hi (iq is never 0 or inf, so no NaN
-// and no min/max per axis). oracle/rr_oracle.c trace4() restates it.
-RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, float tn[kQWidth]) {
+// Per-node terms of the quantised box tests for one ray (iq: rcp3 of the
+// direction). Per axis s = iq * 2^e (exact), o' = (org - o) * iq; a plane at
+// grid coordinate q lies at t = fma(q, s, o'). The near planes use o' minus
+// the axis' margin, the far planes o' plus it (kBoxMargin of the node's
+// largest per-axis |org - o| + 255 * 2^e, times |iq|), so a box holding a
+// triangle woop_test accepts is never rejected by rounding.
+struct Q6Planes {
+    float sx, sy, sz;     // iq * 2^e
+    float nx, ny, nz;     // o' - margin (near planes)
+    float fx, fy, fz;     // o' + margin (far planes)
+};
+RR_D Q6Planes q6_planes(const QNode6& n, float3 o, float3 iq) {
     const uint32_t eb = (uint32_t)f2i(n.org.w);
-    const float sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
-    const float sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
-    const float sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
-    const float ox = (n.org.x - o.x) * iq.x, oy = (n.org.y - o.y) * iq.y, oz = (n.org.z - o.z) * iq.z;
+    const int ex = (int)(eb & 255u) - 128, ey = (int)((eb >> 8) & 255u) - 128, ez = (int)((eb >> 16) & 255u) - 128;
+    Q6Planes p;
+    p.sx = ldexpf(iq.x, ex);
+    p.sy = ldexpf(iq.y, ey);
+    p.sz = ldexpf(iq.z, ez);
+    const float dx = n.org.x - o.x, dy = n.org.y - o.y, dz = n.org.z - o.z;
+    const float ox = dx * iq.x, oy = dy * iq.y, oz = dz * iq.z;
+    const float m = fmaxf(fmaxf(fabsf(dx) + ldexpf(255.0f, ex), fabsf(dy) + ldexpf(255.0f, ey)),
+                          fabsf(dz) + ldexpf(255.0f, ez)) * kBoxMargin;
+    const float mx = m * fabsf(iq.x), my = m * fabsf(iq.y), mz = m * fabsf(iq.z);
+    p.nx = ox - mx;
+    p.ny = oy - my;
+    p.nz = oz - mz;
+    p.fx = ox + mx;
+    p.fy = oy + my;
+    p.fz = oz + mz;
+    return p;
+}
+
+// The six child box tests of a quantised node for one ray: bit c set when
+// child c's box meets [tmin, tcur] (never for an unused slot: the used-slot
+// mask in c.w is applied, which also holds when a NaN ray component makes
+// fmaxf / fminf drop their operands); tn[c] = the entry distance. The near
+// plane is lo for iq >= 0, else hi (iq is never 0 or inf, so no NaN and no
+// min/max per axis). oracle/rr_oracle.c trace4() restates it.
+RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, float tn[kQWidth]) {
+    const Q6Planes pl = q6_planes(n, o, iq);
+    const float sx = pl.sx, sy = pl.sy, sz = pl.sz;
     const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
     // children 0..3: one byte each of the near / far words per axis
     const uint32_t nx = px ? n.a.z : n.b.y, fx = px ? n.b.y : n.a.z;
@@ -625,14 +767,14 @@ RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, floa
         const int sh = c < 4 ? 8 * c : 8 * (c - 4);
         const uint32_t qnx = c < 4 ? nx : nx2, qny = c < 4 ? ny : ny2, qnz = c < 4 ? nz : nz2;
         const uint32_t qfx = c < 4 ? fx : fx2, qfy = c < 4 ? fy : fy2, qfz = c < 4 ? fz : fz2;
-        const float t0 = fmaxf(fmaxf(fmaf((float)((qnx >> sh) & 255u), sx, ox), fmaf((float)((qny >> sh) & 255u), sy, oy)),
-                               fmaxf(fmaf((float)((qnz >> sh) & 255u), sz, oz), tmin));
-        const float t1 = fminf(fminf(fmaf((float)((qfx >> sh) & 255u), sx, ox), fmaf((float)((qfy >> sh) & 255u), sy, oy)),
-                               fminf(fmaf((float)((qfz >> sh) & 255u), sz, oz), tcur));
+        const float t0 = fmaxf(fmaxf(fmaf((float)((qnx >> sh) & 255u), sx, pl.nx), fmaf((float)((qny >> sh) & 255u), sy, pl.ny)),
+                               fmaxf(fmaf((float)((qnz >> sh) & 255u), sz, pl.nz), tmin));
+        const float t1 = fminf(fminf(fmaf((float)((qfx >> sh) & 255u), sx, pl.fx), fmaf((float)((qfy >> sh) & 255u), sy, pl.fy)),
+                               fminf(fmaf((float)((qfz >> sh) & 255u), sz, pl.fz), tcur));
         tn[c] = t0;
         if (t0 <= t1) hits |= 1u << c;
     }
-    return hits;
+    return hits & n.c.w;
 }
 
 // q6_box_hits that keeps only the nearest hit internal child (ties: lower
@@ -645,11 +787,9 @@ RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, floa
 // -10 % on C5, VGPR spill slots 10 -> 2).
 template <bool kNearest = true>
 RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, uint32_t imask, int& best) {
-    const uint32_t eb = (uint32_t)f2i(n.org.w);
-    const float sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
-    const float sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
-    const float sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
-    const float ox = (n.org.x - o.x) * iq.x, oy = (n.org.y - o.y) * iq.y, oz = (n.org.z - o.z) * iq.z;
+    const Q6Planes pl = q6_planes(n, o, iq);
+    const float sx = pl.sx, sy = pl.sy, sz = pl.sz;
+    const uint32_t used = n.c.w;
     const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
     const uint32_t nx = px ? n.a.z : n.b.y, fx = px ? n.b.y : n.a.z;
     const uint32_t ny = py ? n.a.w : n.b.z, fy = py ? n.b.z : n.a.w;
@@ -667,11 +807,11 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
         const int sh = c < 4 ? 8 * c : 8 * (c - 4);
         const uint32_t qnx = c < 4 ? nx : nx2, qny = c < 4 ? ny : ny2, qnz = c < 4 ? nz : nz2;
         const uint32_t qfx = c < 4 ? fx : fx2, qfy = c < 4 ? fy : fy2, qfz = c < 4 ? fz : fz2;
-        const float t0 = fmaxf(fmaxf(fmaf((float)((qnx >> sh) & 255u), sx, ox), fmaf((float)((qny >> sh) & 255u), sy, oy)),
-                               fmaxf(fmaf((float)((qnz >> sh) & 255u), sz, oz), tmin));
-        const float t1 = fminf(fminf(fmaf((float)((qfx >> sh) & 255u), sx, ox), fmaf((float)((qfy >> sh) & 255u), sy, oy)),
-                               fminf(fmaf((float)((qfz >> sh) & 255u), sz, oz), tcur));
-        const bool hit = t0 <= t1;
+        const float t0 = fmaxf(fmaxf(fmaf((float)((qnx >> sh) & 255u), sx, pl.nx), fmaf((float)((qny >> sh) & 255u), sy, pl.ny)),
+                               fmaxf(fmaf((float)((qnz >> sh) & 255u), sz, pl.nz), tmin));
+        const float t1 = fminf(fminf(fmaf((float)((qfx >> sh) & 255u), sx, pl.fx), fmaf((float)((qfy >> sh) & 255u), sy, pl.fy)),
+                               fminf(fmaf((float)((qfz >> sh) & 255u), sz, pl.fz), tcur));
+        const bool hit = t0 <= t1 && ((used >> c) & 1u);
         if (hit) hits |= 1u << c;
         if (hit && ((imask >> c) & 1u) && (best < 0 || (kNearest && t0 < bt))) {
             best = c;
@@ -716,19 +856,20 @@ RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
 // oracle/rr_oracle.c trace4() is the same walk.
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6 {
-    float3 o, d, iq;
+    float3 o, iq;
+    Shear sh;
     float tmin;
     Hit h;
     int node;
     RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_) {
         o = o_;
-        d = d_;
+        sh = make_shear(d_);
         tmin = tmin_;
         h.t = tmax_;
         h.u = h.v = 0.0f;
         h.idx = -1;
         h.orig = -1;
-        iq = rcp3(d);
+        iq = rcp3(d_);
         node = 0;
     }
     template <typename NodeSrc, typename TriP, typename Stack>
@@ -748,7 +889,7 @@ struct TravStateQ6 {
             leaves &= leaves - 1;
             const int ti = (int)nd.a.y + c - __builtin_popcount(imask & ((1u << c) - 1u));
             if (kCount) ++cnt.tris;
-            leaf_test(load_tri(tris, ti), ti, o, d, tmin, h);
+            leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
         }
         if (!inner) {
@@ -780,7 +921,7 @@ RR_D bool traverse(NodeP nodes, TriP tris, int n_tris, float3 o, float3 d, float
         return false;
     }
     TravState<kAnyHit, kCount> ts;
-    ts.start(o, d, tmin, tmax);
+    ts.start(o, d, tmin, tmax, scene_radius(load_node(nodes, 0)));
     st.sp = 0;
     while (!ts.step(nodes, tris, st, cnt)) {
     }

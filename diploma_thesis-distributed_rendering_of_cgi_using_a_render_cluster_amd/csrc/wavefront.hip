@@ -288,7 +288,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     } else {
         const TriPack tp = load_tri(v.tris, h.idx);
         mid = f2i(tp.p1.w);
-        N = norm3(cross3(xyz(tp.p1), xyz(tp.p2)));
+        N = norm3(cross3(sub3(xyz(tp.p1), xyz(tp.p0)), sub3(xyz(tp.p2), xyz(tp.p0))));
     }
     const Mat m = view_mat(v, mid);
     const auto lut = v.lut + kMatLutStride * mid;
@@ -429,6 +429,12 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
         atomicAdd(&tc[slot + 1], b);
     }
 }
+// Traversal-stack pushes dropped for want of room (TravStack::push, the packet
+// stack), summed into word kTravDropWord; a dropped push is a missed subtree.
+__device__ __forceinline__ void flush_drops(unsigned long long* __restrict__ tc, uint32_t n) {
+    for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off);
+    if ((threadIdx.x & 63) == 0 && n) atomicAdd(&tc[kTravDropWord], (unsigned long long)n);
+}
 
 }  // namespace
 struct SceneArgs {
@@ -453,7 +459,8 @@ RR_D void lds_copy(lds_f4w* dst, const float4* __restrict__ src, int n4) {
 // Hull flags of an LDS-resident scene's triangle i (oracle/rr_oracle.c
 // tri_hull, the same float operations): bit 0 when every vertex of every
 // triangle lies behind triangle i's plane on its front side (the cross(e1, e2)
-// direction), up to 2^-12 of the vertex's distance from v0 times |n|_1; bit 1
+// direction, e1 = v1 - v0, e2 = v2 - v0), up to 2^-12 of the vertex's distance
+// from v0 times |n|_1; bit 1
 // the same for the back side. A ray leaving the triangle on a side whose bit is
 // set moves away from a plane the whole scene lies behind: it meets nothing, so
 // its continuation misses and its shadow ray is unoccluded without a traversal
@@ -462,13 +469,12 @@ RR_D void lds_copy(lds_f4w* dst, const float4* __restrict__ src, int n4) {
 // bits kHullShift.. of the staged material word (shade() reads that word anyway).
 RR_D uint32_t hull_flags(lds_tri* tris, int n_tris, int i) {
     const TriPack s = load_tri(tris, i);
-    const float3 v0 = xyz(s.p0), n = cross3(xyz(s.p1), xyz(s.p2));
+    const float3 v0 = xyz(s.p0), n = cross3(sub3(xyz(s.p1), v0), sub3(xyz(s.p2), v0));
     const float an = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
     bool front = true, back = true;
     for (int j = 0; j < n_tris; ++j) {
         const TriPack e = load_tri(tris, j);
-        const float3 w0 = xyz(e.p0);
-        const float3 w[3] = {w0, add3(w0, xyz(e.p1)), add3(w0, xyz(e.p2))};
+        const float3 w[3] = {xyz(e.p0), xyz(e.p1), xyz(e.p2)};
         for (int k = 0; k < 3; ++k) {
             const float3 r = sub3(w[k], v0);
             const float h = dot3(n, r);
@@ -485,12 +491,15 @@ RR_D uint32_t hull_flags(lds_tri* tris, int n_tris, int i) {
 // view; `used` receives the float4 slots taken (LDS layout: scene_lds_f4()).
 // Camera-ray data of one triangle (sorted index i), staged next to the scene
 // by the kernels that trace camera rays of LDS-resident scenes: every camera
-// ray starts at the camera, so tri_test's origin-only terms tv = o - v0,
-// qv = tv x e1 and tn = e2 . qv are computed once per block (the same float
-// operations, so camera_hit's t / u / v are bit-identical to tri_test's), and
-// the triangle's screen rectangle (tri_screen_rect) bins it to the 8x8 tiles
-// whose samples can hit it.
-//   [3i] = (tv, tn), [3i+1] = (qv, 0), [3i+2] = (x0, x1, y0, y1)
+// ray starts at the camera, so woop_test's vertices relative to the origin,
+// v - o, are computed once per block (the same float operations, so
+// camera_hit's t / u / v are bit-identical to woop_test's) — in each of the
+// three axis permutations of rot3, so that a ray reads its own (kz) with a
+// per-lane LDS address instead of permuting per test (18 selects per triangle
+// test) — and the triangle's screen rectangle (tri_screen_rect) bins it to the
+// 8x8 tiles whose samples can hit it.
+//   [13i + 3kz + k] = (rot3(v_k - o, kz), orig id for k = 0, else 0), kz, k = 0..2
+//   [13i + 9] = (x0, x1, y0, y1), [13i + 10..12] = the screen edge lines
 // Screen rectangle of a triangle (pixels, one pixel of slack) and its three
 // edge lines e[k] = (nx, ny, c): nx*x + ny*y + c >= 0 inside, |n| = 1, so the
 // value is a signed distance in pixels. A triangle at or behind the camera
@@ -536,30 +545,33 @@ RR_D void tri_screen_rect(const FrameConsts& fc, const float3 p[3], float r[4], 
     }
 }
 
-// Camera-ray data per triangle in LDS: the origin terms of the triangle test
-// (2 float4), the screen rectangle, the three screen edge lines.
-constexpr int kCamF4 = 6;
+// Camera-ray data per triangle in LDS: the vertices relative to the camera in
+// the three permutations (9 float4), the screen rectangle, the three screen
+// edge lines.
+constexpr int kCamF4 = 13;
+constexpr int kCamRect = 9;  // float4 offset of the screen rectangle, the edge lines follow
 RR_D void stage_camera(lds_f4w* q, lds_tri* tris, int n_tris, const FrameConsts& fc) {
     for (int i = threadIdx.x; i < n_tris; i += kBlock) {
         const TriPack tp = load_tri(tris, i);
-        const float3 v0 = xyz(tp.p0), e1 = xyz(tp.p1), e2 = xyz(tp.p2);
-        const float3 tv = sub3(fc.cam_pos, v0);
-        const float3 qv = cross3(tv, e1);
-        const float tn = dot3(e2, qv);
-        const float3 pts[3] = {v0, add3(v0, e1), add3(v0, e2)};
+        const float3 pts[3] = {xyz(tp.p0), xyz(tp.p1), xyz(tp.p2)};
         float r[4], e[3][3];
         tri_screen_rect(fc, pts, r, e);
-        rr_f4v a, b, c;
-        a.x = tv.x; a.y = tv.y; a.z = tv.z; a.w = tn;
-        b.x = qv.x; b.y = qv.y; b.z = qv.z; b.w = 0.0f;
+        for (int k = 0; k < 3; ++k) {
+            const float3 a = sub3(pts[k], fc.cam_pos);
+            for (int kz = 0; kz < 3; ++kz) {
+                const float3 r = rot3(a, kz);
+                rr_f4v x;
+                x.x = r.x; x.y = r.y; x.z = r.z; x.w = k == 0 ? tp.p0.w : 0.0f;
+                q[kCamF4 * i + 3 * kz + k] = x;
+            }
+        }
+        rr_f4v c;
         c.x = r[0]; c.y = r[1]; c.z = r[2]; c.w = r[3];
-        q[kCamF4 * i] = a;
-        q[kCamF4 * i + 1] = b;
-        q[kCamF4 * i + 2] = c;
+        q[kCamF4 * i + kCamRect] = c;
         for (int k = 0; k < 3; ++k) {
             rr_f4v l;
             l.x = e[k][0]; l.y = e[k][1]; l.z = e[k][2]; l.w = 0.0f;
-            q[kCamF4 * i + 3 + k] = l;
+            q[kCamF4 * i + kCamRect + 1 + k] = l;
         }
     }
 }
@@ -599,7 +611,7 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
         v.nrm = q;
         for (int i = threadIdx.x; i < a.n_tris; i += kBlock) {
             const TriPack tp = load_tri(v.tris, i);
-            const float3 n = norm3(cross3(xyz(tp.p1), xyz(tp.p2)));
+            const float3 n = norm3(cross3(sub3(xyz(tp.p1), xyz(tp.p0)), sub3(xyz(tp.p2), xyz(tp.p0))));
             rr_f4v x;
             x.x = n.x; x.y = n.y; x.z = n.z;
             x.w = i2f(f2i(tp.p1.w) | (int)(hull_flags(v.tris, a.n_tris, i) << kHullShift));
@@ -652,8 +664,8 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
 }
 
 // Closest hit of a camera ray (origin fc.cam_pos) over the triangles whose bits
-// are set in the wave-uniform mask {m0, m1} (sorted indices 0..127): tri_test
-// with the staged origin terms, closest_tri_nb's branch-free accept rule. The
+// are set in the wave-uniform mask {m0, m1} (sorted indices 0..127): woop_test
+// with the staged vertices relative to the camera, closest_tri's accept rule. The
 // rule is order-independent (smaller t, then smaller original id), so the
 // result equals testing every triangle whenever the mask holds every triangle
 // the ray can hit (tile_mask). LDS-resident scenes trace camera rays this way
@@ -668,22 +680,18 @@ template <bool kCount>
 RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float tmin, float tmax, Hit& h,
                      TravCount& cnt) {
     set_miss(h, tmax);
+    const Shear sh = make_shear_unit(d);  // camera_ray_xy: d = dw / |dw|
     for (int w = 0; w < 2; ++w) {
         uint64_t m = w ? m1 : m0;
         while (m) {
             const int i = (int)__builtin_ctzll(m) + 64 * w;
             m &= m - 1;
             if (kCount) ++cnt.tris;
-            const TriPack tp = load_tri(v.tris, i);
-            const float4 ca = lds_ld4(v.cam + kCamF4 * i), cb = lds_ld4(v.cam + kCamF4 * i + 1);
-            const float3 e1 = xyz(tp.p1), e2 = xyz(tp.p2), tv = xyz(ca), qv = xyz(cb);
-            const float3 pv = cross3(d, e2);
-            const float det = dot3(e1, pv);
-            const float un = dot3(tv, pv), vn = dot3(d, qv);
-            if (bary_pass(det, un, vn)) {  // tri_test's order: the division only for rays that meet it
-                const float inv = 1.0f / det;
-                const float u = un * inv, vv = vn * inv, t = ca.w * inv;
-                const int orig = f2i(tp.p0.w);
+            const lds_f4w* q = v.cam + kCamF4 * i + 3 * sh.kz;  // this ray's permutation
+            const float4 ca = lds_ld4(q), cb = lds_ld4(q + 1), cc = lds_ld4(q + 2);
+            float t, u, vv;
+            if (woop_core(sh, xyz(ca), xyz(cb), xyz(cc), t, u, vv)) {
+                const int orig = f2i(ca.w);
                 if (t > tmin && (t < h.t || (t == h.t && orig < h.orig))) {
                     h.t = t;
                     h.u = u;
@@ -705,10 +713,10 @@ RR_D void tile_mask(const FrameConsts& fc, const LdsView& v, int n_tris, float x
     const float X0 = x0 + 0.5f - r, X1 = x1 + 0.5f + r, Y0 = y0 + 0.5f - r, Y1 = y1 + 0.5f + r;
     uint64_t a = 0, b = 0;
     for (int i = 0; i < n_tris; ++i) {
-        const float4 q = lds_ld4(v.cam + kCamF4 * i + 2);
+        const float4 q = lds_ld4(v.cam + kCamF4 * i + kCamRect);
         bool in = !(q.y < X0 || q.x > X1 || q.w < Y0 || q.z > Y1);
         for (int k = 0; k < 3 && in; ++k) {  // the expanded tile wholly outside an edge (+1 px of slack)
-            const float4 l = lds_ld4(v.cam + kCamF4 * i + 3 + k);
+            const float4 l = lds_ld4(v.cam + kCamF4 * i + kCamRect + 1 + k);
             const float m = l.x * (l.x > 0.0f ? X1 : X0) + l.y * (l.y > 0.0f ? Y1 : Y0) + l.z;
             in = m >= -1.0f;
         }
@@ -970,7 +978,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameCons
         [&](int p, uint32_t, const Hit& h) { hits[p] = pack_hit(h); });
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
     if ((threadIdx.x & 63) == 0 && n_traced) atomicAdd(traced, n_traced);
-    if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
+    if (kCount) {
+        flush_counts(tc, 0, cnt.nodes, cnt.tris);
+        flush_drops(tc, st.dropped);
+    }
 }
 
 // Packet traversal (camera rays of the split path, render_split decides): one wave walks the quantised BVH4 for the rays of its 64
@@ -993,9 +1004,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameCons
 constexpr int kPacketStack = 128;  // a node pushes <= 5: bounded by 5 x the hierarchy depth
 template <bool kCount>
 RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk, bool act,
-                       float3 o, float3 d, float tmin, Hit& h, TravCount& cnt) {
+                       float3 o, float3 d, float tmin, Hit& h, TravCount& cnt, uint32_t& dropped) {
     if (!__ballot(act)) return;
     const float3 iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
+    const Shear sh = make_shear(d);
     int node = 0, sp = 0;
     for (;;) {
         const bool live = act;
@@ -1012,7 +1024,7 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
             const TriPack tp = load_tri(tris, ti);
             if ((hm >> c) & 1u) {
                 if (kCount) ++cnt.tris;
-                leaf_test(tp, ti, o, d, tmin, h);
+                leaf_test(tp, ti, sh, o, tmin, h);
             }
         }
         // internal children some lane enters: the representative lane's nearest next
@@ -1044,8 +1056,10 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
         const int base = (int)nd.a.x;
 #pragma unroll
         for (int c = kQWidth - 1; c >= 0; --c)
-            if (c != best && ((inner >> c) & 1u) && sp < kPacketStack)  // never full here
-                stk[sp++] = base + __builtin_popcount(imask & ((1u << c) - 1u));
+            if (c != best && ((inner >> c) & 1u)) {
+                if (sp < kPacketStack) stk[sp++] = base + __builtin_popcount(imask & ((1u << c) - 1u));
+                else ++dropped;  // a missed subtree: reported by the counting pass, tests assert 0
+            }
         node = __builtin_amdgcn_readfirstlane(base + __builtin_popcount(imask & ((1u << best) - 1u)));
     }
 }
@@ -1066,7 +1080,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
     const int ntiles = tiles_x * tiles_y;
     const int npk = ntiles * (np / fc.npix);
     const int nw = gridDim.x * kWavesPerBlock;
-    uint32_t n_traced = 0;
+    uint32_t n_traced = 0, dropped = 0;
     for (int q = xcd_wave_rank(); q < npk; q += nw) {
         const int sl = q / ntiles, t = q - sl * ntiles;
         const int ty = t / tiles_x, tx = t - ty * tiles_x;
@@ -1083,12 +1097,15 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         n_traced += valid && !culled ? 1u : 0u;
         Hit h;
         set_miss(h, tmax);
-        packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt);
+        packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt, dropped);
         if (valid) hits[(size_t)sl * fc.npix + pix] = pack_hit(h);
     }
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
     if (lane == 0 && n_traced) atomicAdd(traced, n_traced);
-    if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
+    if (kCount) {
+        flush_counts(tc, 0, cnt.nodes, cnt.tris);
+        flush_drops(tc, dropped);
+    }
 }
 
 // Camera paths: shade bounce 0 from hits[p]; appends the bounce-1 path queue
@@ -1140,7 +1157,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_extend(SceneArgs 
             tmax = kFltMax;
         },
         [&](int, uint32_t i, const Hit& h) { hits[i] = pack_hit(h); });
-    if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
+    if (kCount) {
+        flush_counts(tc, 2, cnt.nodes, cnt.tris);
+        flush_drops(tc, st.dropped);
+    }
 }
 
 // Bounce b: shade from hits[slot], in the queue's time order (slot_t); appends
@@ -1207,7 +1227,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_shadow_refill(SceneArgs
             L.z = L.z + c.z;
             rad.put(pid, L);
         });
-    if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
+    if (kCount) {
+        flush_counts(tc, 4, cnt.nodes, cnt.tris);
+        flush_drops(tc, st.dropped);
+    }
 }
 
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
@@ -1650,6 +1673,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         flush_counts(tc, 0, cp.nodes, cp.tris);
         flush_counts(tc, 2, ce.nodes, ce.tris);
         flush_counts(tc, 4, cs.nodes, cs.tris);
+        flush_drops(tc, st.dropped);
         const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
         if ((threadIdx.x & 63) == 0) {  // device.hpp kTravWords
             atomicAdd(&tc[6], clk1 - clk0);

@@ -61,7 +61,7 @@ class FrameStats(ctypes.Structure):
                 ("camera_rays_traced", ctypes.c_uint64), ("view_transform", ctypes.c_int32),
                 ("view_transform_substituted", ctypes.c_int32), ("kernel_clock_ghz", ctypes.c_double),
                 ("kernel_wave_fill", ctypes.c_double), ("tile_slices", ctypes.c_int32),
-                ("reserved0", ctypes.c_int32)]
+                ("stack_drops", ctypes.c_int32)]
 
     def as_dict(self) -> dict:
         out = {}
@@ -81,7 +81,7 @@ EXPORTS = [
     "rr_frame_submit", "rr_frame_complete",
     "rr_render_frame_to_memory", "rr_scene_resolution", "rr_encode_image", "rr_last_error",
     "rr_last_warning", "rr_set_ocio_config", "rr_synchronize",
-    "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_frame_state", "rr_debug_bvh",
+    "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_scene_mesh", "rr_debug_frame_state", "rr_debug_bvh",
     "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_qbvh", "rr_debug_bvh_hier", "rr_debug_jpeg_device",
     "rr_debug_bsdf_sample", "rr_debug_fastmath_check",
 ]
@@ -128,6 +128,7 @@ def lib() -> ctypes.CDLL:
         "rr_scene_free": (None, [P]),
         "rr_destroy": (None, [P]),
         "rr_debug_counts": (c_int, [P, i32p, i32p, i32p, i32p]),
+        "rr_debug_scene_mesh": (c_int, [P, f32p, i32p]),
         "rr_debug_frame_state": (c_int, [P, P, i32, ctypes.POINTER(RenderParams), f32p, i32p, f32p, f32p, f32p,
                                          f32p, i32p, f32p]),
         "rr_debug_bvh": (c_int, [P, P, i32, u32p, u32p, i32p, f32p]),
@@ -210,6 +211,15 @@ class Scene:
         v = [ctypes.c_int32() for _ in range(4)]
         _check(lib().rr_debug_counts(self.handle, *[ctypes.byref(x) for x in v]))
         return dict(zip(["triangles", "lights", "materials", "objects"], [x.value for x in v]))
+
+    def mesh(self) -> tuple[np.ndarray, np.ndarray]:
+        """Object-space triangles (n, 3, 3) float32 and the object index of each
+        (rr_debug_scene_mesh)."""
+        n = self.counts()["triangles"]
+        local = np.zeros((max(n, 1), 3, 3), np.float32)
+        obj = np.zeros(max(n, 1), np.int32)
+        _check(lib().rr_debug_scene_mesh(self.handle, _ptr(local, ctypes.c_float), _ptr(obj, ctypes.c_int32)))
+        return local[:n], obj[:n]
 
     def resolution(self, params: RenderParams | None = None) -> tuple[int, int]:
         w, h = ctypes.c_int32(), ctypes.c_int32()

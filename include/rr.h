@@ -149,7 +149,9 @@ typedef struct rr_frame_stats {
      * 32-sample groups when it ran alone (one unit per group); 0 for frames of
      * the other paths. Scheduling only: both give the same bits. */
     int32_t tile_slices;
-    int32_t reserved0;
+    /* RR_FLAG_COUNT_TRAVERSAL: traversal-stack pushes dropped for want of room
+     * over the frame (each a missed subtree; 0 on every bench scene) */
+    int32_t stack_drops;
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */
@@ -269,6 +271,13 @@ void rr_destroy(rr_ctx* ctx);
 
 int rr_debug_counts(rr_scene* scene, int32_t* n_triangles, int32_t* n_lights,
                     int32_t* n_materials, int32_t* n_objects);
+
+/* The scene's triangles in object space as loaded (generators expanded):
+ * tri_local9 n*9 floats (v0 v1 v2), tri_object n object indices (the matrix
+ * of rr_debug_object_matrix that places it). Either pointer may be NULL.
+ * Test infrastructure: pins the device's world transform (k_transform)
+ * against a host restatement; no reference counterpart. */
+int rr_debug_scene_mesh(rr_scene* scene, float* tri_local9, int32_t* tri_object);
 
 /* Evaluate the frame on the device (animation, world transform, LBVH) and read
  * back what the integrator consumes. Any output pointer may be NULL. */

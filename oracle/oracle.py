@@ -269,6 +269,30 @@ def last_build_seconds() -> float:
     return float(L.orc_last_build_seconds())
 
 
+def camera_rays(state, pixels, samples) -> np.ndarray:
+    """Camera rays (n, 8: o, tmin, d, tmax) of the (pixel, sample) pairs of a
+    FrameState's frame, as the oracle's radiance() starts them."""
+    pix = np.ascontiguousarray(pixels, dtype=np.int32)
+    smp = np.ascontiguousarray(samples, dtype=np.int32)
+    cam, ri, rf = _f32(state.camera), np.ascontiguousarray(state.render_ints, np.int32), _f32(state.render_floats)
+    out = np.zeros((len(pix), 8), np.float32)
+    lib().orc_camera_rays(_p(cam, ctypes.c_float), _p(ri, ctypes.c_int32), _p(rf, ctypes.c_float), len(pix),
+                          _p(pix, ctypes.c_int32), _p(smp, ctypes.c_int32), _p(out, ctypes.c_float))
+    return out
+
+
+def stack_drops(reset: bool = False) -> int:
+    """Traversal-stack pushes the oracle dropped for want of room (ORC_MAXDEPTH)
+    since the last reset: each a missed subtree (rr_frame_stats.stack_drops on
+    the GPU)."""
+    L = lib()
+    L.orc_stack_drops.restype = ctypes.c_longlong
+    n = int(L.orc_stack_drops())
+    if reset:
+        L.orc_reset_stack_drops()
+    return n
+
+
 def ray_counts():
     """Ray statistics of the last render (test/debug): (continuations at bounce 0,
     shadow rays at bounce 0, continuations later, shadow rays later) and the

@@ -175,7 +175,7 @@ typedef struct {
     int* child_lf;    /* the same with subtrees of <= ORC_LEAF_MAX leaves as leaf ranges (what trace() walks) */
     int* range;       /* 2 per internal node: first sorted leaf, leaf count */
     float* box;       /* 12 per internal node */
-    float* tri;       /* leaf order: v0 e1 e2 (9) */
+    float* tri;       /* leaf order: v0 v1 v2 (9; rr_device.h TriPack) */
     int* tri_orig;
     int* tri_mat;
     int width;        /* hierarchy trace() walks: 2 (BVH2) or 4 (the quantised wide collapse, ORC_QW children) */
@@ -367,9 +367,7 @@ pack:
     for (int i = 0; i < n; ++i) {
         const float* t = tris9 + 9 * (size_t)B->order[i];
         float* o = B->tri + 9 * (size_t)i;
-        o[0] = t[0]; o[1] = t[1]; o[2] = t[2];
-        o[3] = t[3] - t[0]; o[4] = t[4] - t[1]; o[5] = t[5] - t[2];
-        o[6] = t[6] - t[0]; o[7] = t[7] - t[1]; o[8] = t[8] - t[2];
+        memcpy(o, t, 9 * sizeof(float));
         B->tri_orig[i] = (int)B->order[i];
         B->tri_mat[i] = mats ? mats[B->order[i]] : 0;
     }
@@ -494,8 +492,9 @@ static v3 rcp3(v3 d) {
  *   w5     position of the first leaf child's triangle (the others follow)
  *   w6..11 children 0..3: lo x, lo y, lo z, hi x, hi y, hi z (byte c = child c)
  *   w12..14 children 4, 5: (lo x, lo y), (lo z, hi x), (hi y, hi z) as byte pairs
- *   w15    0
- * An unused slot has lo 255, hi 0 on every axis: its box test always fails. */
+ *   w15    mask of the used slots
+ * An unused slot has lo 255, hi 0 on every axis and its bit of w15 clear: its
+ * box test always fails. */
 #define ORC_QW_MAX 6
 #ifndef ORC_QW
 #define ORC_QW 6 /* children per node (<= ORC_QW_MAX; rr_device.h kQWidth) */
@@ -525,6 +524,7 @@ static void q4_pack(const float lo[3][ORC_QW_MAX], const float hi[3][ORC_QW_MAX]
     o[3] = eb | inner << 24;
     o[4] = inner_base;
     o[5] = tri_base;
+    o[15] = (1u << used) - 1u;  /* used slots */
 }
 
 /* BVH4 collapse of the BVH2 (PLOC, or Karras below 3 triangles), as
@@ -632,45 +632,96 @@ static void lbvh_collapse4(lbvh* B) {
 /* ------------------------------------------------------------ tracing ---- */
 typedef struct { float t, u, v; int idx, orig; } hitrec;
 
-/* plane distances fmaf(b, inv, oi), oi = -(o inv) per ray (rr_device.h slab) */
-static int slab_test(v3 oi, v3 inv, const float* b, float tmin, float tmax, float* tnear) {
+/* Watertight traversal (csrc/rr_device.h, "intersection"): the triangle test
+ * decides a hit exactly in a 2D projection of the ray's own (woop_test), and
+ * every box test widens the box by ORC_BOX_MARGIN (2^-19) of the largest
+ * coordinate involved — the box's distance from the origin plus its extent —
+ * a distance along each axis, margin * |1/d| in t: subtracted from the near
+ * planes, added to the far ones. */
+#define ORC_BOX_MARGIN 0x1p-19f
+
+/* plane distances fmaf(b, inv, oi), oi = -(o inv) per ray, widened by em per
+ * axis (rr_device.h slab) */
+static int slab_test(v3 oi, v3 inv, v3 em, const float* b, float tmin, float tmax, float* tnear) {
     float tx0 = fmaf(b[0], inv.x, oi.x), tx1 = fmaf(b[3], inv.x, oi.x);
     float ty0 = fmaf(b[1], inv.y, oi.y), ty1 = fmaf(b[4], inv.y, oi.y);
     float tz0 = fmaf(b[2], inv.z, oi.z), tz1 = fmaf(b[5], inv.z, oi.z);
-    float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    float tn = fmaxf(fmaxf(fminf(tx0, tx1) - em.x, fminf(ty0, ty1) - em.y), fmaxf(fminf(tz0, tz1) - em.z, tmin));
+    float tf = fminf(fminf(fmaxf(tx0, tx1) + em.x, fmaxf(ty0, ty1) + em.y), fminf(fmaxf(tz0, tz1) + em.z, tmax));
     *tnear = tn;
     return tn <= tf;
 }
-
-/* Moeller-Trumbore with the barycentric test before the division
- * (csrc/rr_device.h bary_pass / tri_test): with a = |det| and the numerators
- * taken with det's sign, the ray meets the triangle iff 0 <= un <= a, vn >= 0,
- * un + vn <= a; only then t, u, v = numerators / det. */
-static int bary_pass(float det, float un, float vn) {
-    int neg = det < 0.0f;
-    float a = neg ? -det : det, su = neg ? -un : un, sv = neg ? -vn : vn;
-    return !(det == 0.0f) && !(su < 0.0f || su > a) && !(sv < 0.0f || su + sv > a);
+/* BVH2 margins of one ray (rr_device.h slab_margin): ORC_BOX_MARGIN (|o|_inf +
+ * r) |1/d| per axis, r = the largest |coordinate| of the scene box */
+static v3 slab_margin(v3 o, v3 inv, float r) {
+    float m = (fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + r) * ORC_BOX_MARGIN;
+    return V(m * fabsf(inv.x), m * fabsf(inv.y), m * fabsf(inv.z));
+}
+/* rr_device.h scene_radius: over the root's 12 box floats, the same fmaxf tree */
+static float scene_radius(const float* r) {
+    float a = fmaxf(fmaxf(fmaxf(fabsf(r[0]), fabsf(r[1])), fmaxf(fabsf(r[2]), fabsf(r[3]))), fmaxf(fabsf(r[4]), fabsf(r[5])));
+    float b = fmaxf(fmaxf(fmaxf(fabsf(r[6]), fabsf(r[7])), fmaxf(fabsf(r[8]), fabsf(r[9]))), fmaxf(fabsf(r[10]), fabsf(r[11])));
+    return fmaxf(a, b);
 }
 
-static int mt_test(v3 o, v3 d, const float* t9, float* t, float* u, float* v) {
-    v3 v0 = V(t9[0], t9[1], t9[2]), e1 = V(t9[3], t9[4], t9[5]), e2 = V(t9[6], t9[7], t9[8]);
-    v3 pv = vcross(d, e2);
-    float det = vdot(e1, pv);
-    v3 tv = vsub(o, v0);
-    v3 qv = vcross(tv, e1);
-    float un = vdot(tv, pv), vn = vdot(d, qv);
-    if (!bary_pass(det, un, vn)) return 0;
+/* Watertight ray/triangle test (Woop, Benthin & Wald, JCGT 2(1) 2013), as
+ * rr_device.h make_shear / woop_core: per ray kz = the axis of the largest |d|
+ * component (ties: x before y before z), (kx, ky) = (kz + 1, kz + 2) mod 3,
+ * sz = 1 / d[kz], sx = d[kx] sz, sy = d[ky] sz; per triangle the vertices
+ * relative to the origin, permuted, sheared to x = a[kx] - sx a[kz],
+ * y = a[ky] - sy a[kz]; edge functions U = cx by - cy bx, V = ax cy - ay cx,
+ * W = bx ay - by ax (no contraction: a shared edge gives exactly opposite
+ * values; one that rounds to 0 recomputed exactly, edge_exact); hit iff no two
+ * of them have opposite signs and det = U + V + W != 0; t = (U sz az + V sz bz
+ * + W sz cz) / det, u = V / det, v = W / det. */
+typedef struct { float sx, sy, sz; int kz; } shear_t;
+static v3 rot3(v3 a, int kz) {
+    int k0 = kz == 0, k1 = kz == 1;
+    return V(k0 ? a.y : (k1 ? a.z : a.x), k0 ? a.z : (k1 ? a.x : a.y), k0 ? a.x : (k1 ? a.y : a.z));
+}
+static shear_t make_shear(v3 d) {
+    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    shear_t s;
+    s.kz = ax >= ay ? (ax >= az ? 0 : 2) : (ay >= az ? 1 : 2);
+    v3 r = rot3(d, s.kz);
+    s.sz = 1.0f / r.z;
+    s.sx = r.x * s.sz;
+    s.sy = r.y * s.sz;
+    return s;
+}
+static float edge_exact(float a, float b, float c, float d, float e) {
+    if (e != 0.0f) return e;
+    return fmaf(a, b, -(a * b)) - fmaf(c, d, -(c * d));
+}
+static int woop_test(const shear_t* s, v3 o, const float* t9, float* t, float* u, float* v) {
+    v3 a = rot3(vsub(V(t9[0], t9[1], t9[2]), o), s->kz);
+    v3 b = rot3(vsub(V(t9[3], t9[4], t9[5]), o), s->kz);
+    v3 c = rot3(vsub(V(t9[6], t9[7], t9[8]), o), s->kz);
+    float ax = fmaf(-s->sx, a.z, a.x), ay = fmaf(-s->sy, a.z, a.y);
+    float bx = fmaf(-s->sx, b.z, b.x), by = fmaf(-s->sy, b.z, b.y);
+    float cx = fmaf(-s->sx, c.z, c.x), cy = fmaf(-s->sy, c.z, c.y);
+    float U = cx * by - cy * bx;
+    float Vv = ax * cy - ay * cx;
+    float W = bx * ay - by * ax;
+    if (U == 0.0f || Vv == 0.0f || W == 0.0f) {
+        U = edge_exact(cx, by, cy, bx, U);
+        Vv = edge_exact(ax, cy, ay, cx, Vv);
+        W = edge_exact(bx, ay, by, ax, W);
+    }
+    if ((U < 0.0f || Vv < 0.0f || W < 0.0f) && (U > 0.0f || Vv > 0.0f || W > 0.0f)) return 0;
+    float det = U + Vv + W;
+    if (det == 0.0f) return 0;
+    float T = fmaf(W, s->sz * c.z, fmaf(Vv, s->sz * b.z, U * (s->sz * a.z)));
     float inv = 1.0f / det;
-    *u = un * inv;
-    *v = vn * inv;
-    *t = vdot(e2, qv) * inv;
+    *t = T * inv;
+    *u = Vv * inv;
+    *v = W * inv;
     return 1;
 }
 
-static void try_leaf(const lbvh* B, int leaf, v3 o, v3 d, float tmin, hitrec* h) {
+static void try_leaf(const lbvh* B, int leaf, const shear_t* s, v3 o, float tmin, hitrec* h) {
     float t, u, v;
-    if (!mt_test(o, d, B->tri + 9 * (size_t)leaf, &t, &u, &v)) return;
+    if (!woop_test(s, o, B->tri + 9 * (size_t)leaf, &t, &u, &v)) return;
     int orig = B->tri_orig[leaf];
     if (t > tmin && (t < h->t || (t == h->t && orig < h->orig))) {
         h->t = t; h->u = u; h->v = v; h->idx = leaf; h->orig = orig;
@@ -678,6 +729,17 @@ static void try_leaf(const lbvh* B, int leaf, v3 o, v3 d, float tmin, hitrec* h)
 }
 
 typedef struct { float t; int slot, ref; } ckey;
+
+/* traversal-stack pushes dropped for want of room (ORC_MAXDEPTH), since the
+ * last orc_reset_stack_drops: each a missed subtree, as on the GPU
+ * (rr_frame_stats.stack_drops) */
+static long long g_drops;
+static void drop_push(void) {
+#pragma omp atomic
+    g_drops += 1;
+}
+long long orc_stack_drops(void) { return g_drops; }
+void orc_reset_stack_drops(void) { g_drops = 0; }
 
 /* Quantised wide walk of rr_device.h TravStateQW: per axis s = iq * 2^e,
  * o' = (org - o) * iq, plane t = fma(q, s, o'), near plane lo for iq >= 0 else
@@ -690,6 +752,7 @@ typedef struct { float t; int slot, ref; } ckey;
 static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hitrec* h) {
     h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
     if (B->n <= 0) return 0;
+    const shear_t sh = make_shear(d);
     const v3 iqv = rcp3(d);
     const float iq[3] = {iqv.x, iqv.y, iqv.z};
     const float oo[3] = {o.x, o.y, o.z};
@@ -699,14 +762,24 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
         const uint32_t* nd = B->q4 + 16 * (size_t)node;
         const uint32_t inner = nd[3] >> 24;
         const float tcur = h->t;
-        float sc[3], of[3];
+        float sc[3], of[3], dif[3], ext[3], onr[3], ofr[3];
         int pos[3];
         for (int a = 0; a < 3; ++a) {
             float org;
             memcpy(&org, nd + a, sizeof org);
-            sc[a] = ldexpf(iq[a], (int)((nd[3] >> (8 * a)) & 255u) - 128);
-            of[a] = (org - oo[a]) * iq[a];
+            const int e = (int)((nd[3] >> (8 * a)) & 255u) - 128;
+            sc[a] = ldexpf(iq[a], e);
+            dif[a] = org - oo[a];
+            of[a] = dif[a] * iq[a];
+            ext[a] = ldexpf(255.0f, e);
             pos[a] = iq[a] >= 0.0f;
+        }
+        /* the node's margin (rr_device.h q6_planes) */
+        const float mg = fmaxf(fmaxf(fabsf(dif[0]) + ext[0], fabsf(dif[1]) + ext[1]), fabsf(dif[2]) + ext[2]) * ORC_BOX_MARGIN;
+        for (int a = 0; a < 3; ++a) {
+            const float ma = mg * fabsf(iq[a]);
+            onr[a] = of[a] - ma;
+            ofr[a] = of[a] + ma;
         }
         /* near / far grid coordinates per axis: children 0..3 one byte of a
          * word, 4 and 5 a byte pair */
@@ -725,20 +798,20 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             for (int a = 0; a < 3; ++a) {
                 const uint32_t qn = c < 4 ? (nw[a] >> (8 * c)) & 255u : (nw2[a] >> (8 * (c - 4))) & 255u;
                 const uint32_t qf = c < 4 ? (fw[a] >> (8 * c)) & 255u : (fw2[a] >> (8 * (c - 4))) & 255u;
-                p0[a] = fmaf((float)qn, sc[a], of[a]);
-                p1[a] = fmaf((float)qf, sc[a], of[a]);
+                p0[a] = fmaf((float)qn, sc[a], onr[a]);
+                p1[a] = fmaf((float)qf, sc[a], ofr[a]);
             }
             const float tn = fmaxf(fmaxf(p0[0], p0[1]), fmaxf(p0[2], tmin));
             const float tf = fminf(fminf(p1[0], p1[1]), fminf(p1[2], tcur));
             const int is_inner = (inner >> c) & 1u;
             const int ref = is_inner ? (int)nd[4] + n_in : ~((int)nd[5] + n_lf);
             if (is_inner) ++n_in; else ++n_lf;
-            const int hit = tn <= tf;
+            const int hit = tn <= tf && ((nd[15] >> c) & 1u);
             k[c].slot = c;
             k[c].ref = ref;
             k[c].t = (hit && is_inner) ? tn : INFINITY;
             if (hit && !is_inner) {
-                try_leaf(B, ~ref, o, d, tmin, h);
+                try_leaf(B, ~ref, &sh, o, tmin, h);
                 if (any && h->idx >= 0) return 1;
             }
         }
@@ -754,7 +827,10 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             continue;
         }
         for (int c = ORC_QW_MAX - 1; c >= 0; --c)
-            if (c != best && k[c].t != INFINITY && sp < ORC_MAXDEPTH) stack[sp++] = k[c].ref;
+            if (c != best && k[c].t != INFINITY) {
+                if (sp < ORC_MAXDEPTH) stack[sp++] = k[c].ref;
+                else drop_push();
+            }
         node = k[best].ref;
     }
     return h->idx >= 0;
@@ -766,26 +842,29 @@ static int trace(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hit
     if (B->width == 4) return trace4(B, o, d, tmin, tmax, any, h);
     h->t = tmax; h->u = h->v = 0.0f; h->idx = -1; h->orig = -1;
     if (B->n <= 0) return 0;
+    const shear_t sh = make_shear(d);
     v3 inv = rcp3(d);
     v3 oi = V(-(o.x * inv.x), -(o.y * inv.y), -(o.z * inv.z));
+    v3 em = slab_margin(o, inv, scene_radius(B->box));
     int stack[ORC_MAXDEPTH];
     int sp = 0, node = 0;
     for (;;) {
         const float* bx = B->box + 12 * (size_t)node;
         float tl, tr;
-        int hl = slab_test(oi, inv, bx, tmin, h->t, &tl);
-        int hr = slab_test(oi, inv, bx + 6, tmin, h->t, &tr);
+        int hl = slab_test(oi, inv, em, bx, tmin, h->t, &tl);
+        int hr = slab_test(oi, inv, em, bx + 6, tmin, h->t, &tr);
         int cl = B->child_lf[2 * node], cr = B->child_lf[2 * node + 1];
         int nl = 0, nr = 0, fl = 0, fr = 0;
         if (hl && cl < 0) { fl = leaf_first(cl); nl = leaf_count(cl); hl = 0; }
         if (hr && cr < 0) { fr = leaf_first(cr); nr = leaf_count(cr); hr = 0; }
         for (int k = 0; k < nl + nr; ++k) {
-            try_leaf(B, k < nl ? fl + k : fr + (k - nl), o, d, tmin, h);
+            try_leaf(B, k < nl ? fl + k : fr + (k - nl), &sh, o, tmin, h);
             if (any && h->idx >= 0) return 1;
         }
         if (hl && hr) {
             int lf = tl <= tr;
             if (sp < ORC_MAXDEPTH) stack[sp++] = lf ? cr : cl;
+            else drop_push();
             node = lf ? cl : cr;
         } else if (hl) node = cl;
         else if (hr) node = cr;
@@ -1029,7 +1108,8 @@ static mat_t load_mat(const float* mats, int id) {
 /* Hull flags of an LDS-resident scene's triangle (csrc/wavefront.hip
  * stage_scene, hull_flags; same float operations): bit 0 when every vertex of
  * every triangle lies behind the triangle's plane on its front side (the
- * cross(e1, e2) direction), up to 2^-12 of the vertex's distance times |n|_1,
+ * cross(e1, e2) direction, e1 = v1 - v0, e2 = v2 - v0), up to 2^-12 of the
+ * vertex's distance times |n|_1,
  * bit 1 the same for the back side. A ray that leaves the triangle on a side
  * whose bit is set moves away from a plane the whole scene lies behind, so it
  * meets nothing: the continuation misses and the shadow ray is unoccluded
@@ -1038,13 +1118,12 @@ static mat_t load_mat(const float* mats, int id) {
 static unsigned tri_hull(const lbvh* B, int i) {
     const float* s = B->tri + 9 * (size_t)i;
     const v3 v0 = V(s[0], s[1], s[2]);
-    const v3 n = vcross(V(s[3], s[4], s[5]), V(s[6], s[7], s[8]));
+    const v3 n = vcross(vsub(V(s[3], s[4], s[5]), v0), vsub(V(s[6], s[7], s[8]), v0));
     const float an = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
     int front = 1, back = 1;
     for (int j = 0; j < B->n; ++j) {
         const float* e = B->tri + 9 * (size_t)j;
-        const v3 w0 = V(e[0], e[1], e[2]);
-        const v3 w[3] = {w0, vadd(w0, V(e[3], e[4], e[5])), vadd(w0, V(e[6], e[7], e[8]))};
+        const v3 w[3] = {V(e[0], e[1], e[2]), V(e[3], e[4], e[5]), V(e[6], e[7], e[8])};
         for (int k = 0; k < 3; ++k) {
             const v3 r = vsub(w[k], v0);
             const float h = vdot(n, r);
@@ -1067,12 +1146,14 @@ static double wall_s(void) {
 }
 static int g_late[32], g_n_late;
 
-static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
+/* The camera ray of (pix, sample) (csrc/wavefront.hip camera_ray_xy): the
+ * subpixel pair is the 16-bit halves of the path key itself (a hash output),
+ * filter-importance sampled; (fx, fy) its subpixel position. */
+static void camera_ray(const scene_t* S, int pix, int sample, uint32_t* key_out, v3* o, v3* d, float* tmin,
+                       float* tmax, float* fx_out, float* fy_out) {
     const float* c = S->cam;
     uint32_t key = pkey(S->seed, (uint32_t)pix, (uint32_t)sample);
     int px = pix % S->W, py = pix / S->W;
-    /* the camera subpixel pair: the 16-bit halves of the path key itself (a
-     * hash output; csrc/wavefront.hip camera_ray_xy) */
     const float ux = (float)(key >> 16) * 1.52587890625e-05f, uy = (float)(key & 0xffffu) * 1.52587890625e-05f;
     float fx = (float)px + 0.5f + lerp_table(S->filter, ORC_FILTER_N, ux);
     float fy = (float)py + 0.5f + lerp_table(S->filter, ORC_FILTER_N, uy);
@@ -1082,9 +1163,20 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
     v3 dw = V(fmaf(c[6], sy, fmaf(c[3], sx, -c[9])), fmaf(c[7], sy, fmaf(c[4], sx, -c[10])),
               fmaf(c[8], sy, fmaf(c[5], sx, -c[11])));
     float il = 1.0f / len;
-    v3 d = vscl(dw, il);
-    v3 o = V(c[0], c[1], c[2]);
-    float tmin = c[14] * len, tmax = c[15] * len;
+    *d = vscl(dw, il);
+    *o = V(c[0], c[1], c[2]);
+    *tmin = c[14] * len;
+    *tmax = c[15] * len;
+    *key_out = key;
+    *fx_out = fx;
+    *fy_out = fy;
+}
+
+static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
+    uint32_t key;
+    v3 o, d;
+    float tmin, tmax, fx, fy;
+    camera_ray(S, pix, sample, &key, &o, &d, &tmin, &tmax, &fx, &fy);
     v3 L = V(0.0f, 0.0f, 0.0f), T = V(1.0f, 1.0f, 1.0f);
     int nd = 0, ng = 0;  /* diffuse / glossy scatters so far (Cycles path_state_next) */
     int esc = 0;         /* the ray leaves a hull side of its triangle (tri_hull): it meets nothing */
@@ -1099,7 +1191,8 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
              * construction keeps every triangle a ray can hit; the accept rule
              * is order-independent, so the result is the same) */
             h.t = tmax; h.u = h.v = 0.0f; h.idx = -1; h.orig = -1;
-            for (int i = 0; i < S->bvh->n; ++i) try_leaf(S->bvh, i, o, d, tmin, &h);
+            const shear_t sh = make_shear(d);
+            for (int i = 0; i < S->bvh->n; ++i) try_leaf(S->bvh, i, &sh, o, tmin, &h);
         } else if (esc) {
             h.t = tmax; h.u = h.v = 0.0f; h.idx = -1; h.orig = -1;
         } else {
@@ -1112,7 +1205,7 @@ static v3 radiance(const scene_t* S, int pix, int sample, long long rays[4]) {
             break;
         }
         const float* tp = S->bvh->tri + 9 * (size_t)h.idx;
-        v3 e1 = V(tp[3], tp[4], tp[5]), e2 = V(tp[6], tp[7], tp[8]);
+        v3 e1 = vsub(V(tp[3], tp[4], tp[5]), V(tp[0], tp[1], tp[2])), e2 = vsub(V(tp[6], tp[7], tp[8]), V(tp[0], tp[1], tp[2]));
         const int mid = S->bvh->tri_mat[h.idx];
         mat_t m = load_mat(S->mats, mid);
         const float* lut = S->luts + ORC_LUT_STRIDE * (size_t)mid;
@@ -1358,14 +1451,13 @@ int orc_trace_brute(int n, const float* tris9, int n_rays, const float* rays, fl
     for (int r = 0; r < n_rays; ++r) {
         const float* R = rays + 8 * (size_t)r;
         v3 o = V(R[0], R[1], R[2]), d = V(R[4], R[5], R[6]);
+        const shear_t sh = make_shear(d);
         float best = R[7];
         int bo = -1;
         float bu = 0, bv = 0;
         for (int i = 0; i < n; ++i) {
-            const float* t = tris9 + 9 * (size_t)i;
-            float pk[9] = {t[0], t[1], t[2], t[3] - t[0], t[4] - t[1], t[5] - t[2], t[6] - t[0], t[7] - t[1], t[8] - t[2]};
             float tt, u, v;
-            if (!mt_test(o, d, pk, &tt, &u, &v)) continue;
+            if (!woop_test(&sh, o, tris9 + 9 * (size_t)i, &tt, &u, &v)) continue;
             if (tt > R[3] && (tt < best || (tt == best && i < bo))) { best = tt; bo = i; bu = u; bv = v; }
         }
         if (hits) { hits[4 * r] = bo >= 0 ? best : R[7]; hits[4 * r + 1] = bu; hits[4 * r + 2] = bv; hits[4 * r + 3] = 0; }
@@ -1545,6 +1637,29 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
     free(S);
     lbvh_free(&B);
     return 0;
+}
+
+/* Camera rays of (pixel, sample) pairs as rays of orc_trace (o, tmin, d,
+ * tmax per ray), for the camera floats / render ints / render floats of
+ * rr_debug_frame_state: tests trace the rays of individual paths. */
+void orc_camera_rays(const float* cam, const int32_t* ri, const float* rf, int n, const int32_t* pix,
+                     const int32_t* sample, float* rays8) {
+    scene_t* S = (scene_t*)calloc(1, sizeof(scene_t));
+    S->cam = cam;
+    S->W = ri[0]; S->H = ri[1]; S->seed = (uint32_t)ri[4];
+    S->inv_w2 = 2.0f / (float)S->W;
+    S->inv_h2 = 2.0f / (float)S->H;
+    orc_filter_table(rf[1], S->filter);
+    for (int i = 0; i < n; ++i) {
+        uint32_t key;
+        v3 o, d;
+        float tmin, tmax, fx, fy;
+        camera_ray(S, pix[i], sample[i], &key, &o, &d, &tmin, &tmax, &fx, &fy);
+        float* r = rays8 + 8 * (size_t)i;
+        r[0] = o.x; r[1] = o.y; r[2] = o.z; r[3] = tmin;
+        r[4] = d.x; r[5] = d.y; r[6] = d.z; r[7] = tmax;
+    }
+    free(S);
 }
 
 /* Expose a few primitives for the known-answer tests. */

@@ -163,6 +163,7 @@ def test_gpu_placement_follows_numa_nodes(tmp_path):
     for r, cpus in enumerate(plan):
         assert len(cpus) == 32 and cpus <= node_cpus[numa_of[r]]
     assert len(set().union(*plan)) == 256  # disjoint
+    assert [sum(1 for c in plan if c <= node_cpus[n]) for n in (0, 1)] == [4, 4]  # four ranks per socket
     # two ranks on one GPU (the one-GPU rehearsal) split that GPU's node
     p2 = b.gpu_placement([5, 5], allowed, numa, lambda n: node_cpus[n])
     assert p2[0] and p2[1] and not p2[0] & p2[1] and p2[0] | p2[1] == node_cpus[1]

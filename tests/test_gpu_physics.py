@@ -191,3 +191,105 @@ def test_c5_frame_bit_exact_reduced(ctx, rr, sc5):
     assert int(np.count_nonzero(rgba != orgba)) == 0
     assert np.array_equal(film, of)
     assert stats.n_triangles == 512 * 20480 + 2
+
+
+def _host_world_tris(path, scene_obj, frame):
+    """World triangles by the host restatement: the object's pose from
+    oracle/host_oracle.py (object_matrix for the scene's explicit objects,
+    rigid_matrix for the generated bodies), rounded to float32 as the upload
+    does (scene.cpp obj_xform), times the object-space vertices in k_transform's
+    order ((m0 x + m1 y) + m2 z) + m3 in float32 (no contraction)."""
+    from oracle import host_oracle as HO
+    scene = HO.load_scene(path)
+    bodies = HO.expand_rigid_bodies(scene)
+    n_explicit = len(scene["objects"])
+    fps, f0 = scene["render"]["fps"], scene["render"]["frame_start"]
+    local, obj = scene_obj.mesh()
+    mats = np.zeros((n_explicit + len(bodies), 3, 4), np.float32)
+    for i in np.unique(obj):
+        M = HO.object_matrix(scene["objects"][i], frame) if i < n_explicit else \
+            HO.rigid_matrix(bodies[i - n_explicit], (frame - f0) / fps)
+        mats[i] = np.asarray(M, np.float64)[:3, :4].astype(np.float32)
+    m = mats[obj]                                           # (n, 3, 4)
+    x, y, z = local[..., 0:1], local[..., 1:2], local[..., 2:3]  # (n, 3, 1)
+    return ((m[:, None, :, 0] * x + m[:, None, :, 1] * y) + m[:, None, :, 2] * z) + m[:, None, :, 3]
+
+
+@pytest.mark.parametrize("path,frames", [(S02, (1, 90, 170)), (S03, (1, 300)), (SC5, (120, 200))])
+def test_device_world_triangles_match_host_restatement(ctx, path, frames):
+    """The device's world transform (k_transform) of the physics stand-ins and
+    C5 equals the host restatement bit for bit, so every parity test that
+    feeds the oracle the device's own world triangles (frame_state) starts
+    from pinned geometry (test_scene.py pins the poses themselves)."""
+    s = ctx.load_scene(path)
+    try:
+        for f in frames:
+            st = ctx.frame_state(s, f)
+            want = _host_world_tris(path, s, f)
+            nbad = int(np.count_nonzero(st.tris != want))
+            assert st.tris.shape == want.shape and nbad == 0, f"frame {f}: {nbad} coordinates differ"
+    finally:
+        s.close()
+
+
+def _band_rows(H, n):
+    return [int(r) for r in np.linspace(0, H - 4, n).astype(int)]
+
+
+@pytest.mark.parametrize("job_name,frames,n_bands", [
+    ("02_physics-standin_170f-5w_naive-fine.toml", [1, 90, 170], 4),
+    ("03_physics-2-standin_480f-8w_dynamic.toml", [300], 4),
+    ("c5_synthetic-10m_240f-8w_dynamic.toml", [150], 2)])
+def test_bench_config_split_path_bands_bit_exact(rr, tmp_path, job_name, frames, n_bands):
+    """The split path at the size the bench renders it (02 / 03: 1920x1080 x
+    64 spp, C5: 3840x2160 x 1024 spp in sample chunks; scene defaults) through
+    BackendRunner.render_frames as bench.py times it, PNG so the written file
+    is lossless: 4-row oracle bands spread over each frame equal the file bit
+    for bit, so the chunking, the queue segments, lane refill and the
+    windowed ray order are compared with the oracle at full size. Neither side
+    drops a traversal-stack push."""
+    import os
+    import time
+    from PIL import Image
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    job = rr.BlenderJob.load_from_file(os.path.join(root, "jobs", job_name))
+    job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": str(tmp_path),
+                                   "output_file_format": "PNG"})
+    runner = rr.BackendRunner(root, params=rr.default_params())
+    try:
+        t0 = time.time()
+        runner.render_frames(job, frames)
+        t_gpu = time.time() - t0
+        scene = runner._scene(rr.parse_with_base_directory_prefix(job.project_file_path, root))
+        O.stack_drops(reset=True)
+        for f in frames:
+            out = rr.naming.output_path_without_extension(str(tmp_path), job.output_file_name_format, f)
+            img = np.asarray(Image.open(out + ".png").convert("RGBA"))
+            st = runner.ctx.frame_state(scene, f)
+            H, W = img.shape[:2]
+            assert (W, H) == (int(st.render_ints[0]), int(st.render_ints[1]))
+            for r0 in _band_rows(H, n_bands):
+                t1 = time.time()
+                _, orgba = O.render_state(st, rows=(r0, r0 + 4), film=False)
+                nbad = int(np.count_nonzero(img[r0:r0 + 4] != orgba[r0:r0 + 4]))
+                print(f"{job_name} frame {f} rows {r0}..{r0 + 3}: {nbad} mismatches "
+                      f"(oracle {time.time() - t1:.1f} s; device frames {t_gpu:.1f} s)")
+                assert nbad == 0
+        assert O.stack_drops() == 0
+    finally:
+        runner.close()
+
+
+@pytest.mark.parametrize("path,frame", [(S02, 90), (S03, 300), (SC5, 150)])
+def test_no_traversal_stack_drops(ctx, rr, path, frame):
+    """The counting pass reports no dropped traversal-stack push (each would be
+    a missed subtree) on any split-path bench scene, camera, extension and
+    shadow rays alike."""
+    s = ctx.load_scene(path)
+    try:
+        p = rr.default_params(width=480, height=270, spp=8, flags=rr.native.RR_FLAG_COUNT_TRAVERSAL)
+        _, _, st = ctx.render_to_memory(s, frame, p)
+        print(f"{path}: nodes per class {list(st.trav_nodes)}, drops {st.stack_drops}")
+        assert st.trav_nodes[0] > 0 and st.stack_drops == 0
+    finally:
+        s.close()

@@ -3,6 +3,7 @@ GPU's checker: Cycles (the reference's renderer) is third-party and absent, so
 the oracle is pinned by analytic known answers instead:
 ray/triangle cases, LBVH == brute force, uniform RNG and disk sampling, BSDF
 identities, the white furnace and the point-light closed form."""
+import dataclasses
 import math
 
 import numpy as np
@@ -87,6 +88,167 @@ def test_ray_triangle_known_cases():
     assert list(prims) == [0, 0, -1, -1, -1, -1]
     assert hits[0, 0] == 1.0 and hits[0, 1] == 0.25 and hits[0, 2] == 0.25
     assert list(occ) == [1, 1, 0, 0, 0, 0]
+
+
+def _rot(seed):
+    q, _ = np.linalg.qr(np.random.default_rng(seed).normal(size=(3, 3)))
+    return q.astype(np.float32)
+
+
+def closed_meshes():
+    """Closed convex meshes whose triangles share their vertices bit for bit:
+    the 04vs cube at two frames (the product's own float32 transform,
+    world_tris), an icosphere of 1,280 triangles rotated in float32, and an
+    axis-aligned cube (rays can run exactly along its faces)."""
+    scene = HO.load_scene(scene_path("04_very-simple-standin.rrscene"))
+    out = {f"04vs-{f}": world_tris(scene, f)[0] for f in (1, 30)}
+    ico = icosphere_tris(3, 1.5)
+    out["ico3"] = (ico.reshape(-1, 3) @ _rot(3).T + np.float32(0.25)).astype(np.float32).reshape(-1, 3, 3)
+    c = np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1) for z in (-1, 1)], np.float32)
+    quads = [(0, 1, 3, 2), (4, 6, 7, 5), (0, 4, 5, 1), (2, 3, 7, 6), (0, 2, 6, 4), (1, 5, 7, 3)]
+    out["aabb"] = np.array([[c[a], c[b], c[cc]] for a, b, cc, _ in quads] +
+                           [[c[a], c[cc], c[d]] for a, _, cc, d in quads], np.float32)
+    return out
+
+
+def edge_vertex_rays(tris, n_edge, seed):
+    """Rays from outside aimed at the mesh's vertices (exactly: d = the
+    normalised difference, in float32) and at random points of its edges, from
+    origins on a sphere three times the mesh's radius."""
+    rng = np.random.default_rng(seed)
+    verts = np.unique(tris.reshape(-1, 3), axis=0)
+    edges = np.concatenate([tris[:, [0, 1]], tris[:, [1, 2]], tris[:, [2, 0]]])
+    t = rng.random((n_edge, 1)).astype(np.float32)
+    e = edges[rng.integers(0, len(edges), n_edge)]
+    pts = np.concatenate([verts, (e[:, 0] + t * (e[:, 1] - e[:, 0])).astype(np.float32)])
+    ctr = tris.reshape(-1, 3).mean(axis=0)
+    rad = np.linalg.norm(tris.reshape(-1, 3) - ctr, axis=1).max()
+    u = rng.normal(size=(len(pts), 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    o = (ctr + 3.0 * rad * u).astype(np.float32)
+    d = pts - o
+    d = (d / np.linalg.norm(d.astype(np.float64), axis=1, keepdims=True)).astype(np.float32)
+    return np.concatenate([o, np.zeros((len(o), 1)), d, np.full((len(o), 1), 1e30)], axis=1).astype(np.float32)
+
+
+def outward_normals(tris):
+    n = np.cross(tris[:, 1] - tris[:, 0], tris[:, 2] - tris[:, 0]).astype(np.float64)
+    ctr = tris.reshape(-1, 3).mean(axis=0)
+    s = np.sign(np.einsum("ij,ij->i", n, tris.mean(axis=1) - ctr))
+    return n * s[:, None]
+
+
+@pytest.mark.parametrize("name", ["04vs-1", "04vs-30", "ico3", "aabb"])
+def test_watertight_edges_and_vertices(name):
+    """Closed meshes hit from outside at their edges and vertices: every ray
+    that reaches the mesh hits a front face first — no ray slips through a
+    shared edge or vertex into the interior (a back face), on the BVH2, the
+    quantised 6-wide walk and brute force alike (woop_test with margins on the
+    box tests). A ray aimed at a surface point can only miss when it grazes
+    the silhouette."""
+    tris = closed_meshes()[name]
+    rays = edge_vertex_rays(tris, 20000, 7)
+    if name == "aabb":  # rays exactly along the faces' planes, at the edges
+        extra = []
+        for a in range(3):
+            for s in (-1.0, 1.0):
+                for b in range(3):
+                    if b == a:
+                        continue
+                    o = np.zeros(3, np.float32)
+                    o[a] = 5.0 * s
+                    o[b] = 1.0
+                    d = np.zeros(3, np.float32)
+                    d[a] = -s
+                    extra.append([*o, 0.0, *d, 1e30])
+        rays = np.concatenate([rays, np.array(extra, np.float32)])
+    bh, bp = O.trace_brute(tris, rays)
+    for width in (2, 4):
+        h, p, occ = O.trace(tris, rays, width=width)
+        assert np.array_equal(p, bp), f"width {width}: {np.count_nonzero(p != bp)} differ from brute force"
+        assert np.array_equal(occ.astype(bool), p >= 0)
+    leaks, lost, through = convex_leaks(tris, rays, bp, bh[:, 0])
+    print(f"{name}: {len(rays)} rays, {int(through.sum())} through the solid, {lost} of them lost, "
+          f"{leaks} hits past the entry point")
+    assert leaks == 0 and lost == 0
+    assert through.mean() > 0.5
+
+
+def convex_leaks(tris, rays, prims, t_hit):
+    """Against the exact (double) entry / exit distances of a closed convex
+    mesh (the largest entering, the smallest leaving face-plane distance):
+    hits farther than the entry point (a path through a crack to the inside
+    of a far face) and rays that pass through the solid, entry to exit longer
+    than 1e-4 of their distance, yet hit nothing (a path through a crack to
+    the other side). A ray grazing the silhouette may hit or miss; on an edge
+    it may hit either face, at the entry distance. Returns (hits past the
+    entry, rays lost, mask of the rays through the solid)."""
+    n = outward_normals(tris)
+    o, d = rays[:, 0:3].astype(np.float64), rays[:, 4:7].astype(np.float64)
+    den = d @ n.T                                            # (rays, faces)
+    num = np.einsum("fk,fk->f", n, tris[:, 0].astype(np.float64))[None, :] - o @ n.T
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tf = num / den
+        t_entry = np.where(den < 0, tf, -np.inf).max(axis=1)
+        t_exit = np.where(den > 0, tf, np.inf).min(axis=1)
+    hit = prims >= 0
+    scale = np.linalg.norm(o - tris.reshape(-1, 3).mean(axis=0), axis=1)
+    late = hit & (t_hit.astype(np.float64) > t_entry + 1e-4 * scale)
+    through = (t_exit - t_entry > 1e-4 * scale) & (t_entry > 0)
+    return int(late.sum()), int((through & ~hit).sum()), through
+
+
+def late_paths_at_edges(tris, state, late):
+    """For late paths (pixel, sample) of oracle.ray_counts(): the distance of
+    each one's camera hit from the nearest triangle edge, relative to the
+    scene's extent (the camera ray traced by the oracle, O.camera_rays)."""
+    pix = [int(p) for p, _ in late]
+    smp = [int(q) for _, q in late]
+    rays = O.camera_rays(state, pix, smp)
+    h, p, _ = O.trace(tris, rays, width=2)
+    t = tris.astype(np.float64)
+    ext = float(np.ptp(t.reshape(-1, 3), axis=0).max())
+    out = []
+    for r, hh, pp in zip(rays, h, p):
+        assert pp >= 0
+        P = r[0:3].astype(np.float64) + float(hh[0]) * r[4:7].astype(np.float64)
+        best = np.inf
+        for a, b in ((0, 1), (1, 2), (2, 0)):
+            A, B = t[:, a], t[:, b]
+            u = np.clip(np.einsum("ij,ij->i", P - A, B - A) / np.einsum("ij,ij->i", B - A, B - A), 0, 1)
+            best = min(best, float(np.linalg.norm(P - (A + u[:, None] * (B - A)), axis=1).min()))
+        out.append(best / ext)
+    return out
+
+
+@pytest.mark.parametrize("frame", [6, 47, 50])
+def test_late_paths_start_at_silhouette_edges(rr, frame):
+    """04vs at 1920x1080 x 4 spp through the traversed hierarchy (the split
+    path's, no hull rule): a path that reaches a second surface of the closed,
+    convex cube started with a camera ray that met the cube exactly on an edge
+    (its hit within 1e-6 of the cube's extent of a triangle edge) — a graze of
+    the silhouette, where the far face's hit distance can round below the near
+    one's; no camera ray passes through a crack (test_watertight_edges_and_
+    vertices). Frames 47 and 50 have such paths, frame 6 (the frame whose
+    path leaked through an edge crack under round 3's triangle test) has none."""
+    scene = HO.load_scene(scene_path("04_very-simple-standin.rrscene"))
+    s = rr.Scene(scene_path("04_very-simple-standin.rrscene"))
+    try:
+        st = s.frame_constants(frame, rr.default_params(spp=4))
+    finally:
+        s.close()
+    tris, mats = world_tris(scene, frame)
+    ri = np.array(st.render_ints, np.int32)
+    ri[7] = 4  # the quantised 6-wide walk of the split path
+    O.render(tris, mats, st.camera, st.lights, st.materials, st.world, ri, st.render_floats, film=False, rgba=False)
+    (c0, s0, c1, s1), late = O.ray_counts()
+    print(f"frame {frame}: continuations {c0} + {c1}, late paths {late}")
+    assert c0 > 0
+    assert (c1 > 0) == (frame != 6) and len(late) == c1
+    st = dataclasses.replace(st, render_ints=ri)
+    d = late_paths_at_edges(tris, st, late)
+    print(f"  camera hits of the late paths: {d} of the extent from an edge")
+    assert all(x < 1e-6 for x in d)
 
 
 def test_lbvh_structure_and_brute_force():
