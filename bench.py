@@ -567,6 +567,11 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=No
             out["issue_util_at_kernel_clock"] = round(out["achieved"] * 1e9 /
                                                       (VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * kc * 1e9), 3)
         out["wave_fill_solo"] = round(float(getattr(cstats, "kernel_wave_fill", 0.0)), 3)
+        lu = (e_wh or {}).get("valu_lane_util") if (timed and timed["whole"]) else (e_sl or {}).get("valu_lane_util")
+        if lu is not None:  # active lanes per issued VALU instruction (PMC, SQ_THREAD_CYCLES_VALU)
+            out["valu_lane_util"] = round(lu, 3)
+            if out.get("frac") is not None:
+                out["frac_lane_weighted"] = round(out["frac"] * lu, 3)
         t_ms = out.get("avg_launch_ms", avg_ms)
         comp = bytes_frame / launches_frame / (t_ms * 1e-3) / 1e9
         tr = e_wh if (e_wh and timed and timed["whole"]) else e_sl

@@ -487,14 +487,31 @@ RR_HD float edge_exact(float a, float b, float c, float d, float e) {
 }
 // make_shear for a unit direction (camera rays): its largest component is at
 // least 1/sqrt(3) in magnitude, inside rcp_rn's range, so no range test.
-RR_HD Shear make_shear_unit(float3 d) {
+RR_HD int shear_axis(float3 d) {
     const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    return ax >= ay ? (ax >= az ? 0 : 2) : (ay >= az ? 1 : 2);
+}
+RR_HD Shear make_shear_unit(float3 d) {
     Shear s;
-    s.kz = ax >= ay ? (ax >= az ? 0 : 2) : (ay >= az ? 1 : 2);
+    s.kz = shear_axis(d);
     const float3 r = rot3(d, s.kz);
     s.sz = rcp_rn(r.z);
     s.sx = r.x * s.sz;
     s.sy = r.y * s.sz;
+    return s;
+}
+// make_shear_unit for a kz known at compile time (the same operations: no
+// per-lane permutation).
+template <int K>
+RR_HD Shear make_shear_unit_k(float3 d) {
+    Shear s;
+    s.kz = K;
+    const float rz = K == 0 ? d.x : (K == 1 ? d.y : d.z);
+    const float rx = K == 0 ? d.y : (K == 1 ? d.z : d.x);
+    const float ry = K == 0 ? d.z : (K == 1 ? d.x : d.y);
+    s.sz = rcp_rn(rz);
+    s.sx = rx * s.sz;
+    s.sy = ry * s.sz;
     return s;
 }
 // The test from the vertices relative to the origin, already permuted (a, b, c
@@ -511,9 +528,12 @@ RR_HD bool woop_core(const Shear& s, float3 a, float3 b, float3 c, float& t, flo
         V = edge_exact(ax, cy, ay, cx, V);
         W = edge_exact(bx, ay, by, ax, W);
     }
-    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+    // the sign test (no two of U, V, W of opposite signs: min < 0 < max
+    // rejects; fminf / fmaxf skip NaN as the comparisons do) and det != 0 as
+    // one predicate: one divergent branch per test, not three
     const float det = U + V + W;
-    if (det == 0.0f) return false;
+    const float mn = fminf(fminf(U, V), W), mx = fmaxf(fmaxf(U, V), W);
+    if (((mn < 0.0f) & (mx > 0.0f)) | (det == 0.0f)) return false;
     const float T = fmaf(W, s.sz * c.z, fmaf(V, s.sz * b.z, U * (s.sz * a.z)));
     const float inv = 1.0f / det;
     t = T * inv;
@@ -532,12 +552,15 @@ struct Hit {
 };
 
 // Accept rule making the closest hit order-independent: smaller t wins; equal t
-// -> smaller original id wins.
+// -> smaller original id wins (bitwise on the predicates: one branch).
+RR_HD bool closer(float t, int orig, float tmin, const Hit& h) {
+    return (t > tmin) & ((t < h.t) | ((t == h.t) & (orig < h.orig)));
+}
 RR_HD void closest_tri(const TriPack& tp, int idx, const Shear& s, float3 o, float tmin, Hit& h) {
     float t, u, v;
     if (!woop_test(s, o, xyz(tp.p0), xyz(tp.p1), xyz(tp.p2), t, u, v)) return;
     const int orig = f2i(tp.p0.w);
-    if (t > tmin && (t < h.t || (t == h.t && orig < h.orig))) {
+    if (closer(t, orig, tmin, h)) {
         h.t = t;
         h.u = u;
         h.v = v;
@@ -709,35 +732,52 @@ struct TravState {
     }
 };
 
+// Radius term of the quantised walk's margins (slab_margin): twice the
+// largest |coordinate| of the root's grid (org .. org + 255 * 2^e per axis),
+// which bounds |org| + 255 * 2^e of every node: the plane distances of the
+// walk are within 8 ulp of |org - o| + 6 ulp of 255 * 2^e (times |iq|) and the
+// projected vertices within 8 ulp of |v - o|, under the margin's 32 ulp of
+// |o|_inf + this.
+RR_HD float q6_margin_radius(const QNode6& root) {
+    const uint32_t eb = (uint32_t)f2i(root.org.w);
+    float r = 0.0f;
+    const float org[3] = {root.org.x, root.org.y, root.org.z};
+    for (int a = 0; a < 3; ++a) {
+        const float hi = org[a] + ldexpf(255.0f, (int)((eb >> (8 * a)) & 255u) - 128);
+        r = fmaxf(r, fmaxf(fabsf(org[a]), fabsf(hi)));
+    }
+    return 2.0f * r;
+}
+
+// Margin distance of one ray of the quantised walk: kBoxMargin (|o|_inf + r),
+// r = q6_margin_radius; in t on axis a it is this times |iq_a| (slab_margin's).
+RR_HD float ray_margin(float3 o, float r) { return (fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + r) * kBoxMargin; }
+
 // Per-node terms of the quantised box tests for one ray (iq: rcp3 of the
-// direction). Per axis s = iq * 2^e (exact), o' = (org - o) * iq; a plane at
-// grid coordinate q lies at t = fma(q, s, o'). The near planes use o' minus
-// the axis' margin, the far planes o' plus it (kBoxMargin of the node's
-// largest per-axis |org - o| + 255 * 2^e, times |iq|), so a box holding a
-// triangle woop_test accepts is never rejected by rounding.
+// direction, m: ray_margin). Per axis s = iq * 2^e (exact); a plane at grid
+// coordinate q lies at t = fma(q, s, (org - o) * iq), the near planes' offsets
+// less the axis' margin m |iq|, the far planes' more, folded into one fma
+// each, so a box holding a triangle woop_test accepts is never rejected by
+// rounding.
 struct Q6Planes {
     float sx, sy, sz;     // iq * 2^e
-    float nx, ny, nz;     // o' - margin (near planes)
-    float fx, fy, fz;     // o' + margin (far planes)
+    float nx, ny, nz;     // (org - o) iq - margin (near planes)
+    float fx, fy, fz;     // (org - o) iq + margin (far planes)
 };
-RR_D Q6Planes q6_planes(const QNode6& n, float3 o, float3 iq) {
+RR_D Q6Planes q6_planes(const QNode6& n, float3 o, float3 iq, float m) {
+    const float3 em = mk3(m * fabsf(iq.x), m * fabsf(iq.y), m * fabsf(iq.z));
     const uint32_t eb = (uint32_t)f2i(n.org.w);
-    const int ex = (int)(eb & 255u) - 128, ey = (int)((eb >> 8) & 255u) - 128, ez = (int)((eb >> 16) & 255u) - 128;
     Q6Planes p;
-    p.sx = ldexpf(iq.x, ex);
-    p.sy = ldexpf(iq.y, ey);
-    p.sz = ldexpf(iq.z, ez);
+    p.sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
+    p.sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
+    p.sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
     const float dx = n.org.x - o.x, dy = n.org.y - o.y, dz = n.org.z - o.z;
-    const float ox = dx * iq.x, oy = dy * iq.y, oz = dz * iq.z;
-    const float m = fmaxf(fmaxf(fabsf(dx) + ldexpf(255.0f, ex), fabsf(dy) + ldexpf(255.0f, ey)),
-                          fabsf(dz) + ldexpf(255.0f, ez)) * kBoxMargin;
-    const float mx = m * fabsf(iq.x), my = m * fabsf(iq.y), mz = m * fabsf(iq.z);
-    p.nx = ox - mx;
-    p.ny = oy - my;
-    p.nz = oz - mz;
-    p.fx = ox + mx;
-    p.fy = oy + my;
-    p.fz = oz + mz;
+    p.nx = fmaf(dx, iq.x, -em.x);
+    p.ny = fmaf(dy, iq.y, -em.y);
+    p.nz = fmaf(dz, iq.z, -em.z);
+    p.fx = fmaf(dx, iq.x, em.x);
+    p.fy = fmaf(dy, iq.y, em.y);
+    p.fz = fmaf(dz, iq.z, em.z);
     return p;
 }
 
@@ -747,8 +787,9 @@ RR_D Q6Planes q6_planes(const QNode6& n, float3 o, float3 iq) {
 // fmaxf / fminf drop their operands); tn[c] = the entry distance. The near
 // plane is lo for iq >= 0, else hi (iq is never 0 or inf, so no NaN and no
 // min/max per axis). oracle/rr_oracle.c trace4() restates it.
-RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, float tn[kQWidth]) {
-    const Q6Planes pl = q6_planes(n, o, iq);
+RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float m, float tmin, float tcur,
+                          float tn[kQWidth]) {
+    const Q6Planes pl = q6_planes(n, o, iq, m);
     const float sx = pl.sx, sy = pl.sy, sz = pl.sz;
     const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
     // children 0..3: one byte each of the near / far words per axis
@@ -786,8 +827,9 @@ RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, floa
 // slot order drops the distance compares and their registers (shadow rays
 // -10 % on C5, VGPR spill slots 10 -> 2).
 template <bool kNearest = true>
-RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, uint32_t imask, int& best) {
-    const Q6Planes pl = q6_planes(n, o, iq);
+RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float m, float tmin, float tcur, uint32_t imask,
+                          int& best) {
+    const Q6Planes pl = q6_planes(n, o, iq, m);
     const float sx = pl.sx, sy = pl.sy, sz = pl.sz;
     const uint32_t used = n.c.w;
     const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
@@ -857,11 +899,13 @@ RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6 {
     float3 o, iq;
+    float mrg;  // ray_margin
     Shear sh;
     float tmin;
     Hit h;
     int node;
-    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_) {
+    // r: q6_margin_radius of the hierarchy's root (the box margins)
+    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_, float r) {
         o = o_;
         sh = make_shear(d_);
         tmin = tmin_;
@@ -870,6 +914,7 @@ struct TravStateQ6 {
         h.idx = -1;
         h.orig = -1;
         iq = rcp3(d_);
+        mrg = ray_margin(o, r);
         node = 0;
     }
     template <typename NodeSrc, typename TriP, typename Stack>
@@ -879,7 +924,7 @@ struct TravStateQ6 {
         const QNode6 nd = q6_load(nodes, node);
         const uint32_t imask = q6_inner(nd);
         int best;
-        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, tmin, tcur, imask, best);
+        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, mrg, tmin, tcur, imask, best);
         uint32_t leaves = hm & ~imask;
         const uint32_t inner = hm & imask;
         // passing leaves in slot order; the loop runs as often as the lane with
@@ -1115,6 +1160,17 @@ RR_HD bool bsdf_sample_onb(const Mat& m, FloatP lut, const BsdfView& vw, float3 
     float x, y;  // the disk sample both lobes start from
     concentric_disk(u1, u2, x, y);
     glossy = ul < ps;
+#if RR_AB_UNIFIED_LOBE
+    {
+        const bool g = glossy;
+        const float3 wl = g ? mk3(dot3(wo, T), dot3(wo, B), cosV) : mk3(0.0f, 0.0f, 1.0f);
+        const float3 l = sample_vndf(wl, g ? m.alpha : 1.0f, x, y);
+        const float3 W = frame3(T, B, N, l.x, l.y, l.z);
+        const float k = 2.0f * dot3(wo, W);
+        const float3 r = mk3(fmaf(W.x, k, -wo.x), fmaf(W.y, k, -wo.y), fmaf(W.z, k, -wo.z));
+        wi = g ? r : W;
+    }
+#else
     // the lobe's direction in the local frame: the GGX half vector (glossy)
     // or the cosine-weighted point (diffuse); one frame3 for both, so a wave
     // whose lanes picked both lobes runs it once
@@ -1133,6 +1189,7 @@ RR_HD bool bsdf_sample_onb(const Mat& m, FloatP lut, const BsdfView& vw, float3 
     } else {
         wi = W;
     }
+#endif
     f = bsdf_eval_v(m, lut, vw, N, wo, wi, pdf);
     return pdf > 0.0f;
 }

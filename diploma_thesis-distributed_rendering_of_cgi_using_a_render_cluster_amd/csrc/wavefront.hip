@@ -677,22 +677,20 @@ RR_D void set_miss(Hit& h, float tmax) {
     h.orig = -1;
 }
 template <bool kCount>
-RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float tmin, float tmax, Hit& h,
-                     TravCount& cnt) {
-    set_miss(h, tmax);
-    const Shear sh = make_shear_unit(d);  // camera_ray_xy: d = dw / |dw|
+RR_D void camera_tris(const LdsView& v, uint64_t m0, uint64_t m1, const Shear& sh, int kz, float tmin, Hit& h,
+                      TravCount& cnt) {
     for (int w = 0; w < 2; ++w) {
         uint64_t m = w ? m1 : m0;
         while (m) {
             const int i = (int)__builtin_ctzll(m) + 64 * w;
             m &= m - 1;
             if (kCount) ++cnt.tris;
-            const lds_f4w* q = v.cam + kCamF4 * i + 3 * sh.kz;  // this ray's permutation
+            const lds_f4w* q = v.cam + kCamF4 * i + 3 * kz;  // this ray's permutation
             const float4 ca = lds_ld4(q), cb = lds_ld4(q + 1), cc = lds_ld4(q + 2);
             float t, u, vv;
             if (woop_core(sh, xyz(ca), xyz(cb), xyz(cc), t, u, vv)) {
                 const int orig = f2i(ca.w);
-                if (t > tmin && (t < h.t || (t == h.t && orig < h.orig))) {
+                if (closer(t, orig, tmin, h)) {
                     h.t = t;
                     h.u = u;
                     h.v = vv;
@@ -701,6 +699,27 @@ RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float
                 }
             }
         }
+    }
+}
+// The camera rays of a wave nearly always share their shear axis (the
+// camera's forward axis dominates every direction of a tile): then kz is a
+// scalar, the shear needs no per-lane permutation and the staged vertices'
+// address no per-lane offset; otherwise the per-lane form. Same bits.
+template <bool kCount>
+RR_D void camera_hit(const LdsView& v, uint64_t m0, uint64_t m1, float3 d, float tmin, float tmax, Hit& h,
+                     TravCount& cnt) {
+    set_miss(h, tmax);
+    // camera_ray_xy: d = dw / |dw|
+    const int kz = shear_axis(d), k0 = __builtin_amdgcn_readfirstlane(kz);
+#ifndef RR_CAM_UNIFORM_KZ
+#define RR_CAM_UNIFORM_KZ 1
+#endif
+    if (RR_CAM_UNIFORM_KZ && __all(kz == k0)) {
+        if (k0 == 0) camera_tris<kCount>(v, m0, m1, make_shear_unit_k<0>(d), 0, tmin, h, cnt);
+        else if (k0 == 1) camera_tris<kCount>(v, m0, m1, make_shear_unit_k<1>(d), 1, tmin, h, cnt);
+        else camera_tris<kCount>(v, m0, m1, make_shear_unit_k<2>(d), 2, tmin, h, cnt);
+    } else {
+        camera_tris<kCount>(v, m0, m1, make_shear_unit(d), kz, tmin, h, cnt);
     }
 }
 
@@ -814,9 +833,15 @@ RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
     __syncthreads();
     return Q6Nodes{sa.qnodes, top, n};
 }
+// The hierarchy's margin radius (q6_margin_radius of the root), wave-uniform.
+RR_D float walk_radius(const SceneArgs& sa, const Q6Nodes& nodes) {
+    if (sa.n_qnodes <= 0) return 0.0f;
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(q6_margin_radius(q6_load(nodes, 0)))));
+}
+// r: q6_margin_radius of the hierarchy (wave-uniform)
 template <typename TS, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
-RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack& st, TravCount& cnt, MapFn&& map,
-                       RayFn&& ray_of, DoneFn&& done) {
+RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, TravStack& st, TravCount& cnt,
+                       MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int nw = gridDim.x * kWavesPerBlock;
@@ -836,7 +861,7 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, TravStack&
                 float3 o, d;
                 float tmin, tmax;
                 ray_of(ks, o, d, tmin, tmax);
-                ts.start(o, d, tmin, tmax);
+                ts.start(o, d, tmin, tmax, r);
                 st.sp = 0;
                 if (n_tris > 0) {
                     j = k;
@@ -966,7 +991,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameCons
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, np, st, cnt, [](int p) { return (uint32_t)p; },
+        nodes, sa.tris, sa.n_tris, np, walk_radius(sa, nodes), st, cnt, [](int p) { return (uint32_t)p; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
             const int sl = (int)fc.div_npix.div(p);
             const int pix = (int)p - sl * fc.npix;
@@ -1004,9 +1029,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameCons
 constexpr int kPacketStack = 128;  // a node pushes <= 5: bounded by 5 x the hierarchy depth
 template <bool kCount>
 RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk, bool act,
-                       float3 o, float3 d, float tmin, Hit& h, TravCount& cnt, uint32_t& dropped) {
+                       float3 o, float3 d, float tmin, float r, Hit& h, TravCount& cnt, uint32_t& dropped) {
     if (!__ballot(act)) return;
     const float3 iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
+    const float mrg = ray_margin(o, r);
     const Shear sh = make_shear(d);
     int node = 0, sp = 0;
     for (;;) {
@@ -1014,7 +1040,7 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
         const QNode6 nd = nodes[node];  // wave-uniform: scalar loads
         const uint32_t imask = q6_inner(nd);
         float tn[kQWidth];
-        const uint32_t hm = live ? q6_box_hits(nd, o, iq, tmin, h.t, tn) : 0u;
+        const uint32_t hm = live ? q6_box_hits(nd, o, iq, mrg, tmin, h.t, tn) : 0u;
         if (kCount && live) ++cnt.nodes;
         // leaf children in slot order (a lane tests those its ray enters)
 #pragma unroll
@@ -1081,6 +1107,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
     const int npk = ntiles * (np / fc.npix);
     const int nw = gridDim.x * kWavesPerBlock;
     uint32_t n_traced = 0, dropped = 0;
+    const float rad = sa.n_qnodes > 0 ? q6_margin_radius(sa.qnodes[0]) : 0.0f;  // wave-uniform (scalar loads)
     for (int q = xcd_wave_rank(); q < npk; q += nw) {
         const int sl = q / ntiles, t = q - sl * ntiles;
         const int ty = t / tiles_x, tx = t - ty * tiles_x;
@@ -1097,7 +1124,8 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         n_traced += valid && !culled ? 1u : 0u;
         Hit h;
         set_miss(h, tmax);
-        packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt, dropped);
+        packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, rad, h, cnt,
+                             dropped);
         if (valid) hits[(size_t)sl * fc.npix + pix] = pack_hit(h);
     }
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
@@ -1149,7 +1177,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_extend(SceneArgs 
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, walk_radius(sa, nodes), st, cnt, [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
@@ -1209,7 +1237,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_shadow_refill(SceneArgs
     TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, walk_radius(sa, nodes), st, cnt, [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
@@ -1850,10 +1878,11 @@ __global__ void k_debug_trace4(const QNode6* __restrict__ nodes, const TriPack* 
     const int nthreads = gridDim.x * kBlock;
     TravStack st{lds_slot(lds_stack), spill, nthreads, 0};
     TravCount cnt;
+    const float rad = n_tris > 0 ? q6_margin_radius(nodes[0]) : 0.0f;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
         TravStateQ6<false> ts;
-        ts.start(xyz(o), xyz(d), o.w, d.w);
+        ts.start(xyz(o), xyz(d), o.w, d.w, rad);
         st.sp = 0;
         if (n_tris > 0)
             while (!ts.step(nodes, tris, st, cnt)) {
@@ -1861,7 +1890,7 @@ __global__ void k_debug_trace4(const QNode6* __restrict__ nodes, const TriPack* 
         hits[i] = make_float4(ts.h.t, ts.h.u, ts.h.v, 0.0f);
         prims[i] = ts.h.orig;
         TravStateQ6<true> ta;
-        ta.start(xyz(o), xyz(d), o.w, d.w);
+        ta.start(xyz(o), xyz(d), o.w, d.w, rad);
         st.sp = 0;
         if (n_tris > 0)
             while (!ta.step(nodes, tris, st, cnt)) {

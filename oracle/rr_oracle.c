@@ -583,10 +583,71 @@ static int c4_gather(const lbvh* B, int ref, int* out) {
     return k + c4_gather(B, B->child[2 * ref + 1], out + k);
 }
 
+/* Research switch (tools/collapse_study.py, not the product): 1 = the wide
+ * nodes chosen by a surface-area dynamic programme over the BVH2 (Ylitie et
+ * al. 2017) instead of the greedy opening of c4_set. */
+static int g_collapse;
+void orc_set_collapse(int mode) { g_collapse = mode; }
+static double box_area_d(const float* b) {
+    double dx = (double)b[3] - b[0], dy = (double)b[4] - b[1], dz = (double)b[5] - b[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+/* dp_dist[6 n + j - 1] = least cost of covering BVH2 subtree n with at most j
+ * entries of a wide node; dp_pick[6 n + j - 1] = 0: n itself is the entry,
+ * a > 0: a entries for the left child, j - a for the right; dp_root[n] = the
+ * left child's share when n is a wide node. */
+static double* dp_dist;
+static unsigned char *dp_pick, *dp_root;
+static double dp_child(const lbvh* B, int ref, int j) { return ref < 0 ? 0.0 : dp_dist[6 * (size_t)ref + j - 1]; }
+static void dp_build(const lbvh* B) {
+    const int ni = B->n - 1;
+    dp_dist = (double*)malloc(sizeof(double) * 6 * (size_t)ni);
+    dp_pick = (unsigned char*)malloc(6 * (size_t)ni);
+    dp_root = (unsigned char*)malloc((size_t)ni);
+    for (int v = ni - 1; v >= 0; --v) {  /* PLOC: children have larger indices */
+        const int l = B->child[2 * v], r = B->child[2 * v + 1];
+        float box[6];
+        for (int a = 0; a < 3; ++a) {
+            box[a] = fminf(B->box[12 * (size_t)v + a], B->box[12 * (size_t)v + 6 + a]);
+            box[3 + a] = fmaxf(B->box[12 * (size_t)v + 3 + a], B->box[12 * (size_t)v + 9 + a]);
+        }
+        double best = INFINITY;
+        int ba = 1;
+        for (int a = 1; a <= 5; ++a) {
+            double c = dp_child(B, l, a) + dp_child(B, r, 6 - a);
+            if (c < best) { best = c; ba = a; }
+        }
+        const double own = box_area_d(box) + best;
+        dp_root[v] = (unsigned char)ba;
+        for (int j = 1; j <= 6; ++j) {
+            double bj = own;
+            int pick = 0;
+            for (int a = 1; a < j; ++a) {
+                double c = dp_child(B, l, a) + dp_child(B, r, j - a);
+                if (c < bj) { bj = c; pick = a; }
+            }
+            dp_dist[6 * (size_t)v + j - 1] = bj;
+            dp_pick[6 * (size_t)v + j - 1] = (unsigned char)pick;
+        }
+    }
+}
+static void dp_expand(const lbvh* B, int v, int side, int j, c4set* S) {
+    const int ref = B->child[2 * v + side];
+    if (ref >= 0 && dp_pick[6 * (size_t)ref + j - 1] != 0) {
+        const int a = dp_pick[6 * (size_t)ref + j - 1];
+        dp_expand(B, ref, 0, a, S);
+        dp_expand(B, ref, 1, j - a, S);
+        return;
+    }
+    c4_put(B, S, S->m++, v, side);
+}
+
 static void lbvh_collapse4(lbvh* B) {
     const int n = B->n;
     B->n4 = 0;
     if (n <= 0) return;
+    const int dp = g_collapse == 1 && n > 2;
+    if (dp) dp_build(B);
     const int ni = n > 1 ? n - 1 : 1;
     int* src = (int*)malloc(sizeof(int) * (size_t)ni);
     int* perm = (int*)malloc(sizeof(int) * (size_t)n);  /* BVH4 triangle position -> sorted leaf */
@@ -596,7 +657,14 @@ static void lbvh_collapse4(lbvh* B) {
     int count = 1, ntri = 0;
     for (int idx = 0; idx < count; ++idx) {
         c4set S;
-        c4_set(B, src[idx], &S);
+        if (dp) {
+            const int a = dp_root[src[idx]];
+            S.m = 0;
+            dp_expand(B, src[idx], 0, a, &S);
+            dp_expand(B, src[idx], 1, 6 - a, &S);
+        } else {
+            c4_set(B, src[idx], &S);
+        }
         int ref[ORC_QW_MAX];
         uint32_t inner = 0;
         const int inner_base = count, tri_base = ntri;
@@ -627,6 +695,7 @@ static void lbvh_collapse4(lbvh* B) {
     free(B->tri); free(B->tri_orig); free(B->tri_mat);
     B->tri = tri; B->tri_orig = orig; B->tri_mat = mat;
     free(src); free(perm);
+    if (dp) { free(dp_dist); free(dp_pick); free(dp_root); }
 }
 
 /* ------------------------------------------------------------ tracing ---- */
@@ -708,9 +777,9 @@ static int woop_test(const shear_t* s, v3 o, const float* t9, float* t, float* u
         Vv = edge_exact(ax, cy, ay, cx, Vv);
         W = edge_exact(bx, ay, by, ax, W);
     }
-    if ((U < 0.0f || Vv < 0.0f || W < 0.0f) && (U > 0.0f || Vv > 0.0f || W > 0.0f)) return 0;
     float det = U + Vv + W;
-    if (det == 0.0f) return 0;
+    float mn = fminf(fminf(U, Vv), W), mx = fmaxf(fmaxf(U, Vv), W);
+    if ((mn < 0.0f && mx > 0.0f) || det == 0.0f) return 0;
     float T = fmaf(W, s->sz * c.z, fmaf(Vv, s->sz * b.z, U * (s->sz * a.z)));
     float inv = 1.0f / det;
     *t = T * inv;
@@ -729,6 +798,14 @@ static void try_leaf(const lbvh* B, int leaf, const shear_t* s, v3 o, float tmin
 }
 
 typedef struct { float t; int slot, ref; } ckey;
+
+/* node visits / triangle tests of trace4 since the last reset (research:
+ * tools/collapse_study.py) */
+static long long g_cnt_nodes, g_cnt_tris;
+void orc_walk_counts(long long* out2, int reset) {
+    out2[0] = g_cnt_nodes; out2[1] = g_cnt_tris;
+    if (reset) g_cnt_nodes = g_cnt_tris = 0;
+}
 
 /* traversal-stack pushes dropped for want of room (ORC_MAXDEPTH), since the
  * last orc_reset_stack_drops: each a missed subtree, as on the GPU
@@ -754,32 +831,35 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
     if (B->n <= 0) return 0;
     const shear_t sh = make_shear(d);
     const v3 iqv = rcp3(d);
+    /* the ray's margin distance (rr_device.h ray_margin, q6_margin_radius of the root) */
+    float rr = 0.0f;
+    for (int a = 0; a < 3; ++a) {
+        float org, hi;
+        memcpy(&org, B->q4 + a, sizeof org);
+        hi = org + ldexpf(255.0f, (int)((B->q4[3] >> (8 * a)) & 255u) - 128);
+        rr = fmaxf(rr, fmaxf(fabsf(org), fabsf(hi)));
+    }
+    const float mrg = (fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + 2.0f * rr) * ORC_BOX_MARGIN;
     const float iq[3] = {iqv.x, iqv.y, iqv.z};
     const float oo[3] = {o.x, o.y, o.z};
     int stack[ORC_MAXDEPTH];
     int sp = 0, node = 0;
+    long long cn = 0, ct = 0;
     for (;;) {
+        ++cn;
         const uint32_t* nd = B->q4 + 16 * (size_t)node;
         const uint32_t inner = nd[3] >> 24;
         const float tcur = h->t;
-        float sc[3], of[3], dif[3], ext[3], onr[3], ofr[3];
+        float sc[3], onr[3], ofr[3];
         int pos[3];
-        for (int a = 0; a < 3; ++a) {
+        for (int a = 0; a < 3; ++a) {  /* rr_device.h q6_planes */
             float org;
             memcpy(&org, nd + a, sizeof org);
-            const int e = (int)((nd[3] >> (8 * a)) & 255u) - 128;
-            sc[a] = ldexpf(iq[a], e);
-            dif[a] = org - oo[a];
-            of[a] = dif[a] * iq[a];
-            ext[a] = ldexpf(255.0f, e);
+            sc[a] = ldexpf(iq[a], (int)((nd[3] >> (8 * a)) & 255u) - 128);
+            const float dif = org - oo[a], ma = mrg * fabsf(iq[a]);
+            onr[a] = fmaf(dif, iq[a], -ma);
+            ofr[a] = fmaf(dif, iq[a], ma);
             pos[a] = iq[a] >= 0.0f;
-        }
-        /* the node's margin (rr_device.h q6_planes) */
-        const float mg = fmaxf(fmaxf(fabsf(dif[0]) + ext[0], fabsf(dif[1]) + ext[1]), fabsf(dif[2]) + ext[2]) * ORC_BOX_MARGIN;
-        for (int a = 0; a < 3; ++a) {
-            const float ma = mg * fabsf(iq[a]);
-            onr[a] = of[a] - ma;
-            ofr[a] = of[a] + ma;
         }
         /* near / far grid coordinates per axis: children 0..3 one byte of a
          * word, 4 and 5 a byte pair */
@@ -811,8 +891,9 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             k[c].ref = ref;
             k[c].t = (hit && is_inner) ? tn : INFINITY;
             if (hit && !is_inner) {
+                ++ct;
                 try_leaf(B, ~ref, &sh, o, tmin, h);
-                if (any && h->idx >= 0) return 1;
+                if (any && h->idx >= 0) goto done;
             }
         }
         /* nearest hit internal child next (ties: lower slot; any-hit rays:
@@ -833,6 +914,11 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             }
         node = k[best].ref;
     }
+done:
+#pragma omp atomic
+    g_cnt_nodes += cn;
+#pragma omp atomic
+    g_cnt_tris += ct;
     return h->idx >= 0;
 }
 

@@ -110,6 +110,11 @@ def cmd_traffic(a):
             e["l2_hit_rate"] = e["TCC_HIT_sum"] / (e["TCC_HIT_sum"] + e["TCC_MISS_sum"])
         if "SQ_WAIT_ANY" in e and e.get("SQ_WAVE_CYCLES", 0) > 0:
             e["wait_frac"] = e["SQ_WAIT_ANY"] / e["SQ_WAVE_CYCLES"]
+        # active lanes per VALU instruction (rocprofiler-sdk counter_defs.yaml
+        # VALUUtilization: THREAD_CYCLES_VALU / (ACTIVE_INST_VALU x wave size));
+        # SQ_INSTS_VALU counts wave-instructions whatever the exec mask
+        if e.get("SQ_ACTIVE_INST_VALU", 0) > 0 and "SQ_THREAD_CYCLES_VALU" in e:
+            e["valu_lane_util"] = e["SQ_THREAD_CYCLES_VALU"] / (64.0 * e["SQ_ACTIVE_INST_VALU"])
         out["kernels"][k] = e
     with open(a.o, "w") as fh:
         json.dump(out, fh, indent=1)

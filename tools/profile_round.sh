@@ -46,7 +46,7 @@ timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INS
     --output-format csv -d "$out/sq1" -o run -- python3 $B > /dev/null
 echo "sq1 done"
 timeout -s KILL 240 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_WR \
-    TCC_HIT_sum TCC_MISS_sum \
+    SQ_THREAD_CYCLES_VALU TCC_HIT_sum TCC_MISS_sum \
     --output-format csv -d "$out/sq2" -o run -- python3 $B > /dev/null
 echo "sq2 done"
 python3 tools/pmc_summary.py stats "$out/trace" > "$out/${tag}_kernel_stats.md"
