@@ -533,9 +533,7 @@ __global__ void k_qw_advance(int32_t* __restrict__ ctl, int bound, const uint32_
 #endif
 constexpr int kPlocR = RR_PLOC_R;
 
-// cluster k: cl[2k] = (lo.xyz, ref bits), cl[2k+1] = (hi.xyz, leaves under it);
-// a PLOC node's d.z / d.w hold the leaf counts of its two children (the BVH4
-// collapse of an older round kept small subtrees as leaves; unused now)
+// cluster k: cl[2k] = (lo.xyz, ref bits), cl[2k+1] = (hi.xyz, 0)
 __device__ __forceinline__ float ploc_area(float4 alo, float4 ahi, float4 blo, float4 bhi) {
     const float dx = fmaxf(ahi.x, bhi.x) - fminf(alo.x, blo.x);
     const float dy = fmaxf(ahi.y, bhi.y) - fminf(alo.y, blo.y);
@@ -560,7 +558,7 @@ __global__ __launch_bounds__(kBlock) void k_ploc_init(int n, const uint32_t* __r
     cl[2 * i] = make_float4(fminf(fminf(a.x, b.x), c.x), fminf(fminf(a.y, b.y), c.y), fminf(fminf(a.z, b.z), c.z),
                             i2f(~i));
     cl[2 * i + 1] = make_float4(fmaxf(fmaxf(a.x, b.x), c.x), fmaxf(fmaxf(a.y, b.y), c.y),
-                                fmaxf(fmaxf(a.z, b.z), c.z), i2f(1));  // .w: leaves under the cluster
+                                fmaxf(fmaxf(a.z, b.z), c.z), 0.0f);
 }
 
 // Nearest neighbour within kPlocR positions (ascending scan, strict <).
@@ -631,11 +629,10 @@ __global__ __launch_bounds__(kBlock) void k_ploc_apply(const int* __restrict__ c
         nd.a = make_float4(alo.x, alo.y, alo.z, ahi.x);
         nd.b = make_float4(ahi.y, ahi.z, blo.x, blo.y);
         nd.c = make_float4(blo.z, bhi.x, bhi.y, bhi.z);
-        nd.d = make_int4(f2i(alo.w), f2i(blo.w), f2i(ahi.w), f2i(bhi.w));  // child refs, child leaf counts
+        nd.d = make_int4(f2i(alo.w), f2i(blo.w), 0, 0);  // child refs
         nodes[idx] = nd;
         cl_out[2 * o] = make_float4(fminf(alo.x, blo.x), fminf(alo.y, blo.y), fminf(alo.z, blo.z), i2f(idx));
-        cl_out[2 * o + 1] = make_float4(fmaxf(ahi.x, bhi.x), fmaxf(ahi.y, bhi.y), fmaxf(ahi.z, bhi.z),
-                                        i2f(f2i(ahi.w) + f2i(bhi.w)));
+        cl_out[2 * o + 1] = make_float4(fmaxf(ahi.x, bhi.x), fmaxf(ahi.y, bhi.y), fmaxf(ahi.z, bhi.z), 0.0f);
     } else {
         cl_out[2 * o] = alo;
         cl_out[2 * o + 1] = ahi;

@@ -179,7 +179,6 @@ typedef struct {
     int* tri_orig;
     int* tri_mat;
     int width;        /* hierarchy trace() walks: 2 (BVH2) or 4 (the quantised wide collapse, ORC_QW children) */
-    int* cnt;         /* 2 per internal node: leaf count of each child subtree (PLOC, Karras) */
     int n4;           /* quantised wide nodes */
     int* child4;      /* ORC_QW per node (derived from the node, for tests): >= 0 node, < 0 ~leaf, ORC_EMPTY4 unused */
     uint32_t* q4;     /* 16 words per node, csrc/rr_device.h QNode6 */
@@ -231,7 +230,7 @@ static void subtree_box(const lbvh* B, const float* tris9, int c, float out[6]) 
 }
 
 static void lbvh_free(lbvh* B) {
-    free(B->child4); free(B->q4); free(B->child_lf); free(B->range); free(B->cnt);
+    free(B->child4); free(B->q4); free(B->child_lf); free(B->range);
     free(B->keys); free(B->order); free(B->child); free(B->box);
     free(B->tri); free(B->tri_orig); free(B->tri_mat);
     memset(B, 0, sizeof *B);
@@ -292,7 +291,6 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats, int 
     B->child = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->child_lf = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->range = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
-    B->cnt = (int*)malloc(sizeof(int) * 2 * (size_t)ni);
     B->box = (float*)malloc(sizeof(float) * 12 * (size_t)ni);
     if (hier == 3 && n > 2) {
         ploc_build(B, tris9);
@@ -301,7 +299,6 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats, int 
     }
     if (n == 1) {
         B->child[0] = ~0; B->child[1] = ~0;
-        B->cnt[0] = B->cnt[1] = 1;
     } else {
         const uint32_t* k = B->keys;
         for (int i = 0; i < n - 1; ++i) {
@@ -325,8 +322,6 @@ static void lbvh_build(lbvh* B, int n, const float* tris9, const int* mats, int 
             B->child[2 * i + 1] = (hi_ == g + 1) ? ~(g + 1) : g + 1;
             B->range[2 * i] = lo_;
             B->range[2 * i + 1] = hi_ - lo_ + 1;
-            B->cnt[2 * i] = g - lo_ + 1;       /* leaves of the left subtree [lo_, g] */
-            B->cnt[2 * i + 1] = hi_ - g;       /* and of the right one [g + 1, hi_] */
         }
     }
     /* boxes bottom-up: children of node i have larger indices or are leaves?
@@ -395,12 +390,9 @@ static void ploc_build(lbvh* B, const float* tris9) {
     float* box = (float*)malloc(sizeof(float) * 6 * (size_t)n);
     float* box2 = (float*)malloc(sizeof(float) * 6 * (size_t)n);
     int* nn = (int*)malloc(sizeof(int) * (size_t)n);
-    int* cn = (int*)malloc(sizeof(int) * (size_t)n);   /* leaves under each cluster */
-    int* cn2 = (int*)malloc(sizeof(int) * (size_t)n);
     for (int i = 0; i < n; ++i) {
         tri_box(tris9 + 9 * (size_t)B->order[i], box + 6 * (size_t)i);
         ref[i] = ~i;
-        cn[i] = 1;
     }
     int cnt = n, next = n - 2;
     while (cnt > 1) {
@@ -433,14 +425,10 @@ static void ploc_build(lbvh* B, const float* tris9) {
                 for (int t = 0; t < 6; ++t) { nb[t] = a[t]; nb[6 + t] = b[t]; }
                 B->child[2 * idx] = ref[i];
                 B->child[2 * idx + 1] = ref[j];
-                B->cnt[2 * idx] = cn[i];
-                B->cnt[2 * idx + 1] = cn[j];
                 for (int t = 0; t < 3; ++t) { o[t] = fminf(a[t], b[t]); o[3 + t] = fmaxf(a[3 + t], b[3 + t]); }
-                cn2[k] = cn[i] + cn[j];
                 ref2[k++] = idx;
             } else {
                 for (int t = 0; t < 6; ++t) o[t] = a[t];
-                cn2[k] = cn[i];
                 ref2[k++] = ref[i];
             }
         }
@@ -448,9 +436,8 @@ static void ploc_build(lbvh* B, const float* tris9) {
         cnt = k;
         int* tr = ref; ref = ref2; ref2 = tr;
         float* tb = box; box = box2; box2 = tb;
-        int* tc = cn; cn = cn2; cn2 = tc;
     }
-    free(ref); free(ref2); free(box); free(box2); free(nn); free(cn); free(cn2);
+    free(ref); free(ref2); free(box); free(box2); free(nn);
 }
 
 /* Quantisation of the BVH4 child boxes (csrc/rr_device.h q4_exponent /
@@ -530,7 +517,7 @@ static void q4_pack(const float lo[3][ORC_QW_MAX], const float hi[3][ORC_QW_MAX]
 /* BVH4 collapse of the BVH2 (PLOC, or Karras below 3 triangles), as
  * csrc/bvh.hip build_bvh4 (k_c4_count / k_c4_emit): breadth first from the
  * root; a node's children start as its BVH2 root's two children. A child
- * subtree of at most ORC_LEAF_TRIS triangles is a leaf entry (never opened);
+ * single triangle is a leaf entry (never opened);
  * while there are fewer than four entries, the internal entry with the
  * largest box measure dx*dy + dy*dz + dz*dx (ties: lowest slot) is replaced
  * by its left child and its right child appended. The internal children of a
@@ -542,18 +529,16 @@ static void q4_pack(const float lo[3][ORC_QW_MAX], const float hi[3][ORC_QW_MAX]
  * tri_mat are permuted into that order, so a leaf ref names the range
  * ~(first | (count - 1) << 28) of it). Boxes are the BVH2 child boxes,
  * quantised by q4_pack. */
-#define ORC_LEAF_TRIS 1
-typedef struct { int m; int ref[ORC_QW_MAX], cnt[ORC_QW_MAX]; float lo[3][ORC_QW_MAX], hi[3][ORC_QW_MAX]; } c4set;
+typedef struct { int m; int ref[ORC_QW_MAX]; float lo[3][ORC_QW_MAX], hi[3][ORC_QW_MAX]; } c4set;
 
 static void c4_put(const lbvh* B, c4set* S, int slot, int node, int side) {
     const float* f = B->box + 12 * (size_t)node + 6 * side;
     for (int a = 0; a < 3; ++a) { S->lo[a][slot] = f[a]; S->hi[a][slot] = f[3 + a]; }
     S->ref[slot] = B->n > 1 ? B->child[2 * node + side] : ~0;
-    S->cnt[slot] = B->n > 1 ? B->cnt[2 * node + side] : 1;
 }
 
-/* an entry that stays a leaf: one triangle, or a subtree of <= ORC_LEAF_TRIS */
-static int c4_leaf(const c4set* S, int c) { return S->ref[c] < 0 || S->cnt[c] <= ORC_LEAF_TRIS; }
+/* an entry that stays a leaf: one triangle (the product's leaves hold one) */
+static int c4_leaf(const c4set* S, int c) { return S->ref[c] < 0; }
 
 static void c4_set(const lbvh* B, int r, c4set* S) {
     c4_put(B, S, 0, r, 0);
@@ -574,13 +559,6 @@ static void c4_set(const lbvh* B, int r, c4set* S) {
         c4_put(B, S, best, cn, 0);
         ++S->m;
     }
-}
-
-/* sorted leaf indices of the subtree ref (left first), returns the count */
-static int c4_gather(const lbvh* B, int ref, int* out) {
-    if (ref < 0) { out[0] = ~ref; return 1; }
-    int k = c4_gather(B, B->child[2 * ref], out);
-    return k + c4_gather(B, B->child[2 * ref + 1], out + k);
 }
 
 /* Research switch (tools/collapse_study.py, not the product): 1 = the wide
@@ -672,8 +650,8 @@ static void lbvh_collapse4(lbvh* B) {
             if (c >= S.m) ref[c] = ORC_EMPTY4;
             else if (!c4_leaf(&S, c)) { src[count] = S.ref[c]; ref[c] = count++; inner |= 1u << c; }
             else if (n == 1) { perm[0] = 0; ref[c] = leaf_ref(0, 1); ntri = 1; }
-            else { /* a leaf entry is one triangle (ORC_LEAF_TRIS 1): position ntri */
-                c4_gather(B, S.ref[c], perm + ntri);
+            else { /* a leaf entry is one triangle: position ntri */
+                perm[ntri] = ~S.ref[c];
                 ref[c] = leaf_ref(ntri, 1);
                 ntri += 1;
             }
