@@ -611,11 +611,13 @@ RR_D TriPack load_tri(lds_tri* p, int i) {
     t.p2 = lds_ld4(q + 2);
     return t;
 }
-struct TravStack {
+// kB: the threads per block of the kernel that owns the stack.
+template <int kB = kBlock>
+struct TravStackT {
     // Bases only: the lane's slots are recomputed from threadIdx/blockIdx at each
     // push/pop, so no per-lane pointer stays live in VGPRs across a kernel's
-    // ray loop (every kernel launches kBlock threads per block).
-    lds_int* lds;   // lds_base: lane slot lds[sp * kBlock + threadIdx.x]
+    // ray loop.
+    lds_int* lds;   // lds_base: lane slot lds[sp * kB + threadIdx.x]
     int* spill;     // spill_base: lane slot spill[(sp - kLdsStack) * stride + global thread]
     int spill_stride;
     int sp;
@@ -627,9 +629,9 @@ struct TravStack {
     // (ORC_MAXDEPTH) and counts its drops too (orc_stack_drops).
     RR_D void push(int x) {
         if (sp < kLdsStack) {
-            lds[sp * kBlock + (int)threadIdx.x] = x;
+            lds[sp * kB + (int)threadIdx.x] = x;
         } else if (sp < kLdsStack + kSpillStack) {
-            spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kBlock + threadIdx.x)] = x;
+            spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)] = x;
         } else {
             ++dropped;
             return;
@@ -638,10 +640,11 @@ struct TravStack {
     }
     RR_D int pop() {
         --sp;
-        if (sp < kLdsStack) return lds[sp * kBlock + (int)threadIdx.x];
-        return spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kBlock + threadIdx.x)];
+        if (sp < kLdsStack) return lds[sp * kB + (int)threadIdx.x];
+        return spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)];
     }
 };
+using TravStack = TravStackT<kBlock>;
 
 RR_D lds_int* lds_slot(int* shared_elem) {
     return (lds_int*)(shared_elem);

@@ -783,6 +783,16 @@ constexpr int kRefillBelow = RR_REFILL_BELOW;
 #define RR_TRACE_WAVES 8
 #endif
 constexpr int kTraceWaves = RR_TRACE_WAVES;
+// Threads per block of the three trace kernels (k_trace_primary / _extend,
+// k_shadow_refill). 1024: two blocks fill a CU at 8 waves per SIMD, so the
+// CU's 160 KB of LDS holds two copies of the hierarchy's top (kTopNodes) next
+// to the two blocks' stacks instead of eight, and the top can be four times
+// deeper (kTopNodes below).
+#ifndef RR_TRACE_BLOCK
+#define RR_TRACE_BLOCK 1024
+#endif
+constexpr int kTraceBlock = RR_TRACE_BLOCK;
+constexpr int kTraceWavesPerBlock = kTraceBlock / 64;
 // Hierarchy of the split path: the PLOC BVH2 collapsed to the quantised BVH4
 // (measured against walking the PLOC BVH2 itself, C5 / 02 / 03 frames at 16 /
 // 64 / 64 spp: 191 -> 139, 174 -> 149, 192 -> 160 ms).
@@ -806,30 +816,37 @@ constexpr int kQStride = 32;   // words between group counters (128 B)
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 // This wave's rank with the waves ordered XCD by XCD (blocks b and b + 8 share
 // an XCD, MI355X_MICROARCH.md): consecutive chunks go to one XCD, so each
-// XCD's L2 serves one eighth of the window instead of all of it.
+// XCD's L2 serves one eighth of the window instead of all of it. kWpb: waves
+// per block of the kernel.
+template <int kWpb = kWavesPerBlock>
 RR_D int xcd_wave_rank() {
     const int G = (int)gridDim.x, bx = (int)blockIdx.x, xcd = bx & 7;
-    return __builtin_amdgcn_readfirstlane((xcd * (G >> 3) + min(xcd, G & 7) + (bx >> 3)) * kWavesPerBlock +
+    return __builtin_amdgcn_readfirstlane((xcd * (G >> 3) + min(xcd, G & 7) + (bx >> 3)) * kWpb +
                                           (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
 }
 // Top of the quantised hierarchy in LDS for the trace kernels (Q6Nodes): the
-// first kTopNodes nodes (breadth-first numbering: the three top levels of the
-// 6-wide hierarchy, 43 nodes, and most of the fourth), copied by the block at
-// launch. 128 nodes = 8 KB beside the 12 KB traversal stack (kLdsStack) keeps
-// 8 blocks of 256 threads (8 waves per SIMD) per CU. Measured on the 4-wide
-// hierarchy per frame slice against no copy (C5 at 16 spp / 02 / 03 at 64
-// spp): 105.8 -> 101.4, 110.5 -> 107.0, 118.2 -> 115.9 ms (extension and
-// shadow traversal -3 to -7 %); on the 6-wide one, 64 nodes with a 16-entry
-// stack measured the same as 128 with 12 (C5 95.0 / 94.7 ms).
+// first kTopNodes nodes (breadth-first numbering: the four top levels of the
+// 6-wide hierarchy and part of the fifth), copied by the block at launch.
+// 512 nodes = 32 KB beside the 48 KB traversal stack of a 1024-thread block
+// (kLdsStack entries per thread): two blocks, 160 KB, fill a CU's LDS at 8
+// waves per SIMD. In the oracle's walk (tools/collapse_study.py) the nodes
+// below 512 take 12.6 of 02's 18.8 node visits per camera ray (10.3 below
+// 128), 10.6 of 03's 19.9 (8.7), 9.5 of C5's 16.9 (8.6): a fifth to a quarter
+// fewer L2 / HBM node fetches than round 3's 128-node copy (eight 256-thread
+// blocks per CU, 8 KB each). That copy against none, measured on the 4-wide
+// hierarchy per frame slice (C5 at 16 spp / 02 / 03 at 64 spp): 105.8 ->
+// 101.4, 110.5 -> 107.0, 118.2 -> 115.9 ms.
 #ifndef RR_TOP_NODES
-#define RR_TOP_NODES 128
+#define RR_TOP_NODES (kTraceBlock >= 1024 ? 512 : 128)
 #endif
 constexpr int kTopNodes = RR_TOP_NODES;
+static_assert((kLdsStack * kTraceBlock * 4 + 64 * kTopNodes) * (2048 / kTraceBlock) <= 160 * 1024,
+              "trace kernels: stack + top copy of 8 waves per SIMD must fit the CU's LDS");
 RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
     lds_f4w* top = (lds_f4w*)top_shared;
     const int n = kTopNodes > 0 ? min(sa.n_qnodes, kTopNodes) : 0;
     const rr_f4v* src = reinterpret_cast<const rr_f4v*>(sa.qnodes);
-    for (int i = threadIdx.x; i < 4 * n; i += kBlock) top[i] = src[i];
+    for (int i = threadIdx.x; i < 4 * n; i += kTraceBlock) top[i] = src[i];
     __syncthreads();
     return Q6Nodes{sa.qnodes, top, n};
 }
@@ -838,14 +855,14 @@ RR_D float walk_radius(const SceneArgs& sa, const Q6Nodes& nodes) {
     if (sa.n_qnodes <= 0) return 0.0f;
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(q6_margin_radius(q6_load(nodes, 0)))));
 }
-// r: q6_margin_radius of the hierarchy (wave-uniform)
-template <typename TS, typename NodeP, typename TriP, typename MapFn, typename RayFn, typename DoneFn>
-RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, TravStack& st, TravCount& cnt,
+// r: q6_margin_radius of the hierarchy (wave-uniform). Blocks of kTraceBlock threads.
+template <typename TS, typename NodeP, typename TriP, typename Stack, typename MapFn, typename RayFn, typename DoneFn>
+RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, Stack& st, TravCount& cnt,
                        MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const int nw = gridDim.x * kWavesPerBlock;
-    const int w = xcd_wave_rank();
+    const int nw = gridDim.x * kTraceWavesPerBlock;
+    const int w = xcd_wave_rank<kTraceWavesPerBlock>();
     // position of the q-th ray of this wave's sequence
     auto gpos = [&](int q) { return ((q >> 6) * nw + w) * 64 + (q & 63); };
     int next = 0;  // wave-uniform cursor into this wave's sequence
@@ -978,15 +995,15 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
 
 // Camera paths: raygen + closest hit -> hits[p].
 template <bool kCount>
-__global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
+__global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
                                                                           float2* __restrict__ hits,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc,
                                                                           uint32_t* __restrict__ traced) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
+    __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
-    TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
+    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
@@ -1165,16 +1182,16 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
 
 // Extension rays entering bounce b: closest hit -> hits[slot].
 template <bool kCount>
-__global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
+__global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
                                                                          float2* __restrict__ hits,
                                                                          int32_t* __restrict__ spill,
                                                                          unsigned long long* __restrict__ tc) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
+    __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
-    TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
+    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
         nodes, sa.tris, sa.n_tris, qm.span, walk_radius(sa, nodes), st, cnt, [&](int m) { return qm.slot_t(m); },
@@ -1225,16 +1242,16 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
 
 // Shadow rays with lane refill: unoccluded -> radiance += contribution.
 template <bool kCount>
-__global__ __launch_bounds__(kBlock, kTraceWaves) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
+__global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
                                                                           Rad rad,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
+    __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
-    TravStack st{lds_slot(lds_stack), spill, (int)(gridDim.x * kBlock), 0};
+    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
         nodes, sa.tris, sa.n_tris, qm.span, walk_radius(sa, nodes), st, cnt, [&](int m) { return qm.slot_t(m); },
@@ -1940,20 +1957,20 @@ constexpr size_t kTileSlabMax = (size_t)16 << 30;
 // and LDS budget admits (a grid-stride loop over more blocks than fit would
 // only queue the surplus behind the first wave of blocks).
 template <typename K>
-int resident_grid(K kernel, size_t dyn_lds = 0) {
+int resident_grid(K kernel, size_t dyn_lds = 0, int block = kBlock) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, dyn_lds) != hipSuccess || per_cu <= 0)
-        per_cu = 4;
-    return device_cu_count() * std::min(per_cu, kMaxBlocksPerCu);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess || per_cu <= 0)
+        per_cu = std::max(1, 1024 / block);
+    return device_cu_count() * std::min(per_cu, kMaxBlocksPerCu * kBlock / block);
 }
 // Resident grid per (kernel, dynamic LDS bytes), cached.
 template <typename K>
-int grid_for(K kernel, size_t dyn_lds) {
+int grid_for(K kernel, size_t dyn_lds, int block = kBlock) {
     static std::map<std::pair<const void*, size_t>, int> cache;
     const auto key = std::make_pair(reinterpret_cast<const void*>(kernel), dyn_lds);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
-    return cache[key] = resident_grid(kernel, dyn_lds);
+    return cache[key] = resident_grid(kernel, dyn_lds, block);
 }
 // Scene bytes staged in LDS (stage_scene), and the cap below which the path
 // kernels take the LDS-resident variant: at most ~12 KB next to the 16 KB
@@ -2007,7 +2024,7 @@ struct TileGrid {
 };
 // Launch geometry of the split (trace / shade) path of large scenes.
 struct SplitGrids {
-    int trace_p, trace_e, shadow, shade_p, shade_e;
+    int trace_p, trace_e, shadow, shade_p, shade_e, packet;
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
@@ -2017,9 +2034,10 @@ struct SplitGrids {
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
         kts = count ? k_shadow_refill<true> : k_shadow_refill<false>;
         ktpk = count ? k_trace_primary_packet<true> : k_trace_primary_packet<false>;
-        trace_p = grid_for(ktp, 0);
-        trace_e = grid_for(kte, 0);
-        shadow = grid_for(kts, 0);
+        trace_p = grid_for(ktp, 0, kTraceBlock);
+        trace_e = grid_for(kte, 0, kTraceBlock);
+        shadow = grid_for(kts, 0, kTraceBlock);
+        packet = grid_for(ktpk, 0);
         shade_p = grid_for(k_shade_primary, 0);
         shade_e = grid_for(k_shade_extend, 0);
     }
@@ -2036,8 +2054,8 @@ int accum_grid() {
     static const int g = resident_grid(k_accumulate);
     return g;
 }
-inline int clamp_grid(long work, int resident) {
-    const long g = (work + kBlock - 1) / kBlock;
+inline int clamp_grid(long work, int resident, int block = kBlock) {
+    const long g = (work + block - 1) / block;
     return (int)std::max<long>(1, std::min<long>(g, resident));
 }
 }  // namespace
@@ -2108,8 +2126,12 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         if ((size_t)std::max(cap_p, cap_e) * kQGroups > p.cap)
             throw std::runtime_error("queue capacity exceeded (split path)");
         pr.begin(st, RR_K_PRIMARY);
-        (packets ? G.ktpk : G.ktp)<<<clamp_grid(np, G.trace_p), kBlock, 0, st>>>(
-            fc, sa, np, p.hits.ptr, p.spill.ptr, tc, tot + camera_traced_slot(base.max_bounces));
+        if (packets)
+            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc,
+                                                               tot + camera_traced_slot(base.max_bounces));
+        else
+            G.ktp<<<clamp_grid(np, G.trace_p, kTraceBlock), kTraceBlock, 0, st>>>(
+                fc, sa, np, p.hits.ptr, p.spill.ptr, tc, tot + camera_traced_slot(base.max_bounces));
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
         k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq,
@@ -2118,14 +2140,15 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         for (int b = 0; b <= base.max_bounces; ++b) {
             pr.begin(st, RR_K_SHADOW);
-            G.kts<<<clamp_grid(np, G.shadow), kBlock, 0, st>>>(sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1},
+            G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1},
                                                                Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.spill.ptr, tc);
             pr.end(st);
             if (b == base.max_bounces) break;
             const int nb = b + 1;  // bounce being traced and shaded
             const QueueIn qin{qpath(b), cap_prev, tot + 2 * b};
             pr.begin(st, RR_K_EXTEND);
-            G.kte<<<clamp_grid(np, G.trace_e), kBlock, 0, st>>>(sa, pq[nb & 1], qin, p.hits.ptr, p.spill.ptr, tc);
+            G.kte<<<clamp_grid(np, G.trace_e, kTraceBlock), kTraceBlock, 0, st>>>(sa, pq[nb & 1], qin, p.hits.ptr, p.spill.ptr,
+                                                                                tc);
             pr.end(st);
             pr.begin(st, RR_K_SHADE);
             k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},

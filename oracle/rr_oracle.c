@@ -779,10 +779,12 @@ typedef struct { float t; int slot, ref; } ckey;
 
 /* node visits / triangle tests of trace4 since the last reset (research:
  * tools/collapse_study.py) */
-static long long g_cnt_nodes, g_cnt_tris;
-void orc_walk_counts(long long* out2, int reset) {
-    out2[0] = g_cnt_nodes; out2[1] = g_cnt_tris;
-    if (reset) g_cnt_nodes = g_cnt_tris = 0;
+static long long g_cnt_nodes, g_cnt_tris, g_cnt_top[4];
+/* out: node visits, triangle tests, visits of nodes below 128 / 256 / 512 / 1024 */
+void orc_walk_counts(long long* out6, int reset) {
+    out6[0] = g_cnt_nodes; out6[1] = g_cnt_tris;
+    for (int k = 0; k < 4; ++k) out6[2 + k] = g_cnt_top[k];
+    if (reset) { g_cnt_nodes = g_cnt_tris = 0; for (int k = 0; k < 4; ++k) g_cnt_top[k] = 0; }
 }
 
 /* traversal-stack pushes dropped for want of room (ORC_MAXDEPTH), since the
@@ -822,9 +824,10 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
     const float oo[3] = {o.x, o.y, o.z};
     int stack[ORC_MAXDEPTH];
     int sp = 0, node = 0;
-    long long cn = 0, ct = 0;
+    long long cn = 0, ct = 0, ctop[4] = {0, 0, 0, 0};
     for (;;) {
         ++cn;
+        for (int k = 0; k < 4; ++k) ctop[k] += node < (128 << k);
         const uint32_t* nd = B->q4 + 16 * (size_t)node;
         const uint32_t inner = nd[3] >> 24;
         const float tcur = h->t;
@@ -893,6 +896,10 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
         node = k[best].ref;
     }
 done:
+    for (int k = 0; k < 4; ++k) {
+#pragma omp atomic
+        g_cnt_top[k] += ctop[k];
+    }
 #pragma omp atomic
     g_cnt_nodes += cn;
 #pragma omp atomic

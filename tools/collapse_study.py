@@ -44,7 +44,7 @@ def world_tris(path, scene_obj, frame):
 def walk(tris, rays, mode):
     L = O.lib()
     L.orc_set_collapse(mode)
-    out = np.zeros(2, np.int64)
+    out = np.zeros(6, np.int64)
     L.orc_walk_counts(out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), 1)
     t0 = time.time()
     h, p, occ = O.trace(tris, rays, width=4)
@@ -97,7 +97,8 @@ def main():
             hh, pp, oo, cnt, dt = walk(tris, rays, mode)
             res[mode] = (pp, oo, cnt)
             print(f"  {name:7s} collapse {mode}: {cnt[0] / len(rays):7.2f} node visits, {cnt[1] / len(rays):6.2f} "
-                  f"triangle tests per ray ({dt:.1f} s)")
+                  f"triangle tests per ray; of the visits to nodes below 128/256/512/1024: "
+                  f"{', '.join(f'{c / len(rays):.2f}' for c in cnt[2:6])} ({dt:.1f} s)")
         assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1]), "results differ"
     s.close()
 
