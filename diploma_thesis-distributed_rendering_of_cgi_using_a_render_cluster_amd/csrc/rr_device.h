@@ -130,9 +130,10 @@ constexpr int kMaxLights = 64;
 constexpr int kBlock = 256;         // threads per block for all path kernels
 // Traversal stack per lane: kLdsStack entries in LDS, the rest (up to the
 // oracle's ORC_MAXDEPTH = 80 in all) in a per-thread HBM spill area. 12 LDS
-// entries (12 KB per 256-thread block) leave room for the split-path trace
-// kernels' top-of-tree node copy (wavefront.hip stage_top) at 8 blocks per CU;
-// 16 entries with half the node copy measured 1-1.5 % slower on C5.
+// entries (48 KB per 1024-thread trace block) leave room for the split-path
+// trace kernels' top-of-tree node copy (wavefront.hip stage_top, 32 KB) at two
+// blocks per CU; 16 entries with half the node copy measured 1-1.5 % slower on
+// C5 (round 3, 256-thread blocks).
 #ifndef RR_LDS_STACK
 #define RR_LDS_STACK 12
 #endif
@@ -692,6 +693,8 @@ struct TravState {
         em = slab_margin(o, invd, r);
         node = 0;
     }
+    template <typename NodeP>
+    RR_D void prime(NodeP) {}
     // One node visit; true when the ray is finished (any-hit: on the first hit).
     template <typename NodeP, typename TriP, typename Stack>
     RR_D bool step(NodeP nodes, TriP tris, Stack& st, TravCount& cnt) {
@@ -892,6 +895,12 @@ RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
     }
     return q6_load(n.g, i);
 }
+// Whether node i is fetched from global memory, and one dword of it (the
+// prefetch touch of TravStateQ6::step).
+RR_D bool q6_global(const QNode6* __restrict__, int) { return true; }
+RR_D bool q6_global(const Q6Nodes& n, int i) { return i >= n.n_top; }
+RR_D float q6_touch(const QNode6* __restrict__ nodes, int i) { return nodes[i].org.x; }
+RR_D float q6_touch(const Q6Nodes& n, int i) { return n.g[i].org.x; }
 
 // Resumable traversal of the quantised 6-wide hierarchy (same contract as
 // TravState), box tests by q6_box_best. Leaf children whose boxes pass are
@@ -920,6 +929,56 @@ struct TravStateQ6 {
         mrg = ray_margin(o, r);
         node = 0;
     }
+#if RR_Q6_PREFETCH
+    template <typename NodeSrc>
+    RR_D void prime(const NodeSrc&) {}
+    // step with the next node chosen before this node's leaf tests and, when
+    // there are leaf tests and the next node lies outside the LDS top copy, one
+    // dword of it loaded ahead of the triangles (its line comes into L2 / L1
+    // while the triangle fetches are in flight; the next step's load then hits
+    // there). The visited nodes and tested triangles are the same: the next node
+    // is chosen from the box tests, which the leaf tests after them never change.
+    template <typename NodeSrc, typename TriP, typename Stack>
+    RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
+        if (kCount) ++cnt.nodes;
+        const QNode6 nd = q6_load(nodes, node);
+        const uint32_t imask = q6_inner(nd);
+        int best;
+        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, mrg, tmin, h.t, imask, best);
+        uint32_t leaves = hm & ~imask;
+        const uint32_t inner = hm & imask;
+        const int leaf0 = (int)nd.a.y;
+        bool fin = false;
+        if (!inner) {
+            if (st.sp == 0) fin = true;
+            else node = st.pop();
+        } else {
+            const uint32_t rest = inner & ~(1u << best);
+            const int base = (int)nd.a.x;
+#pragma unroll
+            for (int c = kQWidth - 1; c >= 0; --c)
+                if ((rest >> c) & 1u) st.push(base + __builtin_popcount(imask & ((1u << c) - 1u)));
+            node = base + __builtin_popcount(imask & ((1u << best) - 1u));
+        }
+        if (leaves) {
+            float touch = 0.0f;
+            if (!fin && q6_global(nodes, node)) touch = q6_touch(nodes, node);
+            do {
+                const int c = __builtin_ctz(leaves);
+                leaves &= leaves - 1;
+                const int ti = leaf0 + c - __builtin_popcount(imask & ((1u << c) - 1u));
+                if (kCount) ++cnt.tris;
+                leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
+                if (kAnyHit && h.idx >= 0) break;
+            } while (leaves);
+            asm volatile("" ::"v"(touch));  // the touch load stays (its value is never used)
+            if (kAnyHit && h.idx >= 0) return true;
+        }
+        return fin;
+    }
+#else
+    template <typename NodeSrc>
+    RR_D void prime(const NodeSrc&) {}
     template <typename NodeSrc, typename TriP, typename Stack>
     RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
         if (kCount) ++cnt.nodes;
@@ -955,6 +1014,7 @@ struct TravStateQ6 {
         node = base + __builtin_popcount(imask & ((1u << best) - 1u));
         return false;
     }
+#endif
 };
 
 // Closest hit (or any hit) over the LBVH, run to completion.

@@ -880,6 +880,7 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, S
                 ray_of(ks, o, d, tmin, tmax);
                 ts.start(o, d, tmin, tmax, r);
                 st.sp = 0;
+                if (n_tris > 0) ts.prime(nodes);
                 if (n_tris > 0) {
                     j = k;
                     js = ks;

@@ -1,7 +1,6 @@
 #!/bin/bash
 # Round-4 A/B call on the GPU box: trace-block size / LDS top depth / box
-# margin variants on the split-path scenes, uniform-kz camera test on the
-# k_tiles scenes. Variants: tools/ab_variants.sh builds (build/ab_<name>).
+# margin variants on the split-path scenes. Variants: tools/ab_variants.sh
+# builds (build/ab_<name>).
 mkdir -p gpurun_out
-timeout -k 10 800 python tools/ab_run.py --rounds 2 main b256 t128 pernode r3 -- scenes/02_physics-standin.rrscene:90:64 scenes/03_physics-2-standin.rrscene:300:64 scenes/c5_synthetic-10m.rrscene:150:16 > gpurun_out/ab4.txt 2>&1 || exit $?
-timeout -k 10 300 python tools/ab_run.py --rounds 3 --frames 40 main nokz r3 -- scenes/04_very-simple-standin.rrscene:5:128 scenes/01_simple-animation.rrscene:20:128 > gpurun_out/ab5.txt 2>&1
+timeout -k 10 1050 python tools/ab_run.py --rounds 2 main pf b256 t128 s8t768 pernode r3 -- scenes/02_physics-standin.rrscene:90:64 scenes/03_physics-2-standin.rrscene:300:64 scenes/c5_synthetic-10m.rrscene:150:16 > gpurun_out/ab4.txt 2>&1
