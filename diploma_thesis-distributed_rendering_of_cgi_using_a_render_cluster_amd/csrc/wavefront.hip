@@ -994,6 +994,136 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
     }
 }
 
+// Ray order of the secondary-ray queues (RR_RAY_SORT, split path): the
+// extension and shadow rays of a bounce are traced in the order of a key made
+// of the cell of their origin (kSortCellBits per axis over the hierarchy's root
+// box, Morton order) and the octant of their direction, so that the rays in
+// flight together start in one region of the scene and head the same way and
+// share the nodes they visit. One counting pass (k_sort_count: the key of each
+// queue position into sort_key, a per-block histogram in LDS added into the
+// global one), one scan of the kSortBuckets counts (k_sort_scan), one scatter
+// of the queue slots to their bucket's range (k_sort_place: ranks from LDS
+// atomics, so the order inside a bucket is arbitrary). The trace kernels then
+// take positions from that order (queue gaps left out). Scheduling only: each
+// ray's hit is written at its own queue slot, so no result changes.
+#ifndef RR_SORT_CELL_BITS
+#define RR_SORT_CELL_BITS 3
+#endif
+constexpr int kSortCellBits = RR_SORT_CELL_BITS;
+constexpr int kSortBuckets = 8 << (3 * kSortCellBits);  // octant x cells
+constexpr int kRaySortItems = 64;                          // queue positions per thread of the sort kernels
+constexpr int kRaySortTile = kRaySortItems * kBlock;
+constexpr uint32_t kSortNone = 0xFFFFFFFFu;
+struct SortBox {
+    float3 lo, sc;  // cell = (p - lo) * sc, sc = 2^kSortCellBits / extent
+};
+RR_D SortBox sort_box(const SceneArgs& sa) {
+    SortBox b;
+    b.lo = b.sc = mk3(0.0f, 0.0f, 0.0f);
+    if (sa.n_qnodes <= 0) return b;
+    const float4 org = sa.qnodes[0].org;  // wave-uniform: scalar loads
+    const uint32_t eb = (uint32_t)f2i(org.w);
+    const float cells = (float)(1 << kSortCellBits);
+    b.lo = mk3(org.x, org.y, org.z);
+    b.sc = mk3(cells / ldexpf(256.0f, (int)(eb & 255u) - 128), cells / ldexpf(256.0f, (int)((eb >> 8) & 255u) - 128),
+               cells / ldexpf(256.0f, (int)((eb >> 16) & 255u) - 128));
+    return b;
+}
+RR_D uint32_t sort_spread(uint32_t v) {  // kSortCellBits <= 5 bits -> every third bit
+    uint32_t r = 0;
+    for (int k = 0; k < kSortCellBits; ++k) r |= ((v >> k) & 1u) << (3 * k);
+    return r;
+}
+RR_D uint32_t ray_sort_key(const SortBox& b, float4 o, float4 d) {
+    const float mx = (float)((1 << kSortCellBits) - 1);
+    const uint32_t cx = (uint32_t)fminf(fmaxf((o.x - b.lo.x) * b.sc.x, 0.0f), mx);
+    const uint32_t cy = (uint32_t)fminf(fmaxf((o.y - b.lo.y) * b.sc.y, 0.0f), mx);
+    const uint32_t cz = (uint32_t)fminf(fmaxf((o.z - b.lo.z) * b.sc.z, 0.0f), mx);
+    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    return (oct << (3 * kSortCellBits)) | (sort_spread(cx) << 2) | (sort_spread(cy) << 1) | sort_spread(cz);
+}
+// The key of every queue position of this block's tile (kSortNone for a gap)
+// and the bucket counts. hist: kSortBuckets words, zeroed before the launch.
+__global__ __launch_bounds__(kBlock) void k_sort_count(SceneArgs sa, QueueIn qi, const float4* __restrict__ ro,
+                                                       const float4* __restrict__ rd, uint32_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kSortBuckets];
+    for (int i = threadIdx.x; i < kSortBuckets; i += kBlock) h[i] = 0;
+    QueueMap qm;
+    qm.init(qi);
+    const SortBox box = sort_box(sa);
+    __syncthreads();
+    const int base = blockIdx.x * kRaySortTile;
+    if (base < qm.span) {  // block-uniform
+        for (int k = 0; k < kRaySortItems; ++k) {
+            const int m = base + k * kBlock + (int)threadIdx.x;
+            const uint32_t i = qm.slot_t(m < qm.span ? m : qm.span - 1);  // all lanes (shuffles)
+            if (m >= qm.span) continue;
+            uint32_t key = kSortNone;
+            if (i != kNoSlot) {
+                key = ray_sort_key(box, ro[i], rd[i]);
+                atomicAdd(&h[key], 1u);
+            }
+            keys[m] = key;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSortBuckets; i += kBlock)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+// Exclusive scan of the bucket counts in place (one block of kBlock threads).
+__global__ __launch_bounds__(kBlock) void k_sort_scan(uint32_t* __restrict__ hist) {
+    constexpr int kPer = kSortBuckets / kBlock;
+    __shared__ uint32_t wsum[kBlock / 64];
+    uint32_t v[kPer], t = 0;
+    for (int k = 0; k < kPer; ++k) {
+        v[k] = hist[threadIdx.x * kPer + k];
+        t += v[k];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = t;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(inc, off);
+        if (lane >= off) inc += o;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - t;
+    for (int k = 0; k < w; ++k) run += wsum[k];
+    for (int k = 0; k < kPer; ++k) {
+        hist[threadIdx.x * kPer + k] = run;
+        run += v[k];
+    }
+}
+// Each valid queue position's slot to order[start of its bucket + rank].
+// hist: the scanned bucket starts, advanced as blocks take their ranges.
+__global__ __launch_bounds__(kBlock) void k_sort_place(QueueIn qi, const uint32_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ hist, uint32_t* __restrict__ order) {
+    __shared__ uint32_t h[kSortBuckets];
+    for (int i = threadIdx.x; i < kSortBuckets; i += kBlock) h[i] = 0;
+    QueueMap qm;
+    qm.init(qi);
+    __syncthreads();
+    const int base = blockIdx.x * kRaySortTile;
+    if (base >= qm.span) return;  // block-uniform
+    for (int k = 0; k < kRaySortItems; ++k) {
+        const int m = base + k * kBlock + (int)threadIdx.x;
+        if (m < qm.span && keys[m] != kSortNone) atomicAdd(&h[keys[m]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSortBuckets; i += kBlock)
+        if (h[i]) h[i] = atomicAdd(&hist[i], h[i]);  // this block's range of bucket i
+    __syncthreads();
+    for (int k = 0; k < kRaySortItems; ++k) {
+        const int m = base + k * kBlock + (int)threadIdx.x;
+        const uint32_t i = qm.slot_t(m < qm.span ? m : qm.span - 1);  // all lanes (shuffles)
+        if (m >= qm.span) continue;
+        const uint32_t key = keys[m];
+        if (key == kSortNone) continue;
+        order[atomicAdd(&h[key], 1u)] = i;
+    }
+}
+
 // Camera paths: raygen + closest hit -> hits[p].
 template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
@@ -1182,8 +1312,10 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
 }
 
 // Extension rays entering bounce b: closest hit -> hits[slot].
+// order: the queue slots in ray-sort order (k_sort_place), or null.
 template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
+                                                                         const uint32_t* __restrict__ order,
                                                                          float2* __restrict__ hits,
                                                                          int32_t* __restrict__ spill,
                                                                          unsigned long long* __restrict__ tc) {
@@ -1195,7 +1327,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, walk_radius(sa, nodes), st, cnt, [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, order ? qm.total : qm.span, walk_radius(sa, nodes), st, cnt,
+        [&](int m) { return order ? order[m] : qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
@@ -1244,7 +1377,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
 // Shadow rays with lane refill: unoccluded -> radiance += contribution.
 template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
-                                                                          Rad rad,
+                                                                          const uint32_t* __restrict__ order, Rad rad,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
@@ -1255,7 +1388,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, walk_radius(sa, nodes), st, cnt, [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, order ? qm.total : qm.span, walk_radius(sa, nodes), st, cnt,
+        [&](int m) { return order ? order[m] : qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
@@ -2027,8 +2161,8 @@ struct TileGrid {
 struct SplitGrids {
     int trace_p, trace_e, shadow, shade_p, shade_e, packet;
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
-    void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
-    void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
+    void (*kte)(SceneArgs, PathQueue, QueueIn, const uint32_t*, float2*, int32_t*, unsigned long long*);
+    void (*kts)(SceneArgs, ShadowQueue, QueueIn, const uint32_t*, Rad, int32_t*, unsigned long long*);
     void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
@@ -2083,6 +2217,7 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
+    sort_key.release(); sort_order.release(); sort_hist.release();
     counters.release(); tile_ctrs.release(); tile_cost.release(); tile_order.release(); spill.release(); tile_slab.release(); film_part.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     mat_lut.release();
@@ -2093,6 +2228,26 @@ void DevPaths::release() {
 }
 
 namespace {
+#ifndef RR_RAY_SORT
+#define RR_RAY_SORT 0
+#endif
+// The secondary-ray order of one queue (k_sort_count / k_sort_scan /
+// k_sort_place over its capacity, kRaySortTile positions per block; blocks past
+// the queue's span return at once), or null without RR_RAY_SORT.
+const uint32_t* sort_rays(DevPaths& p, const SceneArgs& sa, const QueueIn& q, const float4* o, const float4* d,
+                          hipStream_t st) {
+    if (!RR_RAY_SORT) return nullptr;
+    const size_t n = (size_t)q.cap * kQGroups;
+    p.sort_key.ensure(n);
+    p.sort_order.ensure(n);
+    p.sort_hist.ensure(kSortBuckets);
+    const int blocks = (int)((n + kRaySortTile - 1) / kRaySortTile);
+    RR_HIP(hipMemsetAsync(p.sort_hist.ptr, 0, kSortBuckets * sizeof(uint32_t), st));
+    k_sort_count<<<blocks, kBlock, 0, st>>>(sa, q, o, d, p.sort_key.ptr, p.sort_hist.ptr);
+    k_sort_scan<<<1, kBlock, 0, st>>>(p.sort_hist.ptr);
+    k_sort_place<<<blocks, kBlock, 0, st>>>(q, p.sort_key.ptr, p.sort_hist.ptr, p.sort_order.ptr);
+    return p.sort_order.ptr;
+}
 // Large scenes: per chunk trace_primary -> shade_primary -> for each bounce b:
 // shadow(b), trace_extend(b+1), shade_extend(b+1) -> accumulate. Radiance
 // additions per path happen in the same order as the fused kernels'.
@@ -2141,15 +2296,18 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         for (int b = 0; b <= base.max_bounces; ++b) {
             pr.begin(st, RR_K_SHADOW);
-            G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1},
-                                                               Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.spill.ptr, tc);
+            const QueueIn qs{qshadow(b), cap_prev, tot + 2 * b + 1};
+            const uint32_t* so = sort_rays(p, sa, qs, sq.o, sq.d, st);
+            G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(
+                sa, sq, qs, so, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.spill.ptr, tc);
             pr.end(st);
             if (b == base.max_bounces) break;
             const int nb = b + 1;  // bounce being traced and shaded
             const QueueIn qin{qpath(b), cap_prev, tot + 2 * b};
             pr.begin(st, RR_K_EXTEND);
-            G.kte<<<clamp_grid(np, G.trace_e, kTraceBlock), kTraceBlock, 0, st>>>(sa, pq[nb & 1], qin, p.hits.ptr, p.spill.ptr,
-                                                                                tc);
+            const uint32_t* eo = sort_rays(p, sa, qin, pq[nb & 1].o, pq[nb & 1].d, st);
+            G.kte<<<clamp_grid(np, G.trace_e, kTraceBlock), kTraceBlock, 0, st>>>(sa, pq[nb & 1], qin, eo, p.hits.ptr,
+                                                                                p.spill.ptr, tc);
             pr.end(st);
             pr.begin(st, RR_K_SHADE);
             k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},
