@@ -140,7 +140,6 @@ struct DevPaths {
     DevBuf<float4> sh_o, sh_d, sh_c;           // segmented shadow queue
     DevBuf<float2> hits;                       // split path: (t, leaf index) per queue entry
     DevBuf<uint32_t> qctr;                     // split path: grouped queue append counters
-    DevBuf<uint32_t> sort_key, sort_order, sort_hist;  // split path: secondary-ray order (RR_RAY_SORT)
     DevBuf<int32_t> counters;  // per chunk, per bounce b: {paths entering b+1, shadow rays of b}
     DevBuf<int32_t> spill;     // traversal stack spill
     DevBuf<float4> film;

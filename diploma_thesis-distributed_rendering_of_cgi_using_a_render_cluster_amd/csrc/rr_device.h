@@ -693,8 +693,6 @@ struct TravState {
         em = slab_margin(o, invd, r);
         node = 0;
     }
-    template <typename NodeP>
-    RR_D void prime(NodeP) {}
     // One node visit; true when the ray is finished (any-hit: on the first hit).
     template <typename NodeP, typename TriP, typename Stack>
     RR_D bool step(NodeP nodes, TriP tris, Stack& st, TravCount& cnt) {
@@ -738,46 +736,34 @@ struct TravState {
     }
 };
 
-// Radius term of the quantised walk's margins (slab_margin): twice the
-// largest |coordinate| of the root's grid (org .. org + 255 * 2^e per axis),
-// which bounds |org| + 255 * 2^e of every node: the plane distances of the
-// walk are within 8 ulp of |org - o| + 6 ulp of 255 * 2^e (times |iq|) and the
-// projected vertices within 8 ulp of |v - o|, under the margin's 32 ulp of
-// |o|_inf + this.
-RR_HD float q6_margin_radius(const QNode6& root) {
-    const uint32_t eb = (uint32_t)f2i(root.org.w);
-    float r = 0.0f;
-    const float org[3] = {root.org.x, root.org.y, root.org.z};
-    for (int a = 0; a < 3; ++a) {
-        const float hi = org[a] + ldexpf(255.0f, (int)((eb >> (8 * a)) & 255u) - 128);
-        r = fmaxf(r, fmaxf(fabsf(org[a]), fabsf(hi)));
-    }
-    return 2.0f * r;
-}
-
-// Margin distance of one ray of the quantised walk: kBoxMargin (|o|_inf + r),
-// r = q6_margin_radius; in t on axis a it is this times |iq_a| (slab_margin's).
-RR_HD float ray_margin(float3 o, float r) { return (fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + r) * kBoxMargin; }
-
 // Per-node terms of the quantised box tests for one ray (iq: rcp3 of the
-// direction, m: ray_margin). Per axis s = iq * 2^e (exact); a plane at grid
-// coordinate q lies at t = fma(q, s, (org - o) * iq), the near planes' offsets
-// less the axis' margin m |iq|, the far planes' more, folded into one fma
-// each, so a box holding a triangle woop_test accepts is never rejected by
-// rounding.
+// direction). Per axis s = iq * 2^e (exact); a plane at grid coordinate q lies
+// at t = fma(q, s, (org - o) * iq), the near planes' offsets less the axis'
+// margin m |iq|, the far planes' more, folded into one fma each, so a box
+// holding a triangle woop_test accepts is never rejected by rounding. The
+// margin distance m = kBoxMargin (the largest |org - o| + 255 * 2^e over the
+// axes): the node's own distance from the origin plus its extent bound every
+// plane distance of its children and every vertex below it, so the rounding
+// of both tests stays under it. (A per-ray bound, kBoxMargin (|o|_inf + twice
+// the root grid's largest |coordinate|), saved 8 VALU per node visit but was
+// loose deep in the tree: 3.7 % more triangle tests on C5 bounce rays, and
+// measured 1 / 1 / 3.4 % slower on 02 / 03 / C5 frame slices.)
 struct Q6Planes {
     float sx, sy, sz;     // iq * 2^e
     float nx, ny, nz;     // (org - o) iq - margin (near planes)
     float fx, fy, fz;     // (org - o) iq + margin (far planes)
 };
-RR_D Q6Planes q6_planes(const QNode6& n, float3 o, float3 iq, float m) {
-    const float3 em = mk3(m * fabsf(iq.x), m * fabsf(iq.y), m * fabsf(iq.z));
+RR_D Q6Planes q6_planes(const QNode6& n, float3 o, float3 iq) {
     const uint32_t eb = (uint32_t)f2i(n.org.w);
-    Q6Planes p;
-    p.sx = ldexpf(iq.x, (int)(eb & 255u) - 128);
-    p.sy = ldexpf(iq.y, (int)((eb >> 8) & 255u) - 128);
-    p.sz = ldexpf(iq.z, (int)((eb >> 16) & 255u) - 128);
+    const int ex = (int)(eb & 255u) - 128, ey = (int)((eb >> 8) & 255u) - 128, ez = (int)((eb >> 16) & 255u) - 128;
     const float dx = n.org.x - o.x, dy = n.org.y - o.y, dz = n.org.z - o.z;
+    const float m = fmaxf(fmaxf(fabsf(dx) + ldexpf(255.0f, ex), fabsf(dy) + ldexpf(255.0f, ey)),
+                          fabsf(dz) + ldexpf(255.0f, ez)) * kBoxMargin;
+    const float3 em = mk3(m * fabsf(iq.x), m * fabsf(iq.y), m * fabsf(iq.z));
+    Q6Planes p;
+    p.sx = ldexpf(iq.x, ex);
+    p.sy = ldexpf(iq.y, ey);
+    p.sz = ldexpf(iq.z, ez);
     p.nx = fmaf(dx, iq.x, -em.x);
     p.ny = fmaf(dy, iq.y, -em.y);
     p.nz = fmaf(dz, iq.z, -em.z);
@@ -793,9 +779,8 @@ RR_D Q6Planes q6_planes(const QNode6& n, float3 o, float3 iq, float m) {
 // fmaxf / fminf drop their operands); tn[c] = the entry distance. The near
 // plane is lo for iq >= 0, else hi (iq is never 0 or inf, so no NaN and no
 // min/max per axis). oracle/rr_oracle.c trace4() restates it.
-RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float m, float tmin, float tcur,
-                          float tn[kQWidth]) {
-    const Q6Planes pl = q6_planes(n, o, iq, m);
+RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, float tn[kQWidth]) {
+    const Q6Planes pl = q6_planes(n, o, iq);
     const float sx = pl.sx, sy = pl.sy, sz = pl.sz;
     const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
     // children 0..3: one byte each of the near / far words per axis
@@ -833,9 +818,9 @@ RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float m, float t
 // slot order drops the distance compares and their registers (shadow rays
 // -10 % on C5, VGPR spill slots 10 -> 2).
 template <bool kNearest = true>
-RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float m, float tmin, float tcur, uint32_t imask,
+RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, uint32_t imask,
                           int& best) {
-    const Q6Planes pl = q6_planes(n, o, iq, m);
+    const Q6Planes pl = q6_planes(n, o, iq);
     const float sx = pl.sx, sy = pl.sy, sz = pl.sz;
     const uint32_t used = n.c.w;
     const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
@@ -895,12 +880,6 @@ RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
     }
     return q6_load(n.g, i);
 }
-// Whether node i is fetched from global memory, and one dword of it (the
-// prefetch touch of TravStateQ6::step).
-RR_D bool q6_global(const QNode6* __restrict__, int) { return true; }
-RR_D bool q6_global(const Q6Nodes& n, int i) { return i >= n.n_top; }
-RR_D float q6_touch(const QNode6* __restrict__ nodes, int i) { return nodes[i].org.x; }
-RR_D float q6_touch(const Q6Nodes& n, int i) { return n.g[i].org.x; }
 
 // Resumable traversal of the quantised 6-wide hierarchy (same contract as
 // TravState), box tests by q6_box_best. Leaf children whose boxes pass are
@@ -911,13 +890,12 @@ RR_D float q6_touch(const Q6Nodes& n, int i) { return n.g[i].org.x; }
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6 {
     float3 o, iq;
-    float mrg;  // ray_margin
     Shear sh;
     float tmin;
     Hit h;
     int node;
-    // r: q6_margin_radius of the hierarchy's root (the box margins)
-    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_, float r) {
+    // (the last argument, TravState's scene radius, is unused: the margins are per node)
+    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_, float = 0.0f) {
         o = o_;
         sh = make_shear(d_);
         tmin = tmin_;
@@ -926,59 +904,8 @@ struct TravStateQ6 {
         h.idx = -1;
         h.orig = -1;
         iq = rcp3(d_);
-        mrg = ray_margin(o, r);
         node = 0;
     }
-#if RR_Q6_PREFETCH
-    template <typename NodeSrc>
-    RR_D void prime(const NodeSrc&) {}
-    // step with the next node chosen before this node's leaf tests and, when
-    // there are leaf tests and the next node lies outside the LDS top copy, one
-    // dword of it loaded ahead of the triangles (its line comes into L2 / L1
-    // while the triangle fetches are in flight; the next step's load then hits
-    // there). The visited nodes and tested triangles are the same: the next node
-    // is chosen from the box tests, which the leaf tests after them never change.
-    template <typename NodeSrc, typename TriP, typename Stack>
-    RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
-        if (kCount) ++cnt.nodes;
-        const QNode6 nd = q6_load(nodes, node);
-        const uint32_t imask = q6_inner(nd);
-        int best;
-        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, mrg, tmin, h.t, imask, best);
-        uint32_t leaves = hm & ~imask;
-        const uint32_t inner = hm & imask;
-        const int leaf0 = (int)nd.a.y;
-        bool fin = false;
-        if (!inner) {
-            if (st.sp == 0) fin = true;
-            else node = st.pop();
-        } else {
-            const uint32_t rest = inner & ~(1u << best);
-            const int base = (int)nd.a.x;
-#pragma unroll
-            for (int c = kQWidth - 1; c >= 0; --c)
-                if ((rest >> c) & 1u) st.push(base + __builtin_popcount(imask & ((1u << c) - 1u)));
-            node = base + __builtin_popcount(imask & ((1u << best) - 1u));
-        }
-        if (leaves) {
-            float touch = 0.0f;
-            if (!fin && q6_global(nodes, node)) touch = q6_touch(nodes, node);
-            do {
-                const int c = __builtin_ctz(leaves);
-                leaves &= leaves - 1;
-                const int ti = leaf0 + c - __builtin_popcount(imask & ((1u << c) - 1u));
-                if (kCount) ++cnt.tris;
-                leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
-                if (kAnyHit && h.idx >= 0) break;
-            } while (leaves);
-            asm volatile("" ::"v"(touch));  // the touch load stays (its value is never used)
-            if (kAnyHit && h.idx >= 0) return true;
-        }
-        return fin;
-    }
-#else
-    template <typename NodeSrc>
-    RR_D void prime(const NodeSrc&) {}
     template <typename NodeSrc, typename TriP, typename Stack>
     RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
         if (kCount) ++cnt.nodes;
@@ -986,7 +913,7 @@ struct TravStateQ6 {
         const QNode6 nd = q6_load(nodes, node);
         const uint32_t imask = q6_inner(nd);
         int best;
-        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, mrg, tmin, tcur, imask, best);
+        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, tmin, tcur, imask, best);
         uint32_t leaves = hm & ~imask;
         const uint32_t inner = hm & imask;
         // passing leaves in slot order; the loop runs as often as the lane with
@@ -1014,7 +941,6 @@ struct TravStateQ6 {
         node = base + __builtin_popcount(imask & ((1u << best) - 1u));
         return false;
     }
-#endif
 };
 
 // Closest hit (or any hit) over the LBVH, run to completion.
@@ -1223,17 +1149,6 @@ RR_HD bool bsdf_sample_onb(const Mat& m, FloatP lut, const BsdfView& vw, float3 
     float x, y;  // the disk sample both lobes start from
     concentric_disk(u1, u2, x, y);
     glossy = ul < ps;
-#if RR_AB_UNIFIED_LOBE
-    {
-        const bool g = glossy;
-        const float3 wl = g ? mk3(dot3(wo, T), dot3(wo, B), cosV) : mk3(0.0f, 0.0f, 1.0f);
-        const float3 l = sample_vndf(wl, g ? m.alpha : 1.0f, x, y);
-        const float3 W = frame3(T, B, N, l.x, l.y, l.z);
-        const float k = 2.0f * dot3(wo, W);
-        const float3 r = mk3(fmaf(W.x, k, -wo.x), fmaf(W.y, k, -wo.y), fmaf(W.z, k, -wo.z));
-        wi = g ? r : W;
-    }
-#else
     // the lobe's direction in the local frame: the GGX half vector (glossy)
     // or the cosine-weighted point (diffuse); one frame3 for both, so a wave
     // whose lanes picked both lobes runs it once
@@ -1252,7 +1167,6 @@ RR_HD bool bsdf_sample_onb(const Mat& m, FloatP lut, const BsdfView& vw, float3 
     } else {
         wi = W;
     }
-#endif
     f = bsdf_eval_v(m, lut, vw, N, wo, wi, pdf);
     return pdf > 0.0f;
 }

@@ -784,12 +784,15 @@ constexpr int kRefillBelow = RR_REFILL_BELOW;
 #endif
 constexpr int kTraceWaves = RR_TRACE_WAVES;
 // Threads per block of the three trace kernels (k_trace_primary / _extend,
-// k_shadow_refill). 1024: two blocks fill a CU at 8 waves per SIMD, so the
+// k_shadow_refill). With 1024 two blocks fill a CU at 8 waves per SIMD, so the
 // CU's 160 KB of LDS holds two copies of the hierarchy's top (kTopNodes) next
-// to the two blocks' stacks instead of eight, and the top can be four times
-// deeper (kTopNodes below).
+// to the blocks' stacks instead of eight, and the top can be four times deeper
+// (512 nodes); measured against 256-thread blocks with 128 top nodes (per
+// frame slice, 02 / 03 at 64 spp, C5 at 16 spp): 115.4 / 128.4 / 103.0 against
+// 115.5 / 129.1 / 103.2 ms, and 1024 with 128 nodes the same — the nodes
+// between 128 and 512 come from L2 about as fast. 256 stays.
 #ifndef RR_TRACE_BLOCK
-#define RR_TRACE_BLOCK 1024
+#define RR_TRACE_BLOCK 256
 #endif
 constexpr int kTraceBlock = RR_TRACE_BLOCK;
 constexpr int kTraceWavesPerBlock = kTraceBlock / 64;
@@ -825,17 +828,15 @@ RR_D int xcd_wave_rank() {
                                           (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
 }
 // Top of the quantised hierarchy in LDS for the trace kernels (Q6Nodes): the
-// first kTopNodes nodes (breadth-first numbering: the four top levels of the
-// 6-wide hierarchy and part of the fifth), copied by the block at launch.
-// 512 nodes = 32 KB beside the 48 KB traversal stack of a 1024-thread block
-// (kLdsStack entries per thread): two blocks, 160 KB, fill a CU's LDS at 8
-// waves per SIMD. In the oracle's walk (tools/collapse_study.py) the nodes
-// below 512 take 12.6 of 02's 18.8 node visits per camera ray (10.3 below
-// 128), 10.6 of 03's 19.9 (8.7), 9.5 of C5's 16.9 (8.6): a fifth to a quarter
-// fewer L2 / HBM node fetches than round 3's 128-node copy (eight 256-thread
-// blocks per CU, 8 KB each). That copy against none, measured on the 4-wide
-// hierarchy per frame slice (C5 at 16 spp / 02 / 03 at 64 spp): 105.8 ->
-// 101.4, 110.5 -> 107.0, 118.2 -> 115.9 ms.
+// first kTopNodes nodes (breadth-first numbering: the three top levels of the
+// 6-wide hierarchy and most of the fourth), copied by the block at launch.
+// 128 nodes = 8 KB beside the 12 KB traversal stack of a 256-thread block keep
+// 8 blocks (8 waves per SIMD) per CU. In the oracle's walk
+// (tools/collapse_study.py) the nodes below 128 take 10.3 of 02's 18.8 node
+// visits per camera ray, 8.7 of 03's 19.9, 8.6 of C5's 16.9 (below 512: 12.6,
+// 10.6, 9.5 — which measured no faster, RR_TRACE_BLOCK above). The copy
+// against none, measured on the 4-wide hierarchy per frame slice (C5 at 16 spp
+// / 02 / 03 at 64 spp): 105.8 -> 101.4, 110.5 -> 107.0, 118.2 -> 115.9 ms.
 #ifndef RR_TOP_NODES
 #define RR_TOP_NODES (kTraceBlock >= 1024 ? 512 : 128)
 #endif
@@ -850,12 +851,8 @@ RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
     __syncthreads();
     return Q6Nodes{sa.qnodes, top, n};
 }
-// The hierarchy's margin radius (q6_margin_radius of the root), wave-uniform.
-RR_D float walk_radius(const SceneArgs& sa, const Q6Nodes& nodes) {
-    if (sa.n_qnodes <= 0) return 0.0f;
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(q6_margin_radius(q6_load(nodes, 0)))));
-}
-// r: q6_margin_radius of the hierarchy (wave-uniform). Blocks of kTraceBlock threads.
+// r: TravState's scene radius (unused by TravStateQ6, whose margins are per
+// node). Blocks of kTraceBlock threads.
 template <typename TS, typename NodeP, typename TriP, typename Stack, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, Stack& st, TravCount& cnt,
                        MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
@@ -880,7 +877,6 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, S
                 ray_of(ks, o, d, tmin, tmax);
                 ts.start(o, d, tmin, tmax, r);
                 st.sp = 0;
-                if (n_tris > 0) ts.prime(nodes);
                 if (n_tris > 0) {
                     j = k;
                     js = ks;
@@ -994,136 +990,6 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
     }
 }
 
-// Ray order of the secondary-ray queues (RR_RAY_SORT, split path): the
-// extension and shadow rays of a bounce are traced in the order of a key made
-// of the cell of their origin (kSortCellBits per axis over the hierarchy's root
-// box, Morton order) and the octant of their direction, so that the rays in
-// flight together start in one region of the scene and head the same way and
-// share the nodes they visit. One counting pass (k_sort_count: the key of each
-// queue position into sort_key, a per-block histogram in LDS added into the
-// global one), one scan of the kSortBuckets counts (k_sort_scan), one scatter
-// of the queue slots to their bucket's range (k_sort_place: ranks from LDS
-// atomics, so the order inside a bucket is arbitrary). The trace kernels then
-// take positions from that order (queue gaps left out). Scheduling only: each
-// ray's hit is written at its own queue slot, so no result changes.
-#ifndef RR_SORT_CELL_BITS
-#define RR_SORT_CELL_BITS 3
-#endif
-constexpr int kSortCellBits = RR_SORT_CELL_BITS;
-constexpr int kSortBuckets = 8 << (3 * kSortCellBits);  // octant x cells
-constexpr int kRaySortItems = 64;                          // queue positions per thread of the sort kernels
-constexpr int kRaySortTile = kRaySortItems * kBlock;
-constexpr uint32_t kSortNone = 0xFFFFFFFFu;
-struct SortBox {
-    float3 lo, sc;  // cell = (p - lo) * sc, sc = 2^kSortCellBits / extent
-};
-RR_D SortBox sort_box(const SceneArgs& sa) {
-    SortBox b;
-    b.lo = b.sc = mk3(0.0f, 0.0f, 0.0f);
-    if (sa.n_qnodes <= 0) return b;
-    const float4 org = sa.qnodes[0].org;  // wave-uniform: scalar loads
-    const uint32_t eb = (uint32_t)f2i(org.w);
-    const float cells = (float)(1 << kSortCellBits);
-    b.lo = mk3(org.x, org.y, org.z);
-    b.sc = mk3(cells / ldexpf(256.0f, (int)(eb & 255u) - 128), cells / ldexpf(256.0f, (int)((eb >> 8) & 255u) - 128),
-               cells / ldexpf(256.0f, (int)((eb >> 16) & 255u) - 128));
-    return b;
-}
-RR_D uint32_t sort_spread(uint32_t v) {  // kSortCellBits <= 5 bits -> every third bit
-    uint32_t r = 0;
-    for (int k = 0; k < kSortCellBits; ++k) r |= ((v >> k) & 1u) << (3 * k);
-    return r;
-}
-RR_D uint32_t ray_sort_key(const SortBox& b, float4 o, float4 d) {
-    const float mx = (float)((1 << kSortCellBits) - 1);
-    const uint32_t cx = (uint32_t)fminf(fmaxf((o.x - b.lo.x) * b.sc.x, 0.0f), mx);
-    const uint32_t cy = (uint32_t)fminf(fmaxf((o.y - b.lo.y) * b.sc.y, 0.0f), mx);
-    const uint32_t cz = (uint32_t)fminf(fmaxf((o.z - b.lo.z) * b.sc.z, 0.0f), mx);
-    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-    return (oct << (3 * kSortCellBits)) | (sort_spread(cx) << 2) | (sort_spread(cy) << 1) | sort_spread(cz);
-}
-// The key of every queue position of this block's tile (kSortNone for a gap)
-// and the bucket counts. hist: kSortBuckets words, zeroed before the launch.
-__global__ __launch_bounds__(kBlock) void k_sort_count(SceneArgs sa, QueueIn qi, const float4* __restrict__ ro,
-                                                       const float4* __restrict__ rd, uint32_t* __restrict__ keys,
-                                                       uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[kSortBuckets];
-    for (int i = threadIdx.x; i < kSortBuckets; i += kBlock) h[i] = 0;
-    QueueMap qm;
-    qm.init(qi);
-    const SortBox box = sort_box(sa);
-    __syncthreads();
-    const int base = blockIdx.x * kRaySortTile;
-    if (base < qm.span) {  // block-uniform
-        for (int k = 0; k < kRaySortItems; ++k) {
-            const int m = base + k * kBlock + (int)threadIdx.x;
-            const uint32_t i = qm.slot_t(m < qm.span ? m : qm.span - 1);  // all lanes (shuffles)
-            if (m >= qm.span) continue;
-            uint32_t key = kSortNone;
-            if (i != kNoSlot) {
-                key = ray_sort_key(box, ro[i], rd[i]);
-                atomicAdd(&h[key], 1u);
-            }
-            keys[m] = key;
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kSortBuckets; i += kBlock)
-        if (h[i]) atomicAdd(&hist[i], h[i]);
-}
-// Exclusive scan of the bucket counts in place (one block of kBlock threads).
-__global__ __launch_bounds__(kBlock) void k_sort_scan(uint32_t* __restrict__ hist) {
-    constexpr int kPer = kSortBuckets / kBlock;
-    __shared__ uint32_t wsum[kBlock / 64];
-    uint32_t v[kPer], t = 0;
-    for (int k = 0; k < kPer; ++k) {
-        v[k] = hist[threadIdx.x * kPer + k];
-        t += v[k];
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = t;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(inc, off);
-        if (lane >= off) inc += o;
-    }
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    uint32_t run = inc - t;
-    for (int k = 0; k < w; ++k) run += wsum[k];
-    for (int k = 0; k < kPer; ++k) {
-        hist[threadIdx.x * kPer + k] = run;
-        run += v[k];
-    }
-}
-// Each valid queue position's slot to order[start of its bucket + rank].
-// hist: the scanned bucket starts, advanced as blocks take their ranges.
-__global__ __launch_bounds__(kBlock) void k_sort_place(QueueIn qi, const uint32_t* __restrict__ keys,
-                                                       uint32_t* __restrict__ hist, uint32_t* __restrict__ order) {
-    __shared__ uint32_t h[kSortBuckets];
-    for (int i = threadIdx.x; i < kSortBuckets; i += kBlock) h[i] = 0;
-    QueueMap qm;
-    qm.init(qi);
-    __syncthreads();
-    const int base = blockIdx.x * kRaySortTile;
-    if (base >= qm.span) return;  // block-uniform
-    for (int k = 0; k < kRaySortItems; ++k) {
-        const int m = base + k * kBlock + (int)threadIdx.x;
-        if (m < qm.span && keys[m] != kSortNone) atomicAdd(&h[keys[m]], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kSortBuckets; i += kBlock)
-        if (h[i]) h[i] = atomicAdd(&hist[i], h[i]);  // this block's range of bucket i
-    __syncthreads();
-    for (int k = 0; k < kRaySortItems; ++k) {
-        const int m = base + k * kBlock + (int)threadIdx.x;
-        const uint32_t i = qm.slot_t(m < qm.span ? m : qm.span - 1);  // all lanes (shuffles)
-        if (m >= qm.span) continue;
-        const uint32_t key = keys[m];
-        if (key == kSortNone) continue;
-        order[atomicAdd(&h[key], 1u)] = i;
-    }
-}
-
 // Camera paths: raygen + closest hit -> hits[p].
 template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
@@ -1139,7 +1005,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, np, walk_radius(sa, nodes), st, cnt, [](int p) { return (uint32_t)p; },
+        nodes, sa.tris, sa.n_tris, np, 0.0f, st, cnt, [](int p) { return (uint32_t)p; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
             const int sl = (int)fc.div_npix.div(p);
             const int pix = (int)p - sl * fc.npix;
@@ -1177,10 +1043,9 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
 constexpr int kPacketStack = 128;  // a node pushes <= 5: bounded by 5 x the hierarchy depth
 template <bool kCount>
 RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk, bool act,
-                       float3 o, float3 d, float tmin, float r, Hit& h, TravCount& cnt, uint32_t& dropped) {
+                       float3 o, float3 d, float tmin, Hit& h, TravCount& cnt, uint32_t& dropped) {
     if (!__ballot(act)) return;
     const float3 iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
-    const float mrg = ray_margin(o, r);
     const Shear sh = make_shear(d);
     int node = 0, sp = 0;
     for (;;) {
@@ -1188,7 +1053,7 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
         const QNode6 nd = nodes[node];  // wave-uniform: scalar loads
         const uint32_t imask = q6_inner(nd);
         float tn[kQWidth];
-        const uint32_t hm = live ? q6_box_hits(nd, o, iq, mrg, tmin, h.t, tn) : 0u;
+        const uint32_t hm = live ? q6_box_hits(nd, o, iq, tmin, h.t, tn) : 0u;
         if (kCount && live) ++cnt.nodes;
         // leaf children in slot order (a lane tests those its ray enters)
 #pragma unroll
@@ -1255,7 +1120,6 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
     const int npk = ntiles * (np / fc.npix);
     const int nw = gridDim.x * kWavesPerBlock;
     uint32_t n_traced = 0, dropped = 0;
-    const float rad = sa.n_qnodes > 0 ? q6_margin_radius(sa.qnodes[0]) : 0.0f;  // wave-uniform (scalar loads)
     for (int q = xcd_wave_rank(); q < npk; q += nw) {
         const int sl = q / ntiles, t = q - sl * ntiles;
         const int ty = t / tiles_x, tx = t - ty * tiles_x;
@@ -1272,7 +1136,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         n_traced += valid && !culled ? 1u : 0u;
         Hit h;
         set_miss(h, tmax);
-        packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, rad, h, cnt,
+        packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt,
                              dropped);
         if (valid) hits[(size_t)sl * fc.npix + pix] = pack_hit(h);
     }
@@ -1312,10 +1176,8 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
 }
 
 // Extension rays entering bounce b: closest hit -> hits[slot].
-// order: the queue slots in ray-sort order (k_sort_place), or null.
 template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
-                                                                         const uint32_t* __restrict__ order,
                                                                          float2* __restrict__ hits,
                                                                          int32_t* __restrict__ spill,
                                                                          unsigned long long* __restrict__ tc) {
@@ -1327,8 +1189,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, order ? qm.total : qm.span, walk_radius(sa, nodes), st, cnt,
-        [&](int m) { return order ? order[m] : qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, 0.0f, st, cnt, [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
@@ -1377,7 +1238,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
 // Shadow rays with lane refill: unoccluded -> radiance += contribution.
 template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
-                                                                          const uint32_t* __restrict__ order, Rad rad,
+                                                                          Rad rad,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
@@ -1388,8 +1249,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
-        nodes, sa.tris, sa.n_tris, order ? qm.total : qm.span, walk_radius(sa, nodes), st, cnt,
-        [&](int m) { return order ? order[m] : qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, 0.0f, st, cnt, [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
@@ -2030,11 +1890,10 @@ __global__ void k_debug_trace4(const QNode6* __restrict__ nodes, const TriPack* 
     const int nthreads = gridDim.x * kBlock;
     TravStack st{lds_slot(lds_stack), spill, nthreads, 0};
     TravCount cnt;
-    const float rad = n_tris > 0 ? q6_margin_radius(nodes[0]) : 0.0f;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
         TravStateQ6<false> ts;
-        ts.start(xyz(o), xyz(d), o.w, d.w, rad);
+        ts.start(xyz(o), xyz(d), o.w, d.w);
         st.sp = 0;
         if (n_tris > 0)
             while (!ts.step(nodes, tris, st, cnt)) {
@@ -2042,7 +1901,7 @@ __global__ void k_debug_trace4(const QNode6* __restrict__ nodes, const TriPack* 
         hits[i] = make_float4(ts.h.t, ts.h.u, ts.h.v, 0.0f);
         prims[i] = ts.h.orig;
         TravStateQ6<true> ta;
-        ta.start(xyz(o), xyz(d), o.w, d.w, rad);
+        ta.start(xyz(o), xyz(d), o.w, d.w);
         st.sp = 0;
         if (n_tris > 0)
             while (!ta.step(nodes, tris, st, cnt)) {
@@ -2161,8 +2020,8 @@ struct TileGrid {
 struct SplitGrids {
     int trace_p, trace_e, shadow, shade_p, shade_e, packet;
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
-    void (*kte)(SceneArgs, PathQueue, QueueIn, const uint32_t*, float2*, int32_t*, unsigned long long*);
-    void (*kts)(SceneArgs, ShadowQueue, QueueIn, const uint32_t*, Rad, int32_t*, unsigned long long*);
+    void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
+    void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
     void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
@@ -2217,7 +2076,6 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
-    sort_key.release(); sort_order.release(); sort_hist.release();
     counters.release(); tile_ctrs.release(); tile_cost.release(); tile_order.release(); spill.release(); tile_slab.release(); film_part.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     mat_lut.release();
@@ -2228,26 +2086,6 @@ void DevPaths::release() {
 }
 
 namespace {
-#ifndef RR_RAY_SORT
-#define RR_RAY_SORT 0
-#endif
-// The secondary-ray order of one queue (k_sort_count / k_sort_scan /
-// k_sort_place over its capacity, kRaySortTile positions per block; blocks past
-// the queue's span return at once), or null without RR_RAY_SORT.
-const uint32_t* sort_rays(DevPaths& p, const SceneArgs& sa, const QueueIn& q, const float4* o, const float4* d,
-                          hipStream_t st) {
-    if (!RR_RAY_SORT) return nullptr;
-    const size_t n = (size_t)q.cap * kQGroups;
-    p.sort_key.ensure(n);
-    p.sort_order.ensure(n);
-    p.sort_hist.ensure(kSortBuckets);
-    const int blocks = (int)((n + kRaySortTile - 1) / kRaySortTile);
-    RR_HIP(hipMemsetAsync(p.sort_hist.ptr, 0, kSortBuckets * sizeof(uint32_t), st));
-    k_sort_count<<<blocks, kBlock, 0, st>>>(sa, q, o, d, p.sort_key.ptr, p.sort_hist.ptr);
-    k_sort_scan<<<1, kBlock, 0, st>>>(p.sort_hist.ptr);
-    k_sort_place<<<blocks, kBlock, 0, st>>>(q, p.sort_key.ptr, p.sort_hist.ptr, p.sort_order.ptr);
-    return p.sort_order.ptr;
-}
 // Large scenes: per chunk trace_primary -> shade_primary -> for each bounce b:
 // shadow(b), trace_extend(b+1), shade_extend(b+1) -> accumulate. Radiance
 // additions per path happen in the same order as the fused kernels'.
@@ -2296,17 +2134,15 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         for (int b = 0; b <= base.max_bounces; ++b) {
             pr.begin(st, RR_K_SHADOW);
-            const QueueIn qs{qshadow(b), cap_prev, tot + 2 * b + 1};
-            const uint32_t* so = sort_rays(p, sa, qs, sq.o, sq.d, st);
             G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(
-                sa, sq, qs, so, Rad{reinterpret_cast<float*>(p.rad.ptr)}, p.spill.ptr, tc);
+                sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, Rad{reinterpret_cast<float*>(p.rad.ptr)},
+                p.spill.ptr, tc);
             pr.end(st);
             if (b == base.max_bounces) break;
             const int nb = b + 1;  // bounce being traced and shaded
             const QueueIn qin{qpath(b), cap_prev, tot + 2 * b};
             pr.begin(st, RR_K_EXTEND);
-            const uint32_t* eo = sort_rays(p, sa, qin, pq[nb & 1].o, pq[nb & 1].d, st);
-            G.kte<<<clamp_grid(np, G.trace_e, kTraceBlock), kTraceBlock, 0, st>>>(sa, pq[nb & 1], qin, eo, p.hits.ptr,
+            G.kte<<<clamp_grid(np, G.trace_e, kTraceBlock), kTraceBlock, 0, st>>>(sa, pq[nb & 1], qin, p.hits.ptr,
                                                                                 p.spill.ptr, tc);
             pr.end(st);
             pr.begin(st, RR_K_SHADE);

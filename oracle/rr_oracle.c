@@ -682,9 +682,10 @@ typedef struct { float t, u, v; int idx, orig; } hitrec;
 /* Watertight traversal (csrc/rr_device.h, "intersection"): the triangle test
  * decides a hit exactly in a 2D projection of the ray's own (woop_test), and
  * every box test widens the box by ORC_BOX_MARGIN (2^-19) of the largest
- * coordinate involved — the box's distance from the origin plus its extent —
- * a distance along each axis, margin * |1/d| in t: subtracted from the near
- * planes, added to the far ones. */
+ * coordinate involved — a distance along each axis, margin * |1/d| in t:
+ * subtracted from the near planes, added to the far ones. The BVH2 walk takes
+ * it per ray (|o|_inf + the scene box's largest |coordinate|), the quantised
+ * walk per node (the node's largest |org - o| + extent, q6_planes). */
 #define ORC_BOX_MARGIN 0x1p-19f
 
 /* plane distances fmaf(b, inv, oi), oi = -(o inv) per ray, widened by em per
@@ -780,6 +781,10 @@ typedef struct { float t; int slot, ref; } ckey;
 /* node visits / triangle tests of trace4 since the last reset (research:
  * tools/collapse_study.py) */
 static long long g_cnt_nodes, g_cnt_tris, g_cnt_top[4];
+/* research only (tools/margin_study.py): the walk's box margin times this
+ * (1 = the product's); results then may differ from the device's */
+static float g_margin_scale = 1.0f;
+void orc_set_margin_scale(float s) { g_margin_scale = s; }
 /* out: node visits, triangle tests, visits of nodes below 128 / 256 / 512 / 1024 */
 void orc_walk_counts(long long* out6, int reset) {
     out6[0] = g_cnt_nodes; out6[1] = g_cnt_tris;
@@ -811,15 +816,6 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
     if (B->n <= 0) return 0;
     const shear_t sh = make_shear(d);
     const v3 iqv = rcp3(d);
-    /* the ray's margin distance (rr_device.h ray_margin, q6_margin_radius of the root) */
-    float rr = 0.0f;
-    for (int a = 0; a < 3; ++a) {
-        float org, hi;
-        memcpy(&org, B->q4 + a, sizeof org);
-        hi = org + ldexpf(255.0f, (int)((B->q4[3] >> (8 * a)) & 255u) - 128);
-        rr = fmaxf(rr, fmaxf(fabsf(org), fabsf(hi)));
-    }
-    const float mrg = (fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + 2.0f * rr) * ORC_BOX_MARGIN;
     const float iq[3] = {iqv.x, iqv.y, iqv.z};
     const float oo[3] = {o.x, o.y, o.z};
     int stack[ORC_MAXDEPTH];
@@ -833,13 +829,23 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
         const float tcur = h->t;
         float sc[3], onr[3], ofr[3];
         int pos[3];
-        for (int a = 0; a < 3; ++a) {  /* rr_device.h q6_planes */
+        /* rr_device.h q6_planes: the node's margin distance ORC_BOX_MARGIN (the
+         * largest |org - o| + 255 * 2^e over the axes) */
+        float dif[3], ext[3];
+        for (int a = 0; a < 3; ++a) {
             float org;
             memcpy(&org, nd + a, sizeof org);
-            sc[a] = ldexpf(iq[a], (int)((nd[3] >> (8 * a)) & 255u) - 128);
-            const float dif = org - oo[a], ma = mrg * fabsf(iq[a]);
-            onr[a] = fmaf(dif, iq[a], -ma);
-            ofr[a] = fmaf(dif, iq[a], ma);
+            const int e = (int)((nd[3] >> (8 * a)) & 255u) - 128;
+            dif[a] = org - oo[a];
+            ext[a] = ldexpf(255.0f, e);
+            sc[a] = ldexpf(iq[a], e);
+        }
+        const float mrg = fmaxf(fmaxf(fabsf(dif[0]) + ext[0], fabsf(dif[1]) + ext[1]), fabsf(dif[2]) + ext[2]) *
+                          ORC_BOX_MARGIN * g_margin_scale;
+        for (int a = 0; a < 3; ++a) {
+            const float ma = mrg * fabsf(iq[a]);
+            onr[a] = fmaf(dif[a], iq[a], -ma);
+            ofr[a] = fmaf(dif[a], iq[a], ma);
             pos[a] = iq[a] >= 0.0f;
         }
         /* near / far grid coordinates per axis: children 0..3 one byte of a
