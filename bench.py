@@ -593,6 +593,12 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=No
            "traffic_gbs": round(e["traffic_bytes"] / (avg_ms * 1e-3) / 1e9, 1) if e else None,
            "traffic_source": src if e else None,
            "launch_timing": "HIP events around each launch on the library's stream over the timed region"}
+    # PMC bytes per ray the class traced (counting frame's ray counts)
+    cls_rays = {"primary": cstats.camera_rays_traced, "extend": cstats.extension_rays,
+                "shadow": cstats.shadow_rays}.get(cls, 0)
+    if e and cls_rays:
+        hbm["traffic_bytes_per_ray"] = round(e["traffic_bytes"] * launches_frame / float(cls_rays), 1)
+        hbm["fetch_scale"] = e.get("fetch_scale", 2.0)
     base = {"kernel": cls, "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": launches_frame,
             "bytes_per_launch_algorithmic": round((survey_frame if split else bytes_frame) / launches_frame)}
     lat = {k: round(e[k], 3) for k in ("l2_hit_rate", "wait_frac") if e and k in e}
@@ -603,14 +609,16 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=No
                 "frac": round(ach / HBM_PEAK_GBS, 4), **lat, **hbm,
                 "note": "hierarchy + triangles fit in L2/MALL: the kernel waits on cache-hit latency, not HBM "
                         "bandwidth (l2_hit_rate, wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES from the PMC passes); "
-                        "achieved / frac are its PMC HBM rate (FETCH_SIZE x2 + WRITE_SIZE per launch / launch "
-                        "time) for reference only"}
+                        "achieved / frac are its PMC HBM rate (FETCH_SIZE x fetch_scale + WRITE_SIZE per launch / "
+                        "launch time; fetch_scale 1 for these 64 B gathers per tools/fetch_probe.hip) for reference "
+                        "only"}
     ach = per_s(survey_frame)
     return {**base, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), **lat, **hbm,
             "note": "hierarchy above MALL: achieved = SURVEY 8(d) algorithmic bytes (64 B per node visit, 48 B per "
                     "triangle test + ray/hit stream) per launch / launch time; traffic = PMC HBM bytes per launch "
-                    "(FETCH_SIZE counts Infinity-Cache hits, so it is an upper bound on HBM reads)"}
+                    "(FETCH_SIZE x fetch_scale, 1 for these 64 B gathers per tools/fetch_probe.hip, + WRITE_SIZE; "
+                    "FETCH_SIZE counts Infinity-Cache hits, so it is an upper bound on HBM reads)"}
 
 
 def main():

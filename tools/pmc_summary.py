@@ -5,10 +5,14 @@ into profiles/ so bench.py can quote PMC-measured HBM traffic per launch.
   python tools/pmc_summary.py stats  <kernel-trace dir> > profiles/r1_kernel_stats.md
   python tools/pmc_summary.py traffic --fetch <dir> --write <dir> [--sq <dir> ...] -o profiles/r1_pmc.json
 
-HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB;
-on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so the
-corrected read bytes are 2 x FETCH_SIZE x 1024 (the correction is calibrated for
-16 B/lane streaming loads only; raw values are kept beside it).
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB.
+On gfx950 FETCH_SIZE counts 64 B per TCC read request whatever its size:
+tools/fetch_probe.hip measured 0.500 FETCH_SIZE bytes per byte read for a
+coalesced 16 B/lane stream (128 B requests) and 1.000 for random 64 B node
+gathers (profiles/r4_fetch_probe.json). So the read bytes are 2 x FETCH_SIZE x
+1024 for streaming kernels and FETCH_SIZE x 1024 for the traversal kernels,
+whose reads are 64 B node and triangle fetches (GATHER below); the raw value
+and the other bound are kept beside it.
 """
 from __future__ import annotations
 
@@ -22,6 +26,8 @@ import sys
 from collections import defaultdict
 
 _NAME = re.compile(r"(k_\w+)(<[^>(]*>)?")
+# kernels whose reads are 64 B gathers (FETCH_SIZE x 1 per the probe)
+GATHER = ("k_trace_primary", "k_trace_extend", "k_shadow_refill", "k_trace_primary_packet")
 
 
 def short_name(full: str) -> str:
@@ -93,7 +99,8 @@ def cmd_traffic(a):
             if k in dur:
                 durs[k] = {"pmc_pass_avg_ms": dur[k] / 1e6}
     out = {"source": {"fetch": a.fetch, "write": a.write, "sq": a.sq or []},
-           "units": "bytes per launch; fetch_bytes = 2 x FETCH_SIZE(KiB) x 1024 (gfx950 correction)",
+           "units": "bytes per launch; fetch_bytes = 2 x FETCH_SIZE(KiB) x 1024 for streaming kernels, "
+                    "1 x for the traversal kernels (64 B gathers; tools/fetch_probe.hip calibration)",
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, {}).get("FETCH_SIZE", [])
@@ -101,8 +108,9 @@ def cmd_traffic(a):
         n = max(len(f), len(w), 1)
         fr = sum(f) / max(len(f), 1) * 1024.0
         wr = sum(w) / max(len(w), 1) * 1024.0
-        e = {"launches": n, "fetch_size_raw_bytes": fr, "fetch_bytes": 2.0 * fr, "write_bytes": wr,
-             "traffic_bytes": 2.0 * fr + wr}
+        scale = 1.0 if k.split("<")[0] in GATHER else 2.0
+        e = {"launches": n, "fetch_size_raw_bytes": fr, "fetch_scale": scale, "fetch_bytes": scale * fr,
+             "fetch_bytes_if_streaming": 2.0 * fr, "write_bytes": wr, "traffic_bytes": scale * fr + wr}
         for c, vals in extra.get(k, {}).items():
             e[c] = sum(vals) / max(len(vals), 1)
         e.update(durs.get(k, {}))
