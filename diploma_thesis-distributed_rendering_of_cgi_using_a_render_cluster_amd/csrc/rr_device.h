@@ -116,6 +116,7 @@ struct alignas(16) TriPack {
     float4 p2;  // v2.xyz, 0
 };
 static_assert(sizeof(TriPack) == 48, "tri pack is 48 bytes");
+constexpr int kTriF4 = 3;  // float4s per TriPack (LDS staging)
 
 // Leaf refs (< 0) name a range of sorted leaves: ~(first | (count - 1) << 28).
 // The frame hierarchies use single-triangle leaves (count 1, ref = ~index):
@@ -407,7 +408,10 @@ RR_HD bool screen_rect(float3 pos, float3 right, float3 up, float3 back, float h
 // from the origin, the plane distances to about 13). The margin is a distance
 // along an axis; in t it is margin * |1/d| on that axis, subtracted from the
 // near planes and added to the far ones. oracle/rr_oracle.c restates both.
-constexpr float kBoxMargin = 0x1p-19f;
+#ifndef RR_BOX_MARGIN
+#define RR_BOX_MARGIN 0x1p-19f  // (timing builds may set 0)
+#endif
+constexpr float kBoxMargin = RR_BOX_MARGIN;
 
 // Slab test against [bmin,bmax]; inclusive so equal-t candidates survive (the
 // closest hit is then independent of traversal order, see closest_tri()).
@@ -573,6 +577,30 @@ RR_HD void closest_tri(const TriPack& tp, int idx, const Shear& s, float3 o, flo
 RR_HD void leaf_test(const TriPack& tp, int idx, const Shear& s, float3 o, float tmin, Hit& h) {
     closest_tri(tp, idx, s, o, tmin, h);
 }
+#if RR_AB_MT  // timing builds only: round 3's Moller-Trumbore test (not watertight)
+RR_HD void leaf_test_mt(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
+    const float3 v0 = xyz(tp.p0), e1 = sub3(xyz(tp.p1), v0), e2 = sub3(xyz(tp.p2), v0);
+    const float3 pv = cross3(d, e2);
+    const float det = dot3(e1, pv);
+    const float3 tv = sub3(o, v0);
+    const float3 qv = cross3(tv, e1);
+    const float un = dot3(tv, pv), vn = dot3(d, qv);
+    const bool neg = det < 0.0f;
+    const float a = neg ? -det : det, su = neg ? -un : un, sv = neg ? -vn : vn;
+    if (det == 0.0f || su < 0.0f || su > a || sv < 0.0f || su + sv > a) return;
+    const float inv = 1.0f / det;
+    const float t = dot3(e2, qv) * inv;
+    const int orig = f2i(tp.p0.w);
+    if (closer(t, orig, tmin, h)) {
+        h.t = t;
+        h.u = un * inv;
+        h.v = vn * inv;
+        h.idx = idx;
+        h.orig = orig;
+    }
+}
+#endif
+
 
 // Traversal stack: kLdsStack entries in LDS ([entry][thread] -> conflict-free
 // ds_read_b32 across a wave), deeper entries in a per-thread HBM spill area.
@@ -634,7 +662,9 @@ struct TravStackT {
         } else if (sp < kLdsStack + kSpillStack) {
             spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)] = x;
         } else {
+#if !RR_AB_NODROP  // (timing builds only)
             ++dropped;
+#endif
             return;
         }
         ++sp;
@@ -832,9 +862,12 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
     const uint32_t nx2 = px ? lox : hix, fx2 = px ? hix : lox;
     const uint32_t ny2 = py ? loy : hiy, fy2 = py ? hiy : loy;
     const uint32_t nz2 = pz ? loz : hiz, fz2 = pz ? hiz : loz;
+    // The used-slot mask is applied once at the end; the best-slot choice
+    // needs none (internal slots are used slots). bt starts at +inf: the entry
+    // distance of a hit box is finite (t0 <= t1 <= tcur).
     uint32_t hits = 0;
     best = -1;
-    float bt = 0.0f;
+    float bt = __builtin_inff();
 #pragma unroll
     for (int c = 0; c < kQWidth; ++c) {
         const int sh = c < 4 ? 8 * c : 8 * (c - 4);
@@ -844,14 +877,18 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
                                fmaxf(fmaf((float)((qnz >> sh) & 255u), sz, pl.nz), tmin));
         const float t1 = fminf(fminf(fmaf((float)((qfx >> sh) & 255u), sx, pl.fx), fmaf((float)((qfy >> sh) & 255u), sy, pl.fy)),
                                fminf(fmaf((float)((qfz >> sh) & 255u), sz, pl.fz), tcur));
-        const bool hit = t0 <= t1 && ((used >> c) & 1u);
-        if (hit) hits |= 1u << c;
-        if (hit && ((imask >> c) & 1u) && (best < 0 || (kNearest && t0 < bt))) {
+        const bool hit = t0 <= t1;
+        hits |= (uint32_t)hit << c;
+        if (hit && ((imask >> c) & 1u) && (!kNearest ? best < 0 : t0 < bt)) {
             best = c;
             bt = t0;
         }
     }
+#if RR_AB_NOUSED  // (timing builds only)
     return hits;
+#else
+    return hits & used;
+#endif
 }
 
 // Node fetch of the 6-wide walk. The split-path trace kernels keep a copy of
@@ -891,6 +928,9 @@ template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6 {
     float3 o, iq;
     Shear sh;
+#if RR_AB_MT
+    float3 d;
+#endif
     float tmin;
     Hit h;
     int node;
@@ -898,6 +938,9 @@ struct TravStateQ6 {
     RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_, float = 0.0f) {
         o = o_;
         sh = make_shear(d_);
+#if RR_AB_MT
+        d = d_;
+#endif
         tmin = tmin_;
         h.t = tmax_;
         h.u = h.v = 0.0f;
@@ -923,7 +966,11 @@ struct TravStateQ6 {
             leaves &= leaves - 1;
             const int ti = (int)nd.a.y + c - __builtin_popcount(imask & ((1u << c) - 1u));
             if (kCount) ++cnt.tris;
+            #if RR_AB_MT
+            leaf_test_mt(load_tri(tris, ti), ti, o, d, tmin, h);
+#else
             leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
+#endif
             if (kAnyHit && h.idx >= 0) return true;
         }
         if (!inner) {

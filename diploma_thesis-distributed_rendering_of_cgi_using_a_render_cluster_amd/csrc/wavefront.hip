@@ -589,8 +589,8 @@ RR_D LdsView stage_scene(lds_f4w* base, const SceneArgs& a, bool shading, int& u
     lds_copy(q, reinterpret_cast<const float4*>(a.nodes), 4 * a.n_nodes);
     q += 4 * a.n_nodes;
     v.tris = (lds_tri*)q;
-    lds_copy(q, reinterpret_cast<const float4*>(a.tris), 3 * a.n_tris);
-    q += 3 * a.n_tris;
+    lds_copy(q, reinterpret_cast<const float4*>(a.tris), kTriF4 * a.n_tris);
+    q += kTriF4 * a.n_tris;
     v.mats = v.lights = v.filter = v.lut = nullptr;
     if (shading) {
         v.mats = (lds_float*)q;
@@ -1980,7 +1980,7 @@ size_t scene_budget_bytes(const FrameConsts& fc) {  // the residency test's meas
 // per triangle) and the derived material records when shading.
 size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
     const int n_nodes = std::max(fc.n_tris - 1, 1);
-    size_t f4 = 4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris;
+    size_t f4 = 4 * (size_t)n_nodes + kTriF4 * (size_t)fc.n_tris;
     if (shading)
         f4 += (3 + kMatDF4 + kMatLutStride / 4) * (size_t)fc.n_mats + 3 * (size_t)fc.n_lights + kFilterN / 4 +
               (size_t)(1 + kOnbF4) * fc.n_tris;
