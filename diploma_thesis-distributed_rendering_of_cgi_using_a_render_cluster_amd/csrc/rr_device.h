@@ -505,20 +505,6 @@ RR_HD Shear make_shear_unit(float3 d) {
     s.sy = r.y * s.sz;
     return s;
 }
-// make_shear_unit for a kz known at compile time (the same operations: no
-// per-lane permutation).
-template <int K>
-RR_HD Shear make_shear_unit_k(float3 d) {
-    Shear s;
-    s.kz = K;
-    const float rz = K == 0 ? d.x : (K == 1 ? d.y : d.z);
-    const float rx = K == 0 ? d.y : (K == 1 ? d.z : d.x);
-    const float ry = K == 0 ? d.z : (K == 1 ? d.x : d.y);
-    s.sz = rcp_rn(rz);
-    s.sx = rx * s.sz;
-    s.sy = ry * s.sz;
-    return s;
-}
 // The test from the vertices relative to the origin, already permuted (a, b, c
 // = rot3(v - o, kz)).
 RR_HD bool woop_core(const Shear& s, float3 a, float3 b, float3 c, float& t, float& u, float& v) {
