@@ -408,10 +408,7 @@ RR_HD bool screen_rect(float3 pos, float3 right, float3 up, float3 back, float h
 // from the origin, the plane distances to about 13). The margin is a distance
 // along an axis; in t it is margin * |1/d| on that axis, subtracted from the
 // near planes and added to the far ones. oracle/rr_oracle.c restates both.
-#ifndef RR_BOX_MARGIN
-#define RR_BOX_MARGIN 0x1p-19f  // (timing builds may set 0)
-#endif
-constexpr float kBoxMargin = RR_BOX_MARGIN;
+constexpr float kBoxMargin = 0x1p-19f;
 
 // Slab test against [bmin,bmax]; inclusive so equal-t candidates survive (the
 // closest hit is then independent of traversal order, see closest_tri()).
@@ -563,29 +560,6 @@ RR_HD void closest_tri(const TriPack& tp, int idx, const Shear& s, float3 o, flo
 RR_HD void leaf_test(const TriPack& tp, int idx, const Shear& s, float3 o, float tmin, Hit& h) {
     closest_tri(tp, idx, s, o, tmin, h);
 }
-#if RR_AB_MT  // timing builds only: round 3's Moller-Trumbore test (not watertight)
-RR_HD void leaf_test_mt(const TriPack& tp, int idx, float3 o, float3 d, float tmin, Hit& h) {
-    const float3 v0 = xyz(tp.p0), e1 = sub3(xyz(tp.p1), v0), e2 = sub3(xyz(tp.p2), v0);
-    const float3 pv = cross3(d, e2);
-    const float det = dot3(e1, pv);
-    const float3 tv = sub3(o, v0);
-    const float3 qv = cross3(tv, e1);
-    const float un = dot3(tv, pv), vn = dot3(d, qv);
-    const bool neg = det < 0.0f;
-    const float a = neg ? -det : det, su = neg ? -un : un, sv = neg ? -vn : vn;
-    if (det == 0.0f || su < 0.0f || su > a || sv < 0.0f || su + sv > a) return;
-    const float inv = 1.0f / det;
-    const float t = dot3(e2, qv) * inv;
-    const int orig = f2i(tp.p0.w);
-    if (closer(t, orig, tmin, h)) {
-        h.t = t;
-        h.u = un * inv;
-        h.v = vn * inv;
-        h.idx = idx;
-        h.orig = orig;
-    }
-}
-#endif
 
 
 // Traversal stack: kLdsStack entries in LDS ([entry][thread] -> conflict-free
@@ -648,9 +622,7 @@ struct TravStackT {
         } else if (sp < kLdsStack + kSpillStack) {
             spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)] = x;
         } else {
-#if !RR_AB_NODROP  // (timing builds only)
             ++dropped;
-#endif
             return;
         }
         ++sp;
@@ -870,11 +842,7 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
             bt = t0;
         }
     }
-#if RR_AB_NOUSED  // (timing builds only)
-    return hits;
-#else
     return hits & used;
-#endif
 }
 
 // Node fetch of the 6-wide walk. The split-path trace kernels keep a copy of
@@ -914,9 +882,6 @@ template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6 {
     float3 o, iq;
     Shear sh;
-#if RR_AB_MT
-    float3 d;
-#endif
     float tmin;
     Hit h;
     int node;
@@ -924,9 +889,6 @@ struct TravStateQ6 {
     RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_, float = 0.0f) {
         o = o_;
         sh = make_shear(d_);
-#if RR_AB_MT
-        d = d_;
-#endif
         tmin = tmin_;
         h.t = tmax_;
         h.u = h.v = 0.0f;
@@ -952,11 +914,7 @@ struct TravStateQ6 {
             leaves &= leaves - 1;
             const int ti = (int)nd.a.y + c - __builtin_popcount(imask & ((1u << c) - 1u));
             if (kCount) ++cnt.tris;
-            #if RR_AB_MT
-            leaf_test_mt(load_tri(tris, ti), ti, o, d, tmin, h);
-#else
-            leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
-#endif
+                        leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
         }
         if (!inner) {
