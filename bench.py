@@ -424,17 +424,19 @@ def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin 
         done_rows += min(b + h, H) - b
         return tb, dt - tb
 
-    # the first 4-row band measures the per-call hierarchy build against the
-    # render; where the build dominates (C5: ~3.5 s a call), later bands grow
-    # to about the build's cost in rows, so the budget renders more rows. The
-    # later bands tile rows 4.. H and are taken in an order spread over the
-    # frame; the extrapolation uses them alone (the first band is always the
-    # top rows, usually background) unless the frame gets done whole.
-    tb0, tr0 = band(0, 4)
+    # the first 4-row band (the middle rows) measures the per-call hierarchy
+    # build against the render; where the build dominates (C5: ~3.5 s a call),
+    # later bands grow to about the build's cost in rows, so the budget renders
+    # more rows. The later bands tile the other rows and are taken in an order
+    # spread over the frame; the extrapolation uses them alone unless there are
+    # none (then the middle band stands for the frame) or the frame gets done
+    # whole.
+    b0 = (H // 2) // 4 * 4
+    tb0, tr0 = band(b0, 4)
     if tr0 > 0.0:
         band_h = 4 * max(1, min(16, int(round(tb0 / tr0))))
     first = (done_rows, t_render)
-    bands = list(range(4, H, band_h))
+    bands = [b for b in range(0, H, band_h) if b + band_h <= b0 or b >= b0 + 4]
     order = [b for k in range(16) for b in bands[k::16]]
     for b in order:
         if t_used >= budget_s:
@@ -450,8 +452,9 @@ def cpu_baseline(oracle_mod, state, budget_s: float, label: str = "04vs-standin 
     return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads, "kind": "port",
             "host": {"nproc": nproc, "affinity_cores": usable, "cpu_model": model,
                      "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
-            "sample": f"{done_rows} of {H} rows ({band_h}-row bands spread over rows 4..{H} after a first 4-row band "
-                      f"that sizes them and is left out of the extrapolation) of {label} "
+            "sample": f"{done_rows} of {H} rows ({band_h}-row bands spread over the frame after a first 4-row band at "
+                      f"row {b0} that sizes them and stands for the frame only when no other band fits the budget) "
+                      f"of {label} "
                       f"at {int(state.render_ints[0])}x{H}, {int(state.render_ints[2])} spp, "
                       f"{t_used:.1f} s in {len(builds)} band calls; frame time = one hierarchy build "
                       f"({t_build:.3f} s) + the bands' render time extrapolated to the whole frame; "
