@@ -984,7 +984,17 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
 
 // Camera paths: raygen + closest hit -> hits[p].
 template <bool kCount>
+// Positions are pixel-major (RR_CAM_PIXEL_MAJOR): position k is sample
+// k mod S of pixel k / S (S = the chunk's samples per pixel, div_spp), so the
+// 64 lanes of a chunk trace samples of one or two pixels: nearly the same ray,
+// the same nodes and triangles, which one wave's loads fetch together, and the
+// rays in flight on the chip cover a band of pixels S times narrower. Hits
+// are still written at p = sample * npix + pixel (what k_shade_primary reads).
+#ifndef RR_CAM_PIXEL_MAJOR
+#define RR_CAM_PIXEL_MAJOR 1
+#endif
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
+                                                                          FastDiv div_spp,
                                                                           float2* __restrict__ hits,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc,
@@ -997,7 +1007,12 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, np, 0.0f, st, cnt, [](int p) { return (uint32_t)p; },
+        nodes, sa.tris, sa.n_tris, np, 0.0f, st, cnt,
+        [&](int k) {
+            if (!RR_CAM_PIXEL_MAJOR) return (uint32_t)k;
+            const uint32_t pix = div_spp.div((uint32_t)k);
+            return (uint32_t)(k - (int)pix * fc.spp_chunk) * (uint32_t)fc.npix + pix;
+        },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
             const int sl = (int)fc.div_npix.div(p);
             const int pix = (int)p - sl * fc.npix;
@@ -2011,7 +2026,7 @@ struct TileGrid {
 // Launch geometry of the split (trace / shade) path of large scenes.
 struct SplitGrids {
     int trace_p, trace_e, shadow, shade_p, shade_e, packet;
-    void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
+    void (*ktp)(FrameConsts, SceneArgs, int, FastDiv, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
     void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
@@ -2091,7 +2106,10 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
     // at most one triangle per two pixels (02 / 03 yes, C5 no; on the 6-wide
     // hierarchy packets against per-lane walks: 02 / 03 camera rays at 64 spp
     // 12.6 / 12.4 against 16.9 / 15.0 ms)
-    const bool packets = (long)base.n_tris * 2 <= (long)npix;
+#ifndef RR_CAM_PACKETS
+#define RR_CAM_PACKETS 1
+#endif
+    const bool packets = RR_CAM_PACKETS && (long)base.n_tris * 2 <= (long)npix;
     // group counters: [chunk][bounce 0..max][path | shadow][kQGroups * kQStride]
     const size_t per_q = (size_t)kQGroups * kQStride;
     const size_t per_chunk = (size_t)(base.max_bounces + 1) * 2 * per_q;
@@ -2117,7 +2135,8 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
                                                                tot + camera_traced_slot(base.max_bounces));
         else
             G.ktp<<<clamp_grid(np, G.trace_p, kTraceBlock), kTraceBlock, 0, st>>>(
-                fc, sa, np, p.hits.ptr, p.spill.ptr, tc, tot + camera_traced_slot(base.max_bounces));
+                fc, sa, np, FastDiv::make((uint32_t)fc.spp_chunk), p.hits.ptr, p.spill.ptr, tc,
+                tot + camera_traced_slot(base.max_bounces));
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
         k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq,
