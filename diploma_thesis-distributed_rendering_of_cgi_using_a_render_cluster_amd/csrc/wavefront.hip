@@ -1114,8 +1114,14 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
 // tile (one sample) with packet_trace. Tiles are dealt to the waves as
 // trace_refill deals chunks (round-robin over the XCD-ordered waves).
 template <bool kCount>
+// RR_PACKET_PIXEL: a packet is 64 consecutive pixel-major positions (the
+// samples of one or two pixels, as k_trace_primary's chunks) instead of an 8x8
+// tile of one sample.
+#ifndef RR_PACKET_PIXEL
+#define RR_PACKET_PIXEL 0
+#endif
 __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
-    FrameConsts fc, SceneArgs sa, int np, float2* __restrict__ hits, int32_t* __restrict__,
+    FrameConsts fc, SceneArgs sa, int np, FastDiv div_spp, float2* __restrict__ hits, int32_t* __restrict__,
     unsigned long long* __restrict__ tc, uint32_t* __restrict__ traced) {
     __shared__ int stack_all[kWavesPerBlock * kPacketStack];
     lds_int* stk = lds_slot(stack_all) + (threadIdx.x >> 6) * kPacketStack;
@@ -1124,15 +1130,28 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
     const int lane = threadIdx.x & 63;
     const int tiles_x = (fc.W + 7) >> 3, tiles_y = (fc.H + 7) >> 3;
     const int ntiles = tiles_x * tiles_y;
-    const int npk = ntiles * (np / fc.npix);
+    const int npk = RR_PACKET_PIXEL ? (np + 63) / 64 : ntiles * (np / fc.npix);
     const int nw = gridDim.x * kWavesPerBlock;
     uint32_t n_traced = 0, dropped = 0;
     for (int q = xcd_wave_rank(); q < npk; q += nw) {
-        const int sl = q / ntiles, t = q - sl * ntiles;
-        const int ty = t / tiles_x, tx = t - ty * tiles_x;
-        const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
-        const bool valid = px < fc.W && py < fc.H;
-        const int pix = py * fc.W + px;
+        int sl, px, py, pix;
+        bool valid;
+        if (RR_PACKET_PIXEL) {
+            const int k = q * 64 + lane;
+            valid = k < np;
+            pix = (int)div_spp.div((uint32_t)(valid ? k : 0));
+            sl = (valid ? k : 0) - pix * fc.spp_chunk;
+            py = (int)fc.div_w.div((uint32_t)pix);
+            px = pix - py * fc.W;
+        } else {
+            sl = q / ntiles;
+            const int t = q - sl * ntiles;
+            const int ty = t / tiles_x, tx = t - ty * tiles_x;
+            px = tx * 8 + (lane & 7);
+            py = ty * 8 + (lane >> 3);
+            valid = px < fc.W && py < fc.H;
+            pix = py * fc.W + px;
+        }
         float3 o = mk3(0.0f, 0.0f, 0.0f), d = o;
         float tmin = 0.0f, tmax = -1.0f;
         bool culled = true;
@@ -2029,7 +2048,7 @@ struct SplitGrids {
     void (*ktp)(FrameConsts, SceneArgs, int, FastDiv, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
-    void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
+    void (*ktpk)(FrameConsts, SceneArgs, int, FastDiv, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
@@ -2109,7 +2128,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
 #ifndef RR_CAM_PACKETS
 #define RR_CAM_PACKETS 1
 #endif
-    const bool packets = RR_CAM_PACKETS && (long)base.n_tris * 2 <= (long)npix;
+    const bool packets = RR_CAM_PACKETS == 2 || (RR_CAM_PACKETS && (long)base.n_tris * 2 <= (long)npix);
     // group counters: [chunk][bounce 0..max][path | shadow][kQGroups * kQStride]
     const size_t per_q = (size_t)kQGroups * kQStride;
     const size_t per_chunk = (size_t)(base.max_bounces + 1) * 2 * per_q;
@@ -2131,7 +2150,8 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             throw std::runtime_error("queue capacity exceeded (split path)");
         pr.begin(st, RR_K_PRIMARY);
         if (packets)
-            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc,
+            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, FastDiv::make((uint32_t)fc.spp_chunk),
+                                                               p.hits.ptr, p.spill.ptr, tc,
                                                                tot + camera_traced_slot(base.max_bounces));
         else
             G.ktp<<<clamp_grid(np, G.trace_p, kTraceBlock), kTraceBlock, 0, st>>>(

@@ -7,4 +7,4 @@ timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 rc=$?
 tail -3 gpurun_out/r4k_tests.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 480 python tools/ab_run.py --rounds 2 main samp pmnp r3 -- scenes/02_physics-standin.rrscene:90:64 scenes/03_physics-2-standin.rrscene:300:64 scenes/c5_synthetic-10m.rrscene:150:16 > gpurun_out/ab13.txt 2>&1
+timeout -k 10 480 python tools/ab_run.py --rounds 2 main samp pmnp pkpix pkall r3 -- scenes/02_physics-standin.rrscene:90:64 scenes/03_physics-2-standin.rrscene:300:64 scenes/c5_synthetic-10m.rrscene:150:16 > gpurun_out/ab13.txt 2>&1
