@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
             camera_ray(fc, sa.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
             n_traced += culled ? 0u : 1u;
         },
-        [&](int p, uint32_t, const Hit& h) { hits[p] = pack_hit(h); });
+        [&](int, uint32_t p, const Hit& h) { hits[p] = pack_hit(h); });
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
     if ((threadIdx.x & 63) == 0 && n_traced) atomicAdd(traced, n_traced);
     if (kCount) {
