@@ -1118,7 +1118,7 @@ template <bool kCount>
 // samples of one or two pixels, as k_trace_primary's chunks) instead of an 8x8
 // tile of one sample.
 #ifndef RR_PACKET_PIXEL
-#define RR_PACKET_PIXEL 0
+#define RR_PACKET_PIXEL 1
 #endif
 __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
     FrameConsts fc, SceneArgs sa, int np, FastDiv div_spp, float2* __restrict__ hits, int32_t* __restrict__,
@@ -1176,18 +1176,35 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
 
 // Camera paths: shade bounce 0 from hits[p]; appends the bounce-1 path queue
 // and the bounce-0 shadow queue.
-__global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np,
+// RR_SHADE_PIXEL_MAJOR: camera paths are shaded pixel-major (position j is
+// sample j mod S of pixel j / S, as the camera packets run), so the bounce-0
+// shadow rays and the bounce-1 paths are queued with the samples of one pixel
+// side by side: the shadow rays of a chunk start at nearly one point toward
+// one light, the extension rays of a chunk from nearly one point.
+#ifndef RR_SHADE_PIXEL_MAJOR
+#define RR_SHADE_PIXEL_MAJOR 1
+#endif
+__global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np, FastDiv div_spp,
                                                           const float2* __restrict__ hits, Rad rad,
                                                           PathQueue out, ShadowQueue sq, QueueOut qo) {
     const GlobalView v = global_view(sa);
     const int stride = gridDim.x * kBlock;
     for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {
-        const int p = b0 + (int)threadIdx.x;
+        const int j = b0 + (int)threadIdx.x;
+        int p = j, sl = 0, pix = 0;
+        if (j < np) {
+            if (RR_SHADE_PIXEL_MAJOR) {
+                pix = (int)div_spp.div((uint32_t)j);
+                sl = j - pix * fc.spp_chunk;
+                p = sl * fc.npix + pix;
+            } else {
+                sl = (int)fc.div_npix.div((uint32_t)j);
+                pix = j - sl * fc.npix;
+            }
+        }
         ShadeOut so;
         so.cont = so.shadow = false;
-        if (p < np) {
-            const int sl = (int)fc.div_npix.div((uint32_t)p);
-            const int pix = p - sl * fc.npix;
+        if (j < np) {
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             float3 o, d;
             float tmin, tmax;
@@ -2121,12 +2138,15 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
     const SplitGrids G(tc != nullptr);
     const int npix = base.npix;
     const int cpc = counters_per_chunk(base.max_bounces);
-    // camera rays as packets (packet_trace) when triangles are large on screen:
-    // at most one triangle per two pixels (02 / 03 yes, C5 no; on the 6-wide
-    // hierarchy packets against per-lane walks: 02 / 03 camera rays at 64 spp
-    // 12.6 / 12.4 against 16.9 / 15.0 ms)
+    // camera rays as packets (packet_trace) of 64 pixel-major positions (the
+    // samples of one or two pixels: nearly one ray). Per frame slice (02 / 03
+    // at 64 spp, C5 at 16 spp), camera-ray traversal: 8x8-tile packets of one
+    // sample 16.1 / 20.6 ms and per-lane C5 20.4 ms (sample-major) or 17.7 ms
+    // (pixel-major); pixel-major packets 12.5 / 14.1 / 15.6 ms. RR_CAM_PACKETS
+    // (A/B): 0 per-lane walks (k_trace_primary), 1 packets only where a
+    // triangle covers at least two pixels (the round-3 rule), 2 always.
 #ifndef RR_CAM_PACKETS
-#define RR_CAM_PACKETS 1
+#define RR_CAM_PACKETS 2
 #endif
     const bool packets = RR_CAM_PACKETS == 2 || (RR_CAM_PACKETS && (long)base.n_tris * 2 <= (long)npix);
     // group counters: [chunk][bounce 0..max][path | shadow][kQGroups * kQStride]
@@ -2159,7 +2179,8 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
                 tot + camera_traced_slot(base.max_bounces));
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
-        k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq,
+        k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, FastDiv::make((uint32_t)fc.spp_chunk), p.hits.ptr,
+                                                Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq,
                                                 QueueOut{qpath(0), qshadow(0), cap_p});
         pr.end(st);
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
