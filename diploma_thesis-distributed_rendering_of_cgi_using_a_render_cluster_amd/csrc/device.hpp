@@ -172,7 +172,10 @@ struct FrameConsts {
     float half_w, half_h, clip_start, clip_end;
     float inv_w2, inv_h2;  // 2/W, 2/H
     int W, H, npix;
-    FastDiv div_w, div_npix;  // pixel index -> (x, y), path index -> (sample, pixel)
+    // pixel index -> (x, y); split-path index p = pixel * spp_chunk + sample ->
+    // (pixel, sample): pixel-major, so the samples of a pixel are neighbours in
+    // every per-path array (set per chunk, render_split)
+    FastDiv div_w, div_spp;
     int spp_total, spp_chunk, first_sample, max_bounces, n_lights;
     int max_diffuse, max_glossy;  // per-lobe bounce caps (>= 1, setup_frame)
     uint32_t seed;

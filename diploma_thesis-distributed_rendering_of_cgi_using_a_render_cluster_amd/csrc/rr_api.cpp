@@ -388,7 +388,7 @@ FrameConsts make_consts(const FrameSetup& fs, int n_tris) {
     k.H = fs.H;
     k.npix = fs.W * fs.H;
     k.div_w = FastDiv::make((uint32_t)fs.W);
-    k.div_npix = FastDiv::make((uint32_t)k.npix);
+    k.div_spp = FastDiv::make(1u);  // per chunk (render_split)
     k.spp_total = fs.spp;
     k.max_bounces = fs.max_bounces;
     k.max_diffuse = fs.max_diffuse;
@@ -558,6 +558,7 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     r.spp_chunk = choose_spp_chunk(fs);
     r.chunks = (fs.spp + r.spp_chunk - 1) / r.spp_chunk;
     k.spp_chunk = r.spp_chunk;
+    k.div_spp = FastDiv::make((uint32_t)k.spp_chunk);
     render_frame_device(s->dev, c->paths, k, r.chunks, st);
     r.tile_slices = c->paths.last_tile_slices;
     if (fs.view_transform == VIEW_FILMIC) {  // film -> Filmic -> rgba8 (overwrites the kernels' tonemap)

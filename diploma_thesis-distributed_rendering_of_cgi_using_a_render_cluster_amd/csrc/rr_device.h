@@ -914,7 +914,7 @@ struct TravStateQ6 {
             leaves &= leaves - 1;
             const int ti = (int)nd.a.y + c - __builtin_popcount(imask & ((1u << c) - 1u));
             if (kCount) ++cnt.tris;
-                        leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
+            leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
             if (kAnyHit && h.idx >= 0) return true;
         }
         if (!inner) {

@@ -983,18 +983,20 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
 }
 
 // Camera paths: raygen + closest hit -> hits[p].
+// Path index of the split path: p = pixel * spp_chunk + sample (FrameConsts
+// div_spp), pixel-major, so that the 64 lanes of a chunk trace (and shade)
+// samples of one or two pixels: nearly the same ray, the same nodes and
+// triangles, which one wave's loads fetch together, and the rays in flight on
+// the chip cover a band of pixels spp_chunk times narrower than in
+// sample-major order. The per-path arrays (hits, radiance) are indexed by p.
+RR_D void path_of(const FrameConsts& fc, uint32_t p, int& pix, int& sl) {
+    pix = (int)fc.div_spp.div(p);
+    sl = (int)p - pix * fc.spp_chunk;
+}
+// Per-lane camera walks (RR_CAM_PACKETS 0, A/B only: the packet walk below
+// is the default).
 template <bool kCount>
-// Positions are pixel-major (RR_CAM_PIXEL_MAJOR): position k is sample
-// k mod S of pixel k / S (S = the chunk's samples per pixel, div_spp), so the
-// 64 lanes of a chunk trace samples of one or two pixels: nearly the same ray,
-// the same nodes and triangles, which one wave's loads fetch together, and the
-// rays in flight on the chip cover a band of pixels S times narrower. Hits
-// are still written at p = sample * npix + pixel (what k_shade_primary reads).
-#ifndef RR_CAM_PIXEL_MAJOR
-#define RR_CAM_PIXEL_MAJOR 1
-#endif
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(FrameConsts fc, SceneArgs sa, int np,
-                                                                          FastDiv div_spp,
                                                                           float2* __restrict__ hits,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc,
@@ -1007,15 +1009,10 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, np, 0.0f, st, cnt,
-        [&](int k) {
-            if (!RR_CAM_PIXEL_MAJOR) return (uint32_t)k;
-            const uint32_t pix = div_spp.div((uint32_t)k);
-            return (uint32_t)(k - (int)pix * fc.spp_chunk) * (uint32_t)fc.npix + pix;
-        },
+        nodes, sa.tris, sa.n_tris, np, 0.0f, st, cnt, [](int k) { return (uint32_t)k; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
-            const int sl = (int)fc.div_npix.div(p);
-            const int pix = (int)p - sl * fc.npix;
+            int pix, sl;
+            path_of(fc, p, pix, sl);
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             bool culled;  // culled: tmax = -1 < tmin, every box test fails, the ray misses
             camera_ray(fc, sa.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
@@ -1114,44 +1111,26 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
 // tile (one sample) with packet_trace. Tiles are dealt to the waves as
 // trace_refill deals chunks (round-robin over the XCD-ordered waves).
 template <bool kCount>
-// RR_PACKET_PIXEL: a packet is 64 consecutive pixel-major positions (the
-// samples of one or two pixels, as k_trace_primary's chunks) instead of an 8x8
-// tile of one sample.
-#ifndef RR_PACKET_PIXEL
-#define RR_PACKET_PIXEL 1
-#endif
+// A packet is 64 consecutive path indices (path_of: the samples of one or two
+// pixels); an 8x8 tile of one sample per packet (round 3) measured 16.1 / 20.6
+// ms per 02 / 03 frame slice against 12.5 / 14.1.
 __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
-    FrameConsts fc, SceneArgs sa, int np, FastDiv div_spp, float2* __restrict__ hits, int32_t* __restrict__,
+    FrameConsts fc, SceneArgs sa, int np, float2* __restrict__ hits, int32_t* __restrict__,
     unsigned long long* __restrict__ tc, uint32_t* __restrict__ traced) {
     __shared__ int stack_all[kWavesPerBlock * kPacketStack];
     lds_int* stk = lds_slot(stack_all) + (threadIdx.x >> 6) * kPacketStack;
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     const int lane = threadIdx.x & 63;
-    const int tiles_x = (fc.W + 7) >> 3, tiles_y = (fc.H + 7) >> 3;
-    const int ntiles = tiles_x * tiles_y;
-    const int npk = RR_PACKET_PIXEL ? (np + 63) / 64 : ntiles * (np / fc.npix);
+    const int npk = (np + 63) / 64;
     const int nw = gridDim.x * kWavesPerBlock;
     uint32_t n_traced = 0, dropped = 0;
     for (int q = xcd_wave_rank(); q < npk; q += nw) {
-        int sl, px, py, pix;
-        bool valid;
-        if (RR_PACKET_PIXEL) {
-            const int k = q * 64 + lane;
-            valid = k < np;
-            pix = (int)div_spp.div((uint32_t)(valid ? k : 0));
-            sl = (valid ? k : 0) - pix * fc.spp_chunk;
-            py = (int)fc.div_w.div((uint32_t)pix);
-            px = pix - py * fc.W;
-        } else {
-            sl = q / ntiles;
-            const int t = q - sl * ntiles;
-            const int ty = t / tiles_x, tx = t - ty * tiles_x;
-            px = tx * 8 + (lane & 7);
-            py = ty * 8 + (lane >> 3);
-            valid = px < fc.W && py < fc.H;
-            pix = py * fc.W + px;
-        }
+        const int p = q * 64 + lane;
+        const bool valid = p < np;
+        int pix, sl;
+        path_of(fc, (uint32_t)(valid ? p : 0), pix, sl);
+        const int py = (int)fc.div_w.div((uint32_t)pix), px = pix - py * fc.W;
         float3 o = mk3(0.0f, 0.0f, 0.0f), d = o;
         float tmin = 0.0f, tmax = -1.0f;
         bool culled = true;
@@ -1164,7 +1143,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         set_miss(h, tmax);
         packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt,
                              dropped);
-        if (valid) hits[(size_t)sl * fc.npix + pix] = pack_hit(h);
+        if (valid) hits[p] = pack_hit(h);
     }
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
     if (lane == 0 && n_traced) atomicAdd(traced, n_traced);
@@ -1176,35 +1155,20 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
 
 // Camera paths: shade bounce 0 from hits[p]; appends the bounce-1 path queue
 // and the bounce-0 shadow queue.
-// RR_SHADE_PIXEL_MAJOR: camera paths are shaded pixel-major (position j is
-// sample j mod S of pixel j / S, as the camera packets run), so the bounce-0
-// shadow rays and the bounce-1 paths are queued with the samples of one pixel
-// side by side: the shadow rays of a chunk start at nearly one point toward
-// one light, the extension rays of a chunk from nearly one point.
-#ifndef RR_SHADE_PIXEL_MAJOR
-#define RR_SHADE_PIXEL_MAJOR 1
-#endif
-__global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np, FastDiv div_spp,
+// In path-index order (pixel-major), so the bounce-0 shadow rays and the
+// bounce-1 paths are queued with the samples of one pixel side by side.
+__global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np,
                                                           const float2* __restrict__ hits, Rad rad,
                                                           PathQueue out, ShadowQueue sq, QueueOut qo) {
     const GlobalView v = global_view(sa);
     const int stride = gridDim.x * kBlock;
     for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {
-        const int j = b0 + (int)threadIdx.x;
-        int p = j, sl = 0, pix = 0;
-        if (j < np) {
-            if (RR_SHADE_PIXEL_MAJOR) {
-                pix = (int)div_spp.div((uint32_t)j);
-                sl = j - pix * fc.spp_chunk;
-                p = sl * fc.npix + pix;
-            } else {
-                sl = (int)fc.div_npix.div((uint32_t)j);
-                pix = j - sl * fc.npix;
-            }
-        }
+        const int p = b0 + (int)threadIdx.x;
         ShadeOut so;
         so.cont = so.shadow = false;
-        if (j < np) {
+        if (p < np) {
+            int pix, sl;
+            path_of(fc, (uint32_t)p, pix, sl);
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             float3 o, d;
             float tmin, tmax;
@@ -1267,8 +1231,8 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
             const float4 a = in.o[i], b = in.d[i], c = in.t[i];
             pid = f2i(a.w);
             const Hit h = unpack_hit(hits[i]);
-            const int sl = (int)fc.div_npix.div((uint32_t)pid);
-            const int pix = pid - sl * fc.npix;
+            int pix, sl;
+            path_of(fc, (uint32_t)pid, pix, sl);
             const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
             float3 L = rad.get(pid);
             shade(fc, bounce, v, xyz(a), xyz(b), xyz(c), (uint32_t)f2i(b.w), h, key, L, so);
@@ -1351,7 +1315,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
                 acc.z = acc.z + P.z;
                 P = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
-            const float3 L = rad.get((size_t)s * fc.npix + pix);
+            const float3 L = rad.get((size_t)pix * fc.spp_chunk + s);
             P.x = P.x + L.x;
             P.y = P.y + L.y;
             P.z = P.z + L.z;
@@ -2062,10 +2026,10 @@ struct TileGrid {
 // Launch geometry of the split (trace / shade) path of large scenes.
 struct SplitGrids {
     int trace_p, trace_e, shadow, shade_p, shade_e, packet;
-    void (*ktp)(FrameConsts, SceneArgs, int, FastDiv, float2*, int32_t*, unsigned long long*, uint32_t*);
+    void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
-    void (*ktpk)(FrameConsts, SceneArgs, int, FastDiv, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
+    void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
@@ -2159,6 +2123,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         fc.first_sample = c * base.spp_chunk;
         fc.spp_chunk = base.spp_chunk;
         if (fc.first_sample + fc.spp_chunk > base.spp_total) fc.spp_chunk = base.spp_total - fc.first_sample;
+        fc.div_spp = FastDiv::make((uint32_t)fc.spp_chunk);
         const int np = npix * fc.spp_chunk;
         uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr + (size_t)cpc * c);
         uint32_t* qc = p.qctr.ptr + per_chunk * c;
@@ -2170,18 +2135,15 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             throw std::runtime_error("queue capacity exceeded (split path)");
         pr.begin(st, RR_K_PRIMARY);
         if (packets)
-            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, FastDiv::make((uint32_t)fc.spp_chunk),
-                                                               p.hits.ptr, p.spill.ptr, tc,
+            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc,
                                                                tot + camera_traced_slot(base.max_bounces));
         else
             G.ktp<<<clamp_grid(np, G.trace_p, kTraceBlock), kTraceBlock, 0, st>>>(
-                fc, sa, np, FastDiv::make((uint32_t)fc.spp_chunk), p.hits.ptr, p.spill.ptr, tc,
-                tot + camera_traced_slot(base.max_bounces));
+                fc, sa, np, p.hits.ptr, p.spill.ptr, tc, tot + camera_traced_slot(base.max_bounces));
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
-        k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, FastDiv::make((uint32_t)fc.spp_chunk), p.hits.ptr,
-                                                Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1], sq,
-                                                QueueOut{qpath(0), qshadow(0), cap_p});
+        k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1],
+                                                sq, QueueOut{qpath(0), qshadow(0), cap_p});
         pr.end(st);
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         for (int b = 0; b <= base.max_bounces; ++b) {
