@@ -1045,9 +1045,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
 // C5 / 02) are not coherent enough for it at all.
 // act: the lane has a ray; stk: this wave's kPacketStack LDS entries.
 constexpr int kPacketStack = 128;  // a node pushes <= 5: bounded by 5 x the hierarchy depth
-// kAnyHit: shadow rays; a lane whose ray met a triangle drops out of the
-// packet, which ends when no lane is left.
-template <bool kCount, bool kAnyHit = false>
+template <bool kCount>
 RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk, bool act,
                        float3 o, float3 d, float tmin, Hit& h, TravCount& cnt, uint32_t& dropped) {
     if (!__ballot(act)) return;
@@ -1071,10 +1069,6 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
                 if (kCount) ++cnt.tris;
                 leaf_test(tp, ti, sh, o, tmin, h);
             }
-        }
-        if (kAnyHit) {
-            if (h.idx >= 0) act = false;
-            if (!__ballot(act)) break;
         }
         // internal children some lane enters: the representative lane's nearest next
         uint32_t inner = 0;
@@ -1283,53 +1277,6 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
     if (kCount) {
         flush_counts(tc, 4, cnt.nodes, cnt.tris);
         flush_drops(tc, st.dropped);
-    }
-}
-
-// Bounce-0 shadow rays as packets (RR_SHADOW_PACKETS): the queue's chunks of
-// 64 positions (QueueMap::slot_t) hold one shading wave's shadow rays — the
-// samples of one or two pixels toward one light, nearly one ray — so a wave
-// walks them as one packet (packet_trace, any hit) with scalar node loads.
-template <bool kCount>
-__global__ __launch_bounds__(kBlock, kTraceWaves) void k_shadow_packet(SceneArgs sa, ShadowQueue sq, QueueIn qi,
-                                                                      Rad rad, unsigned long long* __restrict__ tc) {
-    __shared__ int stack_all[kWavesPerBlock * kPacketStack];
-    lds_int* stk = lds_slot(stack_all) + (threadIdx.x >> 6) * kPacketStack;
-    QueueMap qm;
-    qm.init(qi);
-    TravCount cnt;
-    uint32_t dropped = 0;
-    const int lane = threadIdx.x & 63;
-    const int npk = (qm.span + 63) / 64;
-    const int nw = gridDim.x * kWavesPerBlock;
-    for (int q = xcd_wave_rank(); q < npk; q += nw) {
-        const int m = q * 64 + lane;
-        const uint32_t i = qm.slot_t(m < qm.span ? m : qm.span - 1);  // all lanes (shuffles)
-        const bool valid = m < qm.span && i != kNoSlot;
-        float3 o = mk3(0.0f, 0.0f, 0.0f), d = mk3(0.0f, 0.0f, 1.0f);
-        float tmax = -1.0f;
-        if (valid) {
-            const float4 a = sq.o[i], b = sq.d[i];
-            o = xyz(a);
-            d = xyz(b);
-            tmax = b.w;
-        }
-        Hit h;
-        set_miss(h, tmax);
-        packet_trace<kCount, true>(sa.qnodes, sa.tris, stk, valid && sa.n_tris > 0, o, d, 0.0f, h, cnt, dropped);
-        if (valid && h.idx < 0) {
-            const int pid = f2i(sq.o[i].w);
-            const float4 c = sq.c[i];
-            float3 L = rad.get(pid);
-            L.x = L.x + c.x;
-            L.y = L.y + c.y;
-            L.z = L.z + c.z;
-            rad.put(pid, L);
-        }
-    }
-    if (kCount) {
-        flush_counts(tc, 4, cnt.nodes, cnt.tris);
-        flush_drops(tc, dropped);
     }
 }
 
@@ -2083,15 +2030,11 @@ struct SplitGrids {
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
     void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
-    void (*ktsp)(SceneArgs, ShadowQueue, QueueIn, Rad, unsigned long long*);                  // shadow packets
-    int shadow_packet;
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
         kts = count ? k_shadow_refill<true> : k_shadow_refill<false>;
         ktpk = count ? k_trace_primary_packet<true> : k_trace_primary_packet<false>;
-        ktsp = count ? k_shadow_packet<true> : k_shadow_packet<false>;
-        shadow_packet = grid_for(ktsp, 0);
         trace_p = grid_for(ktp, 0, kTraceBlock);
         trace_e = grid_for(kte, 0, kTraceBlock);
         shadow = grid_for(kts, 0, kTraceBlock);
@@ -2169,10 +2112,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
 #ifndef RR_CAM_PACKETS
 #define RR_CAM_PACKETS 2
 #endif
-    // bounce-0 shadow rays as packets (k_shadow_packet; A/B switch)
-#ifndef RR_SHADOW_PACKETS
-#define RR_SHADOW_PACKETS 0
-#endif
+
     const bool packets = RR_CAM_PACKETS == 2 || (RR_CAM_PACKETS && (long)base.n_tris * 2 <= (long)npix);
     // group counters: [chunk][bounce 0..max][path | shadow][kQGroups * kQStride]
     const size_t per_q = (size_t)kQGroups * kQStride;
@@ -2209,13 +2149,9 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         for (int b = 0; b <= base.max_bounces; ++b) {
             pr.begin(st, RR_K_SHADOW);
-            if (RR_SHADOW_PACKETS && b == 0)
-                G.ktsp<<<clamp_grid(np, G.shadow_packet), kBlock, 0, st>>>(
-                    sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, Rad{reinterpret_cast<float*>(p.rad.ptr)}, tc);
-            else
-                G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(
-                    sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, Rad{reinterpret_cast<float*>(p.rad.ptr)},
-                    p.spill.ptr, tc);
+            G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(
+                sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, Rad{reinterpret_cast<float*>(p.rad.ptr)},
+                p.spill.ptr, tc);
             pr.end(st);
             if (b == base.max_bounces) break;
             const int nb = b + 1;  // bounce being traced and shaded
