@@ -1307,7 +1307,9 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
             acc = film[pix];
             P = part[pix];
         }
-        for (int s = 0; s < fc.spp_chunk; ++s) {
+        // the pixel's records are contiguous (path index pixel-major): read
+        // four at a time as three float4 when the chunk allows it
+        auto add = [&](int s, float x, float y, float z) {
             const int gs = fc.first_sample + s;
             if (gs > 0 && (gs & (kFilmGroup - 1)) == 0) {  // close the group
                 acc.x = acc.x + P.x;
@@ -1315,10 +1317,25 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(FrameConsts fc, Rad rad,
                 acc.z = acc.z + P.z;
                 P = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
-            const float3 L = rad.get((size_t)pix * fc.spp_chunk + s);
-            P.x = P.x + L.x;
-            P.y = P.y + L.y;
-            P.z = P.z + L.z;
+            P.x = P.x + x;
+            P.y = P.y + y;
+            P.z = P.z + z;
+        };
+        const size_t r0 = (size_t)pix * fc.spp_chunk;
+        int s = 0;
+        if ((fc.spp_chunk & 3) == 0) {
+            const float4* q = reinterpret_cast<const float4*>(rad.p + 3 * r0);
+            for (; s < fc.spp_chunk; s += 4, q += 3) {
+                const float4 a = q[0], b = q[1], c = q[2];
+                add(s, a.x, a.y, a.z);
+                add(s + 1, a.w, b.x, b.y);
+                add(s + 2, b.z, b.w, c.x);
+                add(s + 3, c.y, c.z, c.w);
+            }
+        }
+        for (; s < fc.spp_chunk; ++s) {
+            const float3 L = rad.get(r0 + s);
+            add(s, L.x, L.y, L.z);
         }
         if (last_chunk) {
             acc.x = acc.x + P.x;
