@@ -502,7 +502,9 @@ __global__ __launch_bounds__(kBlock) void k_qw_emit(const int32_t* __restrict__ 
     o.org = make_float4(org[0], org[1], org[2], i2f((int)(eb | inner << 24)));
     o.a = make_uint4((uint32_t)inner_base, (uint32_t)tri_base, w[0], w[1]);
     o.b = make_uint4(w[2], w[3], w[4], w[5]);
-    o.c = make_uint4(w[6], w[7], w[8], (1u << S.m) - 1u);  // used slots
+    // used slots | the largest exponent byte << 8 (q6_planes' margin)
+    const uint32_t emax = max(max(eb & 255u, (eb >> 8) & 255u), (eb >> 16) & 255u);
+    o.c = make_uint4(w[6], w[7], w[8], ((1u << S.m) - 1u) | emax << 8);
     out[idx] = o;
 }
 

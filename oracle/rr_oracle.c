@@ -479,7 +479,7 @@ static v3 rcp3(v3 d) {
  *   w5     position of the first leaf child's triangle (the others follow)
  *   w6..11 children 0..3: lo x, lo y, lo z, hi x, hi y, hi z (byte c = child c)
  *   w12..14 children 4, 5: (lo x, lo y), (lo z, hi x), (hi y, hi z) as byte pairs
- *   w15    mask of the used slots
+ *   w15    mask of the used slots | the largest exponent byte << 8
  * An unused slot has lo 255, hi 0 on every axis and its bit of w15 clear: its
  * box test always fails. */
 #define ORC_QW_MAX 6
@@ -511,7 +511,12 @@ static void q4_pack(const float lo[3][ORC_QW_MAX], const float hi[3][ORC_QW_MAX]
     o[3] = eb | inner << 24;
     o[4] = inner_base;
     o[5] = tri_base;
-    o[15] = (1u << used) - 1u;  /* used slots */
+    {   /* used slots | the largest exponent byte << 8 (rr_device.h q6_planes' margin) */
+        uint32_t emax = eb & 255u;
+        if (((eb >> 8) & 255u) > emax) emax = (eb >> 8) & 255u;
+        if (((eb >> 16) & 255u) > emax) emax = (eb >> 16) & 255u;
+        o[15] = ((1u << used) - 1u) | emax << 8;
+    }
 }
 
 /* BVH4 collapse of the BVH2 (PLOC, or Karras below 3 triangles), as
@@ -830,18 +835,18 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
         float sc[3], onr[3], ofr[3];
         int pos[3];
         /* rr_device.h q6_planes: the node's margin distance ORC_BOX_MARGIN (the
-         * largest |org - o| + 255 * 2^e over the axes) */
-        float dif[3], ext[3];
+         * largest |org - o| + 255 * 2^(the largest e)) */
+        float dif[3];
         for (int a = 0; a < 3; ++a) {
             float org;
             memcpy(&org, nd + a, sizeof org);
             const int e = (int)((nd[3] >> (8 * a)) & 255u) - 128;
             dif[a] = org - oo[a];
-            ext[a] = ldexpf(255.0f, e);
             sc[a] = ldexpf(iq[a], e);
         }
-        const float mrg = fmaxf(fmaxf(fabsf(dif[0]) + ext[0], fabsf(dif[1]) + ext[1]), fabsf(dif[2]) + ext[2]) *
-                          ORC_BOX_MARGIN * g_margin_scale;
+        const float M = ORC_BOX_MARGIN * g_margin_scale;
+        const float mrg = fmaf(fmaxf(fmaxf(fabsf(dif[0]), fabsf(dif[1])), fabsf(dif[2])), M,
+                               ldexpf(255.0f * M, (int)((nd[15] >> 8) & 255u) - 128));
         for (int a = 0; a < 3; ++a) {
             const float ma = mrg * fabsf(iq[a]);
             onr[a] = fmaf(dif[a], iq[a], -ma);
