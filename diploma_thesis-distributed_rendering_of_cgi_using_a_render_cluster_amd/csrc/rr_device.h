@@ -1076,11 +1076,7 @@ RR_HD float3 bsdf_eval_v(const Mat& m, FloatP lut, const BsdfView& vw, float3 N,
     // first entry by lut_at)
     const float cl1 = cosL + sqrt_rn(fmaf((1.0f - a2) * cosL, cosL, a2));
     const float q = a2 * den * den;
-#if RR_SHADE_RCP
-    const float r = rcp_any(3.14159265358979f * X * X * vw.cv1 * cl1);  // the bits of 1 / (...)
-#else
     const float r = 1.0f / (3.14159265358979f * X * X * vw.cv1 * cl1);
-#endif
     const float pdf_s = q * cl1 * r * 0.5f;                 // D G1(V) / (4 cosV)
     const float ks = m.spec_on ? q * cosL * r : 0.0f;       // D G1(V) G1(L) / (4 cosV cosL) * cosL
     const float fh = lut_at(lut, sqrt_rn(fmaf(0.5f, lv, 0.5f)));  // L.H = sqrt((1 + L.V) / 2)

@@ -395,11 +395,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
         sampled = bsdf_sample(m, lut, vw, N, wo, u_lobe, u_b1, u_b2, wi, f, pdf, glossy);
     }
     if (!sampled) return;
-#if RR_SHADE_RCP
-    const float k = rcp_any(pdf);  // f = f * cosL already; the bits of 1 / pdf
-#else
     const float k = 1.0f / pdf;  // f = f * cosL already
-#endif
     T = mk3(T.x * f.x * k, T.y * f.y * k, T.z * f.z * k);
     if (!(max3f(T) > 0.0f)) return;
     if (bounce >= kRrStartBounce) {
