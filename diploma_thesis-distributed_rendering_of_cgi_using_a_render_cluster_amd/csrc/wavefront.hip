@@ -1751,11 +1751,22 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
 }
 
 #if RR_TILES_TU
+// Waves per SIMD the register budget must admit: 4 (<= 128 VGPRs) for the
+// sample-group slices of a frame rendered alone, 5 (<= 96 VGPRs, 42 spill
+// slots) for the whole-tile units of frames that overlap a pending one — the
+// bench's pipelined frames: 04vs / 01 992 / 1,026 against 953 / 970 frames/s
+// at 4 (3 interleaved rounds of 40 frames), while a lone frame's slices ran
+// 1.181 / 1.151 against 1.144 / 1.140 ms; 6 waves (80 VGPRs) 710 frames/s,
+// 3 (137 VGPRs, no spill) 860.
 #ifndef RR_TILES_WAVES
-#define RR_TILES_WAVES 4  // waves per SIMD the register budget must admit (<= 128 VGPRs)
+#define RR_TILES_WAVES 4
+#endif
+#ifndef RR_TILES_WAVES_WHOLE
+#define RR_TILES_WAVES_WHOLE 5
 #endif
 template <bool kCount, bool kWhole>
-__global__ __launch_bounds__(kBlock, RR_TILES_WAVES) void k_tiles(FrameConsts fc, SceneArgs sa,
+__global__ __launch_bounds__(kBlock, kWhole ? RR_TILES_WAVES_WHOLE : RR_TILES_WAVES) void k_tiles(FrameConsts fc,
+                                                                                                 SceneArgs sa,
                                                                   uint32_t* __restrict__ tile_ctr,
                                                                   float4* __restrict__ film,
                                                                   const float* __restrict__ srgb,

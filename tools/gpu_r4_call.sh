@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU call: split-path re-tune on the pixel-major order: lane-refill
-# threshold 44 / 58 (main 52) and 7 waves per SIMD for the trace kernels.
+# Round-4 GPU call: k_tiles at 5 / 6 waves per SIMD against main's 4 (04vs /
+# 01, pipelined frames), two more rounds.
 mkdir -p gpurun_out
-timeout -k 10 480 python tools/ab_run.py --rounds 2 main rf44 rf58 w7 -- scenes/02_physics-standin.rrscene:90:64 scenes/03_physics-2-standin.rrscene:300:64 scenes/c5_synthetic-10m.rrscene:150:16 > gpurun_out/ab20.txt 2>&1
+timeout -k 10 400 python tools/ab_run.py --rounds 3 --frames 40 main tw5 tw6 -- scenes/04_very-simple-standin.rrscene:5:128 scenes/01_simple-animation.rrscene:20:128 > gpurun_out/ab22.txt 2>&1
