@@ -1157,13 +1157,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
 // and the bounce-0 shadow queue.
 // In path-index order (pixel-major), so the bounce-0 shadow rays and the
 // bounce-1 paths are queued with the samples of one pixel side by side.
-// Waves per SIMD of the shading kernels (A/B switch; 0: the compiler's choice,
-// 108-110 VGPRs, 4 waves).
-#ifndef RR_SHADE_WAVES
-#define RR_SHADE_WAVES 0
-#endif
-constexpr int kShadeWaves = RR_SHADE_WAVES > 0 ? RR_SHADE_WAVES : 1;
-__global__ __launch_bounds__(kBlock, kShadeWaves) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np,
+__global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np,
                                                           const float2* __restrict__ hits, Rad rad,
                                                           PathQueue out, ShadowQueue sq, QueueOut qo) {
     const GlobalView v = global_view(sa);
@@ -1218,7 +1212,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
 
 // Bounce b: shade from hits[slot], in the queue's time order (slot_t); appends
 // the next path queue and this bounce's shadow queue.
-__global__ __launch_bounds__(kBlock, kShadeWaves) void k_shade_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in,
+__global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in,
                                                          QueueIn qi, const float2* __restrict__ hits,
                                                          Rad rad, PathQueue out, ShadowQueue sq,
                                                          QueueOut qo) {

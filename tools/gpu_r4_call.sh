@@ -1,9 +1,5 @@
 #!/bin/bash
-# Round-4 GPU call: GPU tests, then k_tiles per-variant occupancy (main: whole
-# tiles at 5 waves, slices at 4) against both at 5 (tw5).
+# Round-4 GPU call: split-path shading kernels at 5 / 6 waves per SIMD against
+# the compiler's 4.
 mkdir -p gpurun_out
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4t_tests.log 2>&1
-rc=$?
-tail -3 gpurun_out/r4t_tests.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python tools/ab_run.py --rounds 3 --frames 40 main tw5 -- scenes/04_very-simple-standin.rrscene:5:128 scenes/01_simple-animation.rrscene:20:128 > gpurun_out/ab23.txt 2>&1
+timeout -k 10 400 python tools/ab_run.py --rounds 2 main sw5 sw6 -- scenes/02_physics-standin.rrscene:90:64 scenes/03_physics-2-standin.rrscene:300:64 scenes/c5_synthetic-10m.rrscene:150:16 > gpurun_out/ab24.txt 2>&1
