@@ -313,11 +313,7 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     // Russian roulette keeps dim0 + 6 (oracle/rr_oracle.c radiance)
     float u_light, u_lobe;
     rng2(key, dim0, u_light, u_lobe);
-    // the origin of the shadow and continuation rays, only where one is
-    // traced or queued: rays that leave a hull side (esc, LDS-resident scenes)
-    // meet nothing and never use it (04vs / 01: every camera hit on the cube)
-    float3 Po = P;
-    if (!esc) Po = offset_ray(P, N);
+    const float3 Po = offset_ray(P, N);
     // next-event estimation toward one uniformly chosen light
     if (fc.n_lights > 0) {
         int li = (int)(u_light * (float)fc.n_lights);
