@@ -1,9 +1,10 @@
 #!/bin/bash
-# Round-4 GPU call: full-frame parity of the lazy ray origin, then its A/B on
-# the k_tiles scenes (pipelined) against the previous commit (head tree).
+# Round-4 final check of the tree on the GPU box: the -m gpu suite, smoke()
+# and the default bench line.
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r4v_tests.log 2>&1
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4_final_tests.log 2>&1
 rc=$?
-tail -3 gpurun_out/r4v_tests.log
+tail -3 gpurun_out/r4_final_tests.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python tools/ab_run.py --rounds 3 --frames 40 main head -- scenes/04_very-simple-standin.rrscene:5:128 scenes/01_simple-animation.rrscene:20:128 > gpurun_out/ab25.txt 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4_final_smoke.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py > gpurun_out/r4_final_bench.json 2> gpurun_out/r4_final_bench.err
