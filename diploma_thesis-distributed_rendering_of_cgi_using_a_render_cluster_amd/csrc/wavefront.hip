@@ -948,6 +948,41 @@ struct QueueMap {
     }
 };
 
+// Queue records are written once and read by the next kernels. RR_NT_QUEUE
+// (A/B switch) bit 0: path-queue stores non-temporal; bit 1: non-temporal
+// loads where a kernel is a record's last reader; bit 2: shadow-queue origin
+// and direction stores non-temporal; bit 3: shadow contribution stores;
+// bit 4: hit record stores.
+#ifndef RR_NT_QUEUE
+#define RR_NT_QUEUE 13
+#endif
+template <int kBit>
+__device__ __forceinline__ void q_put(float4* p, float4 v) {
+    if constexpr ((RR_NT_QUEUE & kBit) != 0) {
+        const rr_f4v w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<rr_f4v*>(p));
+    } else {
+        *p = v;
+    }
+}
+__device__ __forceinline__ void hit_put(float2* p, float2 v) {
+    if constexpr ((RR_NT_QUEUE & 16) != 0) {
+        typedef float rr_f2v __attribute__((ext_vector_type(2)));
+        const rr_f2v w = {v.x, v.y};
+        __builtin_nontemporal_store(w, reinterpret_cast<rr_f2v*>(p));
+    } else {
+        *p = v;
+    }
+}
+__device__ __forceinline__ float4 q_last(const float4* p) {
+    if constexpr ((RR_NT_QUEUE & 2) != 0) {
+        const rr_f4v w = __builtin_nontemporal_load(reinterpret_cast<const rr_f4v*>(p));
+        return make_float4(w.x, w.y, w.z, w.w);
+    } else {
+        return *p;
+    }
+}
+
 // Grouped append: one atomicAdd per queue per wave on its group's counter.
 struct QueueOut {
     uint32_t* ctr_path;    // path queue group counters
@@ -970,15 +1005,15 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
     bs = g * qo.cap + (uint32_t)__shfl((int)bs, 0);
     if (so.cont) {
         const uint32_t s1 = bc + (uint32_t)__popcll(mc & below);
-        out.o[s1] = make_float4(so.o.x, so.o.y, so.o.z, i2f(pid));
-        out.d[s1] = make_float4(so.d.x, so.d.y, so.d.z, i2f((int)so.lob));
-        out.t[s1] = make_float4(so.T.x, so.T.y, so.T.z, so.esc ? 1.0f : 0.0f);
+        q_put<1>(out.o + s1, make_float4(so.o.x, so.o.y, so.o.z, i2f(pid)));
+        q_put<1>(out.d + s1, make_float4(so.d.x, so.d.y, so.d.z, i2f((int)so.lob)));
+        q_put<1>(out.t + s1, make_float4(so.T.x, so.T.y, so.T.z, so.esc ? 1.0f : 0.0f));
     }
     if (so.shadow) {
         const uint32_t s2 = bs + (uint32_t)__popcll(ms & below);
-        sq.o[s2] = make_float4(so.so.x, so.so.y, so.so.z, i2f(pid));
-        sq.d[s2] = make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist);
-        sq.c[s2] = make_float4(so.sc.x, so.sc.y, so.sc.z, so.esc ? 1.0f : 0.0f);
+        q_put<4>(sq.o + s2, make_float4(so.so.x, so.so.y, so.so.z, i2f(pid)));
+        q_put<4>(sq.d + s2, make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist));
+        q_put<8>(sq.c + s2, make_float4(so.sc.x, so.sc.y, so.sc.z, so.esc ? 1.0f : 0.0f));
     }
 }
 
@@ -1018,7 +1053,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
             camera_ray(fc, sa.filter, pix, key, o, d, tmin, tmax, &cull, &culled);
             n_traced += culled ? 0u : 1u;
         },
-        [&](int, uint32_t p, const Hit& h) { hits[p] = pack_hit(h); });
+        [&](int, uint32_t p, const Hit& h) { hit_put(hits + p, pack_hit(h)); });
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
     if ((threadIdx.x & 63) == 0 && n_traced) atomicAdd(traced, n_traced);
     if (kCount) {
@@ -1143,7 +1178,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         set_miss(h, tmax);
         packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt,
                              dropped);
-        if (valid) hits[p] = pack_hit(h);
+        if (valid) hit_put(hits + p, pack_hit(h));
     }
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
     if (lane == 0 && n_traced) atomicAdd(traced, n_traced);
@@ -1203,7 +1238,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
             tmin = 0.0f;
             tmax = kFltMax;
         },
-        [&](int, uint32_t i, const Hit& h) { hits[i] = pack_hit(h); });
+        [&](int, uint32_t i, const Hit& h) { hit_put(hits + i, pack_hit(h)); });
     if (kCount) {
         flush_counts(tc, 2, cnt.nodes, cnt.tris);
         flush_drops(tc, st.dropped);
@@ -1228,7 +1263,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
         so.cont = so.shadow = false;
         const uint32_t i = qm.slot_t(j < count ? j : count - 1);  // all lanes (shuffles)
         if (j < count && i != kNoSlot) {
-            const float4 a = in.o[i], b = in.d[i], c = in.t[i];
+            const float4 a = q_last(in.o + i), b = q_last(in.d + i), c = q_last(in.t + i);
             pid = f2i(a.w);
             const Hit h = unpack_hit(hits[i]);
             int pix, sl;
@@ -1267,7 +1302,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
         [&](int, uint32_t i, const Hit& h) {
             if (h.idx >= 0) return;
             const int pid = f2i(sq.o[i].w);
-            const float4 c = sq.c[i];
+            const float4 c = q_last(sq.c + i);
             float3 L = rad.get(pid);
             L.x = L.x + c.x;
             L.y = L.y + c.y;
