@@ -819,6 +819,46 @@ RR_D int xcd_wave_rank() {
     return __builtin_amdgcn_readfirstlane((xcd * (G >> 3) + min(xcd, G & 7) + (bx >> 3)) * kWpb +
                                           (int)(threadIdx.x >> 6));  // wave-uniform: SGPR
 }
+// Chunks of 64 positions (or packets) dealt to the waves of a trace kernel.
+// Static (ctr null): wave w of nw takes chunks w, w + nw, w + 2 nw, ... Dynamic:
+// the waves of one XCD take that XCD's share of the same order (chunks
+// r nw + first .. r nw + first + n - 1 of round r, where first / n are the
+// XCD's wave ranks) from a counter of its own, one atomic per chunk, so a wave
+// whose rays finished early takes more instead of idling while the chip
+// drains. Chunk ids of one wave still increase, and every id below the end
+// is taken by some wave of its XCD.
+template <int kWpb>
+struct ChunkDealer {
+    uint32_t* ctr;  // this XCD's counter (null: static)
+    int nw, w;      // waves of the launch, this wave's rank (xcd_wave_rank)
+    int first, n;   // ranks of this XCD's waves
+    int taken;      // static: chunks taken so far
+    RR_D void init(uint32_t* ctrs) {
+        const int G = (int)gridDim.x, xcd = (int)blockIdx.x & 7;
+        nw = G * kWpb;
+        w = xcd_wave_rank<kWpb>();
+        first = (xcd * (G >> 3) + min(xcd, G & 7)) * kWpb;
+        n = ((G >> 3) + (xcd < (G & 7) ? 1 : 0)) * kWpb;
+        ctr = ctrs ? ctrs + xcd * kQStride : nullptr;
+        taken = 0;
+    }
+    RR_D int take() {  // every lane of the wave (wave-uniform result)
+        if (!ctr) return (taken++) * nw + w;
+        uint32_t t = 0;
+        if ((threadIdx.x & 63) == 0) t = atomicAdd(ctr, 1u);
+        t = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)t, 0));
+        return (int)(t / (uint32_t)n) * nw + first + (int)(t % (uint32_t)n);
+    }
+};
+#ifndef RR_DYN_DEAL
+#define RR_DYN_DEAL 1
+#endif
+// Dynamic dealing's counters of a consumer of the grouped queue q: word `word`
+// of the first 8 group-counter lines (the producer uses word 0 of each).
+RR_D uint32_t* deal_ctrs(const uint32_t* q, int word) {
+    return RR_DYN_DEAL ? const_cast<uint32_t*>(q) + word : nullptr;
+}
+
 // Top of the quantised hierarchy in LDS for the trace kernels (Q6Nodes): the
 // first kTopNodes nodes (breadth-first numbering: the three top levels of the
 // 6-wide hierarchy and most of the fourth), copied by the block at launch.
@@ -847,14 +887,18 @@ RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
 // node). Blocks of kTraceBlock threads.
 template <typename TS, typename NodeP, typename TriP, typename Stack, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, Stack& st, TravCount& cnt,
-                       MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
+                       uint32_t* deal, MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const int nw = gridDim.x * kTraceWavesPerBlock;
-    const int w = xcd_wave_rank<kTraceWavesPerBlock>();
-    // position of the q-th ray of this wave's sequence
-    auto gpos = [&](int q) { return ((q >> 6) * nw + w) * 64 + (q & 63); };
+    ChunkDealer<kTraceWavesPerBlock> dl;
+    dl.init(deal);
+    // chunks holding this wave's sequence positions next .. next + 63: c0 the
+    // current one, c1 the one after (taken ahead, so its atomic is in flight
+    // while the wave traces)
+    int c0 = dl.take(), c1 = dl.take();
     int next = 0;  // wave-uniform cursor into this wave's sequence
+    // position of the q-th ray of this wave's sequence (next <= q < next + 64)
+    auto gpos = [&](int q) { return ((q >> 6) == (next >> 6) ? c0 : c1) * 64 + (q & 63); };
     TS ts;
     int j = -1;
     uint32_t js = 0;  // queue slot of ray j
@@ -876,7 +920,12 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, S
                     done(k, ks, ts.h);
                 }
             }
+            const int n0 = next;
             next += (int)__popcll(idle);
+            if ((next >> 6) != (n0 >> 6)) {
+                c0 = c1;
+                c1 = dl.take();
+            }
         }
         if (!__ballot(j >= 0)) {
             if (gpos(next) >= count) break;
@@ -1044,7 +1093,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, np, 0.0f, st, cnt, [](int k) { return (uint32_t)k; },
+        nodes, sa.tris, sa.n_tris, np, 0.0f, st, cnt, nullptr, [](int k) { return (uint32_t)k; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
             int pix, sl;
             path_of(fc, p, pix, sl);
@@ -1142,15 +1191,14 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
     }
 }
 
-// Camera paths as packets: a wave traces the 64 camera rays of one 8x8 pixel
-// tile (one sample) with packet_trace. Tiles are dealt to the waves as
-// trace_refill deals chunks (round-robin over the XCD-ordered waves).
+// Camera paths as packets: a wave traces 64 consecutive path indices (path_of:
+// the samples of one or two pixels) with packet_trace; packets are dealt to
+// the waves as trace_refill deals chunks (ChunkDealer, counters `deal`). An
+// 8x8 tile of one sample per packet (round 3) measured 16.1 / 20.6 ms per
+// 02 / 03 frame slice against 12.5 / 14.1.
 template <bool kCount>
-// A packet is 64 consecutive path indices (path_of: the samples of one or two
-// pixels); an 8x8 tile of one sample per packet (round 3) measured 16.1 / 20.6
-// ms per 02 / 03 frame slice against 12.5 / 14.1.
 __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
-    FrameConsts fc, SceneArgs sa, int np, float2* __restrict__ hits, int32_t* __restrict__,
+    FrameConsts fc, SceneArgs sa, int np, float2* __restrict__ hits, uint32_t* __restrict__ deal,
     unsigned long long* __restrict__ tc, uint32_t* __restrict__ traced) {
     __shared__ int stack_all[kWavesPerBlock * kPacketStack];
     lds_int* stk = lds_slot(stack_all) + (threadIdx.x >> 6) * kPacketStack;
@@ -1158,9 +1206,11 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     const int lane = threadIdx.x & 63;
     const int npk = (np + 63) / 64;
-    const int nw = gridDim.x * kWavesPerBlock;
+    ChunkDealer<kWavesPerBlock> dl;
+    dl.init(deal);
     uint32_t n_traced = 0, dropped = 0;
-    for (int q = xcd_wave_rank(); q < npk; q += nw) {
+    for (int q = dl.take(); q < npk;) {
+        const int qn = dl.take();  // the next packet, taken while this one traces
         const int p = q * 64 + lane;
         const bool valid = p < np;
         int pix, sl;
@@ -1179,6 +1229,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt,
                              dropped);
         if (valid) hit_put(hits + p, pack_hit(h));
+        q = qn;
     }
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
     if (lane == 0 && n_traced) atomicAdd(traced, n_traced);
@@ -1231,7 +1282,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, 0.0f, st, cnt, [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, 0.0f, st, cnt, deal_ctrs(qi.ctr, 1), [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
@@ -1291,7 +1342,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, 0.0f, st, cnt, [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, 0.0f, st, cnt, deal_ctrs(qi.ctr, 1), [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
@@ -2092,7 +2143,7 @@ struct SplitGrids {
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
-    void (*ktpk)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);  // packets
+    void (*ktpk)(FrameConsts, SceneArgs, int, float2*, uint32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
@@ -2118,6 +2169,9 @@ int accum_grid() {
     static const int g = resident_grid(k_accumulate);
     return g;
 }
+// Host side of deal_ctrs: the camera packets deal from word 2 of the bounce-0
+// path queue's counter lines (written by k_shade_primary after them, word 0).
+inline uint32_t* deal_host(uint32_t* q, int word) { return RR_DYN_DEAL ? q + word : nullptr; }
 inline int clamp_grid(long work, int resident, int block = kBlock) {
     const long g = (work + block - 1) / block;
     return (int)std::max<long>(1, std::min<long>(g, resident));
@@ -2199,7 +2253,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             throw std::runtime_error("queue capacity exceeded (split path)");
         pr.begin(st, RR_K_PRIMARY);
         if (packets)
-            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr, tc,
+            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, deal_host(qpath(0), 2), tc,
                                                                tot + camera_traced_slot(base.max_bounces));
         else
             G.ktp<<<clamp_grid(np, G.trace_p, kTraceBlock), kTraceBlock, 0, st>>>(
