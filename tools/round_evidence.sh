@@ -5,6 +5,7 @@
 # Everything lands in gpurun_out/; tools/collect_evidence.sh copies it.
 #   tools/round_evidence.sh r3 a   # -m gpu tests, smoke, 04vs (+ serial), 01, 02
 #   tools/round_evidence.sh r3 b   # 03, c5
+#   tools/round_evidence.sh r3 c   # the split-path workloads 02, 03, c5 again
 tag=${1:-r1}
 part=${2:-a}
 S=tools/gpu_steps.sh
@@ -25,6 +26,13 @@ if [ "$part" == "a" ]; then
         $S 300 python bench.py --workload $wl > gpurun_out/ev/bench_$wl.json || exit $?
     done
     $S 200 python bench.py --serial --no-cpu-baseline > gpurun_out/ev/bench_04vs_serial.json || exit $?
+elif [ "$part" == "c" ]; then
+    prof 02 ${tag}_02 02
+    prof 03 ${tag}_03 03
+    prof c5 ${tag}_c5 c5 "--spp 64"
+    for wl in 02 03 c5; do
+        $S 400 python bench.py --workload $wl > gpurun_out/ev/bench_$wl.json || exit $?
+    done
 else
     prof 03 ${tag}_03 03
     prof c5 ${tag}_c5 c5 "--spp 64"
