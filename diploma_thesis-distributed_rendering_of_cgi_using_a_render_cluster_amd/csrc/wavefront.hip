@@ -799,8 +799,9 @@ constexpr int kQStride = 32;   // words between group counters (128 B)
 // map(k) -> slot is called by every lane of the wave (converged: QueueMap
 // shuffles); ray_of(slot, ...) and done(k, slot, hit) per lane.
 // TS: TravStateQ6<kAnyHit, kCount> (quantised 6-wide hierarchy) or TravState (BVH2).
-// Positions 0..count-1 are dealt to the waves in chunks of 64, round-robin
-// (wave w: chunks w, w + waves, ...), so at any time the rays in flight on the
+// Positions 0..count-1 are dealt to the waves in chunks of 64 in round-robin
+// order (ChunkDealer: each XCD's waves take the XCD's share of that order from
+// a counter of their own), so at any time the rays in flight on the
 // whole chip come from one window of about 64 x waves positions: for camera
 // rays one band of the image, for queued rays the entries the producer
 // kernel appended at about the same time (QueueMap::slot_t). Rays of one
