@@ -781,10 +781,11 @@ constexpr int kTraceWaves = RR_TRACE_WAVES;
 // to the blocks' stacks instead of eight, and the top can be four times deeper
 // (512 nodes); measured against 256-thread blocks with 128 top nodes (per
 // frame slice, 02 / 03 at 64 spp, C5 at 16 spp): 115.4 / 128.4 / 103.0 against
-// 115.5 / 129.1 / 103.2 ms, and 1024 with 128 nodes the same — the nodes
-// between 128 and 512 come from L2 about as fast. 256 stays.
+// 115.5 / 129.1 / 103.2 ms with the static deal, and 1024 with 128 nodes the
+// same; with the dynamic deal (ChunkDealer) 84.2 / 89.8 / 73.7 against
+// 84.8 / 90.2 / 74.5 ms (means of two rounds), so 1024.
 #ifndef RR_TRACE_BLOCK
-#define RR_TRACE_BLOCK 256
+#define RR_TRACE_BLOCK 1024
 #endif
 constexpr int kTraceBlock = RR_TRACE_BLOCK;
 constexpr int kTraceWavesPerBlock = kTraceBlock / 64;
