@@ -188,6 +188,50 @@ def pmc_kernels(path: str | None) -> dict:
         return json.load(fh)["kernels"]
 
 
+# kernels reported one by one in kernels_pmc (BASELINE north star: achieved HBM
+# GB/s of the traversal and shading kernels, occupancy), in frame order
+PMC_KERNELS = ("k_trace_primary_packet", "k_trace_primary", "k_shade_primary", "k_shadow_refill", "k_trace_extend",
+               "k_shade_extend", "k_accumulate", "k_tiles")
+
+
+def pmc_kernel_block(ks: dict, src: str | None) -> dict:
+    """Per-kernel PMC figures of the path's traversal and shading kernels (the
+    timed instantiation, not the counting one): HBM GB/s = PMC bytes per launch
+    (FETCH_SIZE x fetch_scale + WRITE_SIZE) over that pass's own mean dispatch
+    time, its fraction of the 8 TB/s peak, L2 hit rate, wait_frac = SQ_WAIT_ANY /
+    SQ_WAVE_CYCLES, valu_lane_util (active lanes per VALU instruction), wave
+    life = a wave's mean lifetime over the dispatch (4 x SQ_WAVE_CYCLES / SQ_WAVES
+    over GRBM_GUI_ACTIVE / 8; how full the persistent grid stays), occupancy =
+    mean resident waves per SIMD (4 x SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8) /
+    1024 SIMDs)."""
+    out = {}
+    for name in PMC_KERNELS:
+        for k, e in ks.items():
+            if k.split("<")[0] != name:
+                continue
+            targs = k.split("<")[1].rstrip(">").split(",") if "<" in k else []
+            if targs and targs[0] != "false":
+                continue  # the counting instantiation
+            ms = e.get("pmc_pass_avg_ms")
+            row = {"launches": e.get("launches")}
+            if ms:
+                gbs = e["traffic_bytes"] / (ms * 1e-3) / 1e9
+                row.update({"pmc_pass_avg_ms": round(ms, 4), "hbm_gbs": round(gbs, 1),
+                            "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)})
+            row["traffic_bytes"] = round(e["traffic_bytes"])
+            for f in ("l2_hit_rate", "wait_frac", "valu_lane_util"):
+                if f in e:
+                    row[f] = round(e[f], 3)
+            gr, wc, nw = e.get("GRBM_GUI_ACTIVE"), e.get("SQ_WAVE_CYCLES"), e.get("SQ_WAVES")
+            if gr and wc and nw:
+                span = gr / 8.0
+                row["wave_life_frac"] = round(4.0 * wc / nw / span, 3)
+                row["occupancy_waves_per_simd"] = round(4.0 * wc / span / SIMDS, 2)
+            out[k] = row
+    return {"source": src, "timing": "each kernel's own mean dispatch time in the PMC pass (profiler-serialised)",
+            "kernels": out} if out else {}
+
+
 def pmc_entry(ks: dict, cls: str, variant: str | None = None):
     """(name, entry) of the class's timed kernel (not the counting
     instantiation) in a PMC summary: `variant` = the template arguments after
@@ -589,9 +633,9 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=No
         return out
     per_s = lambda b: b / launches_frame / (avg_ms * 1e-3) / 1e9  # noqa: E731
     _, e = pmc_entry(ks, cls)
-    hbm = {"hbm_algorithmic_gbs": round(per_s(survey_frame if split else bytes_frame), 2),
-           "hbm_compulsory_gbs": round(per_s(bytes_frame), 2),
+    hbm = {"hbm_compulsory_gbs": round(per_s(bytes_frame), 2),
            "hbm_survey_formula_gbs": round(per_s(survey_frame), 2),
+           "frac_survey_formula": round(per_s(survey_frame) / HBM_PEAK_GBS, 4),
            "traffic": round(e["traffic_bytes"]) if e else None,
            "traffic_gbs": round(e["traffic_bytes"] / (avg_ms * 1e-3) / 1e9, 1) if e else None,
            "traffic_source": src if e else None,
@@ -604,24 +648,30 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=No
         hbm["fetch_scale"] = e.get("fetch_scale", 2.0)
     base = {"kernel": cls, "avg_launch_ms": round(avg_ms, 4), "launches_per_frame": launches_frame,
             "bytes_per_launch_algorithmic": round((survey_frame if split else bytes_frame) / launches_frame)}
-    lat = {k: round(e[k], 3) for k in ("l2_hit_rate", "wait_frac") if e and k in e}
+    lat = {k: round(e[k], 3) for k in ("l2_hit_rate", "wait_frac", "valu_lane_util") if e and k in e}
+    if e is None:  # no PMC summary for this workload: the survey formula, flagged
+        ach = per_s(survey_frame)
+        return {**base, "bound": "unmeasured", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), **hbm,
+                "note": "no PMC summary: achieved = SURVEY 8(d) algorithmic bytes per launch / launch time, which "
+                        "prices every node visit and triangle test as HBM traffic (an upper bound, not a measurement)"}
+    # the bound from the counters: the PMC HBM rate against the peak, and how
+    # much of a wave's life it waits (SQ_WAIT_ANY / SQ_WAVE_CYCLES). Below half
+    # the peak with waves waiting more than half their lives, the kernel is
+    # bound by the latency of its gathers (cache hits included), not bandwidth.
+    ach = e["traffic_bytes"] / (avg_ms * 1e-3) / 1e9
+    wf = e.get("wait_frac")
+    bound = "latency" if (ach < 0.5 * HBM_PEAK_GBS and wf is not None and wf > 0.5) else "hbm"
     resident = n * (64.0 + 48.0) < MALL_BYTES  # hierarchy + triangles fit in the 256 MB MALL
-    if resident and e is not None:
-        ach = e["traffic_bytes"] / (avg_ms * 1e-3) / 1e9
-        return {**base, "bound": "latency", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), **lat, **hbm,
-                "note": "hierarchy + triangles fit in L2/MALL: the kernel waits on cache-hit latency, not HBM "
-                        "bandwidth (l2_hit_rate, wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES from the PMC passes); "
-                        "achieved / frac are its PMC HBM rate (FETCH_SIZE x fetch_scale + WRITE_SIZE per launch / "
-                        "launch time; fetch_scale 1 for these 64 B gathers per tools/fetch_probe.hip) for reference "
-                        "only"}
-    ach = per_s(survey_frame)
-    return {**base, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    return {**base, "bound": bound, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), **lat, **hbm,
-            "note": "hierarchy above MALL: achieved = SURVEY 8(d) algorithmic bytes (64 B per node visit, 48 B per "
-                    "triangle test + ray/hit stream) per launch / launch time; traffic = PMC HBM bytes per launch "
-                    "(FETCH_SIZE x fetch_scale, 1 for these 64 B gathers per tools/fetch_probe.hip, + WRITE_SIZE; "
-                    "FETCH_SIZE counts Infinity-Cache hits, so it is an upper bound on HBM reads)"}
+            "scene_fits_mall": resident,
+            "note": "achieved = PMC HBM bytes per launch (FETCH_SIZE x fetch_scale, 1 for these 64 B gathers per "
+                    "tools/fetch_probe.hip, + WRITE_SIZE; FETCH_SIZE counts Infinity-Cache hits, so an upper "
+                    "bound on HBM reads) / the bench's launch time; bound = latency when that is below half the "
+                    "peak and waves wait more than half their lives (wait_frac), else hbm; frac_survey_formula = "
+                    "SURVEY 8(d)'s algorithmic bytes (64 B per node visit, 48 B per triangle test + ray/hit "
+                    "stream, every one priced as HBM traffic) over the same time"}
 
 
 def main():
@@ -705,7 +755,8 @@ def main():
         runner.render_frames(job, [frame_of(w) for w in range(args.warmup)])
     kernel_ms = [0.0] * 8
     launches = [0] * 8
-    rays = {"camera": 0, "camera_traced": 0, "extension": 0, "shadow": 0}
+    rays = {"camera": 0, "camera_traced": 0, "extension": 0, "extension_escaped": 0, "shadow": 0,
+            "shadow_escaped": 0}
     substituted = []
     tile_modes = {"whole": 0, "sliced": 0}
 
@@ -717,6 +768,8 @@ def main():
         rays["camera_traced"] += st.camera_rays_traced
         rays["extension"] += st.extension_rays
         rays["shadow"] += st.shadow_rays
+        rays["extension_escaped"] += st.extension_rays_escaped
+        rays["shadow_escaped"] += st.shadow_rays_escaped
         substituted.append(st.view_transform_substituted)
         if st.tile_slices == 1:
             tile_modes["whole"] += 1
@@ -812,7 +865,15 @@ def main():
                                 f"{os.environ.get('OMP_NUM_THREADS')} of {usable} usable"}
             except Exception as e:  # baseline is reported, never the target
                 cpu = {"value": None, "unit": "frames/s", "error": str(e)}
-        traced = rays["camera_traced"] + rays["extension"] + rays["shadow"]
+        # rays that entered a traversal: escaped continuations / shadow rays
+        # (k_tiles' hull rule) are spawned and counted, but never walk a node
+        traced = (rays["camera_traced"] + rays["extension"] - rays["extension_escaped"] + rays["shadow"]
+                  - rays["shadow_escaped"])
+        spawned = rays["camera_traced"] + rays["extension"] + rays["shadow"]
+        wl_key = "" if args.workload == "04vs" else f"_{args.workload}"
+        pmc_path = args.pmc_summary or newest_profile("%s_pmc" + wl_key + ".json")
+        kernels_pmc = pmc_kernel_block(pmc_kernels(pmc_path),
+                                       os.path.relpath(pmc_path, ROOT) if pmc_path else None)
         result = {
             "metric": wl["metric"], "value": round(value, 4), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
@@ -832,10 +893,17 @@ def main():
             "mrays_per_s_per_gpu_kernel_time": (
                 round(traced / args.steps / (sum(roof_ms) / max(roof_steps, 1) * 1e-3) / 1e6, 1)
                 if sum(roof_ms) > 0 else None),
-            "rays_per_frame": {k: v // max(args.steps, 1) for k, v in rays.items()},
+            "mrays_spawned_per_s_per_gpu": round(spawned / elapsed / 1e6, 1),
+            "rays_per_frame": {**{k: v // max(args.steps, 1) for k, v in rays.items()},
+                               "traversed": traced // max(args.steps, 1)},
             "rays_note": "camera = W x H x spp samples; camera_traced = those tested against a triangle (the rest "
                          "lie outside the scene's screen rectangle or meet no triangle of their tile and are "
-                         "resolved as background without a ray); mrays_per_s_per_gpu counts traced rays only",
+                         "resolved as background without a ray); extension / shadow = continuation / NEE shadow "
+                         "rays spawned, of which *_escaped left a hull side of their triangle (every vertex of the "
+                         "scene behind that side's plane: they meet nothing) and were resolved without a traversal; "
+                         "traversed = camera_traced + extension + shadow - the escaped ones. mrays_per_s_per_gpu "
+                         "counts traversed rays only; mrays_spawned_per_s_per_gpu counts the escaped ones too",
+            "kernels_pmc": kernels_pmc,
             "whole_job_ceiling_frames_s": dispatch_ceiling(job.to_dict(), world),
             "value_under_reference_master_max": round(min(value, dispatch_ceiling(job.to_dict(), world)["value"]), 4),
             "device_ms_per_frame": round(sum(roof_ms) / max(roof_steps, 1), 3),

@@ -206,10 +206,9 @@ constexpr int kUploadMax = 720;
 // RR_FLAG_COUNT_TRAVERSAL words: [0..5] traversal totals (nodes, triangles per
 // class); k_tiles' counting launch: [6] shader-clock ticks and [7] real-time
 // ticks after the scene staging, [8] waves, [9] real-time ticks from entry,
-// [10] ~first entry, [11] last end (rr_api.cpp fill_stats); every counting
-// launch: [12] traversal-stack pushes dropped for want of room
-constexpr int kTravDropWord = 12;
-constexpr int kTravWords = 13;
+// [10] ~first entry, [11] last end (rr_api.cpp fill_stats). (Traversal-stack
+// drops are counted in every frame, in the chunk counters: drops_slot.)
+constexpr int kTravWords = 12;
 struct UploadSeg {
     float* dst;
     int n;
@@ -262,9 +261,17 @@ size_t jpeg_stream_max_bytes(int W, int H);
 void jpeg_encode_device(const uint8_t* d_rgba, int W, int H, const float* d_tab, const uint32_t* d_huff,
                         int16_t* d_coeffs, JpegDevBufs& b, uint8_t* host_out, hipStream_t st);
 
+// Per chunk: one pair per bounce b = 0..max_bounces {paths entering b+1,
+// shadow rays of b}, one pair of slack, then the words below.
 int counters_per_chunk(int max_bounces);
 // Word of a chunk's counters holding the camera rays traced (counters_per_chunk).
 RR_HD int camera_traced_slot(int max_bounces) { return 2 * (max_bounces + 2); }
+// Traversal-stack pushes dropped for want of room (every frame; a dropped push
+// is a missed subtree, rr_frame_stats.stack_drops).
+RR_HD int drops_slot(int max_bounces) { return 2 * (max_bounces + 2) + 1; }
+// k_tiles: continuations / shadow rays that leave a hull side of their
+// triangle and so are resolved without a traversal (hull_flags); two words.
+RR_HD int escaped_slot(int max_bounces) { return 2 * (max_bounces + 2) + 2; }
 int device_cu_count();
 
 }  // namespace rr

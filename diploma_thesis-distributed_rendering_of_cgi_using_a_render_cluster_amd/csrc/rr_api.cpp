@@ -645,10 +645,14 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
     st->camera_rays = (uint64_t)fs.W * fs.H * fs.spp;
     st->view_transform = fs.view_transform;
     const int cpc = counters_per_chunk(fs.max_bounces);
+    uint64_t drops = 0;
     for (int c = 0; c < r.chunks; ++c) {
         // pair b: {paths entering bounce b+1, shadow rays of bounce b} (wavefront.hip)
         const int32_t* q = &r.counters[(size_t)cpc * c];
         st->camera_rays_traced += (uint64_t)(uint32_t)q[camera_traced_slot(fs.max_bounces)];
+        drops += (uint64_t)(uint32_t)q[drops_slot(fs.max_bounces)];
+        st->extension_rays_escaped += (uint64_t)(uint32_t)q[escaped_slot(fs.max_bounces)];
+        st->shadow_rays_escaped += (uint64_t)(uint32_t)q[escaped_slot(fs.max_bounces) + 1];
         for (int b = 0; b < fs.max_bounces; ++b) st->extension_rays += (uint64_t)q[2 * b];
         for (int b = 0; b <= fs.max_bounces; ++b) st->shadow_rays += (uint64_t)q[2 * b + 1];
         st->primary_continued += (uint64_t)q[0];
@@ -669,7 +673,7 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
         const unsigned long long t0 = ~w[10], t1 = w[11];
         st->kernel_wave_fill = (w[8] && t1 > t0) ? (double)w[9] / (double)w[8] / (double)(t1 - t0) : 0.0;
     }
-    st->stack_drops = (int32_t)std::min<unsigned long long>(r.trav[kTravDropWord], 0x7fffffffull);
+    st->stack_drops = (int32_t)std::min<uint64_t>(drops, 0x7fffffffull);
     st->build_ms = r.rebuilt ? r.build_ms : 0.0;
     st->trace_ms = r.trace_ms;
     st->readback_ms = r.readback_ms;
@@ -1242,16 +1246,16 @@ int rr_debug_qbvh(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* nq, int32_t* c
 int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int32_t n, const float* rays,
                    float* hits, int32_t* prims, uint8_t* occluded) {
     if (!c || !s || n < 0 || (n > 0 && !rays)) return fail(RR_EINVAL, "bad arguments");
-    if (bvh_width < 0 || bvh_width == 1 || bvh_width > 4)
-        return fail(RR_EINVAL, "hierarchy must be 0 (frame's), 2 (LBVH), 3 (PLOC) or 4 (BVH4)");
+    if (bvh_width < 0 || bvh_width == 1 || bvh_width > 5)
+        return fail(RR_EINVAL, "hierarchy must be 0 (frame's), 2 (LBVH), 3 (PLOC), 4 (6-wide) or 5 (6-wide, packets)");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
         PinnedBuf staging;
-        const int hier = bvh_width ? bvh_width : frame_hier_of(s, fs);
+        const int hier = bvh_width == 5 ? kHierQWide : (bvh_width ? bvh_width : frame_hier_of(s, fs));
         prepare_frame(c, s, fs, staging, hier);
-        const int width = hier == kHierQWide ? 4 : 2;
+        const int width = bvh_width == 5 ? 5 : (hier == kHierQWide ? 4 : 2);
         hipStream_t st = c->stream;
         DevBuf<float4> dr, dh;
         DevBuf<int32_t> dp;

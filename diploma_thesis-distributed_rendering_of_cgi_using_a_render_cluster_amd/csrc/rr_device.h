@@ -610,19 +610,20 @@ struct TravStackT {
     int* spill;     // spill_base: lane slot spill[(sp - kLdsStack) * stride + global thread]
     int spill_stride;
     int sp;
-    // pushes dropped for want of room (the counting kernels report them:
-    // rr_frame_stats / kTravWords, tests assert 0 on every bench scene)
-    uint32_t dropped = 0;
+    // the frame's drop counter (device.hpp drops_slot; null: not counted)
+    uint32_t* drops;
     // A push beyond kLdsStack + kSpillStack entries is dropped (a missed
-    // subtree); the oracle's stack has the same capacity and the same rule
-    // (ORC_MAXDEPTH) and counts its drops too (orc_stack_drops).
+    // subtree) and counted at once with an atomic on the frame's drop counter
+    // (no register stays live for it; rr_frame_stats.stack_drops, tests assert
+    // 0 on every bench scene); the oracle's stack has the same capacity and the
+    // same rule (ORC_MAXDEPTH) and counts its drops too (orc_stack_drops).
     RR_D void push(int x) {
         if (sp < kLdsStack) {
             lds[sp * kB + (int)threadIdx.x] = x;
         } else if (sp < kLdsStack + kSpillStack) {
             spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)] = x;
         } else {
-            ++dropped;
+            if (drops) atomicAdd(drops, 1u);
             return;
         }
         ++sp;

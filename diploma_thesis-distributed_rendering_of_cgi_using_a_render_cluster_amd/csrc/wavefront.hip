@@ -429,12 +429,6 @@ __device__ __forceinline__ void flush_counts(unsigned long long* __restrict__ tc
         atomicAdd(&tc[slot + 1], b);
     }
 }
-// Traversal-stack pushes dropped for want of room (TravStack::push, the packet
-// stack), summed into word kTravDropWord; a dropped push is a missed subtree.
-__device__ __forceinline__ void flush_drops(unsigned long long* __restrict__ tc, uint32_t n) {
-    for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off);
-    if ((threadIdx.x & 63) == 0 && n) atomicAdd(&tc[kTravDropWord], (unsigned long long)n);
-}
 
 }  // namespace
 struct SceneArgs {
@@ -885,10 +879,11 @@ RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
     __syncthreads();
     return Q6Nodes{sa.qnodes, top, n};
 }
-// r: TravState's scene radius (unused by TravStateQ6, whose margins are per
-// node). Blocks of kTraceBlock threads.
+// TS: TravStateQ6 (its box margins are per node; the BVH2 walk TravState needs
+// the scene radius in start() and so does not compile here). Blocks of
+// kTraceBlock threads.
 template <typename TS, typename NodeP, typename TriP, typename Stack, typename MapFn, typename RayFn, typename DoneFn>
-RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, Stack& st, TravCount& cnt,
+RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st, TravCount& cnt,
                        uint32_t* deal, MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -913,7 +908,7 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, float r, S
                 float3 o, d;
                 float tmin, tmax;
                 ray_of(ks, o, d, tmin, tmax);
-                ts.start(o, d, tmin, tmax, r);
+                ts.start(o, d, tmin, tmax);
                 st.sp = 0;
                 if (n_tris > 0) {
                     j = k;
@@ -1086,16 +1081,16 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
                                                                           float2* __restrict__ hits,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc,
-                                                                          uint32_t* __restrict__ traced) {
+                                                                          uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
-    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
+    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, np, 0.0f, st, cnt, nullptr, [](int k) { return (uint32_t)k; },
+        nodes, sa.tris, sa.n_tris, np, st, cnt, nullptr, [](int k) { return (uint32_t)k; },
         [&](uint32_t p, float3& o, float3& d, float& tmin, float& tmax) {
             int pix, sl;
             path_of(fc, p, pix, sl);
@@ -1106,11 +1101,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
         },
         [&](int, uint32_t p, const Hit& h) { hit_put(hits + p, pack_hit(h)); });
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
-    if ((threadIdx.x & 63) == 0 && n_traced) atomicAdd(traced, n_traced);
-    if (kCount) {
-        flush_counts(tc, 0, cnt.nodes, cnt.tris);
-        flush_drops(tc, st.dropped);
-    }
+    if ((threadIdx.x & 63) == 0 && n_traced) atomicAdd(tail, n_traced);
+    if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
 }
 
 // Packet traversal (camera rays of the split path, render_split decides): one wave walks the quantised BVH4 for the rays of its 64
@@ -1129,11 +1121,19 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
 // early: C5, about one triangle per pixel, 23.6 -> 33.5 ms at 16 spp; and the
 // shadow rays of camera hits (per-lane 39.7 / 46.8 ms, packets 121 / 86 ms on
 // C5 / 02) are not coherent enough for it at all.
-// act: the lane has a ray; stk: this wave's kPacketStack LDS entries.
-constexpr int kPacketStack = 128;  // a node pushes <= 5: bounded by 5 x the hierarchy depth
-template <bool kCount>
-RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk, bool act,
-                       float3 o, float3 d, float tmin, Hit& h, TravCount& cnt, uint32_t& dropped) {
+// act: the lane has a ray; stk: this wave's kStack LDS entries, gstk: its
+// kPacketSpill further entries in HBM (the per-lane traversal stacks' spill
+// area, which no other kernel uses while the packets trace: the stack's tail
+// of a deep hierarchy), drops: the frame's drop counter (null: not counted).
+// The stack pointer is wave-uniform, so both parts take one address per push.
+// A push beyond both parts (a hierarchy some 880 levels deep) is dropped and
+// counted at once.
+constexpr int kPacketStack = 128;             // a node pushes <= 5: about 25 levels of the 6-wide hierarchy in LDS
+constexpr int kPacketSpill = kSpillStack * 64;  // per wave in HBM (DevPaths::spill holds kSpillStack per lane)
+template <bool kCount, int kStack = kPacketStack>
+RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk,
+                       int* __restrict__ gstk, uint32_t* __restrict__ drops, bool act, float3 o, float3 d, float tmin,
+                       Hit& h, TravCount& cnt) {
     if (!__ballot(act)) return;
     const float3 iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
     const Shear sh = make_shear(d);
@@ -1163,7 +1163,8 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
             if (((imask >> c) & 1u) && __ballot((hm >> c) & 1u)) inner |= 1u << c;
         if (!inner) {
             if (sp == 0) break;
-            node = __builtin_amdgcn_readfirstlane(stk[--sp]);
+            --sp;
+            node = __builtin_amdgcn_readfirstlane(sp < kStack ? stk[sp] : gstk[sp - kStack]);
             continue;
         }
         const uint64_t any = __ballot(hm != 0u);
@@ -1186,8 +1187,15 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
 #pragma unroll
         for (int c = kQWidth - 1; c >= 0; --c)
             if (c != best && ((inner >> c) & 1u)) {
-                if (sp < kPacketStack) stk[sp++] = base + __builtin_popcount(imask & ((1u << c) - 1u));
-                else ++dropped;  // a missed subtree: reported by the counting pass, tests assert 0
+                const int x = base + __builtin_popcount(imask & ((1u << c) - 1u));
+                if (sp < kStack) {
+                    stk[sp++] = x;
+                } else if (sp < kStack + kPacketSpill) {
+                    gstk[sp - kStack] = x;
+                    ++sp;
+                } else if (drops && (threadIdx.x & 63) == 0) {
+                    atomicAdd(drops, 1u);  // a missed subtree
+                }
             }
         node = __builtin_amdgcn_readfirstlane(base + __builtin_popcount(imask & ((1u << best) - 1u)));
     }
@@ -1201,16 +1209,17 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
 template <bool kCount>
 __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
     FrameConsts fc, SceneArgs sa, int np, float2* __restrict__ hits, uint32_t* __restrict__ deal,
-    unsigned long long* __restrict__ tc, uint32_t* __restrict__ traced) {
+    int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, uint32_t* __restrict__ tail) {
     __shared__ int stack_all[kWavesPerBlock * kPacketStack];
     lds_int* stk = lds_slot(stack_all) + (threadIdx.x >> 6) * kPacketStack;
+    int* const gstk = spill + (size_t)wave_id() * kPacketSpill;
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     const int lane = threadIdx.x & 63;
     const int npk = (np + 63) / 64;
     ChunkDealer<kWavesPerBlock> dl;
     dl.init(deal);
-    uint32_t n_traced = 0, dropped = 0;
+    uint32_t n_traced = 0;
     for (int q = dl.take(); q < npk;) {
         const int qn = dl.take();  // the next packet, taken while this one traces
         const int p = q * 64 + lane;
@@ -1228,17 +1237,14 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         n_traced += valid && !culled ? 1u : 0u;
         Hit h;
         set_miss(h, tmax);
-        packet_trace<kCount>(sa.qnodes, sa.tris, stk, valid && !culled && fc.n_tris > 0, o, d, tmin, h, cnt,
-                             dropped);
+        packet_trace<kCount>(sa.qnodes, sa.tris, stk, gstk, tail + 1, valid && !culled && fc.n_tris > 0, o, d, tmin,
+                             h, cnt);
         if (valid) hit_put(hits + p, pack_hit(h));
         q = qn;
     }
     for (int off = 32; off > 0; off >>= 1) n_traced += (uint32_t)__shfl_xor((int)n_traced, off);
-    if (lane == 0 && n_traced) atomicAdd(traced, n_traced);
-    if (kCount) {
-        flush_counts(tc, 0, cnt.nodes, cnt.tris);
-        flush_drops(tc, dropped);
-    }
+    if (lane == 0 && n_traced) atomicAdd(tail, n_traced);
+    if (kCount) flush_counts(tc, 0, cnt.nodes, cnt.tris);
 }
 
 // Camera paths: shade bounce 0 from hits[p]; appends the bounce-1 path queue
@@ -1275,16 +1281,17 @@ template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
                                                                          float2* __restrict__ hits,
                                                                          int32_t* __restrict__ spill,
-                                                                         unsigned long long* __restrict__ tc) {
+                                                                         unsigned long long* __restrict__ tc,
+                                                                         uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
-    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
+    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, 0.0f, st, cnt, deal_ctrs(qi.ctr, 1), [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qi.ctr, 1), [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
@@ -1292,10 +1299,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
             tmax = kFltMax;
         },
         [&](int, uint32_t i, const Hit& h) { hit_put(hits + i, pack_hit(h)); });
-    if (kCount) {
-        flush_counts(tc, 2, cnt.nodes, cnt.tris);
-        flush_drops(tc, st.dropped);
-    }
+    if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
 }
 
 // Bounce b: shade from hits[slot], in the queue's time order (slot_t); appends
@@ -1335,16 +1339,17 @@ template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
                                                                           Rad rad,
                                                                           int32_t* __restrict__ spill,
-                                                                          unsigned long long* __restrict__ tc) {
+                                                                          unsigned long long* __restrict__ tc,
+                                                                          uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
-    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0};
+    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, 0.0f, st, cnt, deal_ctrs(qi.ctr, 1), [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qi.ctr, 1), [&](int m) { return qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
@@ -1362,10 +1367,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
             L.z = L.z + c.z;
             rad.put(pid, L);
         });
-    if (kCount) {
-        flush_counts(tc, 4, cnt.nodes, cnt.tris);
-        flush_drops(tc, st.dropped);
-    }
+    if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
 }
 
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
@@ -1570,15 +1572,20 @@ RR_D TileOrder uniform_order(TileOrder t) {
 
 // Per-lane ray counts of the tile kernel, reduced once per wave at exit into
 // the chunk-0 counter pairs: {0, 1} = bounce 0, {2, 3} = all later bounces
-// (rr_api.cpp fill_stats sums the pairs).
-RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint32_t c1, uint32_t s1, uint32_t* __restrict__ traced,
-                     uint32_t t0) {
+// (rr_api.cpp fill_stats sums the pairs); tail = the chunk's words from
+// camera_traced_slot on: [0] camera rays traced, [2] / [3] continuations /
+// shadow rays that left a hull side (counted in the pairs too, but resolved
+// without a traversal).
+RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint32_t c1, uint32_t s1,
+                     uint32_t* __restrict__ tail, uint32_t t0, uint32_t ec, uint32_t es) {
     // the counts are wave totals already (wave_count): lane 0 adds them
     const uint32_t v[4] = {c0, s0, c1, s1};
     if ((threadIdx.x & 63) == 0) {
         for (int k = 0; k < 4; ++k)
             if (v[k]) atomicAdd(&tot[k], v[k]);
-        if (t0) atomicAdd(traced, t0);
+        if (t0) atomicAdd(&tail[0], t0);
+        if (ec) atomicAdd(&tail[2], ec);
+        if (es) atomicAdd(&tail[3], es);
     }
 }
 
@@ -1659,9 +1666,9 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         clk0 = __builtin_amdgcn_s_memtime();
         rt0 = __builtin_amdgcn_s_memrealtime();
     }
-    TravStack st{stack, spill, stride, 0};
+    TravStack st{stack, spill, stride, 0, tot + drops_slot(fc.max_bounces)};
     TravCount cp, ce, cs;
-    uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0, n_t0 = 0;
+    uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0, n_t0 = 0, n_ec = 0, n_es = 0;
     // The screen rectangle and the tile order come from the root node in LDS,
     // so the compiler cannot tell they are wave-uniform and would keep (and
     // spill) them in VGPRs for the whole kernel: every lane holds the same
@@ -1765,7 +1772,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             bool live = valid;
             for (int b = 0; b <= fc.max_bounces; ++b) {
                 if (!__any(live)) break;
-                bool cont = false, shadow = false;
+                bool cont = false, shadow = false, esc = false;
                 if (live) {
                     ShadeOut so;
                     Hit h;
@@ -1778,6 +1785,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     shade(fc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, fc.n_tris, st, cs});
                     cont = so.cont;
                     shadow = so.shadow;
+                    esc = so.esc;
                     if (so.cont && so.esc) {
                         // the continuation leaves a hull side of its triangle
                         // (hull_flags): its next hit is the world, added here as
@@ -1804,6 +1812,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     n_c1 += wave_count(cont);
                     n_s1 += wave_count(shadow);
                 }
+                n_ec += wave_count(cont && esc);
+                n_es += wave_count(shadow && esc);
             }
             add_to(P, L);
             group_end(s);
@@ -1820,12 +1830,12 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         if (lane == 0)  // this unit's time, for the next launch's hand-out order (k_tile_order)
             atomicAdd(&sl.cost[ty * to.tx + tx], (uint32_t)(__builtin_amdgcn_s_memrealtime() - u_start));
     }
-    flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tot + camera_traced_slot(fc.max_bounces), n_t0);
+    uint32_t* const tail = tot + camera_traced_slot(fc.max_bounces);
+    flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tail, n_t0, n_ec, n_es);
     if (kCount) {
         flush_counts(tc, 0, cp.nodes, cp.tris);
         flush_counts(tc, 2, ce.nodes, ce.tris);
         flush_counts(tc, 4, cs.nodes, cs.tris);
-        flush_drops(tc, st.dropped);
         const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
         if ((threadIdx.x & 63) == 0) {  // device.hpp kTravWords
             atomicAdd(&tc[6], clk1 - clk0);
@@ -1964,7 +1974,7 @@ __global__ void k_debug_trace(const BvhNode* __restrict__ nodes, const TriPack* 
     __shared__ int lds_stack[kLdsStack * kBlock];
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int nthreads = gridDim.x * kBlock;
-    TravStack st{lds_slot(lds_stack), spill, nthreads, 0};
+    TravStack st{lds_slot(lds_stack), spill, nthreads, 0, nullptr};
     TravCount cnt;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
@@ -2004,6 +2014,38 @@ __global__ void k_debug_bsdf(const float* __restrict__ mat12, const float* __res
     ok[i] = good ? (glossy ? 2 : 1) : 0;
 }
 
+// rr_debug_trace width 5: the camera kernel's packet walk over arbitrary rays
+// (64 per wave, closest hit) with a kStack-entry LDS packet stack, small enough
+// to fill on any real hierarchy, so the stack's HBM part is exercised (the
+// per-lane spill area, one kPacketSpill part per wave). Closest hit only:
+// occluded is set to 255.
+template <int kStack>
+__global__ __launch_bounds__(kBlock) void k_debug_packet(const QNode6* __restrict__ nodes,
+                                                         const TriPack* __restrict__ tris, int n_tris, int n,
+                                                         const float4* __restrict__ rays, float4* __restrict__ hits,
+                                                         int32_t* __restrict__ prims, uint8_t* __restrict__ occ,
+                                                         int32_t* __restrict__ spill) {
+    __shared__ int stack_all[kWavesPerBlock * kStack];
+    lds_int* stk = lds_slot(stack_all) + (threadIdx.x >> 6) * kStack;
+    TravCount cnt;
+    for (int b0 = blockIdx.x * kBlock; b0 < n; b0 += gridDim.x * kBlock) {  // block-uniform trip count
+        const int i = b0 + (int)threadIdx.x;
+        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d = make_float4(0.0f, 0.0f, 1.0f, -1.0f);
+        if (i < n) {
+            o = rays[2 * i];
+            d = rays[2 * i + 1];
+        }
+        Hit h;
+        set_miss(h, d.w);
+        packet_trace<false, kStack>(nodes, tris, stk, spill + (size_t)wave_id() * kPacketSpill, nullptr,
+                                    i < n && n_tris > 0, xyz(o), xyz(d), o.w, h, cnt);
+        if (i >= n) continue;
+        hits[i] = make_float4(h.t, h.u, h.v, 0.0f);
+        prims[i] = h.orig;
+        occ[i] = 255;
+    }
+}
+
 __global__ void k_debug_trace4(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
                                int n, const float4* __restrict__ rays, float4* __restrict__ hits,
                                int32_t* __restrict__ prims, uint8_t* __restrict__ occ,
@@ -2011,7 +2053,7 @@ __global__ void k_debug_trace4(const QNode6* __restrict__ nodes, const TriPack* 
     __shared__ int lds_stack[kLdsStack * kBlock];
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int nthreads = gridDim.x * kBlock;
-    TravStack st{lds_slot(lds_stack), spill, nthreads, 0};
+    TravStack st{lds_slot(lds_stack), spill, nthreads, 0, nullptr};
     TravCount cnt;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
@@ -2054,9 +2096,10 @@ int device_cu_count() {
 
 // Per chunk, one pair per bounce b = 0..max_bounces: {paths entering bounce
 // b+1, shadow rays of bounce b}, written by the consuming kernels, +1 pair of
-// slack (k_tiles' unit counter), then camera rays traced (not culled, tested
-// against at least one triangle) and a spare word.
-int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2) + 2; }
+// slack, then camera rays traced (not culled, tested against at least one
+// triangle), traversal-stack drops, and k_tiles' escaped continuations and
+// escaped shadow rays (device.hpp camera_traced_slot .. escaped_slot).
+int counters_per_chunk(int max_bounces) { return 2 * (max_bounces + 2) + 4; }
 
 namespace {
 // LDS-resident scenes render through k_tiles (RR_FLAG_WAVEFRONT: through the
@@ -2143,9 +2186,9 @@ struct TileGrid {
 struct SplitGrids {
     int trace_p, trace_e, shadow, shade_p, shade_e, packet;
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
-    void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*);
-    void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*);
-    void (*ktpk)(FrameConsts, SceneArgs, int, float2*, uint32_t*, unsigned long long*, uint32_t*);  // packets
+    void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*, uint32_t*);
+    void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*, uint32_t*);
+    void (*ktpk)(FrameConsts, SceneArgs, int, float2*, uint32_t*, int32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
@@ -2246,6 +2289,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         fc.div_spp = FastDiv::make((uint32_t)fc.spp_chunk);
         const int np = npix * fc.spp_chunk;
         uint32_t* tot = reinterpret_cast<uint32_t*>(p.counters.ptr + (size_t)cpc * c);
+        uint32_t* tail = tot + camera_traced_slot(base.max_bounces);  // traced, drops (device.hpp)
         uint32_t* qc = p.qctr.ptr + per_chunk * c;
         auto qpath = [&](int b) { return qc + ((size_t)b * 2 + 0) * per_q; };    // paths entering b+1
         auto qshadow = [&](int b) { return qc + ((size_t)b * 2 + 1) * per_q; };  // shadow rays of b
@@ -2255,11 +2299,11 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             throw std::runtime_error("queue capacity exceeded (split path)");
         pr.begin(st, RR_K_PRIMARY);
         if (packets)
-            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, deal_host(qpath(0), 2), tc,
-                                                               tot + camera_traced_slot(base.max_bounces));
+            G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, deal_host(qpath(0), 2),
+                                                               p.spill.ptr, tc, tail);
         else
-            G.ktp<<<clamp_grid(np, G.trace_p, kTraceBlock), kTraceBlock, 0, st>>>(
-                fc, sa, np, p.hits.ptr, p.spill.ptr, tc, tot + camera_traced_slot(base.max_bounces));
+            G.ktp<<<clamp_grid(np, G.trace_p, kTraceBlock), kTraceBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr,
+                                                                                   tc, tail);
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
         k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1],
@@ -2270,14 +2314,14 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             pr.begin(st, RR_K_SHADOW);
             G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(
                 sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, Rad{reinterpret_cast<float*>(p.rad.ptr)},
-                p.spill.ptr, tc);
+                p.spill.ptr, tc, tail);
             pr.end(st);
             if (b == base.max_bounces) break;
             const int nb = b + 1;  // bounce being traced and shaded
             const QueueIn qin{qpath(b), cap_prev, tot + 2 * b};
             pr.begin(st, RR_K_EXTEND);
             G.kte<<<clamp_grid(np, G.trace_e, kTraceBlock), kTraceBlock, 0, st>>>(sa, pq[nb & 1], qin, p.hits.ptr,
-                                                                                p.spill.ptr, tc);
+                                                                                p.spill.ptr, tc, tail);
             pr.end(st);
             pr.begin(st, RR_K_SHADE);
             k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},
@@ -2429,7 +2473,12 @@ void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, f
                         uint8_t* d_occ, hipStream_t st, int width) {
     p.ensure_paths(1);
     const int g = (int)std::min<long>((n + kBlock - 1) / kBlock, p.grid_blocks);
-    if (width == 4) {
+    if (width == 5) {  // packet walk with a 4-entry stack: the fallback runs
+        if (!s.has4) throw std::runtime_error("BVH4 not built");
+        if (n > 0)
+            k_debug_packet<4><<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims,
+                                                    d_occ, p.spill.ptr);
+    } else if (width == 4) {
         if (!s.has4) throw std::runtime_error("BVH4 not built");
         if (n > 0)
             k_debug_trace4<<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 6
+#define RR_ABI_VERSION 7
 
 /* error codes (negative errno values) */
 #define RR_OK 0
@@ -108,9 +108,11 @@ typedef struct rr_frame_timing {
 /* Per-frame statistics (sidecar metrics; never part of the trace JSON). */
 typedef struct rr_frame_stats {
     int32_t width, height, spp, chunks;
-    uint64_t camera_rays;    /* primary rays traced */
-    uint64_t extension_rays; /* bounce rays traced (closest hit) */
-    uint64_t shadow_rays;    /* NEE shadow rays traced (any hit) */
+    uint64_t camera_rays;    /* camera samples, W * H * spp (camera_rays_traced: those traversed) */
+    uint64_t extension_rays; /* continuation rays spawned (closest hit); extension_rays_escaped of them
+                              * are resolved without a traversal */
+    uint64_t shadow_rays;    /* NEE shadow rays spawned (any hit); shadow_rays_escaped of them are
+                              * resolved without a traversal */
     uint64_t primary_continued; /* camera paths that continue past bounce 0 */
     uint64_t primary_shadow;    /* shadow rays spawned at bounce 0 */
     double anim_ms;          /* host animation eval + upload */
@@ -149,9 +151,18 @@ typedef struct rr_frame_stats {
      * 32-sample groups when it ran alone (one unit per group); 0 for frames of
      * the other paths. Scheduling only: both give the same bits. */
     int32_t tile_slices;
-    /* RR_FLAG_COUNT_TRAVERSAL: traversal-stack pushes dropped for want of room
-     * over the frame (each a missed subtree; 0 on every bench scene) */
+    /* traversal-stack pushes dropped for want of room over the frame (each a
+     * missed subtree; counted in every frame; 0 on every bench scene) */
     int32_t stack_drops;
+    /* LDS-resident scenes (k_tiles): continuation / shadow rays of extension_rays /
+     * shadow_rays that leave a hull side of their triangle (every vertex of the
+     * scene lies behind that side's plane), so they meet nothing and are
+     * resolved without a traversal (the continuation adds the world term, the
+     * shadow ray is unoccluded). Rays that entered a traversal =
+     * camera_rays_traced + extension_rays - extension_rays_escaped + shadow_rays
+     * - shadow_rays_escaped. 0 on the split path (every ray is traversed). */
+    uint64_t extension_rays_escaped;
+    uint64_t shadow_rays_escaped;
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */
@@ -316,8 +327,10 @@ int rr_debug_qbvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t* nq
                   int32_t* children, uint32_t* nodes16, int32_t* tri_orig);
 
 /* Trace a batch of rays against the frame's hierarchy. bvh_width: 2 (LBVH),
- * 4 (the quantised 6-wide collapse) or 0 (whichever the frame kernels use for this scene,
- * render_ints[7] of rr_debug_frame_state). rays: n*8 floats
+ * 4 (the quantised 6-wide collapse), 5 (the same hierarchy walked by the camera
+ * kernel's 64-ray packets, with 4 packet-stack entries in LDS so that the
+ * stack's HBM part is used; closest hit only, occluded = 255) or 0 (whichever
+ * the frame kernels use for this scene, render_ints[7] of rr_debug_frame_state). rays: n*8 floats
  * (o.xyz, tmin, d.xyz, tmax). hits: n*4 floats (t, u, v, 0), prims: n original
  * triangle ids (-1 miss), occluded: n bytes (any-hit result). */
 int rr_debug_trace(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t bvh_width,

@@ -113,8 +113,10 @@ def trace_brute(tris: np.ndarray, rays: np.ndarray):
 
 
 def render(tris, tri_mat, camera, lights, materials, world, render_ints, render_floats,
-           rows: tuple[int, int] | None = None, threads: int = 0, film: bool = True, rgba: bool = True):
-    """Full-frame render of the oracle path tracer. Inputs as rr_debug_frame_state."""
+           rows: tuple[int, int] | None = None, threads: int = 0, film: bool = True, rgba: bool = True,
+           row_list=None):
+    """Full-frame render of the oracle path tracer. Inputs as rr_debug_frame_state.
+    rows: a range of rows; row_list: any rows (one hierarchy build for all)."""
     tris = _f32(tris).reshape(-1, 9)
     tri_mat = np.ascontiguousarray(tri_mat, dtype=np.int32)
     cam = _f32(camera)
@@ -130,11 +132,24 @@ def render(tris, tri_mat, camera, lights, materials, world, render_ints, render_
     f = np.zeros((H, W, 4), np.float32) if film else None
     r = np.zeros((H, W, 4), np.uint8) if rgba else None
     r0, r1 = rows if rows else (0, 0)
+    rl = None
+    if row_list is not None:
+        rl = np.ascontiguousarray(row_list, dtype=np.int32)
+        assert rl.size > 0 and rl.min() >= 0 and rl.max() < H
+        lib().orc_set_row_list(_p(rl, ctypes.c_int32), int(rl.size))
+    try:
+        _render_call(tris, tri_mat, cam, lights, mats, world, ri, rf, f, r, r0, r1, threads)
+    finally:
+        if rl is not None:
+            lib().orc_set_row_list(None, 0)
+    return f, r
+
+
+def _render_call(tris, tri_mat, cam, lights, mats, world, ri, rf, f, r, r0, r1, threads):
     lib().orc_render(tris.shape[0], _p(tris, ctypes.c_float), _p(tri_mat, ctypes.c_int32), _p(cam, ctypes.c_float),
                      lights.shape[0], _p(lights, ctypes.c_float), _p(mats, ctypes.c_float),
                      _p(world, ctypes.c_float), _p(ri, ctypes.c_int32), _p(rf, ctypes.c_float),
                      _p(f, ctypes.c_float), _p(r, ctypes.c_uint8), r0, r1, threads)
-    return f, r
 
 
 class rules:

@@ -784,8 +784,13 @@ static void try_leaf(const lbvh* B, int leaf, const shear_t* s, v3 o, float tmin
 typedef struct { float t; int slot, ref; } ckey;
 
 /* node visits / triangle tests of trace4 since the last reset (research:
- * tools/collapse_study.py) */
+ * tools/collapse_study.py, tools/margin_study.py). Counted only while a study
+ * tool has switched counting on (orc_set_walk_counting): the shared totals are
+ * updated atomically once per ray, which would otherwise put every render
+ * thread on one cache line (and slow the CPU baseline). */
 static long long g_cnt_nodes, g_cnt_tris, g_cnt_top[4];
+static int g_count_walks;
+void orc_set_walk_counting(int on) { g_count_walks = on; }
 /* research only (tools/margin_study.py): the walk's box margin times this
  * (1 = the product's); results then may differ from the device's */
 static float g_margin_scale = 1.0f;
@@ -907,14 +912,16 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
         node = k[best].ref;
     }
 done:
-    for (int k = 0; k < 4; ++k) {
+    if (g_count_walks) {
+        for (int k = 0; k < 4; ++k) {
 #pragma omp atomic
-        g_cnt_top[k] += ctop[k];
+            g_cnt_top[k] += ctop[k];
+        }
+#pragma omp atomic
+        g_cnt_nodes += cn;
+#pragma omp atomic
+        g_cnt_tris += ct;
     }
-#pragma omp atomic
-    g_cnt_nodes += cn;
-#pragma omp atomic
-    g_cnt_tris += ct;
     return h->idx >= 0;
 }
 
@@ -1612,6 +1619,13 @@ void orc_ray_counts(long long* out4, int* late32, int* n_late) {
     *n_late = g_n_late;
 }
 
+/* rows rendered by the next orc_render calls instead of [row_begin, row_end)
+ * (NULL: the range): spread sample rows of a large frame with one hierarchy
+ * build (test use; orc_set_row_list(NULL, 0) resets) */
+static const int32_t* g_row_list;
+static int g_n_row_list;
+void orc_set_row_list(const int32_t* rows, int n) { g_row_list = n > 0 ? rows : NULL; g_n_row_list = n > 0 ? n : 0; }
+
 int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const float* cam, int n_lights,
                const float* lights, const float* mats, const float* world, const int32_t* ri, const float* rf,
                float* film, uint8_t* rgba8, int row_begin, int row_end, int threads) {
@@ -1661,13 +1675,13 @@ int orc_render(int n_tris, const float* tris9, const int32_t* tri_mat, const flo
      * still spreads over every thread (per-pixel results do not depend on the
      * split) */
     const int nseg = (S->W + ORC_SEG - 1) / ORC_SEG;
-    const long n_items = (long)(row_end - row_begin) * nseg;
+    const long n_items = (long)(g_row_list ? g_n_row_list : row_end - row_begin) * nseg;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 1)
 #endif
     for (long it = 0; it < n_items; ++it) {
-        const int y = row_begin + (int)(it / nseg);
+        const int y = g_row_list ? g_row_list[it / nseg] : row_begin + (int)(it / nseg);
         const int x0 = (int)(it % nseg) * ORC_SEG;
         const int x1 = x0 + ORC_SEG < S->W ? x0 + ORC_SEG : S->W;
         long long rays[4] = {0, 0, 0, 0};

@@ -7,6 +7,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+if os.path.join(ROOT, "tools") not in sys.path:  # fixture generators (tools/make_split_golden.py)
+    sys.path.append(os.path.join(ROOT, "tools"))
 
 PKG = "diploma_thesis-distributed_rendering_of_cgi_using_a_render_cluster_amd"
 SCENES = os.path.join(ROOT, "scenes")

@@ -210,6 +210,14 @@ def test_ray_counts_match_oracle(ctx, rr, s04, path):
     assert (st.primary_continued, st.primary_shadow) == (c0, s0)
     assert (st.extension_rays, st.shadow_rays) == (c0 + c1, s0 + s1)
     assert c0 > 0 and c1 == 0 and s1 == 0
+    # escaped rays (left a hull side, resolved without a traversal): on the
+    # cube every face is a hull side, so k_tiles traverses no secondary ray;
+    # the split path has no hull rule and traverses them all
+    if path == "tiles":
+        assert (st.extension_rays_escaped, st.shadow_rays_escaped) == (st.extension_rays, st.shadow_rays)
+    else:
+        assert (st.extension_rays_escaped, st.shadow_rays_escaped) == (0, 0)
+    assert st.stack_drops == 0  # counted in every frame, not only the counting pass
 
 
 def test_no_path_enters_the_cube(ctx, rr, s04):

@@ -99,6 +99,22 @@ def test_physics_trace_bit_exact(ctx, s02, hier):
         assert np.array_equal(p2, op) and np.array_equal(o2, oo)
 
 
+def test_packet_walk_spills_its_stack_to_hbm(ctx, s02):
+    """The camera kernel's packet walk (64 rays per wave, one node at a time)
+    with 4 packet-stack entries in LDS: every deeper push goes to the stack's
+    HBM part (rr_debug_trace width 5), and the closest hits equal the per-lane
+    walk of the same hierarchy and the oracle's, so a deep hierarchy costs
+    time, never a subtree (round 4 dropped pushes past 128 entries)."""
+    st = ctx.frame_state(s02, 90)
+    rays = _camera_rays(st, 20000, np.random.default_rng(5))
+    h5, p5, o5 = ctx.trace(s02, 90, rays, width=5)
+    h4, p4, _ = ctx.trace(s02, 90, rays, width=4)
+    oh, op, _ = O.trace(st.tris, rays, width=4)
+    assert np.array_equal(p5, op) and np.array_equal(h5, oh)
+    assert np.array_equal(p5, p4) and (p5 >= 0).mean() > 0.3
+    assert (o5 == 255).all()
+
+
 @pytest.mark.parametrize("frame", [1, 90])
 def test_physics_qbvh_bit_exact(ctx, s02, frame):
     st = ctx.frame_state(s02, frame)
@@ -169,15 +185,15 @@ def test_c5_full_size_qbvh_bit_exact(ctx, sc5):
           f"{np.mean((ch != 0x7FFFFFFF).sum(1)):.2f} children per node")
 
 
-@pytest.mark.parametrize("width", [3, 4])
+@pytest.mark.parametrize("width", [3, 4, 5])
 def test_c5_trace_bit_exact(ctx, sc5, width):
     st = ctx.frame_state(sc5, 200)
     rays = _camera_rays(st, 100000, np.random.default_rng(11))
     hits, prims, occ = ctx.trace(sc5, 200, rays, width=width)
-    oh, op, oo = O.trace(st.tris, rays, width=width)
+    oh, op, oo = O.trace(st.tris, rays, width=min(width, 4))  # 5: packets over the 6-wide hierarchy
     assert np.array_equal(prims, op), f"{np.count_nonzero(prims != op)} prim mismatches"
     assert np.array_equal(hits, oh)
-    assert np.array_equal(occ, oo)
+    assert np.array_equal(occ, oo) or width == 5  # packets: closest hit only
     assert (prims >= 0).mean() > 0.2
 
 
@@ -232,22 +248,24 @@ def test_device_world_triangles_match_host_restatement(ctx, path, frames):
         s.close()
 
 
-def _band_rows(H, n):
-    return [int(r) for r in np.linspace(0, H - 4, n).astype(int)]
+def _band_rows(H, n, h=4):
+    """n bands of h rows spread over a frame of H rows (first and last rows included)."""
+    return [y for r in np.linspace(0, H - h, n).astype(int) for y in range(int(r), int(r) + h)]
 
 
-@pytest.mark.parametrize("job_name,frames,n_bands", [
-    ("02_physics-standin_170f-5w_naive-fine.toml", [1, 90, 170], 4),
-    ("03_physics-2-standin_480f-8w_dynamic.toml", [300], 4),
-    ("c5_synthetic-10m_240f-8w_dynamic.toml", [150], 2)])
-def test_bench_config_split_path_bands_bit_exact(rr, tmp_path, job_name, frames, n_bands):
+@pytest.mark.parametrize("job_name,frames,n_bands,band_h", [
+    ("02_physics-standin_170f-5w_naive-fine.toml", [1, 90, 170], 4, 4),
+    ("03_physics-2-standin_480f-8w_dynamic.toml", [300], 4, 4),
+    ("c5_synthetic-10m_240f-8w_dynamic.toml", [150], 8, 2)])
+def test_bench_config_split_path_bands_bit_exact(rr, tmp_path, job_name, frames, n_bands, band_h):
     """The split path at the size the bench renders it (02 / 03: 1920x1080 x
     64 spp, C5: 3840x2160 x 1024 spp in sample chunks; scene defaults) through
     BackendRunner.render_frames as bench.py times it, PNG so the written file
-    is lossless: 4-row oracle bands spread over each frame equal the file bit
-    for bit, so the chunking, the queue segments, lane refill and the
+    is lossless: oracle bands spread over each frame (C5: 8 bands of 2 rows,
+    rendered by the oracle in one call with one hierarchy build) equal the
+    file bit for bit, so the chunking, the queue segments, lane refill and the
     windowed ray order are compared with the oracle at full size. Neither side
-    drops a traversal-stack push."""
+    drops a traversal-stack push. (Whole 02 / 03 frames: the next test.)"""
     import os
     import time
     from PIL import Image
@@ -268,13 +286,13 @@ def test_bench_config_split_path_bands_bit_exact(rr, tmp_path, job_name, frames,
             st = runner.ctx.frame_state(scene, f)
             H, W = img.shape[:2]
             assert (W, H) == (int(st.render_ints[0]), int(st.render_ints[1]))
-            for r0 in _band_rows(H, n_bands):
-                t1 = time.time()
-                _, orgba = O.render_state(st, rows=(r0, r0 + 4), film=False)
-                nbad = int(np.count_nonzero(img[r0:r0 + 4] != orgba[r0:r0 + 4]))
-                print(f"{job_name} frame {f} rows {r0}..{r0 + 3}: {nbad} mismatches "
-                      f"(oracle {time.time() - t1:.1f} s; device frames {t_gpu:.1f} s)")
-                assert nbad == 0
+            rows = _band_rows(H, n_bands, band_h)
+            t1 = time.time()
+            _, orgba = O.render_state(st, row_list=rows, film=False)
+            nbad = int(np.count_nonzero(img[rows] != orgba[rows]))
+            print(f"{job_name} frame {f}: {len(rows)} rows in {n_bands} bands, {nbad} mismatches "
+                  f"(oracle {time.time() - t1:.1f} s; device frames {t_gpu:.1f} s)")
+            assert nbad == 0
         assert O.stack_drops() == 0
     finally:
         runner.close()
@@ -282,14 +300,60 @@ def test_bench_config_split_path_bands_bit_exact(rr, tmp_path, job_name, frames,
 
 @pytest.mark.parametrize("path,frame", [(S02, 90), (S03, 300), (SC5, 150)])
 def test_no_traversal_stack_drops(ctx, rr, path, frame):
-    """The counting pass reports no dropped traversal-stack push (each would be
-    a missed subtree) on any split-path bench scene, camera, extension and
-    shadow rays alike."""
+    """No dropped traversal-stack push (each would be a missed subtree) on any
+    split-path bench scene, camera, extension and shadow rays alike, in the
+    counting pass and in a normal frame (drops are counted in every frame)."""
     s = ctx.load_scene(path)
     try:
         p = rr.default_params(width=480, height=270, spp=8, flags=rr.native.RR_FLAG_COUNT_TRAVERSAL)
         _, _, st = ctx.render_to_memory(s, frame, p)
-        print(f"{path}: nodes per class {list(st.trav_nodes)}, drops {st.stack_drops}")
-        assert st.trav_nodes[0] > 0 and st.stack_drops == 0
+        _, _, st2 = ctx.render_to_memory(s, frame, rr.default_params(width=480, height=270, spp=8))
+        print(f"{path}: nodes per class {list(st.trav_nodes)}, drops {st.stack_drops} / {st2.stack_drops}")
+        assert st.trav_nodes[0] > 0 and st.stack_drops == 0 and st2.stack_drops == 0
+        assert st2.extension_rays_escaped == 0 and st2.shadow_rays_escaped == 0  # no hull rule here
     finally:
         s.close()
+
+
+@pytest.mark.parametrize("scene,frame,job_name", [
+    ("02_physics-standin.rrscene", 90, "02_physics-standin_170f-5w_naive-fine.toml"),
+    ("03_physics-2-standin.rrscene", 300, "03_physics-2-standin_480f-8w_dynamic.toml")])
+def test_bench_size_split_frames_match_oracle_fixture(rr, ctx, tmp_path, scene, frame, job_name):
+    """Whole frames at the bench size (1920x1080 x 64 spp, every one of the
+    1,080 rows): the frame as BackendRunner.render_frames writes it (PNG, the
+    bench's loop) and the film of render_to_memory equal, row for row, the
+    oracle's render of the same frame state, kept as per-row digests in
+    tests/golden/split_full_frames.json (tools/make_split_golden.py: the state
+    dumped from the device, the oracle run on every core of the build
+    container: a whole frame takes it minutes, more than a GPU test may run).
+    The device's frame state must digest to the fixture's, so both renders
+    start from the same input."""
+    import json
+    import os
+    from PIL import Image
+    import make_split_golden as G
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fx = json.load(open(G.FIXTURE))["frames"][G.key_of(scene, frame)]
+    s = ctx.load_scene(scene_path(scene))
+    try:
+        st = ctx.frame_state(s, frame, rr.default_params())
+        assert G.state_digest(st) == fx["state"], "the device's frame state is not the fixture's input"
+        film, _, stats = ctx.render_to_memory(s, frame, rr.default_params(), film=True, rgba=False)
+    finally:
+        s.close()
+    assert (stats.width, stats.height, stats.spp) == (fx["width"], fx["height"], fx["spp"])
+    bad_film = [y for y, d in enumerate(G.row_digests(film)) if d != fx["film_rows"][y]]
+    job = rr.BlenderJob.load_from_file(os.path.join(root, "jobs", job_name))
+    job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": str(tmp_path),
+                                   "output_file_format": "PNG"})
+    runner = rr.BackendRunner(root, params=rr.default_params())
+    try:
+        runner.render_frames(job, [frame])
+    finally:
+        runner.close()
+    out = rr.naming.output_path_without_extension(str(tmp_path), job.output_file_name_format, frame)
+    img = np.asarray(Image.open(out + ".png").convert("RGBA"))
+    bad_rgba = [y for y, d in enumerate(G.row_digests(img)) if d != fx["rgba8_rows"][y]]
+    print(f"{scene} frame {frame}: {fx['height']} rows, film rows differing {len(bad_film)}, "
+          f"8-bit rows differing {len(bad_rgba)} (oracle {fx['oracle_seconds']} s on {fx['oracle_threads']} threads)")
+    assert not bad_film and not bad_rgba, (bad_film[:10], bad_rgba[:10])

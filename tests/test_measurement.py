@@ -79,3 +79,54 @@ def test_dispatch_ceiling_matches_reference_strategies():
     assert bench.dispatch_ceiling(dyn, 1)["value"] == 80.0
     assert bench.dispatch_ceiling(fine, 1)["value"] == 20.0
     assert bench.dispatch_ceiling(coarse, 8)["value"] == 320.0
+
+
+def _split_stats(n_tris):
+    """Counting-frame stats of a split-path frame (one extension launch)."""
+    return types.SimpleNamespace(camera_rays=1000, extension_rays=500, shadow_rays=400, primary_continued=300,
+                                 primary_shadow=250, trav_nodes=[1000, 8000, 6000], trav_tris=[100, 900, 700],
+                                 n_triangles=n_tris, width=10, height=10, spp=10, chunks=1,
+                                 camera_rays_traced=900)
+
+
+def _roof(tmp_path, entry, n_tris):
+    pmc = tmp_path / "pmc.json"
+    pmc.write_text(json.dumps({"kernels": {"k_trace_extend<false>": entry}}))
+    args = types.SimpleNamespace(workload="c5", pmc_summary=str(pmc))
+    names = ["build", "primary", "extend", "shadow", "accumulate", "shade", "tiles", "x"]
+    ms, launches = [0.0] * 8, [0] * 8
+    ms[2], launches[2], launches[5] = 2.0, 1, 1  # 1 extension launch of 2 ms; a shading launch (split path)
+    return bench.roofline_line(args, "extend", _split_stats(n_tris), ms, launches, names, 1)
+
+
+def test_split_path_bound_comes_from_the_counters(tmp_path):
+    """The split path's bound is derived from its PMC pass: latency when the
+    PMC HBM rate is below half the peak and waves wait more than half their
+    lives, else hbm; frac is the PMC fraction, the SURVEY 8(d) figure beside
+    it as frac_survey_formula."""
+    slow = {"traffic_bytes": 2e12 * 2.0e-3, "wait_frac": 0.59, "l2_hit_rate": 0.36}  # 2 TB/s
+    r = _roof(tmp_path, slow, 10_000_000)
+    assert r["bound"] == "latency" and abs(r["achieved"] - 2000.0) < 1e-6
+    assert abs(r["frac"] - 0.25) < 1e-9 and "frac_survey_formula" in r
+    fast = {"traffic_bytes": 6e12 * 2.0e-3, "wait_frac": 0.7}  # 6 TB/s
+    assert _roof(tmp_path, fast, 10_000_000)["bound"] == "hbm"
+    busy = {"traffic_bytes": 1e12 * 2.0e-3, "wait_frac": 0.3}  # slow, but the waves issue
+    assert _roof(tmp_path, busy, 1000)["bound"] == "hbm"
+
+
+def test_kernels_pmc_block():
+    """Per-kernel PMC rows: the timed instantiation only, GB/s over the pass's
+    own dispatch time, wave life and occupancy from SQ_WAVE_CYCLES."""
+    ks = {"k_trace_extend<false>": {"launches": 4, "traffic_bytes": 8e9, "pmc_pass_avg_ms": 2.0,
+                                    "l2_hit_rate": 0.5, "wait_frac": 0.6, "valu_lane_util": 0.45,
+                                    "GRBM_GUI_ACTIVE": 8 * 1000.0, "SQ_WAVE_CYCLES": 250.0 * 2048, "SQ_WAVES": 2048},
+          "k_trace_extend<true>": {"launches": 1, "traffic_bytes": 1.0, "pmc_pass_avg_ms": 1.0},
+          "k_shade_extend": {"launches": 4, "traffic_bytes": 2e9, "pmc_pass_avg_ms": 1.0}}
+    b = bench.pmc_kernel_block(ks, "profiles/x.json")
+    rows = b["kernels"]
+    assert set(rows) == {"k_trace_extend<false>", "k_shade_extend"}
+    e = rows["k_trace_extend<false>"]
+    assert e["hbm_gbs"] == 4000.0 and e["hbm_frac"] == 0.5
+    assert e["wave_life_frac"] == 1.0 and e["occupancy_waves_per_simd"] == 2.0
+    assert rows["k_shade_extend"]["hbm_gbs"] == 2000.0
+    assert bench.pmc_kernel_block({}, None) == {}

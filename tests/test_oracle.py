@@ -402,6 +402,13 @@ def test_04_frame_is_plausible():
     f2, r2 = O.render(tris, mats, fc["camera"], fc["lights"], fc["materials"], fc["world"], ri, rf,
                       rows=(10, 20), threads=2)
     assert np.array_equal(f2[10:20], film[10:20]) and np.array_equal(r2[10:20], rgba[10:20])
+    # and so do rows picked anywhere in one call (one hierarchy build)
+    rows = [0, 3, 17, 18, 40, 53]
+    f3, r3 = O.render(tris, mats, fc["camera"], fc["lights"], fc["materials"], fc["world"], ri, rf,
+                      row_list=rows, threads=3)
+    assert np.array_equal(f3[rows], film[rows]) and np.array_equal(r3[rows], rgba[rows])
+    others = [y for y in range(54) if y not in rows]
+    assert not f3[others].any() and not r3[others].any()
 
 
 @pytest.mark.parametrize("frame,ground", [(1, False), (30, False), (60, True), (5, True)])

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of library variants (tools/ab_variants.sh builds) on the GPU box,
-one subprocess per variant (RR_LIB_PATH, or a whole package tree of another
-commit under build/ab_<variant>/tree), variants interleaved over `rounds`
+one subprocess per variant (RR_LIB_PATH = ab_builds/<variant>/librr.so),
+variants interleaved over `rounds`
 rounds so that clock drift hits them alike. Per variant and scene:
   * solo: per-class kernel ms of one frame rendered alone (best of 3,
     render_to_memory: k_tiles in sample-group slices);
@@ -76,14 +76,9 @@ def main():
     for r in range(rounds):
         for v in variants:
             env = dict(os.environ)
-            root = ROOT
             if v != "main":
-                tree = os.path.join(ROOT, PKG, "build", "ab_" + v, "tree")
-                if os.path.isdir(tree):  # a whole package tree (another commit, its own ABI and binding)
-                    root = tree
-                else:
-                    env["RR_LIB_PATH"] = os.path.join(ROOT, PKG, "build", "ab_" + v, "librr.so")
-            res = subprocess.run([sys.executable, "-c", CHILD % (root, PKG, scenes, frames)], env=env,
+                env["RR_LIB_PATH"] = os.path.join(ROOT, "ab_builds", v, "librr.so")
+            res = subprocess.run([sys.executable, "-c", CHILD % (ROOT, PKG, scenes, frames)], env=env,
                                  capture_output=True, text=True, timeout=600)
             line = res.stdout.strip().splitlines()[-1] if res.stdout.strip() else res.stderr[-500:]
             print(f"r{r} {v:10s} {line}", flush=True)

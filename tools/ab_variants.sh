@@ -1,14 +1,16 @@
 #!/bin/bash
 # Builds kernel variants of librr.so (same sources, -D switches) into
-# <pkg>/build/ab_<name>/ for A/B timing on the GPU box with RR_LIB_PATH.
+# ab_builds/<name>/librr.so (objects in <pkg>/build/ab_<name>/, which does not
+# travel) for A/B timing on the GPU box with RR_LIB_PATH.
 #   tools/ab_variants.sh name1 "-DFOO=1" name2 "-DFOO=0" ...
 set -e
 PKG=diploma_thesis-distributed_rendering_of_cgi_using_a_render_cluster_amd
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 while [ $# -ge 2 ]; do
-    d=$ROOT/$PKG/build/ab_$1
-    mkdir -p $d/obj
-    make -s -j8 -C $ROOT/$PKG/csrc OUT=$d OBJ=$d/obj EXTRA="$2" $d/librr.so
+    d=$ROOT/ab_builds/$1
+    o=$ROOT/$PKG/build/ab_$1
+    mkdir -p $d $o
+    make -s -j8 -C $ROOT/$PKG/csrc OUT=$d OBJ=$o EXTRA="$2" $d/librr.so
     echo "built $d/librr.so ($2)"
     shift 2
 done

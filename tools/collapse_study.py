@@ -44,12 +44,14 @@ def world_tris(path, scene_obj, frame):
 def walk(tris, rays, mode):
     L = O.lib()
     L.orc_set_collapse(mode)
+    L.orc_set_walk_counting(1)
     out = np.zeros(6, np.int64)
     L.orc_walk_counts(out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), 1)
     t0 = time.time()
     h, p, occ = O.trace(tris, rays, width=4)
     L.orc_walk_counts(out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), 1)
     L.orc_set_collapse(0)
+    L.orc_set_walk_counting(0)
     return h, p, occ, out.copy(), time.time() - t0
 
 

@@ -63,6 +63,7 @@ def main():
     tris, sets = rays(key, frame, npx)
     L = O.lib()
     L.orc_set_margin_scale.argtypes = [ctypes.c_float]
+    L.orc_set_walk_counting(1)
     out = np.zeros(6, np.int64)
     ptr = out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong))
     print(f"{key} frame {frame}: {len(tris)} triangles")
@@ -74,6 +75,7 @@ def main():
             L.orc_walk_counts(ptr, 1)
             print(f"  {name:7s} margin x{sc:<5g}: {out[0] / len(r):7.2f} node visits, {out[1] / len(r):6.2f} triangle tests per ray")
     L.orc_set_margin_scale(1.0)
+    L.orc_set_walk_counting(0)
 
 
 if __name__ == "__main__":

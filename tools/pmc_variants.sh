@@ -10,7 +10,7 @@ mkdir -p gpurun_out/pmcv
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 for v in "$@"; do
     d=gpurun_out/pmcv/$v
-    RR_LIB_PATH=$PWD/$PKG/build/ab_$v/librr.so timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \
+    RR_LIB_PATH=$PWD/ab_builds/$v/librr.so timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \
         --output-format csv -d $d -o run -- python3 tools/render_once.py $frame > /dev/null
     python3 - "$d" "$v" <<'PY'
 import csv, glob, sys, collections
