@@ -269,8 +269,8 @@ RR_HD int camera_traced_slot(int max_bounces) { return 2 * (max_bounces + 2); }
 // Traversal-stack pushes dropped for want of room (every frame; a dropped push
 // is a missed subtree, rr_frame_stats.stack_drops).
 RR_HD int drops_slot(int max_bounces) { return 2 * (max_bounces + 2) + 1; }
-// k_tiles: continuations / shadow rays that leave a hull side of their
-// triangle and so are resolved without a traversal (hull_flags); two words.
+// k_tiles: continuations / shadow rays traversed (two words; the others left
+// a hull side of their triangle, hull_flags, and were resolved without one).
 RR_HD int escaped_slot(int max_bounces) { return 2 * (max_bounces + 2) + 2; }
 int device_cu_count();
 

@@ -645,14 +645,16 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
     st->camera_rays = (uint64_t)fs.W * fs.H * fs.spp;
     st->view_transform = fs.view_transform;
     const int cpc = counters_per_chunk(fs.max_bounces);
-    uint64_t drops = 0;
+    uint64_t drops = 0, ext_traced = 0, sh_traced = 0;
     for (int c = 0; c < r.chunks; ++c) {
         // pair b: {paths entering bounce b+1, shadow rays of bounce b} (wavefront.hip)
         const int32_t* q = &r.counters[(size_t)cpc * c];
         st->camera_rays_traced += (uint64_t)(uint32_t)q[camera_traced_slot(fs.max_bounces)];
         drops += (uint64_t)(uint32_t)q[drops_slot(fs.max_bounces)];
-        st->extension_rays_escaped += (uint64_t)(uint32_t)q[escaped_slot(fs.max_bounces)];
-        st->shadow_rays_escaped += (uint64_t)(uint32_t)q[escaped_slot(fs.max_bounces) + 1];
+        if (r.tile_slices > 0) {  // k_tiles: the traversed ones are counted; the rest escaped
+            ext_traced += (uint64_t)(uint32_t)q[escaped_slot(fs.max_bounces)];
+            sh_traced += (uint64_t)(uint32_t)q[escaped_slot(fs.max_bounces) + 1];
+        }
         for (int b = 0; b < fs.max_bounces; ++b) st->extension_rays += (uint64_t)q[2 * b];
         for (int b = 0; b <= fs.max_bounces; ++b) st->shadow_rays += (uint64_t)q[2 * b + 1];
         st->primary_continued += (uint64_t)q[0];
@@ -674,6 +676,10 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
         st->kernel_wave_fill = (w[8] && t1 > t0) ? (double)w[9] / (double)w[8] / (double)(t1 - t0) : 0.0;
     }
     st->stack_drops = (int32_t)std::min<uint64_t>(drops, 0x7fffffffull);
+    if (r.tile_slices > 0) {
+        st->extension_rays_escaped = st->extension_rays - std::min(ext_traced, st->extension_rays);
+        st->shadow_rays_escaped = st->shadow_rays - std::min(sh_traced, st->shadow_rays);
+    }
     st->build_ms = r.rebuilt ? r.build_ms : 0.0;
     st->trace_ms = r.trace_ms;
     st->readback_ms = r.readback_ms;

@@ -643,6 +643,7 @@ RR_D lds_int* lds_slot(int* shared_elem) {
 // Traversal counters for RR_FLAG_COUNT_TRAVERSAL builds (kCount = true only).
 struct TravCount {
     uint32_t nodes = 0, tris = 0;
+    uint32_t rays = 0;  // k_tiles' out-of-line secondary traversals (counted in every frame)
 };
 
 // Resumable traversal of one ray: start() then step() until it returns true.
@@ -928,6 +929,88 @@ struct TravStateQ6 {
         }
         // nearest hit child next (ties: lower slot, q6_box_best); the other hit
         // children are pushed in descending slot order (so they pop in slot order)
+        const uint32_t rest = inner & ~(1u << best);
+        const int base = (int)nd.a.x;
+#pragma unroll
+        for (int c = kQWidth - 1; c >= 0; --c)
+            if ((rest >> c) & 1u) st.push(base + __builtin_popcount(imask & ((1u << c) - 1u)));
+        node = base + __builtin_popcount(imask & ((1u << best) - 1u));
+        return false;
+    }
+};
+
+// TravStateQ6 with postponed leaf tests (Aila & Laine 2009, "while-while"):
+// a node visit records the leaf children its ray enters (slot mask, the node's
+// first leaf triangle and internal-slot mask) instead of testing them, and the
+// lane then waits; the wave runs its leaf tests together, one triangle per
+// pending lane per step, once at least kLeafPhase of the lanes calling step()
+// have leaves pending (or every one has). With immediate tests, the leaf loop
+// ran as often as the lane with the most entered leaves needed while the
+// others idled (0.46 of the lanes active per VALU instruction on C5). A lane
+// with pending leaves visits no node until they are tested, so the closest-hit
+// bound every box test uses is the same as with immediate tests: the same
+// nodes are visited, the same triangles tested, only in another interleaving
+// across lanes, and the accept rule makes the hit the same (bit-exact).
+#ifndef RR_LEAF_PHASE
+#define RR_LEAF_PHASE 32
+#endif
+template <bool kAnyHit, bool kCount = false>
+struct TravStateQ6D {
+    float3 o, iq;
+    Shear sh;
+    float tmin;
+    Hit h;
+    int node;        // next node to visit, -1: none (the walk ends once the pending leaves are tested)
+    int lbase;       // pending leaves: the node's first leaf triangle
+    uint32_t lmask;  // pending leaf slots (bits 0..5) | the node's internal-slot mask << 8; 0: none
+    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_) {
+        o = o_;
+        sh = make_shear(d_);
+        tmin = tmin_;
+        h.t = tmax_;
+        h.u = h.v = 0.0f;
+        h.idx = -1;
+        h.orig = -1;
+        iq = rcp3(d_);
+        node = 0;
+        lmask = 0;
+    }
+    template <typename NodeSrc, typename TriP, typename Stack>
+    RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
+        const uint64_t act = __ballot(true), pen = __ballot((lmask & 63u) != 0u);
+        if (pen != 0 && (pen == act || __popcll(pen) >= RR_LEAF_PHASE)) {  // leaf phase (wave-uniform)
+            if ((lmask & 63u) == 0u) return false;
+            const int c = __builtin_ctz(lmask);
+            lmask &= lmask - 1u;
+            const uint32_t imask = lmask >> 8;
+            const int ti = lbase + c - __builtin_popcount(imask & ((1u << c) - 1u));
+            if (kCount) ++cnt.tris;
+            leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
+            if (kAnyHit && h.idx >= 0) return true;
+            if ((lmask & 63u) == 0u) lmask = 0u;
+            return lmask == 0u && node < 0;
+        }
+        if (lmask != 0u) return false;  // waits for the leaf phase
+        if (kCount) ++cnt.nodes;
+        const float tcur = h.t;
+        const QNode6 nd = q6_load(nodes, node);
+        const uint32_t imask = q6_inner(nd);
+        int best;
+        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, tmin, tcur, imask, best);
+        const uint32_t leaves = hm & ~imask;
+        const uint32_t inner = hm & imask;
+        if (leaves) {
+            lbase = (int)nd.a.y;
+            lmask = leaves | (imask << 8);
+        }
+        if (!inner) {
+            if (st.sp == 0) {
+                node = -1;
+                return lmask == 0u;
+            }
+            node = st.pop();
+            return false;
+        }
         const uint32_t rest = inner & ~(1u << best);
         const int base = (int)nd.a.x;
 #pragma unroll

@@ -786,8 +786,13 @@ constexpr int kTraceWavesPerBlock = kTraceBlock / 64;
 // Hierarchy of the split path: the PLOC BVH2 collapsed to the quantised BVH4
 // (measured against walking the PLOC BVH2 itself, C5 / 02 / 03 frames at 16 /
 // 64 / 64 spp: 191 -> 139, 174 -> 149, 192 -> 160 ms).
+// RR_LEAF_DEFER (A/B): 1 = the walk with postponed leaf tests (TravStateQ6D).
+#ifndef RR_LEAF_DEFER
+#define RR_LEAF_DEFER 0
+#endif
 template <bool kAnyHit, bool kCount>
-using SplitTrav = TravStateQ6<kAnyHit, kCount>;
+using SplitTrav = typename std::conditional<RR_LEAF_DEFER != 0, TravStateQ6D<kAnyHit, kCount>,
+                                            TravStateQ6<kAnyHit, kCount>>::type;
 constexpr int kQGroups = 64;   // append groups per queue (one lane each in QueueMap)
 constexpr int kQStride = 32;   // words between group counters (128 B)
 
@@ -1574,18 +1579,23 @@ RR_D TileOrder uniform_order(TileOrder t) {
 // the chunk-0 counter pairs: {0, 1} = bounce 0, {2, 3} = all later bounces
 // (rr_api.cpp fill_stats sums the pairs); tail = the chunk's words from
 // camera_traced_slot on: [0] camera rays traced, [2] / [3] continuations /
-// shadow rays that left a hull side (counted in the pairs too, but resolved
-// without a traversal).
+// shadow rays traversed (per lane: the out-of-line traversals, TravCount::rays;
+// the other continuations and shadow rays left a hull side and were resolved
+// without a traversal, rr_frame_stats *_escaped).
 RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint32_t c1, uint32_t s1,
-                     uint32_t* __restrict__ tail, uint32_t t0, uint32_t ec, uint32_t es) {
-    // the counts are wave totals already (wave_count): lane 0 adds them
+                     uint32_t* __restrict__ tail, uint32_t t0, uint32_t ext_traced, uint32_t sh_traced) {
+    for (int off = 32; off > 0; off >>= 1) {
+        ext_traced += (uint32_t)__shfl_xor((int)ext_traced, off);
+        sh_traced += (uint32_t)__shfl_xor((int)sh_traced, off);
+    }
+    // the other counts are wave totals already (wave_count): lane 0 adds them
     const uint32_t v[4] = {c0, s0, c1, s1};
     if ((threadIdx.x & 63) == 0) {
         for (int k = 0; k < 4; ++k)
             if (v[k]) atomicAdd(&tot[k], v[k]);
         if (t0) atomicAdd(&tail[0], t0);
-        if (ec) atomicAdd(&tail[2], ec);
-        if (es) atomicAdd(&tail[3], es);
+        if (ext_traced) atomicAdd(&tail[2], ext_traced);
+        if (sh_traced) atomicAdd(&tail[3], sh_traced);
     }
 }
 
@@ -1597,14 +1607,19 @@ RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint3
 // frames/s; solo launches -1 %). Their state goes through the call's stack
 // frame; the register budget stays at 4 waves per SIMD (5 measured slower
 // solo, +-0 pipelined).
+// cnt.rays counts the calls in every frame (the secondary rays k_tiles traverses:
+// the rest left a hull side, rr_frame_stats *_escaped), at no cost to the
+// sample loop: cnt lives in memory (its address is taken).
 template <bool kCount>
 __device__ __noinline__ bool shadow_trace(const LdsView& v, int n_tris, float3 so, float3 sd, float dist, TravStack& st,
                                           TravCount& cnt) {
+    ++cnt.rays;
     Hit hs;
     return traverse<true, kCount>(v.nodes, v.tris, n_tris, so, sd, 0.0f, dist, st, hs, cnt);
 }
 template <bool kCount>
 __device__ __noinline__ Hit ext_trace(const LdsView& v, int n_tris, float3 o, float3 d, TravStack& st, TravCount& cnt) {
+    ++cnt.rays;
     Hit h;
     traverse<false, kCount>(v.nodes, v.tris, n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
     return h;
@@ -1668,7 +1683,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     }
     TravStack st{stack, spill, stride, 0, tot + drops_slot(fc.max_bounces)};
     TravCount cp, ce, cs;
-    uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0, n_t0 = 0, n_ec = 0, n_es = 0;
+    uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0, n_t0 = 0;
     // The screen rectangle and the tile order come from the root node in LDS,
     // so the compiler cannot tell they are wave-uniform and would keep (and
     // spill) them in VGPRs for the whole kernel: every lane holds the same
@@ -1772,7 +1787,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             bool live = valid;
             for (int b = 0; b <= fc.max_bounces; ++b) {
                 if (!__any(live)) break;
-                bool cont = false, shadow = false, esc = false;
+                bool cont = false, shadow = false;
                 if (live) {
                     ShadeOut so;
                     Hit h;
@@ -1785,7 +1800,6 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     shade(fc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, fc.n_tris, st, cs});
                     cont = so.cont;
                     shadow = so.shadow;
-                    esc = so.esc;
                     if (so.cont && so.esc) {
                         // the continuation leaves a hull side of its triangle
                         // (hull_flags): its next hit is the world, added here as
@@ -1812,8 +1826,6 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                     n_c1 += wave_count(cont);
                     n_s1 += wave_count(shadow);
                 }
-                n_ec += wave_count(cont && esc);
-                n_es += wave_count(shadow && esc);
             }
             add_to(P, L);
             group_end(s);
@@ -1831,7 +1843,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             atomicAdd(&sl.cost[ty * to.tx + tx], (uint32_t)(__builtin_amdgcn_s_memrealtime() - u_start));
     }
     uint32_t* const tail = tot + camera_traced_slot(fc.max_bounces);
-    flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tail, n_t0, n_ec, n_es);
+    flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tail, n_t0, ce.rays, cs.rays);
     if (kCount) {
         flush_counts(tc, 0, cp.nodes, cp.tris);
         flush_counts(tc, 2, ce.nodes, ce.tris);

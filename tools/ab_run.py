@@ -21,6 +21,9 @@ CHILD = r'''
 import importlib, json, sys, tempfile, time
 sys.path.insert(0, %r)
 rr = importlib.import_module(%r)
+import os as _os
+if _os.environ.get("AB_ABI"):  # an older library (its stats struct is a prefix of this binding's)
+    rr.native.RR_ABI_VERSION = int(_os.environ["AB_ABI"])
 specs, n_pipe = %r, %d
 out = {}
 with rr.RenderContext(0) as ctx:
@@ -78,6 +81,9 @@ def main():
             env = dict(os.environ)
             if v != "main":
                 env["RR_LIB_PATH"] = os.path.join(ROOT, "ab_builds", v, "librr.so")
+                abi = os.path.join(ROOT, "ab_builds", v, "ABI")
+                if os.path.exists(abi):  # e.g. a previous round's library, ABI 6
+                    env["AB_ABI"] = open(abi).read().strip()
             res = subprocess.run([sys.executable, "-c", CHILD % (ROOT, PKG, scenes, frames)], env=env,
                                  capture_output=True, text=True, timeout=600)
             line = res.stdout.strip().splitlines()[-1] if res.stdout.strip() else res.stderr[-500:]
