@@ -173,8 +173,9 @@ RR_D ScreenCull screen_cull(const FrameConsts& fc, NodeP nodes) {
 
 // culled (optional): set when the ray's subpixel position is outside the
 // scene's screen rectangle (the ray misses everything).
-template <typename FloatP>
-__device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt, int px, int py,
+// CF: FrameConsts, or CamFields (the camera fields of k_tiles, read from LDS).
+template <typename FloatP, typename CF = FrameConsts>
+__device__ __forceinline__ void camera_ray_xy(const CF& fc, FloatP filt, int px, int py,
                                               uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
                                               const ScreenCull* cull = nullptr, bool* culled = nullptr) {
     // the subpixel pair: the 16-bit halves of the path key itself (a hash
@@ -211,6 +212,47 @@ __device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, i
                                            const ScreenCull* cull = nullptr, bool* culled = nullptr) {
     const int py = (int)fc.div_w.div((uint32_t)pix);
     camera_ray_xy(fc, filt, pix - py * fc.W, py, key, o, d, tmin, tmax, cull, culled);
+}
+
+// The camera fields of FrameConsts that camera_ray_xy reads. RR_TILES_CAM_LDS
+// (A/B): k_tiles stages them in LDS (5 float4) and reads them per sample with
+// volatile loads, so that they hold no scalar registers across the sample loop
+// (the kernel's arguments fill the SGPR file and spill into VGPR lanes).
+struct CamFields {
+    float3 cam_pos, cam_right, cam_up, cam_back;
+    float half_w, half_h, clip_start, clip_end, inv_w2, inv_h2;
+};
+#ifndef RR_TILES_CAM_LDS
+#define RR_TILES_CAM_LDS 0
+#endif
+RR_D float4 lds_ld4_volatile(const lds_f4w* p) {
+    const rr_f4v v = *(const volatile lds_f4w*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+RR_D CamFields load_cam(const lds_f4w* q) {
+    const float4 a = lds_ld4_volatile(q), b = lds_ld4_volatile(q + 1), c = lds_ld4_volatile(q + 2),
+                 d = lds_ld4_volatile(q + 3), e = lds_ld4_volatile(q + 4);
+    CamFields f;
+    f.cam_pos = xyz(a);
+    f.half_w = a.w;
+    f.cam_right = xyz(b);
+    f.half_h = b.w;
+    f.cam_up = xyz(c);
+    f.inv_w2 = c.w;
+    f.cam_back = xyz(d);
+    f.inv_h2 = d.w;
+    f.clip_start = e.x;
+    f.clip_end = e.y;
+    return f;
+}
+RR_D void store_cam(lds_f4w* q, const FrameConsts& fc) {
+    if (threadIdx.x == 0) {
+        q[0] = rr_f4v{fc.cam_pos.x, fc.cam_pos.y, fc.cam_pos.z, fc.half_w};
+        q[1] = rr_f4v{fc.cam_right.x, fc.cam_right.y, fc.cam_right.z, fc.half_h};
+        q[2] = rr_f4v{fc.cam_up.x, fc.cam_up.y, fc.cam_up.z, fc.inv_w2};
+        q[3] = rr_f4v{fc.cam_back.x, fc.cam_back.y, fc.cam_back.z, fc.inv_h2};
+        q[4] = rr_f4v{fc.clip_start, fc.clip_end, 0.0f, 0.0f};
+    }
 }
 
 // Staged material word of LDS-resident scenes: material id | hull_flags << kHullShift.
@@ -1671,7 +1713,7 @@ template <bool kCount, bool kWhole>
 RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
                      const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
-                     const TileSlices sl, unsigned long long rt_entry) {
+                     const TileSlices sl, unsigned long long rt_entry, const lds_f4w* cam_lds) {
     const int stride = gridDim.x * kBlock;
     // counting instantiation only: the wave's shader-clock and real-time
     // counters at start and end give the clock the kernel ran at (read-only
@@ -1782,7 +1824,11 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             uint32_t lob = 0;
             float tmin = 0.0f, tmax = -1.0f;
             bool culled = true;
+#if RR_TILES_CAM_LDS
+            if (valid) camera_ray_xy(load_cam(cam_lds), v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
+#else
             if (valid) camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
+#endif
             n_t0 += wave_count(!culled);
             bool live = valid;
             for (int b = 0; b <= fc.max_bounces; ++b) {
@@ -1886,11 +1932,14 @@ __global__ __launch_bounds__(kBlock, kWhole ? RR_TILES_WAVES_WHOLE : RR_TILES_WA
                                                                   TileSlices sl) {
     const unsigned long long rt_entry = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ int lds_stack[kLdsStack * kBlock];
+    __shared__ rr_f4v cam_lds[5];  // RR_TILES_CAM_LDS
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(lds_stack);
+    if (RR_TILES_CAM_LDS) store_cam((lds_f4w*)cam_lds, fc);  // stage_scene ends with a barrier
     int used;
     const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
-    tiles_body<kCount, kWhole>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry);
+    tiles_body<kCount, kWhole>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry,
+                               (const lds_f4w*)cam_lds);
 }
 
 #endif  // RR_TILES_TU
