@@ -890,8 +890,8 @@ struct TravStateQ6 {
     float tmin;
     Hit h;
     int node;
-    // (the last argument, TravState's scene radius, is unused: the margins are per node)
-    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_, float = 0.0f) {
+    // (no scene radius, unlike TravState::start: the margins are per node, q6_planes)
+    RR_D void start(float3 o_, float3 d_, float tmin_, float tmax_) {
         o = o_;
         sh = make_shear(d_);
         tmin = tmin_;

@@ -278,7 +278,8 @@ constexpr uint32_t kGlossyOne = 0x10000u;
 // diffuse_bounce >= max_diffuse_bounce or glossy_bounce >= max_glossy_bounce
 // after the increment; the caps here are >= 1 (setup_frame), so a cap of 0
 // ("direct light only") behaves as Cycles': the camera hit still scatters once.
-RR_D bool path_capped(const FrameConsts& fc, int bounce, uint32_t lob) {
+template <typename FC>
+RR_D bool path_capped(const FC& fc, int bounce, uint32_t lob) {
     return bounce >= fc.max_bounces || (int)(lob & 0xffffu) >= fc.max_diffuse || (int)(lob >> 16) >= fc.max_glossy;
 }
 
@@ -302,8 +303,10 @@ struct EmitShadow {
 // (emission, then NEE, then the next bounce), with the shadow-ray state dead
 // before the continuation's registers are needed. out.shadow still reports
 // that a shadow ray was traced.
-template <typename View, typename Shadow = EmitShadow>
-__device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const View& v, float3 o, float3 d,
+// FC: FrameConsts or ShadeConsts (the fields shade() reads: world,
+// clamp_indirect, the bounce caps, n_lights).
+template <typename View, typename Shadow = EmitShadow, typename FC = FrameConsts>
+__device__ __forceinline__ void shade(const FC& fc, int bounce, const View& v, float3 o, float3 d,
                                       float3 T, uint32_t lob, const Hit& h, uint32_t key, float3& L, ShadeOut& out,
                                       const Shadow& trace_shadow = Shadow{}) {
     out.cont = false;
@@ -452,6 +455,15 @@ __device__ __forceinline__ void shade(const FrameConsts& fc, int bounce, const V
     out.T = T;
     out.lob = lob + (glossy ? kGlossyOne : 1u);
 }
+
+// The frame constants shade() reads, for the out-of-line continuation of the
+// tile kernel's paths (tiles_continue): passed by value, because a reference
+// to the kernel's FrameConsts argument would put the whole struct in scratch.
+struct ShadeConsts {
+    float3 world;
+    float clamp_indirect;
+    int max_bounces, max_diffuse, max_glossy, n_lights, n_tris;
+};
 
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kMaxBlocksPerCu = 8;  // grid cap per CU
@@ -1685,6 +1697,56 @@ struct InlineShadow {
 // across the unit loop).
 RR_D uint32_t wave_count(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
+// Bounces 1 .. max_bounces of the tile kernel's paths whose camera hit
+// continues into the scene (the continuation does not leave a hull side):
+// out of line, so that the sample loop holds one shading point, bounce 0,
+// with its bounce-dependent terms folded (dimensions, clamp, Russian
+// roulette), and carries no bounce loop. On 04vs / 01 (a cube) no path gets
+// here but for a camera ray through an edge crack. The same shade() calls in
+// the same order as the loop it replaces, so the same bits. Measured against
+// the loop (three interleaved rounds, 04vs / 01 frame 5 / 20 at 128 spp):
+// solo 1.150 / 1.104 -> 1.068 / 1.021 ms, pipelined 995 / 1,030 -> 1,108 /
+// 1,167 frames/s. Returns L; the wave totals of its continuations and shadow
+// rays are added to this wave's LDS counters ctr[0..1] by its first active
+// lane. (Built without -amdgpu-prealloc-sgpr-spill-vgprs, which makes
+// hipcc 7.2 crash on the call.)
+template <bool kCount>
+__device__ __noinline__ float3 tiles_continue(ShadeConsts sc, LdsView v, float3 o, float3 d, float3 T, uint32_t lob,
+                                              uint32_t key, float3 L, TravStack& st, TravCount& ce, TravCount& cs,
+                                              lds_uint* ctr) {
+    uint32_t nc = 0, ns = 0;
+    bool live = true;
+    for (int b = 1; b <= sc.max_bounces; ++b) {
+        if (!__any(live)) break;
+        bool cont = false, shadow = false;
+        if (live) {
+            ShadeOut so;
+            const Hit h = ext_trace<kCount>(v, sc.n_tris, o, d, st, ce);
+            shade(sc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, sc.n_tris, st, cs});
+            cont = so.cont;
+            shadow = so.shadow;
+            if (so.cont && so.esc) {  // leaves a hull side: the world term, as in tiles_body
+                add_to(L, clamp_contrib(mul3(so.T, sc.world), sc.clamp_indirect));
+                live = false;
+            } else if (so.cont) {
+                o = so.o;
+                d = so.d;
+                T = so.T;
+                lob = so.lob;
+            } else {
+                live = false;
+            }
+        }
+        nc += wave_count(cont);
+        ns += wave_count(shadow);
+    }
+    if ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(__ballot(true))) {
+        ctr[0] += nc;
+        ctr[1] += ns;
+    }
+    return L;
+}
+
 // Sample-group slices of the box tiles (load balance: a heavy tile does not
 // run as one wave's unit at the end of the launch). Slab of tile t: one plane
 // per sample group g (group sum, 3 x 64 floats: x, y, z per lane), folded in
@@ -1713,7 +1775,8 @@ template <bool kCount, bool kWhole>
 RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
                      const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
-                     const TileSlices sl, unsigned long long rt_entry, const lds_f4w* cam_lds) {
+                     const TileSlices sl, unsigned long long rt_entry, const lds_f4w* cam_lds,
+                     lds_uint* cont_ctr) {
     const int stride = gridDim.x * kBlock;
     // counting instantiation only: the wave's shader-clock and real-time
     // counters at start and end give the clock the kernel ran at (read-only
@@ -1820,8 +1883,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         }
         for (int s = s_lo; s < s_run; ++s) {
             const uint32_t key = sample_key(pk, (uint32_t)s);
-            float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, T = mk3(1.0f, 1.0f, 1.0f), L = o;
-            uint32_t lob = 0;
+            float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, L = o;
             float tmin = 0.0f, tmax = -1.0f;
             bool culled = true;
 #if RR_TILES_CAM_LDS
@@ -1830,49 +1892,34 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             if (valid) camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
 #endif
             n_t0 += wave_count(!culled);
-            bool live = valid;
-            for (int b = 0; b <= fc.max_bounces; ++b) {
-                if (!__any(live)) break;
-                bool cont = false, shadow = false;
-                if (live) {
-                    ShadeOut so;
-                    Hit h;
-                    if (b == 0) {  // the camera ray against the tile's triangles (wave-uniform masks)
-                        set_miss(h, tmax);
-                        if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);
-                    } else {
-                        h = ext_trace<kCount>(v, fc.n_tris, o, d, st, ce);
-                    }
-                    shade(fc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, fc.n_tris, st, cs});
-                    cont = so.cont;
-                    shadow = so.shadow;
-                    if (so.cont && so.esc) {
-                        // the continuation leaves a hull side of its triangle
-                        // (hull_flags): its next hit is the world, added here as
-                        // bounce b + 1's shade() would add it (T x world, clamped),
-                        // and the path ends without that iteration
-                        add_to(L, clamp_contrib(mul3(so.T, fc.world), fc.clamp_indirect));
-                        live = false;
-                    } else if (so.cont) {
-                        o = so.o;
-                        d = so.d;
-                        T = so.T;
-                        lob = so.lob;
-                    } else {
-                        live = false;
-                    }
-                }
-                // counted with the whole wave active: a ballot inside `if (live)`
-                // would land in the counters of live lanes only, and lane 0 (the
-                // one flush_rays reads) may be dead by then
-                if (b == 0) {
-                    n_c0 += wave_count(cont);
-                    n_s0 += wave_count(shadow);
-                } else {
-                    n_c1 += wave_count(cont);
-                    n_s1 += wave_count(shadow);
+            bool cont = false, shadow = false;
+            if (valid) {  // bounce 0: the camera ray against the tile's triangles (wave-uniform masks)
+                Hit h;
+                set_miss(h, tmax);
+                if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);
+                ShadeOut so;
+                shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), 0u, h, key, L, so,
+                      InlineShadow<kCount>{v, fc.n_tris, st, cs});
+                cont = so.cont;
+                shadow = so.shadow;
+                if (so.cont && so.esc) {
+                    // the continuation leaves a hull side of its triangle
+                    // (hull_flags): its next hit is the world, added here as
+                    // bounce 1's shade() would add it (T x world, clamped),
+                    // and the path ends
+                    add_to(L, clamp_contrib(mul3(so.T, fc.world), fc.clamp_indirect));
+                } else if (so.cont) {  // bounces 1.. out of line
+                    const ShadeConsts sc{fc.world, fc.clamp_indirect, fc.max_bounces, fc.max_diffuse,
+                                         fc.max_glossy, fc.n_lights, fc.n_tris};
+                    L = tiles_continue<kCount>(sc, v, so.o, so.d, so.T, so.lob, key, L, st, ce, cs,
+                                               cont_ctr + 2 * (threadIdx.x >> 6));
                 }
             }
+            // counted with the whole wave active: a ballot inside `if (valid)`
+            // would land in the counters of valid lanes only, and lane 0 (the
+            // one flush_rays reads) may lie outside the image
+            n_c0 += wave_count(cont);
+            n_s0 += wave_count(shadow);
             add_to(P, L);
             group_end(s);
         }
@@ -1889,6 +1936,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             atomicAdd(&sl.cost[ty * to.tx + tx], (uint32_t)(__builtin_amdgcn_s_memrealtime() - u_start));
     }
     uint32_t* const tail = tot + camera_traced_slot(fc.max_bounces);
+    n_c1 = cont_ctr[2 * (threadIdx.x >> 6)];  // the later bounces (tiles_continue)
+    n_s1 = cont_ctr[2 * (threadIdx.x >> 6) + 1];
     flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tail, n_t0, ce.rays, cs.rays);
     if (kCount) {
         flush_counts(tc, 0, cp.nodes, cp.tris);
@@ -1932,14 +1981,16 @@ __global__ __launch_bounds__(kBlock, kWhole ? RR_TILES_WAVES_WHOLE : RR_TILES_WA
                                                                   TileSlices sl) {
     const unsigned long long rt_entry = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ int lds_stack[kLdsStack * kBlock];
-    __shared__ rr_f4v cam_lds[5];  // RR_TILES_CAM_LDS
+    __shared__ rr_f4v cam_lds[5];                      // RR_TILES_CAM_LDS
+    __shared__ uint32_t cont_ctr[2 * kWavesPerBlock];  // tiles_continue's ray counts per wave
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(lds_stack);
     if (RR_TILES_CAM_LDS) store_cam((lds_f4w*)cam_lds, fc);  // stage_scene ends with a barrier
+    if (threadIdx.x < 2 * kWavesPerBlock) cont_ctr[threadIdx.x] = 0u;
     int used;
     const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
     tiles_body<kCount, kWhole>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry,
-                               (const lds_f4w*)cam_lds);
+                               (const lds_f4w*)cam_lds, (lds_uint*)cont_ctr);
 }
 
 #endif  // RR_TILES_TU

@@ -16,7 +16,7 @@ import sys
 CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                     "diploma_thesis-distributed_rendering_of_cgi_using_a_render_cluster_amd", "csrc")
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-TU_FLAGS = {"tiles.hip": os.environ.get("RR_TILES_TUFLAGS", "-fno-slp-vectorize -mllvm -amdgpu-prealloc-sgpr-spill-vgprs").split()}
+TU_FLAGS = {"tiles.hip": os.environ.get("RR_TILES_TUFLAGS", "-fno-slp-vectorize").split()}
 
 
 def usage(src, extra):
