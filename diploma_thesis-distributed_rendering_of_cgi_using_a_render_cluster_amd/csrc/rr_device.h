@@ -952,7 +952,7 @@ struct TravStateQ6 {
 // nodes are visited, the same triangles tested, only in another interleaving
 // across lanes, and the accept rule makes the hit the same (bit-exact).
 #ifndef RR_LEAF_PHASE
-#define RR_LEAF_PHASE 32
+#define RR_LEAF_PHASE 12
 #endif
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6D {

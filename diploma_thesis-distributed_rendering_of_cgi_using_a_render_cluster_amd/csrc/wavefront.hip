@@ -173,9 +173,8 @@ RR_D ScreenCull screen_cull(const FrameConsts& fc, NodeP nodes) {
 
 // culled (optional): set when the ray's subpixel position is outside the
 // scene's screen rectangle (the ray misses everything).
-// CF: FrameConsts, or CamFields (the camera fields of k_tiles, read from LDS).
-template <typename FloatP, typename CF = FrameConsts>
-__device__ __forceinline__ void camera_ray_xy(const CF& fc, FloatP filt, int px, int py,
+template <typename FloatP>
+__device__ __forceinline__ void camera_ray_xy(const FrameConsts& fc, FloatP filt, int px, int py,
                                               uint32_t key, float3& o, float3& d, float& tmin, float& tmax,
                                               const ScreenCull* cull = nullptr, bool* culled = nullptr) {
     // the subpixel pair: the 16-bit halves of the path key itself (a hash
@@ -212,47 +211,6 @@ __device__ __forceinline__ void camera_ray(const FrameConsts& fc, FloatP filt, i
                                            const ScreenCull* cull = nullptr, bool* culled = nullptr) {
     const int py = (int)fc.div_w.div((uint32_t)pix);
     camera_ray_xy(fc, filt, pix - py * fc.W, py, key, o, d, tmin, tmax, cull, culled);
-}
-
-// The camera fields of FrameConsts that camera_ray_xy reads. RR_TILES_CAM_LDS
-// (A/B): k_tiles stages them in LDS (5 float4) and reads them per sample with
-// volatile loads, so that they hold no scalar registers across the sample loop
-// (the kernel's arguments fill the SGPR file and spill into VGPR lanes).
-struct CamFields {
-    float3 cam_pos, cam_right, cam_up, cam_back;
-    float half_w, half_h, clip_start, clip_end, inv_w2, inv_h2;
-};
-#ifndef RR_TILES_CAM_LDS
-#define RR_TILES_CAM_LDS 0
-#endif
-RR_D float4 lds_ld4_volatile(const lds_f4w* p) {
-    const rr_f4v v = *(const volatile lds_f4w*)p;
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-RR_D CamFields load_cam(const lds_f4w* q) {
-    const float4 a = lds_ld4_volatile(q), b = lds_ld4_volatile(q + 1), c = lds_ld4_volatile(q + 2),
-                 d = lds_ld4_volatile(q + 3), e = lds_ld4_volatile(q + 4);
-    CamFields f;
-    f.cam_pos = xyz(a);
-    f.half_w = a.w;
-    f.cam_right = xyz(b);
-    f.half_h = b.w;
-    f.cam_up = xyz(c);
-    f.inv_w2 = c.w;
-    f.cam_back = xyz(d);
-    f.inv_h2 = d.w;
-    f.clip_start = e.x;
-    f.clip_end = e.y;
-    return f;
-}
-RR_D void store_cam(lds_f4w* q, const FrameConsts& fc) {
-    if (threadIdx.x == 0) {
-        q[0] = rr_f4v{fc.cam_pos.x, fc.cam_pos.y, fc.cam_pos.z, fc.half_w};
-        q[1] = rr_f4v{fc.cam_right.x, fc.cam_right.y, fc.cam_right.z, fc.half_h};
-        q[2] = rr_f4v{fc.cam_up.x, fc.cam_up.y, fc.cam_up.z, fc.inv_w2};
-        q[3] = rr_f4v{fc.cam_back.x, fc.cam_back.y, fc.cam_back.z, fc.inv_h2};
-        q[4] = rr_f4v{fc.clip_start, fc.clip_end, 0.0f, 0.0f};
-    }
 }
 
 // Staged material word of LDS-resident scenes: material id | hull_flags << kHullShift.
@@ -840,9 +798,15 @@ constexpr int kTraceWavesPerBlock = kTraceBlock / 64;
 // Hierarchy of the split path: the PLOC BVH2 collapsed to the quantised BVH4
 // (measured against walking the PLOC BVH2 itself, C5 / 02 / 03 frames at 16 /
 // 64 / 64 spp: 191 -> 139, 174 -> 149, 192 -> 160 ms).
-// RR_LEAF_DEFER (A/B): 1 = the walk with postponed leaf tests (TravStateQ6D).
+// The walk with postponed leaf tests (TravStateQ6D, rr_device.h), leaf phase
+// once 12 of the lanes have leaves pending. Per frame slice against testing
+// leaves at once (TravStateQ6; 02 / 03 at 64 spp, C5 at 16 spp, two
+// interleaved rounds, profiles/r5_ab_leaf_defer.txt): 87.4 / 94.8 / 73.0 ->
+// 82.7 / 89.1 / 70.3 ms (extension and shadow traversal -6 to -9 %); a phase
+// threshold of 4 / 8 / 16 / 24 / 32 / 48 lanes: 86.6 / 83.6 / 82.5 / 85.2 /
+// 91.1 / 118.6 ms on 02. RR_LEAF_DEFER=0 (A/B): leaves at once.
 #ifndef RR_LEAF_DEFER
-#define RR_LEAF_DEFER 0
+#define RR_LEAF_DEFER 1
 #endif
 template <bool kAnyHit, bool kCount>
 using SplitTrav = typename std::conditional<RR_LEAF_DEFER != 0, TravStateQ6D<kAnyHit, kCount>,
@@ -1775,8 +1739,7 @@ template <bool kCount, bool kWhole>
 RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restrict__ tile_ctr, float4* __restrict__ film,
                      const float* __restrict__ srgb, uchar4* __restrict__ out, uint32_t* __restrict__ tot,
                      int32_t* __restrict__ spill, unsigned long long* __restrict__ tc, lds_int* stack,
-                     const TileSlices sl, unsigned long long rt_entry, const lds_f4w* cam_lds,
-                     lds_uint* cont_ctr) {
+                     const TileSlices sl, unsigned long long rt_entry, lds_uint* cont_ctr) {
     const int stride = gridDim.x * kBlock;
     // counting instantiation only: the wave's shader-clock and real-time
     // counters at start and end give the clock the kernel ran at (read-only
@@ -1886,11 +1849,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             float3 o = mk3(0.0f, 0.0f, 0.0f), d = o, L = o;
             float tmin = 0.0f, tmax = -1.0f;
             bool culled = true;
-#if RR_TILES_CAM_LDS
-            if (valid) camera_ray_xy(load_cam(cam_lds), v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
-#else
             if (valid) camera_ray_xy(fc, v.filter, px, py, key, o, d, tmin, tmax, &cull, &culled);
-#endif
             n_t0 += wave_count(!culled);
             bool cont = false, shadow = false;
             if (valid) {  // bounce 0: the camera ray against the tile's triangles (wave-uniform masks)
@@ -1981,16 +1940,14 @@ __global__ __launch_bounds__(kBlock, kWhole ? RR_TILES_WAVES_WHOLE : RR_TILES_WA
                                                                   TileSlices sl) {
     const unsigned long long rt_entry = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ int lds_stack[kLdsStack * kBlock];
-    __shared__ rr_f4v cam_lds[5];                      // RR_TILES_CAM_LDS
     __shared__ uint32_t cont_ctr[2 * kWavesPerBlock];  // tiles_continue's ray counts per wave
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(lds_stack);
-    if (RR_TILES_CAM_LDS) store_cam((lds_f4w*)cam_lds, fc);  // stage_scene ends with a barrier
-    if (threadIdx.x < 2 * kWavesPerBlock) cont_ctr[threadIdx.x] = 0u;
+    if (threadIdx.x < 2 * kWavesPerBlock) cont_ctr[threadIdx.x] = 0u;  // stage_scene ends with a barrier
     int used;
     const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
     tiles_body<kCount, kWhole>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry,
-                               (const lds_f4w*)cam_lds, (lds_uint*)cont_ctr);
+                               (lds_uint*)cont_ctr);
 }
 
 #endif  // RR_TILES_TU
