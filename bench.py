@@ -655,23 +655,44 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=No
                 "frac": round(ach / HBM_PEAK_GBS, 4), **hbm,
                 "note": "no PMC summary: achieved = SURVEY 8(d) algorithmic bytes per launch / launch time, which "
                         "prices every node visit and triangle test as HBM traffic (an upper bound, not a measurement)"}
-    # the bound from the counters: the PMC HBM rate against the peak, and how
-    # much of a wave's life it waits (SQ_WAIT_ANY / SQ_WAVE_CYCLES). Below half
-    # the peak with waves waiting more than half their lives, the kernel is
-    # bound by the latency of its gathers (cache hits included), not bandwidth.
+    # the bound from the counters: the PMC HBM rate against the peak, how much
+    # of a wave's life it waits (SQ_WAIT_ANY / SQ_WAVE_CYCLES) and its vector
+    # issue rate (SQ_INSTS_VALU per launch / launch time against 0.5 wave-
+    # instructions per clock per SIMD at 2.4 GHz). At half the HBM peak or
+    # more: hbm. Below it, waves waiting more than half their lives: bound by
+    # the latency of the gathers (cache hits included), not bandwidth.
+    # Otherwise the waves are issuing: valu (achieved / frac are then the issue
+    # rate, the HBM rate stays beside it).
     ach = e["traffic_bytes"] / (avg_ms * 1e-3) / 1e9
     wf = e.get("wait_frac")
-    bound = "latency" if (ach < 0.5 * HBM_PEAK_GBS and wf is not None and wf > 0.5) else "hbm"
+    v = e.get("SQ_INSTS_VALU")
+    issue = v / (avg_ms * 1e-3) if v else None
+    if ach >= 0.5 * HBM_PEAK_GBS:
+        bound = "hbm"
+    elif wf is not None and wf > 0.5:
+        bound = "latency"
+    else:
+        bound = "valu" if issue else "hbm"
     resident = n * (64.0 + 48.0) < MALL_BYTES  # hierarchy + triangles fit in the 256 MB MALL
-    return {**base, "bound": bound, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), **lat, **hbm,
-            "scene_fits_mall": resident,
-            "note": "achieved = PMC HBM bytes per launch (FETCH_SIZE x fetch_scale, 1 for these 64 B gathers per "
-                    "tools/fetch_probe.hip, + WRITE_SIZE; FETCH_SIZE counts Infinity-Cache hits, so an upper "
-                    "bound on HBM reads) / the bench's launch time; bound = latency when that is below half the "
-                    "peak and waves wait more than half their lives (wait_frac), else hbm; frac_survey_formula = "
-                    "SURVEY 8(d)'s algorithmic bytes (64 B per node visit, 48 B per triangle test + ray/hit "
-                    "stream, every one priced as HBM traffic) over the same time"}
+    out = {**base, "bound": bound, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), **lat, **hbm,
+           "hbm_gbs_pmc": round(ach, 2), "hbm_frac_pmc": round(ach / HBM_PEAK_GBS, 4),
+           "scene_fits_mall": resident,
+           "note": "hbm_gbs_pmc = PMC HBM bytes per launch (FETCH_SIZE x fetch_scale, 1 for these 64 B gathers per "
+                   "tools/fetch_probe.hip, + WRITE_SIZE; FETCH_SIZE counts Infinity-Cache hits, so an upper "
+                   "bound on HBM reads) / the bench's launch time; bound = hbm at half the HBM peak or more, "
+                   "else latency when waves wait more than half their lives (wait_frac), else valu (issue rate "
+                   "SQ_INSTS_VALU / launch time vs 0.5 wave-instr/clk/SIMD x 1024 SIMDs at 2.4 GHz: achieved / "
+                   "frac are then that rate); frac_survey_formula = SURVEY 8(d)'s algorithmic bytes (64 B per "
+                   "node visit, 48 B per triangle test + ray/hit stream, every one priced as HBM traffic) over the "
+                   "same time"}
+    if issue:
+        out["valu_per_launch"] = round(v)
+        out["valu_issue_frac"] = round(issue / valu_peak_per_s(), 4)
+    if bound == "valu":
+        out.update({"achieved": round(issue / 1e9, 1), "peak": round(valu_peak_per_s() / 1e9, 1),
+                    "unit": "G wave-instr/s", "frac": round(issue / valu_peak_per_s(), 4)})
+    return out
 
 
 def main():

@@ -261,12 +261,23 @@ struct EmitShadow {
 // (emission, then NEE, then the next bounce), with the shadow-ray state dead
 // before the continuation's registers are needed. out.shadow still reports
 // that a shadow ray was traced.
+// ... and the continuation: handed back in ShadeOut (out.o / d / T / lob), or,
+// with an in-place handler (Cont::kInline: called as on_cont(origin,
+// direction, throughput, lobe counters, leaves a hull side, L)), taken over at
+// the point it is sampled, so that its ray is never held past shade() (k_tiles:
+// held to the sample loop's join, the compiler spilled it to scratch in every
+// sample, most of that kernel's HBM write traffic).
+struct EmitCont {
+    static constexpr bool kInline = false;
+    RR_D void operator()(float3, float3, float3, uint32_t, bool, float3&) const {}
+};
+
 // FC: FrameConsts or ShadeConsts (the fields shade() reads: world,
 // clamp_indirect, the bounce caps, n_lights).
-template <typename View, typename Shadow = EmitShadow, typename FC = FrameConsts>
+template <typename View, typename Shadow = EmitShadow, typename FC = FrameConsts, typename Cont = EmitCont>
 __device__ __forceinline__ void shade(const FC& fc, int bounce, const View& v, float3 o, float3 d,
                                       float3 T, uint32_t lob, const Hit& h, uint32_t key, float3& L, ShadeOut& out,
-                                      const Shadow& trace_shadow = Shadow{}) {
+                                      const Shadow& trace_shadow = Shadow{}, const Cont& on_cont = Cont{}) {
     out.cont = false;
     out.shadow = false;
     out.esc = false;
@@ -408,6 +419,10 @@ __device__ __forceinline__ void shade(const FC& fc, int bounce, const View& v, f
         T = mk3(T.x * iq, T.y * iq, T.z * iq);
     }
     out.cont = true;
+    if constexpr (Cont::kInline) {
+        on_cont(Po, wi, T, lob + (glossy ? kGlossyOne : 1u), esc, L);
+        return;
+    }
     out.o = Po;
     out.d = wi;
     out.T = T;
@@ -1597,16 +1612,12 @@ RR_D TileOrder uniform_order(TileOrder t) {
 // the chunk-0 counter pairs: {0, 1} = bounce 0, {2, 3} = all later bounces
 // (rr_api.cpp fill_stats sums the pairs); tail = the chunk's words from
 // camera_traced_slot on: [0] camera rays traced, [2] / [3] continuations /
-// shadow rays traversed (per lane: the out-of-line traversals, TravCount::rays;
-// the other continuations and shadow rays left a hull side and were resolved
-// without a traversal, rr_frame_stats *_escaped).
+// shadow rays traversed (the out-of-line traversals; the other continuations
+// and shadow rays left a hull side and were resolved without a traversal,
+// rr_frame_stats *_escaped).
 RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint32_t c1, uint32_t s1,
                      uint32_t* __restrict__ tail, uint32_t t0, uint32_t ext_traced, uint32_t sh_traced) {
-    for (int off = 32; off > 0; off >>= 1) {
-        ext_traced += (uint32_t)__shfl_xor((int)ext_traced, off);
-        sh_traced += (uint32_t)__shfl_xor((int)sh_traced, off);
-    }
-    // the other counts are wave totals already (wave_count): lane 0 adds them
+    // the counts are wave totals (wave_count, TileTrav::wctr): lane 0 adds them
     const uint32_t v[4] = {c0, s0, c1, s1};
     if ((threadIdx.x & 63) == 0) {
         for (int k = 0; k < 4; ++k)
@@ -1625,21 +1636,55 @@ RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint3
 // frames/s; solo launches -1 %). Their state goes through the call's stack
 // frame; the register budget stays at 4 waves per SIMD (5 measured slower
 // solo, +-0 pipelined).
-// cnt.rays counts the calls in every frame (the secondary rays k_tiles traverses:
-// the rest left a hull side, rr_frame_stats *_escaped), at no cost to the
-// sample loop: cnt lives in memory (its address is taken).
-template <bool kCount>
-__device__ __noinline__ bool shadow_trace(const LdsView& v, int n_tris, float3 so, float3 sd, float dist, TravStack& st,
-                                          TravCount& cnt) {
-    ++cnt.rays;
-    Hit hs;
-    return traverse<true, kCount>(v.nodes, v.tris, n_tris, so, sd, 0.0f, dist, st, hs, cnt);
+// Everything the out-of-line traversals need, passed by value: the traversal
+// stack's LDS and HBM parts (the TravStack is built in the callee), the frame's
+// drop counter, this wave's LDS counters (wctr: [0] continuations and [1]
+// shadow rays of bounces >= 1, tiles_continue; [2] continuation and [3] shadow
+// rays traversed, rr_frame_stats *_escaped) and the counting pass's totals
+// (tc, null otherwise). Round 4 passed the stack and the counters by
+// reference, which put them (and the LdsView) in scratch: written by every
+// wave at launch, and every wave's scratch lines went back to HBM — most of
+// k_tiles' 124-140 MB of PMC traffic per launch against 41 MB compulsory.
+struct TileTrav {
+    lds_int* lds;
+    int* spill;
+    int stride;
+    uint32_t* drops;
+    lds_uint* wctr;
+    unsigned long long* tc;
+};
+// Active lanes of the wave whose predicate holds: the tile kernel's ray
+// counters are wave totals kept in scalar registers (no per-lane VGPRs live
+// across the unit loop).
+RR_D uint32_t wave_count(bool p) { return (uint32_t)__popcll(__ballot(p)); }
+// *p += n by the first active lane (n: a wave total).
+RR_D void wave_add(lds_uint* p, uint32_t n) {
+    if ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(__ballot(true))) *p += n;
 }
 template <bool kCount>
-__device__ __noinline__ Hit ext_trace(const LdsView& v, int n_tris, float3 o, float3 d, TravStack& st, TravCount& cnt) {
-    ++cnt.rays;
+__device__ __noinline__ bool shadow_trace(LdsView v, int n_tris, float3 so, float3 sd, float dist, TileTrav tt) {
+    wave_add(tt.wctr + 3, wave_count(true));
+    TravStack st{tt.lds, tt.spill, tt.stride, 0, tt.drops};
+    TravCount cnt;
+    Hit hs;
+    const bool occ = traverse<true, kCount>(v.nodes, v.tris, n_tris, so, sd, 0.0f, dist, st, hs, cnt);
+    if (kCount) {
+        atomicAdd(&tt.tc[4], (unsigned long long)cnt.nodes);
+        atomicAdd(&tt.tc[5], (unsigned long long)cnt.tris);
+    }
+    return occ;
+}
+template <bool kCount>
+__device__ __noinline__ Hit ext_trace(LdsView v, int n_tris, float3 o, float3 d, TileTrav tt) {
+    wave_add(tt.wctr + 2, wave_count(true));
+    TravStack st{tt.lds, tt.spill, tt.stride, 0, tt.drops};
+    TravCount cnt;
     Hit h;
     traverse<false, kCount>(v.nodes, v.tris, n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
+    if (kCount) {
+        atomicAdd(&tt.tc[2], (unsigned long long)cnt.nodes);
+        atomicAdd(&tt.tc[3], (unsigned long long)cnt.tris);
+    }
     return h;
 }
 // The tile kernel's shadow rays, traced inside shade() (any hit over the
@@ -1647,19 +1692,13 @@ __device__ __noinline__ Hit ext_trace(const LdsView& v, int n_tris, float3 o, fl
 template <bool kCount>
 struct InlineShadow {
     static constexpr bool kInline = true;
-    const LdsView& v;
+    LdsView v;
     int n_tris;
-    TravStack& st;
-    TravCount& cnt;
+    TileTrav tt;
     RR_D bool operator()(float3 so, float3 sd, float dist) const {
-        return shadow_trace<kCount>(v, n_tris, so, sd, dist, st, cnt);
+        return shadow_trace<kCount>(v, n_tris, so, sd, dist, tt);
     }
 };
-
-// Active lanes of the wave whose predicate holds: the tile kernel's ray
-// counters are wave totals kept in scalar registers (no per-lane VGPRs live
-// across the unit loop).
-RR_D uint32_t wave_count(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
 // Bounces 1 .. max_bounces of the tile kernel's paths whose camera hit
 // continues into the scene (the continuation does not leave a hull side):
@@ -1671,13 +1710,11 @@ RR_D uint32_t wave_count(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 // the loop (three interleaved rounds, 04vs / 01 frame 5 / 20 at 128 spp):
 // solo 1.150 / 1.104 -> 1.068 / 1.021 ms, pipelined 995 / 1,030 -> 1,108 /
 // 1,167 frames/s. Returns L; the wave totals of its continuations and shadow
-// rays are added to this wave's LDS counters ctr[0..1] by its first active
-// lane. (Built without -amdgpu-prealloc-sgpr-spill-vgprs, which makes
-// hipcc 7.2 crash on the call.)
+// rays go to this wave's LDS counters tt.wctr[0..1]. (Built without
+// -amdgpu-prealloc-sgpr-spill-vgprs, which makes hipcc 7.2 crash on the call.)
 template <bool kCount>
 __device__ __noinline__ float3 tiles_continue(ShadeConsts sc, LdsView v, float3 o, float3 d, float3 T, uint32_t lob,
-                                              uint32_t key, float3 L, TravStack& st, TravCount& ce, TravCount& cs,
-                                              lds_uint* ctr) {
+                                              uint32_t key, float3 L, TileTrav tt) {
     uint32_t nc = 0, ns = 0;
     bool live = true;
     for (int b = 1; b <= sc.max_bounces; ++b) {
@@ -1685,8 +1722,8 @@ __device__ __noinline__ float3 tiles_continue(ShadeConsts sc, LdsView v, float3 
         bool cont = false, shadow = false;
         if (live) {
             ShadeOut so;
-            const Hit h = ext_trace<kCount>(v, sc.n_tris, o, d, st, ce);
-            shade(sc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, sc.n_tris, st, cs});
+            const Hit h = ext_trace<kCount>(v, sc.n_tris, o, d, tt);
+            shade(sc, b, v, o, d, T, lob, h, key, L, so, InlineShadow<kCount>{v, sc.n_tris, tt});
             cont = so.cont;
             shadow = so.shadow;
             if (so.cont && so.esc) {  // leaves a hull side: the world term, as in tiles_body
@@ -1704,12 +1741,34 @@ __device__ __noinline__ float3 tiles_continue(ShadeConsts sc, LdsView v, float3 
         nc += wave_count(cont);
         ns += wave_count(shadow);
     }
-    if ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(__ballot(true))) {
-        ctr[0] += nc;
-        ctr[1] += ns;
-    }
+    wave_add(tt.wctr, nc);
+    wave_add(tt.wctr + 1, ns);
     return L;
 }
+
+// RR_TILES_CONT_INPLACE: bit 0 the whole-tile variant, bit 1 the sample-group
+// variant take the continuation inside shade() (else after it, from ShadeOut).
+#ifndef RR_TILES_CONT_INPLACE
+#define RR_TILES_CONT_INPLACE 1
+#endif
+// The bounce-0 continuation of k_tiles, taken over inside shade(): a ray that
+// leaves a hull side of its triangle meets the world (T x world, clamped, as
+// bounce 1's shade() would add it, and the path ends); any other goes on out
+// of line (tiles_continue).
+template <bool kCount>
+struct TileCont {
+    static constexpr bool kInline = true;
+    ShadeConsts sc;
+    LdsView v;
+    TileTrav tt;
+    uint32_t key;
+    RR_D void operator()(float3 o, float3 d, float3 T, uint32_t lob, bool esc, float3& L) const {
+        if (esc)
+            add_to(L, clamp_contrib(mul3(T, sc.world), sc.clamp_indirect));
+        else
+            L = tiles_continue<kCount>(sc, v, o, d, T, lob, key, L, tt);
+    }
+};
 
 // Sample-group slices of the box tiles (load balance: a heavy tile does not
 // run as one wave's unit at the end of the launch). Slab of tile t: one plane
@@ -1749,8 +1808,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         clk0 = __builtin_amdgcn_s_memtime();
         rt0 = __builtin_amdgcn_s_memrealtime();
     }
-    TravStack st{stack, spill, stride, 0, tot + drops_slot(fc.max_bounces)};
-    TravCount cp, ce, cs;
+    const TileTrav tt{stack, spill, stride, tot + drops_slot(fc.max_bounces), cont_ctr + 4 * (threadIdx.x >> 6), tc};
+    TravCount cp;
     uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0, n_t0 = 0;
     // The screen rectangle and the tile order come from the root node in LDS,
     // so the compiler cannot tell they are wave-uniform and would keep (and
@@ -1857,22 +1916,19 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
                 set_miss(h, tmax);
                 if (!culled) camera_hit<kCount>(v, cm0, cm1, d, tmin, tmax, h, cp);
                 ShadeOut so;
-                shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), 0u, h, key, L, so,
-                      InlineShadow<kCount>{v, fc.n_tris, st, cs});
+                const ShadeConsts sc{fc.world, fc.clamp_indirect, fc.max_bounces, fc.max_diffuse, fc.max_glossy,
+                                     fc.n_lights, fc.n_tris};
+                if constexpr ((RR_TILES_CONT_INPLACE & (kWhole ? 1 : 2)) != 0) {
+                    // the continuation (escape to the world, or bounces 1.. out of line) is taken inside
+                    shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), 0u, h, key, L, so,
+                          InlineShadow<kCount>{v, fc.n_tris, tt}, TileCont<kCount>{sc, v, tt, key});
+                } else {
+                    shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), 0u, h, key, L, so,
+                          InlineShadow<kCount>{v, fc.n_tris, tt});
+                    if (so.cont) TileCont<kCount>{sc, v, tt, key}(so.o, so.d, so.T, so.lob, so.esc, L);
+                }
                 cont = so.cont;
                 shadow = so.shadow;
-                if (so.cont && so.esc) {
-                    // the continuation leaves a hull side of its triangle
-                    // (hull_flags): its next hit is the world, added here as
-                    // bounce 1's shade() would add it (T x world, clamped),
-                    // and the path ends
-                    add_to(L, clamp_contrib(mul3(so.T, fc.world), fc.clamp_indirect));
-                } else if (so.cont) {  // bounces 1.. out of line
-                    const ShadeConsts sc{fc.world, fc.clamp_indirect, fc.max_bounces, fc.max_diffuse,
-                                         fc.max_glossy, fc.n_lights, fc.n_tris};
-                    L = tiles_continue<kCount>(sc, v, so.o, so.d, so.T, so.lob, key, L, st, ce, cs,
-                                               cont_ctr + 2 * (threadIdx.x >> 6));
-                }
             }
             // counted with the whole wave active: a ballot inside `if (valid)`
             // would land in the counters of valid lanes only, and lane 0 (the
@@ -1895,13 +1951,11 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             atomicAdd(&sl.cost[ty * to.tx + tx], (uint32_t)(__builtin_amdgcn_s_memrealtime() - u_start));
     }
     uint32_t* const tail = tot + camera_traced_slot(fc.max_bounces);
-    n_c1 = cont_ctr[2 * (threadIdx.x >> 6)];  // the later bounces (tiles_continue)
-    n_s1 = cont_ctr[2 * (threadIdx.x >> 6) + 1];
-    flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tail, n_t0, ce.rays, cs.rays);
+    n_c1 = tt.wctr[0];  // the later bounces (tiles_continue)
+    n_s1 = tt.wctr[1];
+    flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tail, n_t0, tt.wctr[2], tt.wctr[3]);
     if (kCount) {
         flush_counts(tc, 0, cp.nodes, cp.tris);
-        flush_counts(tc, 2, ce.nodes, ce.tris);
-        flush_counts(tc, 4, cs.nodes, cs.tris);
         const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
         if ((threadIdx.x & 63) == 0) {  // device.hpp kTravWords
             atomicAdd(&tc[6], clk1 - clk0);
@@ -1940,10 +1994,10 @@ __global__ __launch_bounds__(kBlock, kWhole ? RR_TILES_WAVES_WHOLE : RR_TILES_WA
                                                                   TileSlices sl) {
     const unsigned long long rt_entry = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ int lds_stack[kLdsStack * kBlock];
-    __shared__ uint32_t cont_ctr[2 * kWavesPerBlock];  // tiles_continue's ray counts per wave
+    __shared__ uint32_t cont_ctr[4 * kWavesPerBlock];  // per wave: TileTrav::wctr
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(lds_stack);
-    if (threadIdx.x < 2 * kWavesPerBlock) cont_ctr[threadIdx.x] = 0u;  // stage_scene ends with a barrier
+    if (threadIdx.x < 4 * kWavesPerBlock) cont_ctr[threadIdx.x] = 0u;  // stage_scene ends with a barrier
     int used;
     const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
     tiles_body<kCount, kWhole>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry,

@@ -110,8 +110,10 @@ def test_split_path_bound_comes_from_the_counters(tmp_path):
     assert abs(r["frac"] - 0.25) < 1e-9 and "frac_survey_formula" in r
     fast = {"traffic_bytes": 6e12 * 2.0e-3, "wait_frac": 0.7}  # 6 TB/s
     assert _roof(tmp_path, fast, 10_000_000)["bound"] == "hbm"
-    busy = {"traffic_bytes": 1e12 * 2.0e-3, "wait_frac": 0.3}  # slow, but the waves issue
-    assert _roof(tmp_path, busy, 1000)["bound"] == "hbm"
+    busy = {"traffic_bytes": 1e12 * 2.0e-3, "wait_frac": 0.3, "SQ_INSTS_VALU": 614.4e9 * 2.0e-3}
+    r = _roof(tmp_path, busy, 1000)  # slow memory, but the waves issue: half the VALU issue peak
+    assert r["bound"] == "valu" and r["unit"] == "G wave-instr/s" and abs(r["frac"] - 0.5) < 1e-3
+    assert r["hbm_gbs_pmc"] == 1000.0
 
 
 def test_kernels_pmc_block():
