@@ -1167,6 +1167,9 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
 // A push beyond both parts (a hierarchy some 880 levels deep) is dropped and
 // counted at once.
 constexpr int kPacketStack = 128;             // a node pushes <= 5: about 25 levels of the 6-wide hierarchy in LDS
+#ifndef RR_CAM_BEAM
+#define RR_CAM_BEAM 1  // packet_trace_beam for camera packets (0: packet_trace, per-lane box tests)
+#endif
 constexpr int kPacketSpill = kSpillStack * 64;  // per wave in HBM (DevPaths::spill holds kSpillStack per lane)
 template <bool kCount, int kStack = kPacketStack>
 RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk,
@@ -1239,6 +1242,150 @@ RR_D void packet_trace(const QNode6* __restrict__ nodes, const TriPack* __restri
     }
 }
 
+// Camera packets with one box test per child for the whole packet (the
+// beam), RR_CAM_BEAM (default; camera traversal per 02 / 03 / C5 frame slice
+// 10.06 / 11.08 / 11.48 -> 7.26 / 8.02 / 9.95 ms, whole slices -2.6 / -3.0 /
+// -1.5 %, profiles/r5_ab_camera_beam.txt). Camera rays share their origin exactly (camera_ray_xy:
+// fc.cam_pos, a pinhole) and their directions differ by a pixel's footprint, so
+// the per-lane box tests of packet_trace compute 64 nearly equal answers per
+// child. Here lanes 0..5 test child 0..5 once for the packet over the interval
+// of the lanes' reciprocal directions: per axis the plane distances of the
+// quantised box, widened by twice the node's margin m (q6_planes widens them
+// by m), times the end of the interval that gives the smallest near / largest
+// far distance; a child passes when the largest near (and the smallest tmin)
+// is at most the smallest far (and the largest closest hit so far). The
+// per-lane test's rounding stays under m/8 |iq| (every plane distance is at
+// most 2^19 m, kBoxMargin), and so does this test's, so every child some
+// lane's own test opens is opened (a superset; an axis whose reciprocals
+// change sign in the packet does not cull). Leaf children that pass are
+// tested by every lane that has a ray, with the lane's own watertight test and
+// accept rule: each ray meets at least the triangles its own walk would test,
+// and a triangle it meets beyond them is one whose box its own test rejects
+// (so no hit of it is accepted), so the closest hit is the same (bit-exact).
+// Internal children that pass are visited nearest first by the packet's near
+// distance, the others pushed as in packet_trace (same stack and HBM part).
+template <bool kCount, int kStack = kPacketStack>
+RR_D void packet_trace_beam(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk,
+                            int* __restrict__ gstk, uint32_t* __restrict__ drops, bool act, float3 o, float3 d,
+                            float tmin, Hit& h, TravCount& cnt) {
+    const uint64_t am = __ballot(act);
+    if (!am) return;
+    const int rl = (int)__builtin_ctzll(am);
+    const float ox = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, o.x), rl));
+    const float oy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, o.y), rl));
+    const float oz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, o.z), rl));
+    const int lane = (int)(threadIdx.x & 63);
+    const Shear sh = make_shear(d);
+    const float3 iq = mk3(q4_rcp(d.x), q4_rcp(d.y), q4_rcp(d.z));
+    // packet intervals over the active lanes (wave-uniform)
+    auto wred = [&](float x, bool mx) {
+        x = act ? x : (mx ? -__builtin_huge_valf() : __builtin_huge_valf());
+        for (int off = 32; off > 0; off >>= 1) {
+            const float y = __shfl_xor(x, off);
+            x = mx ? fmaxf(x, y) : fminf(x, y);
+        }
+        return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+    };
+    const float ilx = wred(iq.x, false), ily = wred(iq.y, false), ilz = wred(iq.z, false);
+    const float ihx = wred(iq.x, true), ihy = wred(iq.y, true), ihz = wred(iq.z, true);
+    const float t_lo = wred(tmin, false);
+    float t_hi = wred(h.t, true);
+    int node = 0, sp = 0;
+    for (;;) {
+        const QNode6 nd = nodes[node];  // wave-uniform: scalar loads
+        const uint32_t imask = q6_inner(nd);
+        if (kCount && act) ++cnt.nodes;
+        // this lane's child (lanes 0..5) against the packet
+        bool pass = false;
+        float tnear = 0.0f;
+        if (lane < kQWidth) {
+            const uint32_t eb = (uint32_t)f2i(nd.org.w);
+            const float dx = nd.org.x - ox, dy = nd.org.y - oy, dz = nd.org.z - oz;
+            const float m2 = 2.0f * fmaf(fmaxf(fmaxf(fabsf(dx), fabsf(dy)), fabsf(dz)), kBoxMargin,
+                                         ldexpf(255.0f * kBoxMargin, (int)((nd.c.w >> 8) & 255u) - 128));
+            const int c = lane;
+            const int s8 = c < 4 ? 8 * c : 0;
+            const int s16 = c == 5 ? 8 : 0;
+            // children 0..3: a byte of a.z, a.w, b.x (lo) / b.y, b.z, b.w (hi); 4, 5: byte pairs of c.x .. c.z
+            const uint32_t qlx = c < 4 ? (nd.a.z >> s8) & 255u : ((nd.c.x & 0xffffu) >> s16) & 255u;
+            const uint32_t qly = c < 4 ? (nd.a.w >> s8) & 255u : ((nd.c.x >> 16) >> s16) & 255u;
+            const uint32_t qlz = c < 4 ? (nd.b.x >> s8) & 255u : ((nd.c.y & 0xffffu) >> s16) & 255u;
+            const uint32_t qhx = c < 4 ? (nd.b.y >> s8) & 255u : ((nd.c.y >> 16) >> s16) & 255u;
+            const uint32_t qhy = c < 4 ? (nd.b.z >> s8) & 255u : ((nd.c.z & 0xffffu) >> s16) & 255u;
+            const uint32_t qhz = c < 4 ? (nd.b.w >> s8) & 255u : ((nd.c.z >> 16) >> s16) & 255u;
+            // per axis: near / far distance over the packet's reciprocal interval [il, ih]
+            auto axis = [&](float dd, int e, uint32_t ql, uint32_t qh, float il, float ih, float& nr, float& fr) {
+                const float lo = dd + ldexpf((float)ql, e) - m2, hi = dd + ldexpf((float)qh, e) + m2;
+                if (il > 0.0f) {  // every lane's iq >= 0: lo is the near plane
+                    nr = lo * (lo >= 0.0f ? il : ih);
+                    fr = hi * (hi >= 0.0f ? ih : il);
+                } else if (ih < 0.0f) {  // every lane's iq < 0: hi is the near plane
+                    nr = hi * (hi >= 0.0f ? il : ih);
+                    fr = lo * (lo >= 0.0f ? ih : il);
+                } else {
+                    nr = -__builtin_huge_valf();
+                    fr = __builtin_huge_valf();
+                }
+            };
+            float n0, f0, n1, f1, n2, f2;
+            axis(dx, (int)(eb & 255u) - 128, qlx, qhx, ilx, ihx, n0, f0);
+            axis(dy, (int)((eb >> 8) & 255u) - 128, qly, qhy, ily, ihy, n1, f1);
+            axis(dz, (int)((eb >> 16) & 255u) - 128, qlz, qhz, ilz, ihz, n2, f2);
+            tnear = fmaxf(fmaxf(n0, n1), fmaxf(n2, t_lo));
+            const float tfar = fminf(fminf(f0, f1), fminf(f2, t_hi));
+            pass = tnear <= tfar && ((nd.c.w >> c) & 1u);
+        }
+        const uint32_t hm = (uint32_t)__ballot(pass);
+        // leaf children that pass: every lane with a ray tests its ray
+        uint32_t leaves = hm & ~imask;
+        if (leaves) {
+            do {
+                const int c = __builtin_ctz(leaves);
+                leaves &= leaves - 1u;
+                const int ti = (int)nd.a.y + c - __builtin_popcount(imask & ((1u << c) - 1u));
+                const TriPack tp = load_tri(tris, ti);
+                if (act) {
+                    if (kCount) ++cnt.tris;
+                    leaf_test(tp, ti, sh, o, tmin, h);
+                }
+            } while (leaves);
+            t_hi = wred(h.t, true);  // the packet's largest closest hit so far
+        }
+        const uint32_t inner = hm & imask;
+        if (!inner) {
+            if (sp == 0) break;
+            --sp;
+            node = __builtin_amdgcn_readfirstlane(sp < kStack ? stk[sp] : gstk[sp - kStack]);
+            continue;
+        }
+        // nearest internal child by the packet's near distance (ties: lower slot) next
+        int best = -1;
+        float bt = 0.0f;
+        for (uint32_t r = inner; r; r &= r - 1u) {
+            const int c = __builtin_ctz(r);
+            const float tc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tnear), c));
+            if (best < 0 || tc < bt) {
+                best = c;
+                bt = tc;
+            }
+        }
+        const int base = (int)nd.a.x;
+        for (int c = kQWidth - 1; c >= 0; --c)
+            if (c != best && ((inner >> c) & 1u)) {
+                const int x = base + __builtin_popcount(imask & ((1u << c) - 1u));
+                if (sp < kStack) {
+                    stk[sp++] = x;
+                } else if (sp < kStack + kPacketSpill) {
+                    gstk[sp - kStack] = x;
+                    ++sp;
+                } else if (drops && lane == 0) {
+                    atomicAdd(drops, 1u);  // a missed subtree
+                }
+            }
+        node = __builtin_amdgcn_readfirstlane(base + __builtin_popcount(imask & ((1u << best) - 1u)));
+    }
+}
+
 // Camera paths as packets: a wave traces 64 consecutive path indices (path_of:
 // the samples of one or two pixels) with packet_trace; packets are dealt to
 // the waves as trace_refill deals chunks (ChunkDealer, counters `deal`). An
@@ -1275,8 +1422,13 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
         n_traced += valid && !culled ? 1u : 0u;
         Hit h;
         set_miss(h, tmax);
+#if RR_CAM_BEAM
+        packet_trace_beam<kCount>(sa.qnodes, sa.tris, stk, gstk, tail + 1, valid && !culled && fc.n_tris > 0, o, d,
+                                  tmin, h, cnt);
+#else
         packet_trace<kCount>(sa.qnodes, sa.tris, stk, gstk, tail + 1, valid && !culled && fc.n_tris > 0, o, d, tmin,
                              h, cnt);
+#endif
         if (valid) hit_put(hits + p, pack_hit(h));
         q = qn;
     }
