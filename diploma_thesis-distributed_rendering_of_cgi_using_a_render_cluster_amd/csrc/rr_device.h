@@ -591,7 +591,25 @@ RR_D BvhNode load_node(lds_node* p, int i) {
                     __builtin_bit_cast(int, d.w));
     return n;
 }
-RR_D TriPack load_tri(const TriPack* __restrict__ p, int i) { return p[i]; }
+// RR_TRI_NT (A/B): triangle records through non-temporal loads (streaming
+// cache policy), so that they do not push hierarchy nodes out of the caches
+#ifndef RR_TRI_NT
+#define RR_TRI_NT 0
+#endif
+RR_D TriPack load_tri(const TriPack* __restrict__ p, int i) {
+#if RR_TRI_NT
+    const rr_f4v* q = reinterpret_cast<const rr_f4v*>(p + i);
+    TriPack t;
+    const rr_f4v a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1),
+                 c = __builtin_nontemporal_load(q + 2);
+    t.p0 = make_float4(a.x, a.y, a.z, a.w);
+    t.p1 = make_float4(b.x, b.y, b.z, b.w);
+    t.p2 = make_float4(c.x, c.y, c.z, c.w);
+    return t;
+#else
+    return p[i];
+#endif
+}
 RR_D TriPack load_tri(lds_tri* p, int i) {
     const __attribute__((address_space(3))) rr_f4v* q = (const __attribute__((address_space(3))) rr_f4v*)(p + i);
     TriPack t;
@@ -633,7 +651,44 @@ struct TravStackT {
         if (sp < kLdsStack) return lds[sp * kB + (int)threadIdx.x];
         return spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)];
     }
+    // Grouped entries of the 6-wide walk (RR_STACK_GROUP): one entry per node
+    // for all the internal children it leaves for later, first child index << 6
+    // | the mask of their ranks among the node's internal children (internal
+    // children are consecutive nodes: child of rank k = first + k). pop_group
+    // takes the lowest rank and keeps the entry while ranks remain, so the
+    // children come off in the order single pushes in descending slot order
+    // gave (the walk visits the same nodes in the same order).
+    RR_D int pop_group() {
+        const int i = sp - 1;
+        const bool in_lds = i < kLdsStack;
+        const int gi = (i - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x);
+        const int e = in_lds ? lds[i * kB + (int)threadIdx.x] : spill[gi];
+        const int node = (int)((uint32_t)e >> 6) + __builtin_ctz((uint32_t)e & 63u);
+        const int rest = e & (e - 1);  // the lowest rank bit cleared
+        if ((rest & 63) == 0) {
+            sp = i;
+        } else if (in_lds) {
+            lds[i * kB + (int)threadIdx.x] = rest;
+        } else {
+            spill[gi] = rest;
+        }
+        return node;
+    }
 };
+// The ranks among a node's internal children (imask) of the internal slots in
+// rest (a subset of imask), as a mask: bit k = the internal child of rank k.
+RR_D uint32_t q6_rank_mask(uint32_t rest, uint32_t imask) {
+    uint32_t r = 0, k = 0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        r |= ((rest >> c) & 1u) << k;
+        k += (imask >> c) & 1u;
+    }
+    return r;
+}
+#ifndef RR_STACK_GROUP
+#define RR_STACK_GROUP 0
+#endif
 using TravStack = TravStackT<kBlock>;
 
 RR_D lds_int* lds_slot(int* shared_elem) {
@@ -810,6 +865,10 @@ RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, floa
 // hit (the bound never shrinks), so the order decides nothing but the speed:
 // slot order drops the distance compares and their registers (shadow rays
 // -10 % on C5, VGPR spill slots 10 -> 2).
+#ifndef RR_PK_BOX
+#define RR_PK_BOX 0  // A/B: the child box planes two at a time through packed fma
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
 template <bool kNearest = true>
 RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, uint32_t imask,
                           int& best) {
@@ -831,6 +890,38 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
     uint32_t hits = 0;
     best = -1;
     float bt = __builtin_inff();
+#if RR_PK_BOX
+    // two children per packed fma (v_pk_fma_f32: the same fma per half, the
+    // same bits as the scalar form)
+    const f2v vsx = {sx, sx}, vsy = {sy, sy}, vsz = {sz, sz};
+    const f2v vnx = {pl.nx, pl.nx}, vny = {pl.ny, pl.ny}, vnz = {pl.nz, pl.nz};
+    const f2v vfx = {pl.fx, pl.fx}, vfy = {pl.fy, pl.fy}, vfz = {pl.fz, pl.fz};
+#pragma unroll
+    for (int pr = 0; pr < kQWidth / 2; ++pr) {
+        const int sh = pr < 2 ? 16 * pr : 0;
+        const uint32_t qnx = pr < 2 ? nx : nx2, qny = pr < 2 ? ny : ny2, qnz = pr < 2 ? nz : nz2;
+        const uint32_t qfx = pr < 2 ? fx : fx2, qfy = pr < 2 ? fy : fy2, qfz = pr < 2 ? fz : fz2;
+        auto q2 = [&](uint32_t w) {
+            return f2v{(float)((w >> sh) & 255u), (float)((w >> (sh + 8)) & 255u)};
+        };
+        const f2v anx = __builtin_elementwise_fma(q2(qnx), vsx, vnx), any = __builtin_elementwise_fma(q2(qny), vsy, vny),
+                  anz = __builtin_elementwise_fma(q2(qnz), vsz, vnz);
+        const f2v afx = __builtin_elementwise_fma(q2(qfx), vsx, vfx), afy = __builtin_elementwise_fma(q2(qfy), vsy, vfy),
+                  afz = __builtin_elementwise_fma(q2(qfz), vsz, vfz);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = 2 * pr + k;
+            const float t0 = fmaxf(fmaxf(anx[k], any[k]), fmaxf(anz[k], tmin));
+            const float t1 = fminf(fminf(afx[k], afy[k]), fminf(afz[k], tcur));
+            const bool hit = t0 <= t1;
+            hits |= (uint32_t)hit << c;
+            if (hit && ((imask >> c) & 1u) && (!kNearest ? best < 0 : t0 < bt)) {
+                best = c;
+                bt = t0;
+            }
+        }
+    }
+#else
 #pragma unroll
     for (int c = 0; c < kQWidth; ++c) {
         const int sh = c < 4 ? 8 * c : 8 * (c - 4);
@@ -847,6 +938,7 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
             bt = t0;
         }
     }
+#endif
     return hits & used;
 }
 
@@ -855,7 +947,25 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
 // so those are the top levels of the tree, which every ray visits — each of
 // those visits becomes a ds_read instead of an L2 round trip. Which copy a
 // node comes from changes no bit of it.
-RR_D QNode6 q6_load(const QNode6* __restrict__ nodes, int i) { return nodes[i]; }
+#ifndef RR_NODE_NT
+#define RR_NODE_NT 0  // A/B: hierarchy nodes through non-temporal loads
+#endif
+RR_D QNode6 q6_load(const QNode6* __restrict__ nodes, int i) {
+#if RR_NODE_NT
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const u4v* q = reinterpret_cast<const u4v*>(nodes + i);
+    const u4v w0 = __builtin_nontemporal_load(q), w1 = __builtin_nontemporal_load(q + 1),
+              w2 = __builtin_nontemporal_load(q + 2), w3 = __builtin_nontemporal_load(q + 3);
+    QNode6 r;
+    r.org = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z), __uint_as_float(w0.w));
+    r.a = make_uint4(w1.x, w1.y, w1.z, w1.w);
+    r.b = make_uint4(w2.x, w2.y, w2.z, w2.w);
+    r.c = make_uint4(w3.x, w3.y, w3.z, w3.w);
+    return r;
+#else
+    return nodes[i];
+#endif
+}
 struct Q6Nodes {
     const QNode6* __restrict__ g;
     lds_f4w* top;  // nodes [0, n_top): 4 float4 each (QNode6 layout)
@@ -924,16 +1034,20 @@ struct TravStateQ6 {
         }
         if (!inner) {
             if (st.sp == 0) return true;
-            node = st.pop();
+            node = RR_STACK_GROUP ? st.pop_group() : st.pop();
             return false;
         }
         // nearest hit child next (ties: lower slot, q6_box_best); the other hit
         // children are pushed in descending slot order (so they pop in slot order)
         const uint32_t rest = inner & ~(1u << best);
         const int base = (int)nd.a.x;
+#if RR_STACK_GROUP
+        if (rest) st.push((int)(((uint32_t)base << 6) | q6_rank_mask(rest, imask)));
+#else
 #pragma unroll
         for (int c = kQWidth - 1; c >= 0; --c)
             if ((rest >> c) & 1u) st.push(base + __builtin_popcount(imask & ((1u << c) - 1u)));
+#endif
         node = base + __builtin_popcount(imask & ((1u << best) - 1u));
         return false;
     }
@@ -1008,14 +1122,18 @@ struct TravStateQ6D {
                 node = -1;
                 return lmask == 0u;
             }
-            node = st.pop();
+            node = RR_STACK_GROUP ? st.pop_group() : st.pop();
             return false;
         }
         const uint32_t rest = inner & ~(1u << best);
         const int base = (int)nd.a.x;
+#if RR_STACK_GROUP
+        if (rest) st.push((int)(((uint32_t)base << 6) | q6_rank_mask(rest, imask)));
+#else
 #pragma unroll
         for (int c = kQWidth - 1; c >= 0; --c)
             if ((rest >> c) & 1u) st.push(base + __builtin_popcount(imask & ((1u << c) - 1u)));
+#endif
         node = base + __builtin_popcount(imask & ((1u << best) - 1u));
         return false;
     }
