@@ -918,6 +918,8 @@ void build_ploc(DevScene& s, hipStream_t st) {
 void build_qbvh(DevScene& s, hipStream_t st) {
     const int n = s.n_tris;
     const int ni = n > 1 ? n - 1 : 1;
+    // the walks' grouped stack entries hold a node index in 26 bits (rr_device.h pop_group)
+    if (ni >= (1 << 26)) throw std::runtime_error("scene too large for the 6-wide hierarchy (2^26 nodes)");
     s.qnodes.ensure((size_t)ni);
     s.qtris.ensure((size_t)n);
     s.q_src.ensure((size_t)ni);

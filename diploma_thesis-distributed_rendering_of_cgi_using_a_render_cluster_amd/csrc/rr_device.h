@@ -686,8 +686,12 @@ RR_D uint32_t q6_rank_mask(uint32_t rest, uint32_t imask) {
     }
     return r;
 }
+// RR_STACK_GROUP (default): the 6-wide walks push one grouped entry per node
+// (pop_group) instead of one entry per child: per 02 / 03 / C5 frame slice
+// 80.5 / 86.7 / 69.6 -> 79.0 / 85.5 / 69.3 ms (profiles/r5_ab_walk.txt). The
+// oracle's walk keeps the same entries, so both stacks fill (and drop) alike.
 #ifndef RR_STACK_GROUP
-#define RR_STACK_GROUP 0
+#define RR_STACK_GROUP 1
 #endif
 using TravStack = TravStackT<kBlock>;
 

@@ -901,14 +901,32 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             if (k[c].t != INFINITY && (best < 0 || (!any && k[c].t < k[best].t))) best = c;
         if (best < 0) {
             if (sp == 0) break;
-            node = stack[--sp];
+            /* grouped entries (rr_device.h TravStackT::pop_group): the lowest
+             * rank left; the entry stays while ranks remain */
+            const int e = stack[sp - 1];
+            int r = 0;
+            while (!((e >> r) & 1)) ++r;
+            node = (int)((unsigned)e >> 6) + r;
+            const int rest = e & (e - 1);
+            if ((rest & 63) == 0) --sp; else stack[sp - 1] = rest;
             continue;
         }
-        for (int c = ORC_QW_MAX - 1; c >= 0; --c)
-            if (c != best && k[c].t != INFINITY) {
-                if (sp < ORC_MAXDEPTH) stack[sp++] = k[c].ref;
+        /* the other hit internal children as one entry: the node's first
+         * internal child << 6 | their ranks among its internal children (they
+         * come off in slot order, as single pushes in descending slot order
+         * would give; node indices below 2^26, as the device build checks) */
+        {
+            unsigned rm = 0;
+            for (int c = 0, rank = 0; c < ORC_QW_MAX; ++c) {
+                if (!((inner >> c) & 1u)) continue;
+                if (c != best && k[c].t != INFINITY) rm |= 1u << rank;
+                ++rank;
+            }
+            if (rm) {
+                if (sp < ORC_MAXDEPTH) stack[sp++] = (int)((nd[4] << 6) | rm);
                 else drop_push();
             }
+        }
         node = k[best].ref;
     }
 done:
