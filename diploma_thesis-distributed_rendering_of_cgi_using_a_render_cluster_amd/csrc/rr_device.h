@@ -978,7 +978,25 @@ struct Q6Nodes {
 RR_D uint4 f4_bits(float4 v) {
     return make_uint4((uint32_t)f2i(v.x), (uint32_t)f2i(v.y), (uint32_t)f2i(v.z), (uint32_t)f2i(v.w));
 }
+#ifndef RR_FLAT_TOP
+#define RR_FLAT_TOP 0
+#endif
 RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
+#if RR_FLAT_TOP
+    // one generic (flat) pointer for both copies: a wave whose lanes read
+    // both takes one set of loads, not the two branches in turn (where the LDS
+    // reads waited for the HBM loads, whose registers they reuse)
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const u4v* top_g = (const u4v*)(const rr_f4v*)n.top;
+    const u4v* q = i < n.n_top ? top_g + 4 * i : reinterpret_cast<const u4v*>(n.g + i);
+    const u4v w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+    QNode6 r;
+    r.org = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z), __uint_as_float(w0.w));
+    r.a = make_uint4(w1.x, w1.y, w1.z, w1.w);
+    r.b = make_uint4(w2.x, w2.y, w2.z, w2.w);
+    r.c = make_uint4(w3.x, w3.y, w3.z, w3.w);
+    return r;
+#endif
     if (i < n.n_top) {
         const lds_f4w* q = n.top + 4 * i;
         QNode6 r;
