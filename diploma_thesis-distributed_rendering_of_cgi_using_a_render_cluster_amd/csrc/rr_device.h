@@ -978,8 +978,11 @@ struct Q6Nodes {
 RR_D uint4 f4_bits(float4 v) {
     return make_uint4((uint32_t)f2i(v.x), (uint32_t)f2i(v.y), (uint32_t)f2i(v.z), (uint32_t)f2i(v.w));
 }
+// RR_FLAT_TOP (default): per 02 / 03 / C5 frame slice 78.5 / 85.0 / 69.1 ->
+// 78.4 / 84.8 / 68.7 ms (profiles/r5_ab_lds.txt; the branchy form measured
+// within 0.5 % of it, and the 4 x 16 B of a node arrive either way).
 #ifndef RR_FLAT_TOP
-#define RR_FLAT_TOP 0
+#define RR_FLAT_TOP 1
 #endif
 RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
 #if RR_FLAT_TOP
