@@ -911,6 +911,19 @@ void build_ploc(DevScene& s, hipStream_t st) {
     }
 }
 
+// The shading terms of each triangle of the split path, in leaf order: the
+// unit geometric normal (the same norm3(cross3(e1, e2)) shade() computes
+// from the triangle record, contraction off: the same bits) and the material
+// id, one 16 B read per shading point instead of the 48 B record and a cross
+// product (wavefront.hip shade(), RR_SHADE_NRM).
+__global__ __launch_bounds__(kBlock) void k_tri_nrm(const TriPack* __restrict__ tris, int n, float4* __restrict__ out) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const TriPack tp = tris[i];
+    const float3 N = norm3(cross3(sub3(xyz(tp.p1), xyz(tp.p0)), sub3(xyz(tp.p2), xyz(tp.p0))));
+    out[i] = make_float4(N.x, N.y, N.z, tp.p1.w);
+}
+
 // Quantised 6-wide hierarchy of the built BVH2 (kernels above): one count / scan / emit /
 // advance round per level; the host learns the frontier size every 4 levels
 // (one synchronisation) and sizes the next launches by it (a level has at
@@ -952,6 +965,8 @@ void build_qbvh(DevScene& s, hipStream_t st) {
         }
     }
     std::swap(s.tris, s.qtris);  // the traversal and shading read the 6-wide hierarchy's leaf order
+    s.tnrm.ensure((size_t)std::max(n, 1));
+    if (n > 0) k_tri_nrm<<<cdiv(n, kBlock), kBlock, 0, st>>>(s.tris.ptr, n, s.tnrm.ptr);
     s.has4 = true;
 }
 

@@ -1093,6 +1093,15 @@ struct TravStateQ6 {
 #ifndef RR_LEAF_PHASE
 #define RR_LEAF_PHASE 12
 #endif
+#ifndef RR_LEAF_SPEC
+#define RR_LEAF_SPEC 0
+#endif
+#ifndef RR_SPEC_BLK
+#define RR_SPEC_BLK 8
+#endif
+#ifndef RR_SPEC_PEN
+#define RR_SPEC_PEN 40
+#endif
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6D {
     float3 o, iq;
@@ -1113,7 +1122,60 @@ struct TravStateQ6D {
         iq = rcp3(d_);
         node = 0;
         lmask = 0;
+#if RR_LEAF_SPEC
+        lmask2 = 0;
+#endif
     }
+#if RR_LEAF_SPEC
+    // Speculative walks (RR_LEAF_SPEC, A/B; Aila & Laine's speculative
+    // traversal): a lane with one pending leaf set goes on visiting nodes and
+    // holds a second set if it meets one; it waits only with two sets (or
+    // with nothing left to visit). The leaf phase starts once RR_SPEC_BLK
+    // lanes wait or RR_SPEC_PEN lanes have leaves pending. The bound of the
+    // box tests may then lag the pending tests (more nodes visited, the same
+    // closest hit by the accept rule).
+    int lbase2;
+    uint32_t lmask2;
+    template <typename NodeSrc, typename TriP, typename Stack>
+    RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
+        const bool p1 = (lmask & 63u) != 0u;
+        const bool blocked = lmask2 != 0u || (p1 && node < 0);
+        const uint64_t act = __ballot(true), pen = __ballot(p1), blk = __ballot(blocked);
+        if (pen != 0 && (blk == act || __popcll(blk) >= RR_SPEC_BLK || __popcll(pen) >= RR_SPEC_PEN)) {
+            if (!p1) return false;
+            const int c = __builtin_ctz(lmask);
+            lmask &= lmask - 1u;
+            const uint32_t imask = lmask >> 8;
+            const int ti = lbase + c - __builtin_popcount(imask & ((1u << c) - 1u));
+            if (kCount) ++cnt.tris;
+            leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
+            if (kAnyHit && h.idx >= 0) return true;
+            if ((lmask & 63u) == 0u) {  // the second set moves up
+                lmask = lmask2;
+                lbase = lbase2;
+                lmask2 = 0u;
+            }
+            return lmask == 0u && node < 0;
+        }
+        if (blocked) return false;
+        if (kCount) ++cnt.nodes;
+        const float tcur = h.t;
+        const QNode6 nd = q6_load(nodes, node);
+        const uint32_t imask = q6_inner(nd);
+        int best;
+        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, tmin, tcur, imask, best);
+        const uint32_t leaves = hm & ~imask;
+        const uint32_t inner = hm & imask;
+        if (leaves) {
+            if (p1) {
+                lbase2 = (int)nd.a.y;
+                lmask2 = leaves | (imask << 8);
+            } else {
+                lbase = (int)nd.a.y;
+                lmask = leaves | (imask << 8);
+            }
+        }
+#else
     template <typename NodeSrc, typename TriP, typename Stack>
     RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
         const uint64_t act = __ballot(true), pen = __ballot((lmask & 63u) != 0u);
@@ -1142,6 +1204,7 @@ struct TravStateQ6D {
             lbase = (int)nd.a.y;
             lmask = leaves | (imask << 8);
         }
+#endif
         if (!inner) {
             if (st.sp == 0) {
                 node = -1;

@@ -101,7 +101,13 @@ struct SceneView {
     lds_f4w* nrm = nullptr;   // LDS scenes, shading kernels: unit geometric normal per triangle
     lds_f4w* matd = nullptr;  // LDS scenes, shading kernels: each material with its derived terms (kMatDF4)
     lds_f4w* onb = nullptr;   // LDS scenes, shading kernels: make_onb of both sides' normals (kOnbF4 per triangle)
+    const float4* gnrm = nullptr;  // HBM scenes, shading kernels: DevScene::tnrm (RR_SHADE_NRM)
 };
+// RR_SHADE_NRM (A/B): the split path's shading reads each hit triangle's
+// normal and material from DevScene::tnrm (16 B) instead of its 48 B record.
+#ifndef RR_SHADE_NRM
+#define RR_SHADE_NRM 0
+#endif
 using GlobalView = SceneView<const BvhNode*, const TriPack*, const float*>;
 using LdsView = SceneView<lds_node*, lds_tri*, lds_float*>;
 
@@ -299,6 +305,10 @@ __device__ __forceinline__ void shade(const FC& fc, int bounce, const View& v, f
         // table offsets become 24-bit multiplies (full rate) instead of
         // v_mul_lo_u32 / v_mad_u64_u32
         __builtin_assume(mid >= 0 && mid < 4096);
+    } else if (RR_SHADE_NRM && v.gnrm) {
+        const float4 nm = v.gnrm[h.idx];  // k_tri_nrm: the same normal, precomputed
+        N = xyz(nm);
+        mid = f2i(nm.w);
     } else {
         const TriPack tp = load_tri(v.tris, h.idx);
         mid = f2i(tp.p1.w);
@@ -1443,8 +1453,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
 // bounce-1 paths are queued with the samples of one pixel side by side.
 __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np,
                                                           const float2* __restrict__ hits, Rad rad,
-                                                          PathQueue out, ShadowQueue sq, QueueOut qo) {
-    const GlobalView v = global_view(sa);
+                                                          PathQueue out, ShadowQueue sq, QueueOut qo,
+                                                          const float4* __restrict__ tnrm) {
+    GlobalView v = global_view(sa);
+    v.gnrm = tnrm;
     const int stride = gridDim.x * kBlock;
     for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {
         const int p = b0 + (int)threadIdx.x;
@@ -1500,11 +1512,12 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
 __global__ __launch_bounds__(kBlock, RR_SHADE_COMPACT ? 5 : 1) void k_shade_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in,
                                                          QueueIn qi, const float2* __restrict__ hits,
                                                          Rad rad, PathQueue out, ShadowQueue sq,
-                                                         QueueOut qo) {
+                                                         QueueOut qo, const float4* __restrict__ tnrm) {
     QueueMap qm;
     qm.init(qi);
     const int count = qm.span;
-    const GlobalView v = global_view(sa);
+    GlobalView v = global_view(sa);
+    v.gnrm = tnrm;
     const int stride = gridDim.x * kBlock;
     int pid = 0;
 #if RR_SHADE_COMPACT
@@ -2673,7 +2686,7 @@ namespace {
 // shadow(b), trace_extend(b+1), shade_extend(b+1) -> accumulate. Radiance
 // additions per path happen in the same order as the fused kernels'.
 void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_t st, const SceneArgs& sa,
-                  unsigned long long* tc, PathQueue pq[2], const ShadowQueue& sq) {
+                  unsigned long long* tc, PathQueue pq[2], const ShadowQueue& sq, const float4* tnrm) {
     KernelProfiler& pr = p.prof;
     const SplitGrids G(tc != nullptr);
     const int npix = base.npix;
@@ -2721,7 +2734,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         pr.end(st);
         pr.begin(st, RR_K_SHADE);
         k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1],
-                                                sq, QueueOut{qpath(0), qshadow(0), cap_p});
+                                                sq, QueueOut{qpath(0), qshadow(0), cap_p}, tnrm);
         pr.end(st);
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         for (int b = 0; b <= base.max_bounces; ++b) {
@@ -2736,7 +2749,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
                 pr.begin(st, RR_K_SHADE);
                 k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},
                                                        p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)},
-                                                       pq[(nb + 1) & 1], sq, QueueOut{qpath(nb), qshadow(nb), cap_e});
+                                                       pq[(nb + 1) & 1], sq, QueueOut{qpath(nb), qshadow(nb), cap_e}, tnrm);
                 pr.end(st);
                 cap_prev = cap_e;
                 continue;
@@ -2756,7 +2769,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             pr.begin(st, RR_K_SHADE);
             k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},
                                                    p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[(nb + 1) & 1], sq,
-                                                   QueueOut{qpath(nb), qshadow(nb), cap_e});
+                                                   QueueOut{qpath(nb), qshadow(nb), cap_e}, tnrm);
             pr.end(st);
             cap_prev = cap_e;
         }
@@ -2850,7 +2863,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     const SceneArgs sa{s.nodes.ptr, s.qnodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
                        p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.nq};
-    render_split(p, base, n_chunks, st, sa, tc, pq, sq);
+    render_split(p, base, n_chunks, st, sa, tc, pq, sq, s.has4 ? s.tnrm.ptr : nullptr);
     RR_HIP(hipGetLastError());
 }
 
