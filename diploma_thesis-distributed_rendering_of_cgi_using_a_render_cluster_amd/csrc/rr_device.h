@@ -1020,6 +1020,7 @@ RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
 // oracle/rr_oracle.c trace4() is the same walk.
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6 {
+    static constexpr bool kAny = kAnyHit;
     float3 o, iq;
     Shear sh;
     float tmin;
@@ -1104,6 +1105,7 @@ struct TravStateQ6 {
 #endif
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6D {
+    static constexpr bool kAny = kAnyHit;
     float3 o, iq;
     Shear sh;
     float tmin;

@@ -930,6 +930,9 @@ RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
 // TS: TravStateQ6 (its box margins are per node; the BVH2 walk TravState needs
 // the scene radius in start() and so does not compile here). Blocks of
 // kTraceBlock threads.
+#ifndef RR_SHADOW_CACHE
+#define RR_SHADOW_CACHE 0
+#endif
 template <typename TS, typename NodeP, typename TriP, typename Stack, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st, TravCount& cnt,
                        uint32_t* deal, MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
@@ -947,6 +950,12 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st,
     TS ts;
     int j = -1;
     uint32_t js = 0;  // queue slot of ray j
+    // RR_SHADOW_CACHE (any-hit walks): the triangle that occluded this lane's
+    // previous ray is tested first; if it occludes the new ray too, the walk
+    // is skipped. An any-hit query answers only whether the segment is
+    // blocked, and a triangle the exact test accepts inside the segment means
+    // the walk would find a blocker too (maybe another): the same answer.
+    int occ = -1;
     for (;;) {
         const uint64_t idle = __ballot(j < 0);
         if (gpos(next) < count && idle) {  // wave-uniform
@@ -958,7 +967,14 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st,
                 ray_of(ks, o, d, tmin, tmax);
                 ts.start(o, d, tmin, tmax);
                 st.sp = 0;
-                if (n_tris > 0) {
+                bool cached = false;
+                if constexpr (TS::kAny && RR_SHADOW_CACHE) {
+                    if (occ >= 0 && n_tris > 0) {
+                        leaf_test(load_tri(tris, occ), occ, ts.sh, ts.o, ts.tmin, ts.h);
+                        cached = ts.h.idx >= 0;
+                    }
+                }
+                if (n_tris > 0 && !cached) {
                     j = k;
                     js = ks;
                 } else {
@@ -979,6 +995,9 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st,
         for (;;) {
             if (j >= 0 && ts.step(nodes, tris, st, cnt)) {
                 done(j, js, ts.h);
+                if constexpr (TS::kAny && RR_SHADOW_CACHE) {
+                    if (ts.h.idx >= 0) occ = ts.h.idx;
+                }
                 j = -1;
             }
             const int na = (int)__popcll(__ballot(j >= 0));
