@@ -933,6 +933,9 @@ RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
 #ifndef RR_SHADOW_CACHE
 #define RR_SHADOW_CACHE 0
 #endif
+#ifndef RR_HIT_CACHE
+#define RR_HIT_CACHE 0
+#endif
 template <typename TS, typename NodeP, typename TriP, typename Stack, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st, TravCount& cnt,
                        uint32_t* deal, MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
@@ -974,6 +977,13 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st,
                         cached = ts.h.idx >= 0;
                     }
                 }
+                // RR_HIT_CACHE (closest-hit walks): the lane's previous hit
+                // triangle is tested first, so the walk starts with its
+                // distance as the bound; the accept rule makes the closest hit
+                // the same as testing that triangle anywhere in the walk
+                if constexpr (!TS::kAny && RR_HIT_CACHE) {
+                    if (occ >= 0 && n_tris > 0) leaf_test(load_tri(tris, occ), occ, ts.sh, ts.o, ts.tmin, ts.h);
+                }
                 if (n_tris > 0 && !cached) {
                     j = k;
                     js = ks;
@@ -995,7 +1005,7 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st,
         for (;;) {
             if (j >= 0 && ts.step(nodes, tris, st, cnt)) {
                 done(j, js, ts.h);
-                if constexpr (TS::kAny && RR_SHADOW_CACHE) {
+                if constexpr ((TS::kAny && RR_SHADOW_CACHE) || (!TS::kAny && RR_HIT_CACHE)) {
                     if (ts.h.idx >= 0) occ = ts.h.idx;
                 }
                 j = -1;
