@@ -103,10 +103,12 @@ struct SceneView {
     lds_f4w* onb = nullptr;   // LDS scenes, shading kernels: make_onb of both sides' normals (kOnbF4 per triangle)
     const float4* gnrm = nullptr;  // HBM scenes, shading kernels: DevScene::tnrm (RR_SHADE_NRM)
 };
-// RR_SHADE_NRM (A/B): the split path's shading reads each hit triangle's
-// normal and material from DevScene::tnrm (16 B) instead of its 48 B record.
+// RR_SHADE_NRM (default): the split path's shading reads each hit triangle's
+// normal and material from DevScene::tnrm (16 B) instead of its 48 B record
+// and a cross product: shading per 02 / 03 / C5 frame slice 11.34 / 11.49 /
+// 9.18 -> 10.77 / 10.85 / 8.61 ms (profiles/r5_ab_spec.txt).
 #ifndef RR_SHADE_NRM
-#define RR_SHADE_NRM 0
+#define RR_SHADE_NRM 1
 #endif
 using GlobalView = SceneView<const BvhNode*, const TriPack*, const float*>;
 using LdsView = SceneView<lds_node*, lds_tri*, lds_float*>;
