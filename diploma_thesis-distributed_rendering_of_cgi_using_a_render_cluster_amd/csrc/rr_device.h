@@ -591,25 +591,7 @@ RR_D BvhNode load_node(lds_node* p, int i) {
                     __builtin_bit_cast(int, d.w));
     return n;
 }
-// RR_TRI_NT (A/B): triangle records through non-temporal loads (streaming
-// cache policy), so that they do not push hierarchy nodes out of the caches
-#ifndef RR_TRI_NT
-#define RR_TRI_NT 0
-#endif
-RR_D TriPack load_tri(const TriPack* __restrict__ p, int i) {
-#if RR_TRI_NT
-    const rr_f4v* q = reinterpret_cast<const rr_f4v*>(p + i);
-    TriPack t;
-    const rr_f4v a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1),
-                 c = __builtin_nontemporal_load(q + 2);
-    t.p0 = make_float4(a.x, a.y, a.z, a.w);
-    t.p1 = make_float4(b.x, b.y, b.z, b.w);
-    t.p2 = make_float4(c.x, c.y, c.z, c.w);
-    return t;
-#else
-    return p[i];
-#endif
-}
+RR_D TriPack load_tri(const TriPack* __restrict__ p, int i) { return p[i]; }
 RR_D TriPack load_tri(lds_tri* p, int i) {
     const __attribute__((address_space(3))) rr_f4v* q = (const __attribute__((address_space(3))) rr_f4v*)(p + i);
     TriPack t;
@@ -869,10 +851,6 @@ RR_D uint32_t q6_box_hits(const QNode6& n, float3 o, float3 iq, float tmin, floa
 // hit (the bound never shrinks), so the order decides nothing but the speed:
 // slot order drops the distance compares and their registers (shadow rays
 // -10 % on C5, VGPR spill slots 10 -> 2).
-#ifndef RR_PK_BOX
-#define RR_PK_BOX 0  // A/B: the child box planes two at a time through packed fma
-#endif
-typedef float f2v __attribute__((ext_vector_type(2)));
 template <bool kNearest = true>
 RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, float tcur, uint32_t imask,
                           int& best) {
@@ -894,38 +872,6 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
     uint32_t hits = 0;
     best = -1;
     float bt = __builtin_inff();
-#if RR_PK_BOX
-    // two children per packed fma (v_pk_fma_f32: the same fma per half, the
-    // same bits as the scalar form)
-    const f2v vsx = {sx, sx}, vsy = {sy, sy}, vsz = {sz, sz};
-    const f2v vnx = {pl.nx, pl.nx}, vny = {pl.ny, pl.ny}, vnz = {pl.nz, pl.nz};
-    const f2v vfx = {pl.fx, pl.fx}, vfy = {pl.fy, pl.fy}, vfz = {pl.fz, pl.fz};
-#pragma unroll
-    for (int pr = 0; pr < kQWidth / 2; ++pr) {
-        const int sh = pr < 2 ? 16 * pr : 0;
-        const uint32_t qnx = pr < 2 ? nx : nx2, qny = pr < 2 ? ny : ny2, qnz = pr < 2 ? nz : nz2;
-        const uint32_t qfx = pr < 2 ? fx : fx2, qfy = pr < 2 ? fy : fy2, qfz = pr < 2 ? fz : fz2;
-        auto q2 = [&](uint32_t w) {
-            return f2v{(float)((w >> sh) & 255u), (float)((w >> (sh + 8)) & 255u)};
-        };
-        const f2v anx = __builtin_elementwise_fma(q2(qnx), vsx, vnx), any = __builtin_elementwise_fma(q2(qny), vsy, vny),
-                  anz = __builtin_elementwise_fma(q2(qnz), vsz, vnz);
-        const f2v afx = __builtin_elementwise_fma(q2(qfx), vsx, vfx), afy = __builtin_elementwise_fma(q2(qfy), vsy, vfy),
-                  afz = __builtin_elementwise_fma(q2(qfz), vsz, vfz);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int c = 2 * pr + k;
-            const float t0 = fmaxf(fmaxf(anx[k], any[k]), fmaxf(anz[k], tmin));
-            const float t1 = fminf(fminf(afx[k], afy[k]), fminf(afz[k], tcur));
-            const bool hit = t0 <= t1;
-            hits |= (uint32_t)hit << c;
-            if (hit && ((imask >> c) & 1u) && (!kNearest ? best < 0 : t0 < bt)) {
-                best = c;
-                bt = t0;
-            }
-        }
-    }
-#else
 #pragma unroll
     for (int c = 0; c < kQWidth; ++c) {
         const int sh = c < 4 ? 8 * c : 8 * (c - 4);
@@ -942,7 +888,6 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
             bt = t0;
         }
     }
-#endif
     return hits & used;
 }
 
@@ -951,25 +896,7 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
 // so those are the top levels of the tree, which every ray visits — each of
 // those visits becomes a ds_read instead of an L2 round trip. Which copy a
 // node comes from changes no bit of it.
-#ifndef RR_NODE_NT
-#define RR_NODE_NT 0  // A/B: hierarchy nodes through non-temporal loads
-#endif
-RR_D QNode6 q6_load(const QNode6* __restrict__ nodes, int i) {
-#if RR_NODE_NT
-    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-    const u4v* q = reinterpret_cast<const u4v*>(nodes + i);
-    const u4v w0 = __builtin_nontemporal_load(q), w1 = __builtin_nontemporal_load(q + 1),
-              w2 = __builtin_nontemporal_load(q + 2), w3 = __builtin_nontemporal_load(q + 3);
-    QNode6 r;
-    r.org = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z), __uint_as_float(w0.w));
-    r.a = make_uint4(w1.x, w1.y, w1.z, w1.w);
-    r.b = make_uint4(w2.x, w2.y, w2.z, w2.w);
-    r.c = make_uint4(w3.x, w3.y, w3.z, w3.w);
-    return r;
-#else
-    return nodes[i];
-#endif
-}
+RR_D QNode6 q6_load(const QNode6* __restrict__ nodes, int i) { return nodes[i]; }
 struct Q6Nodes {
     const QNode6* __restrict__ g;
     lds_f4w* top;  // nodes [0, n_top): 4 float4 each (QNode6 layout)
@@ -1020,7 +947,6 @@ RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
 // oracle/rr_oracle.c trace4() is the same walk.
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6 {
-    static constexpr bool kAny = kAnyHit;
     float3 o, iq;
     Shear sh;
     float tmin;
@@ -1094,18 +1020,11 @@ struct TravStateQ6 {
 #ifndef RR_LEAF_PHASE
 #define RR_LEAF_PHASE 12
 #endif
-#ifndef RR_LEAF_SPEC
-#define RR_LEAF_SPEC 0
-#endif
-#ifndef RR_SPEC_BLK
-#define RR_SPEC_BLK 8
-#endif
-#ifndef RR_SPEC_PEN
-#define RR_SPEC_PEN 40
+#ifndef RR_LEAF_PHASE_ANY
+#define RR_LEAF_PHASE_ANY RR_LEAF_PHASE  // the any-hit (shadow) walks' threshold
 #endif
 template <bool kAnyHit, bool kCount = false>
 struct TravStateQ6D {
-    static constexpr bool kAny = kAnyHit;
     float3 o, iq;
     Shear sh;
     float tmin;
@@ -1124,64 +1043,11 @@ struct TravStateQ6D {
         iq = rcp3(d_);
         node = 0;
         lmask = 0;
-#if RR_LEAF_SPEC
-        lmask2 = 0;
-#endif
     }
-#if RR_LEAF_SPEC
-    // Speculative walks (RR_LEAF_SPEC, A/B; Aila & Laine's speculative
-    // traversal): a lane with one pending leaf set goes on visiting nodes and
-    // holds a second set if it meets one; it waits only with two sets (or
-    // with nothing left to visit). The leaf phase starts once RR_SPEC_BLK
-    // lanes wait or RR_SPEC_PEN lanes have leaves pending. The bound of the
-    // box tests may then lag the pending tests (more nodes visited, the same
-    // closest hit by the accept rule).
-    int lbase2;
-    uint32_t lmask2;
-    template <typename NodeSrc, typename TriP, typename Stack>
-    RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
-        const bool p1 = (lmask & 63u) != 0u;
-        const bool blocked = lmask2 != 0u || (p1 && node < 0);
-        const uint64_t act = __ballot(true), pen = __ballot(p1), blk = __ballot(blocked);
-        if (pen != 0 && (blk == act || __popcll(blk) >= RR_SPEC_BLK || __popcll(pen) >= RR_SPEC_PEN)) {
-            if (!p1) return false;
-            const int c = __builtin_ctz(lmask);
-            lmask &= lmask - 1u;
-            const uint32_t imask = lmask >> 8;
-            const int ti = lbase + c - __builtin_popcount(imask & ((1u << c) - 1u));
-            if (kCount) ++cnt.tris;
-            leaf_test(load_tri(tris, ti), ti, sh, o, tmin, h);
-            if (kAnyHit && h.idx >= 0) return true;
-            if ((lmask & 63u) == 0u) {  // the second set moves up
-                lmask = lmask2;
-                lbase = lbase2;
-                lmask2 = 0u;
-            }
-            return lmask == 0u && node < 0;
-        }
-        if (blocked) return false;
-        if (kCount) ++cnt.nodes;
-        const float tcur = h.t;
-        const QNode6 nd = q6_load(nodes, node);
-        const uint32_t imask = q6_inner(nd);
-        int best;
-        const uint32_t hm = q6_box_best<!kAnyHit>(nd, o, iq, tmin, tcur, imask, best);
-        const uint32_t leaves = hm & ~imask;
-        const uint32_t inner = hm & imask;
-        if (leaves) {
-            if (p1) {
-                lbase2 = (int)nd.a.y;
-                lmask2 = leaves | (imask << 8);
-            } else {
-                lbase = (int)nd.a.y;
-                lmask = leaves | (imask << 8);
-            }
-        }
-#else
     template <typename NodeSrc, typename TriP, typename Stack>
     RR_D bool step(const NodeSrc& nodes, TriP tris, Stack& st, TravCount& cnt) {
         const uint64_t act = __ballot(true), pen = __ballot((lmask & 63u) != 0u);
-        if (pen != 0 && (pen == act || __popcll(pen) >= RR_LEAF_PHASE)) {  // leaf phase (wave-uniform)
+        if (pen != 0 && (pen == act || __popcll(pen) >= (kAnyHit ? RR_LEAF_PHASE_ANY : RR_LEAF_PHASE))) {  // leaf phase
             if ((lmask & 63u) == 0u) return false;
             const int c = __builtin_ctz(lmask);
             lmask &= lmask - 1u;
@@ -1206,7 +1072,6 @@ struct TravStateQ6D {
             lbase = (int)nd.a.y;
             lmask = leaves | (imask << 8);
         }
-#endif
         if (!inner) {
             if (st.sp == 0) {
                 node = -1;

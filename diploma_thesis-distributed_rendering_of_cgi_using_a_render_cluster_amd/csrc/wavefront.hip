@@ -932,12 +932,6 @@ RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
 // TS: TravStateQ6 (its box margins are per node; the BVH2 walk TravState needs
 // the scene radius in start() and so does not compile here). Blocks of
 // kTraceBlock threads.
-#ifndef RR_SHADOW_CACHE
-#define RR_SHADOW_CACHE 0
-#endif
-#ifndef RR_HIT_CACHE
-#define RR_HIT_CACHE 0
-#endif
 template <typename TS, typename NodeP, typename TriP, typename Stack, typename MapFn, typename RayFn, typename DoneFn>
 RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st, TravCount& cnt,
                        uint32_t* deal, MapFn&& map, RayFn&& ray_of, DoneFn&& done) {
@@ -955,12 +949,6 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st,
     TS ts;
     int j = -1;
     uint32_t js = 0;  // queue slot of ray j
-    // RR_SHADOW_CACHE (any-hit walks): the triangle that occluded this lane's
-    // previous ray is tested first; if it occludes the new ray too, the walk
-    // is skipped. An any-hit query answers only whether the segment is
-    // blocked, and a triangle the exact test accepts inside the segment means
-    // the walk would find a blocker too (maybe another): the same answer.
-    int occ = -1;
     for (;;) {
         const uint64_t idle = __ballot(j < 0);
         if (gpos(next) < count && idle) {  // wave-uniform
@@ -972,21 +960,7 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st,
                 ray_of(ks, o, d, tmin, tmax);
                 ts.start(o, d, tmin, tmax);
                 st.sp = 0;
-                bool cached = false;
-                if constexpr (TS::kAny && RR_SHADOW_CACHE) {
-                    if (occ >= 0 && n_tris > 0) {
-                        leaf_test(load_tri(tris, occ), occ, ts.sh, ts.o, ts.tmin, ts.h);
-                        cached = ts.h.idx >= 0;
-                    }
-                }
-                // RR_HIT_CACHE (closest-hit walks): the lane's previous hit
-                // triangle is tested first, so the walk starts with its
-                // distance as the bound; the accept rule makes the closest hit
-                // the same as testing that triangle anywhere in the walk
-                if constexpr (!TS::kAny && RR_HIT_CACHE) {
-                    if (occ >= 0 && n_tris > 0) leaf_test(load_tri(tris, occ), occ, ts.sh, ts.o, ts.tmin, ts.h);
-                }
-                if (n_tris > 0 && !cached) {
+                if (n_tris > 0) {
                     j = k;
                     js = ks;
                 } else {
@@ -1007,9 +981,6 @@ RR_D void trace_refill(NodeP nodes, TriP tris, int n_tris, int count, Stack& st,
         for (;;) {
             if (j >= 0 && ts.step(nodes, tris, st, cnt)) {
                 done(j, js, ts.h);
-                if constexpr ((TS::kAny && RR_SHADOW_CACHE) || (!TS::kAny && RR_HIT_CACHE)) {
-                    if (ts.h.idx >= 0) occ = ts.h.idx;
-                }
                 j = -1;
             }
             const int na = (int)__popcll(__ballot(j >= 0));
@@ -1535,12 +1506,9 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
     if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
 }
 
-#ifndef RR_SHADE_COMPACT
-#define RR_SHADE_COMPACT 0
-#endif
 // Bounce b: shade from hits[slot], in the queue's time order (slot_t); appends
 // the next path queue and this bounce's shadow queue.
-__global__ __launch_bounds__(kBlock, RR_SHADE_COMPACT ? 5 : 1) void k_shade_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in,
+__global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bounce, SceneArgs sa, PathQueue in,
                                                          QueueIn qi, const float2* __restrict__ hits,
                                                          Rad rad, PathQueue out, ShadowQueue sq,
                                                          QueueOut qo, const float4* __restrict__ tnrm) {
@@ -1551,66 +1519,6 @@ __global__ __launch_bounds__(kBlock, RR_SHADE_COMPACT ? 5 : 1) void k_shade_exte
     v.gnrm = tnrm;
     const int stride = gridDim.x * kBlock;
     int pid = 0;
-#if RR_SHADE_COMPACT
-    // Most extension rays of a bounce miss (02: about 70 %), and a miss only
-    // adds the world term (shade()'s first lines). Each wave walks its windows
-    // of 64 queue positions, settles the misses at once and gathers the slots
-    // of the hits in LDS; a full batch of 64 hits is then shaded with every
-    // lane busy. Per path the same additions in the same order (bit-exact);
-    // only the order of the appended records changes.
-    __shared__ uint32_t hit_slots[kWavesPerBlock * 128];
-    lds_uint* const hs = (lds_uint*)hit_slots + 128 * (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    int nbuf = 0;  // wave-uniform
-    for (int b0 = blockIdx.x * kBlock;; b0 += stride) {
-        if (b0 < count) {
-            const int j = b0 + (int)threadIdx.x;
-            const uint32_t i = qm.slot_t(j < count ? j : count - 1);  // all lanes (shuffles)
-            bool hit = false;
-            if (j < count && i != kNoSlot) {
-                const Hit h = unpack_hit(hits[i]);
-                if (h.idx < 0) {  // shade() of a miss at bounce > 0
-                    const int p = f2i(in.o[i].w);
-                    const float4 c4 = q_last(in.t + i);
-                    float3 L = rad.get(p);
-                    add_to(L, clamp_contrib(mul3(xyz(c4), fc.world), fc.clamp_indirect));
-                    rad.put(p, L);
-                } else {
-                    hit = true;
-                }
-            }
-            const uint64_t mh = __ballot(hit);
-            if (hit) hs[nbuf + (int)__popcll(mh & below)] = i;
-            nbuf += (int)__popcll(mh);
-            __builtin_amdgcn_wave_barrier();
-        } else if (nbuf == 0) {
-            break;
-        }
-        if (nbuf < 64 && b0 < count) continue;
-        // shade a batch: the first min(64, nbuf) gathered hits
-        ShadeOut so;
-        so.cont = so.shadow = false;
-        if (lane < nbuf) {
-            const uint32_t i = hs[lane];
-            const float4 a = q_last(in.o + i), b = q_last(in.d + i), c = q_last(in.t + i);
-            pid = f2i(a.w);
-            const Hit h = unpack_hit(hits[i]);
-            int pix, sl;
-            path_of(fc, (uint32_t)pid, pix, sl);
-            const uint32_t key = path_key(fc.seed, (uint32_t)pix, (uint32_t)(fc.first_sample + sl));
-            float3 L = rad.get(pid);
-            shade(fc, bounce, v, xyz(a), xyz(b), xyz(c), (uint32_t)f2i(b.w), h, key, L, so);
-            rad.put(pid, L);
-        }
-        emit_grouped(so, pid, out, sq, qo);
-        // keep the rest (at most 63) at the front
-        const uint32_t rest = 64 + lane < nbuf ? hs[64 + lane] : 0u;
-        if (64 + lane < nbuf) hs[lane] = rest;
-        nbuf = nbuf > 64 ? nbuf - 64 : 0;
-        __builtin_amdgcn_wave_barrier();
-    }
-#else
     for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
         const int j = b0 + (int)threadIdx.x;
         ShadeOut so;
@@ -1629,7 +1537,6 @@ __global__ __launch_bounds__(kBlock, RR_SHADE_COMPACT ? 5 : 1) void k_shade_exte
         }
         emit_grouped(so, pid, out, sq, qo);
     }
-#endif
 }
 
 // Shadow rays with lane refill: unoccluded -> radiance += contribution.
@@ -1666,77 +1573,6 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
             rad.put(pid, L);
         });
     if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
-}
-
-// One launch for a bounce's two walks (RR_MERGE_TRACE, A/B): each wave
-// traces extension rays (k_trace_extend's body) until their queue is dealt
-// out, then shadow rays (k_shadow_refill's), so the waves that finish the
-// first queue early fill the chip with the second instead of both launches
-// draining separately. The walks are independent (the extension walk writes
-// hits, the shadow walk adds to the radiance records, which the next shading
-// kernel reads after both).
-#ifndef RR_MERGE_TRACE
-#define RR_MERGE_TRACE 0
-#endif
-template <bool kCount>
-__device__ __noinline__ void both_extend(const Q6Nodes nodes, const SceneArgs& sa, const PathQueue& in, const QueueIn& qe,
-                                         float2* __restrict__ hits, TravStackT<kTraceBlock> st,
-                                         unsigned long long* __restrict__ tc) {
-    QueueMap qm;
-    qm.init(qe);
-    TravCount cnt;
-    trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qe.ctr, 1), [&](int m) { return qm.slot_t(m); },
-        [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
-            o = xyz(in.o[i]);
-            d = xyz(in.d[i]);
-            tmin = 0.0f;
-            tmax = kFltMax;
-        },
-        [&](int, uint32_t i, const Hit& h) { hit_put(hits + i, pack_hit(h)); });
-    if (kCount) flush_counts(tc, 2, cnt.nodes, cnt.tris);
-}
-template <bool kCount>
-__device__ __noinline__ void both_shadow(const Q6Nodes nodes, const SceneArgs& sa, const ShadowQueue& sq,
-                                         const QueueIn& qs, Rad rad, TravStackT<kTraceBlock> st,
-                                         unsigned long long* __restrict__ tc) {
-    QueueMap qm;
-    qm.init(qs);
-    TravCount cnt;
-    trace_refill<SplitTrav<true, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qs.ctr, 1), [&](int m) { return qm.slot_t(m); },
-        [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
-            const float4 a = sq.o[i], b = sq.d[i];
-            o = xyz(a);
-            d = xyz(b);
-            tmin = 0.0f;
-            tmax = b.w;
-        },
-        [&](int, uint32_t i, const Hit& h) {
-            if (h.idx >= 0) return;
-            const int pid = f2i(sq.o[i].w);
-            const float4 c = q_last(sq.c + i);
-            float3 L = rad.get(pid);
-            L.x = L.x + c.x;
-            L.y = L.y + c.y;
-            L.z = L.z + c.z;
-            rad.put(pid, L);
-        });
-    if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
-}
-template <bool kCount>
-__global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_both(SceneArgs sa, PathQueue in, QueueIn qe,
-                                                                       float2* __restrict__ hits, ShadowQueue sq,
-                                                                       QueueIn qs, Rad rad,
-                                                                       int32_t* __restrict__ spill,
-                                                                       unsigned long long* __restrict__ tc,
-                                                                       uint32_t* __restrict__ tail) {
-    __shared__ int lds_stack[kLdsStack * kTraceBlock];
-    __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const Q6Nodes nodes = stage_top(sa, top_nodes);
-    const TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
-    both_extend<kCount>(nodes, sa, in, qe, hits, st, tc);
-    both_shadow<kCount>(nodes, sa, sq, qs, rad, st, tc);
 }
 
 // K11 (+K12 on the last chunk): film += radiance of this chunk's samples in
@@ -2638,23 +2474,19 @@ struct TileGrid {
 };
 // Launch geometry of the split (trace / shade) path of large scenes.
 struct SplitGrids {
-    int trace_p, trace_e, shadow, shade_p, shade_e, packet, trace_b;
+    int trace_p, trace_e, shadow, shade_p, shade_e, packet;
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*, uint32_t*);
-    void (*ktb)(SceneArgs, PathQueue, QueueIn, float2*, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*,
-                uint32_t*);
     void (*ktpk)(FrameConsts, SceneArgs, int, float2*, uint32_t*, int32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
         kts = count ? k_shadow_refill<true> : k_shadow_refill<false>;
-        ktb = count ? k_trace_both<true> : k_trace_both<false>;
         ktpk = count ? k_trace_primary_packet<true> : k_trace_primary_packet<false>;
         trace_p = grid_for(ktp, 0, kTraceBlock);
         trace_e = grid_for(kte, 0, kTraceBlock);
         shadow = grid_for(kts, 0, kTraceBlock);
-        trace_b = grid_for(ktb, 0, kTraceBlock);
         packet = grid_for(ktpk, 0);
         shade_p = grid_for(k_shade_primary, 0);
         shade_e = grid_for(k_shade_extend, 0);
@@ -2769,22 +2601,6 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         pr.end(st);
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         for (int b = 0; b <= base.max_bounces; ++b) {
-            if (RR_MERGE_TRACE && b < base.max_bounces) {  // the shadow walk of b and the extension walk into b + 1
-                const int nb = b + 1;
-                pr.begin(st, RR_K_EXTEND);
-                G.ktb<<<clamp_grid(np, G.trace_b, kTraceBlock), kTraceBlock, 0, st>>>(
-                    sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, tot + 2 * b}, p.hits.ptr, sq,
-                    QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, Rad{reinterpret_cast<float*>(p.rad.ptr)},
-                    p.spill.ptr, tc, tail);
-                pr.end(st);
-                pr.begin(st, RR_K_SHADE);
-                k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},
-                                                       p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)},
-                                                       pq[(nb + 1) & 1], sq, QueueOut{qpath(nb), qshadow(nb), cap_e}, tnrm);
-                pr.end(st);
-                cap_prev = cap_e;
-                continue;
-            }
             pr.begin(st, RR_K_SHADOW);
             G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(
                 sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, Rad{reinterpret_cast<float*>(p.rad.ptr)},
