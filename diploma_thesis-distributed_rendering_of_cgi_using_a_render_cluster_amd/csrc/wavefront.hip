@@ -1683,9 +1683,6 @@ __global__ __launch_bounds__(kBlock) void k_world(FrameConsts fc, float4* __rest
 // whose samples are all culled camera rays, fill the tail.
 constexpr int kTile = 8;  // 8x8 pixels = one wave
 constexpr int kTileShards = 8;      // k_tiles unit counters (one per block % 8)
-#ifndef RR_TILE_STEAL
-#define RR_TILE_STEAL 0
-#endif
 constexpr int kTileCtrStride = 32;  // words between them (128 B)
 
 struct TileOrder {
@@ -2019,25 +2016,12 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     }
     bg = make_float4(uniform_f(bg.x), uniform_f(bg.y), uniform_f(bg.z), 0.0f);
     const uchar4 bg_px = __builtin_bit_cast(uchar4, uniform_i(__builtin_bit_cast(int, tonemap(fc, bg, srgb))));
-#if RR_TILE_STEAL
-    int sh_off = 0;  // RR_TILE_STEAL: once this shard is dealt out, the wave takes units of the next shards
-#endif
     for (;;) {
         int t, k = 0, nk = 1;  // tile, slice, slices of this tile
         int u = 0;
-#if RR_TILE_STEAL
-        const int sh = shard + sh_off < n_shards ? shard + sh_off : shard + sh_off - n_shards;
-        if (lane == 0) u = (int)atomicAdd(tile_ctr + sh * kTileCtrStride, 1u);
-        u = __builtin_amdgcn_readlane(u, 0) * n_shards + sh;
-        if (u >= n_units) {
-            if (++sh_off >= n_shards) break;
-            continue;
-        }
-#else
         if (lane == 0) u = (int)atomicAdd(tile_ctr + shard * kTileCtrStride, 1u);
         u = __builtin_amdgcn_readlane(u, 0) * n_shards + shard;
         if (u >= n_units) break;
-#endif
         if (u < n_sliced) {  // box tiles in the order of k_tile_order (the heaviest first)
             const int j = kWhole ? u : u / n_slices;
             k = kWhole ? 0 : u - j * n_slices;
