@@ -1252,16 +1252,17 @@ int rr_debug_qbvh(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* nq, int32_t* c
 int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int32_t n, const float* rays,
                    float* hits, int32_t* prims, uint8_t* occluded) {
     if (!c || !s || n < 0 || (n > 0 && !rays)) return fail(RR_EINVAL, "bad arguments");
-    if (bvh_width < 0 || bvh_width == 1 || bvh_width > 5)
-        return fail(RR_EINVAL, "hierarchy must be 0 (frame's), 2 (LBVH), 3 (PLOC), 4 (6-wide) or 5 (6-wide, packets)");
+    if (bvh_width < 0 || bvh_width == 1 || bvh_width > 6)
+        return fail(RR_EINVAL, "hierarchy must be 0 (frame's), 2 (LBVH), 3 (PLOC), 4 (6-wide), 5 (6-wide, packets) "
+                               "or 6 (6-wide, one LDS stack entry)");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
         set_device(c);
         PinnedBuf staging;
-        const int hier = bvh_width == 5 ? kHierQWide : (bvh_width ? bvh_width : frame_hier_of(s, fs));
+        const int hier = bvh_width >= 5 ? kHierQWide : (bvh_width ? bvh_width : frame_hier_of(s, fs));
         prepare_frame(c, s, fs, staging, hier);
-        const int width = bvh_width == 5 ? 5 : (hier == kHierQWide ? 4 : 2);
+        const int width = bvh_width >= 5 ? bvh_width : (hier == kHierQWide ? 4 : 2);
         hipStream_t st = c->stream;
         DevBuf<float4> dr, dh;
         DevBuf<int32_t> dp;

@@ -600,28 +600,30 @@ RR_D TriPack load_tri(lds_tri* p, int i) {
     t.p2 = lds_ld4(q + 2);
     return t;
 }
-// kB: the threads per block of the kernel that owns the stack.
-template <int kB = kBlock>
+// kB: the threads per block of the kernel that owns the stack; kL: its LDS
+// entries per lane (rr_debug_trace width 6 runs the 6-wide walk with 1, so
+// nearly every entry lives in the HBM part).
+template <int kB = kBlock, int kL = kLdsStack>
 struct TravStackT {
     // Bases only: the lane's slots are recomputed from threadIdx/blockIdx at each
     // push/pop, so no per-lane pointer stays live in VGPRs across a kernel's
     // ray loop.
     lds_int* lds;   // lds_base: lane slot lds[sp * kB + threadIdx.x]
-    int* spill;     // spill_base: lane slot spill[(sp - kLdsStack) * stride + global thread]
+    int* spill;     // spill_base: lane slot spill[(sp - kL) * stride + global thread]
     int spill_stride;
     int sp;
     // the frame's drop counter (device.hpp drops_slot; null: not counted)
     uint32_t* drops;
-    // A push beyond kLdsStack + kSpillStack entries is dropped (a missed
+    // A push beyond kL + kSpillStack entries is dropped (a missed
     // subtree) and counted at once with an atomic on the frame's drop counter
     // (no register stays live for it; rr_frame_stats.stack_drops, tests assert
     // 0 on every bench scene); the oracle's stack has the same capacity and the
     // same rule (ORC_MAXDEPTH) and counts its drops too (orc_stack_drops).
     RR_D void push(int x) {
-        if (sp < kLdsStack) {
+        if (sp < kL) {
             lds[sp * kB + (int)threadIdx.x] = x;
-        } else if (sp < kLdsStack + kSpillStack) {
-            spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)] = x;
+        } else if (sp < kL + kSpillStack) {
+            spill[(sp - kL) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)] = x;
         } else {
             if (drops) atomicAdd(drops, 1u);
             return;
@@ -630,8 +632,8 @@ struct TravStackT {
     }
     RR_D int pop() {
         --sp;
-        if (sp < kLdsStack) return lds[sp * kB + (int)threadIdx.x];
-        return spill[(sp - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)];
+        if (sp < kL) return lds[sp * kB + (int)threadIdx.x];
+        return spill[(sp - kL) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)];
     }
     // Grouped entries of the 6-wide walk (RR_STACK_GROUP): one entry per node
     // for all the internal children it leaves for later, first child index << 6
@@ -642,8 +644,8 @@ struct TravStackT {
     // gave (the walk visits the same nodes in the same order).
     RR_D int pop_group() {
         const int i = sp - 1;
-        const bool in_lds = i < kLdsStack;
-        const int gi = (i - kLdsStack) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x);
+        const bool in_lds = i < kL;
+        const int gi = (i - kL) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x);
         const int e = in_lds ? lds[i * kB + (int)threadIdx.x] : spill[gi];
         const int node = (int)((uint32_t)e >> 6) + __builtin_ctz((uint32_t)e & 63u);
         const int rest = e & (e - 1);  // the lowest rank bit cleared

@@ -2336,14 +2336,17 @@ __global__ __launch_bounds__(kBlock) void k_debug_packet(const QNode6* __restric
     }
 }
 
+// kL: LDS stack entries per lane (kLdsStack; 1 for rr_debug_trace width 6,
+// which puts nearly every stack entry in the HBM part)
+template <int kL>
 __global__ void k_debug_trace4(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, int n_tris,
                                int n, const float4* __restrict__ rays, float4* __restrict__ hits,
                                int32_t* __restrict__ prims, uint8_t* __restrict__ occ,
                                int32_t* __restrict__ spill) {
-    __shared__ int lds_stack[kLdsStack * kBlock];
+    __shared__ int lds_stack[kL * kBlock];
     const int gtid = blockIdx.x * kBlock + threadIdx.x;
     const int nthreads = gridDim.x * kBlock;
-    TravStack st{lds_slot(lds_stack), spill, nthreads, 0, nullptr};
+    TravStackT<kBlock, kL> st{lds_slot(lds_stack), spill, nthreads, 0, nullptr};
     TravCount cnt;
     for (int i = gtid; i < n; i += nthreads) {
         const float4 o = rays[2 * i], d = rays[2 * i + 1];
@@ -2768,11 +2771,16 @@ void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, f
         if (n > 0)
             k_debug_packet<4><<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims,
                                                     d_occ, p.spill.ptr);
-    } else if (width == 4) {
+    } else if (width == 4 || width == 6) {  // 6: the same walk with one LDS stack entry per lane
         if (!s.has4) throw std::runtime_error("BVH4 not built");
-        if (n > 0)
-            k_debug_trace4<<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,
-                                                 p.spill.ptr);
+        if (n > 0) {
+            if (width == 6)
+                k_debug_trace4<1><<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims,
+                                                        d_occ, p.spill.ptr);
+            else
+                k_debug_trace4<kLdsStack><<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits,
+                                                                d_prims, d_occ, p.spill.ptr);
+        }
     } else if (n > 0)
         k_debug_trace<<<g, kBlock, 0, st>>>(s.nodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims, d_occ,
                                             p.spill.ptr);

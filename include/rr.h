@@ -329,7 +329,9 @@ int rr_debug_qbvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t* nq
 /* Trace a batch of rays against the frame's hierarchy. bvh_width: 2 (LBVH),
  * 4 (the quantised 6-wide collapse), 5 (the same hierarchy walked by the camera
  * kernel's 64-ray packets, with 4 packet-stack entries in LDS so that the
- * stack's HBM part is used; closest hit only, occluded = 255) or 0 (whichever
+ * stack's HBM part is used; closest hit only, occluded = 255), 6 (the
+ * 6-wide per-lane walk with one LDS stack entry per lane, so that its grouped
+ * entries live in the HBM part) or 0 (whichever
  * the frame kernels use for this scene, render_ints[7] of rr_debug_frame_state). rays: n*8 floats
  * (o.xyz, tmin, d.xyz, tmax). hits: n*4 floats (t, u, v, 0), prims: n original
  * triangle ids (-1 miss), occluded: n bytes (any-hit result). */

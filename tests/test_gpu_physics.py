@@ -115,6 +115,22 @@ def test_packet_walk_spills_its_stack_to_hbm(ctx, s02):
     assert (o5 == 255).all()
 
 
+def test_grouped_stack_entries_in_hbm(ctx, s02):
+    """The per-lane 6-wide walk with one LDS stack entry per lane
+    (rr_debug_trace width 6): nearly every grouped stack entry (first internal
+    child + rank mask, rewritten in place as its children come off) lives in
+    the stack's HBM part; closest hits and any-hit answers equal the default
+    walk's (12 LDS entries) and the oracle's."""
+    st = ctx.frame_state(s02, 90)
+    rays = _camera_rays(st, 20000, np.random.default_rng(9))  # camera + random secondary rays
+    h6, p6, o6 = ctx.trace(s02, 90, rays, width=6)
+    h4, p4, o4 = ctx.trace(s02, 90, rays, width=4)
+    oh, op, oo = O.trace(st.tris, rays, width=4)
+    assert np.array_equal(p6, op) and np.array_equal(h6, oh) and np.array_equal(o6, oo)
+    assert np.array_equal(p6, p4) and np.array_equal(o6, o4)
+    assert (p6 >= 0).mean() > 0.2 and 0 < o6.mean() < 1
+
+
 @pytest.mark.parametrize("frame", [1, 90])
 def test_physics_qbvh_bit_exact(ctx, s02, frame):
     st = ctx.frame_state(s02, frame)
