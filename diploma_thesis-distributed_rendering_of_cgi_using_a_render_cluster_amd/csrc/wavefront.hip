@@ -98,10 +98,13 @@ struct SceneView {
     FloatP mats, lights, filter;
     FloatP lut;  // material tables (kMatLutStride floats per material, build_material_lut)
     lds_f4w* cam = nullptr;  // LDS scenes, camera kernels: 3 float4 per triangle (stage_camera)
-    lds_f4w* nrm = nullptr;   // LDS scenes, shading kernels: unit geometric normal per triangle
+    // unit geometric normal + material per triangle: LDS scenes' staged copy
+    // (shading kernels), HBM scenes' DevScene::tnrm (RR_SHADE_NRM) — one
+    // member for both, so the LDS view passed to k_tiles' out-of-line calls
+    // stays the size it was
+    typename std::conditional<std::is_same<FloatP, lds_float*>::value, lds_f4w*, const float4*>::type nrm = nullptr;
     lds_f4w* matd = nullptr;  // LDS scenes, shading kernels: each material with its derived terms (kMatDF4)
     lds_f4w* onb = nullptr;   // LDS scenes, shading kernels: make_onb of both sides' normals (kOnbF4 per triangle)
-    const float4* gnrm = nullptr;  // HBM scenes, shading kernels: DevScene::tnrm (RR_SHADE_NRM)
 };
 // RR_SHADE_NRM (default): the split path's shading reads each hit triangle's
 // normal and material from DevScene::tnrm (16 B) instead of its 48 B record
@@ -307,8 +310,8 @@ __device__ __forceinline__ void shade(const FC& fc, int bounce, const View& v, f
         // table offsets become 24-bit multiplies (full rate) instead of
         // v_mul_lo_u32 / v_mad_u64_u32
         __builtin_assume(mid >= 0 && mid < 4096);
-    } else if (RR_SHADE_NRM && v.gnrm) {
-        const float4 nm = v.gnrm[h.idx];  // k_tri_nrm: the same normal, precomputed
+    } else if (RR_SHADE_NRM && v.nrm) {
+        const float4 nm = v.nrm[h.idx];  // k_tri_nrm: the same normal, precomputed
         N = xyz(nm);
         mid = f2i(nm.w);
     } else {
@@ -1458,7 +1461,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
                                                           PathQueue out, ShadowQueue sq, QueueOut qo,
                                                           const float4* __restrict__ tnrm) {
     GlobalView v = global_view(sa);
-    v.gnrm = tnrm;
+    v.nrm = tnrm;
     const int stride = gridDim.x * kBlock;
     for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {
         const int p = b0 + (int)threadIdx.x;
@@ -1516,7 +1519,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
     qm.init(qi);
     const int count = qm.span;
     GlobalView v = global_view(sa);
-    v.gnrm = tnrm;
+    v.nrm = tnrm;
     const int stride = gridDim.x * kBlock;
     int pid = 0;
     for (int b0 = blockIdx.x * kBlock; b0 < count; b0 += stride) {
