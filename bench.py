@@ -614,6 +614,9 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=No
             out["issue_util_at_kernel_clock"] = round(out["achieved"] * 1e9 /
                                                       (VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * kc * 1e9), 3)
         out["wave_fill_solo"] = round(float(getattr(cstats, "kernel_wave_fill", 0.0)), 3)
+        # spread of the counting launch's wave starts and ends over its span
+        out["wave_entry_spread_solo"] = round(float(getattr(cstats, "kernel_entry_spread", 0.0)), 3)
+        out["wave_exit_spread_solo"] = round(float(getattr(cstats, "kernel_exit_spread", 0.0)), 3)
         lu = (e_wh or {}).get("valu_lane_util") if (timed and timed["whole"]) else (e_sl or {}).get("valu_lane_util")
         if lu is not None:  # active lanes per issued VALU instruction (PMC, SQ_THREAD_CYCLES_VALU)
             out["valu_lane_util"] = round(lu, 3)

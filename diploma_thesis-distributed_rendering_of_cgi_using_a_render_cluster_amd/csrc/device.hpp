@@ -207,9 +207,10 @@ constexpr int kUploadMax = 720;
 // RR_FLAG_COUNT_TRAVERSAL words: [0..5] traversal totals (nodes, triangles per
 // class); k_tiles' counting launch: [6] shader-clock ticks and [7] real-time
 // ticks after the scene staging, [8] waves, [9] real-time ticks from entry,
-// [10] ~first entry, [11] last end (rr_api.cpp fill_stats). (Traversal-stack
-// drops are counted in every frame, in the chunk counters: drops_slot.)
-constexpr int kTravWords = 12;
+// [10] ~first entry, [11] last end, [12] last entry, [13] ~first end
+// (rr_api.cpp fill_stats). (Traversal-stack drops are counted in every
+// frame, in the chunk counters: drops_slot.)
+constexpr int kTravWords = 14;
 struct UploadSeg {
     float* dst;
     int n;

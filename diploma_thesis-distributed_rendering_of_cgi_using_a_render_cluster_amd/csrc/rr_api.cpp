@@ -674,6 +674,9 @@ void fill_stats(rr_frame_stats* st, const FrameSetup& fs, const FrameRun& r, int
         st->kernel_clock_ghz = w[7] ? 0.1 * (double)w[6] / (double)w[7] : 0.0;
         const unsigned long long t0 = ~w[10], t1 = w[11];
         st->kernel_wave_fill = (w[8] && t1 > t0) ? (double)w[9] / (double)w[8] / (double)(t1 - t0) : 0.0;
+        const unsigned long long e1 = w[12], x0 = ~w[13];
+        st->kernel_entry_spread = (w[8] && t1 > t0 && e1 >= t0) ? (double)(e1 - t0) / (double)(t1 - t0) : 0.0;
+        st->kernel_exit_spread = (w[8] && t1 > t0 && t1 >= x0) ? (double)(t1 - x0) / (double)(t1 - t0) : 0.0;
     }
     st->stack_drops = (int32_t)std::min<uint64_t>(drops, 0x7fffffffull);
     if (r.tile_slices > 0) {

@@ -2134,6 +2134,8 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             atomicAdd(&tc[9], rt1 - rt_entry);
             atomicMax(&tc[10], ~rt_entry);  // the first entry, complemented (the words start at 0)
             atomicMax(&tc[11], rt1);
+            atomicMax(&tc[12], rt_entry);  // the last entry
+            atomicMax(&tc[13], ~rt1);      // the first end, complemented
         }
     }
 }

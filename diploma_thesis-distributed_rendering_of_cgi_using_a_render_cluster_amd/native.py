@@ -21,7 +21,7 @@ RR_OK, RR_ENOENT, RR_EIO, RR_ENOMEM, RR_ENODEV, RR_EINVAL, RR_ENOTSUP = 0, -2, -
 RR_EBUSY = -16
 RR_MAX_FRAMES_IN_FLIGHT = 3
 RR_VIEW_SCENE, RR_VIEW_STANDARD, RR_VIEW_RAW, RR_VIEW_FILMIC = -1, 0, 1, 2
-RR_ABI_VERSION = 7
+RR_ABI_VERSION = 8
 QWIDTH = 6  # children per quantised node of the split path (rr_device.h kQWidth)
 RR_CAM_FLOATS, RR_LIGHT_FLOATS, RR_MAT_FLOATS, RR_RENDER_INTS, RR_RENDER_FLOATS = 16, 12, 12, 10, 4
 
@@ -62,7 +62,8 @@ class FrameStats(ctypes.Structure):
                 ("view_transform_substituted", ctypes.c_int32), ("kernel_clock_ghz", ctypes.c_double),
                 ("kernel_wave_fill", ctypes.c_double), ("tile_slices", ctypes.c_int32),
                 ("stack_drops", ctypes.c_int32),
-                ("extension_rays_escaped", ctypes.c_uint64), ("shadow_rays_escaped", ctypes.c_uint64)]
+                ("extension_rays_escaped", ctypes.c_uint64), ("shadow_rays_escaped", ctypes.c_uint64),
+                ("kernel_entry_spread", ctypes.c_double), ("kernel_exit_spread", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         out = {}

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 7
+#define RR_ABI_VERSION 8
 
 /* error codes (negative errno values) */
 #define RR_OK 0
@@ -163,6 +163,12 @@ typedef struct rr_frame_stats {
      * - shadow_rays_escaped. 0 on the split path (every ray is traversed). */
     uint64_t extension_rays_escaped;
     uint64_t shadow_rays_escaped;
+    /* RR_FLAG_COUNT_TRAVERSAL, LDS-resident scenes (with kernel_wave_fill):
+     * the spread of the tile kernel's wave starts (last start - first start)
+     * and of its wave ends (last end - first end), each over the launch's span;
+     * 0 when not measured */
+    double kernel_entry_spread;
+    double kernel_exit_spread;
 } rr_frame_stats;
 
 /* Fill p with "use the scene's value" for every field. */

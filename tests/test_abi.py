@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(rr):
 
 
 def test_abi_version(rr):
-    assert rr.lib().rr_abi_version() == 7 == rr.native.RR_ABI_VERSION
+    assert rr.lib().rr_abi_version() == 8 == rr.native.RR_ABI_VERSION
 
 
 def test_struct_layouts_match_header(rr):
