@@ -1685,7 +1685,10 @@ __global__ __launch_bounds__(kBlock) void k_world(FrameConsts fc, float4* __rest
 // and shading work, so the long tiles start early and the background tiles,
 // whose samples are all culled camera rays, fill the tail.
 constexpr int kTile = 8;  // 8x8 pixels = one wave
-constexpr int kTileShards = 8;      // k_tiles unit counters (one per block % 8)
+#ifndef RR_TILE_SHARDS
+#define RR_TILE_SHARDS 8
+#endif
+constexpr int kTileShards = RR_TILE_SHARDS;  // k_tiles unit counters (one per block % 8)
 constexpr int kTileCtrStride = 32;  // words between them (128 B)
 
 struct TileOrder {
