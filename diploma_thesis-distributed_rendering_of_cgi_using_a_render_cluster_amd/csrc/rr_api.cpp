@@ -1296,6 +1296,25 @@ int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int
     });
 }
 
+int rr_debug_tile_costs(rr_ctx* c, int32_t capacity, uint32_t* costs, int32_t* order, int32_t* n_tiles) {
+    if (!c || capacity < 0 || !n_tiles || (capacity > 0 && (!costs || !order))) return fail(RR_EINVAL, "bad arguments");
+    return guarded([&] {
+        if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
+        *n_tiles = 0;
+        const FrameSlot* sl = c->last_enqueued;
+        if (!sl || !sl->tiles) return RR_OK;  // no tile frame yet
+        set_device(c);
+        const size_t n = std::min(sl->tile_cost.cap, sl->tile_order.cap);
+        *n_tiles = (int32_t)n;
+        const size_t m = std::min<size_t>(n, (size_t)capacity);
+        if (m > 0) {
+            RR_HIP(hipMemcpy(costs, sl->tile_cost.ptr, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            RR_HIP(hipMemcpy(order, sl->tile_order.ptr, m * sizeof(int32_t), hipMemcpyDeviceToHost));
+        }
+        return RR_OK;
+    });
+}
+
 int rr_debug_fastmath_check(rr_ctx* c, uint32_t lo, uint64_t n, uint64_t* counts5) {
     if (!c || !counts5 || n > (1ull << 32) - lo) return fail(RR_EINVAL, "bad arguments");
     return guarded([&] {

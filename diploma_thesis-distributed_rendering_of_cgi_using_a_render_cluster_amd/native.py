@@ -85,7 +85,7 @@ EXPORTS = [
     "rr_last_warning", "rr_set_ocio_config", "rr_synchronize",
     "rr_scene_free", "rr_destroy", "rr_debug_counts", "rr_debug_scene_mesh", "rr_debug_frame_state", "rr_debug_bvh",
     "rr_debug_trace", "rr_debug_object_matrix", "rr_debug_qbvh", "rr_debug_bvh_hier", "rr_debug_jpeg_device",
-    "rr_debug_bsdf_sample", "rr_debug_fastmath_check",
+    "rr_debug_bsdf_sample", "rr_debug_fastmath_check", "rr_debug_tile_costs",
 ]
 
 _lib = None
@@ -142,6 +142,8 @@ def lib() -> ctypes.CDLL:
         "rr_debug_object_matrix": (c_int, [P, i32, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]),
         "rr_debug_bsdf_sample": (c_int, [P, f32p, f32p, f32p, i32, f32p, f32p, f32p, f32p, i32p]),
         "rr_debug_fastmath_check": (c_int, [P, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+        "rr_debug_tile_costs": (c_int, [P, c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
+                                        ctypes.POINTER(ctypes.c_int32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -410,6 +412,17 @@ class RenderContext:
         out = (ctypes.c_uint64 * 5)()
         _check(lib().rr_debug_fastmath_check(self.handle, int(lo), int(n), out), self.handle)
         return tuple(int(v) for v in out)
+
+    def tile_costs(self, capacity: int = 1 << 20):
+        """rr_debug_tile_costs: (per-tile real-time ticks of the last tile frame's
+        units, the box tiles' hand-out order it used), each of the slot buffers' length."""
+        costs = np.zeros(capacity, np.uint32)
+        order = np.zeros(capacity, np.int32)
+        n = ctypes.c_int32(0)
+        _check(lib().rr_debug_tile_costs(self.handle, capacity, _ptr(costs, ctypes.c_uint32),
+                                         _ptr(order, ctypes.c_int32), ctypes.byref(n)), self.handle)
+        m = min(int(n.value), capacity)
+        return costs[:m], order[:m]
 
     def trace(self, scene: Scene, frame: int, rays: np.ndarray, width: int = 0):
         """rr_debug_trace; width 0 = the hierarchy the frame kernels use."""

@@ -361,6 +361,15 @@ int rr_debug_bsdf_sample(rr_ctx* ctx, const float* mat12, const float* n3, const
  * sqrt_any mismatches (must be 0), [3] = rcp_rn mismatches with |x| in
  * [2^-126, 2^126) (must be 0), [4] = rcp_rn mismatches outside it. Test
  * infrastructure for the bit-exactness claim; no reference counterpart. */
+/* The tile kernel's scheduling record of the last frame enqueued (LDS-resident
+ * scenes): per screen tile (8x8 pixels, row-major), the real-time ticks
+ * (100 MHz) its work units took in that frame's k_tiles launch (0 for tiles
+ * outside the scene's screen box), and the box tiles' hand-out order that
+ * launch used (built from the launch before it; its first entries are the
+ * box tiles). Up to `capacity` entries of each; *n_tiles = the length of the
+ * slot's buffers (at least the frame's tile count; 0: no tile frame yet). */
+int rr_debug_tile_costs(rr_ctx* ctx, int32_t capacity, uint32_t* costs, int32_t* order, int32_t* n_tiles);
+
 int rr_debug_fastmath_check(rr_ctx* ctx, uint32_t lo, uint64_t n, uint64_t* counts5);
 
 /* Host animation evaluation: object_to_world matrix (row-major 4x4, f64) of
