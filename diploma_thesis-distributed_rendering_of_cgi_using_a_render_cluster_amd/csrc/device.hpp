@@ -211,6 +211,9 @@ constexpr int kUploadMax = 720;
 // (rr_api.cpp fill_stats). (Traversal-stack drops are counted in every
 // frame, in the chunk counters: drops_slot.)
 constexpr int kTravWords = 14;
+// k_tiles' counting launch also logs each box unit u < kUnitLog: words
+// kTravWords + 2u / + 2u + 1 = its start / end real-time ticks (rr_debug_tile_costs)
+constexpr int kUnitLog = 1 << 16;
 struct UploadSeg {
     float* dst;
     int n;

@@ -1296,8 +1296,11 @@ int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int
     });
 }
 
-int rr_debug_tile_costs(rr_ctx* c, int32_t capacity, uint32_t* costs, int32_t* order, int32_t* n_tiles) {
-    if (!c || capacity < 0 || !n_tiles || (capacity > 0 && (!costs || !order))) return fail(RR_EINVAL, "bad arguments");
+int rr_debug_tile_costs(rr_ctx* c, int32_t capacity, uint32_t* costs, int32_t* order, int32_t* n_tiles,
+                        uint64_t* unit_log, int32_t unit_capacity) {
+    if (!c || capacity < 0 || !n_tiles || (capacity > 0 && (!costs || !order)) || unit_capacity < 0 ||
+        (unit_capacity > 0 && !unit_log))
+        return fail(RR_EINVAL, "bad arguments");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         *n_tiles = 0;
@@ -1310,6 +1313,13 @@ int rr_debug_tile_costs(rr_ctx* c, int32_t capacity, uint32_t* costs, int32_t* o
         if (m > 0) {
             RR_HIP(hipMemcpy(costs, sl->tile_cost.ptr, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
             RR_HIP(hipMemcpy(order, sl->tile_order.ptr, m * sizeof(int32_t), hipMemcpyDeviceToHost));
+        }
+        const size_t nu = std::min<size_t>((size_t)unit_capacity, kUnitLog);
+        if (nu > 0) {
+            std::memset(unit_log, 0, 2 * nu * sizeof(uint64_t));
+            if (sl->trav_counts.cap >= (size_t)(kTravWords + 2 * kUnitLog))
+                RR_HIP(hipMemcpy(unit_log, sl->trav_counts.ptr + kTravWords, 2 * nu * sizeof(uint64_t),
+                                 hipMemcpyDeviceToHost));
         }
         return RR_OK;
     });

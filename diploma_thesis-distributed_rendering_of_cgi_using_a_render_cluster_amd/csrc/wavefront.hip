@@ -2120,8 +2120,14 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
             film[pix] = acc;
             out[pix] = tonemap(fc, acc, srgb);
         }
-        if (lane == 0)  // this unit's time, for the next launch's hand-out order (k_tile_order)
-            atomicAdd(&sl.cost[ty * to.tx + tx], (uint32_t)(__builtin_amdgcn_s_memrealtime() - u_start));
+        if (lane == 0) {  // this unit's time, for the next launch's hand-out order (k_tile_order)
+            const unsigned long long u_end = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(&sl.cost[ty * to.tx + tx], (uint32_t)(u_end - u_start));
+            if (kCount && u < kUnitLog) {  // the counting launch's unit log (device.hpp kUnitLog)
+                tc[kTravWords + 2 * u] = u_start;
+                tc[kTravWords + 2 * u + 1] = u_end;
+            }
+        }
     }
     uint32_t* const tail = tot + camera_traced_slot(fc.max_bounces);
     n_c1 = tt.wctr[0];  // the later bounces (tiles_continue)
@@ -2655,8 +2661,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         p.counters.ensure(n_ctr);  // zeroed by k_tile_order
         unsigned long long* tc = nullptr;
         if (p.count_traversal) {
-            p.trav_counts.ensure(kTravWords);
-            RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, kTravWords * sizeof(unsigned long long), st));
+            p.trav_counts.ensure(kTravWords + 2 * kUnitLog);
+            RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, (kTravWords + 2 * kUnitLog) * sizeof(unsigned long long), st));
             tc = p.trav_counts.ptr;
         }
         const SceneArgs sa{s.nodes.ptr, s.qnodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,

@@ -143,7 +143,7 @@ def lib() -> ctypes.CDLL:
         "rr_debug_bsdf_sample": (c_int, [P, f32p, f32p, f32p, i32, f32p, f32p, f32p, f32p, i32p]),
         "rr_debug_fastmath_check": (c_int, [P, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
         "rr_debug_tile_costs": (c_int, [P, c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
-                                        ctypes.POINTER(ctypes.c_int32)]),
+                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint64), c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -413,16 +413,20 @@ class RenderContext:
         _check(lib().rr_debug_fastmath_check(self.handle, int(lo), int(n), out), self.handle)
         return tuple(int(v) for v in out)
 
-    def tile_costs(self, capacity: int = 1 << 20):
+    def tile_costs(self, capacity: int = 1 << 20, units: int = 1 << 16):
         """rr_debug_tile_costs: (per-tile real-time ticks of the last tile frame's
-        units, the box tiles' hand-out order it used), each of the slot buffers' length."""
+        units, the box tiles' hand-out order it used, each of the slot buffers'
+        length; per box unit u its (start, end) ticks when that frame was a
+        counting frame, shape (units, 2))."""
         costs = np.zeros(capacity, np.uint32)
         order = np.zeros(capacity, np.int32)
+        log = np.zeros((max(units, 1), 2), np.uint64)
         n = ctypes.c_int32(0)
         _check(lib().rr_debug_tile_costs(self.handle, capacity, _ptr(costs, ctypes.c_uint32),
-                                         _ptr(order, ctypes.c_int32), ctypes.byref(n)), self.handle)
+                                         _ptr(order, ctypes.c_int32), ctypes.byref(n),
+                                         _ptr(log, ctypes.c_uint64), units), self.handle)
         m = min(int(n.value), capacity)
-        return costs[:m], order[:m]
+        return costs[:m], order[:m], log[:units]
 
     def trace(self, scene: Scene, frame: int, rays: np.ndarray, width: int = 0):
         """rr_debug_trace; width 0 = the hierarchy the frame kernels use."""

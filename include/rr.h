@@ -367,8 +367,13 @@ int rr_debug_bsdf_sample(rr_ctx* ctx, const float* mat12, const float* n3, const
  * outside the scene's screen box), and the box tiles' hand-out order that
  * launch used (built from the launch before it; its first entries are the
  * box tiles). Up to `capacity` entries of each; *n_tiles = the length of the
- * slot's buffers (at least the frame's tile count; 0: no tile frame yet). */
-int rr_debug_tile_costs(rr_ctx* ctx, int32_t capacity, uint32_t* costs, int32_t* order, int32_t* n_tiles);
+ * slot's buffers (at least the frame's tile count; 0: no tile frame yet).
+ * unit_log (may be null): when that frame was rendered with
+ * RR_FLAG_COUNT_TRAVERSAL, per box work unit u (hand-out number, below
+ * unit_capacity and 65536) its start and end real-time ticks (2 per unit;
+ * 0, 0: not logged). */
+int rr_debug_tile_costs(rr_ctx* ctx, int32_t capacity, uint32_t* costs, int32_t* order, int32_t* n_tiles,
+                        uint64_t* unit_log, int32_t unit_capacity);
 
 int rr_debug_fastmath_check(rr_ctx* ctx, uint32_t lo, uint64_t n, uint64_t* counts5);
 

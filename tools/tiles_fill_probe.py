@@ -30,29 +30,32 @@ def main():
         pc = rr.default_params(flags=rr.native.RR_FLAG_COUNT_TRAVERSAL, **kw)
         pt = rr.default_params(flags=rr.native.RR_FLAG_PROFILE_KERNELS, **kw)
         ctx.render_to_memory(s, frame, pt, film=False, rgba=True)
-        st = ctx.render_to_memory(s, frame, pc, film=False, rgba=True)[2]
         best = min(sum(ctx.render_to_memory(s, frame, pt, film=False, rgba=True)[2].kernel_ms) for _ in range(3))
+        st = ctx.render_to_memory(s, frame, pc, film=False, rgba=True)[2]  # last: its unit log is read below
         out = {"lib": os.environ.get("RR_LIB_PATH", "in-tree"), "wave_fill": round(st.kernel_wave_fill, 3),
                "entry_spread": round(st.kernel_entry_spread, 3), "exit_spread": round(st.kernel_exit_spread, 3),
                "tile_slices": st.tile_slices, "solo_kernel_ms": round(best, 3)}
         if hasattr(ctx, "tile_costs"):
-            # the units of the last frame (one of the solo renders): per tile, ticks of 10 ns summed
-            # over its slices; the box tiles in the hand-out order that launch used
-            costs, order = ctx.tile_costs()
-            n = ((st.width + 7) // 8) * ((st.height + 7) // 8)
-            c = costs[:n].astype(np.float64) * 1e-5  # ms
-            box = int(np.count_nonzero(c))
-            unit = c[c > 0] / max(st.tile_slices, 1)
-            o = order[:box]
-            pos = {int(t): i for i, t in enumerate(o)}
-            heavy = np.argsort(-c)[:20]
-            out.update({"box_tiles": box, "unit_ms_mean": round(float(unit.mean()), 4) if box else 0,
-                        "unit_ms_p99": round(float(np.percentile(unit, 99)), 4) if box else 0,
-                        "unit_ms_max": round(float(unit.max()), 4) if box else 0,
-                        "sum_unit_ms_over_waves": round(float(c.sum()) / 4096.0, 4),
-                        "heaviest_20_order_positions": [pos.get(int(t), -1) for t in heavy],
-                        "cost_decile_ms_by_order": [round(float(c[o[i * box // 10:(i + 1) * box // 10]].mean()), 4)
-                                                    for i in range(10)] if box >= 10 else []})
+            costs, order, log = ctx.tile_costs()
+            logged = np.nonzero(log[:, 1])[0]  # box units u (hand-out numbers) of the counting launch
+            if logged.size:
+                st0 = log[logged, 0].astype(np.float64)
+                en = log[logged, 1].astype(np.float64)
+                t0 = st0.min()
+                span = en.max() - t0
+                dur = (en - st0) * 1e-5  # ms
+                j = logged // max(st.tile_slices, 1)  # position in the hand-out order
+                last = np.argsort(-en)[:10]
+                dec = np.array_split(np.argsort(j), 10)
+                out.update({
+                    "units_logged": int(logged.size), "unit_ms_mean": round(float(dur.mean()), 4),
+                    "unit_ms_max": round(float(dur.max()), 4),
+                    "last_unit_start_frac": round(float((st0.max() - t0) / span), 3),
+                    "unit_ms_by_order_decile": [round(float(dur[d].mean()), 4) for d in dec],
+                    "start_frac_by_order_decile": [round(float(((st0[d] - t0) / span).mean()), 3) for d in dec],
+                    "last10_ending": [{"u": int(logged[i]), "pos_frac": round(float(j[i]) / max(1, int(j.max())), 3),
+                                       "start_frac": round(float((st0[i] - t0) / span), 3),
+                                       "ms": round(float(dur[i]), 4)} for i in last]})
         print(json.dumps(out), flush=True)
         s.close()
 
