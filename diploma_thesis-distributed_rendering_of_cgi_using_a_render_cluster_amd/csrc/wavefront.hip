@@ -1818,12 +1818,14 @@ RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint3
 // reference, which put them (and the LdsView) in scratch: written by every
 // wave at launch, and every wave's scratch lines went back to HBM — most of
 // k_tiles' 124-140 MB of PMC traffic per launch against 41 MB compulsory.
+constexpr int kWctr = 8;  // LDS counter words per wave of k_tiles (TileTrav::wctr)
 struct TileTrav {
     lds_int* lds;
     int* spill;
     int stride;
     uint32_t* drops;
-    lds_uint* wctr;
+    lds_uint* wctr;  // this wave's kWctr LDS words: [0] / [1] bounce-1.. continuation / shadow rays, [2] / [3]
+                     // traversed extension / shadow rays, counting launches: [4..7] their nodes / triangles
     unsigned long long* tc;
 };
 // Active lanes of the wave whose predicate holds: the tile kernel's ray
@@ -1841,9 +1843,10 @@ __device__ __noinline__ bool shadow_trace(LdsView v, int n_tris, float3 so, floa
     TravCount cnt;
     Hit hs;
     const bool occ = traverse<true, kCount>(v.nodes, v.tris, n_tris, so, sd, 0.0f, dist, st, hs, cnt);
-    if (kCount) {
-        atomicAdd(&tt.tc[4], (unsigned long long)cnt.nodes);
-        atomicAdd(&tt.tc[5], (unsigned long long)cnt.tris);
+    if (kCount) {  // the wave's LDS words, flushed once per wave (a global atomic per lane and call
+                   // serialised the counting launch on one address)
+        __hip_atomic_fetch_add(tt.wctr + 6, cnt.nodes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(tt.wctr + 7, cnt.tris, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     return occ;
 }
@@ -1855,8 +1858,8 @@ __device__ __noinline__ Hit ext_trace(LdsView v, int n_tris, float3 o, float3 d,
     Hit h;
     traverse<false, kCount>(v.nodes, v.tris, n_tris, o, d, 0.0f, kFltMax, st, h, cnt);
     if (kCount) {
-        atomicAdd(&tt.tc[2], (unsigned long long)cnt.nodes);
-        atomicAdd(&tt.tc[3], (unsigned long long)cnt.tris);
+        __hip_atomic_fetch_add(tt.wctr + 4, cnt.nodes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(tt.wctr + 5, cnt.tris, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     return h;
 }
@@ -1981,7 +1984,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         clk0 = __builtin_amdgcn_s_memtime();
         rt0 = __builtin_amdgcn_s_memrealtime();
     }
-    const TileTrav tt{stack, spill, stride, tot + drops_slot(fc.max_bounces), cont_ctr + 4 * (threadIdx.x >> 6), tc};
+    const TileTrav tt{stack, spill, stride, tot + drops_slot(fc.max_bounces), cont_ctr + kWctr * (threadIdx.x >> 6), tc};
     TravCount cp;
     uint32_t n_c0 = 0, n_s0 = 0, n_c1 = 0, n_s1 = 0, n_t0 = 0;
     // The screen rectangle and the tile order come from the root node in LDS,
@@ -2133,6 +2136,12 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
     n_c1 = tt.wctr[0];  // the later bounces (tiles_continue)
     n_s1 = tt.wctr[1];
     flush_rays(tot, n_c0, n_s0, n_c1, n_s1, tail, n_t0, tt.wctr[2], tt.wctr[3]);
+    if (kCount && lane == 0) {  // the secondary walks' node / triangle counts of this wave
+        atomicAdd(&tc[2], (unsigned long long)tt.wctr[4]);
+        atomicAdd(&tc[3], (unsigned long long)tt.wctr[5]);
+        atomicAdd(&tc[4], (unsigned long long)tt.wctr[6]);
+        atomicAdd(&tc[5], (unsigned long long)tt.wctr[7]);
+    }
     if (kCount) {
         flush_counts(tc, 0, cp.nodes, cp.tris);
         const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
@@ -2175,10 +2184,10 @@ __global__ __launch_bounds__(kBlock, kWhole ? RR_TILES_WAVES_WHOLE : RR_TILES_WA
                                                                   TileSlices sl) {
     const unsigned long long rt_entry = kCount ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ int lds_stack[kLdsStack * kBlock];
-    __shared__ uint32_t cont_ctr[4 * kWavesPerBlock];  // per wave: TileTrav::wctr
+    __shared__ uint32_t cont_ctr[kWctr * kWavesPerBlock];  // per wave: TileTrav::wctr
     extern __shared__ float4 dyn4[];
     lds_int* stack = lds_slot(lds_stack);
-    if (threadIdx.x < 4 * kWavesPerBlock) cont_ctr[threadIdx.x] = 0u;  // stage_scene ends with a barrier
+    if (threadIdx.x < kWctr * kWavesPerBlock) cont_ctr[threadIdx.x] = 0u;  // stage_scene ends with a barrier
     int used;
     const LdsView v = stage_scene<true>((lds_f4w*)dyn4, sa, true, used, &fc);
     tiles_body<kCount, kWhole>(fc, v, tile_ctr, film, srgb, out, tot, spill, tc, stack, sl, rt_entry,
