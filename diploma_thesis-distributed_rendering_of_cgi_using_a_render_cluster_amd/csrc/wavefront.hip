@@ -1819,6 +1819,9 @@ RR_D void flush_rays(uint32_t* __restrict__ tot, uint32_t c0, uint32_t s0, uint3
 // wave at launch, and every wave's scratch lines went back to HBM — most of
 // k_tiles' 124-140 MB of PMC traffic per launch against 41 MB compulsory.
 constexpr int kWctr = 8;  // LDS counter words per wave of k_tiles (TileTrav::wctr)
+#ifndef RR_TILES_LOG_ALWAYS
+#define RR_TILES_LOG_ALWAYS 0  // diagnostic builds: the unit log in every k_tiles launch, not only counting ones
+#endif
 struct TileTrav {
     lds_int* lds;
     int* spill;
@@ -2126,7 +2129,7 @@ RR_D void tiles_body(const FrameConsts& fc, const LdsView& v, uint32_t* __restri
         if (lane == 0) {  // this unit's time, for the next launch's hand-out order (k_tile_order)
             const unsigned long long u_end = __builtin_amdgcn_s_memrealtime();
             atomicAdd(&sl.cost[ty * to.tx + tx], (uint32_t)(u_end - u_start));
-            if (kCount && u < kUnitLog) {  // the counting launch's unit log (device.hpp kUnitLog)
+            if ((kCount || RR_TILES_LOG_ALWAYS) && u < kUnitLog) {  // the counting launch's unit log (device.hpp kUnitLog)
                 tc[kTravWords + 2 * u] = u_start;
                 tc[kTravWords + 2 * u + 1] = u_end;
             }
@@ -2669,7 +2672,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
         const size_t n_ctr = (size_t)cpc * n_chunks;
         p.counters.ensure(n_ctr);  // zeroed by k_tile_order
         unsigned long long* tc = nullptr;
-        if (p.count_traversal) {
+        if (p.count_traversal || RR_TILES_LOG_ALWAYS) {  // (RR_TILES_LOG_ALWAYS: diagnostic builds log every launch's units)
             p.trav_counts.ensure(kTravWords + 2 * kUnitLog);
             RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, (kTravWords + 2 * kUnitLog) * sizeof(unsigned long long), st));
             tc = p.trav_counts.ptr;

@@ -30,9 +30,15 @@ def main():
         pc = rr.default_params(flags=rr.native.RR_FLAG_COUNT_TRAVERSAL, **kw)
         pt = rr.default_params(flags=rr.native.RR_FLAG_PROFILE_KERNELS, **kw)
         ctx.render_to_memory(s, frame, pt, film=False, rgba=True)
-        best = min(sum(ctx.render_to_memory(s, frame, pt, film=False, rgba=True)[2].kernel_ms) for _ in range(3))
-        st = ctx.render_to_memory(s, frame, pc, film=False, rgba=True)[2]  # last: its unit log is read below
-        out = {"lib": os.environ.get("RR_LIB_PATH", "in-tree"), "wave_fill": round(st.kernel_wave_fill, 3),
+        solo_log = os.environ.get("RR_PROBE_SOLO_LOG") == "1"  # a library built with RR_TILES_LOG_ALWAYS=1
+        if solo_log:  # the unit log of the last solo (non-counting) launch
+            st = ctx.render_to_memory(s, frame, pc, film=False, rgba=True)[2]
+            best = min(sum(ctx.render_to_memory(s, frame, pt, film=False, rgba=True)[2].kernel_ms) for _ in range(3))
+        else:  # the counting launch's
+            best = min(sum(ctx.render_to_memory(s, frame, pt, film=False, rgba=True)[2].kernel_ms) for _ in range(3))
+            st = ctx.render_to_memory(s, frame, pc, film=False, rgba=True)[2]
+        out = {"lib": os.environ.get("RR_LIB_PATH", "in-tree"), "log_of": "solo" if solo_log else "counting",
+               "wave_fill": round(st.kernel_wave_fill, 3),
                "entry_spread": round(st.kernel_entry_spread, 3), "exit_spread": round(st.kernel_exit_spread, 3),
                "tile_slices": st.tile_slices, "solo_kernel_ms": round(best, 3)}
         if hasattr(ctx, "tile_costs"):
