@@ -31,8 +31,11 @@ def main():
         pt = rr.default_params(flags=rr.native.RR_FLAG_PROFILE_KERNELS, **kw)
         ctx.render_to_memory(s, frame, pt, film=False, rgba=True)
         solo_log = os.environ.get("RR_PROBE_SOLO_LOG") == "1"  # a library built with RR_TILES_LOG_ALWAYS=1
+        prev_costs = None
         if solo_log:  # the unit log of the last solo (non-counting) launch
             st = ctx.render_to_memory(s, frame, pc, film=False, rgba=True)[2]
+            ctx.render_to_memory(s, frame, pt, film=False, rgba=True)
+            prev_costs = ctx.tile_costs(units=0)[0].copy()  # recorded by the launch 3 frames (one slot) before the last
             best = min(sum(ctx.render_to_memory(s, frame, pt, film=False, rgba=True)[2].kernel_ms) for _ in range(3))
         else:  # the counting launch's
             best = min(sum(ctx.render_to_memory(s, frame, pt, film=False, rgba=True)[2].kernel_ms) for _ in range(3))
@@ -62,6 +65,25 @@ def main():
                     "last10_ending": [{"u": int(logged[i]), "pos_frac": round(float(j[i]) / max(1, int(j.max())), 3),
                                        "start_frac": round(float((st0[i] - t0) / span), 3),
                                        "ms": round(float(dur[i]), 4)} for i in last]})
+            if prev_costs is not None:  # does the last launch's hand-out order follow the costs it was built from?
+                nzt = np.nonzero(prev_costs[:((st.width + 7) // 8) * ((st.height + 7) // 8)])[0]
+                tx = (st.width + 7) // 8
+                if nzt.size:
+                    xs, ys = nzt % tx, nzt // tx
+                    bx0, by0, bw = int(xs.min()), int(ys.min()), int(xs.max() - xs.min() + 1)
+                    bh = int(ys.max() - ys.min() + 1)
+                    nb = bw * bh
+                    o = order[:nb]
+                    if sorted(o.tolist()) == list(range(nb)):
+                        scr = (by0 + o // bw) * tx + (bx0 + o % bw)
+                        pc_ms = prev_costs[scr].astype(np.float64) * 1e-5
+                        out["order_check"] = {"box": [bx0, by0, bw, bh],
+                                              "prev_cost_ms_by_order_decile": [round(float(v.mean()), 4) for v in
+                                                                               np.array_split(pc_ms, 10)],
+                                              "cur_cost_ms_by_order_decile": [round(float(v.mean()), 4) for v in
+                                                                              np.array_split(costs[scr].astype(np.float64) * 1e-5, 10)]}
+                    else:
+                        out["order_check"] = {"box_guess_failed": [bx0, by0, bw, bh]}
         print(json.dumps(out), flush=True)
         s.close()
 
