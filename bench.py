@@ -613,8 +613,11 @@ def roofline_line(args, cls, cstats, kernel_ms, launches, names, steps, timed=No
             out["kernel_clock_ghz"] = round(kc, 3)
             out["issue_util_at_kernel_clock"] = round(out["achieved"] * 1e9 /
                                                       (VALU_ISSUE_PER_CLK_PER_SIMD * SIMDS * kc * 1e9), 3)
+        # the counting launch (k_tiles<true, false>: a slower variant of the sliced
+        # kernel) — its waves' mean life over the launch and the spread of their
+        # starts and ends; a production launch's own unit log (DESIGN.md,
+        # tools/tiles_fill_probe.py) shows a shorter tail
         out["wave_fill_solo"] = round(float(getattr(cstats, "kernel_wave_fill", 0.0)), 3)
-        # spread of the counting launch's wave starts and ends over its span
         out["wave_entry_spread_solo"] = round(float(getattr(cstats, "kernel_entry_spread", 0.0)), 3)
         out["wave_exit_spread_solo"] = round(float(getattr(cstats, "kernel_exit_spread", 0.0)), 3)
         lu = (e_wh or {}).get("valu_lane_util") if (timed and timed["whole"]) else (e_sl or {}).get("valu_lane_util")
