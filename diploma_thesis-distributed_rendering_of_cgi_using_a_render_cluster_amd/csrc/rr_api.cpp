@@ -413,7 +413,10 @@ int choose_spp_chunk(const FrameSetup& fs) {
     // record 16 B, two path-queue slots 2 x 48 B, shadow slot 48 B), so the
     // default 256M paths take ~43 GB of the 288 GB HBM (a 1080p 128 spp frame
     // is one chunk); np stays below 2^31 for 32-bit queue indices.
-    constexpr long kChunkPaths = 256L << 20;
+#ifndef RR_CHUNK_MPATHS
+#define RR_CHUNK_MPATHS 256
+#endif
+    constexpr long kChunkPaths = (long)RR_CHUNK_MPATHS << 20;
     const long target = kChunkPaths;
     long c = target / std::max(1, fs.W * fs.H);
     if (c < 1) c = 1;
