@@ -409,12 +409,16 @@ FrameConsts make_consts(const FrameSetup& fs, int n_tris) {
 
 int choose_spp_chunk(const FrameSetup& fs) {
     if (fs.spp_per_chunk > 0) return std::min(fs.spp_per_chunk, fs.spp);
-    // Paths in flight per chunk: the SoA path state is 160 B/path (radiance
-    // record 16 B, two path-queue slots 2 x 48 B, shadow slot 48 B), so the
-    // default 256M paths take ~43 GB of the 288 GB HBM (a 1080p 128 spp frame
-    // is one chunk); np stays below 2^31 for 32-bit queue indices.
+    // Paths in flight per chunk: the SoA path state is 168 B/path (radiance
+    // record 16 B, two path-queue slots 2 x 48 B, shadow slot 48 B, hit 8 B),
+    // so the default 512M paths take ~86 GB of the 288 GB HBM (a 1080p frame
+    // up to 256 spp, a 4K frame's 64 spp, is one chunk; frames of the split
+    // path share one copy); np stays below 2^31 for 32-bit queue indices.
+    // Per full C5 frame (4K, 1024 spp) 256M / 512M / 1G paths per chunk:
+    // 4,113 / 4,016 / 4,088 ms (profiles/r5_ab_chunk.txt): half the launches
+    // and their tails.
 #ifndef RR_CHUNK_MPATHS
-#define RR_CHUNK_MPATHS 256
+#define RR_CHUNK_MPATHS 512
 #endif
     constexpr long kChunkPaths = (long)RR_CHUNK_MPATHS << 20;
     const long target = kChunkPaths;
