@@ -637,3 +637,25 @@ def test_empty_scene_is_the_world(ctx, rr, tmp_path):
         np.testing.assert_allclose(film[..., :3], np.broadcast_to(fs.world, (24, 40, 3)), rtol=1e-6)
     finally:
         s.close()
+
+
+def test_tile_schedule_record(ctx, rr, s04):
+    """rr_debug_tile_costs after a counting tile frame: every screen tile of the
+    scene's box that holds work has a unit time, the hand-out order of the
+    launch is a permutation of the box tiles, and the unit log holds a start
+    before the end of every sliced unit (4 per box tile at 128 spp)."""
+    p = rr.default_params(width=320, height=180, spp=128, flags=rr.native.RR_FLAG_COUNT_TRAVERSAL)
+    for _ in range(4):  # every frame slot has run a launch, so the last order is built from costs
+        _, _, st = ctx.render_to_memory(s04, 5, p, film=False, rgba=True)
+    assert st.tile_slices == 4
+    costs, order, log = ctx.tile_costs()
+    n = ((320 + 7) // 8) * ((180 + 7) // 8)
+    assert costs.shape[0] >= n
+    busy = np.nonzero(costs[:n])[0]
+    assert busy.size > 0
+    xs, ys = busy % ((320 + 7) // 8), busy // ((320 + 7) // 8)
+    nb = int((xs.max() - xs.min() + 1) * (ys.max() - ys.min() + 1))
+    assert sorted(order[:nb].tolist()) == list(range(nb))
+    logged = np.nonzero(log[:, 1])[0]
+    assert logged.size >= 4 * busy.size
+    assert (log[logged, 0] <= log[logged, 1]).all() and (log[logged, 0] > 0).all()
