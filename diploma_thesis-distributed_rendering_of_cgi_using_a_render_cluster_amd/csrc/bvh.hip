@@ -861,6 +861,7 @@ void DevScene::release() {
     hist.release(); scan_part.release(); children.release(); node_parent.release();
     leaf_parent.release(); flags.release(); nodes.release(); tris.release(); qnodes.release(); qtris.release(); q_src.release(); q_cnt.release(); q_tcnt.release(); q_ctl.release();
     range.release();
+    tnrm.release();
     for (int k = 0; k < 2; ++k) ploc_cl[k].release();
     ploc_nn.release(); ploc_keep.release(); ploc_mrg.release(); ploc_ctl.release();
     has4 = false;

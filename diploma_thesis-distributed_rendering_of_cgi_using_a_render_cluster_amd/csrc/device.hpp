@@ -141,6 +141,7 @@ struct DevPaths {
     DevBuf<float4> sh_o, sh_d, sh_c;           // segmented shadow queue
     DevBuf<float2> hits;                       // split path: (t, leaf index) per queue entry
     DevBuf<uint32_t> qctr;                     // split path: grouped queue append counters
+    DevBuf<uint32_t> perm;                     // split path, RR_RAY_SORT: queue position -> slot (k_sort_queue)
     DevBuf<int32_t> counters;  // per chunk, per bounce b: {paths entering b+1, shadow rays of b}
     DevBuf<int32_t> spill;     // traversal stack spill
     DevBuf<float4> film;
@@ -161,6 +162,7 @@ struct DevPaths {
     bool force_wavefront = false;  // RR_FLAG_WAVEFRONT: LDS-resident scenes take the split path, not k_tiles
     bool tile_whole = false;       // k_tiles: one work unit per tile (the frame overlaps a pending one)
     int last_tile_slices = 0;      // render_frame_device: k_tiles units per box tile of the last frame (0: not k_tiles)
+    bool last_unit_logged = false; // render_frame_device: the last k_tiles launch wrote its unit log (trav_counts)
     int grid_blocks = 0;  // persistent grid for path kernels
     void ensure_paths(size_t n);
     void ensure_tiles();  // k_tiles: only the traversal stack spill area

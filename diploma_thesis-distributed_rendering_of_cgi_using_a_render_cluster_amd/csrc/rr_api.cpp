@@ -112,6 +112,7 @@ struct FrameSlot {
     std::string out_path, format;
     int quality = 0;
     bool jpeg = false, want_rgba = false, count = false;
+    bool unit_logged = false;  // its k_tiles launch wrote the unit log into trav_counts (rr_debug_tile_costs)
     float* film_out = nullptr;
     FrameRun r{};
     rr_frame_timing tm{};
@@ -428,6 +429,29 @@ int choose_spp_chunk(const FrameSetup& fs) {
     return (int)c;
 }
 
+// The chunk a frame renders with: choose_spp_chunk, lowered when the path
+// state of that many paths (168 B each, DevPaths::ensure_paths) would not fit
+// in 85 % of the device memory free now plus what this context's path buffers
+// already hold — a smaller GPU, or several ranks sharing one, gets more chunks
+// instead of RR_ENOMEM. Chunking changes no bit of the image
+// (test_chunking_and_determinism); an explicit spp_per_chunk is kept as asked.
+int fit_spp_chunk(const FrameSetup& fs, const DevPaths& p) {
+    const int c = choose_spp_chunk(fs);
+    if (fs.spp_per_chunk > 0) return c;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return c;
+    }
+    constexpr size_t kPathStateBytes = 168;
+    const double usable = 0.85 * ((double)free_b + (double)p.cap * kPathStateBytes);
+    const double npix = std::max(1.0, (double)fs.W * fs.H);
+    // ensure_paths' slack: a persistent grid's threads + 1/64 of the paths
+    const double slack = (double)std::max(p.grid_blocks, 256 * 8) * kBlock;  // 8: kMaxBlocksPerCu
+    const long fit = (long)((usable / kPathStateBytes - slack) / (1.0 + 1.0 / 64.0) / npix);
+    return (int)std::max<long>(1, std::min<long>(c, fit));
+}
+
 // Device JPEG encode of an RGBA8 frame (transform into c->jpeg_coeffs +
 // Huffman coding) into the slot's pinned stream buffer, on the context stream.
 void enqueue_jpeg_device(rr_ctx* c, FrameSlot& sl, const uint8_t* d_rgba, int W, int H, const float* d_tab) {
@@ -562,12 +586,13 @@ void enqueue_frame(rr_ctx* c, FrameSlot& sl) {
     r.rebuilt = prepare_frame(c, s, fs, sl.host_upload);
     RR_HIP(hipEventRecord(sl.ev[1], st));
     FrameConsts k = make_consts(fs, s->dev.n_tris);
-    r.spp_chunk = choose_spp_chunk(fs);
+    r.spp_chunk = fit_spp_chunk(fs, c->paths);
     r.chunks = (fs.spp + r.spp_chunk - 1) / r.spp_chunk;
     k.spp_chunk = r.spp_chunk;
     k.div_spp = FastDiv::make((uint32_t)k.spp_chunk);
     render_frame_device(s->dev, c->paths, k, r.chunks, st);
     r.tile_slices = c->paths.last_tile_slices;
+    sl.unit_logged = c->paths.last_unit_logged;
     if (fs.view_transform == VIEW_FILMIC) {  // film -> Filmic -> rgba8 (overwrites the kernels' tonemap)
         c->paths.prof.begin(st, RR_K_ACCUM);
         view_filmic_device(c->filmic, k, c->paths.film.ptr, reinterpret_cast<uchar4*>(c->paths.rgba8.ptr), st);
@@ -1262,9 +1287,9 @@ int rr_debug_qbvh(rr_ctx* c, rr_scene* s, int32_t frame, int32_t* nq, int32_t* c
 int rr_debug_trace(rr_ctx* c, rr_scene* s, int32_t frame, int32_t bvh_width, int32_t n, const float* rays,
                    float* hits, int32_t* prims, uint8_t* occluded) {
     if (!c || !s || n < 0 || (n > 0 && !rays)) return fail(RR_EINVAL, "bad arguments");
-    if (bvh_width < 0 || bvh_width == 1 || bvh_width > 6)
+    if (bvh_width < 0 || bvh_width == 1 || bvh_width > 7)
         return fail(RR_EINVAL, "hierarchy must be 0 (frame's), 2 (LBVH), 3 (PLOC), 4 (6-wide), 5 (6-wide, packets) "
-                               "or 6 (6-wide, one LDS stack entry)");
+                               "6 (6-wide, one LDS stack entry) or 7 (6-wide, beam packets)");
     return guarded([&] {
         if (!idle(c)) return fail(RR_EBUSY, "submitted frames are pending");
         FrameSetup fs = setup_frame(s->desc, frame, nullptr);
@@ -1324,7 +1349,8 @@ int rr_debug_tile_costs(rr_ctx* c, int32_t capacity, uint32_t* costs, int32_t* o
         const size_t nu = std::min<size_t>((size_t)unit_capacity, kUnitLog);
         if (nu > 0) {
             std::memset(unit_log, 0, 2 * nu * sizeof(uint64_t));
-            if (sl->trav_counts.cap >= (size_t)(kTravWords + 2 * kUnitLog))
+            // only the launch that wrote it (a counting frame): an older frame's log stays unreported
+            if (sl->unit_logged && sl->trav_counts.cap >= (size_t)(kTravWords + 2 * kUnitLog))
                 RR_HIP(hipMemcpy(unit_log, sl->trav_counts.ptr + kTravWords, 2 * nu * sizeof(uint64_t),
                                  hipMemcpyDeviceToHost));
         }

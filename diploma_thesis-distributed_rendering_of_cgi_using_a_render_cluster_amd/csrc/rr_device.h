@@ -686,7 +686,6 @@ RR_D lds_int* lds_slot(int* shared_elem) {
 // Traversal counters for RR_FLAG_COUNT_TRAVERSAL builds (kCount = true only).
 struct TravCount {
     uint32_t nodes = 0, tris = 0;
-    uint32_t rays = 0;  // k_tiles' out-of-line secondary traversals (counted in every frame)
 };
 
 // Resumable traversal of one ray: start() then step() until it returns true.

@@ -1047,6 +1047,129 @@ struct QueueMap {
     }
 };
 
+// Coherence order of a grouped queue before it is traced (round 6,
+// RR_RAY_SORT). The consumers take a queue in time order
+// (QueueMap::slot_t), chunk by chunk: a chunk holds about one producer batch,
+// the continuing samples of one pixel (pixel-major path order), so its rays
+// share an origin region but leave it in every direction, and the 64 lanes of
+// a trace wave walk 64 unrelated parts of the hierarchy. k_sort_queue
+// reorders each window of kSortWin consecutive positions — offset row w of all
+// 64 groups, the batches the producer waves appended at about the same time, so
+// the rays in flight on the chip at any moment are the same set as before —
+// by a direction bin (octahedral map of d on a 2^(b/2) x 2^(b/2) grid, bins in
+// Morton order), stable within a bin, gaps (kNoSlot) last, and writes the
+// order as perm[position] = queue slot. The trace kernels then map position m
+// to perm[m] instead of slot_t(m); they still write each hit at its queue slot
+// and the shading kernels still read in slot_t order, so which wave traces a
+// ray changes and nothing a path computes (bit-exact, as with lane refill and
+// dynamic dealing). The per-wave multisplit (one ballot per key bit) makes
+// the order deterministic.
+// Measured and NOT used (profiles/r6_ab_ray_sort.txt; C5 at 16 spp, 02 / 03 at
+// 64 spp, best solo slice of two interleaved rounds; the sorted build passes
+// the split-path parity subset, bit-exact): extension rays sorted, 64 bins,
+// extension traversal + sort 28.21 -> 32.08 / 34.06 -> 36.83 / 37.83 -> 40.73
+// ms (+14 / +8 / +8 %); 16 / 256 bins +10 / +17 % on C5; shadow rays sorted
+// 21.54 -> 22.30 / 26.41 -> 27.06 / 28.27 -> 29.02 ms; both, whole slices
+// 68.8 -> 72.9 / 78.3 -> 81.8 / 85.1 -> 88.8 ms. A producer batch is the
+// continuing samples of ONE pixel: their rays leave one point of one surface,
+// and most bounce rays end nearby, so the walk's lower levels (where the
+// per-ray node and triangle fetches are) are shared by the rays of a batch,
+// whatever their directions. Grouping by direction trades that origin
+// coherence for a far-field coherence the short diffuse rays rarely use (the
+// same finding as round 4's global origin-cell x octant buckets, +10 to +13 %).
+#ifndef RR_RAY_SORT
+#define RR_RAY_SORT 0  // bit 0: extension rays (k_trace_extend), bit 1: shadow rays (k_shadow_refill); A/B only
+#endif
+#ifndef RR_SORT_BITS
+#define RR_SORT_BITS 6  // direction bins = 2^bits (even)
+#endif
+static_assert(RR_SORT_BITS % 2 == 0 && RR_SORT_BITS >= 2 && RR_SORT_BITS <= 10, "RR_SORT_BITS: even, 2..10");
+constexpr int kSortBins = 1 << RR_SORT_BITS;
+constexpr int kSortWin = 4096;  // positions per window = 64 chunks = one offset row of the 64 groups
+constexpr int kSortBlock = 1024;
+constexpr int kSortItems = kSortWin / kSortBlock;
+constexpr int kSortWaves = kSortBlock / 64;
+constexpr int kSortHist = (kSortBins + 1) * kSortWaves;  // [key][wave], key kSortBins = gap
+static_assert(kSortWin == 64 * kQGroups, "a window is one offset row of every group");
+RR_D uint32_t dir_bin(float3 d) {
+    constexpr int G = 1 << (RR_SORT_BITS / 2);
+    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float u = d.x / s, v = d.y / s;
+    if (d.z < 0.0f) {  // lower hemisphere folded onto the square's corners
+        const float fu = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
+        v = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
+        u = fu;
+    }
+    // fmaxf first: a NaN lands in cell 0
+    const uint32_t iu = (uint32_t)fminf(fmaxf((u * 0.5f + 0.5f) * G, 0.0f), (float)(G - 1));
+    const uint32_t iv = (uint32_t)fminf(fmaxf((v * 0.5f + 0.5f) * G, 0.0f), (float)(G - 1));
+    uint32_t key = 0;
+#pragma unroll
+    for (int b = 0; b < RR_SORT_BITS / 2; ++b) key |= (((iu >> b) & 1u) << (2 * b)) | (((iv >> b) & 1u) << (2 * b + 1));
+    return key;
+}
+__global__ __launch_bounds__(kSortBlock) void k_sort_queue(QueueIn qi, const float4* __restrict__ dir,
+                                                           uint32_t* __restrict__ perm) {
+    __shared__ uint32_t hist[kSortHist];
+    __shared__ uint32_t wtot[kSortWaves];
+    QueueMap qm;
+    qm.init(QueueIn{qi.ctr, qi.cap, nullptr});
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int nwin = qm.span / kSortWin;
+    for (int w = blockIdx.x; w < nwin; w += gridDim.x) {
+        for (int i = threadIdx.x; i < kSortHist; i += kSortBlock) hist[i] = 0u;
+        __syncthreads();
+        uint32_t slot[kSortItems], key[kSortItems], rank[kSortItems];
+#pragma unroll
+        for (int j = 0; j < kSortItems; ++j) {  // wave wv: window positions 256 wv .. 256 wv + 255
+            const int m = w * kSortWin + (wv * kSortItems + j) * 64 + lane;
+            slot[j] = qm.slot_t(m);
+            key[j] = slot[j] == kNoSlot ? (uint32_t)kSortBins : dir_bin(xyz(dir[slot[j]]));
+            uint64_t peers = ~0ull;  // lanes holding the same key
+#pragma unroll
+            for (int b = 0; b <= RR_SORT_BITS; ++b) {
+                const bool bit = (key[j] >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                peers &= bit ? bb : ~bb;
+            }
+            const uint32_t base = hist[key[j] * kSortWaves + wv];  // this wave's earlier items of the key
+            rank[j] = base + (uint32_t)__popcll(peers & below);
+            if ((peers & below) == 0ull) hist[key[j] * kSortWaves + wv] = base + (uint32_t)__popcll(peers);
+        }
+        __syncthreads();
+        // exclusive scan of hist in [key][wave] order: the window's stable order
+        constexpr int kPer = (kSortHist + kSortBlock - 1) / kSortBlock;
+        uint32_t hv[kPer], sum = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int idx = threadIdx.x * kPer + k;
+            hv[k] = idx < kSortHist ? hist[idx] : 0u;
+            sum += hv[k];
+        }
+        uint32_t inc = sum;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)inc, off);
+            if (lane >= off) inc += t;
+        }
+        if (lane == 63) wtot[wv] = inc;
+        __syncthreads();
+        uint32_t run = inc - sum;
+        for (int q = 0; q < wv; ++q) run += wtot[q];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int idx = threadIdx.x * kPer + k;
+            if (idx < kSortHist) hist[idx] = run;
+            run += hv[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kSortItems; ++j)
+            perm[(size_t)w * kSortWin + hist[key[j] * kSortWaves + wv] + rank[j]] = slot[j];
+        __syncthreads();
+    }
+}
+
 // Queue records are written once and read by the next kernels. RR_NT_QUEUE
 // (A/B switch) bit 0: path-queue stores non-temporal; bit 1: non-temporal
 // loads where a kernel is a record's last reader; bit 2: shadow-queue origin
@@ -1486,6 +1609,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_primary(FrameConsts fc, SceneA
 // Extension rays entering bounce b: closest hit -> hits[slot].
 template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(SceneArgs sa, PathQueue in, QueueIn qi,
+                                                                         const uint32_t* __restrict__ perm,
                                                                          float2* __restrict__ hits,
                                                                          int32_t* __restrict__ spill,
                                                                          unsigned long long* __restrict__ tc,
@@ -1498,7 +1622,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qi.ctr, 1), [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qi.ctr, 1),
+        [&](int m) { return perm ? perm[m] : qm.slot_t(m); },  // perm: k_sort_queue's order (wave-uniform branch)
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             o = xyz(in.o[i]);
             d = xyz(in.d[i]);
@@ -1545,7 +1670,7 @@ __global__ __launch_bounds__(kBlock) void k_shade_extend(FrameConsts fc, int bou
 // Shadow rays with lane refill: unoccluded -> radiance += contribution.
 template <bool kCount>
 __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(SceneArgs sa, ShadowQueue sq, QueueIn qi,
-                                                                          Rad rad,
+                                                                          const uint32_t* __restrict__ perm, Rad rad,
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc,
                                                                           uint32_t* __restrict__ tail) {
@@ -1557,7 +1682,8 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
-        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qi.ctr, 1), [&](int m) { return qm.slot_t(m); },
+        nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qi.ctr, 1),
+        [&](int m) { return perm ? perm[m] : qm.slot_t(m); },
         [&](uint32_t i, float3& o, float3& d, float& tmin, float& tmax) {
             const float4 a = sq.o[i], b = sq.d[i];
             o = xyz(a);
@@ -2335,7 +2461,7 @@ __global__ void k_debug_bsdf(const float* __restrict__ mat12, const float* __res
 // to fill on any real hierarchy, so the stack's HBM part is exercised (the
 // per-lane spill area, one kPacketSpill part per wave). Closest hit only:
 // occluded is set to 255.
-template <int kStack>
+template <int kStack, bool kBeam = false>
 __global__ __launch_bounds__(kBlock) void k_debug_packet(const QNode6* __restrict__ nodes,
                                                          const TriPack* __restrict__ tris, int n_tris, int n,
                                                          const float4* __restrict__ rays, float4* __restrict__ hits,
@@ -2353,8 +2479,12 @@ __global__ __launch_bounds__(kBlock) void k_debug_packet(const QNode6* __restric
         }
         Hit h;
         set_miss(h, d.w);
-        packet_trace<false, kStack>(nodes, tris, stk, spill + (size_t)wave_id() * kPacketSpill, nullptr,
-                                    i < n && n_tris > 0, xyz(o), xyz(d), o.w, h, cnt);
+        if constexpr (kBeam)  // the camera kernel's walk (RR_CAM_BEAM): rays of a packet must share their origin
+            packet_trace_beam<false, kStack>(nodes, tris, stk, spill + (size_t)wave_id() * kPacketSpill, nullptr,
+                                             i < n && n_tris > 0, xyz(o), xyz(d), o.w, h, cnt);
+        else
+            packet_trace<false, kStack>(nodes, tris, stk, spill + (size_t)wave_id() * kPacketSpill, nullptr,
+                                        i < n && n_tris > 0, xyz(o), xyz(d), o.w, h, cnt);
         if (i >= n) continue;
         hits[i] = make_float4(h.t, h.u, h.v, 0.0f);
         prims[i] = h.orig;
@@ -2451,18 +2581,9 @@ int grid_for(K kernel, size_t dyn_lds, int block = kBlock) {
     if (it != cache.end()) return it->second;
     return cache[key] = resident_grid(kernel, dyn_lds, block);
 }
-// Scene bytes staged in LDS (stage_scene), and the cap below which the path
-// kernels take the LDS-resident variant: at most ~12 KB next to the 16 KB
-// traversal stack and the <= 8 KB segment prefix keeps 4 blocks of the
-// register-limited kernels per CU.
-constexpr size_t kLdsSceneMax = 16 * 1024;
-size_t scene_budget_bytes(const FrameConsts& fc) {  // the residency test's measure (scene_in_lds)
-    const int n_nodes = std::max(fc.n_tris - 1, 1);
-    return 16 * (4 * (size_t)n_nodes + 3 * (size_t)fc.n_tris + (3 + kMatLutStride / 4) * (size_t)fc.n_mats +
-                 3 * (size_t)fc.n_lights + kFilterN / 4);
-}
-// What stage_scene stages (without the camera data): + the normals (1 float4
-// per triangle) and the derived material records when shading.
+// What stage_scene stages (without the camera data): the hierarchy and the
+// triangle records, + the normals / shading frames (1 + kOnbF4 float4 per
+// triangle) and the derived material records when shading.
 size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
     const int n_nodes = std::max(fc.n_tris - 1, 1);
     size_t f4 = 4 * (size_t)n_nodes + kTriF4 * (size_t)fc.n_tris;
@@ -2473,13 +2594,34 @@ size_t scene_lds_bytes(const FrameConsts& fc, bool shading) {
 }
 }  // namespace
 
-
+// k_tiles' LDS per block: its static arrays (the traversal stack of kLdsStack
+// entries per lane, kWctr counter words per wave: 12,416 B, as hipcc reports
+// for every k_tiles instantiation) + the dynamic part TileGrid allocates — the
+// staged scene (stage_scene) and the camera-relative vertices (stage_camera,
+// kCamF4 float4 per triangle). ONE function for both the residency decision
+// and the launch (VERDICT r5 Weak 7: the decision used to count only the
+// hierarchy, triangles, materials, lights and filter table, about half of
+// what the launch then allocated).
+constexpr size_t kTilesStaticLds = sizeof(int) * (size_t)(kLdsStack * kBlock + kWctr * kWavesPerBlock);
+size_t tiles_dyn_lds_bytes(const FrameConsts& fc) {
+    return scene_lds_bytes(fc, true) + 16 * (size_t)kCamF4 * (size_t)fc.n_tris;
+}
+// A scene is LDS-resident (k_tiles) when one block's LDS leaves at least
+// kTilesMinBlocks blocks per CU (160 KB; 3 x 4 waves = 3 waves per SIMD).
+// Measured on dense soups in the 04vs stand-in (tools/lds_residency_study.py,
+// profiles/r5_lds_residency.txt): k_tiles ahead of the split path down to 3
+// blocks per CU (70 triangles: 19.2 against 20.0 ms), level at 2 (90: 20.3
+// against 20.4 ms); below 3 the split path takes the scene. And at most 128
+// triangles (camera_hit's per-tile triangle mask).
+constexpr int kTilesMinBlocks = 3;
+constexpr size_t kCuLds = 160 * 1024;
 bool scene_in_lds(int n_tris, int n_mats, int n_lights) {
     FrameConsts fc{};
     fc.n_tris = n_tris;
     fc.n_mats = n_mats;
     fc.n_lights = n_lights;
-    return n_tris > 0 && n_tris <= 128 && scene_budget_bytes(fc) <= kLdsSceneMax;  // 128: camera_hit's mask
+    return n_tris > 0 && n_tris <= 128 &&
+           kTilesMinBlocks * (kTilesStaticLds + tiles_dyn_lds_bytes(fc)) <= kCuLds;
 }
 
 bool frame_uses_tiles(const FrameConsts& base, bool force_wavefront) {
@@ -2496,17 +2638,17 @@ struct TileGrid {
     size_t dyn;
     int grid;
     TileGrid(const FrameConsts& fc, bool count, bool whole) {
-        dyn = scene_lds_bytes(fc, true) + 16 * kCamF4 * (size_t)fc.n_tris;
+        dyn = tiles_dyn_lds_bytes(fc);  // what scene_in_lds counted
         kx = tiles_kernel(count, whole);
         grid = grid_for(kx, dyn);
     }
 };
 // Launch geometry of the split (trace / shade) path of large scenes.
 struct SplitGrids {
-    int trace_p, trace_e, shadow, shade_p, shade_e, packet;
+    int trace_p, trace_e, shadow, shade_p, shade_e, packet, sort;
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
-    void (*kte)(SceneArgs, PathQueue, QueueIn, float2*, int32_t*, unsigned long long*, uint32_t*);
-    void (*kts)(SceneArgs, ShadowQueue, QueueIn, Rad, int32_t*, unsigned long long*, uint32_t*);
+    void (*kte)(SceneArgs, PathQueue, QueueIn, const uint32_t*, float2*, int32_t*, unsigned long long*, uint32_t*);
+    void (*kts)(SceneArgs, ShadowQueue, QueueIn, const uint32_t*, Rad, int32_t*, unsigned long long*, uint32_t*);
     void (*ktpk)(FrameConsts, SceneArgs, int, float2*, uint32_t*, int32_t*, unsigned long long*, uint32_t*);  // packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
@@ -2519,6 +2661,7 @@ struct SplitGrids {
         packet = grid_for(ktpk, 0);
         shade_p = grid_for(k_shade_primary, 0);
         shade_e = grid_for(k_shade_extend, 0);
+        sort = grid_for(k_sort_queue, 0, kSortBlock);
     }
 };
 // Slots per append group for a producer of `grid` blocks over at most `work`
@@ -2564,6 +2707,7 @@ void DevPaths::release() {
     for (DevBuf<float4>* b : {&rad, &ps_o[0], &ps_d[0], &ps_t[0], &ps_o[1], &ps_d[1], &ps_t[1], &sh_o, &sh_d,
                               &sh_c, &film})
         b->release();
+    perm.release();
     counters.release(); tile_ctrs.release(); tile_cost.release(); tile_order.release(); spill.release(); tile_slab.release(); film_part.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     mat_lut.release();
@@ -2616,6 +2760,7 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
         const uint32_t cap_p = group_cap(np, gsp), cap_e = group_cap(np, gse);
         if ((size_t)std::max(cap_p, cap_e) * kQGroups > p.cap)
             throw std::runtime_error("queue capacity exceeded (split path)");
+        if (RR_RAY_SORT) p.perm.ensure((size_t)kQGroups * (((size_t)std::max(cap_p, cap_e) + 63) / 64 * 64));
         pr.begin(st, RR_K_PRIMARY);
         if (packets)
             G.ktpk<<<clamp_grid(np, G.packet), kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, deal_host(qpath(0), 2),
@@ -2629,18 +2774,35 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
                                                 sq, QueueOut{qpath(0), qshadow(0), cap_p}, tnrm);
         pr.end(st);
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
+        // k_sort_queue's grid: a queue of groups of cap_prev slots spans at most
+        // ceil(cap_prev / 64) windows
+        auto sort_queue = [&](const uint32_t* ctr, const float4* dir) {
+            const long wins = ((long)cap_prev + 63) / 64;
+            k_sort_queue<<<(int)std::max<long>(1, std::min<long>(wins, G.sort)), kSortBlock, 0, st>>>(
+                QueueIn{ctr, cap_prev, nullptr}, dir, p.perm.ptr);
+        };
         for (int b = 0; b <= base.max_bounces; ++b) {
             pr.begin(st, RR_K_SHADOW);
+            const uint32_t* perm_s = nullptr;
+            if (RR_RAY_SORT & 2) {
+                sort_queue(qshadow(b), sq.d);
+                perm_s = p.perm.ptr;
+            }
             G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(
-                sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, Rad{reinterpret_cast<float*>(p.rad.ptr)},
+                sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, perm_s, Rad{reinterpret_cast<float*>(p.rad.ptr)},
                 p.spill.ptr, tc, tail);
             pr.end(st);
             if (b == base.max_bounces) break;
             const int nb = b + 1;  // bounce being traced and shaded
             const QueueIn qin{qpath(b), cap_prev, tot + 2 * b};
             pr.begin(st, RR_K_EXTEND);
-            G.kte<<<clamp_grid(np, G.trace_e, kTraceBlock), kTraceBlock, 0, st>>>(sa, pq[nb & 1], qin, p.hits.ptr,
-                                                                                p.spill.ptr, tc, tail);
+            const uint32_t* perm_e = nullptr;
+            if (RR_RAY_SORT & 1) {
+                sort_queue(qpath(b), pq[nb & 1].d);
+                perm_e = p.perm.ptr;
+            }
+            G.kte<<<clamp_grid(np, G.trace_e, kTraceBlock), kTraceBlock, 0, st>>>(sa, pq[nb & 1], qin, perm_e,
+                                                                                p.hits.ptr, p.spill.ptr, tc, tail);
             pr.end(st);
             pr.begin(st, RR_K_SHADE);
             k_shade_extend<<<gse, kBlock, 0, st>>>(fc, nb, sa, pq[nb & 1], QueueIn{qpath(b), cap_prev, nullptr},
@@ -2662,6 +2824,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     const int npix = base.npix;
     const size_t npaths = (size_t)npix * base.spp_chunk;
     p.last_tile_slices = 0;
+    p.last_unit_logged = false;
     if (frame_uses_tiles(base, p.force_wavefront)) {  // one launch: all samples of every tile
         const TileGrid G(base, p.count_traversal, p.tile_whole);
         p.ensure_tiles();
@@ -2676,6 +2839,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
             p.trav_counts.ensure(kTravWords + 2 * kUnitLog);
             RR_HIP(hipMemsetAsync(p.trav_counts.ptr, 0, (kTravWords + 2 * kUnitLog) * sizeof(unsigned long long), st));
             tc = p.trav_counts.ptr;
+            p.last_unit_logged = true;
         }
         const SceneArgs sa{s.nodes.ptr, s.qnodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
                            p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.nq};
@@ -2792,11 +2956,16 @@ void trace_batch_device(DevScene& s, DevPaths& p, int n, const float4* d_rays, f
                         uint8_t* d_occ, hipStream_t st, int width) {
     p.ensure_paths(1);
     const int g = (int)std::min<long>((n + kBlock - 1) / kBlock, p.grid_blocks);
-    if (width == 5) {  // packet walk with a 4-entry stack: the fallback runs
+    if (width == 5 || width == 7) {  // packet walk (7: beam) with a 4-entry stack: the HBM part runs
         if (!s.has4) throw std::runtime_error("BVH4 not built");
-        if (n > 0)
-            k_debug_packet<4><<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits, d_prims,
-                                                    d_occ, p.spill.ptr);
+        if (n > 0) {
+            if (width == 7)
+                k_debug_packet<4, true><<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits,
+                                                              d_prims, d_occ, p.spill.ptr);
+            else
+                k_debug_packet<4><<<g, kBlock, 0, st>>>(s.qnodes.ptr, s.tris.ptr, s.n_tris, n, d_rays, d_hits,
+                                                        d_prims, d_occ, p.spill.ptr);
+        }
     } else if (width == 4 || width == 6) {  // 6: the same walk with one LDS stack entry per lane
         if (!s.has4) throw std::runtime_error("BVH4 not built");
         if (n > 0) {

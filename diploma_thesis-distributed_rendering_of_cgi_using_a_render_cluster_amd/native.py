@@ -241,11 +241,14 @@ class Scene:
         world = np.zeros(3, np.float32)
         ri = np.zeros(RR_RENDER_INTS, np.int32)
         rf = np.zeros(RR_RENDER_FLOATS, np.float32)
+        tm = np.zeros(max(c["triangles"], 1), np.int32)
         _check(lib().rr_debug_frame_state(None, self.handle, int(frame), ctypes.byref(params) if params else None,
-                                          None, None, _ptr(cam, ctypes.c_float), _ptr(lights, ctypes.c_float),
+                                          None, _ptr(tm, ctypes.c_int32), _ptr(cam, ctypes.c_float),
+                                          _ptr(lights, ctypes.c_float),
                                           _ptr(mats, ctypes.c_float), _ptr(world, ctypes.c_float),
                                           _ptr(ri, ctypes.c_int32), _ptr(rf, ctypes.c_float)))
-        return FrameState(np.zeros((0, 3, 3), np.float32), np.zeros(0, np.int32), cam, lights[:nl], mats[:nm],
+        # tris stay empty (world triangles need the device); tri_mat is the scene's, per triangle
+        return FrameState(np.zeros((0, 3, 3), np.float32), tm[:c["triangles"]], cam, lights[:nl], mats[:nm],
                           world, ri, rf)
 
     def object_matrix(self, obj: int, frame: float) -> np.ndarray:

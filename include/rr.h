@@ -337,7 +337,10 @@ int rr_debug_qbvh(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t* nq
  * kernel's 64-ray packets, with 4 packet-stack entries in LDS so that the
  * stack's HBM part is used; closest hit only, occluded = 255), 6 (the
  * 6-wide per-lane walk with one LDS stack entry per lane, so that its grouped
- * entries live in the HBM part) or 0 (whichever
+ * entries live in the HBM part), 7 (the camera kernel's default packet walk,
+ * one box test per child for the whole packet — packet_trace_beam — with the
+ * same 4-entry LDS stack as 5; exact only for packets whose rays share one
+ * origin, as camera rays do; closest hit only) or 0 (whichever
  * the frame kernels use for this scene, render_ints[7] of rr_debug_frame_state). rays: n*8 floats
  * (o.xyz, tmin, d.xyz, tmax). hits: n*4 floats (t, u, v, 0), prims: n original
  * triangle ids (-1 miss), occluded: n bytes (any-hit result). */
@@ -353,14 +356,6 @@ int rr_debug_trace(rr_ctx* ctx, rr_scene* scene, int32_t frame_index, int32_t bv
 int rr_debug_bsdf_sample(rr_ctx* ctx, const float* mat12, const float* n3, const float* wo3, int32_t n,
                          const float* u, float* wi3, float* f3, float* pdf, int32_t* ok);
 
-/* The per-sample path's square roots and reciprocals (rr_device.h sqrt_rn /
- * sqrt_any / rcp_rn) against the device's correctly rounded sqrtf and
- * 1.0f / x, over the float bit patterns lo .. lo + n - 1: counts5[0] =
- * sqrt_rn mismatches with the argument in its range (+-0 or [2^-96, FLT_MAX];
- * must be 0), [1] = sqrt_rn mismatches outside it (not called there), [2] =
- * sqrt_any mismatches (must be 0), [3] = rcp_rn mismatches with |x| in
- * [2^-126, 2^126) (must be 0), [4] = rcp_rn mismatches outside it. Test
- * infrastructure for the bit-exactness claim; no reference counterpart. */
 /* The tile kernel's scheduling record of the last frame enqueued (LDS-resident
  * scenes): per screen tile (8x8 pixels, row-major), the real-time ticks
  * (100 MHz) its work units took in that frame's k_tiles launch (0 for tiles
@@ -375,6 +370,14 @@ int rr_debug_bsdf_sample(rr_ctx* ctx, const float* mat12, const float* n3, const
 int rr_debug_tile_costs(rr_ctx* ctx, int32_t capacity, uint32_t* costs, int32_t* order, int32_t* n_tiles,
                         uint64_t* unit_log, int32_t unit_capacity);
 
+/* The per-sample path's square roots and reciprocals (rr_device.h sqrt_rn /
+ * sqrt_any / rcp_rn) against the device's correctly rounded sqrtf and
+ * 1.0f / x, over the float bit patterns lo .. lo + n - 1: counts5[0] =
+ * sqrt_rn mismatches with the argument in its range (+-0 or [2^-96, FLT_MAX];
+ * must be 0), [1] = sqrt_rn mismatches outside it (not called there), [2] =
+ * sqrt_any mismatches (must be 0), [3] = rcp_rn mismatches with |x| in
+ * [2^-126, 2^126) (must be 0), [4] = rcp_rn mismatches outside it. Test
+ * infrastructure for the bit-exactness claim; no reference counterpart. */
 int rr_debug_fastmath_check(rr_ctx* ctx, uint32_t lo, uint64_t n, uint64_t* counts5);
 
 /* Host animation evaluation: object_to_world matrix (row-major 4x4, f64) of

