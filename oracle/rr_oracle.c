@@ -783,6 +783,17 @@ static void try_leaf(const lbvh* B, int leaf, const shear_t* s, v3 o, float tmin
 
 typedef struct { float t; int slot, ref; } ckey;
 
+#ifdef ORC_WALK_STUDY
+/* research build only: [0] node visits whose entry distance (as tested at the
+ * parent) exceeds the closest hit at visit time, [1] grouped-entry pops whose
+ * every child lies beyond it */
+static long long g_cnt_study[2];
+void orc_walk_study(long long* out2, int reset) {
+    out2[0] = g_cnt_study[0]; out2[1] = g_cnt_study[1];
+    if (reset) g_cnt_study[0] = g_cnt_study[1] = 0;
+}
+#endif
+
 /* node visits / triangle tests of trace4 since the last reset (research:
  * tools/collapse_study.py, tools/margin_study.py). Counted only while a study
  * tool has switched counting on (orc_set_walk_counting): the shared totals are
@@ -831,7 +842,18 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
     int stack[ORC_MAXDEPTH];
     int sp = 0, node = 0;
     long long cn = 0, ct = 0, ctop[4] = {0, 0, 0, 0};
+#ifdef ORC_WALK_STUDY
+    /* research build only (tools/walk_study.py): the entry distance of every
+     * stacked child, to count the visits a pop-time test against the current
+     * closest hit would skip */
+    float stk_t[ORC_MAXDEPTH][ORC_QW_MAX];
+    float node_t = -INFINITY;
+    long long cull = 0, cull_grp = 0;
+#endif
     for (;;) {
+#ifdef ORC_WALK_STUDY
+        if (node_t > h->t) ++cull;
+#endif
         ++cn;
         for (int k = 0; k < 4; ++k) ctop[k] += node < (128 << k);
         const uint32_t* nd = B->q4 + 16 * (size_t)node;
@@ -907,6 +929,15 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
             int r = 0;
             while (!((e >> r) & 1)) ++r;
             node = (int)((unsigned)e >> 6) + r;
+#ifdef ORC_WALK_STUDY
+            node_t = stk_t[sp - 1][r];
+            {
+                float mn = INFINITY;
+                for (int q = 0; q < ORC_QW_MAX; ++q)
+                    if ((e >> q) & 1) mn = fminf(mn, stk_t[sp - 1][q]);
+                if (mn > h->t) ++cull_grp;  /* the whole entry beyond the hit: one pop for all its children */
+            }
+#endif
             const int rest = e & (e - 1);
             if ((rest & 63) == 0) --sp; else stack[sp - 1] = rest;
             continue;
@@ -923,13 +954,31 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
                 ++rank;
             }
             if (rm) {
+#ifdef ORC_WALK_STUDY
+                if (sp < ORC_MAXDEPTH)
+                    for (int c = 0, rank = 0; c < ORC_QW_MAX; ++c) {
+                        if (!((inner >> c) & 1u)) continue;
+                        stk_t[sp][rank++] = k[c].t;
+                    }
+#endif
                 if (sp < ORC_MAXDEPTH) stack[sp++] = (int)((nd[4] << 6) | rm);
                 else drop_push();
             }
         }
         node = k[best].ref;
+#ifdef ORC_WALK_STUDY
+        node_t = k[best].t;
+#endif
     }
 done:
+#ifdef ORC_WALK_STUDY
+    if (g_count_walks) {
+#pragma omp atomic
+        g_cnt_study[0] += cull;
+#pragma omp atomic
+        g_cnt_study[1] += cull_grp;
+    }
+#endif
     if (g_count_walks) {
         for (int k = 0; k < 4; ++k) {
 #pragma omp atomic
