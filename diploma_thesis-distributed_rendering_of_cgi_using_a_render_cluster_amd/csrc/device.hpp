@@ -139,6 +139,7 @@ struct DevPaths {
     DevBuf<float4> rad;                        // per path (p-indexed) radiance record
     DevBuf<float4> ps_o[2], ps_d[2], ps_t[2];  // segmented path queue, ping-pong per bounce
     DevBuf<float4> sh_o, sh_d, sh_c;           // segmented shadow queue
+    DevBuf<unsigned long long> shmask;         // split path, RR_SHADOW_BEAM: per 64 camera paths, which have a bounce-0 shadow ray
     DevBuf<float2> hits;                       // split path: (t, leaf index) per queue entry
     DevBuf<uint32_t> qctr;                     // split path: grouped queue append counters
     DevBuf<uint32_t> perm;                     // split path, RR_RAY_SORT: queue position -> slot (k_sort_queue)

@@ -1655,6 +1655,143 @@ int orc_trace_w(int n, const float* tris9, int width, int n_rays, const float* r
     return 0;
 }
 
+#ifdef ORC_WALK_STUDY
+/* Research build only (tools/beam_study.py): the device's any-hit beam packet
+ * walk (wavefront.hip packet_shadow_beam) over packets of rays starts[k] ..
+ * starts[k + 1] - 1 (at most 64; 8 floats each: o, tmin, d, tmax), against
+ * the per-lane any-hit walk.
+ * out: [0] packets, [1] beam node visits (per packet), [2] beam leaf tests
+ * (summed over lanes), [3] per-lane node visits, [4] per-lane leaf tests,
+ * [5] rays whose occlusion differs, [6] blocked rays. */
+static float st_min(const float* v, int n, int mx) {
+    float r = mx ? -INFINITY : INFINITY;
+    for (int i = 0; i < n; ++i) r = mx ? fmaxf(r, v[i]) : fminf(r, v[i]);
+    return r;
+}
+int orc_study_beam(int n, const float* tris9, int n_packets, const int* starts, const float* rays, long long* out) {
+    lbvh B;
+    lbvh_build(&B, n, tris9, NULL, 3);
+    lbvh_collapse4(&B);
+    B.width = 4;
+    for (int k = 0; k < 7; ++k) out[k] = 0;
+    for (int pk = 0; pk < n_packets; ++pk) {
+        const int p0 = starts[pk];
+        const int m = starts[pk + 1] - p0 < 64 ? starts[pk + 1] - p0 : 64;
+        if (m <= 0) continue;
+        float ox[64], oy[64], oz[64], ix[64], iy[64], iz[64], dx[64], dy[64], dz[64], tm[64];
+        shear_t sh[64];
+        hitrec h[64];
+        int live[64], occ_ref[64];
+        for (int i = 0; i < m; ++i) {
+            const float* R = rays + 8 * (size_t)(p0 + i);
+            v3 o = V(R[0], R[1], R[2]), d = V(R[4], R[5], R[6]);
+            v3 iq = rcp3(d);
+            ox[i] = o.x; oy[i] = o.y; oz[i] = o.z; dx[i] = d.x; dy[i] = d.y; dz[i] = d.z;
+            ix[i] = iq.x; iy[i] = iq.y; iz[i] = iq.z; tm[i] = R[7];
+            sh[i] = make_shear(d);
+            h[i].t = R[7]; h[i].u = h[i].v = 0.0f; h[i].idx = -1; h[i].orig = -1;
+            live[i] = 1;
+            long long save[6];
+            orc_walk_counts(save, 1);
+            hitrec hr;
+            occ_ref[i] = trace4(&B, o, d, 0.0f, R[7], 1, &hr);
+            long long c6[6];
+            orc_walk_counts(c6, 1);
+            out[3] += c6[0]; out[4] += c6[1];
+        }
+        const float ol[3] = {st_min(ox, m, 0), st_min(oy, m, 0), st_min(oz, m, 0)};
+        const float oh[3] = {st_min(ox, m, 1), st_min(oy, m, 1), st_min(oz, m, 1)};
+        const float il[3] = {st_min(ix, m, 0), st_min(iy, m, 0), st_min(iz, m, 0)};
+        const float ih[3] = {st_min(ix, m, 1), st_min(iy, m, 1), st_min(iz, m, 1)};
+        const float dl[3] = {st_min(dx, m, 0), st_min(dy, m, 0), st_min(dz, m, 0)};
+        const float dh[3] = {st_min(dx, m, 1), st_min(dy, m, 1), st_min(dz, m, 1)};
+        const float t_hi = st_min(tm, m, 1);
+        int stack[4096], sp = 0, node = 0, n_live = m;
+        ++out[0];
+        for (;;) {
+            ++out[1];
+            const uint32_t* nd = B.q4 + 16 * (size_t)node;
+            const uint32_t inner = nd[3] >> 24;
+            float org[3];
+            memcpy(org, nd, sizeof org);
+            float mo = 0.0f;
+            for (int a = 0; a < 3; ++a) mo = fmaxf(mo, fmaxf(fabsf(org[a] - oh[a]), fabsf(org[a] - ol[a])));
+            const float m2 = 2.0f * fmaf(mo, ORC_BOX_MARGIN, ldexpf(255.0f * ORC_BOX_MARGIN, (int)((nd[15] >> 8) & 255u) - 128));
+            float tn[ORC_QW_MAX];
+            int pass[ORC_QW_MAX];
+            for (int c = 0; c < ORC_QW_MAX; ++c) {
+                float nr3[3], fr3[3];
+                for (int a = 0; a < 3; ++a) {
+                    const int e = (int)((nd[3] >> (8 * a)) & 255u) - 128;
+                    uint32_t ql, qh;
+                    if (c < 4) { ql = (nd[6 + a] >> (8 * c)) & 255u; qh = (nd[9 + a] >> (8 * c)) & 255u; }
+                    else {
+                        const uint32_t lo2 = (nd[12 + a / 2] >> (16 * (a & 1))) & 0xffffu;
+                        const uint32_t hi2 = (nd[12 + (3 + a) / 2] >> (16 * ((3 + a) & 1))) & 0xffffu;
+                        ql = (lo2 >> (8 * (c - 4))) & 255u; qh = (hi2 >> (8 * (c - 4))) & 255u;
+                    }
+                    const float lo = (org[a] - oh[a]) + ldexpf((float)ql, e) - m2;
+                    const float hi = (org[a] - ol[a]) + ldexpf((float)qh, e) + m2;
+                    float nr, fr;
+                    if (il[a] > 0.0f) { nr = lo * (lo >= 0.0f ? il[a] : ih[a]); fr = hi * (hi >= 0.0f ? ih[a] : il[a]); }
+                    else if (ih[a] < 0.0f) { nr = hi * (hi >= 0.0f ? il[a] : ih[a]); fr = lo * (lo >= 0.0f ? ih[a] : il[a]); }
+                    else {
+                        fr = INFINITY; nr = 0.0f;
+                        if (lo > 0.0f) nr = dh[a] > 0.0f ? lo / dh[a] : INFINITY;
+                        if (hi < 0.0f) nr = dl[a] < 0.0f ? hi / dl[a] : INFINITY;
+                    }
+                    nr3[a] = nr; fr3[a] = fr;
+                }
+                tn[c] = fmaxf(fmaxf(nr3[0], nr3[1]), fmaxf(nr3[2], 0.0f));
+                const float tf = fminf(fminf(fr3[0], fr3[1]), fminf(fr3[2], t_hi));
+                pass[c] = tn[c] <= tf && ((nd[15] >> c) & 1u);
+            }
+            int n_lf = 0, n_in = 0, best = -1;
+            for (int c = 0; c < ORC_QW_MAX; ++c) {
+                const int is_inner = (inner >> c) & 1u;
+                if (!is_inner) {
+                    if (pass[c]) {
+                        const int ti = (int)nd[5] + n_lf;
+                        for (int i = 0; i < m; ++i) {
+                            if (!live[i]) continue;
+                            ++out[2];
+                            try_leaf(&B, ti, &sh[i], V(ox[i], oy[i], oz[i]), 0.0f, &h[i]);
+                            if (h[i].idx >= 0) { live[i] = 0; --n_live; }
+                        }
+                    }
+                    ++n_lf;
+                } else {
+                    if (pass[c] && (best < 0 || tn[c] < tn[best])) best = c;
+                    ++n_in;
+                }
+            }
+            if (n_live == 0) break;
+            if (best < 0) {
+                if (sp == 0) break;
+                node = stack[--sp];
+                continue;
+            }
+            for (int c = ORC_QW_MAX - 1, rank; c >= 0; --c) {
+                if (!((inner >> c) & 1u) || c == best || !pass[c]) continue;
+                rank = 0;
+                for (int q = 0; q < c; ++q) rank += (inner >> q) & 1u;
+                if (sp < 4096) stack[sp++] = (int)nd[4] + rank;
+            }
+            int rb = 0;
+            for (int q = 0; q < best; ++q) rb += (inner >> q) & 1u;
+            node = (int)nd[4] + rb;
+        }
+        for (int i = 0; i < m; ++i) {
+            const int occ = h[i].idx >= 0;
+            out[5] += occ != occ_ref[i];
+            out[6] += occ;
+        }
+    }
+    lbvh_free(&B);
+    return 0;
+}
+#endif
+
 int orc_trace(int n, const float* tris9, int n_rays, const float* rays, float* hits, int32_t* prims,
               uint8_t* occluded) {
     return orc_trace_w(n, tris9, 2, n_rays, rays, hits, prims, occluded);
