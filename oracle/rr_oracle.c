@@ -788,6 +788,8 @@ typedef struct { float t; int slot, ref; } ckey;
  * parent) exceeds the closest hit at visit time, [1] grouped-entry pops whose
  * every child lies beyond it */
 static long long g_cnt_study[2];
+static int g_study_order; /* 1: grouped entries pop nearest first; 2: and skip children beyond the hit */
+void orc_study_order(int mode) { g_study_order = mode; }
 void orc_walk_study(long long* out2, int reset) {
     out2[0] = g_cnt_study[0]; out2[1] = g_cnt_study[1];
     if (reset) g_cnt_study[0] = g_cnt_study[1] = 0;
@@ -922,15 +924,28 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
         for (int c = 0; c < ORC_QW_MAX; ++c)
             if (k[c].t != INFINITY && (best < 0 || (!any && k[c].t < k[best].t))) best = c;
         if (best < 0) {
+#ifdef ORC_WALK_STUDY
+        pop_again:
+#endif
             if (sp == 0) break;
             /* grouped entries (rr_device.h TravStackT::pop_group): the lowest
              * rank left; the entry stays while ranks remain */
             const int e = stack[sp - 1];
             int r = 0;
             while (!((e >> r) & 1)) ++r;
+#ifdef ORC_WALK_STUDY
+            if (g_study_order)  /* research: the entry's nearest child first */
+                for (int q = r + 1; q < ORC_QW_MAX; ++q)
+                    if (((e >> q) & 1) && stk_t[sp - 1][q] < stk_t[sp - 1][r]) r = q;
+#endif
             node = (int)((unsigned)e >> 6) + r;
 #ifdef ORC_WALK_STUDY
             node_t = stk_t[sp - 1][r];
+            if (g_study_order > 1 && node_t > h->t) {  /* research: skip what lies beyond the hit */
+                const int rest2 = e & ~(1 << r);
+                if ((rest2 & 63) == 0) --sp; else stack[sp - 1] = rest2;
+                goto pop_again;
+            }
             {
                 float mn = INFINITY;
                 for (int q = 0; q < ORC_QW_MAX; ++q)
@@ -938,7 +953,11 @@ static int trace4(const lbvh* B, v3 o, v3 d, float tmin, float tmax, int any, hi
                 if (mn > h->t) ++cull_grp;  /* the whole entry beyond the hit: one pop for all its children */
             }
 #endif
+#ifdef ORC_WALK_STUDY
+            const int rest = e & ~(1 << r);
+#else
             const int rest = e & (e - 1);
+#endif
             if ((rest & 63) == 0) --sp; else stack[sp - 1] = rest;
             continue;
         }

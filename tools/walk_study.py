@@ -49,6 +49,7 @@ def main():
         return r
 
     CS.walk = walk
+    L.orc_study_order(int(os.environ.get("WALK_ORDER", "0")))
     CS.main()
 
 
