@@ -18,7 +18,7 @@ for p in "" _01 _02 _03 _c5; do
         grep '^{' $d/trace_serial_bench.json > profiles/${tag}${p}_serial_bench_under_rocprof.json
     fi
 done
-for wl in 04vs 01 02 03 c5 04vs_serial; do
+for wl in 04vs 01 02 03 c5 04vs_serial 04vs_driver_config; do
     f=gpurun_out/ev/bench_$wl.json
     if [ -f $f ] && grep -q '^{' $f; then grep '^{' $f > profiles/${tag}_bench_$wl.json; else echo "skip bench $wl"; fi
 done
