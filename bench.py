@@ -51,7 +51,7 @@ JOB = os.path.join(ROOT, "jobs", "04_very-simple_demo_10f-1w.toml")
 WORKLOADS = {
     # 40 steps (4 passes over the 10-frame job): at ~3 ms a frame the fill and
     # drain of the two-frame pipeline would otherwise weigh ~15 % of a 10-step run
-    "04vs": {"job": JOB, "metric": METRIC, "steps": 40, "warmup": 4,
+    "04vs": {"job": JOB, "metric": METRIC, "steps": 40, "warmup": 4, "device_warmup_s": 0.3,
              "data": "synthetic: 04_very-simple stand-in scene (01_simple-animation content; the 04 .blend is "
                      "missing from the reference), frames of the 04vs demo job, JPEG q90 written per frame",
              "workload": "04vs-standin, 1 frame per step: 1920x1080, 128 spp, max 12 bounces, "
@@ -59,6 +59,7 @@ WORKLOADS = {
                          "JPEG q90 encode/write"},
     "01": {"job": os.path.join(ROOT, "jobs", "01_simple-animation_600f-8w_dynamic.toml"),
            "metric": "job frames/sec at 1/2/4/8 MI355X (01_simple-animation)", "steps": 40, "warmup": 4,
+           "device_warmup_s": 0.3,
            "data": "01_simple-animation.rrscene exported from the reference's .blend (Filmic rendered as "
                    "Standard: no OCIO LUTs in the image), frames of the 600-frame job, JPEG q90 written per frame",
            "workload": "01-simple-animation, 1 frame per step: 1920x1080, 128 spp, max 12 bounces, "
@@ -98,6 +99,9 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=None, help="default: 2 (1 for c5)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="04vs")
     ap.add_argument("--spp", type=int, default=0, help="override the scene's samples (0 = scene)")
+    ap.add_argument("--device-warmup-s", type=float, default=None,
+                    help="frames of the job rendered for this long before the warmup steps (GPU clock ramp; "
+                         "default 0.3 s for the k_tiles workloads 04vs / 01, 0 otherwise)")
     ap.add_argument("--no-profile", action="store_true", help="time without per-kernel HIP events")
     ap.add_argument("--serial", action="store_true",
                     help="one rr_render_frame per step (no overlap of frame N's encode with N+1's render)")
@@ -798,6 +802,24 @@ def main():
     flags = 0 if args.no_profile else rr.native.RR_FLAG_PROFILE_KERNELS
     runner = rr.BackendRunner(ROOT, device=device, params=rr.default_params(flags=flags, spp=args.spp))
 
+    # Device warm-up before the W warmup steps: frames of the same job, pipelined
+    # as the timed loop renders them, for a fixed wall time. A k_tiles frame is
+    # ~1 ms, so W = 5 warmup steps keep the GPU busy for ~6 ms, and the timed
+    # region then starts before the engine clock has ramped: on one box, 20
+    # timed frames after 5 warmup frames ran at 1,057-1,072 frames/s, the same
+    # 20 frames after 100 more at 1,125 (tools/pipeline_timeline.py,
+    # profiles/r6_pipeline_timeline.txt); every later repetition in the same
+    # process ran at 1,123-1,132. The timed region is unchanged: exactly K steps
+    # of full per-frame work between barrier + synchronize.
+    warm_s = wl.get("device_warmup_s", 0.0) if args.device_warmup_s is None else args.device_warmup_s
+    device_warmup = {"frames": 0, "seconds": 0.0}
+    if warm_s > 0:
+        tw = time.perf_counter()
+        while time.perf_counter() - tw < warm_s:
+            runner.render_frames(job, [frame_of(device_warmup["frames"] + i) for i in range(8)])
+            device_warmup["frames"] += 8
+        device_warmup["seconds"] = round(time.perf_counter() - tw, 3)
+
     if args.serial:
         for w in range(args.warmup):
             runner.render_frame(job, frame_of(w))
@@ -931,6 +953,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": wl["data"],
+            "device_warmup": {**device_warmup, "note": "frames of the job rendered before the W warmup steps so "
+                              "the timed region starts at the engine clock it keeps (GPU clock ramp); not timed"},
             "config": {"workload": wl["workload"], "job": os.path.basename(wl["job"]),
                        "resolution": f"{int(last_stats.width)}x{int(last_stats.height)}", "spp": int(last_stats.spp),
                        "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)",
