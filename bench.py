@@ -815,8 +815,11 @@ def main():
     device_warmup = {"frames": 0, "seconds": 0.0}
     if warm_s > 0:
         tw = time.perf_counter()
+        # the timed steps' own frames, so that per-launch averages over the whole
+        # process (the PMC passes of tools/profile_round.sh) stay those frames'
         while time.perf_counter() - tw < warm_s:
-            runner.render_frames(job, [frame_of(device_warmup["frames"] + i) for i in range(8)])
+            runner.render_frames(job, [frame_of(args.warmup + (device_warmup["frames"] + i) % args.steps)
+                                       for i in range(8)])
             device_warmup["frames"] += 8
         device_warmup["seconds"] = round(time.perf_counter() - tw, 3)
 
@@ -953,8 +956,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": wl["data"],
-            "device_warmup": {**device_warmup, "note": "frames of the job rendered before the W warmup steps so "
-                              "the timed region starts at the engine clock it keeps (GPU clock ramp); not timed"},
+            "device_warmup": {**device_warmup, "note": "the timed steps' frames rendered before the W warmup steps "
+                              "so the timed region starts at the engine clock it keeps (GPU clock ramp); not timed"},
             "config": {"workload": wl["workload"], "job": os.path.basename(wl["job"]),
                        "resolution": f"{int(last_stats.width)}x{int(last_stats.height)}", "spp": int(last_stats.spp),
                        "parallelism": f"frame-parallel x{world} (one worker per GPU, no collective)",
