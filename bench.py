@@ -817,9 +817,14 @@ def main():
         tw = time.perf_counter()
         # the timed steps' own frames, so that per-launch averages over the whole
         # process (the PMC passes of tools/profile_round.sh) stay those frames'
+        # (--serial: one frame at a time, as its timed loop renders them)
         while time.perf_counter() - tw < warm_s:
-            runner.render_frames(job, [frame_of(args.warmup + (device_warmup["frames"] + i) % args.steps)
-                                       for i in range(8)])
+            batch = [frame_of(args.warmup + (device_warmup["frames"] + i) % args.steps) for i in range(8)]
+            if args.serial:
+                for f in batch:
+                    runner.render_frame(job, f)
+            else:
+                runner.render_frames(job, batch)
             device_warmup["frames"] += 8
         device_warmup["seconds"] = round(time.perf_counter() - tw, 3)
 
