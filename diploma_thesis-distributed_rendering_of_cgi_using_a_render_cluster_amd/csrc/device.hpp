@@ -71,6 +71,7 @@ struct DevScene {
     DevBuf<BvhNode> nodes;  // max(n-1, 1)
     DevBuf<TriPack> tris;   // n, leaf order (after a BVH4 collapse: the BVH4's leaf order)
     DevBuf<QNode6> qnodes;     // quantised 6-wide collapse of `nodes` (split path), <= n-1
+    DevBuf<QNode6H> qwide;     // the same nodes with fp16 bounds (RR_WIDE_NODES: what the split path's walks read)
     DevBuf<float4> tnrm;       // split path, per triangle in leaf order: unit geometric normal, material id (shading)
     DevBuf<TriPack> qtris;     // collapse scratch: the triangles in the collapse's leaf order (swapped into `tris`)
     DevBuf<int32_t> q_src;     // wide node -> its BVH2 root (collapse scratch)

@@ -483,6 +483,7 @@ struct SceneArgs {
     const float* mat_lut;    // kMatLutStride floats per material
     int n_nodes, n_tris, n_mats, n_lights;
     int n_qnodes;            // its node count
+    const QNode6H* qwide;    // the same nodes with fp16 bounds (RR_WIDE_NODES; null otherwise)
 };
 
 namespace {
@@ -924,13 +925,31 @@ RR_D uint32_t* deal_ctrs(const uint32_t* q, int word) {
 constexpr int kTopNodes = RR_TOP_NODES;
 static_assert((kLdsStack * kTraceBlock * 4 + 64 * kTopNodes) * (2048 / kTraceBlock) <= 160 * 1024,
               "trace kernels: stack + top copy of 8 waves per SIMD must fit the CU's LDS");
-RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
+// With RR_WIDE_NODES the copy holds the fp16-bound nodes, 128 B each: half
+// as many in the same LDS (kTopF4 float4 per node).
+#if RR_WIDE_NODES
+using TopNodes = Q6NodesW;
+constexpr int kTopF4 = 8;
+#else
+using TopNodes = Q6Nodes;
+constexpr int kTopF4 = 4;
+#endif
+constexpr int kTopCount = kTopNodes * 4 / kTopF4;  // nodes in the LDS copy
+RR_D TopNodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
     lds_f4w* top = (lds_f4w*)top_shared;
-    const int n = kTopNodes > 0 ? min(sa.n_qnodes, kTopNodes) : 0;
+    const int n = kTopCount > 0 ? min(sa.n_qnodes, kTopCount) : 0;
+#if RR_WIDE_NODES
+    const rr_f4v* src = reinterpret_cast<const rr_f4v*>(sa.qwide);
+#else
     const rr_f4v* src = reinterpret_cast<const rr_f4v*>(sa.qnodes);
-    for (int i = threadIdx.x; i < 4 * n; i += kTraceBlock) top[i] = src[i];
+#endif
+    for (int i = threadIdx.x; i < kTopF4 * n; i += kTraceBlock) top[i] = src[i];
     __syncthreads();
+#if RR_WIDE_NODES
+    return Q6NodesW{sa.qwide, top, n};
+#else
     return Q6Nodes{sa.qnodes, top, n};
+#endif
 }
 // TS: TravStateQ6 (its box margins are per node; the BVH2 walk TravState needs
 // the scene radius in start() and so does not compile here). Blocks of
@@ -1279,7 +1298,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
                                                                           uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const Q6Nodes nodes = stage_top(sa, top_nodes);
+    const TopNodes nodes = stage_top(sa, top_nodes);
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
@@ -1844,7 +1863,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
                                                                          uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const Q6Nodes nodes = stage_top(sa, top_nodes);
+    const TopNodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
@@ -1904,7 +1923,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
                                                                           uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const Q6Nodes nodes = stage_top(sa, top_nodes);
+    const TopNodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
@@ -3199,7 +3218,8 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     const SceneArgs sa{s.nodes.ptr, s.qnodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
-                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.nq};
+                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.nq,
+                       RR_WIDE_NODES ? s.qwide.ptr : nullptr};
     render_split(p, base, n_chunks, st, sa, tc, pq, sq, s.has4 ? s.tnrm.ptr : nullptr);
     RR_HIP(hipGetLastError());
 }
