@@ -862,7 +862,6 @@ void DevScene::release() {
     leaf_parent.release(); flags.release(); nodes.release(); tris.release(); qnodes.release(); qtris.release(); q_src.release(); q_cnt.release(); q_tcnt.release(); q_ctl.release();
     range.release();
     tnrm.release();
-    qwide.release();
     for (int k = 0; k < 2; ++k) ploc_cl[k].release();
     ploc_nn.release(); ploc_keep.release(); ploc_mrg.release(); ploc_ctl.release();
     has4 = false;
@@ -926,14 +925,6 @@ __global__ __launch_bounds__(kBlock) void k_tri_nrm(const TriPack* __restrict__ 
     out[i] = make_float4(N.x, N.y, N.z, tp.p1.w);
 }
 
-// The fp16-bound copy of the 6-wide nodes the split path's walks read
-// (RR_WIDE_NODES, rr_device.h QNode6H): the same bounds, two bytes each.
-__global__ __launch_bounds__(kBlock) void k_q6_widen(const QNode6* __restrict__ q, int n, QNode6H* __restrict__ out) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    out[i] = q6_widen(q[i]);
-}
-
 // Quantised 6-wide hierarchy of the built BVH2 (kernels above): one count / scan / emit /
 // advance round per level; the host learns the frontier size every 4 levels
 // (one synchronisation) and sizes the next launches by it (a level has at
@@ -975,10 +966,6 @@ void build_qbvh(DevScene& s, hipStream_t st) {
         }
     }
     std::swap(s.tris, s.qtris);  // the traversal and shading read the 6-wide hierarchy's leaf order
-    if (RR_WIDE_NODES) {
-        s.qwide.ensure((size_t)std::max(s.nq, 1));
-        if (s.nq > 0) k_q6_widen<<<cdiv(s.nq, kBlock), kBlock, 0, st>>>(s.qnodes.ptr, s.nq, s.qwide.ptr);
-    }
     s.tnrm.ensure((size_t)std::max(n, 1));
     if (n > 0) k_tri_nrm<<<cdiv(n, kBlock), kBlock, 0, st>>>(s.tris.ptr, n, s.tnrm.ptr);
     s.has4 = true;

@@ -71,7 +71,6 @@ struct DevScene {
     DevBuf<BvhNode> nodes;  // max(n-1, 1)
     DevBuf<TriPack> tris;   // n, leaf order (after a BVH4 collapse: the BVH4's leaf order)
     DevBuf<QNode6> qnodes;     // quantised 6-wide collapse of `nodes` (split path), <= n-1
-    DevBuf<QNode6H> qwide;     // the same nodes with fp16 bounds (RR_WIDE_NODES: what the split path's walks read)
     DevBuf<float4> tnrm;       // split path, per triangle in leaf order: unit geometric normal, material id (shading)
     DevBuf<TriPack> qtris;     // collapse scratch: the triangles in the collapse's leaf order (swapped into `tris`)
     DevBuf<int32_t> q_src;     // wide node -> its BVH2 root (collapse scratch)
@@ -140,7 +139,6 @@ struct DevPaths {
     DevBuf<float4> rad;                        // per path (p-indexed) radiance record
     DevBuf<float4> ps_o[2], ps_d[2], ps_t[2];  // segmented path queue, ping-pong per bounce
     DevBuf<float4> sh_o, sh_d, sh_c;           // segmented shadow queue
-    DevBuf<unsigned long long> shmask;         // split path, RR_SHADOW_BEAM: per 64 camera paths, which have a bounce-0 shadow ray
     DevBuf<float2> hits;                       // split path: (t, leaf index) per queue entry
     DevBuf<uint32_t> qctr;                     // split path: grouped queue append counters
     DevBuf<uint32_t> perm;                     // split path, RR_RAY_SORT: queue position -> slot (k_sort_queue)

@@ -58,15 +58,6 @@ static_assert(sizeof(BvhNode) == 64, "node must be one 64-byte line");
 // its box test always fails. oracle/rr_oracle.c q4_pack / trace4 restate the
 // layout and the walk.
 constexpr int kQWidth = 6;
-// RR_WIDE_NODES (A/B only, off): the split path's walks read the fp16-bound
-// copy of the nodes (QNode6H below) instead of the byte form. Measured slower
-// (profiles/r6_ab_wide_nodes.txt; 02 extension traversal 33.9 -> 54.2 ms at 8
-// waves per SIMD with spills, 38.5 at 6 without): v_fma_mix_f32 issues at half
-// rate on gfx950 (tools/mix_rate_probe.hip), so it costs what the byte
-// conversion it replaces did, and the nodes move twice the bytes.
-#ifndef RR_WIDE_NODES
-#define RR_WIDE_NODES 0
-#endif
 struct alignas(16) QNode6 {
     float4 org;
     uint4 a, b, c;
@@ -78,41 +69,8 @@ RR_HD int q6_ref(const QNode6& n, int c) {
     const uint32_t inner = q6_inner(n), below = inner & ((1u << c) - 1u);
     return ((inner >> c) & 1u) ? (int)n.a.x + __builtin_popcount(below) : ~((int)n.a.y + (c - __builtin_popcount(below)));
 }
-// Grid coordinate (0..255) of child c's lo (hi) bound on axis a in the layout above.
-RR_HD uint32_t q6_bound(const QNode6& n, int a, bool hi, int c) {
-    if (c < 4) {
-        const uint32_t w = hi ? (a == 0 ? n.b.y : (a == 1 ? n.b.z : n.b.w)) : (a == 0 ? n.a.z : (a == 1 ? n.a.w : n.b.x));
-        return (w >> (8 * c)) & 255u;
-    }
-    const uint32_t pair = hi ? (a == 0 ? n.c.y >> 16 : (a == 1 ? n.c.z & 0xffffu : n.c.z >> 16))
-                             : (a == 0 ? n.c.x & 0xffffu : (a == 1 ? n.c.x >> 16 : n.c.y & 0xffffu));
-    return (pair >> (8 * (c - 4))) & 255u;
-}
-
-// The same node with its 36 child bounds as binary16 (RR_WIDE_NODES, round
-// 6). An integer 0..255 is exact in binary16, and the box test's fused
-// multiply-add takes the half straight from its word (v_fma_mix_f32 with
-// op_sel widens the fp16 operand exactly inside the instruction), so a node
-// visit drops the 36 byte-to-float conversions (v_cvt_f32_ubyteN) of the byte
-// form while every plane distance keeps the bits of fmaf((float)q, s, n): the
-// same boxes pass and the walk is the same. Two 64 B lines instead of one,
-// derived from the byte nodes after each build (bvh.hip k_q6_widen).
-//   org   QNode6::org
-//   hdr   x: first internal child, y: first leaf triangle, z: QNode6::c.w, w: 0
-//   w     18 words: lo x, lo y, lo z, hi x, hi y, hi z, three words per axis,
-//         word k of an axis holding children 2k (low half) and 2k + 1 (high half)
-struct alignas(16) QNode6H {
-    float4 org;
-    uint4 hdr;
-    uint4 w[5];  // words 0..17 (18, 19 unused)
-    uint4 pad;
-};
-static_assert(sizeof(QNode6H) == 128, "fp16-bound node is two 64-byte lines");
-RR_HD uint32_t q6_inner(const QNode6H& n) { return (uint32_t)__builtin_bit_cast(int, n.org.w) >> 24; }
 RR_HD int q6_first_inner(const QNode6& n) { return (int)n.a.x; }
-RR_HD int q6_first_inner(const QNode6H& n) { return (int)n.hdr.x; }
 RR_HD int q6_first_leaf(const QNode6& n) { return (int)n.a.y; }
-RR_HD int q6_first_leaf(const QNode6H& n) { return (int)n.hdr.y; }
 
 constexpr int kQExpMin = -64, kQExpMax = 100;
 
@@ -940,72 +898,6 @@ RR_D uint32_t q6_box_best(const QNode6& n, float3 o, float3 iq, float tmin, floa
     return hits & used;
 }
 
-// q6_box_best on the fp16-bound node: the same planes, the same fmaf per
-// plane (the half widened exactly: fmaf((float)q, s, n) bit for bit), the
-// same choices; per axis the near / far words are chosen once for three
-// children pairs.
-RR_D float q6h_half(uint32_t w, int hi) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? w >> 16 : w)); }
-template <bool kNearest = true>
-RR_D uint32_t q6_box_best(const QNode6H& n, float3 o, float3 iq, float tmin, float tcur, uint32_t imask, int& best) {
-    const Q6Planes pl = q6_planes_of(n.org, n.hdr.z, o, iq);
-    const uint32_t L[18] = {n.w[0].x, n.w[0].y, n.w[0].z, n.w[0].w, n.w[1].x, n.w[1].y, n.w[1].z, n.w[1].w, n.w[2].x,
-                            n.w[2].y, n.w[2].z, n.w[2].w, n.w[3].x, n.w[3].y, n.w[3].z, n.w[3].w, n.w[4].x, n.w[4].y};
-    const bool px = iq.x >= 0.0f, py = iq.y >= 0.0f, pz = iq.z >= 0.0f;
-    uint32_t nw[3][3], fw[3][3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        nw[0][k] = px ? L[k] : L[9 + k];
-        fw[0][k] = px ? L[9 + k] : L[k];
-        nw[1][k] = py ? L[3 + k] : L[12 + k];
-        fw[1][k] = py ? L[12 + k] : L[3 + k];
-        nw[2][k] = pz ? L[6 + k] : L[15 + k];
-        fw[2][k] = pz ? L[15 + k] : L[6 + k];
-    }
-    uint32_t hits = 0;
-    best = -1;
-    float bt = __builtin_inff();
-#pragma unroll
-    for (int c = 0; c < kQWidth; ++c) {
-        const int k = c >> 1, h = c & 1;
-        const float t0 = fmaxf(fmaxf(fmaf(q6h_half(nw[0][k], h), pl.sx, pl.nx), fmaf(q6h_half(nw[1][k], h), pl.sy, pl.ny)),
-                               fmaxf(fmaf(q6h_half(nw[2][k], h), pl.sz, pl.nz), tmin));
-        const float t1 = fminf(fminf(fmaf(q6h_half(fw[0][k], h), pl.sx, pl.fx), fmaf(q6h_half(fw[1][k], h), pl.sy, pl.fy)),
-                               fminf(fmaf(q6h_half(fw[2][k], h), pl.sz, pl.fz), tcur));
-        const bool hit = t0 <= t1;
-        hits |= (uint32_t)hit << c;
-        if (hit && ((imask >> c) & 1u) && (!kNearest ? best < 0 : t0 < bt)) {
-            best = c;
-            bt = t0;
-        }
-    }
-    return hits & n.hdr.z;
-}
-// The fp16-bound node of a byte node (k_q6_widen).
-RR_D QNode6H q6_widen(const QNode6& n) {
-    QNode6H r;
-    r.org = n.org;
-    r.hdr = make_uint4(n.a.x, n.a.y, n.c.w, 0u);
-    uint32_t L[20];
-#pragma unroll
-    for (int hi = 0; hi < 2; ++hi)
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const uint32_t q0 = q6_bound(n, a, hi != 0, 2 * k), q1 = q6_bound(n, a, hi != 0, 2 * k + 1);
-                L[9 * hi + 3 * a + k] = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)q0) |
-                                        ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)q1) << 16);
-            }
-    L[18] = L[19] = 0u;
-    r.w[0] = make_uint4(L[0], L[1], L[2], L[3]);
-    r.w[1] = make_uint4(L[4], L[5], L[6], L[7]);
-    r.w[2] = make_uint4(L[8], L[9], L[10], L[11]);
-    r.w[3] = make_uint4(L[12], L[13], L[14], L[15]);
-    r.w[4] = make_uint4(L[16], L[17], L[18], L[19]);
-    r.pad = make_uint4(0u, 0u, 0u, 0u);
-    return r;
-}
-
 // Node fetch of the 6-wide walk. The split-path trace kernels keep a copy of
 // the first n_top nodes in LDS (Q6Nodes): nodes are numbered breadth first,
 // so those are the top levels of the tree, which every ray visits — each of
@@ -1052,31 +944,6 @@ RR_D QNode6 q6_load(const Q6Nodes& n, int i) {
         return r;
     }
     return q6_load(n.g, i);
-}
-// The fp16-bound nodes (RR_WIDE_NODES): global array + the LDS copy of the
-// first n_top (8 float4 per node), one flat pointer as above; the pad word of
-// a node is not read.
-RR_D QNode6H q6_load(const QNode6H* __restrict__ nodes, int i) { return nodes[i]; }
-struct Q6NodesW {
-    const QNode6H* __restrict__ g;
-    lds_f4w* top;  // nodes [0, n_top): 8 float4 each (QNode6H layout)
-    int n_top;
-};
-RR_D QNode6H q6_load(const Q6NodesW& n, int i) {
-    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-    const u4v* top_g = (const u4v*)(const rr_f4v*)n.top;
-    const u4v* q = i < n.n_top ? top_g + 8 * i : reinterpret_cast<const u4v*>(n.g + i);
-    const u4v w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4], w5 = q[5], w6 = q[6];
-    QNode6H r;
-    r.org = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z), __uint_as_float(w0.w));
-    r.hdr = make_uint4(w1.x, w1.y, w1.z, w1.w);
-    r.w[0] = make_uint4(w2.x, w2.y, w2.z, w2.w);
-    r.w[1] = make_uint4(w3.x, w3.y, w3.z, w3.w);
-    r.w[2] = make_uint4(w4.x, w4.y, w4.z, w4.w);
-    r.w[3] = make_uint4(w5.x, w5.y, w5.z, w5.w);
-    r.w[4] = make_uint4(w6.x, w6.y, w6.z, w6.w);
-    r.pad = make_uint4(0u, 0u, 0u, 0u);
-    return r;
 }
 
 // Resumable traversal of the quantised 6-wide hierarchy (same contract as

@@ -483,7 +483,6 @@ struct SceneArgs {
     const float* mat_lut;    // kMatLutStride floats per material
     int n_nodes, n_tris, n_mats, n_lights;
     int n_qnodes;            // its node count
-    const QNode6H* qwide;    // the same nodes with fp16 bounds (RR_WIDE_NODES; null otherwise)
 };
 
 namespace {
@@ -925,31 +924,13 @@ RR_D uint32_t* deal_ctrs(const uint32_t* q, int word) {
 constexpr int kTopNodes = RR_TOP_NODES;
 static_assert((kLdsStack * kTraceBlock * 4 + 64 * kTopNodes) * (2048 / kTraceBlock) <= 160 * 1024,
               "trace kernels: stack + top copy of 8 waves per SIMD must fit the CU's LDS");
-// With RR_WIDE_NODES the copy holds the fp16-bound nodes, 128 B each: half
-// as many in the same LDS (kTopF4 float4 per node).
-#if RR_WIDE_NODES
-using TopNodes = Q6NodesW;
-constexpr int kTopF4 = 8;
-#else
-using TopNodes = Q6Nodes;
-constexpr int kTopF4 = 4;
-#endif
-constexpr int kTopCount = kTopNodes * 4 / kTopF4;  // nodes in the LDS copy
-RR_D TopNodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
+RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
     lds_f4w* top = (lds_f4w*)top_shared;
-    const int n = kTopCount > 0 ? min(sa.n_qnodes, kTopCount) : 0;
-#if RR_WIDE_NODES
-    const rr_f4v* src = reinterpret_cast<const rr_f4v*>(sa.qwide);
-#else
+    const int n = kTopNodes > 0 ? min(sa.n_qnodes, kTopNodes) : 0;
     const rr_f4v* src = reinterpret_cast<const rr_f4v*>(sa.qnodes);
-#endif
-    for (int i = threadIdx.x; i < kTopF4 * n; i += kTraceBlock) top[i] = src[i];
+    for (int i = threadIdx.x; i < 4 * n; i += kTraceBlock) top[i] = src[i];
     __syncthreads();
-#if RR_WIDE_NODES
-    return Q6NodesW{sa.qwide, top, n};
-#else
     return Q6Nodes{sa.qnodes, top, n};
-#endif
 }
 // TS: TravStateQ6 (its box margins are per node; the BVH2 walk TravState needs
 // the scene radius in start() and so does not compile here). Blocks of
@@ -1231,11 +1212,9 @@ struct QueueOut {
     uint32_t cap;          // slots per group (both queues)
 };
 
-// kShadow false: the continuations only (the shadow ray is the caller's).
-template <bool kShadow = true>
 __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQueue out, ShadowQueue sq,
                                              const QueueOut& qo) {
-    const uint64_t mc = __ballot(so.cont), ms = kShadow ? __ballot(so.shadow) : 0ull;
+    const uint64_t mc = __ballot(so.cont), ms = __ballot(so.shadow);
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint32_t g = wave_id() % kQGroups;
@@ -1252,7 +1231,7 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
         q_put<1>(out.d + s1, make_float4(so.d.x, so.d.y, so.d.z, i2f((int)so.lob)));
         q_put<1>(out.t + s1, make_float4(so.T.x, so.T.y, so.T.z, so.esc ? 1.0f : 0.0f));
     }
-    if (kShadow && so.shadow) {
+    if (so.shadow) {
         const uint32_t s2 = bs + (uint32_t)__popcll(ms & below);
         q_put<4>(sq.o + s2, make_float4(so.so.x, so.so.y, so.so.z, i2f(pid)));
         q_put<4>(sq.d + s2, make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist));
@@ -1260,20 +1239,13 @@ __device__ __forceinline__ void emit_grouped(const ShadeOut& so, int pid, PathQu
     }
 }
 
-// RR_SHADOW_BEAM (A/B only, off): bounce-0 shadow rays toward a sun as beam
-// packets (k_shadow_packet). Measured slower (profiles/r6_ab_shadow_beam.txt;
-// 02 / 03 / C5 frame slices at 64 spp, shadow traversal 26.2 / 28.2 / 79.7 ->
-// 26.9 / 28.8 / 84.1 ms, shading +0.4 to +1.5 ms); parity-green.
-#ifndef RR_SHADOW_BEAM
-#define RR_SHADOW_BEAM 0
-#endif
 // Minimum waves per SIMD of the split path's shading kernels (their launch
 // bounds; 1: the compiler's choice, 90 / 91 VGPRs = 5 waves). A/B switch: 6
 // waves (80 VGPRs, 3 / 6 spill slots) made shading 10.3 / 10.4 / 34.2 ->
 // 13.2 / 13.3 / 44.1 ms per 02 / 03 / C5 slice (profiles/r6_ab_shadow_beam.txt,
-// sw6); RR_SHADOW_BEAM builds take 5 (k_shade_primary would be at 100 VGPRs).
+// sw6).
 #ifndef RR_SHADE_WAVES
-#define RR_SHADE_WAVES (RR_SHADOW_BEAM ? 5 : 1)
+#define RR_SHADE_WAVES 1
 #endif
 constexpr int kShadeWaves = RR_SHADE_WAVES;
 
@@ -1298,7 +1270,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
                                                                           uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const TopNodes nodes = stage_top(sa, top_nodes);
+    const Q6Nodes nodes = stage_top(sa, top_nodes);
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
@@ -1562,190 +1534,6 @@ RR_D void packet_trace_beam(const QNode6* __restrict__ nodes, const TriPack* __r
     }
 }
 
-// Smallest (mx false) or largest x over the wave's lanes with `act`
-// (wave-uniform; +-inf when none).
-RR_D float wave_extreme(bool act, float x, bool mx) {
-    x = act ? x : (mx ? -__builtin_huge_valf() : __builtin_huge_valf());
-    for (int off = 32; off > 0; off >>= 1) {
-        const float y = __shfl_xor(x, off);
-        x = mx ? fmaxf(x, y) : fminf(x, y);
-    }
-    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
-}
-// Whether the origins of the `act` lanes lie within kBeamSpread pixel
-// footprints of each other (largest extent of their box against the footprint
-// at the farthest origin's camera distance; pix = 2 half_w / W, the footprint
-// per unit distance): a pixel on a silhouette has samples on surfaces far
-// apart, and a beam from all of them would sweep that whole width to the
-// light (tools/beam_study.py: 500 - 1,000 node visits per such packet on 02
-// against 10 for the others). Wave-uniform.
-#ifndef RR_BEAM_SPREAD
-#define RR_BEAM_SPREAD 4.0f
-#endif
-constexpr float kBeamSpread = RR_BEAM_SPREAD;
-[[maybe_unused]] RR_D bool beam_coherent(bool act, float3 o, float3 cam, float pix) {
-    const float3 oc = sub3(o, cam);
-    const float dc = wave_extreme(act, fmaxf(fmaxf(fabsf(oc.x), fabsf(oc.y)), fabsf(oc.z)), true);  // >= |o - cam| / sqrt(3)
-    const float spread = fmaxf(fmaxf(wave_extreme(act, o.x, true) - wave_extreme(act, o.x, false),
-                                     wave_extreme(act, o.y, true) - wave_extreme(act, o.y, false)),
-                               wave_extreme(act, o.z, true) - wave_extreme(act, o.z, false));
-    return spread <= kBeamSpread * 1.7320508f * dc * pix;  // (false for NaN)
-}
-
-// Bounce-0 shadow rays toward a sun as beam packets (RR_SHADOW_BEAM, round
-// 6). The lanes hold the sun's shadow rays of 64 consecutive path indices —
-// samples of one pixel (pixel-major order), whose camera rays hit one small
-// patch of surface — so they share one direction exactly and leave nearly one
-// point: nearly one ray, as camera packets are. (Rays toward a disk or point
-// light span the light's solid angle; as beams they tested about ten times the
-// triangles per ray of their own walks on 02, tools/beam_study.py, so they stay
-// queued, k_shadow_refill.) The beam test of packet_trace_beam, widened for
-// origins that differ: per axis the lanes' origins span [ol, oh], so a plane
-// at x lies at (x - oh) .. (x - ol) from them; the lo planes take x - oh, the
-// hi planes x - ol (the box grown by the origins' spread), then the same
-// near / far choice over the reciprocal interval; an axis whose direction
-// component changes sign in the packet has no far plane, and a slab wholly on
-// one side of every origin is reached no sooner than its distance over the
-// largest component toward it. The margin is the node's for the farthest
-// origin of the interval (q6_planes: kBoxMargin times the largest |org - o| +
-// the extent), at least each lane's own, doubled as for camera packets, so
-// every child a lane's own box test (q6_box_best with its o, rcp3 reciprocal,
-// tmin 0 and tmax) opens is opened. Leaf children that pass are tested by
-// every lane whose ray is not yet blocked, with its own watertight test and
-// accept rule (tmin < t < tmax); a lane is done at its first hit, the packet
-// when every lane is. The answer is whether some triangle blocks the segment —
-// an accepted triangle lies in boxes the lane's own walk opens (the margins),
-// and the beam tests every triangle the lane's walk would — so it is the
-// per-lane any-hit walk's, bit for bit, whatever the visiting order
-// (tools/beam_study.py restates this walk on the CPU and compares every ray's
-// occlusion with the oracle's walk). Returns the lane's "blocked" (false for
-// lanes without a ray).
-template <bool kCount, int kStack = kPacketStack>
-RR_D bool packet_shadow_beam(const QNode6* __restrict__ nodes, const TriPack* __restrict__ tris, lds_int* stk,
-                             int* __restrict__ gstk, uint32_t* __restrict__ drops, bool act, float3 o, float3 d,
-                             float tmax, TravCount& cnt) {
-    if (!__ballot(act)) return false;
-    const int lane = (int)(threadIdx.x & 63);
-    auto wred = [&](float x, bool mx) { return wave_extreme(act, x, mx); };
-    const float olx = wred(o.x, false), oly = wred(o.y, false), olz = wred(o.z, false);
-    const float ohx = wred(o.x, true), ohy = wred(o.y, true), ohz = wred(o.z, true);
-    const Shear sh = make_shear(d);
-    const float3 iq = rcp3(d);  // the per-lane walk's reciprocal (TravStateQ6D::start)
-    const float ilx = wred(iq.x, false), ily = wred(iq.y, false), ilz = wred(iq.z, false);
-    const float ihx = wred(iq.x, true), ihy = wred(iq.y, true), ihz = wred(iq.z, true);
-    // direction intervals, for axes whose direction component changes sign in the packet
-    const float dlx = wred(d.x, false), dly = wred(d.y, false), dlz = wred(d.z, false);
-    const float dhx = wred(d.x, true), dhy = wred(d.y, true), dhz = wred(d.z, true);
-    const float t_hi = wred(tmax, true);
-    Hit h;
-    set_miss(h, tmax);
-    bool live = act;  // a ray not yet blocked
-    int node = 0, sp = 0;
-    for (;;) {
-        const QNode6 nd = nodes[node];  // wave-uniform: scalar loads
-        const uint32_t imask = q6_inner(nd);
-        if (kCount && live) ++cnt.nodes;
-        bool pass = false;
-        float tnear = 0.0f;
-        if (lane < kQWidth) {
-            const uint32_t eb = (uint32_t)f2i(nd.org.w);
-            // node origin relative to the far (l) and near (h) end of each origin interval
-            const float dxl = nd.org.x - ohx, dxh = nd.org.x - olx;
-            const float dyl = nd.org.y - ohy, dyh = nd.org.y - oly;
-            const float dzl = nd.org.z - ohz, dzh = nd.org.z - olz;
-            const float mo = fmaxf(fmaxf(fmaxf(fabsf(dxl), fabsf(dxh)), fmaxf(fabsf(dyl), fabsf(dyh))),
-                                   fmaxf(fabsf(dzl), fabsf(dzh)));
-            const float m2 = 2.0f * fmaf(mo, kBoxMargin, ldexpf(255.0f * kBoxMargin, (int)((nd.c.w >> 8) & 255u) - 128));
-            const int c = lane;
-            const int s8 = c < 4 ? 8 * c : 0;
-            const int s16 = c == 5 ? 8 : 0;
-            const uint32_t qlx = c < 4 ? (nd.a.z >> s8) & 255u : ((nd.c.x & 0xffffu) >> s16) & 255u;
-            const uint32_t qly = c < 4 ? (nd.a.w >> s8) & 255u : ((nd.c.x >> 16) >> s16) & 255u;
-            const uint32_t qlz = c < 4 ? (nd.b.x >> s8) & 255u : ((nd.c.y & 0xffffu) >> s16) & 255u;
-            const uint32_t qhx = c < 4 ? (nd.b.y >> s8) & 255u : ((nd.c.y >> 16) >> s16) & 255u;
-            const uint32_t qhy = c < 4 ? (nd.b.z >> s8) & 255u : ((nd.c.z & 0xffffu) >> s16) & 255u;
-            const uint32_t qhz = c < 4 ? (nd.b.w >> s8) & 255u : ((nd.c.z >> 16) >> s16) & 255u;
-            // lo / hi: the slab relative to the origins, lo from the largest
-            // origin, hi from the smallest (the slab grown by their spread)
-            auto axis = [&](float dl, float dh, int e, uint32_t ql, uint32_t qh, float il, float ih, float dmn,
-                            float dmx, float& nr, float& fr) {
-                const float lo = dl + ldexpf((float)ql, e) - m2, hi = dh + ldexpf((float)qh, e) + m2;
-                if (il > 0.0f) {  // every lane's iq > 0: lo is the near plane
-                    nr = lo * (lo >= 0.0f ? il : ih);
-                    fr = hi * (hi >= 0.0f ? ih : il);
-                } else if (ih < 0.0f) {  // every lane's iq < 0: hi is the near plane
-                    nr = hi * (hi >= 0.0f ? il : ih);
-                    fr = lo * (lo >= 0.0f ? ih : il);
-                } else {
-                    // the component changes sign (or is 0) in the packet: no far
-                    // plane, but a slab wholly above (below) every origin is
-                    // reached no sooner than its distance over the largest
-                    // positive (negative) component; never without one
-                    fr = __builtin_huge_valf();
-                    nr = 0.0f;
-                    if (lo > 0.0f) nr = dmx > 0.0f ? lo / dmx : __builtin_huge_valf();
-                    if (hi < 0.0f) nr = dmn < 0.0f ? hi / dmn : __builtin_huge_valf();
-                }
-            };
-            float n0, f0, n1, f1, n2, f2;
-            axis(dxl, dxh, (int)(eb & 255u) - 128, qlx, qhx, ilx, ihx, dlx, dhx, n0, f0);
-            axis(dyl, dyh, (int)((eb >> 8) & 255u) - 128, qly, qhy, ily, ihy, dly, dhy, n1, f1);
-            axis(dzl, dzh, (int)((eb >> 16) & 255u) - 128, qlz, qhz, ilz, ihz, dlz, dhz, n2, f2);
-            tnear = fmaxf(fmaxf(n0, n1), fmaxf(n2, 0.0f));
-            const float tfar = fminf(fminf(f0, f1), fminf(f2, t_hi));
-            pass = tnear <= tfar && ((nd.c.w >> c) & 1u);
-        }
-        const uint32_t hm = (uint32_t)__ballot(pass);
-        uint32_t leaves = hm & ~imask;
-        if (leaves) {
-            do {
-                const int c = __builtin_ctz(leaves);
-                leaves &= leaves - 1u;
-                const int ti = (int)nd.a.y + c - __builtin_popcount(imask & ((1u << c) - 1u));
-                const TriPack tp = load_tri(tris, ti);
-                if (live) {
-                    if (kCount) ++cnt.tris;
-                    leaf_test(tp, ti, sh, o, 0.0f, h);
-                    live = h.idx < 0;
-                }
-            } while (leaves);
-            if (!__ballot(live)) break;  // every ray blocked
-        }
-        const uint32_t inner = hm & imask;
-        if (!inner) {
-            if (sp == 0) break;
-            --sp;
-            node = __builtin_amdgcn_readfirstlane(sp < kStack ? stk[sp] : gstk[sp - kStack]);
-            continue;
-        }
-        int best = -1;
-        float bt = 0.0f;
-        for (uint32_t r = inner; r; r &= r - 1u) {
-            const int c = __builtin_ctz(r);
-            const float tc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tnear), c));
-            if (best < 0 || tc < bt) {
-                best = c;
-                bt = tc;
-            }
-        }
-        const int base = (int)nd.a.x;
-        for (int c = kQWidth - 1; c >= 0; --c)
-            if (c != best && ((inner >> c) & 1u)) {
-                const int x = base + __builtin_popcount(imask & ((1u << c) - 1u));
-                if (sp < kStack) {
-                    stk[sp++] = x;
-                } else if (sp < kStack + kPacketSpill) {
-                    gstk[sp - kStack] = x;
-                    ++sp;
-                } else if (drops && lane == 0) {
-                    atomicAdd(drops, 1u);  // a missed subtree
-                }
-            }
-        node = __builtin_amdgcn_readfirstlane(base + __builtin_popcount(imask & ((1u << best) - 1u)));
-    }
-    return act && !live;
-}
-
 // Camera paths as packets: a wave traces 64 consecutive path indices (path_of:
 // the samples of one or two pixels) with packet_trace; packets are dealt to
 // the waves as trace_refill deals chunks (ChunkDealer, counters `deal`). An
@@ -1801,24 +1589,13 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_trace_primary_packet(
 // and the bounce-0 shadow queue.
 // In path-index order (pixel-major), so the bounce-0 shadow rays and the
 // bounce-1 paths are queued with the samples of one pixel side by side.
-// RR_SHADOW_BEAM: a bounce-0 shadow ray toward a sun (the only rays with
-// distance kFltMax) is not queued when the wave's sun rays leave points close
-// together (beam_coherent; a wave is one pixel's samples at 64 per chunk): path
-// p's goes to slot p of the arrays bq (the bounce-2 path queue's, idle until
-// k_shade_extend of bounce 1 writes it; the shadow queue's slots are the
-// queued rays') and bit p % 64 of smask[p / 64] says it is there
-// (k_shadow_packet traces them as one beam). The others are queued.
 __global__ __launch_bounds__(kBlock, kShadeWaves) void k_shade_primary(FrameConsts fc, SceneArgs sa, int np,
                                                           const float2* __restrict__ hits, Rad rad,
                                                           PathQueue out, ShadowQueue sq, QueueOut qo,
-                                                          const float4* __restrict__ tnrm, ShadowQueue bq,
-                                                          unsigned long long* __restrict__ smask) {
+                                                          const float4* __restrict__ tnrm) {
     GlobalView v = global_view(sa);
     v.nrm = tnrm;
     const int stride = gridDim.x * kBlock;
-#if RR_SHADOW_BEAM
-    const float pix = 2.0f * fc.half_w / (float)fc.W;
-#endif
     for (int b0 = blockIdx.x * kBlock; b0 < np; b0 += stride) {
         const int p = b0 + (int)threadIdx.x;
         ShadeOut so;
@@ -1835,21 +1612,7 @@ __global__ __launch_bounds__(kBlock, kShadeWaves) void k_shade_primary(FrameCons
             shade(fc, 0, v, o, d, mk3(1.0f, 1.0f, 1.0f), 0u, h, key, L, so);
             rad.put(p, L);
         }
-#if RR_SHADOW_BEAM
-        const bool sun = so.shadow && so.sdist == kFltMax;
-        const bool beam = sun && beam_coherent(sun, so.so, fc.cam_pos, pix);
-        const uint64_t ms = __ballot(beam);  // p of lane 0 is a multiple of 64 (kBlock-aligned b0)
-        if (beam) {
-            q_put<4>(bq.o + p, make_float4(so.so.x, so.so.y, so.so.z, i2f(p)));
-            q_put<4>(bq.d + p, make_float4(so.sd.x, so.sd.y, so.sd.z, so.sdist));
-            q_put<8>(bq.c + p, make_float4(so.sc.x, so.sc.y, so.sc.z, so.esc ? 1.0f : 0.0f));
-            so.shadow = false;  // not queued
-        }
-        if ((threadIdx.x & 63) == 0 && p < np) smask[p >> 6] = ms;
         emit_grouped(so, p, out, sq, qo);
-#else
-        emit_grouped(so, p, out, sq, qo);
-#endif
     }
 }
 
@@ -1863,7 +1626,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
                                                                          uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const TopNodes nodes = stage_top(sa, top_nodes);
+    const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
@@ -1923,7 +1686,7 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
                                                                           uint32_t* __restrict__ tail) {
     __shared__ int lds_stack[kLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
-    const TopNodes nodes = stage_top(sa, top_nodes);
+    const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
     TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
@@ -1948,60 +1711,6 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
             L.z = L.z + c.z;
             rad.put(pid, L);
         });
-    if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
-}
-
-// Bounce-0 sun shadow rays as packets (RR_SHADOW_BEAM): packet q = paths
-// 64 q .. 64 q + 63 (one pixel's samples at 64 per chunk), the lanes of
-// smask[q] hold a ray at slot p (k_shade_primary); dealt as the camera packets
-// are (ChunkDealer, counters `deal`); the rays are in bq (k_shade_primary's
-// beam records). An unblocked ray adds its contribution to
-// its path's radiance, as k_shadow_refill does for the queued ones (a path
-// has one bounce-0 shadow ray: one of the two kernels adds it). total: the
-// bounce's shadow-ray count (ray statistics; k_shadow_refill stored the
-// queued ones before).
-template <bool kCount>
-__global__ __launch_bounds__(kBlock, kTraceWaves) void k_shadow_packet(
-    SceneArgs sa, ShadowQueue bq, int np, const unsigned long long* __restrict__ smask, Rad rad,
-    uint32_t* __restrict__ deal, int32_t* __restrict__ spill, unsigned long long* __restrict__ tc,
-    uint32_t* __restrict__ tail, uint32_t* __restrict__ total) {
-    __shared__ int stack_all[kWavesPerBlock * kPacketStack];
-    lds_int* stk = lds_slot(stack_all) + (threadIdx.x >> 6) * kPacketStack;
-    int* const gstk = spill + (size_t)wave_id() * kPacketSpill;
-    TravCount cnt;
-    const int lane = threadIdx.x & 63;
-    const int npk = (np + 63) / 64;
-    ChunkDealer<kWavesPerBlock> dl;
-    dl.init(deal);
-    uint32_t n_rays = 0;
-    for (int q = dl.take(); q < npk;) {
-        const int qn = dl.take();  // the next packet, taken while this one traces
-        const uint64_t m = smask[q];
-        const int p = q * 64 + lane;
-        const bool ray = ((m >> lane) & 1ull) != 0ull;
-        float3 o = mk3(0.0f, 0.0f, 0.0f), d = mk3(0.0f, 0.0f, 1.0f);
-        float tmax = 0.0f;
-        if (ray) {
-            const float4 a = bq.o[p], b = bq.d[p];
-            o = xyz(a);
-            d = xyz(b);
-            tmax = b.w;
-        }
-        n_rays += ray ? 1u : 0u;
-        const bool blocked =
-            packet_shadow_beam<kCount>(sa.qnodes, sa.tris, stk, gstk, tail + 1, ray && sa.n_tris > 0, o, d, tmax, cnt);
-        if (ray && !blocked) {
-            const float4 c = q_last(bq.c + p);
-            float3 L = rad.get(p);
-            L.x = L.x + c.x;
-            L.y = L.y + c.y;
-            L.z = L.z + c.z;
-            rad.put(p, L);
-        }
-        q = qn;
-    }
-    for (int off = 32; off > 0; off >>= 1) n_rays += (uint32_t)__shfl_xor((int)n_rays, off);
-    if (lane == 0 && n_rays) atomicAdd(total, n_rays);
     if (kCount) flush_counts(tc, 4, cnt.nodes, cnt.tris);
 }
 
@@ -2946,24 +2655,20 @@ struct TileGrid {
 };
 // Launch geometry of the split (trace / shade) path of large scenes.
 struct SplitGrids {
-    int trace_p, trace_e, shadow, shade_p, shade_e, packet, sort, shadow_pk;
+    int trace_p, trace_e, shadow, shade_p, shade_e, packet, sort;
     void (*ktp)(FrameConsts, SceneArgs, int, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kte)(SceneArgs, PathQueue, QueueIn, const uint32_t*, float2*, int32_t*, unsigned long long*, uint32_t*);
     void (*kts)(SceneArgs, ShadowQueue, QueueIn, const uint32_t*, Rad, int32_t*, unsigned long long*, uint32_t*);
     void (*ktpk)(FrameConsts, SceneArgs, int, float2*, uint32_t*, int32_t*, unsigned long long*, uint32_t*);  // packets
-    void (*kspk)(SceneArgs, ShadowQueue, int, const unsigned long long*, Rad, uint32_t*, int32_t*, unsigned long long*,
-                 uint32_t*, uint32_t*);  // bounce-0 shadow packets
     explicit SplitGrids(bool count) {
         ktp = count ? k_trace_primary<true> : k_trace_primary<false>;
         kte = count ? k_trace_extend<true> : k_trace_extend<false>;
         kts = count ? k_shadow_refill<true> : k_shadow_refill<false>;
         ktpk = count ? k_trace_primary_packet<true> : k_trace_primary_packet<false>;
-        kspk = count ? k_shadow_packet<true> : k_shadow_packet<false>;
         trace_p = grid_for(ktp, 0, kTraceBlock);
         trace_e = grid_for(kte, 0, kTraceBlock);
         shadow = grid_for(kts, 0, kTraceBlock);
         packet = grid_for(ktpk, 0);
-        shadow_pk = grid_for(kspk, 0);
         shade_p = grid_for(k_shade_primary, 0);
         shade_e = grid_for(k_shade_extend, 0);
         sort = grid_for(k_sort_queue, 0, kSortBlock);
@@ -2998,7 +2703,6 @@ void DevPaths::ensure_paths(size_t n) {
                                   &sh_c})
             b->ensure(n);
         hits.ensure(n);
-        if (RR_SHADOW_BEAM) shmask.ensure(n / 64 + 1);
         cap = n;
     }
     spill.ensure((size_t)kSpillStack * grid_blocks * kBlock);
@@ -3014,7 +2718,6 @@ void DevPaths::release() {
                               &sh_c, &film})
         b->release();
     perm.release();
-    shmask.release();
     counters.release(); tile_ctrs.release(); tile_cost.release(); tile_order.release(); spill.release(); tile_slab.release(); film_part.release(); hits.release(); qctr.release();
     rgba8.release(); filter_table.release(); srgb_lut.release(); lights.release(); materials.release();
     mat_lut.release();
@@ -3076,12 +2779,9 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             G.ktp<<<clamp_grid(np, G.trace_p, kTraceBlock), kTraceBlock, 0, st>>>(fc, sa, np, p.hits.ptr, p.spill.ptr,
                                                                                    tc, tail);
         pr.end(st);
-        // beam records of k_shade_primary (RR_SHADOW_BEAM): the bounce-2 path
-        // queue's arrays, free until k_shade_extend of bounce 1 writes them
-        const ShadowQueue beam_q{pq[0].o, pq[0].d, pq[0].t};
         pr.begin(st, RR_K_SHADE);
         k_shade_primary<<<gsp, kBlock, 0, st>>>(fc, sa, np, p.hits.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, pq[1],
-                                                sq, QueueOut{qpath(0), qshadow(0), cap_p}, tnrm, beam_q, p.shmask.ptr);
+                                                sq, QueueOut{qpath(0), qshadow(0), cap_p}, tnrm);
         pr.end(st);
         uint32_t cap_prev = cap_p;  // group capacity of the producer of the current queues
         // k_sort_queue's grid: a queue of groups of cap_prev slots spans at most
@@ -3101,12 +2801,6 @@ void render_split(DevPaths& p, const FrameConsts& base, int n_chunks, hipStream_
             G.kts<<<clamp_grid(np, G.shadow, kTraceBlock), kTraceBlock, 0, st>>>(
                 sa, sq, QueueIn{qshadow(b), cap_prev, tot + 2 * b + 1}, perm_s, Rad{reinterpret_cast<float*>(p.rad.ptr)},
                 p.spill.ptr, tc, tail);
-            // bounce-0 sun rays of coherent pixels: beam packets in path order
-            // (k_shade_primary's smask and beam records)
-            if (RR_SHADOW_BEAM && b == 0)
-                G.kspk<<<clamp_grid(np, G.shadow_pk), kBlock, 0, st>>>(
-                    sa, beam_q, np, p.shmask.ptr, Rad{reinterpret_cast<float*>(p.rad.ptr)}, deal_host(qshadow(0), 1),
-                    p.spill.ptr, tc, tail, tot + 1);
             pr.end(st);
             if (b == base.max_bounces) break;
             const int nb = b + 1;  // bounce being traced and shaded
@@ -3218,8 +2912,7 @@ void render_frame_device(DevScene& s, DevPaths& p, const FrameConsts& base, int 
     PathQueue pq[2] = {{p.ps_o[0].ptr, p.ps_d[0].ptr, p.ps_t[0].ptr}, {p.ps_o[1].ptr, p.ps_d[1].ptr, p.ps_t[1].ptr}};
     ShadowQueue sq{p.sh_o.ptr, p.sh_d.ptr, p.sh_c.ptr};
     const SceneArgs sa{s.nodes.ptr, s.qnodes.ptr, s.tris.ptr, p.materials.ptr, p.lights.ptr, p.filter_table.ptr,
-                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.nq,
-                       RR_WIDE_NODES ? s.qwide.ptr : nullptr};
+                       p.mat_lut.ptr, std::max(s.n_tris - 1, 1), s.n_tris, base.n_mats, base.n_lights, s.nq};
     render_split(p, base, n_chunks, st, sa, tc, pq, sq, s.has4 ? s.tnrm.ptr : nullptr);
     RR_HIP(hipGetLastError());
 }

@@ -1676,7 +1676,7 @@ int orc_trace_w(int n, const float* tris9, int width, int n_rays, const float* r
 
 #ifdef ORC_WALK_STUDY
 /* Research build only (tools/beam_study.py): the device's any-hit beam packet
- * walk (wavefront.hip packet_shadow_beam) over packets of rays starts[k] ..
+ * walk (packet_shadow_beam of commit 76f0210) over packets of rays starts[k] ..
  * starts[k + 1] - 1 (at most 64; 8 floats each: o, tmin, d, tmax), against
  * the per-lane any-hit walk.
  * out: [0] packets, [1] beam node visits (per packet), [2] beam leaf tests

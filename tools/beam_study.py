@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Work of the bounce-0 shadow-ray beam packets (wavefront.hip
-packet_shadow_beam) against per-lane any-hit walks, on the CPU (research):
+"""Work of the bounce-0 shadow-ray beam packets (the device walk
+packet_shadow_beam of commit 76f0210, measured slower and removed) against
+per-lane any-hit walks, on the CPU (research):
 the oracle built with ORC_WALK_STUDY runs the device's beam walk over packets
 of one pixel's shadow rays and checks that every ray's occlusion equals the
 per-lane walk's. Rays: `spp` camera rays per sampled pixel, their hits, and a
@@ -107,7 +108,7 @@ def main():
     keep = hit.reshape(npx, spp)
     print(f"{key} frame {frame}: {len(tris)} triangles, {npx} pixels x {spp} samples")
     # mixed: one pixel's rays of camera hits in one packet (padding: repeat the pixel's first ray)
-    # the device's spread test (packet_shadow_beam): origins within kBeamSpread pixel footprints
+    # the device's spread test (beam_coherent of commit 76f0210): origins within 4 pixel footprints
     cam_pos = np.asarray(st.camera, np.float64)[:3]
 
     def coherent(g, spread=4.0):
