@@ -133,16 +133,28 @@ RR_HD int leaf_count(int ref) { return ((~ref) >> 28) + 1; }
 constexpr int kMaxLights = 64;
 constexpr int kBlock = 256;         // threads per block for all path kernels
 // Traversal stack per lane: kLdsStack entries in LDS, the rest (up to the
-// oracle's ORC_MAXDEPTH = 80 in all) in a per-thread HBM spill area. 12 LDS
-// entries (48 KB per 1024-thread trace block) leave room for the split-path
-// trace kernels' top-of-tree node copy (wavefront.hip stage_top, 32 KB) at two
-// blocks per CU; 16 entries with half the node copy measured 1-1.5 % slower on
-// C5 (round 3, 256-thread blocks).
+// oracle's ORC_MAXDEPTH = kStackCap = 80 in all) in a per-thread HBM spill
+// area. 12 LDS entries (k_tiles, the debug walks; 16 with half the node copy
+// measured 1-1.5 % slower on C5 in round 3, 256-thread blocks).
 #ifndef RR_LDS_STACK
 #define RR_LDS_STACK 12
 #endif
+constexpr int kStackCap = 80;
 constexpr int kLdsStack = RR_LDS_STACK;
-constexpr int kSpillStack = 80 - kLdsStack;
+constexpr int kSpillStack = kStackCap - kLdsStack;
+// The split path's trace kernels (round 6): 8 LDS entries per lane, 32 KB per
+// 1,024-thread block, leave 48 KB for the top of the hierarchy (768 nodes,
+// wavefront.hip kTopNodes) at two blocks per CU; against 12 entries and 512
+// nodes: C5 frame slices -1.0 % (extension walks -1.8 %), 02 / 03 unchanged;
+// 10 / 640 no better, 6 / 896 level, 4 / 1,024 +5 % (spills;
+// profiles/r6_ab_lds_top.txt).
+#ifndef RR_TRACE_LDS_STACK
+#define RR_TRACE_LDS_STACK 8
+#endif
+constexpr int kTraceLdsStack = RR_TRACE_LDS_STACK;
+// entries per lane of the spill area (DevPaths::spill): what the stack with
+// the fewest LDS entries needs to reach kStackCap
+constexpr int kSpillLane = kStackCap - (kTraceLdsStack < kLdsStack ? kTraceLdsStack : kLdsStack);
 constexpr int kDimsPerBounce = 8;   // RNG dimensions consumed per bounce
 constexpr int kRrStartBounce = 3;   // Russian roulette from this bounce on
 
@@ -605,8 +617,8 @@ RR_D TriPack load_tri(lds_tri* p, int i) {
 }
 // kB: the threads per block of the kernel that owns the stack; kL: its LDS
 // entries per lane (rr_debug_trace width 6 runs the 6-wide walk with 1, so
-// nearly every entry lives in the HBM part).
-template <int kB = kBlock, int kL = kLdsStack>
+// nearly every entry lives in the HBM part); kS: its HBM entries per lane.
+template <int kB = kBlock, int kL = kLdsStack, int kS = kSpillStack>
 struct TravStackT {
     // Bases only: the lane's slots are recomputed from threadIdx/blockIdx at each
     // push/pop, so no per-lane pointer stays live in VGPRs across a kernel's
@@ -617,7 +629,7 @@ struct TravStackT {
     int sp;
     // the frame's drop counter (device.hpp drops_slot; null: not counted)
     uint32_t* drops;
-    // A push beyond kL + kSpillStack entries is dropped (a missed
+    // A push beyond kL + kS entries is dropped (a missed
     // subtree) and counted at once with an atomic on the frame's drop counter
     // (no register stays live for it; rr_frame_stats.stack_drops, tests assert
     // 0 on every bench scene); the oracle's stack has the same capacity and the
@@ -625,7 +637,7 @@ struct TravStackT {
     RR_D void push(int x) {
         if (sp < kL) {
             lds[sp * kB + (int)threadIdx.x] = x;
-        } else if (sp < kL + kSpillStack) {
+        } else if (sp < kL + kS) {
             spill[(sp - kL) * spill_stride + (int)(blockIdx.x * kB + threadIdx.x)] = x;
         } else {
             if (drops) atomicAdd(drops, 1u);

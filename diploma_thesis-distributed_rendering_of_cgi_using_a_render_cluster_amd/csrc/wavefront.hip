@@ -919,10 +919,10 @@ RR_D uint32_t* deal_ctrs(const uint32_t* q, int word) {
 // against none, measured on the 4-wide hierarchy per frame slice (C5 at 16 spp
 // / 02 / 03 at 64 spp): 105.8 -> 101.4, 110.5 -> 107.0, 118.2 -> 115.9 ms.
 #ifndef RR_TOP_NODES
-#define RR_TOP_NODES (kTraceBlock >= 1024 ? 512 : 128)
+#define RR_TOP_NODES (kTraceBlock >= 1024 ? 768 : 128)  // 768 with 8-entry LDS stacks (rr_device.h kTraceLdsStack)
 #endif
 constexpr int kTopNodes = RR_TOP_NODES;
-static_assert((kLdsStack * kTraceBlock * 4 + 64 * kTopNodes) * (2048 / kTraceBlock) <= 160 * 1024,
+static_assert((kTraceLdsStack * kTraceBlock * 4 + 64 * kTopNodes) * (2048 / kTraceBlock) <= 160 * 1024,
               "trace kernels: stack + top copy of 8 waves per SIMD must fit the CU's LDS");
 RR_D Q6Nodes stage_top(const SceneArgs& sa, rr_f4v* top_shared) {
     lds_f4w* top = (lds_f4w*)top_shared;
@@ -1268,10 +1268,11 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_primary(Fram
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc,
                                                                           uint32_t* __restrict__ tail) {
-    __shared__ int lds_stack[kLdsStack * kTraceBlock];
+    __shared__ int lds_stack[kTraceLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
-    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
+    TravStackT<kTraceBlock, kTraceLdsStack, kStackCap - kTraceLdsStack> st{lds_slot(lds_stack), spill,
+                                                                        (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     const ScreenCull cull = screen_cull(fc, sa.nodes);
     uint32_t n_traced = 0;  // camera rays of this lane that are not culled
@@ -1624,12 +1625,13 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_trace_extend(Scene
                                                                          int32_t* __restrict__ spill,
                                                                          unsigned long long* __restrict__ tc,
                                                                          uint32_t* __restrict__ tail) {
-    __shared__ int lds_stack[kLdsStack * kTraceBlock];
+    __shared__ int lds_stack[kTraceLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
-    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
+    TravStackT<kTraceBlock, kTraceLdsStack, kStackCap - kTraceLdsStack> st{lds_slot(lds_stack), spill,
+                                                                        (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     trace_refill<SplitTrav<false, kCount>>(
         nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qi.ctr, 1),
@@ -1684,12 +1686,13 @@ __global__ __launch_bounds__(kTraceBlock, kTraceWaves) void k_shadow_refill(Scen
                                                                           int32_t* __restrict__ spill,
                                                                           unsigned long long* __restrict__ tc,
                                                                           uint32_t* __restrict__ tail) {
-    __shared__ int lds_stack[kLdsStack * kTraceBlock];
+    __shared__ int lds_stack[kTraceLdsStack * kTraceBlock];
     __shared__ rr_f4v top_nodes[4 * (kTopNodes > 0 ? kTopNodes : 1)];
     const Q6Nodes nodes = stage_top(sa, top_nodes);
     QueueMap qm;
     qm.init(qi);
-    TravStackT<kTraceBlock> st{lds_slot(lds_stack), spill, (int)(gridDim.x * kTraceBlock), 0, tail + 1};
+    TravStackT<kTraceBlock, kTraceLdsStack, kStackCap - kTraceLdsStack> st{lds_slot(lds_stack), spill,
+                                                                        (int)(gridDim.x * kTraceBlock), 0, tail + 1};
     TravCount cnt;
     trace_refill<SplitTrav<true, kCount>>(
         nodes, sa.tris, sa.n_tris, qm.span, st, cnt, deal_ctrs(qi.ctr, 1),
@@ -2705,12 +2708,12 @@ void DevPaths::ensure_paths(size_t n) {
         hits.ensure(n);
         cap = n;
     }
-    spill.ensure((size_t)kSpillStack * grid_blocks * kBlock);
+    spill.ensure((size_t)kSpillLane * grid_blocks * kBlock);
 }
 
 void DevPaths::ensure_tiles() {
     if (grid_blocks == 0) grid_blocks = device_cu_count() * kMaxBlocksPerCu;
-    spill.ensure((size_t)kSpillStack * grid_blocks * kBlock);
+    spill.ensure((size_t)kSpillLane * grid_blocks * kBlock);
 }
 
 void DevPaths::release() {
