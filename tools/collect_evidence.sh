@@ -23,4 +23,4 @@ for wl in 04vs 01 02 03 c5 04vs_serial 04vs_driver_config; do
     if [ -f $f ] && grep -q '^{' $f; then grep '^{' $f > profiles/${tag}_bench_$wl.json; else echo "skip bench $wl"; fi
 done
 if [ -f gpurun_out/ev/smoke.log ]; then grep -v '^===' gpurun_out/ev/smoke.log > profiles/${tag}_smoke.log; fi
-if [ -f gpurun_out/ev_log.txt ]; then grep -E '[0-9]+ passed' gpurun_out/ev_log.txt | head -1 > profiles/${tag}_gpu_tests.txt; fi
+if [ -f gpurun_out/ev_log.txt ]; then grep -E '[0-9]+ passed' gpurun_out/ev_log.txt | head -1 > profiles/${tag}_gpu_tests_summary.txt; fi
